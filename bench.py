@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""bench.py — FEC encode+decode throughput on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch: fecgpu_encode_batch over
+every window (sender: repair generation) then fecgpu_decode_batch over every
+window (receiver: recovery of the erased sources), inputs already resident in
+HBM.  value = source-packet bytes (sum of packet lengths, no prefix or
+padding) of all ranks x steps / max-over-ranks wall time.
+
+Workloads (BASELINE.json configs):
+  --config 2 (default): XOR k=8 r=2, 65,536 windows x 8 x 1200 B per GPU,
+                        one source erased per XOR group (e = r = 2)
+  --config 3          : GF(2^8) Cauchy k=16 r=4, 262,144 windows x 16 x 1200 B,
+                        exactly r sources erased per window
+  --config 4          : GF(2^8) k=32 r=8, mixed MTU 1200/9000 LENPREFIX,
+                        131,072 windows per GPU (1M over 8), i.i.d. 10% erasures
+Multi-GPU: one process per GPU (torchrun), windows sharded by rank with no
+data-path collective (weak scaling); RCCL only carries the barrier and the
+max-over-ranks time reduction.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+_ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(_ROOT, "quic-fec-eps_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import fecgpu  # noqa: E402
+from fecgpu import workloads  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(workloads.CONFIGS))
+    ap.add_argument("--nwin", type=int, default=0, help="windows per GPU (0 = config default)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU work for the cpu_baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
+    """Time the CPU oracle (oracle/fec_oracle.c, kind "port") on a bounded
+    sample of the same workload: same packets, same erasure stream."""
+    sys.path.insert(0, os.path.join(_ROOT, "oracle"))
+    import numpy as np
+    import oracle as O  # test/baseline infrastructure only
+
+    O.lib()
+    if threads <= 0:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    scheme = O.XOR if cfg.scheme == "xor" else O.GF256
+
+    def run(nw: int):
+        S = O.sym_lens(cfg.workload, workloads.SEED, 0, nw, cfg.k, cfg.L)
+        wins = O.make_windows(cfg.workload, workloads.SEED, 0, nw, cfg.k, cfg.r, cfg.L, cfg.stride)
+        pres = O.presents(cfg.erasure, workloads.SEED, 0, nw, scheme, cfg.k, cfg.r)
+        src = int(sum(O.lib().orc_pkt_len(cfg.workload, workloads.SEED, w, j, cfg.k, cfg.L)
+                      for w in range(nw) for j in range(cfg.k)))
+        t0 = time.perf_counter()
+        O.encode_batch(scheme, cfg.k, cfg.r, S, wins, threads)
+        O.decode_batch(scheme, cfg.k, cfg.r, S, wins, pres, threads)
+        return time.perf_counter() - t0, src
+
+    nw = 4 * threads
+    dt, src = run(nw)
+    while dt < 0.5 and nw < 1 << 20:
+        nw *= 4
+        dt, src = run(nw)
+    nw = max(nw, int(nw * seconds / max(dt, 1e-3)))
+    dt, src = run(nw)
+    return {"value": round(src / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{nw} windows of {cfg.name} (encode+decode, same packets and erasures), "
+                      f"{dt:.1f} s on {threads} host threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    cfg = workloads.CONFIGS[args.config]
+    nwin = args.nwin or cfg.nwin_per_gpu
+    w0 = rank * nwin  # this rank's shard of the global window range
+    ctx = fecgpu.Context()
+    batch = workloads.Batch.allocate(cfg, nwin, dev)
+    batch.synthesize(ctx, w0)
+    batch.make_erasures(ctx, w0)
+    src_bytes = batch.source_bytes()      # per rank, per step
+    alg = batch.algorithmic_bytes()       # {'encode': B, 'decode': B} per launch
+
+    # warmup
+    for _ in range(args.warmup):
+        batch.encode(ctx)
+        batch.decode(ctx)
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1, e2 in ev:
+        e0.record()
+        batch.encode(ctx)
+        e1.record()
+        batch.decode(ctx)
+        e2.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    enc_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
+    dec_ms = sum(b.elapsed_time(c) for _, b, c in ev) / args.steps
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(src_bytes)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed = float(t.item())
+    total_src = float(tot.item()) * args.steps
+    value = total_src / elapsed / 1e9
+
+    verify = None if args.no_verify else batch.verify(ctx, w0)
+
+    if rank == 0:
+        dom = "decode" if dec_ms > enc_ms else "encode"
+        dom_ms = max(enc_ms, dec_ms)
+        achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+        cpu = None
+        if args.cpu_seconds > 0 and world == 1:
+            cpu = cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads)
+        line = {
+            "metric": "GB/s source-packet bytes FEC encode+decode, device-resident, per MI355X",
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (on-device splitmix64 packets, seeded erasures)",
+            "config": {
+                "workload": cfg.name,
+                "scheme": cfg.scheme, "k": cfg.k, "r": cfg.r,
+                "windows_per_gpu": nwin, "packet_bytes": cfg.L if cfg.workload == 0 else "1200|9000 mixed",
+                "erasures": cfg.erasure_desc,
+                "parallelism": f"window-shard x{world}",
+            },
+            "kernels_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "alg_bytes_per_launch": alg[dom],
+            },
+            "roofline_other": {
+                k2: round(alg[k2] / (ms * 1e-3) / 1e9, 1)
+                for k2, ms in (("encode", enc_ms), ("decode", dec_ms))
+            },
+            "cpu_baseline": cpu,
+            "verify": verify,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if verify is not None and not verify.get("ok", False):
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,141 @@
+/*
+ * fecgpu.h — C ABI of the MI355X FEC engine (drop-in boundary).
+ *
+ * What each entry point replaces.  The reference fec branch
+ * (holzingk/quic-fec-eps, /root/reference/README.md:7) is not mounted: no
+ * Rust source exists here to cite by file:line.  The entry points below
+ * replace the branch's FEC encoder / decoder / frame API named in
+ * BASELINE.json "north_star" (the per-packet calls the quiche Connection
+ * makes on send and recv: SURVEY.md §3 call stacks A and B), and follow
+ * quiche's own C FFI conventions (opaque handles, caller-owned buffers,
+ * ssize_t results with negative error codes).
+ * INTEGRATION.md shows the Rust `extern "C"` block a maintainer adds to
+ * call them.
+ *
+ * Coding contract: SURVEY.md Appendix A (field GF(2^8)/0x11D, systematic
+ * Cauchy rows C[i][j] = inv((k+i) ^ j) or interleaved XOR groups j mod r,
+ * FIXED or LENPREFIX framing).
+ *
+ * Batch layout (A.4): window w is (k + r) symbols, sources 0..k-1 then
+ * repairs k..k+r-1.  With win_off == NULL window w starts at
+ * win + w*(k+r)*stride and every symbol occupies `stride` bytes (multiple of
+ * 16, >= S).  With win_off != NULL window w starts at win + win_off[w] and
+ * its symbol stride is round_up(S_w, 16).  S_w = sym_len[w], or sym_len_all
+ * when sym_len == NULL.  Bytes [S_w, stride) of a symbol are padding: the
+ * kernels compute on whole 16-byte columns, so padding of written symbols
+ * holds the code applied to the inputs' padding (zero in, zero out).
+ *
+ * Pointers are device pointers (hipMalloc / torch) unless FECGPU_F_HOST_PTRS
+ * is set, in which case every buffer argument is host memory and the call
+ * stages through device memory owned by the ctx and returns synchronously.
+ * `stream` is a hipStream_t (NULL = the default stream).  Device-pointer
+ * calls are asynchronous on that stream unless FECGPU_F_SYNC is set.
+ *
+ * Threading: a ctx may be used by one thread at a time; distinct ctxs are
+ * independent.  Errors are returned, never raised; there is no CPU fallback.
+ */
+#ifndef FECGPU_H
+#define FECGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <sys/types.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FECGPU_ABI_VERSION 1
+
+/* errors (mirror quiche's QUICHE_ERR_DONE = -1, QUICHE_ERR_BUFFER_TOO_SHORT = -2 style) */
+enum fecgpu_error {
+    FECGPU_ERR_DONE = -1,             /* nothing to do / no more data */
+    FECGPU_ERR_BUFFER_TOO_SHORT = -2, /* caller buffer too small */
+    FECGPU_ERR_INVALID_ARG = -3,
+    FECGPU_ERR_UNSUPPORTED = -4,      /* valid but not implemented (e.g. r > 8) */
+    FECGPU_ERR_DEVICE = -5,           /* HIP error or no GPU */
+    FECGPU_ERR_UNRECOVERABLE = -6,    /* too many erasures in a window */
+};
+
+enum fecgpu_scheme { FECGPU_SCHEME_XOR = 0, FECGPU_SCHEME_GF256 = 1 };
+enum fecgpu_matrix { FECGPU_MATRIX_CAUCHY = 0 };
+enum fecgpu_framing { FECGPU_FRAMING_FIXED = 0, FECGPU_FRAMING_LENPREFIX = 1 };
+
+/* per-window decode status */
+enum fecgpu_status { FECGPU_STATUS_OK = 0, FECGPU_STATUS_UNRECOVERABLE = 1 };
+
+#define FECGPU_F_HOST_PTRS 1u
+#define FECGPU_F_SYNC 2u
+
+#define FECGPU_MAX_K 64
+#define FECGPU_MAX_R 8
+
+typedef struct fecgpu_code {
+    uint32_t scheme;  /* enum fecgpu_scheme */
+    uint32_t matrix;  /* enum fecgpu_matrix (GF256 only) */
+    uint32_t framing; /* enum fecgpu_framing */
+    uint16_t k;       /* source symbols per window, 1..64 */
+    uint16_t r;       /* repair symbols per window, 1..8, k + r <= 64, XOR: r <= k */
+    uint32_t poly;    /* field polynomial, 0x11D (0 = default) */
+} fecgpu_code;
+
+typedef struct fecgpu_ctx fecgpu_ctx;
+
+int         fecgpu_abi_version(void);
+const char *fecgpu_strerror(ssize_t err);
+/* message of the last FECGPU_ERR_DEVICE on this thread ("" if none) */
+const char *fecgpu_last_error(void);
+/* 0 if the code is valid and supported, else a negative error */
+ssize_t     fecgpu_code_check(const fecgpu_code *code);
+
+/* ctx over devs[0..ndev-1] (NULL/0 = current device).  Batches with device
+ * pointers run on the device of the pointers; host-pointer batches are split
+ * over the ctx's devices. */
+ssize_t fecgpu_ctx_new(const int *devs, int ndev, fecgpu_ctx **out);
+void    fecgpu_ctx_free(fecgpu_ctx *ctx);
+
+/* ---- batch entry points (hot path) ---------------------------------- */
+
+/* Repair generation: writes repairs k..k+r-1 of every
+ * window from its sources.  Returns nwin or a negative error. */
+ssize_t fecgpu_encode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *win,
+                            const uint64_t *win_off, const uint32_t *sym_len,
+                            uint32_t sym_len_all, uint32_t stride, uint64_t nwin,
+                            uint32_t flags, void *stream);
+
+/* Recovery: present[w] bit i = symbol i received.
+ * Missing sources are recovered in place; status[w] = FECGPU_STATUS_*.
+ * Symbols whose bit is clear are never read.  XOR recovers every group with
+ * exactly one missing source and its repair, even when others are lost.
+ * Returns nwin or a negative error. */
+ssize_t fecgpu_decode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *win,
+                            const uint64_t *win_off, const uint32_t *sym_len,
+                            uint32_t sym_len_all, uint32_t stride, uint64_t nwin,
+                            const uint64_t *present, uint8_t *status, uint32_t flags,
+                            void *stream);
+
+/* ---- synthetic workload / verification (bench + tests) ---- */
+
+/* Fill sources of windows w0..w0+nwin-1 on the device (workload 0: FIXED,
+ * every packet L bytes; 1: mixed MTU 1200/9000, 10% shortened, LENPREFIX).
+ * Writes sym_len[w] (device, may be NULL for workload 0).  stride must hold
+ * the largest symbol (9002 for workload 1).  Device pointers only. */
+ssize_t fecgpu_synth_batch(fecgpu_ctx *ctx, const fecgpu_code *code, int workload,
+                           uint64_t seed, uint64_t w0, uint8_t *win, uint32_t *sym_len,
+                           uint32_t L, uint32_t stride, uint64_t nwin, void *stream);
+
+/* Erasure masks (0: none, 1: exactly r sources, 2: i.i.d. p = 0.1). */
+ssize_t fecgpu_erasure_batch(fecgpu_ctx *ctx, const fecgpu_code *code, int erasure,
+                             uint64_t seed, uint64_t w0, uint64_t *present, uint64_t nwin,
+                             void *stream);
+
+/* XOR-accumulates the batch digest into *digest
+ * (device u64, caller zeroes it). */
+ssize_t fecgpu_digest_batch(fecgpu_ctx *ctx, const fecgpu_code *code, const uint8_t *win,
+                            const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
+                            uint64_t w0, uint64_t nwin, uint64_t *digest, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

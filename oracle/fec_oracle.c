@@ -1,0 +1,336 @@
+/*
+ * fec_oracle.c — CPU restatement of the FEC coding contract.
+ * TEST INFRASTRUCTURE ONLY (see fec_oracle.h).  PARITY UNPINNED.
+ *
+ * What it follows.  The reference fec branch is not mounted
+ * (/root/reference/README.md:1-8 is the whole reference; the branch is named
+ * only by URL at README.md:7), so nothing here can cite a reference file:line
+ * for the arithmetic.  Every function cites the clause of the build-owned
+ * contract it restates: SURVEY.md Appendix A (A.1 field, A.2 matrices, A.3
+ * framing, A.4 layout, A.5 PRNG, A.6 digest) and SURVEY.md §8a rows a1-a9.
+ * Workload definitions (payload, MTU, shortening, erasure streams) are
+ * DESIGN.md §Workloads.
+ *
+ * Deliberately written the slow, obvious way: byte loops, log/exp tables,
+ * textbook Gauss-Jordan with pivot search.  It shares no code with the HIP
+ * product (quic-fec-eps_amd/csrc).
+ */
+#include "fec_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- A.1 --- */
+/* GF(2^8), reduction polynomial x^8+x^4+x^3+x^2+1 (0x11D), generator 2.
+ * SURVEY.md Appendix A.1; §8a a1. */
+static uint8_t g_exp[512];
+static int     g_log[256];
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+
+static void gf_build(void) {
+    unsigned x = 1;
+    for (int i = 0; i < 255; i++) {
+        g_exp[i] = (uint8_t)x;
+        g_log[x] = i;
+        x <<= 1;
+        if (x & 0x100) x ^= 0x11D;
+    }
+    for (int i = 255; i < 512; i++) g_exp[i] = g_exp[i - 255];
+    g_log[0] = -1;
+}
+static void gf_init(void) { pthread_once(&g_once, gf_build); }
+
+uint8_t orc_gf_exp(int i) { gf_init(); return g_exp[((i % 255) + 255) % 255]; }
+int     orc_gf_log(uint8_t a) { gf_init(); return g_log[a]; }
+
+uint8_t orc_gf_mul(uint8_t a, uint8_t b) {
+    gf_init();
+    if (a == 0 || b == 0) return 0;
+    return g_exp[g_log[a] + g_log[b]];
+}
+
+uint8_t orc_gf_inv(uint8_t a) {
+    gf_init();
+    if (a == 0) return 0; /* undefined; callers never ask */
+    return g_exp[255 - g_log[a]];
+}
+
+/* ---------------------------------------------------------------- A.2 --- */
+/* Systematic Cauchy generator rows: C[i][j] = inv((k+i) xor j), i<r, j<k
+ * (ISA-L gf_gen_cauchy1_matrix layout).  SURVEY.md Appendix A.2; §8a a5. */
+void orc_cauchy(int k, int r, uint8_t *C) {
+    for (int i = 0; i < r; i++)
+        for (int j = 0; j < k; j++) C[i * k + j] = orc_gf_inv((uint8_t)((k + i) ^ j));
+}
+
+/* ---------------------------------------------------------------- A.5 --- */
+uint64_t orc_sm64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+/* sub-stream seeds */
+#define TAG_PAY 0x5041594C4F414400ull
+#define TAG_MTU 0x4D54550000000000ull
+#define TAG_LEN 0x4C454E0000000000ull
+#define TAG_ERA 0x4552415345000000ull
+#define P10 429496730u /* 0.1 * 2^32, rounded */
+
+uint32_t orc_pkt_len(int workload, uint64_t seed, uint64_t w, int j, int k, uint32_t L) {
+    (void)k;
+    if (workload == 0) return L; /* fixed */
+    uint32_t mtu = (orc_sm64(orc_sm64(seed ^ TAG_MTU) + w) & 1) ? 9000u : 1200u;
+    uint64_t h = orc_sm64(orc_sm64(seed ^ TAG_LEN) + ((w << 8) | (uint64_t)j));
+    if ((uint32_t)h < P10) return 64u + (uint32_t)((h >> 32) % (uint64_t)(mtu - 63u));
+    return mtu;
+}
+
+uint32_t orc_sym_len(int workload, uint64_t seed, uint64_t w, int k, uint32_t L) {
+    if (workload == 0) return L;
+    uint32_t mx = 0;
+    for (int j = 0; j < k; j++) {
+        uint32_t l = orc_pkt_len(workload, seed, w, j, k, L);
+        if (l > mx) mx = l;
+    }
+    return 2u + mx; /* A.3 LENPREFIX: u16be len || payload || 0-pad */
+}
+
+static uint8_t payload_byte(uint64_t spay, uint64_t w, int j, uint32_t o) {
+    uint64_t word = orc_sm64(spay + ((w << 24) | ((uint64_t)j << 16) | (uint64_t)(o >> 3)));
+    return (uint8_t)(word >> (8 * (o & 7)));
+}
+
+/* A.3 framing + A.4 layout, one window's sources. */
+void orc_fill_window(int workload, uint64_t seed, uint64_t w, int k, int r, uint32_t L,
+                     uint32_t stride, uint8_t *win) {
+    uint64_t spay = orc_sm64(seed ^ TAG_PAY);
+    memset(win, 0, (size_t)(k + r) * stride);
+    for (int j = 0; j < k; j++) {
+        uint8_t *s = win + (size_t)j * stride;
+        uint32_t len = orc_pkt_len(workload, seed, w, j, k, L);
+        if (workload == 0) {
+            for (uint32_t o = 0; o < len; o++) s[o] = payload_byte(spay, w, j, o);
+        } else {
+            s[0] = (uint8_t)(len >> 8);
+            s[1] = (uint8_t)len;
+            for (uint32_t o = 0; o < len; o++) s[2 + o] = payload_byte(spay, w, j, o);
+        }
+    }
+}
+
+/* erasure streams: 0 none, 1 exactly-r (GF: partial Fisher-Yates over
+ * sources; XOR: one source per group), 2 i.i.d. p=0.1 over all k+r symbols */
+uint64_t orc_present(int erasure, uint64_t seed, uint64_t w, int scheme, int k, int r) {
+    uint64_t all = (k + r >= 64) ? ~0ull : ((1ull << (k + r)) - 1);
+    uint64_t sera = orc_sm64(seed ^ TAG_ERA);
+    if (erasure == 0) return all;
+    if (erasure == 2) {
+        uint64_t p = all;
+        for (int i = 0; i < k + r; i++)
+            if ((uint32_t)orc_sm64(sera + ((w << 8) | (uint64_t)i)) < P10) p &= ~(1ull << i);
+        return p;
+    }
+    uint64_t p = all;
+    if (scheme == ORC_GF256) {
+        int perm[64];
+        for (int j = 0; j < k; j++) perm[j] = j;
+        int e = r < k ? r : k;
+        for (int t = 0; t < e; t++) {
+            uint64_t h = orc_sm64(sera + ((w << 8) | (uint64_t)t));
+            int u = t + (int)(h % (uint64_t)(k - t));
+            int tmp = perm[t]; perm[t] = perm[u]; perm[u] = tmp;
+            p &= ~(1ull << perm[t]);
+        }
+    } else {
+        for (int g = 0; g < r; g++) {
+            int n = (k - g + r - 1) / r;
+            if (n <= 0) continue;
+            int idx = (int)(orc_sm64(sera + ((w << 8) | (uint64_t)g)) % (uint64_t)n);
+            p &= ~(1ull << (g + idx * r));
+        }
+    }
+    return p;
+}
+
+/* ----------------------------------------------------------- a4 / a5 --- */
+void orc_encode(int scheme, int k, int r, uint32_t S, uint32_t stride, uint8_t *win) {
+    if (scheme == ORC_XOR) {
+        /* a4: R_g = xor of S_j, j = g (mod r) */
+        for (int g = 0; g < r; g++) {
+            uint8_t *R = win + (size_t)(k + g) * stride;
+            memset(R, 0, S);
+            for (int j = g; j < k; j += r) {
+                const uint8_t *s = win + (size_t)j * stride;
+                for (uint32_t p = 0; p < S; p++) R[p] ^= s[p];
+            }
+        }
+        return;
+    }
+    /* a5: R_i = sum_j C[i][j] * S_j */
+    uint8_t C[64 * 64];
+    orc_cauchy(k, r, C);
+    for (int i = 0; i < r; i++) {
+        uint8_t *R = win + (size_t)(k + i) * stride;
+        memset(R, 0, S);
+        for (int j = 0; j < k; j++) {
+            const uint8_t *s = win + (size_t)j * stride;
+            uint8_t c = C[i * k + j];
+            for (uint32_t p = 0; p < S; p++) R[p] ^= orc_gf_mul(c, s[p]);
+        }
+    }
+}
+
+/* Gauss-Jordan inverse of an n x n matrix over GF(2^8); returns 0 if singular. */
+static int gf_invert(int n, const uint8_t *A, uint8_t *Ainv) {
+    uint8_t M[16][32];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < 2 * n; j++)
+            M[i][j] = j < n ? A[i * n + j] : (uint8_t)(j - n == i);
+    for (int c = 0; c < n; c++) {
+        int p = -1;
+        for (int i = c; i < n; i++)
+            if (M[i][c]) { p = i; break; }
+        if (p < 0) return 0;
+        if (p != c)
+            for (int j = 0; j < 2 * n; j++) { uint8_t t = M[c][j]; M[c][j] = M[p][j]; M[p][j] = t; }
+        uint8_t iv = orc_gf_inv(M[c][c]);
+        for (int j = 0; j < 2 * n; j++) M[c][j] = orc_gf_mul(M[c][j], iv);
+        for (int i = 0; i < n; i++) {
+            if (i == c || !M[i][c]) continue;
+            uint8_t f = M[i][c];
+            for (int j = 0; j < 2 * n; j++) M[i][j] ^= orc_gf_mul(f, M[c][j]);
+        }
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) Ainv[i * n + j] = M[i][n + j];
+    return 1;
+}
+
+/* ----------------------------------------------------- a6 / a7 / a8 --- */
+int orc_decode(int scheme, int k, int r, uint32_t S, uint32_t stride, uint64_t present,
+               uint8_t *win) {
+    if (scheme == ORC_XOR) {
+        /* a8: a group with exactly one missing source and its repair present */
+        int status = ORC_OK;
+        for (int g = 0; g < r; g++) {
+            int miss = -1, nmiss = 0;
+            for (int j = g; j < k; j += r)
+                if (!((present >> j) & 1)) { miss = j; nmiss++; }
+            if (nmiss == 0) continue;
+            if (nmiss > 1 || !((present >> (k + g)) & 1)) { status = ORC_UNRECOVERABLE; continue; }
+            uint8_t *out = win + (size_t)miss * stride;
+            memcpy(out, win + (size_t)(k + g) * stride, S);
+            for (int j = g; j < k; j += r) {
+                if (j == miss) continue;
+                const uint8_t *s = win + (size_t)j * stride;
+                for (uint32_t p = 0; p < S; p++) out[p] ^= s[p];
+            }
+        }
+        return status;
+    }
+    /* a7: MDS solve with the first e present repairs */
+    int miss[64], e = 0, sel[64], nrep = 0;
+    for (int j = 0; j < k; j++)
+        if (!((present >> j) & 1)) miss[e++] = j;
+    if (e == 0) return ORC_OK;
+    for (int i = 0; i < r; i++)
+        if ((present >> (k + i)) & 1) sel[nrep++] = i;
+    if (nrep < e || e > 16) return ORC_UNRECOVERABLE;
+    uint8_t C[64 * 64], A[16 * 16], Ai[16 * 16];
+    orc_cauchy(k, r, C);
+    for (int t = 0; t < e; t++)
+        for (int u = 0; u < e; u++) A[t * e + u] = C[sel[t] * k + miss[u]];
+    if (!gf_invert(e, A, Ai)) return ORC_UNRECOVERABLE;
+    uint8_t s[16];
+    for (uint32_t p = 0; p < S; p++) {
+        for (int t = 0; t < e; t++) {
+            uint8_t v = win[(size_t)(k + sel[t]) * stride + p];
+            for (int j = 0; j < k; j++)
+                if ((present >> j) & 1) v ^= orc_gf_mul(C[sel[t] * k + j], win[(size_t)j * stride + p]);
+            s[t] = v;
+        }
+        for (int u = 0; u < e; u++) {
+            uint8_t v = 0;
+            for (int t = 0; t < e; t++) v ^= orc_gf_mul(Ai[u * e + t], s[t]);
+            win[(size_t)miss[u] * stride + p] = v;
+        }
+    }
+    return ORC_OK;
+}
+
+/* ---------------------------------------------------------------- A.6 --- */
+/* Window digest: XOR over symbols i and 8-byte little-endian words t of
+ * sm64(word ^ (w-independent key (i<<16)|t)); bytes >= S count as zero. The
+ * batch digest XORs window digests mixed with the window id. */
+uint64_t orc_window_digest(int k, int r, uint32_t S, uint32_t stride, const uint8_t *win) {
+    uint64_t d = 0;
+    for (int i = 0; i < k + r; i++) {
+        const uint8_t *s = win + (size_t)i * stride;
+        for (uint32_t t = 0; t * 8 < S; t++) {
+            uint64_t word = 0;
+            for (int b = 0; b < 8; b++) {
+                uint32_t o = t * 8 + b;
+                if (o < S) word |= (uint64_t)s[o] << (8 * b);
+            }
+            d ^= orc_sm64(word ^ (((uint64_t)i << 16) | t));
+        }
+    }
+    return d;
+}
+
+/* --------------------------------------------------------------- batch --- */
+typedef struct {
+    int op, scheme, k, r;
+    const uint32_t *S;
+    uint32_t stride;
+    uint64_t lo, hi;
+    const uint64_t *present;
+    uint8_t *status, *wins;
+} job_t;
+
+static void *run_job(void *p) {
+    job_t *j = (job_t *)p;
+    size_t wbytes = (size_t)(j->k + j->r) * j->stride;
+    for (uint64_t w = j->lo; w < j->hi; w++) {
+        uint8_t *win = j->wins + w * wbytes;
+        if (j->op == 0)
+            orc_encode(j->scheme, j->k, j->r, j->S[w], j->stride, win);
+        else
+            j->status[w] = (uint8_t)orc_decode(j->scheme, j->k, j->r, j->S[w], j->stride,
+                                               j->present[w], win);
+    }
+    return NULL;
+}
+
+static void run_batch(job_t proto, uint64_t nwin, int nthreads) {
+    gf_init();
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    job_t jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = proto;
+        jobs[t].lo = nwin * (uint64_t)t / (uint64_t)nthreads;
+        jobs[t].hi = nwin * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        if (nthreads == 1) run_job(&jobs[t]);
+        else pthread_create(&th[t], NULL, run_job, &jobs[t]);
+    }
+    if (nthreads > 1)
+        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+void orc_encode_batch(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                      uint64_t nwin, uint8_t *wins, int nthreads) {
+    job_t j = {0, scheme, k, r, S, stride, 0, 0, NULL, NULL, wins};
+    run_batch(j, nwin, nthreads);
+}
+
+void orc_decode_batch(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                      uint64_t nwin, const uint64_t *present, uint8_t *status, uint8_t *wins,
+                      int nthreads) {
+    job_t j = {1, scheme, k, r, S, stride, 0, 0, present, status, wins};
+    run_batch(j, nwin, nthreads);
+}

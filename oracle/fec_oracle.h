@@ -1,0 +1,77 @@
+/*
+ * fec_oracle.h — CPU oracle for the FEC hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * link or call this.  The product (quic-fec-eps_amd/, libfecgpu.so) never
+ * does: it has no CPU fallback.
+ *
+ * PARITY UNPINNED.  The reference (holzingk/quic-fec-eps, fec branch;
+ * /root/reference/README.md:7) is mounted as a README only: no Rust source,
+ * no Cargo.lock, no tests, no golden vectors.  This file
+ * restates the coding contract the build owns
+ * and is pinned only by
+ *   - GF(2^8)/0x11D known-answer facts and an exhaustive
+ *     cross-check against sympy.polys.galoistools (tests/test_oracle_field.py),
+ *   - an independent numpy restatement (oracle/np_oracle.py) that generated
+ *     the committed fixtures in tests/golden/ (tests/golden/make_golden.py),
+ *   - algebraic invariants (decode∘erase∘encode = id, MDS decodability).
+ * Decode output is pinned by construction (recovered bytes == originals).
+ *
+ * Layout (Appendix A.4): a window is (k + r) symbols of `stride` bytes,
+ * sources 0..k-1 then repairs k..k+r-1; only bytes [0, S) of each symbol are
+ * meaningful (A.3).
+ */
+#ifndef FEC_ORACLE_H
+#define FEC_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_XOR = 0, ORC_GF256 = 1 };
+enum { ORC_FIXED = 0, ORC_LENPREFIX = 1 };
+enum { ORC_OK = 0, ORC_UNRECOVERABLE = 1 };
+
+/* A.1 field */
+uint8_t orc_gf_mul(uint8_t a, uint8_t b);
+uint8_t orc_gf_inv(uint8_t a);
+uint8_t orc_gf_exp(int i);
+int     orc_gf_log(uint8_t a);
+/* A.2 matrix: C[i*k + j] = inv((k + i) ^ j) */
+void    orc_cauchy(int k, int r, uint8_t *C);
+
+/* A.5 PRNG / workload */
+uint64_t orc_sm64(uint64_t x);
+/* packet length of source j of window w for a workload */
+uint32_t orc_pkt_len(int workload, uint64_t seed, uint64_t w, int j, int k, uint32_t L);
+/* symbol length S of window w */
+uint32_t orc_sym_len(int workload, uint64_t seed, uint64_t w, int k, uint32_t L);
+/* fill the k source symbols of window w (framing applied, zero padded to stride) */
+void     orc_fill_window(int workload, uint64_t seed, uint64_t w, int k, int r, uint32_t L,
+                         uint32_t stride, uint8_t *win);
+/* present mask (bit i: symbol i received) for window w */
+uint64_t orc_present(int erasure, uint64_t seed, uint64_t w, int scheme, int k, int r);
+
+/* coding: in place on one window */
+void orc_encode(int scheme, int k, int r, uint32_t S, uint32_t stride, uint8_t *win);
+/* recovers missing sources in place; returns ORC_OK or ORC_UNRECOVERABLE.
+ * For XOR, recoverable groups are recovered even when the window is not. */
+int  orc_decode(int scheme, int k, int r, uint32_t S, uint32_t stride, uint64_t present,
+                uint8_t *win);
+
+/* A.6 digest of one window's emitted bytes: repairs, then sources (all of them) */
+uint64_t orc_window_digest(int k, int r, uint32_t S, uint32_t stride, const uint8_t *win);
+
+/* batch helpers (uniform stride, windows back to back), pthreads over windows */
+void orc_encode_batch(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                      uint64_t nwin, uint8_t *wins, int nthreads);
+void orc_decode_batch(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                      uint64_t nwin, const uint64_t *present, uint8_t *status, uint8_t *wins,
+                      int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,212 @@
+"""Independent numpy restatement of the coding contract — TEST INFRASTRUCTURE ONLY.
+
+Written separately from fec_oracle.c (different derivations on purpose):
+  * field multiply by carry-less shift-and-add with reduction by 0x11D
+    (no log/exp tables), inverse by exhaustive search;
+  * encode as a vectorised matrix product through a 256x256 product table;
+  * decode by solving the full (k+r) x k generator system restricted to the
+    received rows with Gauss-Jordan on the augmented byte matrix.
+Used to cross-check the C oracle and to generate tests/golden/ fixtures
+(tests/golden/make_golden.py).  PARITY UNPINNED: the
+reference fec branch is not mounted (/root/reference/README.md:7 is a URL).
+Contract clauses: SURVEY.md Appendix A.1-A.6, DESIGN.md §Workloads.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M64 = (1 << 64) - 1
+POLY = 0x11D
+
+
+def clmul_mod(a: int, b: int) -> int:
+    """A.1: a*b in GF(2^8)/0x11D by shift-and-add."""
+    p = 0
+    for _ in range(8):
+        if b & 1:
+            p ^= a
+        b >>= 1
+        a <<= 1
+        if a & 0x100:
+            a ^= POLY
+    return p
+
+
+_MUL = np.array([[clmul_mod(a, b) for b in range(256)] for a in range(256)], np.uint8)
+_INV = np.zeros(256, np.uint8)
+for _a in range(1, 256):
+    _INV[_a] = int(np.nonzero(_MUL[_a] == 1)[0][0])
+
+
+def mul_table() -> np.ndarray:
+    return _MUL
+
+
+def inv(a: int) -> int:
+    return int(_INV[a])
+
+
+def cauchy(k: int, r: int) -> np.ndarray:
+    """A.2: C[i][j] = inv((k+i) ^ j)."""
+    return np.array([[_INV[(k + i) ^ j] for j in range(k)] for i in range(r)], np.uint8)
+
+
+def generator(scheme: str, k: int, r: int) -> np.ndarray:
+    """Systematic (k+r) x k generator: identity on top, repair rows below."""
+    G = np.zeros((k + r, k), np.uint8)
+    G[:k] = np.eye(k, dtype=np.uint8)
+    if scheme == "xor":
+        for g in range(r):
+            G[k + g, g::r] = 1
+    else:
+        G[k:] = cauchy(k, r)
+    return G
+
+
+def matmul(A: np.ndarray, X: np.ndarray) -> np.ndarray:
+    """GF(2^8) product A (m x n) times X (n x L)."""
+    out = np.zeros((A.shape[0], X.shape[1]), np.uint8)
+    for i in range(A.shape[0]):
+        acc = np.zeros(X.shape[1], np.uint8)
+        for j in range(A.shape[1]):
+            if A[i, j]:
+                acc ^= _MUL[A[i, j]][X[j]]
+        out[i] = acc
+    return out
+
+
+def encode(scheme: str, k: int, r: int, src: np.ndarray) -> np.ndarray:
+    """src [k, L] -> repairs [r, L]."""
+    return matmul(generator(scheme, k, r)[k:], src)
+
+
+def decode(scheme: str, k: int, r: int, sym: np.ndarray, present: int):
+    """sym [k+r, L] with garbage in erased rows -> (sources [k, L], ok).
+
+    GF: solve G[rows] x = sym[rows] over k unknowns by Gauss-Jordan on the
+    augmented matrix, using received sources plus the first e received repairs.
+    XOR: per group (A.2), one missing member and its repair present.
+    """
+    L = sym.shape[1]
+    src = sym[:k].copy()
+    missing = [j for j in range(k) if not (present >> j) & 1]
+    if not missing:
+        return src, True
+    if scheme == "xor":
+        ok = True
+        for g in range(r):
+            grp = list(range(g, k, r))
+            miss = [j for j in grp if j in missing]
+            if not miss:
+                continue
+            if len(miss) > 1 or not (present >> (k + g)) & 1:
+                ok = False
+                continue
+            acc = sym[k + g].copy()
+            for j in grp:
+                if j != miss[0]:
+                    acc ^= sym[j]
+            src[miss[0]] = acc
+        return src, ok
+    reps = [k + i for i in range(r) if (present >> (k + i)) & 1]
+    if len(reps) < len(missing):
+        return src, False
+    rows = [j for j in range(k) if (present >> j) & 1] + reps[: len(missing)]
+    G = generator("gf", k, r)
+    A = np.concatenate([G[rows], sym[rows]], axis=1).astype(np.uint8)  # k x (k+L)
+    n = k
+    for c in range(n):
+        piv = next(i for i in range(c, n) if A[i, c])
+        A[[c, piv]] = A[[piv, c]]
+        A[c] = _MUL[_INV[A[c, c]]][A[c]]
+        for i in range(n):
+            if i != c and A[i, c]:
+                A[i] ^= _MUL[A[i, c]][A[c]]
+    return A[:, k:k + L].copy(), True
+
+
+# ------------------------------------------------------------ workloads ---
+TAG_PAY = 0x5041594C4F414400
+TAG_MTU = 0x4D54550000000000
+TAG_LEN = 0x4C454E0000000000
+TAG_ERA = 0x4552415345000000
+P10 = 429496730
+
+
+def sm64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M64
+    return x ^ (x >> 31)
+
+
+def sm64_np(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def pkt_len(workload: int, seed: int, w: int, j: int, L: int) -> int:
+    if workload == 0:
+        return L
+    mtu = 9000 if sm64((sm64(seed ^ TAG_MTU) + w) & M64) & 1 else 1200
+    h = sm64((sm64(seed ^ TAG_LEN) + ((w << 8) | j)) & M64)
+    if (h & 0xFFFFFFFF) < P10:
+        return 64 + (h >> 32) % (mtu - 63)
+    return mtu
+
+
+def payload(seed: int, w: int, j: int, n: int) -> np.ndarray:
+    spay = sm64(seed ^ TAG_PAY)
+    words = np.arange((n + 7) // 8, dtype=np.uint64) + np.uint64(((w << 24) | (j << 16)) & M64)
+    with np.errstate(over="ignore"):
+        hw = sm64_np(words + np.uint64(spay))
+    return hw.view(np.uint8)[:n].copy()  # little-endian host
+
+
+def window(workload: int, seed: int, w: int, k: int, L: int):
+    """-> (list of k packets, S, symbols [k, S])"""
+    pkts = [payload(seed, w, j, pkt_len(workload, seed, w, j, L)) for j in range(k)]
+    if workload == 0:
+        S = L
+        return pkts, S, np.stack(pkts)
+    S = 2 + max(len(p) for p in pkts)
+    sym = np.zeros((k, S), np.uint8)
+    for j, p in enumerate(pkts):
+        sym[j, 0], sym[j, 1] = len(p) >> 8, len(p) & 0xFF
+        sym[j, 2:2 + len(p)] = p
+    return pkts, S, sym
+
+
+def present(erasure: int, seed: int, w: int, scheme: str, k: int, r: int) -> int:
+    allm = (1 << (k + r)) - 1
+    sera = sm64(seed ^ TAG_ERA)
+    if erasure == 0:
+        return allm
+    p = allm
+    if erasure == 2:
+        for i in range(k + r):
+            if (sm64((sera + ((w << 8) | i)) & M64) & 0xFFFFFFFF) < P10:
+                p &= ~(1 << i)
+        return p
+    if scheme == "gf":
+        perm = list(range(k))
+        for t in range(min(r, k)):
+            u = t + sm64((sera + ((w << 8) | t)) & M64) % (k - t)
+            perm[t], perm[u] = perm[u], perm[t]
+            p &= ~(1 << perm[t])
+        return p
+    for g in range(r):
+        n = (k - g + r - 1) // r
+        if n <= 0:
+            continue
+        idx = sm64((sera + ((w << 8) | g)) & M64) % n
+        p &= ~(1 << (g + idx * r))
+    return p
+
+
+def deframe(sym: np.ndarray) -> np.ndarray:
+    """a9: LENPREFIX symbol -> packet payload."""
+    n = (int(sym[0]) << 8) | int(sym[1])
+    return sym[2:2 + n]

@@ -1,0 +1,146 @@
+"""ctypes wrapper over oracle/_build/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, always as the checker, never as the measured or shipped path.
+PARITY UNPINNED: see fec_oracle.h for what pins the oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+XOR, GF256 = 0, 1
+FIXED_WL, MIXED_WL = 0, 1            # workloads
+ERA_NONE, ERA_EXACT, ERA_IID = 0, 1, 2
+OK, UNRECOVERABLE = 0, 1
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc only)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8, u32, u64, i32 = ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        vp = ctypes.c_void_p
+        sig = {
+            "orc_gf_mul": (u8, [u8, u8]),
+            "orc_gf_inv": (u8, [u8]),
+            "orc_gf_exp": (u8, [i32]),
+            "orc_gf_log": (i32, [u8]),
+            "orc_cauchy": (None, [i32, i32, vp]),
+            "orc_sm64": (u64, [u64]),
+            "orc_pkt_len": (u32, [i32, u64, u64, i32, i32, u32]),
+            "orc_sym_len": (u32, [i32, u64, u64, i32, u32]),
+            "orc_fill_window": (None, [i32, u64, u64, i32, i32, u32, u32, vp]),
+            "orc_present": (u64, [i32, u64, u64, i32, i32, i32]),
+            "orc_encode": (None, [i32, i32, i32, u32, u32, vp]),
+            "orc_decode": (i32, [i32, i32, i32, u32, u32, u64, vp]),
+            "orc_window_digest": (u64, [i32, i32, u32, u32, vp]),
+            "orc_encode_batch": (None, [i32, i32, i32, vp, u32, u64, vp, i32]),
+            "orc_decode_batch": (None, [i32, i32, i32, vp, u32, u64, vp, vp, vp, i32]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def gf_mul(a: int, b: int) -> int:
+    return lib().orc_gf_mul(a, b)
+
+
+def gf_inv(a: int) -> int:
+    return lib().orc_gf_inv(a)
+
+
+def cauchy(k: int, r: int) -> np.ndarray:
+    C = np.zeros((r, k), np.uint8)
+    lib().orc_cauchy(k, r, _p(C))
+    return C
+
+
+def sm64(x: int) -> int:
+    return lib().orc_sm64(x & 0xFFFFFFFFFFFFFFFF)
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def sym_lens(workload: int, seed: int, w0: int, nwin: int, k: int, L: int) -> np.ndarray:
+    f = lib().orc_sym_len
+    return np.array([f(workload, seed, w0 + w, k, L) for w in range(nwin)], np.uint32)
+
+
+def make_windows(workload: int, seed: int, w0: int, nwin: int, k: int, r: int, L: int,
+                 stride: int) -> np.ndarray:
+    """[nwin, k+r, stride] u8 with sources filled, repairs zero (A.3/A.4)."""
+    wins = np.zeros((nwin, k + r, stride), np.uint8)
+    f = lib().orc_fill_window
+    for w in range(nwin):
+        f(workload, seed, w0 + w, k, r, L, stride, _p(wins[w]))
+    return wins
+
+
+def presents(erasure: int, seed: int, w0: int, nwin: int, scheme: int, k: int, r: int) -> np.ndarray:
+    f = lib().orc_present
+    return np.array([f(erasure, seed, w0 + w, scheme, k, r) for w in range(nwin)], np.uint64)
+
+
+def encode_batch(scheme: int, k: int, r: int, S: np.ndarray, wins: np.ndarray, nthreads: int = 1):
+    nwin, _, stride = wins.shape
+    S = np.ascontiguousarray(S, np.uint32)
+    lib().orc_encode_batch(scheme, k, r, _p(S), stride, nwin, _p(wins), nthreads)
+
+
+def decode_batch(scheme: int, k: int, r: int, S: np.ndarray, wins: np.ndarray,
+                 present: np.ndarray, nthreads: int = 1) -> np.ndarray:
+    nwin, _, stride = wins.shape
+    S = np.ascontiguousarray(S, np.uint32)
+    present = np.ascontiguousarray(present, np.uint64)
+    status = np.zeros(nwin, np.uint8)
+    lib().orc_decode_batch(scheme, k, r, _p(S), stride, nwin, _p(present), _p(status), _p(wins),
+                           nthreads)
+    return status
+
+
+def erase(wins: np.ndarray, present: np.ndarray, k: int, r: int, fill: int = 0) -> None:
+    """Overwrite every symbol whose present bit is clear (proves decode never reads it)."""
+    for w in range(wins.shape[0]):
+        p = int(present[w])
+        for i in range(k + r):
+            if not (p >> i) & 1:
+                wins[w, i, :] = fill
+
+
+def window_digest(k: int, r: int, S: int, win: np.ndarray) -> int:
+    return lib().orc_window_digest(k, r, S, win.shape[-1], _p(np.ascontiguousarray(win)))
+
+
+def batch_digest(k: int, r: int, S: np.ndarray, wins: np.ndarray, w0: int = 0) -> int:
+    """XOR over windows of sm64(window_digest + global window id)."""
+    d = 0
+    for w in range(wins.shape[0]):
+        d ^= sm64(window_digest(k, r, int(S[w]), wins[w]) + w0 + w)
+    return d

@@ -1,0 +1,421 @@
+// fec_capi.cpp — C ABI (include/fecgpu.h) over the gfx950 kernels.
+//
+// Validation happens before any HIP call so argument errors are reported the
+// same on hosts without a GPU.  There is no CPU fallback: without a device
+// every compute entry point returns FECGPU_ERR_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/fecgpu.h"
+#include "fec_internal.h"
+
+using namespace fecgpu;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+ssize_t dev_err(hipError_t e, const char *what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return FECGPU_ERR_DEVICE;
+}
+
+#define HIP_TRY(expr, what)                          \
+    do {                                             \
+        hipError_t e_ = (expr);                      \
+        if (e_ != hipSuccess) return dev_err(e_, what); \
+    } while (0)
+
+uint8_t host_gf_mul(uint8_t a, uint8_t b) {
+    static constexpr GfTables t = make_gf_tables();
+    if (!a || !b) return 0;
+    return t.exp[t.log[a] + t.log[b]];
+}
+uint8_t host_gf_inv(uint8_t a) {
+    static constexpr GfTables t = make_gf_tables();
+    return t.exp[255 - t.log[a]];
+}
+
+struct EncTables {
+    uint4 *ab = nullptr;
+    uint32_t *c = nullptr;
+};
+
+}  // namespace
+
+struct fecgpu_ctx {
+    std::vector<int> devs;
+    std::mutex mu;
+    // (device, k, r) -> Cauchy encode tables on that device
+    std::map<std::tuple<int, int, int>, EncTables> enc;
+    // host-pointer staging per device
+    std::map<int, std::pair<void *, size_t>> stage;
+};
+
+extern "C" {
+
+int fecgpu_abi_version(void) { return FECGPU_ABI_VERSION; }
+
+const char *fecgpu_strerror(ssize_t err) {
+    switch (err) {
+        case FECGPU_ERR_DONE: return "done";
+        case FECGPU_ERR_BUFFER_TOO_SHORT: return "buffer too short";
+        case FECGPU_ERR_INVALID_ARG: return "invalid argument";
+        case FECGPU_ERR_UNSUPPORTED: return "unsupported";
+        case FECGPU_ERR_DEVICE: return "device error";
+        case FECGPU_ERR_UNRECOVERABLE: return "unrecoverable";
+        default: return err >= 0 ? "ok" : "unknown error";
+    }
+}
+
+const char *fecgpu_last_error(void) { return g_last_error.c_str(); }
+
+ssize_t fecgpu_code_check(const fecgpu_code *code) {
+    if (!code) return FECGPU_ERR_INVALID_ARG;
+    if (code->scheme != FECGPU_SCHEME_XOR && code->scheme != FECGPU_SCHEME_GF256)
+        return FECGPU_ERR_INVALID_ARG;
+    if (code->framing != FECGPU_FRAMING_FIXED && code->framing != FECGPU_FRAMING_LENPREFIX)
+        return FECGPU_ERR_INVALID_ARG;
+    if (code->k < 1 || code->r < 1) return FECGPU_ERR_INVALID_ARG;
+    if (code->k + code->r > FECGPU_MAX_K) return FECGPU_ERR_UNSUPPORTED;
+    if (code->r > FECGPU_MAX_R) return FECGPU_ERR_UNSUPPORTED;
+    if (code->scheme == FECGPU_SCHEME_XOR && code->r > code->k) return FECGPU_ERR_INVALID_ARG;
+    if (code->scheme == FECGPU_SCHEME_GF256 && code->matrix != FECGPU_MATRIX_CAUCHY)
+        return FECGPU_ERR_UNSUPPORTED;
+    if (code->poly != 0 && code->poly != 0x11D) return FECGPU_ERR_UNSUPPORTED;
+    return 0;
+}
+
+ssize_t fecgpu_ctx_new(const int *devs, int ndev, fecgpu_ctx **out) {
+    if (!out || ndev < 0 || (ndev > 0 && !devs)) return FECGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) {
+        g_last_error = "no HIP device";
+        return FECGPU_ERR_DEVICE;
+    }
+    auto *c = new fecgpu_ctx();
+    if (ndev == 0) {
+        int d = 0;
+        HIP_TRY(hipGetDevice(&d), "hipGetDevice");
+        c->devs.push_back(d);
+    } else {
+        for (int i = 0; i < ndev; i++) {
+            if (devs[i] < 0 || devs[i] >= count) {
+                delete c;
+                return FECGPU_ERR_INVALID_ARG;
+            }
+            c->devs.push_back(devs[i]);
+        }
+    }
+    *out = c;
+    return 0;
+}
+
+void fecgpu_ctx_free(fecgpu_ctx *ctx) {
+    if (!ctx) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto &kv : ctx->enc) {
+        (void)hipSetDevice(std::get<0>(kv.first));
+        (void)hipFree(kv.second.ab);
+        (void)hipFree(kv.second.c);
+    }
+    for (auto &kv : ctx->stage) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second.first);
+    }
+    (void)hipSetDevice(cur);
+    delete ctx;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Cauchy tables for (k, r) on the current device, built once per ctx.
+ssize_t get_enc_tables(fecgpu_ctx *ctx, int k, int r, EncTables &out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    auto key = std::make_tuple(dev, k, r);
+    auto it = ctx->enc.find(key);
+    if (it != ctx->enc.end()) {
+        out = it->second;
+        return 0;
+    }
+    std::vector<uint4> ab((size_t)k * r);
+    std::vector<uint32_t> cc((size_t)k * r);
+    for (int j = 0; j < k; j++)
+        for (int i = 0; i < r; i++) {
+            const uint8_t coef = host_gf_inv((uint8_t)((k + i) ^ j));  // A.2 Cauchy
+            const CoefTab t = make_coef_tab(coef);
+            ab[(size_t)j * r + i] = make_uint4(t.a_lo, t.a_hi, t.b_lo, t.b_hi);
+            cc[(size_t)j * r + i] = t.c;
+        }
+    EncTables t;
+    HIP_TRY(hipMalloc(&t.ab, ab.size() * sizeof(uint4)), "hipMalloc");
+    HIP_TRY(hipMalloc(&t.c, cc.size() * sizeof(uint32_t)), "hipMalloc");
+    HIP_TRY(hipMemcpy(t.ab, ab.data(), ab.size() * sizeof(uint4), hipMemcpyHostToDevice), "hipMemcpy");
+    HIP_TRY(hipMemcpy(t.c, cc.data(), cc.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy");
+    ctx->enc[key] = t;
+    out = t;
+    return 0;
+}
+
+// Windows per workgroup: fill the 256 lanes with whole passes over the
+// flattened column range while keeping the LDS footprint small enough for
+// >= 4 workgroups per CU.
+int choose_wpb(uint32_t ncol, uint32_t lds_per_win, uint32_t lds_budget) {
+    int maxw = kMaxWpb;
+    if (lds_per_win) maxw = std::max(1, std::min<int>(maxw, (int)(lds_budget / lds_per_win)));
+    if (ncol == 0) return maxw;
+    int best = 1;
+    double best_u = -1;
+    for (int w = 1; w <= maxw; w++) {
+        const uint64_t slots = (uint64_t)w * ncol;
+        const uint64_t passes = (slots + kBlock - 1) / kBlock;
+        const double u = (double)slots / (double)(passes * kBlock);
+        // prefer >= 2 passes per workgroup so setup is amortised
+        const double score = u - (passes < 2 ? 0.05 : 0.0);
+        if (score > best_u + 1e-9) {
+            best_u = score;
+            best = w;
+        }
+    }
+    return best;
+}
+
+ssize_t validate_batch(const fecgpu_code *code, const void *win, const uint32_t *sym_len,
+                       uint32_t sym_len_all, uint32_t stride, const uint64_t *win_off) {
+    ssize_t rc = fecgpu_code_check(code);
+    if (rc) return rc;
+    if (!win) return FECGPU_ERR_INVALID_ARG;
+    if (!win_off) {
+        if (stride == 0 || (stride & 15)) return FECGPU_ERR_INVALID_ARG;
+        if (!sym_len && sym_len_all > stride) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    }
+    if (!sym_len && sym_len_all == 0) return FECGPU_ERR_INVALID_ARG;
+    if ((reinterpret_cast<uintptr_t>(win) & 15) != 0) return FECGPU_ERR_INVALID_ARG;
+    return 0;
+}
+
+struct HostStage {
+    // device copies for a host-pointer call
+    uint8_t *win = nullptr;
+    uint64_t *off = nullptr;
+    uint32_t *len = nullptr;
+    uint64_t *pres = nullptr;
+    uint8_t *status = nullptr;
+    size_t win_bytes = 0;
+};
+
+ssize_t stage_alloc(fecgpu_ctx *ctx, size_t bytes, void **p) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    auto &s = ctx->stage[dev];
+    if (s.second < bytes) {
+        if (s.first) HIP_TRY(hipFree(s.first), "hipFree");
+        s.first = nullptr;
+        s.second = 0;
+        HIP_TRY(hipMalloc(&s.first, bytes), "hipMalloc staging");
+        s.second = bytes;
+    }
+    *p = s.first;
+    return 0;
+}
+
+size_t host_window_bytes(const fecgpu_code *code, const uint64_t *win_off, const uint32_t *sym_len,
+                         uint32_t sym_len_all, uint32_t stride, uint64_t nwin) {
+    const int n = code->k + code->r;
+    if (!win_off) return (size_t)nwin * n * stride;
+    size_t mx = 0;
+    for (uint64_t w = 0; w < nwin; w++) {
+        const uint32_t S = sym_len ? sym_len[w] : sym_len_all;
+        mx = std::max(mx, (size_t)win_off[w] + (size_t)n * ((S + 15u) & ~15u));
+    }
+    return mx;
+}
+
+ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
+                  const uint64_t *win_off, const uint32_t *sym_len, uint32_t sym_len_all,
+                  uint32_t stride, uint64_t nwin, const uint64_t *present, uint8_t *status,
+                  uint32_t flags, void *stream) {
+    if (!ctx) return FECGPU_ERR_INVALID_ARG;
+    ssize_t rc = validate_batch(code, win, sym_len, sym_len_all, stride, win_off);
+    if (rc) return rc;
+    if (decode && (!present || !status)) return FECGPU_ERR_INVALID_ARG;
+    if (nwin == 0) return 0;
+    const int k = code->k, r = code->r, scheme = (int)code->scheme;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+
+    // host pointers: stage everything on the ctx's first device, synchronously
+    HostStage hs;
+    int prev_dev = -1;
+    if (flags & FECGPU_F_HOST_PTRS) {
+        HIP_TRY(hipGetDevice(&prev_dev), "hipGetDevice");
+        HIP_TRY(hipSetDevice(ctx->devs[0]), "hipSetDevice");
+        hs.win_bytes = host_window_bytes(code, win_off, sym_len, sym_len_all, stride, nwin);
+        const size_t o_off = (hs.win_bytes + 255) & ~size_t(255);
+        const size_t o_len = o_off + (win_off ? ((nwin * 8 + 255) & ~size_t(255)) : 0);
+        const size_t o_pres = o_len + (sym_len ? ((nwin * 4 + 255) & ~size_t(255)) : 0);
+        const size_t o_stat = o_pres + (decode ? ((nwin * 8 + 255) & ~size_t(255)) : 0);
+        const size_t total = o_stat + (decode ? nwin : 0) + 256;
+        void *base = nullptr;
+        rc = stage_alloc(ctx, total, &base);
+        if (rc) return rc;
+        uint8_t *b = static_cast<uint8_t *>(base);
+        hs.win = b;
+        HIP_TRY(hipMemcpyAsync(hs.win, win, hs.win_bytes, hipMemcpyHostToDevice, s), "H2D win");
+        if (win_off) {
+            hs.off = reinterpret_cast<uint64_t *>(b + o_off);
+            HIP_TRY(hipMemcpyAsync(hs.off, win_off, nwin * 8, hipMemcpyHostToDevice, s), "H2D off");
+        }
+        if (sym_len) {
+            hs.len = reinterpret_cast<uint32_t *>(b + o_len);
+            HIP_TRY(hipMemcpyAsync(hs.len, sym_len, nwin * 4, hipMemcpyHostToDevice, s), "H2D len");
+        }
+        if (decode) {
+            hs.pres = reinterpret_cast<uint64_t *>(b + o_pres);
+            hs.status = b + o_stat;
+            HIP_TRY(hipMemcpyAsync(hs.pres, present, nwin * 8, hipMemcpyHostToDevice, s), "H2D present");
+        }
+    }
+
+    BatchArgs a{};
+    a.win = hs.win ? hs.win : win;
+    a.win_off = hs.win ? hs.off : win_off;
+    a.sym_len = hs.win ? hs.len : sym_len;
+    a.present = hs.win ? hs.pres : present;
+    a.status = hs.win ? hs.status : status;
+    a.nwin = nwin;
+    a.S_all = sym_len_all;
+    a.stride = stride;
+    a.k = k;
+    a.r = r;
+    for (int g = 0; g < kMaxR; g++) {
+        uint64_t m = 0;
+        if (g < r)
+            for (int j = g; j < k; j += r) m |= 1ull << j;
+        a.gmask[g] = m;
+    }
+    // column estimate for the windows-per-workgroup choice
+    uint32_t ncol = 0;
+    if (!sym_len) ncol = (sym_len_all + 15u) >> 4;
+    else if (!win_off) ncol = stride >> 4;
+
+    LaunchPlan p{};
+    if (!decode) {
+        if (scheme == FECGPU_SCHEME_GF256) {
+            EncTables t;
+            rc = get_enc_tables(ctx, k, r, t);
+            if (rc) return rc;
+            a.enc_ab = t.ab;
+            a.enc_c = t.c;
+            p.lds_bytes = (uint32_t)(k * r * 20);
+        }
+        p.wpb = choose_wpb(ncol, 0, 0);
+    } else {
+        if (scheme == FECGPU_SCHEME_GF256) {
+            p.win_lds = gf_dec_win_lds(k, r);
+            p.wpb = choose_wpb(ncol, p.win_lds, 40 * 1024);
+            p.lds_bytes = p.win_lds * (uint32_t)p.wpb;
+        } else {
+            p.wpb = choose_wpb(ncol, 0, 0);
+        }
+    }
+    a.wpb = p.wpb;
+    a.win_lds = p.win_lds;
+    p.blocks = (nwin + p.wpb - 1) / p.wpb;
+    if (p.blocks > 0x7FFFFFFFull) return FECGPU_ERR_UNSUPPORTED;
+
+    hipError_t e = decode ? launch_decode(scheme, a, p, s) : launch_encode(scheme, a, p, s);
+    if (e != hipSuccess) return dev_err(e, decode ? "decode launch" : "encode launch");
+
+    if (hs.win) {
+        HIP_TRY(hipMemcpyAsync(win, hs.win, hs.win_bytes, hipMemcpyDeviceToHost, s), "D2H win");
+        if (decode)
+            HIP_TRY(hipMemcpyAsync(status, hs.status, nwin, hipMemcpyDeviceToHost, s), "D2H status");
+        HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+        HIP_TRY(hipSetDevice(prev_dev), "hipSetDevice");
+    } else if (flags & FECGPU_F_SYNC) {
+        HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+    }
+    return (ssize_t)nwin;
+}
+
+}  // namespace
+
+extern "C" {
+
+ssize_t fecgpu_encode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *win,
+                            const uint64_t *win_off, const uint32_t *sym_len,
+                            uint32_t sym_len_all, uint32_t stride, uint64_t nwin,
+                            uint32_t flags, void *stream) {
+    return run_batch(ctx, code, false, win, win_off, sym_len, sym_len_all, stride, nwin, nullptr,
+                     nullptr, flags, stream);
+}
+
+ssize_t fecgpu_decode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *win,
+                            const uint64_t *win_off, const uint32_t *sym_len,
+                            uint32_t sym_len_all, uint32_t stride, uint64_t nwin,
+                            const uint64_t *present, uint8_t *status, uint32_t flags,
+                            void *stream) {
+    return run_batch(ctx, code, true, win, win_off, sym_len, sym_len_all, stride, nwin, present,
+                     status, flags, stream);
+}
+
+ssize_t fecgpu_synth_batch(fecgpu_ctx *ctx, const fecgpu_code *code, int workload, uint64_t seed,
+                           uint64_t w0, uint8_t *win, uint32_t *sym_len, uint32_t L,
+                           uint32_t stride, uint64_t nwin, void *stream) {
+    if (!ctx || !win) return FECGPU_ERR_INVALID_ARG;
+    ssize_t rc = fecgpu_code_check(code);
+    if (rc) return rc;
+    if (workload != 0 && workload != 1) return FECGPU_ERR_INVALID_ARG;
+    if (stride == 0 || (stride & 15)) return FECGPU_ERR_INVALID_ARG;
+    if (workload == 0 && (L == 0 || L > stride)) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    if (workload == 1 && (stride < 9002 || !sym_len)) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    if (nwin > 0x7FFFFFFFull) return FECGPU_ERR_UNSUPPORTED;
+    SynthArgs a{win, sym_len, seed, w0, nwin, L, stride, code->k, code->r, workload};
+    hipError_t e = launch_synth(a, reinterpret_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return dev_err(e, "synth launch");
+    return (ssize_t)nwin;
+}
+
+ssize_t fecgpu_erasure_batch(fecgpu_ctx *ctx, const fecgpu_code *code, int erasure, uint64_t seed,
+                             uint64_t w0, uint64_t *present, uint64_t nwin, void *stream) {
+    if (!ctx || !present) return FECGPU_ERR_INVALID_ARG;
+    ssize_t rc = fecgpu_code_check(code);
+    if (rc) return rc;
+    if (erasure < 0 || erasure > 2) return FECGPU_ERR_INVALID_ARG;
+    EraseArgs a{present, seed, w0, nwin, code->k, code->r, (int)code->scheme, erasure};
+    hipError_t e = launch_erasure(a, reinterpret_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return dev_err(e, "erasure launch");
+    return (ssize_t)nwin;
+}
+
+ssize_t fecgpu_digest_batch(fecgpu_ctx *ctx, const fecgpu_code *code, const uint8_t *win,
+                            const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
+                            uint64_t w0, uint64_t nwin, uint64_t *digest, void *stream) {
+    if (!ctx || !win || !digest) return FECGPU_ERR_INVALID_ARG;
+    ssize_t rc = fecgpu_code_check(code);
+    if (rc) return rc;
+    if (stride == 0 || (stride & 15)) return FECGPU_ERR_INVALID_ARG;
+    if (!sym_len && (sym_len_all == 0 || sym_len_all > stride)) return FECGPU_ERR_INVALID_ARG;
+    if (nwin > 0x7FFFFFFFull) return FECGPU_ERR_UNSUPPORTED;
+    DigestArgs a{win, sym_len, digest, w0, nwin, sym_len_all, stride, code->k, code->r};
+    hipError_t e = launch_digest(a, reinterpret_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return dev_err(e, "digest launch");
+    return (ssize_t)nwin;
+}
+
+}  // extern "C"

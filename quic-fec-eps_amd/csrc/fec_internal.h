@@ -1,0 +1,74 @@
+// fec_internal.h — launch-side interface between the C ABI (fec_capi.cpp)
+// and the gfx950 kernels (fec_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fec_spec.h"
+
+namespace fecgpu {
+
+constexpr int kBlock = 256;   // 4 waves of 64
+constexpr int kMaxWpb = 64;   // windows per workgroup (per-window header in static LDS)
+constexpr int kMaxK = 64;
+constexpr int kMaxR = 8;
+
+// Geometry + decode inputs of one batch, passed by value as the kernel argument.
+struct BatchArgs {
+    uint8_t *win;
+    const uint64_t *win_off;   // nullable: ragged windows
+    const uint32_t *sym_len;   // nullable: every window S_all
+    const uint64_t *present;   // decode
+    uint8_t *status;           // decode
+    const uint4 *enc_ab;       // encode tables [k][r] (TA lo/hi, TB lo/hi)
+    const uint32_t *enc_c;     // encode tables [k][r] (TC)
+    uint64_t nwin;
+    uint64_t gmask[kMaxR];     // XOR: members of group g (bit j)
+    uint32_t S_all;
+    uint32_t stride;
+    int k, r;
+    int wpb;                   // windows per workgroup
+    uint32_t win_lds;          // decode: LDS bytes per window region
+};
+
+struct LaunchPlan {
+    int wpb;
+    uint32_t lds_bytes;  // dynamic LDS per workgroup
+    uint32_t win_lds;    // per-window region (decode)
+    uint64_t blocks;
+};
+
+// Per-window LDS region of the GF decode kernel: tables [k][R] uint4 + [k][R] u32,
+// input symbol list (64 B), output symbol list (16 B).
+inline uint32_t gf_dec_win_lds(int k, int R) { return (uint32_t)(k * R * 20 + 80 + 15) & ~15u; }
+
+hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s);
+hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s);
+
+struct SynthArgs {
+    uint8_t *win;
+    uint32_t *sym_len;
+    uint64_t seed, w0, nwin;
+    uint32_t L, stride;
+    int k, r, workload;
+};
+hipError_t launch_synth(const SynthArgs &a, hipStream_t s);
+
+struct EraseArgs {
+    uint64_t *present;
+    uint64_t seed, w0, nwin;
+    int k, r, scheme, erasure;
+};
+hipError_t launch_erasure(const EraseArgs &a, hipStream_t s);
+
+struct DigestArgs {
+    const uint8_t *win;
+    const uint32_t *sym_len;
+    uint64_t *digest;
+    uint64_t w0, nwin;
+    uint32_t S_all, stride;
+    int k, r;
+};
+hipError_t launch_digest(const DigestArgs &a, hipStream_t s);
+
+}  // namespace fecgpu

@@ -1,0 +1,90 @@
+// fec_spec.h — the coding contract shared by host runtime and gfx950 kernels.
+//
+// A.1 field GF(2^8)/0x11D generator 2, A.2 systematic
+// Cauchy rows C[i][j] = inv((k+i) ^ j) / XOR groups j mod r, A.3 framing,
+// A.5 splitmix64 streams.  Workload and digest definitions: DESIGN.md.
+// The reference fec branch is not mounted (/root/reference/README.md:7),
+// so these are build-owned choices (parity unpinned).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define FEC_HD __host__ __device__ __forceinline__
+#else
+#define FEC_HD inline
+#endif
+
+namespace fecgpu {
+
+// ---------------------------------------------------------------- A.1 ----
+struct GfTables {
+    uint8_t exp[512];
+    uint8_t log[256];
+};
+
+constexpr GfTables make_gf_tables() {
+    GfTables t{};
+    unsigned x = 1;
+    for (int i = 0; i < 255; i++) {
+        t.exp[i] = (uint8_t)x;
+        t.log[x] = (uint8_t)i;
+        x <<= 1;
+        if (x & 0x100) x ^= 0x11D;
+    }
+    for (int i = 255; i < 512; i++) t.exp[i] = t.exp[i - 255];
+    t.log[0] = 0;  // never used: callers test for zero first
+    return t;
+}
+
+// multiply by x (=2) in GF(2^8)/0x11D, one byte in the low 8 bits
+FEC_HD uint32_t gf_xtime(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x1Du : 0u)) & 0xFFu; }
+
+// Product table of one coefficient c for the byte-permute multiply
+// (DESIGN.md §GF multiply):  a data byte x = x[2:0] | x[5:3]<<3 | x[7:6]<<6
+// gives  c*x = TA[x & 7] ^ TB[(x >> 3) & 7] ^ TC[x >> 6].
+// TA/TB are 8-entry byte tables (lo dword = entries 0..3, hi = 4..7),
+// TC a 4-entry table, so each lookup is one v_perm_b32.
+struct CoefTab {
+    uint32_t a_lo, a_hi, b_lo, b_hi;
+    uint32_t c;
+};
+
+FEC_HD CoefTab make_coef_tab(uint32_t c) {
+    uint32_t p[8];
+    p[0] = c & 0xFFu;
+    for (int b = 1; b < 8; b++) p[b] = gf_xtime(p[b - 1]);
+    CoefTab t;
+    // entries v = 0..3 of a 3-bit table over basis (q0, q1, q2): 0, q0, q1, q0^q1
+    t.a_lo = (p[0] << 8) ^ (p[1] << 16) ^ ((p[0] ^ p[1]) << 24);
+    t.a_hi = t.a_lo ^ (p[2] * 0x01010101u);
+    t.b_lo = (p[3] << 8) ^ (p[4] << 16) ^ ((p[3] ^ p[4]) << 24);
+    t.b_hi = t.b_lo ^ (p[5] * 0x01010101u);
+    t.c = (p[6] << 8) ^ (p[7] << 16) ^ ((p[6] ^ p[7]) << 24);
+    return t;
+}
+
+// ---------------------------------------------------------------- A.5 ----
+FEC_HD uint64_t sm64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+constexpr uint64_t TAG_PAY = 0x5041594C4F414400ull;
+constexpr uint64_t TAG_MTU = 0x4D54550000000000ull;
+constexpr uint64_t TAG_LEN = 0x4C454E0000000000ull;
+constexpr uint64_t TAG_ERA = 0x4552415345000000ull;
+constexpr uint32_t P10 = 429496730u;  // 0.1 * 2^32
+
+// packet length of source j of window w
+FEC_HD uint32_t pkt_len(int workload, uint64_t smtu, uint64_t slen, uint64_t w, int j, uint32_t L) {
+    if (workload == 0) return L;
+    uint32_t mtu = (sm64(smtu + w) & 1) ? 9000u : 1200u;
+    uint64_t h = sm64(slen + ((w << 8) | (uint64_t)j));
+    if ((uint32_t)h < P10) return 64u + (uint32_t)((h >> 32) % (uint64_t)(mtu - 63u));
+    return mtu;
+}
+
+}  // namespace fecgpu

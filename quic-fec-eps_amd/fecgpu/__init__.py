@@ -1,0 +1,227 @@
+"""fecgpu — Python host layer over the MI355X FEC engine's C ABI (include/fecgpu.h).
+
+The product path is libfecgpu.so (gfx950 HIP kernels + C++ runtime), loaded
+in-tree from quic-fec-eps_amd/lib/.  There is no CPU fallback: if the library
+is missing, importing this package raises; if no GPU is present, every compute
+call raises FecError(FECGPU_ERR_DEVICE).
+
+Reference interface mirrored: the fec branch's FEC encoder/decoder/frame API
+(BASELINE.json north_star; branch not mounted, /root/reference/README.md:7),
+restated as batch calls:
+  encode_batch  — repair generation for many windows
+  decode_batch  — erasure recovery in place
+plus on-device workload synthesis, erasure streams and run digests used by
+bench.py and the parity tests.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libfecgpu.so")
+
+# enums of include/fecgpu.h
+ERR_DONE, ERR_BUFFER_TOO_SHORT, ERR_INVALID_ARG = -1, -2, -3
+ERR_UNSUPPORTED, ERR_DEVICE, ERR_UNRECOVERABLE = -4, -5, -6
+SCHEME_XOR, SCHEME_GF256 = 0, 1
+MATRIX_CAUCHY = 0
+FRAMING_FIXED, FRAMING_LENPREFIX = 0, 1
+STATUS_OK, STATUS_UNRECOVERABLE = 0, 1
+F_HOST_PTRS, F_SYNC = 1, 2
+MAX_K, MAX_R = 64, 8
+WORKLOAD_FIXED, WORKLOAD_MIXED = 0, 1
+ERASURE_NONE, ERASURE_EXACT, ERASURE_IID = 0, 1, 2
+
+# every symbol include/fecgpu.h declares (tests check the library exports them)
+EXPORTS = (
+    "fecgpu_abi_version", "fecgpu_strerror", "fecgpu_last_error", "fecgpu_code_check",
+    "fecgpu_ctx_new", "fecgpu_ctx_free", "fecgpu_encode_batch", "fecgpu_decode_batch",
+    "fecgpu_synth_batch", "fecgpu_erasure_batch", "fecgpu_digest_batch",
+)
+
+
+class FecError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = f"{what}: {_lib().fecgpu_strerror(code).decode()} ({code})"
+        detail = _lib().fecgpu_last_error().decode()
+        if code == ERR_DEVICE and detail:
+            msg += f" [{detail}]"
+        super().__init__(msg)
+
+
+class fecgpu_code(ctypes.Structure):
+    _fields_ = [
+        ("scheme", ctypes.c_uint32),
+        ("matrix", ctypes.c_uint32),
+        ("framing", ctypes.c_uint32),
+        ("k", ctypes.c_uint16),
+        ("r", ctypes.c_uint16),
+        ("poly", ctypes.c_uint32),
+    ]
+
+
+_L = None
+
+
+def _lib():
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libfecgpu.so not built at {LIB_PATH}: run `make -C quic-fec-eps_amd` "
+                "or __graft_entry__.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, u64, i32, sz = (ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int,
+                                 ctypes.c_ssize_t)
+        cp = ctypes.POINTER(fecgpu_code)
+        sigs = {
+            "fecgpu_abi_version": (i32, []),
+            "fecgpu_strerror": (ctypes.c_char_p, [sz]),
+            "fecgpu_last_error": (ctypes.c_char_p, []),
+            "fecgpu_code_check": (sz, [cp]),
+            "fecgpu_ctx_new": (sz, [vp, i32, ctypes.POINTER(vp)]),
+            "fecgpu_ctx_free": (None, [vp]),
+            "fecgpu_encode_batch": (sz, [vp, cp, vp, vp, vp, u32, u32, u64, u32, vp]),
+            "fecgpu_decode_batch": (sz, [vp, cp, vp, vp, vp, u32, u32, u64, vp, vp, u32, vp]),
+            "fecgpu_synth_batch": (sz, [vp, cp, i32, u64, u64, vp, vp, u32, u32, u64, vp]),
+            "fecgpu_erasure_batch": (sz, [vp, cp, i32, u64, u64, vp, u64, vp]),
+            "fecgpu_digest_batch": (sz, [vp, cp, vp, vp, u32, u32, u64, u64, vp, vp]),
+        }
+        for name, (res, args) in sigs.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _L = L
+    return _L
+
+
+def lib():
+    """The loaded ctypes library (raises ImportError if not built)."""
+    return _lib()
+
+
+_lib()  # fail loudly at import when the native library is missing
+
+
+@dataclass(frozen=True)
+class Code:
+    """fecgpu_code: scheme 'xor' | 'gf256', k sources, r repairs per window."""
+    scheme: str
+    k: int
+    r: int
+    framing: str = "fixed"
+
+    @property
+    def c(self) -> fecgpu_code:
+        return fecgpu_code(SCHEME_XOR if self.scheme == "xor" else SCHEME_GF256, MATRIX_CAUCHY,
+                           FRAMING_FIXED if self.framing == "fixed" else FRAMING_LENPREFIX,
+                           self.k, self.r, 0x11D)
+
+    @property
+    def scheme_id(self) -> int:
+        return SCHEME_XOR if self.scheme == "xor" else SCHEME_GF256
+
+    def check(self) -> int:
+        return _lib().fecgpu_code_check(ctypes.byref(self.c))
+
+
+def _check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise FecError(rc, what)
+    return rc
+
+
+def _ptr(t) -> int | None:
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    if hasattr(t, "data_ptr"):
+        return t.data_ptr()
+    if hasattr(t, "ctypes"):  # numpy
+        return t.ctypes.data
+    raise TypeError(type(t))
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        try:
+            import torch
+            if torch.cuda.is_available():
+                return torch.cuda.current_stream().cuda_stream
+        except Exception:  # pragma: no cover
+            pass
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+class Context:
+    """fecgpu_ctx over the given devices (default: the current device)."""
+
+    def __init__(self, devices=None):
+        self._h = ctypes.c_void_p()
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = _lib().fecgpu_ctx_new(ctypes.cast(arr, ctypes.c_void_p), len(devices),
+                                       ctypes.byref(self._h))
+        else:
+            rc = _lib().fecgpu_ctx_new(None, 0, ctypes.byref(self._h))
+        _check(rc, "fecgpu_ctx_new")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            _lib().fecgpu_ctx_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ batch ---
+    def encode_batch(self, code: Code, win, *, nwin: int, stride: int, sym_len=None,
+                     sym_len_all: int = 0, win_off=None, flags: int = 0, stream=None) -> int:
+        return _check(_lib().fecgpu_encode_batch(
+            self._h, ctypes.byref(code.c), _ptr(win), _ptr(win_off), _ptr(sym_len),
+            sym_len_all, stride, nwin, flags, _stream(stream) if not flags & F_HOST_PTRS else None),
+            "fecgpu_encode_batch")
+
+    def decode_batch(self, code: Code, win, present, status, *, nwin: int, stride: int,
+                     sym_len=None, sym_len_all: int = 0, win_off=None, flags: int = 0,
+                     stream=None) -> int:
+        return _check(_lib().fecgpu_decode_batch(
+            self._h, ctypes.byref(code.c), _ptr(win), _ptr(win_off), _ptr(sym_len),
+            sym_len_all, stride, nwin, _ptr(present), _ptr(status), flags,
+            _stream(stream) if not flags & F_HOST_PTRS else None), "fecgpu_decode_batch")
+
+    def synth_batch(self, code: Code, workload: int, seed: int, w0: int, win, sym_len, *,
+                    L: int, stride: int, nwin: int, stream=None) -> int:
+        return _check(_lib().fecgpu_synth_batch(
+            self._h, ctypes.byref(code.c), workload, seed, w0, _ptr(win), _ptr(sym_len), L,
+            stride, nwin, _stream(stream)), "fecgpu_synth_batch")
+
+    def erasure_batch(self, code: Code, erasure: int, seed: int, w0: int, present, *, nwin: int,
+                      stream=None) -> int:
+        return _check(_lib().fecgpu_erasure_batch(
+            self._h, ctypes.byref(code.c), erasure, seed, w0, _ptr(present), nwin,
+            _stream(stream)), "fecgpu_erasure_batch")
+
+    def digest_batch(self, code: Code, win, digest, *, nwin: int, stride: int, w0: int = 0,
+                     sym_len=None, sym_len_all: int = 0, stream=None) -> int:
+        return _check(_lib().fecgpu_digest_batch(
+            self._h, ctypes.byref(code.c), _ptr(win), _ptr(sym_len), sym_len_all, stride, w0,
+            nwin, _ptr(digest), _stream(stream)), "fecgpu_digest_batch")
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m

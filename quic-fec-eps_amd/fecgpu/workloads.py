@@ -1,0 +1,172 @@
+"""Benchmark workloads of BASELINE.json configs 2-4 on device memory.
+
+Everything here runs on the GPU through libfecgpu (synthesis, erasure masks,
+encode, decode); torch only provides device memory, streams and the
+post-run bookkeeping (byte counts, verification against a saved copy).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import (ERASURE_EXACT, ERASURE_IID, STATUS_OK, WORKLOAD_FIXED, WORKLOAD_MIXED, Code,
+               Context, round_up)
+
+SEED = 0x5EEDFEC0
+
+
+@dataclass(frozen=True)
+class Config:
+    name: str
+    scheme: str
+    k: int
+    r: int
+    workload: int          # 0 fixed L, 1 mixed MTU (LENPREFIX)
+    L: int
+    nwin_per_gpu: int
+    erasure: int
+    erasure_desc: str
+
+    @property
+    def code(self) -> Code:
+        return Code(self.scheme, self.k, self.r,
+                    "fixed" if self.workload == WORKLOAD_FIXED else "lenprefix")
+
+    @property
+    def stride(self) -> int:
+        return round_up(self.L if self.workload == WORKLOAD_FIXED else 9002, 16)
+
+
+CONFIGS = {
+    2: Config("cfg2-xor-k8r2-1200B-64k", "xor", 8, 2, WORKLOAD_FIXED, 1200, 65536, ERASURE_EXACT,
+              "one source per XOR group (e=r=2)"),
+    3: Config("cfg3-gf256-k16r4-1200B-256k", "gf256", 16, 4, WORKLOAD_FIXED, 1200, 262144,
+              ERASURE_EXACT, "exactly r=4 sources per window"),
+    4: Config("cfg4-gf256-k32r8-mixedMTU-1M/8", "gf256", 32, 8, WORKLOAD_MIXED, 0, 131072,
+              ERASURE_IID, "i.i.d. p=0.1 over all k+r symbols"),
+}
+
+
+def _bits(x: torch.Tensor, n: int) -> torch.Tensor:
+    """[nwin] int64 masks -> [nwin, n] bool (bit i)."""
+    sh = torch.arange(n, device=x.device, dtype=torch.int64)
+    return ((x.unsqueeze(1) >> sh) & 1).bool()
+
+
+@dataclass
+class Batch:
+    cfg: Config
+    nwin: int
+    win: torch.Tensor        # [nwin * (k+r) * stride] u8
+    sym_len: torch.Tensor    # [nwin] int32 (u32)
+    present: torch.Tensor    # [nwin] int64 (u64)
+    status: torch.Tensor     # [nwin] u8
+
+    @staticmethod
+    def allocate(cfg: Config, nwin: int, dev) -> "Batch":
+        n = cfg.k + cfg.r
+        win = torch.zeros(nwin * n * cfg.stride, dtype=torch.uint8, device=dev)
+        sym_len = torch.full((nwin,), cfg.L, dtype=torch.int32, device=dev)
+        present = torch.zeros(nwin, dtype=torch.int64, device=dev)
+        status = torch.zeros(nwin, dtype=torch.uint8, device=dev)
+        return Batch(cfg, nwin, win, sym_len, present, status)
+
+    @property
+    def view(self) -> torch.Tensor:
+        return self.win.view(self.nwin, self.cfg.k + self.cfg.r, self.cfg.stride)
+
+    def _len_args(self):
+        if self.cfg.workload == WORKLOAD_FIXED:
+            return dict(sym_len=None, sym_len_all=self.cfg.L)
+        return dict(sym_len=self.sym_len, sym_len_all=0)
+
+    def synthesize(self, ctx: Context, w0: int) -> None:
+        c = self.cfg
+        ctx.synth_batch(c.code, c.workload, SEED, w0, self.win,
+                        self.sym_len if c.workload == WORKLOAD_MIXED else None,
+                        L=c.L, stride=c.stride, nwin=self.nwin)
+
+    def make_erasures(self, ctx: Context, w0: int) -> None:
+        c = self.cfg
+        ctx.erasure_batch(c.code, c.erasure, SEED, w0, self.present, nwin=self.nwin)
+
+    def encode(self, ctx: Context) -> None:
+        c = self.cfg
+        ctx.encode_batch(c.code, self.win, nwin=self.nwin, stride=c.stride, **self._len_args())
+
+    def decode(self, ctx: Context) -> None:
+        c = self.cfg
+        ctx.decode_batch(c.code, self.win, self.present, self.status, nwin=self.nwin,
+                         stride=c.stride, **self._len_args())
+
+    # ---------------------------------------------------------- accounting ---
+    def source_bytes(self) -> int:
+        """Sum of packet lengths (no prefix, no padding)."""
+        c = self.cfg
+        if c.workload == WORKLOAD_FIXED:
+            return self.nwin * c.k * c.L
+        hdr = self.view[:, :c.k, :2].to(torch.int64)
+        return int((hdr[..., 0] * 256 + hdr[..., 1]).sum().item())
+
+    def expected_outputs(self):
+        """Per window: sources the decoder recovers, symbols it reads, unrecoverable flag."""
+        c = self.cfg
+        pres = _bits(self.present, c.k + c.r)
+        miss = ~pres[:, :c.k]
+        if c.scheme == "xor":
+            ne = torch.zeros(self.nwin, dtype=torch.int64, device=self.win.device)
+            reads = torch.zeros_like(ne)
+            bad = torch.zeros(self.nwin, dtype=torch.bool, device=self.win.device)
+            for g in range(c.r):
+                members = list(range(g, c.k, c.r))
+                nm = miss[:, members].sum(1)
+                rec = (nm == 1) & pres[:, c.k + g]
+                ne += rec.long()
+                reads += rec.long() * len(members)
+                bad |= (nm >= 1) & ~rec
+            return ne, reads, bad
+        e = miss.sum(1)
+        reps = pres[:, c.k:].sum(1)
+        ok = (e <= reps) & (e > 0)
+        ne = torch.where(ok, e, torch.zeros_like(e))
+        reads = torch.where(ok, torch.full_like(e, c.k), torch.zeros_like(e))
+        return ne, reads, e > reps
+
+    def algorithmic_bytes(self) -> dict:
+        """HBM bytes each kernel must move: encode (k+r)*S, decode (reads+writes)*S."""
+        c = self.cfg
+        S = self.sym_len.to(torch.int64)
+        ne, reads, _ = self.expected_outputs()
+        enc = int(((c.k + c.r) * S).sum().item())
+        dec = int(((reads + ne) * S).sum().item())
+        return {"encode": enc, "decode": dec}
+
+    # --------------------------------------------------------- verification ---
+    def verify(self, ctx: Context, w0: int, chunk: int = 8192) -> dict:
+        """Poison every erased symbol, decode once, and compare each window's
+        sources with a copy taken before poisoning (all on device)."""
+        c = self.cfg
+        self.encode(ctx)
+        v = self.view
+        saved = v[:, :c.k].clone()
+        pres = _bits(self.present, c.k + c.r)
+        for s in range(0, self.nwin, chunk):
+            blk = v[s:s + chunk]
+            blk[~pres[s:s + chunk]] = 0xAB
+        self.decode(ctx)
+        torch.cuda.synchronize()
+        _, _, bad_expect = self.expected_outputs()
+        ok_status = self.status == STATUS_OK
+        mismatched = 0
+        for s in range(0, self.nwin, chunk):
+            eq = (v[s:s + chunk, :c.k] == saved[s:s + chunk]).flatten(1).all(1)
+            mismatched += int((ok_status[s:s + chunk] & ~eq).sum().item())
+        unrec = int((~ok_status).sum().item())
+        status_agree = bool(((~ok_status) == bad_expect).all().item())
+        del saved
+        # restore the erased symbols so the buffer is reusable
+        self.synthesize(ctx, w0)
+        return {"ok": mismatched == 0 and status_agree, "windows": self.nwin,
+                "mismatched_ok_windows": mismatched, "unrecoverable": unrec,
+                "status_matches_expected": status_agree}

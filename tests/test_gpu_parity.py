@@ -1,0 +1,300 @@
+"""GPU parity: libfecgpu.so (gfx950 kernels, through the C ABI) vs the CPU oracle.
+
+Bit-exact on every emitted byte [0, S) of every symbol; byte work has no
+tolerance.  Sizes: small windows the oracle finishes in seconds, the committed
+golden fixtures, and the BASELINE.json full sizes through size-independent
+properties (encode -> erase -> decode round trip on every window, linearity)
+plus sampled windows against the oracle.
+PARITY UNPINNED vs the reference fec branch (not mounted).
+"""
+import glob
+import itertools
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import fecgpu  # noqa: E402
+import oracle as O  # noqa: E402
+from fecgpu import workloads as WL  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+SEED = 1234567
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    O.build()
+    c = fecgpu.Context()
+    yield c
+    c.close()
+
+
+def _scheme(s):
+    return O.XOR if s == "xor" else O.GF256
+
+
+def _cmp_emitted(a: np.ndarray, b: np.ndarray, S: np.ndarray, what: str):
+    """Compare bytes [0, S_w) of every symbol of every window."""
+    for w in range(a.shape[0]):
+        s = int(S[w])
+        if not np.array_equal(a[w, :, :s], b[w, :, :s]):
+            bad = np.argwhere(a[w, :, :s] != b[w, :, :s])
+            raise AssertionError(f"{what}: window {w} differs at (sym, byte) {bad[:5].tolist()}")
+
+
+def gpu_run(ctx, scheme, k, r, wins, S, present, uniform: bool, poison=0xAB):
+    """Encode on the GPU, poison erased symbols, decode on the GPU.
+    Returns (encoded, decoded, status) as numpy."""
+    nwin, n, stride = wins.shape
+    code = fecgpu.Code(scheme, k, r)
+    d = torch.from_numpy(wins.copy()).cuda()
+    sl = torch.from_numpy(S.astype(np.int32)).cuda()
+    kw = dict(sym_len=None, sym_len_all=int(S[0])) if uniform else dict(sym_len=sl)
+    ctx.encode_batch(code, d, nwin=nwin, stride=stride, **kw)
+    torch.cuda.synchronize()
+    enc = d.cpu().numpy()
+    pres_t = torch.from_numpy(present.astype(np.int64)).cuda()
+    mask = torch.from_numpy(np.array([[(int(p) >> i) & 1 for i in range(n)] for p in present],
+                                     dtype=bool)).cuda()
+    d[~mask] = poison
+    status = torch.full((nwin,), 7, dtype=torch.uint8, device="cuda")
+    ctx.decode_batch(code, d, pres_t, status, nwin=nwin, stride=stride, **kw)
+    torch.cuda.synchronize()
+    return enc, d.cpu().numpy(), status.cpu().numpy()
+
+
+def oracle_run(scheme, k, r, wins, S, present, poison=0xAB):
+    enc = wins.copy()
+    O.encode_batch(_scheme(scheme), k, r, S, enc, 4)
+    dec = enc.copy()
+    O.erase(dec, present, k, r, fill=poison)
+    st = O.decode_batch(_scheme(scheme), k, r, S, dec, present, 4)
+    return enc, dec, st
+
+
+CASES = [
+    # scheme, k, r, workload, L, erasure, nwin
+    ("xor", 8, 2, 0, 1200, 1, 64),
+    ("xor", 4, 1, 0, 100, 1, 33),
+    ("xor", 5, 3, 0, 17, 2, 64),
+    ("xor", 8, 2, 1, 0, 2, 12),
+    ("xor", 8, 8, 0, 48, 2, 40),
+    ("gf256", 16, 4, 0, 1200, 1, 64),
+    ("gf256", 32, 8, 1, 0, 2, 12),
+    ("gf256", 1, 1, 0, 1, 1, 5),
+    ("gf256", 56, 8, 0, 64, 1, 9),
+    ("gf256", 10, 7, 0, 33, 2, 70),
+    ("gf256", 3, 5, 0, 16, 1, 8),
+    ("gf256", 8, 2, 0, 1500, 2, 100),
+    ("gf256", 20, 6, 1, 0, 1, 6),
+]
+
+
+@pytest.mark.parametrize("scheme,k,r,wl,L,era,nwin", CASES)
+def test_encode_decode_vs_oracle(ctx, scheme, k, r, wl, L, era, nwin):
+    S = O.sym_lens(wl, SEED, 0, nwin, k, L)
+    stride = O.round_up(int(S.max()), 16) + (16 if wl == 0 else 0)
+    wins = O.make_windows(wl, SEED, 0, nwin, k, r, L, stride)
+    present = O.presents(era, SEED, 0, nwin, _scheme(scheme), k, r)
+    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, present, uniform=(wl == 0))
+    oe, od, os_ = oracle_run(scheme, k, r, wins, S, present)
+    _cmp_emitted(ge, oe, S, "encode")
+    assert np.array_equal(gs, os_), (gs, os_)
+    _cmp_emitted(gd, od, S, "decode")
+    # recovered windows equal the original sources
+    for w in range(nwin):
+        if gs[w] == 0:
+            s = int(S[w])
+            assert np.array_equal(gd[w, :k, :s], wins[w, :k, :s])
+
+
+@pytest.mark.parametrize("scheme,k,r", [("gf256", 4, 3), ("xor", 6, 3), ("gf256", 5, 2),
+                                        ("xor", 3, 1)])
+def test_every_erasure_pattern(ctx, scheme, k, r):
+    """All 2^(k+r) present masks, one window each: status and bytes vs oracle."""
+    n = k + r
+    nwin = 1 << n
+    L = 40
+    wins = O.make_windows(0, SEED, 7, 1, k, r, L, 48)
+    wins = np.repeat(wins, nwin, axis=0)
+    S = np.full(nwin, L, np.uint32)
+    present = np.arange(nwin, dtype=np.uint64)
+    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, present, uniform=True)
+    oe, od, os_ = oracle_run(scheme, k, r, wins, S, present)
+    _cmp_emitted(ge, oe, S, "encode")
+    assert np.array_equal(gs, os_)
+    _cmp_emitted(gd, od, S, "decode")
+    if scheme == "gf256":  # MDS: recoverable iff missing sources <= present repairs
+        for p in range(nwin):
+            miss = sum(1 for j in range(k) if not (p >> j) & 1)
+            reps = sum(1 for i in range(r) if (p >> (k + i)) & 1)
+            assert gs[p] == (0 if miss <= reps else 1)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(HERE, "golden", "*.npz"))),
+                         ids=lambda p: os.path.basename(p)[:-4])
+def test_golden_fixtures(ctx, path):
+    z = np.load(path)
+    scheme_id, k, r, L, era, nwin, w0, seed = (int(x) for x in z["meta"])
+    scheme = "xor" if scheme_id == 0 else "gf256"
+    stride = O.round_up(L, 16)
+    wins = np.zeros((nwin, k + r, stride), np.uint8)
+    wins[:, :k, :L] = z["src"]
+    S = np.full(nwin, L, np.uint32)
+    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, z["present"], uniform=True)
+    assert np.array_equal(ge[:, k:, :L], z["repair"])
+    assert np.array_equal(gs, z["status"])
+    ok = z["status"] == 0
+    assert np.array_equal(gd[ok, :k, :L], z["decoded"][ok])
+
+
+def test_ragged_layout(ctx):
+    """win_off != NULL: per-window stride round_up(S_w, 16), windows at arbitrary 16-B offsets."""
+    k, r, nwin = 6, 3, 17
+    rng = np.random.default_rng(5)
+    S = rng.integers(1, 300, nwin).astype(np.uint32)
+    strides = [O.round_up(int(s), 16) for s in S]
+    offs, pos = [], 0
+    for w in range(nwin):
+        pos += 16 * int(rng.integers(0, 4))
+        offs.append(pos)
+        pos += (k + r) * strides[w]
+    for scheme in ("gf256", "xor"):
+        buf = np.zeros(pos + 64, np.uint8)
+        ref = []
+        for w in range(nwin):
+            win = np.zeros((k + r, strides[w]), np.uint8)
+            win[:k, :S[w]] = rng.integers(0, 256, (k, int(S[w])), dtype=np.uint8)
+            ref.append(win)
+            buf[offs[w]:offs[w] + win.size] = win.ravel()
+        present = O.presents(1, SEED, 0, nwin, _scheme(scheme), k, r)
+        d = torch.from_numpy(buf).cuda()
+        off_t = torch.tensor(offs, dtype=torch.int64).cuda()
+        sl = torch.from_numpy(S.astype(np.int32)).cuda()
+        code = fecgpu.Code(scheme, k, r)
+        ctx.encode_batch(code, d, nwin=nwin, stride=0, sym_len=sl, win_off=off_t)
+        st = torch.zeros(nwin, dtype=torch.uint8, device="cuda")
+        enc = d.cpu().numpy()
+        for w in range(nwin):  # erase in place on device
+            for i in range(k + r):
+                if not (int(present[w]) >> i) & 1:
+                    a = offs[w] + i * strides[w]
+                    d[a:a + strides[w]] = 0xCD
+        ctx.decode_batch(code, d, torch.from_numpy(present.astype(np.int64)).cuda(), st,
+                         nwin=nwin, stride=0, sym_len=sl, win_off=off_t)
+        out = d.cpu().numpy()
+        for w in range(nwin):
+            o = ref[w].copy()
+            O.encode_batch(_scheme(scheme), k, r, np.array([S[w]], np.uint32), o[None], 1)
+            got = enc[offs[w]:offs[w] + o.size].reshape(o.shape)
+            assert np.array_equal(got[:, :S[w]], o[:, :S[w]]), (scheme, w)
+            rec = out[offs[w]:offs[w] + o.size].reshape(o.shape)
+            assert st[w].item() == 0
+            assert np.array_equal(rec[:k, :S[w]], o[:k, :S[w]]), (scheme, w)
+
+
+def test_host_pointer_mode(ctx):
+    k, r, nwin, L = 16, 4, 50, 1200
+    S = np.full(nwin, L, np.uint32)
+    wins = O.make_windows(0, SEED, 0, nwin, k, r, L, 1216)
+    present = O.presents(1, SEED, 0, nwin, O.GF256, k, r)
+    code = fecgpu.Code("gf256", k, r)
+    h = wins.copy()
+    ctx.encode_batch(code, h, nwin=nwin, stride=1216, sym_len_all=L, flags=fecgpu.F_HOST_PTRS)
+    oe, od, os_ = oracle_run("gf256", k, r, wins, S, present)
+    _cmp_emitted(h, oe, S, "host encode")
+    O.erase(h, present, k, r, fill=0x11)
+    st = np.zeros(nwin, np.uint8)
+    ctx.decode_batch(code, h, present, st, nwin=nwin, stride=1216, sym_len_all=L,
+                     flags=fecgpu.F_HOST_PTRS)
+    assert np.array_equal(st, os_)
+    _cmp_emitted(h, od, S, "host decode")
+
+
+def test_zero_windows_and_errors(ctx):
+    code = fecgpu.Code("gf256", 4, 2)
+    d = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    assert ctx.encode_batch(code, d, nwin=0, stride=64, sym_len_all=10) == 0
+    with pytest.raises(fecgpu.FecError) as e:
+        ctx.encode_batch(code, d, nwin=1, stride=60, sym_len_all=10)  # stride % 16
+    assert e.value.code == fecgpu.ERR_INVALID_ARG
+    with pytest.raises(fecgpu.FecError) as e:
+        ctx.encode_batch(code, d, nwin=1, stride=64, sym_len_all=100)  # S > stride
+    assert e.value.code == fecgpu.ERR_BUFFER_TOO_SHORT
+    with pytest.raises(fecgpu.FecError) as e:
+        ctx.encode_batch(fecgpu.Code("gf256", 60, 9), d, nwin=1, stride=64, sym_len_all=10)
+    assert e.value.code == fecgpu.ERR_UNSUPPORTED
+
+
+# ------------------------------------------------ workload generators ---
+@pytest.mark.parametrize("cfgid", [2, 3, 4])
+def test_synth_erasure_digest_vs_oracle(ctx, cfgid):
+    cfg = WL.CONFIGS[cfgid]
+    nwin, w0 = 24, 1000
+    b = WL.Batch.allocate(cfg, nwin, torch.device("cuda"))
+    b.synthesize(ctx, w0)
+    b.make_erasures(ctx, w0)
+    torch.cuda.synchronize()
+    S = O.sym_lens(cfg.workload, WL.SEED, w0, nwin, cfg.k, cfg.L)
+    wins = O.make_windows(cfg.workload, WL.SEED, w0, nwin, cfg.k, cfg.r, cfg.L, cfg.stride)
+    got = b.view.cpu().numpy()
+    assert np.array_equal(got[:, :cfg.k], wins[:, :cfg.k])
+    if cfg.workload == 1:
+        assert np.array_equal(b.sym_len.cpu().numpy().astype(np.uint32), S)
+    pres = O.presents(cfg.erasure, WL.SEED, w0, nwin, _scheme(cfg.scheme), cfg.k, cfg.r)
+    assert np.array_equal(b.present.cpu().numpy().astype(np.uint64), pres)
+    b.encode(ctx)
+    dg = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.digest_batch(cfg.code, b.win, dg, nwin=nwin, stride=cfg.stride, w0=w0,
+                     **b._len_args())
+    O.encode_batch(_scheme(cfg.scheme), cfg.k, cfg.r, S, wins, 4)
+    want = O.batch_digest(cfg.k, cfg.r, S, wins, w0)
+    assert (int(dg.item()) & (2**64 - 1)) == want
+
+
+# --------------------------------------------------- full BASELINE sizes ---
+@pytest.mark.parametrize("cfgid,nwin", [(2, 65536), (3, 262144), (4, 16384)])
+def test_full_size_roundtrip(ctx, cfgid, nwin):
+    """Every window: encode -> poison erased -> decode == original sources, status as
+    predicted from the masks; 32 sampled windows bit-exact vs the oracle."""
+    cfg = WL.CONFIGS[cfgid]
+    b = WL.Batch.allocate(cfg, nwin, torch.device("cuda"))
+    b.synthesize(ctx, 0)
+    b.make_erasures(ctx, 0)
+    b.encode(ctx)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(cfgid)
+    sample = np.sort(rng.choice(nwin, 32, replace=False))
+    enc = b.view[torch.from_numpy(sample).cuda()].cpu().numpy()
+    res = b.verify(ctx, 0)
+    assert res["ok"], res
+    if cfgid != 4:
+        assert res["unrecoverable"] == 0
+    for i, w in enumerate(sample):
+        S = O.sym_lens(cfg.workload, WL.SEED, int(w), 1, cfg.k, cfg.L)
+        win = O.make_windows(cfg.workload, WL.SEED, int(w), 1, cfg.k, cfg.r, cfg.L, cfg.stride)
+        O.encode_batch(_scheme(cfg.scheme), cfg.k, cfg.r, S, win, 1)
+        _cmp_emitted(enc[i:i + 1], win, S, f"cfg{cfgid} window {w}")
+
+
+def test_linearity_full_size(ctx):
+    """encode(A xor B) == encode(A) xor encode(B) over 262,144 k=16 r=4 windows."""
+    cfg = WL.CONFIGS[3]
+    nwin = 262144
+    a = WL.Batch.allocate(cfg, nwin, torch.device("cuda"))
+    a.synthesize(ctx, 0)
+    bsrc = a.view[:, :cfg.k].roll(1, dims=0).clone()
+    a.encode(ctx)
+    ra = a.view[:, cfg.k:].clone()
+    a.view[:, :cfg.k] = bsrc
+    a.encode(ctx)
+    rb = a.view[:, cfg.k:].clone()
+    a.synthesize(ctx, 0)
+    a.view[:, :cfg.k] ^= bsrc
+    a.encode(ctx)
+    assert torch.equal(a.view[:, cfg.k:], ra ^ rb)
