@@ -33,7 +33,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import fecgpu  # noqa: E402
-from fecgpu import workloads  # noqa: E402
+from fecgpu import shard, workloads  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
@@ -52,24 +52,26 @@ def parse():
     return ap.parse_args()
 
 
+def log(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
     """Time the CPU oracle (oracle/fec_oracle.c, kind "port") on a bounded
     sample of the same workload: same packets, same erasure stream."""
     sys.path.insert(0, os.path.join(_ROOT, "oracle"))
-    import numpy as np
     import oracle as O  # test/baseline infrastructure only
 
     O.lib()
     if threads <= 0:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
     scheme = O.XOR if cfg.scheme == "xor" else O.GF256
+    win_bytes = (cfg.k + cfg.r) * cfg.stride
+    max_nw = max(threads, (2 << 30) // win_bytes)  # sample buffer <= 2 GiB
 
     def run(nw: int):
-        S = O.sym_lens(cfg.workload, workloads.SEED, 0, nw, cfg.k, cfg.L)
-        wins = O.make_windows(cfg.workload, workloads.SEED, 0, nw, cfg.k, cfg.r, cfg.L, cfg.stride)
-        pres = O.presents(cfg.erasure, workloads.SEED, 0, nw, scheme, cfg.k, cfg.r)
-        src = int(sum(O.lib().orc_pkt_len(cfg.workload, workloads.SEED, w, j, cfg.k, cfg.L)
-                      for w in range(nw) for j in range(cfg.k)))
+        wins, S, pres, src = O.make_batch(cfg.workload, workloads.SEED, 0, nw, scheme, cfg.erasure,
+                                          cfg.k, cfg.r, cfg.L, cfg.stride, threads)
         t0 = time.perf_counter()
         O.encode_batch(scheme, cfg.k, cfg.r, S, wins, threads)
         O.decode_batch(scheme, cfg.k, cfg.r, S, wins, pres, threads)
@@ -77,11 +79,21 @@ def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
 
     nw = 4 * threads
     dt, src = run(nw)
-    while dt < 0.5 and nw < 1 << 20:
-        nw *= 4
+    while dt < 0.25 and nw < max_nw:
+        nw = min(max_nw, nw * 4)
         dt, src = run(nw)
-    nw = max(nw, int(nw * seconds / max(dt, 1e-3)))
-    dt, src = run(nw)
+    # scale to ~seconds of work; repeat the capped sample if it is still short
+    per_win = dt / nw
+    nw = min(max_nw, max(nw, int(seconds / per_win)))
+    reps = min(20, max(1, int(seconds / (per_win * nw) + 0.5)))
+    tot_dt, tot_src = 0.0, 0
+    for _ in range(reps):
+        dt, src = run(nw)
+        tot_dt += dt
+        tot_src += src
+        if tot_dt >= seconds:
+            break
+    dt, src = tot_dt, tot_src
     return {"value": round(src / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"{nw} windows of {cfg.name} (encode+decode, same packets and erasures), "
                       f"{dt:.1f} s on {threads} host threads"}
@@ -101,15 +113,16 @@ def main():
 
     cfg = workloads.CONFIGS[args.config]
     nwin = args.nwin or cfg.nwin_per_gpu
-    w0 = rank * nwin  # this rank's shard of the global window range
+    w0, nwin = shard.weak_shard(rank, world, nwin)  # this rank's global window range
     ctx = fecgpu.Context()
     batch = workloads.Batch.allocate(cfg, nwin, dev)
+    log(f"rank {rank}: {cfg.name}, windows [{w0}, {w0 + nwin}), {batch.win.numel() / 2**30:.2f} GiB")
     batch.synthesize(ctx, w0)
     batch.make_erasures(ctx, w0)
     src_bytes = batch.source_bytes()      # per rank, per step
     alg = batch.algorithmic_bytes()       # {'encode': B, 'decode': B} per launch
 
-    # warmup
+    log("warmup")
     for _ in range(args.warmup):
         batch.encode(ctx)
         batch.decode(ctx)
@@ -134,16 +147,13 @@ def main():
     enc_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
     dec_ms = sum(b.elapsed_time(c) for _, b, c in ev) / args.steps
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    tot = torch.tensor([float(src_bytes)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    elapsed = float(t.item())
-    total_src = float(tot.item()) * args.steps
+    log(f"timed {args.steps} steps: {elapsed:.4f} s (encode {enc_ms:.3f} ms, decode {dec_ms:.3f} ms)")
+    elapsed, tot = shard.reduce_run(elapsed, src_bytes, dev)
+    total_src = float(tot) * args.steps
     value = total_src / elapsed / 1e9
 
     verify = None if args.no_verify else batch.verify(ctx, w0)
+    log(f"verify: {verify}")
 
     if rank == 0:
         dom = "decode" if dec_ms > enc_ms else "encode"
@@ -151,6 +161,7 @@ def main():
         achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
+            log("cpu baseline")
             cpu = cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads)
         line = {
             "metric": "GB/s source-packet bytes FEC encode+decode, device-resident, per MI355X",

@@ -114,6 +114,52 @@ ssize_t fecgpu_decode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *w
                             const uint64_t *present, uint8_t *status, uint32_t flags,
                             void *stream);
 
+/* ---- per-connection objects: the Connection's per-packet FEC API -------
+ * (§3 call stacks A/B).  The sender appends every
+ * protected payload as a source symbol and reads repair symbols back; the
+ * receiver files sources and repairs by (window, index) and reads recovered
+ * packets back.  Complete windows are queued and run through the batch
+ * entry points above (host pointers, ragged layout) `batch` windows at a
+ * time.  All buffers are host memory. */
+typedef struct fecgpu_encoder fecgpu_encoder;
+typedef struct fecgpu_decoder fecgpu_decoder;
+
+ssize_t fecgpu_encoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t max_len,
+                           uint32_t batch, fecgpu_encoder **out);
+void    fecgpu_encoder_free(fecgpu_encoder *enc);
+/* Append one source packet; win and idx receive its window id and index.
+ * Closing the k-th packet of a window queues it; `batch` queued windows are
+ * encoded on the GPU.  FIXED framing: every packet of a window same length. */
+ssize_t fecgpu_encoder_add_source(fecgpu_encoder *enc, const uint8_t *pkt, size_t len,
+                                  uint64_t *win, uint16_t *idx);
+/* Close the open window early (missing sources become empty/zero packets);
+ * returns its window id, FECGPU_ERR_DONE if no window is open. */
+ssize_t fecgpu_encoder_close_window(fecgpu_encoder *enc);
+/* Encode every queued window now; returns the number encoded. */
+ssize_t fecgpu_encoder_flush(fecgpu_encoder *enc);
+/* Copy repair i of window win (S bytes); FECGPU_ERR_DONE until encoded. */
+ssize_t fecgpu_encoder_repair(fecgpu_encoder *enc, uint64_t win, uint16_t i, uint8_t *out,
+                              size_t cap);
+/* Drop an encoded window's buffers. */
+ssize_t fecgpu_encoder_release(fecgpu_encoder *enc, uint64_t win);
+
+ssize_t fecgpu_decoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t max_len,
+                           uint32_t batch, fecgpu_decoder **out);
+void    fecgpu_decoder_free(fecgpu_decoder *dec);
+/* File a received source packet / repair symbol (repair length = S). */
+ssize_t fecgpu_decoder_add_source(fecgpu_decoder *dec, uint64_t win, uint16_t idx,
+                                  const uint8_t *pkt, size_t len);
+ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *dec, uint64_t win, uint16_t idx,
+                                  const uint8_t *sym, size_t len);
+/* Decode every window that can now recover a missing source; returns the
+ * number of source packets recovered. */
+ssize_t fecgpu_decoder_flush(fecgpu_decoder *dec);
+/* Copy source packet idx of window win (received or recovered, de-framed);
+ * returns its length, FECGPU_ERR_DONE if it is not available. */
+ssize_t fecgpu_decoder_recovered(fecgpu_decoder *dec, uint64_t win, uint16_t idx, uint8_t *out,
+                                 size_t cap);
+ssize_t fecgpu_decoder_release(fecgpu_decoder *dec, uint64_t win);
+
 /* ---- synthetic workload / verification (bench + tests) ---- */
 
 /* Fill sources of windows w0..w0+nwin-1 on the device (workload 0: FIXED,

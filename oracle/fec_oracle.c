@@ -334,3 +334,53 @@ void orc_decode_batch(int scheme, int k, int r, const uint32_t *S, uint32_t stri
     job_t j = {1, scheme, k, r, S, stride, 0, 0, present, status, wins};
     run_batch(j, nwin, nthreads);
 }
+
+/* ------------------------------------------------ batch workload fill --- */
+typedef struct {
+    int workload, scheme, erasure, k, r;
+    uint64_t seed, w0, lo, hi;
+    uint32_t L, stride;
+    uint8_t *wins;
+    uint32_t *S;
+    uint64_t *present;
+    uint64_t src_bytes;
+} fill_t;
+
+static void *run_fill(void *p) {
+    fill_t *f = (fill_t *)p;
+    size_t wbytes = (size_t)(f->k + f->r) * f->stride;
+    f->src_bytes = 0;
+    for (uint64_t i = f->lo; i < f->hi; i++) {
+        uint64_t w = f->w0 + i;
+        orc_fill_window(f->workload, f->seed, w, f->k, f->r, f->L, f->stride, f->wins + i * wbytes);
+        f->S[i] = orc_sym_len(f->workload, f->seed, w, f->k, f->L);
+        f->present[i] = orc_present(f->erasure, f->seed, w, f->scheme, f->k, f->r);
+        for (int j = 0; j < f->k; j++) f->src_bytes += orc_pkt_len(f->workload, f->seed, w, j, f->k, f->L);
+    }
+    return NULL;
+}
+
+/* Fill nwin windows (sources, S, present masks) in parallel; returns the sum
+ * of packet lengths (source-packet bytes). */
+uint64_t orc_make_batch(int workload, uint64_t seed, uint64_t w0, uint64_t nwin, int scheme,
+                        int erasure, int k, int r, uint32_t L, uint32_t stride, uint8_t *wins,
+                        uint32_t *S, uint64_t *present, int nthreads) {
+    gf_init();
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    fill_t f[256];
+    for (int t = 0; t < nthreads; t++) {
+        fill_t x = {workload, scheme, erasure, k, r, seed, w0,
+                    nwin * (uint64_t)t / (uint64_t)nthreads, nwin * (uint64_t)(t + 1) / (uint64_t)nthreads,
+                    L, stride, wins, S, present, 0};
+        f[t] = x;
+        pthread_create(&th[t], NULL, run_fill, &f[t]);
+    }
+    uint64_t total = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        total += f[t].src_bytes;
+    }
+    return total;
+}

@@ -71,6 +71,11 @@ void orc_decode_batch(int scheme, int k, int r, const uint32_t *S, uint32_t stri
                       uint64_t nwin, const uint64_t *present, uint8_t *status, uint8_t *wins,
                       int nthreads);
 
+/* parallel fill of nwin windows + S + present masks; returns source-packet bytes */
+uint64_t orc_make_batch(int workload, uint64_t seed, uint64_t w0, uint64_t nwin, int scheme,
+                        int erasure, int k, int r, uint32_t L, uint32_t stride, uint8_t *wins,
+                        uint32_t *S, uint64_t *present, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,6 +52,8 @@ def lib():
             "orc_window_digest": (u64, [i32, i32, u32, u32, vp]),
             "orc_encode_batch": (None, [i32, i32, i32, vp, u32, u64, vp, i32]),
             "orc_decode_batch": (None, [i32, i32, i32, vp, u32, u64, vp, vp, vp, i32]),
+            "orc_make_batch": (u64, [i32, u64, u64, u64, i32, i32, i32, i32, u32, u32, vp, vp, vp,
+                                     i32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -101,6 +103,17 @@ def make_windows(workload: int, seed: int, w0: int, nwin: int, k: int, r: int, L
     for w in range(nwin):
         f(workload, seed, w0 + w, k, r, L, stride, _p(wins[w]))
     return wins
+
+
+def make_batch(workload: int, seed: int, w0: int, nwin: int, scheme: int, erasure: int, k: int,
+               r: int, L: int, stride: int, nthreads: int = 1):
+    """-> (wins [nwin, k+r, stride], S [nwin], present [nwin], source-packet bytes)."""
+    wins = np.zeros((nwin, k + r, stride), np.uint8)
+    S = np.zeros(nwin, np.uint32)
+    pres = np.zeros(nwin, np.uint64)
+    src = lib().orc_make_batch(workload, seed, w0, nwin, scheme, erasure, k, r, L, stride,
+                               _p(wins), _p(S), _p(pres), nthreads)
+    return wins, S, pres, int(src)
 
 
 def presents(erasure: int, seed: int, w0: int, nwin: int, scheme: int, k: int, r: int) -> np.ndarray:

@@ -347,23 +347,24 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, int lane, uint8_t *regio
         return;
     }
     WAVE_SYNC();
-    // D[u][q] for idx = u*k + q; Ainv[u][t] = xr of lane u*8 + t
+    // D[u][q] for idx = u*k + q; Ainv[u][t] = xr of lane u*8 + t.
+    // Every __shfl runs with the whole wave active: ds_bpermute reads 0 from a
+    // source lane that is masked off, so no shuffle may sit inside a branch.
     const int kr = k - e;
     for (int base = 0; base < e * k; base += 64) {
         const int idx = base + lane;
         const int du = idx / k, dq = idx - du * k;
         const bool live = idx < e * k;
-        uint32_t c = 0;
-        if (dq < kr) {
-            const uint32_t j = live ? insym[dq] : 0u;
-            for (int tt = 0; tt < e; tt++) {
-                const uint32_t ai = __shfl(xr, ((du & 7) * 8 + tt) & 63, 64);
-                const int st = __shfl(my_sel, tt, 64);
-                c ^= gf_mul_lds(ex, lg, ai, gf_inv_lds(ex, lg, (uint32_t)((k + st) ^ j)));
-            }
-        } else {
-            c = __shfl(xr, ((du & 7) * 8 + (dq - kr)) & 63, 64);
+        const bool is_src = dq < kr;
+        const uint32_t j = (live && is_src) ? insym[dq] : 0u;
+        uint32_t csrc = 0;
+        for (int tt = 0; tt < e; tt++) {
+            const uint32_t ai = __shfl(xr, ((du & 7) * 8 + tt) & 63, 64);
+            const int st = __shfl(my_sel, tt, 64);
+            if (is_src) csrc ^= gf_mul_lds(ex, lg, ai, gf_inv_lds(ex, lg, (uint32_t)((k + st) ^ j)));
         }
+        const uint32_t crep = __shfl(xr, ((du & 7) * 8 + (is_src ? 0 : dq - kr)) & 63, 64);
+        const uint32_t c = is_src ? csrc : crep;
         if (live) {
             const CoefTab ct = make_coef_tab(c);
             tab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);

@@ -73,6 +73,15 @@ def _lib():
             raise ImportError(
                 f"libfecgpu.so not built at {LIB_PATH}: run `make -C quic-fec-eps_amd` "
                 "or __graft_entry__.build() (no CPU fallback exists)")
+        # One HIP runtime per process: torch's wheel bundles its own
+        # libamdhip64 (NEEDED as "libamdhip64.so", SONAME libamdhip64.so.7).
+        # Loading torch first makes libfecgpu's libamdhip64.so.7 dependency
+        # resolve to that same runtime; loading libfecgpu first would pull in
+        # /opt/rocm's copy and torch would then load a second one.
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # pragma: no cover - non-torch hosts use /opt/rocm's runtime
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, u32, u64, i32, sz = (ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int,
                                  ctypes.c_ssize_t)
