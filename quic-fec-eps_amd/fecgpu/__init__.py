@@ -39,6 +39,12 @@ EXPORTS = (
     "fecgpu_abi_version", "fecgpu_strerror", "fecgpu_last_error", "fecgpu_code_check",
     "fecgpu_ctx_new", "fecgpu_ctx_free", "fecgpu_encode_batch", "fecgpu_decode_batch",
     "fecgpu_synth_batch", "fecgpu_erasure_batch", "fecgpu_digest_batch",
+    "fecgpu_encoder_new", "fecgpu_encoder_free", "fecgpu_encoder_add_source",
+    "fecgpu_encoder_close_window", "fecgpu_encoder_flush", "fecgpu_encoder_repair",
+    "fecgpu_encoder_release",
+    "fecgpu_decoder_new", "fecgpu_decoder_free", "fecgpu_decoder_add_source",
+    "fecgpu_decoder_add_repair", "fecgpu_decoder_flush", "fecgpu_decoder_recovered",
+    "fecgpu_decoder_release",
 )
 
 
@@ -98,6 +104,22 @@ def _lib():
             "fecgpu_synth_batch": (sz, [vp, cp, i32, u64, u64, vp, vp, u32, u32, u64, vp]),
             "fecgpu_erasure_batch": (sz, [vp, cp, i32, u64, u64, vp, u64, vp]),
             "fecgpu_digest_batch": (sz, [vp, cp, vp, vp, u32, u32, u64, u64, vp, vp]),
+            "fecgpu_encoder_new": (sz, [vp, cp, u32, u32, ctypes.POINTER(vp)]),
+            "fecgpu_encoder_free": (None, [vp]),
+            "fecgpu_encoder_add_source": (sz, [vp, vp, ctypes.c_size_t,
+                                               ctypes.POINTER(ctypes.c_uint64),
+                                               ctypes.POINTER(ctypes.c_uint16)]),
+            "fecgpu_encoder_close_window": (sz, [vp]),
+            "fecgpu_encoder_flush": (sz, [vp]),
+            "fecgpu_encoder_repair": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
+            "fecgpu_encoder_release": (sz, [vp, u64]),
+            "fecgpu_decoder_new": (sz, [vp, cp, u32, u32, ctypes.POINTER(vp)]),
+            "fecgpu_decoder_free": (None, [vp]),
+            "fecgpu_decoder_add_source": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
+            "fecgpu_decoder_add_repair": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
+            "fecgpu_decoder_flush": (sz, [vp]),
+            "fecgpu_decoder_recovered": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
+            "fecgpu_decoder_release": (sz, [vp, u64]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -230,6 +252,91 @@ class Context:
         return _check(_lib().fecgpu_digest_batch(
             self._h, ctypes.byref(code.c), _ptr(win), _ptr(sym_len), sym_len_all, stride, w0,
             nwin, _ptr(digest), _stream(stream)), "fecgpu_digest_batch")
+
+
+class Encoder:
+    """Per-connection sender (fecgpu_encoder_*): append packets, read repairs."""
+
+    def __init__(self, ctx: Context, code: Code, max_len: int, batch: int = 64):
+        self._ctx = ctx  # keep the ctx alive
+        self.code = code
+        self._h = ctypes.c_void_p()
+        _check(_lib().fecgpu_encoder_new(ctx.handle, ctypes.byref(code.c), max_len, batch,
+                                         ctypes.byref(self._h)), "fecgpu_encoder_new")
+
+    def add_source(self, pkt: bytes) -> tuple[int, int]:
+        w, i = ctypes.c_uint64(), ctypes.c_uint16()
+        _check(_lib().fecgpu_encoder_add_source(self._h, pkt, len(pkt), ctypes.byref(w),
+                                                ctypes.byref(i)), "fecgpu_encoder_add_source")
+        return w.value, i.value
+
+    def close_window(self) -> int:
+        return _check(_lib().fecgpu_encoder_close_window(self._h), "fecgpu_encoder_close_window")
+
+    def flush(self) -> int:
+        return _check(_lib().fecgpu_encoder_flush(self._h), "fecgpu_encoder_flush")
+
+    def repair(self, win: int, i: int, cap: int = 65538) -> bytes | None:
+        buf = ctypes.create_string_buffer(cap)
+        n = _lib().fecgpu_encoder_repair(self._h, win, i, buf, cap)
+        if n == ERR_DONE:
+            return None
+        return buf.raw[:_check(n, "fecgpu_encoder_repair")]
+
+    def release(self, win: int) -> int:
+        return _lib().fecgpu_encoder_release(self._h, win)
+
+    def close(self):
+        if self._h:
+            _lib().fecgpu_encoder_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Decoder:
+    """Per-connection receiver (fecgpu_decoder_*): file packets, read recovered ones."""
+
+    def __init__(self, ctx: Context, code: Code, max_len: int, batch: int = 64):
+        self._ctx = ctx
+        self.code = code
+        self._h = ctypes.c_void_p()
+        _check(_lib().fecgpu_decoder_new(ctx.handle, ctypes.byref(code.c), max_len, batch,
+                                         ctypes.byref(self._h)), "fecgpu_decoder_new")
+
+    def add_source(self, win: int, idx: int, pkt: bytes) -> int:
+        return _lib().fecgpu_decoder_add_source(self._h, win, idx, pkt, len(pkt))
+
+    def add_repair(self, win: int, idx: int, sym: bytes) -> int:
+        return _lib().fecgpu_decoder_add_repair(self._h, win, idx, sym, len(sym))
+
+    def flush(self) -> int:
+        return _check(_lib().fecgpu_decoder_flush(self._h), "fecgpu_decoder_flush")
+
+    def recovered(self, win: int, idx: int, cap: int = 65536) -> bytes | None:
+        buf = ctypes.create_string_buffer(cap)
+        n = _lib().fecgpu_decoder_recovered(self._h, win, idx, buf, cap)
+        if n == ERR_DONE:
+            return None
+        return buf.raw[:_check(n, "fecgpu_decoder_recovered")]
+
+    def release(self, win: int) -> int:
+        return _lib().fecgpu_decoder_release(self._h, win)
+
+    def close(self):
+        if self._h:
+            _lib().fecgpu_decoder_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def round_up(x: int, m: int) -> int:

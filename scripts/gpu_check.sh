@@ -1,6 +1,8 @@
 #!/bin/bash
-# One gpurun call: smoke, GPU parity tests, bench, rocprofv3 kernel stats.
-# Each GPU step has its own time limit; a fault/abort/timeout stops the script.
+# One gpurun call = a list of steps, e.g.
+#   gpurun -- 'bash scripts/gpu_check.sh smoke pytest bench2 prof2'
+# Each GPU step has its own time limit; a fault / abort / timeout stops the
+# script (no further GPU work in that call).  Test failures (rc 1) continue.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
@@ -11,22 +13,41 @@ step() {  # name timeout cmd...
     timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
     local rc=$?
     echo "== $name rc=$rc"
-    tail -n 15 "gpurun_out/$name.log"
+    tail -n 25 "gpurun_out/$name.log"
     if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 3 ]; then
         echo "stopping after $name (rc=$rc)"
         exit $rc
     fi
     return 0
 }
-WHAT=${1:-all}
-if [ "$WHAT" = all ] || [ "$WHAT" = test ] || [ "$WHAT" = first ]; then
-    step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-    step pytest 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider
-fi
-if [ "$WHAT" = all ] || [ "$WHAT" = bench ] || [ "$WHAT" = first ]; then
-    step bench2 600 python bench.py --config 2 --steps 20 --warmup 3
-    [ "$WHAT" = first ] || step bench3 600 python bench.py --config 3 --steps 10 --warmup 2 --cpu-seconds 5
-    [ "$WHAT" = first ] || step bench4 600 python bench.py --config 4 --steps 5 --warmup 1 --cpu-seconds 5
-    step prof2 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof2 -o run -- python bench.py --config 2 --steps 10 --warmup 2 --cpu-seconds 0
-fi
+prof() {  # name config extra-args...
+    local name=$1 cfg=$2; shift 2
+    step "$name" 600 rocprofv3 --kernel-trace --stats -f csv -d "gpurun_out/$name" -o run -- \
+        python bench.py --config "$cfg" --steps 10 --warmup 2 --cpu-seconds 0 "$@"
+}
+pmc() {  # name config counters...
+    local name=$1 cfg=$2; shift 2
+    step "$name" 600 rocprofv3 --kernel-trace --pmc "$@" -f csv -d "gpurun_out/$name" -o run -- \
+        python bench.py --config "$cfg" --steps 3 --warmup 1 --cpu-seconds 0 --no-verify
+}
+[ $# -eq 0 ] && set -- smoke pytest bench2 prof2
+for s in "$@"; do
+    case $s in
+        smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        pytest) step pytest 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+        pytest-x) step pytest 1100 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+        bench2) step bench2 600 python bench.py --config 2 --steps 20 --warmup 3 ;;
+        bench3) step bench3 600 python bench.py --config 3 --steps 10 --warmup 2 --cpu-seconds 10 ;;
+        bench4) step bench4 600 python bench.py --config 4 --steps 5 --warmup 1 --cpu-seconds 10 ;;
+        prof2) prof prof2 2 ;;
+        prof3) prof prof3 3 ;;
+        prof4) prof prof4 4 ;;
+        pmc2r) pmc pmc2r 2 FETCH_SIZE ;;
+        pmc2w) pmc pmc2w 2 WRITE_SIZE ;;
+        pmc3r) pmc pmc3r 3 FETCH_SIZE ;;
+        pmc3w) pmc pmc3w 3 WRITE_SIZE ;;
+        micro) step micro 600 python scripts/microbench.py ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
 echo "== done"

@@ -1,0 +1,126 @@
+"""Per-connection encoder/decoder objects (the Connection's per-packet API) on the GPU.
+
+test_loopsim_* is the BASELINE.json config-1 stand-in: a 10 MB
+stream in 1200-B packets through the XOR k=4 r=1 sender, a seeded lossy channel
+and the receiver; every packet of every recoverable window must come back
+byte-identical.  (The reference runs this over quiche client<->server on
+loopback; Rust quiche is not available here.)
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import fecgpu  # noqa: E402
+import np_oracle as N  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    assert torch.cuda.is_available()
+    c = fecgpu.Context()
+    yield c
+    c.close()
+
+
+def _stream(nbytes, seed):
+    return N.payload(seed, 0, 0, nbytes).tobytes() if nbytes < 1 << 16 else b"".join(
+        N.payload(seed, i, 1, min(1 << 16, nbytes - (i << 16))).tobytes()
+        for i in range((nbytes + (1 << 16) - 1) >> 16))
+
+
+def _run(ctx, code, data, mtu, loss, seed, batch=256, vary=False):
+    rng = np.random.default_rng(seed)
+    pkts, pos = [], 0
+    while pos < len(data):
+        n = mtu if not vary else int(rng.integers(1, mtu + 1))
+        pkts.append(data[pos:pos + n])
+        pos += n
+    enc = fecgpu.Encoder(ctx, code, max_len=mtu, batch=batch)
+    dec = fecgpu.Decoder(ctx, code, max_len=mtu, batch=batch)
+    ids = []
+    lost_src = rng.random(len(pkts)) < loss
+    for p, lost in zip(pkts, lost_src):
+        w, i = enc.add_source(p)
+        ids.append((w, i))
+        if not lost:
+            assert dec.add_source(w, i, p) == 0
+    last = enc.close_window() if len(pkts) % code.k else ids[-1][0]
+    enc.flush()
+    nwin = ids[-1][0] + 1
+    assert last == nwin - 1
+    # the sender signals the short last window: its padding sources are known-empty
+    pad = b"" if code.framing == "lenprefix" else b"\0" * len(pkts[-1])
+    for i in range(ids[-1][1] + 1, code.k):
+        assert dec.add_source(nwin - 1, i, pad) == 0
+    rep_lost = rng.random((nwin, code.r)) < loss
+    for w in range(nwin):
+        for i in range(code.r):
+            rep = enc.repair(w, i)
+            assert rep is not None
+            if not rep_lost[w, i]:
+                assert dec.add_repair(w, i, rep) == 0
+    dec.flush()
+    got, missing = [], 0
+    for (w, i), p in zip(ids, pkts):
+        q = dec.recovered(w, i)
+        if q is None:
+            missing += 1
+        else:
+            assert q == p, (w, i)
+        got.append(q)
+    # expected losses after recovery, from the masks alone
+    exp_missing = 0
+    for w in range(nwin):
+        idx = [t for t, (ww, _) in enumerate(ids) if ww == w]
+        lost = [bool(lost_src[t]) for t in idx] + [False] * (code.k - len(idx))
+        rl = list(rep_lost[w])
+        if code.scheme == "xor":
+            for g in range(code.r):
+                mem = [j for j in range(len(idx)) if j % code.r == g]
+                nl = sum(lost[j] for j in mem)
+                if nl == 1 and not rl[g]:
+                    continue
+                exp_missing += nl
+        else:
+            nl = sum(lost[:len(idx)])
+            if nl > code.r - sum(rl):
+                exp_missing += nl
+    assert missing == exp_missing
+    return len(pkts), missing
+
+
+def test_loopsim_xor_k4r1_10MB(ctx):
+    data = _stream(10 * 1024 * 1024, 11)
+    code = fecgpu.Code("xor", 4, 1, "lenprefix")
+    n, missing = _run(ctx, code, data, 1200, 0.02, 3)
+    assert n == (len(data) + 1199) // 1200
+    assert missing < n * 0.01
+
+
+def test_conn_gf_variable_lengths(ctx):
+    data = _stream(2 * 1024 * 1024, 12)
+    code = fecgpu.Code("gf256", 16, 4, "lenprefix")
+    n, missing = _run(ctx, code, data, 1350, 0.08, 5, batch=32, vary=True)
+    assert missing < n * 0.05
+
+
+def test_conn_fixed_framing(ctx):
+    data = _stream(600 * 1000, 13)
+    code = fecgpu.Code("gf256", 8, 3, "fixed")
+    _run(ctx, code, data, 1000, 0.1, 7, batch=8)
+
+
+def test_conn_errors(ctx):
+    code = fecgpu.Code("gf256", 4, 2, "fixed")
+    enc = fecgpu.Encoder(ctx, code, max_len=100, batch=4)
+    with pytest.raises(fecgpu.FecError):
+        enc.add_source(b"x" * 101)              # > max_len
+    enc.add_source(b"a" * 50)
+    with pytest.raises(fecgpu.FecError):
+        enc.add_source(b"b" * 49)               # FIXED: lengths must match in a window
+    assert enc.repair(0, 0) is None             # not encoded yet
+    dec = fecgpu.Decoder(ctx, code, max_len=100, batch=4)
+    assert dec.add_source(0, 5, b"z" * 10) == fecgpu.ERR_INVALID_ARG  # idx >= k
+    assert dec.recovered(0, 1) is None
