@@ -49,6 +49,8 @@ def parse():
                     help="target CPU work for the cpu_baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--grid-mult", type=int, default=0, help="tuning: persistent grid multiplier")
+    ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
     return ap.parse_args()
 
 
@@ -115,6 +117,10 @@ def main():
     nwin = args.nwin or cfg.nwin_per_gpu
     w0, nwin = shard.weak_shard(rank, world, nwin)  # this rank's global window range
     ctx = fecgpu.Context()
+    if args.grid_mult:
+        ctx.set_tuning("grid_mult", args.grid_mult)
+    if args.wpb:
+        ctx.set_tuning("wpb", args.wpb)
     batch = workloads.Batch.allocate(cfg, nwin, dev)
     log(f"rank {rank}: {cfg.name}, windows [{w0}, {w0 + nwin}), {batch.win.numel() / 2**30:.2f} GiB")
     batch.synthesize(ctx, w0)

@@ -93,6 +93,9 @@ ssize_t     fecgpu_code_check(const fecgpu_code *code);
  * over the ctx's devices. */
 ssize_t fecgpu_ctx_new(const int *devs, int ndev, fecgpu_ctx **out);
 void    fecgpu_ctx_free(fecgpu_ctx *ctx);
+/* Launch tuning knobs (0 = automatic): "grid_mult" (persistent grid =
+ * resident workgroups x value), "wpb" (windows per workgroup, group mode). */
+ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value);
 
 /* ---- batch entry points (hot path) ---------------------------------- */
 

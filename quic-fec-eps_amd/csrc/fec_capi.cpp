@@ -58,6 +58,9 @@ struct fecgpu_ctx {
     std::map<std::tuple<int, int, int>, EncTables> enc;
     // host-pointer staging per device
     std::map<int, std::pair<void *, size_t>> stage;
+    // tuning knobs (fecgpu_ctx_set_tuning): 0 = automatic
+    int grid_mult = 1;
+    int wpb_override = 0;
 };
 
 extern "C" {
@@ -119,6 +122,21 @@ ssize_t fecgpu_ctx_new(const int *devs, int ndev, fecgpu_ctx **out) {
     }
     *out = c;
     return 0;
+}
+
+ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
+    if (!ctx || !key) return FECGPU_ERR_INVALID_ARG;
+    if (!std::strcmp(key, "grid_mult")) {
+        if (value < 0 || value > 64) return FECGPU_ERR_INVALID_ARG;
+        ctx->grid_mult = value ? (int)value : 1;
+        return 0;
+    }
+    if (!std::strcmp(key, "wpb")) {
+        if (value < 0 || value > kMaxWpb) return FECGPU_ERR_INVALID_ARG;
+        ctx->wpb_override = (int)value;
+        return 0;
+    }
+    return FECGPU_ERR_UNSUPPORTED;
 }
 
 void fecgpu_ctx_free(fecgpu_ctx *ctx) {
@@ -314,6 +332,11 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
     else if (!win_off) ncol = stride >> 4;
 
     LaunchPlan p{};
+    p.grid_mult = ctx->grid_mult;
+    // flat slot space when every window has the same geometry (GF decode
+    // always plans per window in LDS, so it always runs in group mode)
+    p.flat = !win_off && !sym_len && !(decode && scheme == FECGPU_SCHEME_GF256);
+    a.ncol = (sym_len_all + 15u) >> 4;
     if (!decode) {
         if (scheme == FECGPU_SCHEME_GF256) {
             EncTables t;
@@ -333,10 +356,12 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
             p.wpb = choose_wpb(ncol, 0, 0);
         }
     }
+    if (ctx->wpb_override > 0 && !p.flat) {
+        p.wpb = std::min(ctx->wpb_override, kMaxWpb);
+        if (p.win_lds) p.lds_bytes = p.win_lds * (uint32_t)p.wpb;
+    }
     a.wpb = p.wpb;
     a.win_lds = p.win_lds;
-    p.blocks = (nwin + p.wpb - 1) / p.wpb;
-    if (p.blocks > 0x7FFFFFFFull) return FECGPU_ERR_UNSUPPORTED;
 
     hipError_t e = decode ? launch_decode(scheme, a, p, s) : launch_encode(scheme, a, p, s);
     if (e != hipSuccess) return dev_err(e, decode ? "decode launch" : "encode launch");

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "fec_spec.h"
 
 namespace fecgpu {
@@ -24,18 +26,22 @@ struct BatchArgs {
     const uint32_t *enc_c;     // encode tables [k][r] (TC)
     uint64_t nwin;
     uint64_t gmask[kMaxR];     // XOR: members of group g (bit j)
+    uint64_t step_win;         // flat mode: (grid threads) / ncol
+    uint32_t step_col;         // flat mode: (grid threads) % ncol
+    uint32_t ncol;             // flat mode: 16-byte columns per symbol
     uint32_t S_all;
     uint32_t stride;
     int k, r;
-    int wpb;                   // windows per workgroup
-    uint32_t win_lds;          // decode: LDS bytes per window region
+    int wpb;                   // group mode: windows per workgroup
+    uint32_t win_lds;          // GF decode: LDS bytes per window region
 };
 
 struct LaunchPlan {
+    bool flat;           // uniform S and stride: flat slot space
     int wpb;
     uint32_t lds_bytes;  // dynamic LDS per workgroup
-    uint32_t win_lds;    // per-window region (decode)
-    uint64_t blocks;
+    uint32_t win_lds;    // per-window region (GF decode)
+    int grid_mult;       // resident blocks x grid_mult (tuning; default 1)
 };
 
 // Per-window LDS region of the GF decode kernel: tables [k][R] uint4 + [k][R] u32,

@@ -1,33 +1,55 @@
 // fec_kernels.hip — gfx950 kernels of the FEC hot path.
 //
-// Work decomposition.  A workgroup of 256 threads owns
-// `wpb` consecutive windows.  Their 16-byte symbol columns are flattened into
-// one slot range (prefix sum of per-window column counts in LDS), so a wave
-// streams columns of one or two windows and no lane idles on a short window.
-// A lane owns one 16-byte column and walks the window's k input symbols with
-// coalesced 16-B loads (consecutive lanes = consecutive columns of one symbol
-// row), accumulating up to r outputs in registers, then stores them.
+// Work decomposition.  The unit of work is a *slot*: one
+// 16-byte column of one window.  A lane owns a slot and walks the window's
+// input symbols with coalesced 16-B loads (consecutive lanes = consecutive
+// columns of one symbol row), accumulates up to r outputs in registers and
+// stores them.  All kernels are persistent: the grid is sized to the blocks
+// that fit the chip at once and loops, so no partial last wave of blocks.
+//   flat mode  — every window has the same S and stride: slot s -> window
+//                s / ncol, column s % ncol, advanced incrementally.
+//   group mode — per-window S or ragged offsets, and every GF decode: a
+//                workgroup takes `wpb` windows at a time, plans them in LDS
+//                (geometry, and for GF decode the per-window decode tables),
+//                then streams the flattened column range of those windows.
 //
 // GF(2^8) multiply (DESIGN.md §GF multiply): a coefficient c becomes three
-// byte tables (3+3+2 bits of the data byte) and each lookup is one
-// v_perm_b32 on four packed bytes, so c*x for 4 bytes costs 3 v_perm + 3
-// v_xor, and the bit-field split of the data (5 VALU per dword) is shared by
-// every output.  Tables are wave-uniform (encode) or per window (decode) and
-// read from LDS as broadcasts.
+// byte tables over 3+3+2 bits of the data byte, so c*x for four packed bytes
+// is 3 v_perm_b32 + 3 v_xor; the bit-field split of the data (5 VALU per
+// dword) is shared by every output.
 #include "fec_internal.h"
+
+#ifndef FECGPU_NT
+#define FECGPU_NT 0  // nontemporal (streaming) loads/stores; A/B build knob
+#endif
 
 namespace fecgpu {
 
 __constant__ GfTables c_gf = make_gf_tables();
 
 // ------------------------------------------------------------ helpers ---
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
-    return *reinterpret_cast<const uint4 *>(p);
+#if FECGPU_NT
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+#else
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(p);
+#endif
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ void st16(uint8_t *p, uint4 v) { *reinterpret_cast<uint4 *>(p) = v; }
+__device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
+    const u32x4 x = {v.x, v.y, v.z, v.w};
+#if FECGPU_NT
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
+#else
+    *reinterpret_cast<u32x4 *>(p) = x;
+#endif
+}
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
     return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
+__device__ __forceinline__ uint4 zero4() { return make_uint4(0, 0, 0, 0); }
 
 struct Split {
     uint32_t a[4], b[4], c[4];
@@ -69,207 +91,263 @@ __device__ __forceinline__ void win_geom(const BatchArgs &a, uint64_t w, uint64_
     }
 }
 
-// Inclusive scan of ncol over the block's windows by wave 0 (nb <= 64).
+// Inclusive scan of per-window column counts by wave 0 (nb <= 64).
 __device__ __forceinline__ void block_prefix(uint32_t *pfx, uint32_t v, int lane) {
     uint32_t x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o, 64);
+        const uint32_t y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
     }
     pfx[lane + 1] = x;
     if (lane == 0) pfx[0] = 0;
 }
 
-#define WAVE_SYNC()                                                  \
-    do {                                                             \
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");      \
-        __builtin_amdgcn_wave_barrier();                             \
+#define WAVE_SYNC()                                             \
+    do {                                                        \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); \
+        __builtin_amdgcn_wave_barrier();                        \
     } while (0)
 
-// ============================================================ encode ===
-// XOR (a4): R_g = xor of S_j, j = g mod r.  STEP loads in flight per lane.
-template <int R>
-__global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
-    __shared__ uint32_t s_pfx[kMaxWpb + 1];
-    __shared__ uint64_t s_base[kMaxWpb];
-    __shared__ uint32_t s_stride[kMaxWpb];
-    constexpr int STEP = R >= 4 ? R : R * ((4 + R - 1) / R);
-    const int tid = threadIdx.x, k = a.k;
-    const uint64_t w0 = (uint64_t)blockIdx.x * a.wpb;
-    const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
-    if (tid < 64) {
-        uint32_t ncol = 0;
-        if (tid < nb) {
-            uint64_t base; uint32_t stride, S;
-            win_geom(a, w0 + tid, base, stride, S);
-            s_base[tid] = base;
-            s_stride[tid] = stride;
-            ncol = (S + 15u) >> 4;
+// ------------------------------------------------------ slot iterators ---
+// Flat mode: lane slots s, s + G, s + 2G, ... with (window, column) carried
+// incrementally (G = grid threads, G / ncol and G % ncol precomputed on host).
+template <class Body>
+__device__ __forceinline__ void for_flat_slots(const BatchArgs &a, Body &&body) {
+    const uint32_t ncol = a.ncol;
+    const uint64_t total = a.nwin * ncol;
+    uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= total) return;
+    uint64_t w = s / ncol;
+    uint32_t col = (uint32_t)(s - w * ncol);
+    const uint64_t G = (uint64_t)gridDim.x * kBlock;
+    const uint64_t wbytes = (uint64_t)(a.k + a.r) * a.stride;
+    for (; s < total; s += G) {
+        body(a.win + w * wbytes + col * 16u, a.stride, w, col);
+        col += a.step_col;
+        w += a.step_win;
+        if (col >= ncol) {
+            col -= ncol;
+            w++;
         }
-        block_prefix(s_pfx, ncol, tid);
-    }
-    __syncthreads();
-    const uint32_t total = s_pfx[nb];
-    int wl = 0;
-    for (uint32_t s = tid; s < total; s += kBlock) {
-        while (s >= s_pfx[wl + 1]) wl++;
-        const uint32_t col = s - s_pfx[wl];
-        uint8_t *base = reinterpret_cast<uint8_t *>(s_base[wl]) + col * 16u;
-        const uint32_t stride = s_stride[wl];
-        uint4 acc[R];
-#pragma unroll
-        for (int g = 0; g < R; g++) acc[g] = make_uint4(0, 0, 0, 0);
-        for (int j0 = 0; j0 < k; j0 += STEP) {
-            uint4 v[STEP];
-#pragma unroll
-            for (int t = 0; t < STEP; t++)
-                v[t] = (j0 + t < k) ? ld16(base + (size_t)(j0 + t) * stride) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (int t = 0; t < STEP; t++) acc[t % R] = xor4(acc[t % R], v[t]);
-        }
-#pragma unroll
-        for (int g = 0; g < R; g++) st16(base + (size_t)(k + g) * stride, acc[g]);
     }
 }
 
-// GF(2^8) (a5): R_i = sum_j C[i][j] * S_j with kernel-uniform tables in LDS.
+// Group mode header: geometry of windows [w0, w0 + nb) into LDS; `ncol_eff`
+// lets a plan drop windows with nothing to do (decode).
+struct GroupLds {
+    uint32_t pfx[kMaxWpb + 1];
+    uint64_t base[kMaxWpb];
+    uint32_t stride[kMaxWpb];
+    uint32_t ncol[kMaxWpb];
+};
+
+// Streams the flattened columns of the current group: body(base_of_column, stride, wl).
+template <class Body>
+__device__ __forceinline__ void for_group_slots(const GroupLds &g, int nb, Body &&body) {
+    const uint32_t total = g.pfx[nb];
+    int wl = 0;
+    for (uint32_t s = threadIdx.x; s < total; s += kBlock) {
+        while (s >= g.pfx[wl + 1]) wl++;
+        const uint32_t col = s - g.pfx[wl];
+        body(reinterpret_cast<uint8_t *>(g.base[wl]) + col * 16u, g.stride[wl], wl);
+    }
+}
+
+__device__ __forceinline__ void group_geometry(const BatchArgs &a, GroupLds &g, uint64_t w0, int nb) {
+    const int tid = threadIdx.x;
+    if (tid < nb) {
+        uint64_t base; uint32_t stride, S;
+        win_geom(a, w0 + tid, base, stride, S);
+        g.base[tid] = base;
+        g.stride[tid] = stride;
+        g.ncol[tid] = (S + 15u) >> 4;
+    }
+}
+
+// ============================================================== bodies ===
+// XOR encode (a4): R_g = xor of S_j, j = g (mod r).  All loads of a slot are
+// issued before the xors (8 x 16 B in flight per lane at k = 8).
 template <int R>
+__device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, int k) {
+    constexpr int STEP = R * ((8 + R - 1) / R);
+    uint4 acc[R];
+#pragma unroll
+    for (int g = 0; g < R; g++) acc[g] = zero4();
+    for (int j0 = 0; j0 < k; j0 += STEP) {
+        uint4 v[STEP];
+#pragma unroll
+        for (int t = 0; t < STEP; t++)
+            v[t] = (j0 + t < k) ? ld16(base + (size_t)(j0 + t) * stride) : zero4();
+#pragma unroll
+        for (int t = 0; t < STEP; t++) acc[t % R] = xor4(acc[t % R], v[t]);
+    }
+#pragma unroll
+    for (int g = 0; g < R; g++) st16(base + (size_t)(k + g) * stride, acc[g]);
+}
+
+// GF encode (a5): R_i = sum_j C[i][j] * S_j, tables [j][i] in LDS (broadcast reads).
+template <int R>
+__device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, int k,
+                                               const uint4 *tab, const uint32_t *tc) {
+    constexpr int U = R <= 4 ? 4 : 2;
+    uint4 acc[R];
+#pragma unroll
+    for (int m = 0; m < R; m++) acc[m] = zero4();
+    for (int j0 = 0; j0 < k; j0 += U) {
+        uint4 v[U];
+#pragma unroll
+        for (int t = 0; t < U; t++)
+            v[t] = (j0 + t < k) ? ld16(base + (size_t)(j0 + t) * stride) : zero4();
+#pragma unroll
+        for (int t = 0; t < U; t++) {
+            if (j0 + t < k) {
+                const Split sp = split(v[t]);
+                const int row = (j0 + t) * R;
+#pragma unroll
+                for (int m = 0; m < R; m++) gmac(acc[m], sp, tab[row + m], tc[row + m]);
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < R; m++) st16(base + (size_t)(k + m) * stride, acc[m]);
+}
+
+// XOR decode (a6/a8), planned inline from the window's present mask: every
+// group with exactly one missing source and its repair present is rebuilt as
+// repair ^ (other members).  Loads of all recoverable groups are issued first.
+// Returns the window status (1 if some source stays missing).
+template <int R>
+__device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t *base,
+                                                    uint32_t stride, uint64_t pres) {
+    const int k = a.k;
+    const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
+    const uint64_t miss = ~pres & kmask;
+    uint32_t bad = 0;
+#pragma unroll
+    for (int g = 0; g < R; g++) {
+        const uint64_t gm = a.gmask[g];
+        const uint64_t mg = miss & gm;
+        if (!mg) continue;
+        const bool rec = ((mg & (mg - 1)) == 0) && ((pres >> (k + g)) & 1);
+        if (!rec) {
+            bad = 1;
+            continue;
+        }
+        const int m = __ffsll((unsigned long long)mg) - 1;
+        uint4 acc = ld16(base + (size_t)(k + g) * stride);
+        for (int j0 = g; j0 < k; j0 += 8 * R) {
+            uint4 v[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                const int j = j0 + t * R;
+                v[t] = (j < k && j != m) ? ld16(base + (size_t)j * stride) : zero4();
+            }
+#pragma unroll
+            for (int t = 0; t < 8; t++) acc = xor4(acc, v[t]);
+        }
+        st16(base + (size_t)m * stride, acc);
+    }
+    return bad;
+}
+
+// ============================================================ encode ===
+template <int R, bool FLAT>
+__global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
+    if constexpr (FLAT) {
+        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t) {
+            xor_encode_slot<R>(p, stride, a.k);
+        });
+    } else {
+        __shared__ GroupLds g;
+        for (uint64_t grp = blockIdx.x; grp * a.wpb < a.nwin; grp += gridDim.x) {
+            const uint64_t w0 = grp * a.wpb;
+            const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
+            group_geometry(a, g, w0, nb);
+            __syncthreads();
+            if (threadIdx.x < 64) block_prefix(g.pfx, (int)threadIdx.x < nb ? g.ncol[threadIdx.x] : 0u, threadIdx.x);
+            __syncthreads();
+            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int) {
+                xor_encode_slot<R>(p, stride, a.k);
+            });
+            __syncthreads();
+        }
+    }
+}
+
+template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void gf_encode_kernel(BatchArgs a) {
     extern __shared__ uint4 dyn[];
-    __shared__ uint32_t s_pfx[kMaxWpb + 1];
-    __shared__ uint64_t s_base[kMaxWpb];
-    __shared__ uint32_t s_stride[kMaxWpb];
-    constexpr int U = 4;
-    const int tid = threadIdx.x, k = a.k;
+    const int k = a.k;
     uint4 *tab = dyn;
     uint32_t *tc = reinterpret_cast<uint32_t *>(dyn + k * R);
-    for (int i = tid; i < k * R; i += kBlock) {
+    for (int i = threadIdx.x; i < k * R; i += kBlock) {
         tab[i] = a.enc_ab[i];
         tc[i] = a.enc_c[i];
     }
-    const uint64_t w0 = (uint64_t)blockIdx.x * a.wpb;
-    const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
-    if (tid < 64) {
-        uint32_t ncol = 0;
-        if (tid < nb) {
-            uint64_t base; uint32_t stride, S;
-            win_geom(a, w0 + tid, base, stride, S);
-            s_base[tid] = base;
-            s_stride[tid] = stride;
-            ncol = (S + 15u) >> 4;
-        }
-        block_prefix(s_pfx, ncol, tid);
-    }
     __syncthreads();
-    const uint32_t total = s_pfx[nb];
-    int wl = 0;
-    for (uint32_t s = tid; s < total; s += kBlock) {
-        while (s >= s_pfx[wl + 1]) wl++;
-        const uint32_t col = s - s_pfx[wl];
-        uint8_t *base = reinterpret_cast<uint8_t *>(s_base[wl]) + col * 16u;
-        const uint32_t stride = s_stride[wl];
-        uint4 acc[R];
-#pragma unroll
-        for (int m = 0; m < R; m++) acc[m] = make_uint4(0, 0, 0, 0);
-        for (int j0 = 0; j0 < k; j0 += U) {
-            uint4 v[U];
-#pragma unroll
-            for (int t = 0; t < U; t++)
-                v[t] = (j0 + t < k) ? ld16(base + (size_t)(j0 + t) * stride) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (int t = 0; t < U; t++) {
-                if (j0 + t < k) {
-                    const Split sp = split(v[t]);
-                    const int row = (j0 + t) * R;
-#pragma unroll
-                    for (int m = 0; m < R; m++) gmac(acc[m], sp, tab[row + m], tc[row + m]);
-                }
-            }
+    if constexpr (FLAT) {
+        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t) {
+            gf_encode_slot<R>(p, stride, k, tab, tc);
+        });
+    } else {
+        __shared__ GroupLds g;
+        for (uint64_t grp = blockIdx.x; grp * a.wpb < a.nwin; grp += gridDim.x) {
+            const uint64_t w0 = grp * a.wpb;
+            const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
+            group_geometry(a, g, w0, nb);
+            __syncthreads();
+            if (threadIdx.x < 64) block_prefix(g.pfx, (int)threadIdx.x < nb ? g.ncol[threadIdx.x] : 0u, threadIdx.x);
+            __syncthreads();
+            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int) {
+                gf_encode_slot<R>(p, stride, k, tab, tc);
+            });
+            __syncthreads();
         }
-#pragma unroll
-        for (int m = 0; m < R; m++) st16(base + (size_t)(k + m) * stride, acc[m]);
     }
 }
 
 // ============================================================ decode ===
-// Window plan (a6) for XOR by one wave: every group with exactly one missing
-// source and its repair present becomes an output (group g, missing m).
-__device__ void plan_xor(const BatchArgs &a, uint64_t w, int lane, uint8_t *outg, uint8_t *outm,
-                         uint8_t &ne_out) {
-    const int k = a.k, r = a.r;
-    const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
-    const uint64_t pres = a.present[w];
-    const uint64_t miss = ~pres & kmask;
-    bool rec = false, bad = false;
-    uint64_t gm = 0;
-    if (lane < r) {
-        gm = a.gmask[lane];
-        const int nm = __popcll(miss & gm);
-        const bool rp = (pres >> (k + lane)) & 1;
-        rec = (nm == 1) && rp;
-        bad = (nm >= 1) && !rec;
-    }
-    const uint64_t recm = __ballot(rec);
-    const uint64_t badm = __ballot(bad);
-    if (rec) {
-        const int u = __popcll(recm & ((1ull << lane) - 1));
-        outg[u] = (uint8_t)lane;
-        outm[u] = (uint8_t)(__ffsll((unsigned long long)(miss & gm)) - 1);
-    }
-    if (lane == 0) {
-        ne_out = (uint8_t)__popcll(recm);
-        a.status[w] = badm ? 1 : 0;
-    }
-}
-
-template <int R>
+template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
-    __shared__ uint32_t s_pfx[kMaxWpb + 1];
-    __shared__ uint64_t s_base[kMaxWpb];
-    __shared__ uint32_t s_stride[kMaxWpb];
-    __shared__ uint32_t s_ncol[kMaxWpb];
-    __shared__ uint8_t s_ne[kMaxWpb];
-    __shared__ uint8_t s_outg[kMaxWpb][kMaxR];
-    __shared__ uint8_t s_outm[kMaxWpb][kMaxR];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k, r = a.r;
-    const uint64_t w0 = (uint64_t)blockIdx.x * a.wpb;
-    const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
-    for (int wl = wave; wl < nb; wl += kBlock / 64) {
-        plan_xor(a, w0 + wl, lane, s_outg[wl], s_outm[wl], s_ne[wl]);
-        if (lane == 0) {
-            uint64_t base; uint32_t stride, S;
-            win_geom(a, w0 + wl, base, stride, S);
-            s_base[wl] = base;
-            s_stride[wl] = stride;
-            s_ncol[wl] = (S + 15u) >> 4;
-        }
-    }
-    __syncthreads();
-    if (tid < 64) block_prefix(s_pfx, (tid < nb && s_ne[tid]) ? s_ncol[tid] : 0u, tid);
-    __syncthreads();
-    const uint32_t total = s_pfx[nb];
-    int wl = 0;
-    for (uint32_t s = tid; s < total; s += kBlock) {
-        while (s >= s_pfx[wl + 1]) wl++;
-        const uint32_t col = s - s_pfx[wl];
-        uint8_t *base = reinterpret_cast<uint8_t *>(s_base[wl]) + col * 16u;
-        const uint32_t stride = s_stride[wl];
-        const int ne = s_ne[wl];
-        for (int u = 0; u < ne; u++) {
-            const int g = s_outg[wl][u], m = s_outm[wl][u];
-            uint4 acc = ld16(base + (size_t)(k + g) * stride);
-            for (int j0 = g; j0 < k; j0 += 4 * r) {
-                uint4 v[4];
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const int j = j0 + t * r;
-                    v[t] = (j < k && j != m) ? ld16(base + (size_t)j * stride) : make_uint4(0, 0, 0, 0);
+    if constexpr (FLAT) {
+        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t w, uint32_t col) {
+            const uint32_t bad = xor_decode_slot<R>(a, p, stride, a.present[w]);
+            if (col == 0) a.status[w] = (uint8_t)bad;
+        });
+    } else {
+        __shared__ GroupLds g;
+        __shared__ uint64_t s_pres[kMaxWpb];
+        for (uint64_t grp = blockIdx.x; grp * a.wpb < a.nwin; grp += gridDim.x) {
+            const uint64_t w0 = grp * a.wpb;
+            const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
+            group_geometry(a, g, w0, nb);
+            if ((int)threadIdx.x < nb) s_pres[threadIdx.x] = a.present[w0 + threadIdx.x];
+            __syncthreads();
+            if (threadIdx.x < 64) {
+                uint32_t n = 0;
+                const int t = threadIdx.x;
+                if (t < nb) {
+                    // status from the mask alone; drop windows with nothing to rebuild
+                    const uint64_t kmask = (a.k >= 64) ? ~0ull : ((1ull << a.k) - 1);
+                    const uint64_t miss = ~s_pres[t] & kmask;
+                    uint32_t bad = 0, any = 0;
+                    for (int gi = 0; gi < a.r; gi++) {
+                        const uint64_t mg = miss & a.gmask[gi];
+                        if (!mg) continue;
+                        if ((mg & (mg - 1)) == 0 && ((s_pres[t] >> (a.k + gi)) & 1)) any = 1;
+                        else bad = 1;
+                    }
+                    a.status[w0 + t] = (uint8_t)bad;
+                    n = any ? g.ncol[t] : 0u;
                 }
-#pragma unroll
-                for (int t = 0; t < 4; t++) acc = xor4(acc, v[t]);
+                block_prefix(g.pfx, n, t);
             }
-            st16(base + (size_t)m * stride, acc);
+            __syncthreads();
+            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int wl) {
+                (void)xor_decode_slot<R>(a, p, stride, s_pres[wl]);
+            });
+            __syncthreads();
         }
     }
 }
@@ -318,7 +396,9 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, int lane, uint8_t *regio
         insym[k - e + lane] = (uint8_t)(k + my_sel);
         outsym[lane] = (uint8_t)my_m;
     }
-    // [A | I], A[t][u] = inv((k + sel_t) ^ m_u); lane = t*8 + u
+    // [A | I], A[t][u] = inv((k + sel_t) ^ m_u); lane = t*8 + u.  Every
+    // __shfl below runs with the whole wave active: ds_bpermute returns 0 for
+    // a source lane that is masked off, so no shuffle sits inside a branch.
     const int t = lane >> 3, u = lane & 7;
     const int sel_t = __shfl(my_sel, t & 7, 64);
     const int m_u = __shfl(my_m, u, 64);
@@ -348,8 +428,6 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, int lane, uint8_t *regio
     }
     WAVE_SYNC();
     // D[u][q] for idx = u*k + q; Ainv[u][t] = xr of lane u*8 + t.
-    // Every __shfl runs with the whole wave active: ds_bpermute reads 0 from a
-    // source lane that is masked off, so no shuffle may sit inside a branch.
     const int kr = k - e;
     for (int base = 0; base < e * k; base += 64) {
         const int idx = base + lane;
@@ -382,67 +460,54 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
     extern __shared__ uint4 dyn[];
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
-    __shared__ uint32_t s_pfx[kMaxWpb + 1];
-    __shared__ uint64_t s_base[kMaxWpb];
-    __shared__ uint32_t s_stride[kMaxWpb];
-    __shared__ uint32_t s_ncol[kMaxWpb];
+    __shared__ GroupLds g;
     __shared__ uint8_t s_ne[kMaxWpb];
-    constexpr int U = 4;
+    constexpr int U = R <= 4 ? 4 : 2;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
     uint8_t *regions = reinterpret_cast<uint8_t *>(dyn);
     for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
     for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
     __syncthreads();
-    const uint64_t w0 = (uint64_t)blockIdx.x * a.wpb;
-    const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
-    for (int wl = wave; wl < nb; wl += kBlock / 64) {
-        plan_gf<R>(a, w0 + wl, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log, s_ne[wl]);
-        if (lane == 0) {
-            uint64_t base; uint32_t stride, S;
-            win_geom(a, w0 + wl, base, stride, S);
-            s_base[wl] = base;
-            s_stride[wl] = stride;
-            s_ncol[wl] = (S + 15u) >> 4;
-        }
-    }
-    __syncthreads();
-    if (tid < 64) block_prefix(s_pfx, (tid < nb && s_ne[tid]) ? s_ncol[tid] : 0u, tid);
-    __syncthreads();
-    const uint32_t total = s_pfx[nb];
-    int wl = 0;
-    for (uint32_t s = tid; s < total; s += kBlock) {
-        while (s >= s_pfx[wl + 1]) wl++;
-        const uint32_t col = s - s_pfx[wl];
-        uint8_t *base = reinterpret_cast<uint8_t *>(s_base[wl]) + col * 16u;
-        const uint32_t stride = s_stride[wl];
-        const int ne = s_ne[wl];
-        const uint8_t *region = regions + (size_t)wl * a.win_lds;
-        const uint4 *tab = reinterpret_cast<const uint4 *>(region);
-        const uint32_t *tc = reinterpret_cast<const uint32_t *>(region + k * R * 16);
-        const uint8_t *insym = region + k * R * 20;
-        const uint8_t *outsym = insym + 64;
-        uint4 acc[R];
+    for (uint64_t grp = blockIdx.x; grp * a.wpb < a.nwin; grp += gridDim.x) {
+        const uint64_t w0 = grp * a.wpb;
+        const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
+        group_geometry(a, g, w0, nb);
+        for (int wl = wave; wl < nb; wl += kBlock / 64)
+            plan_gf<R>(a, w0 + wl, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log, s_ne[wl]);
+        __syncthreads();
+        if (tid < 64) block_prefix(g.pfx, (tid < nb && s_ne[tid]) ? g.ncol[tid] : 0u, tid);
+        __syncthreads();
+        for_group_slots(g, nb, [&](uint8_t *base, uint32_t stride, int wl) {
+            const int ne = s_ne[wl];
+            const uint8_t *region = regions + (size_t)wl * a.win_lds;
+            const uint4 *tab = reinterpret_cast<const uint4 *>(region);
+            const uint32_t *tc = reinterpret_cast<const uint32_t *>(region + k * R * 16);
+            const uint8_t *insym = region + k * R * 20;
+            const uint8_t *outsym = insym + 64;
+            uint4 acc[R];
 #pragma unroll
-        for (int m = 0; m < R; m++) acc[m] = make_uint4(0, 0, 0, 0);
-        for (int q0 = 0; q0 < k; q0 += U) {
-            uint4 v[U];
+            for (int m = 0; m < R; m++) acc[m] = zero4();
+            for (int q0 = 0; q0 < k; q0 += U) {
+                uint4 v[U];
 #pragma unroll
-            for (int t = 0; t < U; t++)
-                v[t] = (q0 + t < k) ? ld16(base + (size_t)insym[q0 + t] * stride) : make_uint4(0, 0, 0, 0);
+                for (int t = 0; t < U; t++)
+                    v[t] = (q0 + t < k) ? ld16(base + (size_t)insym[q0 + t] * stride) : zero4();
 #pragma unroll
-            for (int t = 0; t < U; t++) {
-                if (q0 + t < k) {
-                    const Split sp = split(v[t]);
-                    const int row = (q0 + t) * R;
+                for (int t = 0; t < U; t++) {
+                    if (q0 + t < k) {
+                        const Split sp = split(v[t]);
+                        const int row = (q0 + t) * R;
 #pragma unroll
-                    for (int m = 0; m < R; m++)
-                        if (m < ne) gmac(acc[m], sp, tab[row + m], tc[row + m]);
+                        for (int m = 0; m < R; m++)
+                            if (m < ne) gmac(acc[m], sp, tab[row + m], tc[row + m]);
+                    }
                 }
             }
-        }
 #pragma unroll
-        for (int m = 0; m < R; m++)
-            if (m < ne) st16(base + (size_t)outsym[m] * stride, acc[m]);
+            for (int m = 0; m < R; m++)
+                if (m < ne) st16(base + (size_t)outsym[m] * stride, acc[m]);
+        });
+        __syncthreads();
     }
 }
 
@@ -488,7 +553,8 @@ __global__ __launch_bounds__(kBlock) void synth_kernel(SynthArgs a) {
             }
             out[b >> 2] |= byte << (8 * (b & 3));
         }
-        st16(win + (size_t)j * a.stride + c * 16, make_uint4(out[0], out[1], out[2], out[3]));
+        *reinterpret_cast<uint4 *>(win + (size_t)j * a.stride + c * 16) =
+            make_uint4(out[0], out[1], out[2], out[3]);
     }
 }
 
@@ -555,39 +621,71 @@ __global__ __launch_bounds__(kBlock) void digest_kernel(DigestArgs a) {
 }
 
 // ========================================================== launchers ===
-#define DISPATCH_R(R_, KERNEL, ...)                                                      \
-    switch (R_) {                                                                        \
-        case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                       \
-        case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                       \
-        case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;                       \
-        case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                       \
-        case 5: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break;                       \
-        case 6: hipLaunchKernelGGL(KERNEL<6>, __VA_ARGS__); break;                       \
-        case 7: hipLaunchKernelGGL(KERNEL<7>, __VA_ARGS__); break;                       \
-        case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                       \
-        default: return hipErrorInvalidValue;                                            \
-    }
+namespace {
 
-hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
-    if (p.blocks == 0) return hipSuccess;
-    const dim3 grid((unsigned)p.blocks), block(kBlock);
-    if (scheme == 0) {
-        DISPATCH_R(a.r, xor_encode_kernel, grid, block, 0, s, a);
+// Persistent grid: blocks resident on the whole chip for this kernel and LDS size.
+int resident_blocks(const void *fn, uint32_t lds) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1024;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, lds) != hipSuccess || per < 1) per = 1;
+    return cus * per;
+}
+
+template <class K>
+hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, bool flat) {
+    const void *fn = reinterpret_cast<const void *>(kernel);
+    uint64_t want;
+    if (flat) {
+        const uint64_t total = a.nwin * a.ncol;
+        want = (total + kBlock - 1) / kBlock;
     } else {
-        DISPATCH_R(a.r, gf_encode_kernel, grid, block, p.lds_bytes, s, a);
+        want = (a.nwin + a.wpb - 1) / a.wpb;
     }
+    const uint64_t res = (uint64_t)resident_blocks(fn, p.lds_bytes) * (uint64_t)(p.grid_mult > 0 ? p.grid_mult : 1);
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(want, res));
+    if (flat) {
+        const uint64_t G = grid * kBlock;
+        a.step_win = G / a.ncol;
+        a.step_col = (uint32_t)(G % a.ncol);
+    }
+    hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(kBlock), p.lds_bytes, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
-    if (p.blocks == 0) return hipSuccess;
-    const dim3 grid((unsigned)p.blocks), block(kBlock);
-    if (scheme == 0) {
-        DISPATCH_R(a.r, xor_decode_kernel, grid, block, 0, s, a);
-    } else {
-        DISPATCH_R(a.r, gf_decode_kernel, grid, block, p.lds_bytes, s, a);
+}  // namespace
+
+#define DISPATCH_R(R_, EXPR)                    \
+    switch (R_) {                               \
+        case 1: { constexpr int RR = 1; return EXPR; } \
+        case 2: { constexpr int RR = 2; return EXPR; } \
+        case 3: { constexpr int RR = 3; return EXPR; } \
+        case 4: { constexpr int RR = 4; return EXPR; } \
+        case 5: { constexpr int RR = 5; return EXPR; } \
+        case 6: { constexpr int RR = 6; return EXPR; } \
+        case 7: { constexpr int RR = 7; return EXPR; } \
+        case 8: { constexpr int RR = 8; return EXPR; } \
+        default: return hipErrorInvalidValue;   \
     }
-    return hipGetLastError();
+
+hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
+    if (a.nwin == 0) return hipSuccess;
+    const bool flat = p.flat;
+    if (scheme == 0) {
+        if (flat) DISPATCH_R(a.r, launch(xor_encode_kernel<RR, true>, a, p, s, true))
+        else DISPATCH_R(a.r, launch(xor_encode_kernel<RR, false>, a, p, s, false))
+    }
+    if (flat) DISPATCH_R(a.r, launch(gf_encode_kernel<RR, true>, a, p, s, true))
+    else DISPATCH_R(a.r, launch(gf_encode_kernel<RR, false>, a, p, s, false))
+}
+
+hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
+    if (a.nwin == 0) return hipSuccess;
+    if (scheme == 0) {
+        if (p.flat) DISPATCH_R(a.r, launch(xor_decode_kernel<RR, true>, a, p, s, true))
+        else DISPATCH_R(a.r, launch(xor_decode_kernel<RR, false>, a, p, s, false))
+    }
+    DISPATCH_R(a.r, launch(gf_decode_kernel<RR>, a, p, s, false))
 }
 
 hipError_t launch_synth(const SynthArgs &a, hipStream_t s) {

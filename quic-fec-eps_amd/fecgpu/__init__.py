@@ -20,7 +20,8 @@ import os
 from dataclasses import dataclass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libfecgpu.so")
+LIB_PATH = os.environ.get("FECGPU_LIB") or os.path.join(os.path.dirname(_HERE), "lib",
+                                                        "libfecgpu.so")
 
 # enums of include/fecgpu.h
 ERR_DONE, ERR_BUFFER_TOO_SHORT, ERR_INVALID_ARG = -1, -2, -3
@@ -37,7 +38,8 @@ ERASURE_NONE, ERASURE_EXACT, ERASURE_IID = 0, 1, 2
 # every symbol include/fecgpu.h declares (tests check the library exports them)
 EXPORTS = (
     "fecgpu_abi_version", "fecgpu_strerror", "fecgpu_last_error", "fecgpu_code_check",
-    "fecgpu_ctx_new", "fecgpu_ctx_free", "fecgpu_encode_batch", "fecgpu_decode_batch",
+    "fecgpu_ctx_new", "fecgpu_ctx_free", "fecgpu_ctx_set_tuning",
+    "fecgpu_encode_batch", "fecgpu_decode_batch",
     "fecgpu_synth_batch", "fecgpu_erasure_batch", "fecgpu_digest_batch",
     "fecgpu_encoder_new", "fecgpu_encoder_free", "fecgpu_encoder_add_source",
     "fecgpu_encoder_close_window", "fecgpu_encoder_flush", "fecgpu_encoder_repair",
@@ -99,6 +101,7 @@ def _lib():
             "fecgpu_code_check": (sz, [cp]),
             "fecgpu_ctx_new": (sz, [vp, i32, ctypes.POINTER(vp)]),
             "fecgpu_ctx_free": (None, [vp]),
+            "fecgpu_ctx_set_tuning": (sz, [vp, ctypes.c_char_p, ctypes.c_int64]),
             "fecgpu_encode_batch": (sz, [vp, cp, vp, vp, vp, u32, u32, u64, u32, vp]),
             "fecgpu_decode_batch": (sz, [vp, cp, vp, vp, vp, u32, u32, u64, vp, vp, u32, vp]),
             "fecgpu_synth_batch": (sz, [vp, cp, i32, u64, u64, vp, vp, u32, u32, u64, vp]),
@@ -207,6 +210,9 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def set_tuning(self, key: str, value: int) -> None:
+        _check(_lib().fecgpu_ctx_set_tuning(self._h, key.encode(), value), "fecgpu_ctx_set_tuning")
 
     def close(self):
         if self._h:
