@@ -59,7 +59,7 @@ struct fecgpu_ctx {
     // host-pointer staging per device
     std::map<int, std::pair<void *, size_t>> stage;
     // tuning knobs (fecgpu_ctx_set_tuning): 0 = automatic
-    int grid_mult = 1;
+    int grid_mult = 0;
     int wpb_override = 0;
 };
 
@@ -128,7 +128,7 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
     if (!ctx || !key) return FECGPU_ERR_INVALID_ARG;
     if (!std::strcmp(key, "grid_mult")) {
         if (value < 0 || value > 64) return FECGPU_ERR_INVALID_ARG;
-        ctx->grid_mult = value ? (int)value : 1;
+        ctx->grid_mult = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "wpb")) {

@@ -22,6 +22,10 @@
 #ifndef FECGPU_NT
 #define FECGPU_NT 0  // nontemporal (streaming) loads/stores; A/B build knob
 #endif
+#ifndef FECGPU_PIPE
+#define FECGPU_PIPE 0  // register double-buffered input loads in the GF bodies (A/B: no gain,
+                       // costs VGPRs / occupancy on decode; profiles/r01 notes)
+#endif
 
 namespace fecgpu {
 
@@ -175,40 +179,70 @@ __device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, 
 #pragma unroll
     for (int g = 0; g < R; g++) acc[g] = zero4();
     for (int j0 = 0; j0 < k; j0 += STEP) {
+        // branch-free: rows past k re-read row k-1 (cache hit) and are not accumulated
         uint4 v[STEP];
 #pragma unroll
-        for (int t = 0; t < STEP; t++)
-            v[t] = (j0 + t < k) ? ld16(base + (size_t)(j0 + t) * stride) : zero4();
+        for (int t = 0; t < STEP; t++) v[t] = ld16(base + (uint32_t)min(j0 + t, k - 1) * stride);
 #pragma unroll
-        for (int t = 0; t < STEP; t++) acc[t % R] = xor4(acc[t % R], v[t]);
+        for (int t = 0; t < STEP; t++)
+            if (j0 + t < k) acc[t % R] = xor4(acc[t % R], v[t]);
     }
 #pragma unroll
     for (int g = 0; g < R; g++) st16(base + (size_t)(k + g) * stride, acc[g]);
+}
+
+// Software-pipelined GF multiply-accumulate over k inputs of one slot:
+// acc[m] ^= D[q][m] * in_q for q < k, m < min(ne, R).  Inputs are loaded U at
+// a time into one of two register buffers while the other is multiplied, so
+// every wave keeps U 16-B loads in flight through the VALU phase.
+// `addr(q)` gives input q's column address, tables are [q][m] in LDS.
+template <int R, int U, class Addr>
+__device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne, Addr &&addr,
+                                                 const uint4 *tab, const uint32_t *tc) {
+    uint4 va[U], vb[U];
+    auto load = [&](uint4(&v)[U], int q0) {
+#pragma unroll
+        for (int t = 0; t < U; t++) v[t] = ld16(addr(min(q0 + t, k - 1)));  // past k: unused re-read
+    };
+    auto mul = [&](const uint4(&v)[U], int q0) {
+#pragma unroll
+        for (int t = 0; t < U; t++) {
+            if (q0 + t < k) {
+                const Split sp = split(v[t]);
+                const int row = (q0 + t) * R;
+#pragma unroll
+                for (int m = 0; m < R; m++)
+                    if (m < ne) gmac(acc[m], sp, tab[row + m], tc[row + m]);
+            }
+        }
+    };
+#if FECGPU_PIPE
+    load(va, 0);
+    for (int q0 = 0; q0 < k; q0 += 2 * U) {
+        if (q0 + U < k) load(vb, q0 + U);
+        mul(va, q0);
+        if (q0 + U >= k) break;
+        if (q0 + 2 * U < k) load(va, q0 + 2 * U);
+        mul(vb, q0 + U);
+    }
+#else
+    (void)vb;
+    for (int q0 = 0; q0 < k; q0 += U) {
+        load(va, q0);
+        mul(va, q0);
+    }
+#endif
 }
 
 // GF encode (a5): R_i = sum_j C[i][j] * S_j, tables [j][i] in LDS (broadcast reads).
 template <int R>
 __device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, int k,
                                                const uint4 *tab, const uint32_t *tc) {
-    constexpr int U = R <= 4 ? 4 : 2;
+    constexpr int U = 4;
     uint4 acc[R];
 #pragma unroll
     for (int m = 0; m < R; m++) acc[m] = zero4();
-    for (int j0 = 0; j0 < k; j0 += U) {
-        uint4 v[U];
-#pragma unroll
-        for (int t = 0; t < U; t++)
-            v[t] = (j0 + t < k) ? ld16(base + (size_t)(j0 + t) * stride) : zero4();
-#pragma unroll
-        for (int t = 0; t < U; t++) {
-            if (j0 + t < k) {
-                const Split sp = split(v[t]);
-                const int row = (j0 + t) * R;
-#pragma unroll
-                for (int m = 0; m < R; m++) gmac(acc[m], sp, tab[row + m], tc[row + m]);
-            }
-        }
-    }
+    gf_mac_pipelined<R, U>(acc, k, R, [&](int q) { return base + (uint32_t)q * stride; }, tab, tc);
 #pragma unroll
     for (int m = 0; m < R; m++) st16(base + (size_t)(k + m) * stride, acc[m]);
 }
@@ -462,7 +496,7 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
     __shared__ uint8_t s_log[256];
     __shared__ GroupLds g;
     __shared__ uint8_t s_ne[kMaxWpb];
-    constexpr int U = R <= 4 ? 4 : 2;
+    constexpr int U = 4;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
     uint8_t *regions = reinterpret_cast<uint8_t *>(dyn);
     for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
@@ -487,22 +521,8 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
             uint4 acc[R];
 #pragma unroll
             for (int m = 0; m < R; m++) acc[m] = zero4();
-            for (int q0 = 0; q0 < k; q0 += U) {
-                uint4 v[U];
-#pragma unroll
-                for (int t = 0; t < U; t++)
-                    v[t] = (q0 + t < k) ? ld16(base + (size_t)insym[q0 + t] * stride) : zero4();
-#pragma unroll
-                for (int t = 0; t < U; t++) {
-                    if (q0 + t < k) {
-                        const Split sp = split(v[t]);
-                        const int row = (q0 + t) * R;
-#pragma unroll
-                        for (int m = 0; m < R; m++)
-                            if (m < ne) gmac(acc[m], sp, tab[row + m], tc[row + m]);
-                    }
-                }
-            }
+            gf_mac_pipelined<R, U>(acc, k, ne,
+                                   [&](int q) { return base + (uint32_t)insym[q] * stride; }, tab, tc);
 #pragma unroll
             for (int m = 0; m < R; m++)
                 if (m < ne) st16(base + (size_t)outsym[m] * stride, acc[m]);
@@ -642,8 +662,16 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
     } else {
         want = (a.nwin + a.wpb - 1) / a.wpb;
     }
-    const uint64_t res = (uint64_t)resident_blocks(fn, p.lds_bytes) * (uint64_t)(p.grid_mult > 0 ? p.grid_mult : 1);
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(want, res));
+    // Flat mode: persistent, 2 x resident workgroups (measured best on cfg2/cfg3).
+    // Group mode: one workgroup per group unless a multiplier is forced — the
+    // dispatcher's dynamic assignment balances uneven windows better than a
+    // static round-robin over persistent workgroups (cfg4 mixed MTU).
+    uint64_t grid = want;
+    if (flat || p.grid_mult > 0) {
+        const int mult = p.grid_mult > 0 ? p.grid_mult : 2;
+        grid = std::min<uint64_t>(want, (uint64_t)resident_blocks(fn, p.lds_bytes) * (uint64_t)mult);
+    }
+    grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, 0x7FFFFFFFull));
     if (flat) {
         const uint64_t G = grid * kBlock;
         a.step_win = G / a.ncol;

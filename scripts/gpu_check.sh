@@ -47,11 +47,16 @@ for s in "$@"; do
         pmc3r) pmc pmc3r 3 FETCH_SIZE ;;
         pmc3w) pmc pmc3w 3 WRITE_SIZE ;;
         micro) step micro 600 python scripts/microbench.py ;;
-        ab*)  # abN: baseline vs NT build vs grid x2, config N, interleaved twice
+        probe) step probe 300 ./scripts/stream_probe ;;
+        ab*)  # abN: default build vs every lib/libfecgpu_*.so variant, config N, interleaved twice
             c=${s#ab}
             for rep in 1 2; do
                 step ab${c}_base_$rep 300 python bench.py --config $c --steps 20 --warmup 3 --cpu-seconds 0 --no-verify
-                FECGPU_LIB=quic-fec-eps_amd/lib/libfecgpu_nt.so step ab${c}_nt_$rep 300 python bench.py --config $c --steps 20 --warmup 3 --cpu-seconds 0 --no-verify
+                for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
+                    [ -e "$v" ] || continue
+                    n=$(basename $v .so); n=${n#libfecgpu_}
+                    FECGPU_LIB=$v step ab${c}_${n}_$rep 300 python bench.py --config $c --steps 20 --warmup 3 --cpu-seconds 0 --no-verify
+                done
                 step ab${c}_g2_$rep 300 python bench.py --config $c --steps 20 --warmup 3 --cpu-seconds 0 --no-verify --grid-mult 2
             done ;;
         *) echo "unknown step $s"; exit 2 ;;
