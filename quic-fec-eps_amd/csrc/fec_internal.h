@@ -29,6 +29,7 @@ struct BatchArgs {
     uint64_t step_win;         // flat mode: (grid threads) / ncol
     uint32_t step_col;         // flat mode: (grid threads) % ncol
     uint32_t ncol;             // flat mode: 16-byte columns per symbol
+    uint32_t nx;               // XCD regions (8, or 1 for tiny grids)
     uint32_t S_all;
     uint32_t stride;
     int k, r;

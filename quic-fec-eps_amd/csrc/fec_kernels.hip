@@ -22,6 +22,9 @@
 #ifndef FECGPU_NT
 #define FECGPU_NT 0  // nontemporal (streaming) loads/stores; A/B build knob
 #endif
+#ifndef FECGPU_XCD
+#define FECGPU_XCD 1  // XCD-aware split of the work units (A/B knob)
+#endif
 #ifndef FECGPU_PIPE
 #define FECGPU_PIPE 0  // register double-buffered input loads in the GF bodies (A/B: no gain,
                        // costs VGPRs / occupancy on decode; profiles/r01 notes)
@@ -114,20 +117,38 @@ __device__ __forceinline__ void block_prefix(uint32_t *pfx, uint32_t v, int lane
     } while (0)
 
 // ------------------------------------------------------ slot iterators ---
-// Flat mode: lane slots s, s + G, s + 2G, ... with (window, column) carried
-// incrementally (G = grid threads, G / ncol and G % ncol precomputed on host).
+// XCD-aware work split (speed only, never correctness): the dispatcher deals
+// workgroups round-robin over the 8 XCDs, so b, b + 8, b + 16, ... share an
+// L2.  Work units (256-slot chunks, or window groups) are cut into `nx`
+// contiguous regions and region b % nx is walked by workgroups b / nx, so
+// neighbouring units — which share the 128-B lines straddling 1200-B symbol
+// rows and window edges — are fetched through one L2 instead of two.
+struct XcdRange {
+    uint64_t cur, hi, step;
+};
+
+__device__ __forceinline__ XcdRange xcd_range(uint64_t nunits, uint32_t nx) {
+    const uint32_t bx = blockIdx.x % nx, bi = blockIdx.x / nx, nbx = gridDim.x / nx;
+    const uint64_t lo = nunits * bx / nx, hi = nunits * (bx + 1) / nx;
+    return {lo + bi, hi, nbx};
+}
+
+// Flat mode: the lane's slots are chunk*256 + tid for its region's chunks;
+// (window, column) advance incrementally by the per-iteration slot step
+// (step / ncol and step % ncol precomputed on host).
 template <class Body>
 __device__ __forceinline__ void for_flat_slots(const BatchArgs &a, Body &&body) {
     const uint32_t ncol = a.ncol;
     const uint64_t total = a.nwin * ncol;
-    uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (s >= total) return;
+    XcdRange xr = xcd_range((total + kBlock - 1) / kBlock, a.nx);
+    if (xr.cur >= xr.hi) return;
+    uint64_t s = xr.cur * kBlock + threadIdx.x;
     uint64_t w = s / ncol;
     uint32_t col = (uint32_t)(s - w * ncol);
-    const uint64_t G = (uint64_t)gridDim.x * kBlock;
     const uint64_t wbytes = (uint64_t)(a.k + a.r) * a.stride;
-    for (; s < total; s += G) {
-        body(a.win + w * wbytes + col * 16u, a.stride, w, col);
+    for (; xr.cur < xr.hi; xr.cur += xr.step) {
+        if (s < total) body(a.win + w * wbytes + col * 16u, a.stride, w, col);
+        s += xr.step * kBlock;
         col += a.step_col;
         w += a.step_win;
         if (col >= ncol) {
@@ -294,8 +315,9 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
         });
     } else {
         __shared__ GroupLds g;
-        for (uint64_t grp = blockIdx.x; grp * a.wpb < a.nwin; grp += gridDim.x) {
-            const uint64_t w0 = grp * a.wpb;
+        for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi;
+             xr.cur += xr.step) {
+            const uint64_t w0 = xr.cur * a.wpb;
             const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
             group_geometry(a, g, w0, nb);
             __syncthreads();
@@ -326,8 +348,9 @@ __global__ __launch_bounds__(kBlock) void gf_encode_kernel(BatchArgs a) {
         });
     } else {
         __shared__ GroupLds g;
-        for (uint64_t grp = blockIdx.x; grp * a.wpb < a.nwin; grp += gridDim.x) {
-            const uint64_t w0 = grp * a.wpb;
+        for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi;
+             xr.cur += xr.step) {
+            const uint64_t w0 = xr.cur * a.wpb;
             const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
             group_geometry(a, g, w0, nb);
             __syncthreads();
@@ -352,8 +375,9 @@ __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
     } else {
         __shared__ GroupLds g;
         __shared__ uint64_t s_pres[kMaxWpb];
-        for (uint64_t grp = blockIdx.x; grp * a.wpb < a.nwin; grp += gridDim.x) {
-            const uint64_t w0 = grp * a.wpb;
+        for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi;
+             xr.cur += xr.step) {
+            const uint64_t w0 = xr.cur * a.wpb;
             const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
             group_geometry(a, g, w0, nb);
             if ((int)threadIdx.x < nb) s_pres[threadIdx.x] = a.present[w0 + threadIdx.x];
@@ -502,8 +526,9 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
     for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
     for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
     __syncthreads();
-    for (uint64_t grp = blockIdx.x; grp * a.wpb < a.nwin; grp += gridDim.x) {
-        const uint64_t w0 = grp * a.wpb;
+    for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi;
+         xr.cur += xr.step) {
+        const uint64_t w0 = xr.cur * a.wpb;
         const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
         group_geometry(a, g, w0, nb);
         for (int wl = wave; wl < nb; wl += kBlock / 64)
@@ -655,13 +680,9 @@ int resident_blocks(const void *fn, uint32_t lds) {
 template <class K>
 hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, bool flat) {
     const void *fn = reinterpret_cast<const void *>(kernel);
-    uint64_t want;
-    if (flat) {
-        const uint64_t total = a.nwin * a.ncol;
-        want = (total + kBlock - 1) / kBlock;
-    } else {
-        want = (a.nwin + a.wpb - 1) / a.wpb;
-    }
+    // work units: 256-slot chunks (flat) or window groups
+    const uint64_t want = flat ? (a.nwin * a.ncol + kBlock - 1) / kBlock
+                               : (a.nwin + a.wpb - 1) / a.wpb;
     // Flat mode: persistent, 2 x resident workgroups (measured best on cfg2/cfg3).
     // Group mode: one workgroup per group unless a multiplier is forced — the
     // dispatcher's dynamic assignment balances uneven windows better than a
@@ -671,11 +692,23 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
         const int mult = p.grid_mult > 0 ? p.grid_mult : 2;
         grid = std::min<uint64_t>(want, (uint64_t)resident_blocks(fn, p.lds_bytes) * (uint64_t)mult);
     }
-    grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, 0x7FFFFFFFull));
+    // XCD regions: grid a multiple of 8 so every region has the same walkers
+    a.nx = FECGPU_XCD ? 8 : 1;
+    if (a.nx == 1) {
+        grid = std::max<uint64_t>(1, std::min(grid, want));
+    } else if (want < 8) {
+        a.nx = 1;
+        grid = std::max<uint64_t>(1, want);
+    } else if (grid >= want) {
+        grid = (want + 7) / 8 * 8;  // one unit per workgroup
+    } else {
+        grid = std::max<uint64_t>(8, grid / 8 * 8);
+    }
+    grid = std::min<uint64_t>(grid, 0x7FFFFFF8ull);
     if (flat) {
-        const uint64_t G = grid * kBlock;
-        a.step_win = G / a.ncol;
-        a.step_col = (uint32_t)(G % a.ncol);
+        const uint64_t step = grid / a.nx * kBlock;  // slots per iteration
+        a.step_win = step / a.ncol;
+        a.step_col = (uint32_t)(step % a.ncol);
     }
     hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(kBlock), p.lds_bytes, s, a);
     return hipGetLastError();
