@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--grid-mult", type=int, default=0, help="tuning: persistent grid multiplier")
     ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
+    ap.add_argument("--bpc", type=int, default=0, help="tuning: persistent workgroups per CU")
     return ap.parse_args()
 
 
@@ -121,6 +122,8 @@ def main():
         ctx.set_tuning("grid_mult", args.grid_mult)
     if args.wpb:
         ctx.set_tuning("wpb", args.wpb)
+    if args.bpc:
+        ctx.set_tuning("blocks_per_cu", args.bpc)
     batch = workloads.Batch.allocate(cfg, nwin, dev)
     log(f"rank {rank}: {cfg.name}, windows [{w0}, {w0 + nwin}), {batch.win.numel() / 2**30:.2f} GiB")
     batch.synthesize(ctx, w0)

@@ -60,6 +60,7 @@ struct fecgpu_ctx {
     std::map<int, std::pair<void *, size_t>> stage;
     // tuning knobs (fecgpu_ctx_set_tuning): 0 = automatic
     int grid_mult = 0;
+    int blocks_per_cu = 0;
     int wpb_override = 0;
 };
 
@@ -129,6 +130,11 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
     if (!std::strcmp(key, "grid_mult")) {
         if (value < 0 || value > 64) return FECGPU_ERR_INVALID_ARG;
         ctx->grid_mult = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "blocks_per_cu")) {
+        if (value < 0 || value > 64) return FECGPU_ERR_INVALID_ARG;
+        ctx->blocks_per_cu = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "wpb")) {
@@ -333,6 +339,7 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
 
     LaunchPlan p{};
     p.grid_mult = ctx->grid_mult;
+    p.blocks_per_cu = ctx->blocks_per_cu;
     // flat slot space when every window has the same geometry (GF decode
     // always plans per window in LDS, so it always runs in group mode)
     p.flat = !win_off && !sym_len && !(decode && scheme == FECGPU_SCHEME_GF256);

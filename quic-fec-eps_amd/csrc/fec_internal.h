@@ -42,7 +42,8 @@ struct LaunchPlan {
     int wpb;
     uint32_t lds_bytes;  // dynamic LDS per workgroup
     uint32_t win_lds;    // per-window region (GF decode)
-    int grid_mult;       // resident blocks x grid_mult (tuning; default 1)
+    int grid_mult;       // resident blocks x grid_mult (tuning; 0 = automatic)
+    int blocks_per_cu;   // persistent grid of CUs x blocks_per_cu (tuning; 0 = automatic)
 };
 
 // Per-window LDS region of the GF decode kernel: tables [k][R] uint4 + [k][R] u32,

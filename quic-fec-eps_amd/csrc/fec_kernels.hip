@@ -25,6 +25,9 @@
 #ifndef FECGPU_XCD
 #define FECGPU_XCD 1  // XCD-aware split of the work units (A/B knob)
 #endif
+#ifndef FECGPU_XOR_LOADS
+#define FECGPU_XOR_LOADS 8  // XOR encode: input rows loaded per batch (rounded up to r)
+#endif
 #ifndef FECGPU_PIPE
 #define FECGPU_PIPE 0  // register double-buffered input loads in the GF bodies (A/B: no gain,
                        // costs VGPRs / occupancy on decode; profiles/r01 notes)
@@ -195,7 +198,7 @@ __device__ __forceinline__ void group_geometry(const BatchArgs &a, GroupLds &g, 
 // issued before the xors (8 x 16 B in flight per lane at k = 8).
 template <int R>
 __device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, int k) {
-    constexpr int STEP = R * ((8 + R - 1) / R);
+    constexpr int STEP = R * ((FECGPU_XOR_LOADS + R - 1) / R);
     uint4 acc[R];
 #pragma unroll
     for (int g = 0; g < R; g++) acc[g] = zero4();
@@ -688,7 +691,12 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
     // dispatcher's dynamic assignment balances uneven windows better than a
     // static round-robin over persistent workgroups (cfg4 mixed MTU).
     uint64_t grid = want;
-    if (flat || p.grid_mult > 0) {
+    if (p.blocks_per_cu > 0) {
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        grid = std::min<uint64_t>(want, (uint64_t)cus * (uint64_t)p.blocks_per_cu);
+    } else if (flat || p.grid_mult > 0) {
         const int mult = p.grid_mult > 0 ? p.grid_mult : 2;
         grid = std::min<uint64_t>(want, (uint64_t)resident_blocks(fn, p.lds_bytes) * (uint64_t)mult);
     }

@@ -48,6 +48,16 @@ for s in "$@"; do
         pmc3w) pmc pmc3w 3 WRITE_SIZE ;;
         micro) step micro 600 python scripts/microbench.py ;;
         probe) step probe 300 ./scripts/stream_probe ;;
+        layout) step layout 300 ./scripts/layout_probe ;;
+        readp) step readp 300 ./scripts/read_probe ;;
+        sweep*)  # sweepN: blocks-per-CU sweep of config N, default lib + every variant lib
+            c=${s#sweep}
+            step sweep${c}_base 400 python scripts/sweep.py --config $c
+            for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
+                [ -e "$v" ] || continue
+                n=$(basename $v .so); n=${n#libfecgpu_}
+                FECGPU_LIB=$v step sweep${c}_$n 400 python scripts/sweep.py --config $c
+            done ;;
         ab*)  # abN: default build vs every lib/libfecgpu_*.so variant, config N, interleaved twice
             c=${s#ab}
             for rep in 1 2; do
