@@ -340,6 +340,10 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
     LaunchPlan p{};
     p.grid_mult = ctx->grid_mult;
     p.blocks_per_cu = ctx->blocks_per_cu;
+    // XOR is pure streaming: HBM delivers most with few bytes in flight
+    // (2 persistent workgroups per CU, ~8 MB chip-wide; scripts/read_probe.hip,
+    // scripts/sweep.py).  GF kernels need full occupancy to hide VALU work.
+    if (p.blocks_per_cu == 0 && p.grid_mult == 0 && scheme == FECGPU_SCHEME_XOR) p.blocks_per_cu = 2;
     // flat slot space when every window has the same geometry (GF decode
     // always plans per window in LDS, so it always runs in group mode)
     p.flat = !win_off && !sym_len && !(decode && scheme == FECGPU_SCHEME_GF256);

@@ -26,7 +26,8 @@
 #define FECGPU_XCD 1  // XCD-aware split of the work units (A/B knob)
 #endif
 #ifndef FECGPU_XOR_LOADS
-#define FECGPU_XOR_LOADS 8  // XOR encode: input rows loaded per batch (rounded up to r)
+#define FECGPU_XOR_LOADS 4  // XOR encode: input rows loaded per batch (rounded up to r);
+                            // 4 beat 2 and 8 at 2 workgroups/CU (scripts/sweep.py, r01)
 #endif
 #ifndef FECGPU_PIPE
 #define FECGPU_PIPE 0  // register double-buffered input loads in the GF bodies (A/B: no gain,
