@@ -55,6 +55,21 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(cfgid: int, kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary for this config (profiles/rNN_cfgN_traffic.json, written by
+    scripts/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(_ROOT, "profiles", f"r*_cfg{cfgid}_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        return int(d["kernels"][kernel]["traffic_bytes"]), os.path.relpath(files[-1], _ROOT)
+    except (KeyError, ValueError, OSError):
+        return None, None
+
+
 def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -168,6 +183,7 @@ def main():
         dom = "decode" if dec_ms > enc_ms else "encode"
         dom_ms = max(enc_ms, dec_ms)
         achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(args.config, dom) if nwin == cfg.nwin_per_gpu else (None, None)
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
             log("cpu baseline")
@@ -200,7 +216,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": alg[dom],
             },
             "roofline_other": {

@@ -29,6 +29,9 @@
 #define FECGPU_XOR_LOADS 4  // XOR encode: input rows loaded per batch (rounded up to r);
                             // 4 beat 2 and 8 at 2 workgroups/CU (scripts/sweep.py, r01)
 #endif
+#ifndef FECGPU_GF_U
+#define FECGPU_GF_U 4  // GF bodies: input rows loaded per batch
+#endif
 #ifndef FECGPU_PIPE
 #define FECGPU_PIPE 0  // register double-buffered input loads in the GF bodies (A/B: no gain,
                        // costs VGPRs / occupancy on decode; profiles/r01 notes)
@@ -263,7 +266,7 @@ __device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne,
 template <int R>
 __device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, int k,
                                                const uint4 *tab, const uint32_t *tc) {
-    constexpr int U = 4;
+    constexpr int U = FECGPU_GF_U;
     uint4 acc[R];
 #pragma unroll
     for (int m = 0; m < R; m++) acc[m] = zero4();
@@ -524,7 +527,7 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
     __shared__ uint8_t s_log[256];
     __shared__ GroupLds g;
     __shared__ uint8_t s_ne[kMaxWpb];
-    constexpr int U = 4;
+    constexpr int U = FECGPU_GF_U;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
     uint8_t *regions = reinterpret_cast<uint8_t *>(dyn);
     for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];

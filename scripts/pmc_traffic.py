@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the fecgpu kernels from two rocprofv3 --pmc passes.
+
+  python scripts/pmc_traffic.py --config 2 --fetch gpurun_out/pmc2r --write gpurun_out/pmc2w \
+         --out profiles/r01_cfg2_traffic.json
+
+MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reports exactly half the bytes of a
+wide coalesced streaming read on gfx950, so read bytes = 2 x FETCH_SIZE x 1024;
+WRITE_SIZE (KB) is exact for 16-B-per-lane streaming stores.  FETCH_SIZE and
+WRITE_SIZE are collected in separate passes (they do not fit one TCC pass).
+"""
+import argparse
+import collections
+import csv
+import json
+import statistics
+
+
+def per_kernel(path, counter):
+    out = collections.defaultdict(list)
+    for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
+        n = r["Kernel_Name"]
+        if r["Counter_Name"] == counter and "fecgpu" in n and ("encode" in n or "decode" in n):
+            out["encode" if "encode" in n else "decode"].append(float(r["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in out.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    f = per_kernel(a.fetch, "FETCH_SIZE")
+    w = per_kernel(a.write, "WRITE_SIZE")
+    res = {"config": a.config, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
+           "read = 2 x FETCH_SIZE x 1024 (gfx950 correction), write = WRITE_SIZE x 1024",
+           "kernels": {}}
+    for k in sorted(set(f) | set(w)):
+        rd = 2 * f.get(k, 0) * 1024
+        wr = w.get(k, 0) * 1024
+        res["kernels"][k] = {"read_bytes": int(rd), "write_bytes": int(wr), "traffic_bytes": int(rd + wr)}
+    json.dump(res, open(a.out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
