@@ -30,7 +30,10 @@
                             // 4 beat 2 and 8 at 2 workgroups/CU (scripts/sweep.py, r01)
 #endif
 #ifndef FECGPU_GF_U
-#define FECGPU_GF_U 4  // GF bodies: input rows loaded per batch
+// GF bodies: input rows loaded per batch.  Swept on the box (scripts/sweep.py):
+// r = 4 runs best with 2 rows in flight per lane (fewer bytes in flight keep
+// HBM efficient), r = 8 with 8 (its long VALU phase needs more loads queued).
+#define FECGPU_GF_U (R <= 4 ? 2 : 8)
 #endif
 #ifndef FECGPU_PIPE
 #define FECGPU_PIPE 0  // register double-buffered input loads in the GF bodies (A/B: no gain,
