@@ -93,6 +93,10 @@ ssize_t     fecgpu_code_check(const fecgpu_code *code);
  * over the ctx's devices. */
 ssize_t fecgpu_ctx_new(const int *devs, int ndev, fecgpu_ctx **out);
 void    fecgpu_ctx_free(fecgpu_ctx *ctx);
+/* Pinned (page-locked) host memory for FECGPU_F_HOST_PTRS buffers: with it the
+ * host-pointer batches overlap H2D copies, kernels and D2H copies. */
+ssize_t fecgpu_host_alloc(size_t bytes, void **out);
+void    fecgpu_host_free(void *p);
 /* Launch tuning knobs (0 = automatic): "grid_mult" (persistent grid =
  * resident workgroups x value), "wpb" (windows per workgroup, group mode). */
 ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value);

@@ -49,6 +49,16 @@ struct EncTables {
     uint32_t *c = nullptr;
 };
 
+constexpr int kPipeSlots = 3;
+
+// Streams, events and device staging slots of the host-pointer pipeline.
+struct HostPipe {
+    hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+    hipEvent_t h2d_done[kPipeSlots] = {}, comp_done[kPipeSlots] = {}, d2h_done[kPipeSlots] = {};
+    uint8_t *slot[kPipeSlots] = {};
+    size_t slot_bytes = 0;
+};
+
 }  // namespace
 
 struct fecgpu_ctx {
@@ -58,6 +68,7 @@ struct fecgpu_ctx {
     std::map<std::tuple<int, int, int>, EncTables> enc;
     // host-pointer staging per device
     std::map<int, std::pair<void *, size_t>> stage;
+    std::map<int, HostPipe> pipes;
     // tuning knobs (fecgpu_ctx_set_tuning): 0 = automatic
     int grid_mult = 0;
     int blocks_per_cu = 0;
@@ -158,8 +169,35 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second.first);
     }
+    for (auto &kv : ctx->pipes) {
+        HostPipe &hp = kv.second;
+        (void)hipSetDevice(kv.first);
+        if (hp.h2d) (void)hipStreamSynchronize(hp.d2h);
+        for (int i = 0; i < kPipeSlots; i++) {
+            if (hp.slot[i]) (void)hipFree(hp.slot[i]);
+            if (hp.h2d_done[i]) (void)hipEventDestroy(hp.h2d_done[i]);
+            if (hp.comp_done[i]) (void)hipEventDestroy(hp.comp_done[i]);
+            if (hp.d2h_done[i]) (void)hipEventDestroy(hp.d2h_done[i]);
+        }
+        if (hp.h2d) {
+            (void)hipStreamDestroy(hp.h2d);
+            (void)hipStreamDestroy(hp.comp);
+            (void)hipStreamDestroy(hp.d2h);
+        }
+    }
     (void)hipSetDevice(cur);
     delete ctx;
+}
+
+ssize_t fecgpu_host_alloc(size_t bytes, void **out) {
+    if (!out || bytes == 0) return FECGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocDefault), "hipHostMalloc");
+    return 0;
+}
+
+void fecgpu_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
 }
 
 }  // extern "C"
@@ -270,6 +308,12 @@ size_t host_window_bytes(const fecgpu_code *code, const uint64_t *win_off, const
     return mx;
 }
 
+ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
+                      hipStream_t s);
+ssize_t run_host_pipelined(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
+                           const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
+                           uint64_t nwin, const uint64_t *present, uint8_t *status);
+
 ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
                   const uint64_t *win_off, const uint32_t *sym_len, uint32_t sym_len_all,
                   uint32_t stride, uint64_t nwin, const uint64_t *present, uint8_t *status,
@@ -282,7 +326,11 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
     const int k = code->k, r = code->r, scheme = (int)code->scheme;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
-    // host pointers: stage everything on the ctx's first device, synchronously
+    // host pointers, uniform layout: chunked copy/compute pipeline
+    if ((flags & FECGPU_F_HOST_PTRS) && !win_off)
+        return run_host_pipelined(ctx, code, decode, win, sym_len, sym_len_all, stride, nwin,
+                                  present, status);
+    // host pointers, ragged layout: stage everything once, synchronously
     HostStage hs;
     int prev_dev = -1;
     if (flags & FECGPU_F_HOST_PTRS) {
@@ -324,6 +372,29 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
     a.nwin = nwin;
     a.S_all = sym_len_all;
     a.stride = stride;
+    rc = launch_device(ctx, code, decode, a, s);
+    if (rc) return rc;
+
+    if (hs.win) {
+        HIP_TRY(hipMemcpyAsync(win, hs.win, hs.win_bytes, hipMemcpyDeviceToHost, s), "D2H win");
+        if (decode)
+            HIP_TRY(hipMemcpyAsync(status, hs.status, nwin, hipMemcpyDeviceToHost, s), "D2H status");
+        HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+        HIP_TRY(hipSetDevice(prev_dev), "hipSetDevice");
+    } else if (flags & FECGPU_F_SYNC) {
+        HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+    }
+    return (ssize_t)nwin;
+}
+
+// Plan and launch one batch whose pointers are all device pointers.
+ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
+                      hipStream_t s) {
+    ssize_t rc = 0;
+    const int k = code->k, r = code->r, scheme = (int)code->scheme;
+    const uint32_t *sym_len = a.sym_len;
+    const uint64_t *win_off = a.win_off;
+    const uint32_t sym_len_all = a.S_all, stride = a.stride;
     a.k = k;
     a.r = r;
     for (int g = 0; g < kMaxR; g++) {
@@ -376,16 +447,94 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
 
     hipError_t e = decode ? launch_decode(scheme, a, p, s) : launch_encode(scheme, a, p, s);
     if (e != hipSuccess) return dev_err(e, decode ? "decode launch" : "encode launch");
+    return rc;
+}
 
-    if (hs.win) {
-        HIP_TRY(hipMemcpyAsync(win, hs.win, hs.win_bytes, hipMemcpyDeviceToHost, s), "D2H win");
-        if (decode)
-            HIP_TRY(hipMemcpyAsync(status, hs.status, nwin, hipMemcpyDeviceToHost, s), "D2H status");
-        HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
-        HIP_TRY(hipSetDevice(prev_dev), "hipSetDevice");
-    } else if (flags & FECGPU_F_SYNC) {
-        HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+// Host-pointer batch with the uniform layout, pipelined:
+// the windows are cut into ~64 MB chunks; chunk i's H2D copy (its own stream),
+// kernel (compute stream) and D2H copy (its own stream) overlap with chunks
+// i-1 and i+1 through three device staging slots and events.  Only the bytes
+// each side needs cross PCIe: encode sends the k source rows and returns the r
+// repair rows (2-D copies over the window pitch); decode sends whole windows
+// and returns the k source rows plus status.  Pinned host memory
+// (fecgpu_host_alloc) makes the copies asynchronous DMA.
+ssize_t run_host_pipelined(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
+                           const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
+                           uint64_t nwin, const uint64_t *present, uint8_t *status) {
+    const int k = code->k, r = code->r;
+    const size_t wbytes = (size_t)(k + r) * stride;
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev), "hipGetDevice");
+    const int dev = ctx->devs[0];
+    HIP_TRY(hipSetDevice(dev), "hipSetDevice");
+    HostPipe &hp = ctx->pipes[dev];
+    const uint64_t cw_max = std::max<uint64_t>(1, (64ull << 20) / wbytes);
+    const size_t need = cw_max * wbytes;
+    const size_t o_len = (need + 255) & ~size_t(255);
+    const size_t o_pres = o_len + ((cw_max * 4 + 255) & ~size_t(255));
+    const size_t o_stat = o_pres + ((cw_max * 8 + 255) & ~size_t(255));
+    const size_t slot_bytes = o_stat + ((cw_max + 255) & ~size_t(255));
+    if (!hp.h2d) {
+        HIP_TRY(hipStreamCreateWithFlags(&hp.h2d, hipStreamNonBlocking), "stream");
+        HIP_TRY(hipStreamCreateWithFlags(&hp.comp, hipStreamNonBlocking), "stream");
+        HIP_TRY(hipStreamCreateWithFlags(&hp.d2h, hipStreamNonBlocking), "stream");
+        for (int i = 0; i < kPipeSlots; i++) {
+            HIP_TRY(hipEventCreateWithFlags(&hp.h2d_done[i], hipEventDisableTiming), "event");
+            HIP_TRY(hipEventCreateWithFlags(&hp.comp_done[i], hipEventDisableTiming), "event");
+            HIP_TRY(hipEventCreateWithFlags(&hp.d2h_done[i], hipEventDisableTiming), "event");
+        }
     }
+    if (hp.slot_bytes < slot_bytes) {
+        HIP_TRY(hipDeviceSynchronize(), "sync");
+        for (int i = 0; i < kPipeSlots; i++) {
+            if (hp.slot[i]) HIP_TRY(hipFree(hp.slot[i]), "hipFree");
+            hp.slot[i] = nullptr;
+        }
+        for (int i = 0; i < kPipeSlots; i++) HIP_TRY(hipMalloc(&hp.slot[i], slot_bytes), "hipMalloc slot");
+        hp.slot_bytes = slot_bytes;
+    }
+    const uint64_t nchunk = (nwin + cw_max - 1) / cw_max;
+    for (uint64_t c = 0; c < nchunk; c++) {
+        const int sl = (int)(c % kPipeSlots);
+        const uint64_t w0 = c * cw_max, cw = std::min<uint64_t>(cw_max, nwin - w0);
+        uint8_t *d = hp.slot[sl];
+        uint8_t *h = win + w0 * wbytes;
+        if (c >= (uint64_t)kPipeSlots) HIP_TRY(hipStreamWaitEvent(hp.h2d, hp.d2h_done[sl], 0), "wait");
+        if (decode) {
+            HIP_TRY(hipMemcpyAsync(d, h, cw * wbytes, hipMemcpyHostToDevice, hp.h2d), "H2D");
+            HIP_TRY(hipMemcpyAsync(d + o_pres, present + w0, cw * 8, hipMemcpyHostToDevice, hp.h2d), "H2D");
+        } else {
+            HIP_TRY(hipMemcpy2DAsync(d, wbytes, h, wbytes, (size_t)k * stride, cw, hipMemcpyHostToDevice,
+                                     hp.h2d), "H2D 2D");
+        }
+        if (sym_len)
+            HIP_TRY(hipMemcpyAsync(d + o_len, sym_len + w0, cw * 4, hipMemcpyHostToDevice, hp.h2d), "H2D");
+        HIP_TRY(hipEventRecord(hp.h2d_done[sl], hp.h2d), "record");
+        HIP_TRY(hipStreamWaitEvent(hp.comp, hp.h2d_done[sl], 0), "wait");
+        BatchArgs a{};
+        a.win = d;
+        a.sym_len = sym_len ? reinterpret_cast<const uint32_t *>(d + o_len) : nullptr;
+        a.present = decode ? reinterpret_cast<const uint64_t *>(d + o_pres) : nullptr;
+        a.status = decode ? d + o_stat : nullptr;
+        a.nwin = cw;
+        a.S_all = sym_len_all;
+        a.stride = stride;
+        ssize_t rc = launch_device(ctx, code, decode, a, hp.comp);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(hp.comp_done[sl], hp.comp), "record");
+        HIP_TRY(hipStreamWaitEvent(hp.d2h, hp.comp_done[sl], 0), "wait");
+        if (decode) {
+            HIP_TRY(hipMemcpy2DAsync(h, wbytes, d, wbytes, (size_t)k * stride, cw, hipMemcpyDeviceToHost,
+                                     hp.d2h), "D2H 2D");
+            HIP_TRY(hipMemcpyAsync(status + w0, d + o_stat, cw, hipMemcpyDeviceToHost, hp.d2h), "D2H");
+        } else {
+            HIP_TRY(hipMemcpy2DAsync(h + (size_t)k * stride, wbytes, d + (size_t)k * stride, wbytes,
+                                     (size_t)r * stride, cw, hipMemcpyDeviceToHost, hp.d2h), "D2H 2D");
+        }
+        HIP_TRY(hipEventRecord(hp.d2h_done[sl], hp.d2h), "record");
+    }
+    HIP_TRY(hipStreamSynchronize(hp.d2h), "sync");
+    HIP_TRY(hipSetDevice(prev), "hipSetDevice");
     return (ssize_t)nwin;
 }
 

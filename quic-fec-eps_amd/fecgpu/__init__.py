@@ -39,6 +39,7 @@ ERASURE_NONE, ERASURE_EXACT, ERASURE_IID = 0, 1, 2
 EXPORTS = (
     "fecgpu_abi_version", "fecgpu_strerror", "fecgpu_last_error", "fecgpu_code_check",
     "fecgpu_ctx_new", "fecgpu_ctx_free", "fecgpu_ctx_set_tuning",
+    "fecgpu_host_alloc", "fecgpu_host_free",
     "fecgpu_encode_batch", "fecgpu_decode_batch",
     "fecgpu_synth_batch", "fecgpu_erasure_batch", "fecgpu_digest_batch",
     "fecgpu_encoder_new", "fecgpu_encoder_free", "fecgpu_encoder_add_source",
@@ -102,6 +103,8 @@ def _lib():
             "fecgpu_ctx_new": (sz, [vp, i32, ctypes.POINTER(vp)]),
             "fecgpu_ctx_free": (None, [vp]),
             "fecgpu_ctx_set_tuning": (sz, [vp, ctypes.c_char_p, ctypes.c_int64]),
+            "fecgpu_host_alloc": (sz, [ctypes.c_size_t, ctypes.POINTER(vp)]),
+            "fecgpu_host_free": (None, [vp]),
             "fecgpu_encode_batch": (sz, [vp, cp, vp, vp, vp, u32, u32, u64, u32, vp]),
             "fecgpu_decode_batch": (sz, [vp, cp, vp, vp, vp, u32, u32, u64, vp, vp, u32, vp]),
             "fecgpu_synth_batch": (sz, [vp, cp, i32, u64, u64, vp, vp, u32, u32, u64, vp]),
@@ -258,6 +261,30 @@ class Context:
         return _check(_lib().fecgpu_digest_batch(
             self._h, ctypes.byref(code.c), _ptr(win), _ptr(sym_len), sym_len_all, stride, w0,
             nwin, _ptr(digest), _stream(stream)), "fecgpu_digest_batch")
+
+
+class PinnedBuffer:
+    """Page-locked host memory (fecgpu_host_alloc) viewed as a numpy uint8 array."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+        self._p = ctypes.c_void_p()
+        _check(_lib().fecgpu_host_alloc(nbytes, ctypes.byref(self._p)), "fecgpu_host_alloc")
+        buf = (ctypes.c_uint8 * nbytes).from_address(self._p.value)
+        self.array = np.frombuffer(buf, dtype=np.uint8)
+        self.nbytes = nbytes
+
+    def close(self):
+        if self._p:
+            self.array = None
+            _lib().fecgpu_host_free(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Encoder:

@@ -27,6 +27,7 @@ class Config:
     nwin_per_gpu: int
     erasure: int
     erasure_desc: str
+    host: bool = False     # windows live in pinned host memory (config 5: PCIe inclusive)
 
     @property
     def code(self) -> Code:
@@ -45,6 +46,10 @@ CONFIGS = {
               ERASURE_EXACT, "exactly r=4 sources per window"),
     4: Config("cfg4-gf256-k32r8-mixedMTU-1M/8", "gf256", 32, 8, WORKLOAD_MIXED, 0, 131072,
               ERASURE_IID, "i.i.d. p=0.1 over all k+r symbols"),
+    5: Config("cfg5-stream-xor-k8r2-1200B-pinned-host", "xor", 8, 2, WORKLOAD_FIXED, 1200, 65536,
+              ERASURE_EXACT, "one source per XOR group (e=r=2)", host=True),
+    6: Config("cfg5gf-stream-gf256-k8r2-1200B-pinned-host", "gf256", 8, 2, WORKLOAD_FIXED, 1200,
+              65536, ERASURE_EXACT, "exactly r=2 sources per window", host=True),
 }
 
 
@@ -173,3 +178,74 @@ class Batch:
         return {"ok": mismatched == 0 and status_agree, "windows": self.nwin,
                 "mismatched_ok_windows": mismatched, "unrecoverable": unrec,
                 "status_matches_expected": status_agree}
+
+
+@dataclass
+class HostBatch:
+    """Config 5: the windows live in pinned host memory and every call crosses
+    PCIe through the library's chunked H2D / kernel / D2H pipeline
+    (FECGPU_F_HOST_PTRS).  Same packets and erasures as the device batches."""
+    cfg: Config
+    nwin: int
+    buf: object              # fecgpu.PinnedBuffer
+    present: "np.ndarray"
+    status: "np.ndarray"
+
+    @staticmethod
+    def allocate(cfg: Config, nwin: int, dev) -> "HostBatch":
+        import numpy as np
+        from . import PinnedBuffer
+        buf = PinnedBuffer(nwin * (cfg.k + cfg.r) * cfg.stride)
+        return HostBatch(cfg, nwin, buf, np.zeros(nwin, np.uint64), np.zeros(nwin, np.uint8))
+
+    @property
+    def view(self):
+        return self.buf.array.reshape(self.nwin, self.cfg.k + self.cfg.r, self.cfg.stride)
+
+    def synthesize(self, ctx: Context, w0: int, dev=None) -> None:
+        d = Batch.allocate(self.cfg, self.nwin, dev or torch.device("cuda"))
+        d.synthesize(ctx, w0)
+        d.make_erasures(ctx, w0)
+        self.buf.array[:] = d.win.cpu().numpy()
+        self.present[:] = d.present.cpu().numpy().view("uint64")
+        del d
+
+    def make_erasures(self, ctx: Context, w0: int) -> None:
+        pass  # drawn in synthesize()
+
+    def encode(self, ctx: Context) -> None:
+        from . import F_HOST_PTRS
+        ctx.encode_batch(self.cfg.code, self.buf.array, nwin=self.nwin, stride=self.cfg.stride,
+                         sym_len_all=self.cfg.L, flags=F_HOST_PTRS)
+
+    def decode(self, ctx: Context) -> None:
+        from . import F_HOST_PTRS
+        ctx.decode_batch(self.cfg.code, self.buf.array, self.present, self.status, nwin=self.nwin,
+                         stride=self.cfg.stride, sym_len_all=self.cfg.L, flags=F_HOST_PTRS)
+
+    def source_bytes(self) -> int:
+        return self.nwin * self.cfg.k * self.cfg.L
+
+    def algorithmic_bytes(self) -> dict:
+        """PCIe bytes per call: encode sends k rows, returns r rows; decode sends
+        whole windows + masks, returns k rows + status."""
+        c, n = self.cfg, self.nwin
+        return {"encode": n * (c.k + c.r) * c.stride,
+                "decode": n * ((c.k + c.r) * c.stride + 8 + c.k * c.stride + 1)}
+
+    def verify(self, ctx: Context, w0: int) -> dict:
+        import numpy as np
+        c = self.cfg
+        self.encode(ctx)
+        v = self.view
+        saved = v[:, :c.k].copy()
+        for i in range(c.k + c.r):
+            erased = ((self.present >> np.uint64(i)) & np.uint64(1)) == 0
+            v[erased, i] = 0xAB
+        self.decode(ctx)
+        ok = self.status == STATUS_OK
+        eq = (v[:, :c.k, :c.L] == saved[:, :, :c.L]).reshape(self.nwin, -1).all(1)
+        mism = int((ok & ~eq).sum())
+        v[:, :c.k] = saved
+        return {"ok": mism == 0 and bool(ok.all()), "windows": self.nwin,
+                "mismatched_ok_windows": mism, "unrecoverable": int((~ok).sum())}

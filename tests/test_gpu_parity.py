@@ -216,6 +216,27 @@ def test_host_pointer_mode(ctx):
     _cmp_emitted(h, od, S, "host decode")
 
 
+@pytest.mark.parametrize("cfgid", [5, 6])
+def test_pinned_host_pipeline_matches_device_path(ctx, cfgid):
+    """FECGPU_F_HOST_PTRS over pinned memory, > 3 pipeline chunks (slot reuse): repairs
+    and recovered sources equal the device-resident path on the same windows."""
+    cfg = WL.CONFIGS[cfgid]
+    nwin = 40000  # 480 MB of windows -> 8 chunks of 64 MB
+    hb = WL.HostBatch.allocate(cfg, nwin, torch.device("cuda"))
+    hb.synthesize(ctx, 77)
+    db = WL.Batch.allocate(cfg, nwin, torch.device("cuda"))
+    db.synthesize(ctx, 77)
+    db.make_erasures(ctx, 77)
+    assert np.array_equal(hb.present, db.present.cpu().numpy().view(np.uint64))
+    hb.encode(ctx)
+    db.encode(ctx)
+    torch.cuda.synchronize()
+    assert np.array_equal(hb.buf.array, db.win.cpu().numpy())
+    res = hb.verify(ctx, 77)
+    assert res["ok"] and res["unrecoverable"] == 0, res
+    hb.buf.close()
+
+
 def test_zero_windows_and_errors(ctx):
     code = fecgpu.Code("gf256", 4, 2)
     d = torch.zeros(4096, dtype=torch.uint8, device="cuda")
