@@ -167,6 +167,32 @@ ssize_t fecgpu_decoder_recovered(fecgpu_decoder *dec, uint64_t win, uint16_t idx
                                  size_t cap);
 ssize_t fecgpu_decoder_release(fecgpu_decoder *dec, uint64_t win);
 
+/* ---- FEC frames on the wire --------------------
+ * QUIC varint-coded frames (RFC 9000 §16 integers):
+ *   SOURCE_ID: type | window | index                    (next to a source payload)
+ *   REPAIR   : type | window | k | r | index | length | symbol bytes
+ * Frame types sit in QUIC's extension space.  Host-only, no device calls. */
+#define FECGPU_FRAME_SOURCE_ID 0xfec0u
+#define FECGPU_FRAME_REPAIR 0xfec1u
+
+typedef struct fecgpu_frame {
+    uint64_t type;           /* FECGPU_FRAME_* */
+    uint64_t win;            /* window id */
+    uint16_t k, r;           /* REPAIR: code shape */
+    uint16_t idx;            /* source index (SOURCE_ID) or repair index (REPAIR) */
+    const uint8_t *payload;  /* REPAIR: points into the parsed buffer */
+    size_t payload_len;
+} fecgpu_frame;
+
+ssize_t fecgpu_frame_source_id_len(uint64_t win, uint16_t idx);
+ssize_t fecgpu_frame_write_source_id(uint8_t *buf, size_t cap, uint64_t win, uint16_t idx);
+ssize_t fecgpu_frame_repair_len(uint64_t win, uint16_t k, uint16_t r, uint16_t idx, size_t sym_len);
+ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16_t k, uint16_t r,
+                                  uint16_t idx, const uint8_t *sym, size_t sym_len);
+/* Parse one frame at buf; returns bytes consumed or a negative error
+ * (BUFFER_TOO_SHORT on truncation, INVALID_ARG on an unknown type or bad field). */
+ssize_t fecgpu_frame_parse(const uint8_t *buf, size_t len, fecgpu_frame *out);
+
 /* ---- synthetic workload / verification (bench + tests) ---- */
 
 /* Fill sources of windows w0..w0+nwin-1 on the device (workload 0: FIXED,

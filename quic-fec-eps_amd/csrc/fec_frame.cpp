@@ -1,0 +1,124 @@
+// fec_frame.cpp — FEC frame wire format.
+//
+// The fec branch's frame types and header fields are not mounted
+// (/root/reference/README.md:7), so this is the build's
+// own encoding, written in QUIC's idiom: every integer is a QUIC
+// variable-length integer (RFC 9000 §16) and a frame is
+//   SOURCE_ID: type | window | index
+//   REPAIR   : type | window | k | r | index | length | repair symbol bytes
+// with frame types in the reserved-for-extensions space.  A Connection puts a
+// SOURCE_ID frame next to each protected payload and carries repair symbols
+// in REPAIR frames; the receiver parses both and feeds fecgpu_decoder_*.
+// Pure host code: no device calls.
+#include <cstring>
+
+#include "../../include/fecgpu.h"
+
+namespace {
+
+size_t varint_len(uint64_t v) {
+    if (v < (1ull << 6)) return 1;
+    if (v < (1ull << 14)) return 2;
+    if (v < (1ull << 30)) return 4;
+    return 8;
+}
+
+uint8_t *varint_put(uint8_t *p, uint64_t v) {
+    const size_t n = varint_len(v);
+    const uint64_t tag = n == 1 ? 0 : n == 2 ? 1 : n == 4 ? 2 : 3;
+    for (size_t i = 0; i < n; i++) p[i] = (uint8_t)(v >> (8 * (n - 1 - i)));
+    p[0] = (uint8_t)((p[0] & 0x3F) | (tag << 6));
+    return p + n;
+}
+
+// returns bytes consumed, 0 if truncated
+size_t varint_get(const uint8_t *p, size_t len, uint64_t *v) {
+    if (len == 0) return 0;
+    const size_t n = (size_t)1 << (p[0] >> 6);
+    if (len < n) return 0;
+    uint64_t x = p[0] & 0x3F;
+    for (size_t i = 1; i < n; i++) x = (x << 8) | p[i];
+    *v = x;
+    return n;
+}
+
+}  // namespace
+
+extern "C" {
+
+ssize_t fecgpu_frame_source_id_len(uint64_t win, uint16_t idx) {
+    return (ssize_t)(varint_len(FECGPU_FRAME_SOURCE_ID) + varint_len(win) + varint_len(idx));
+}
+
+ssize_t fecgpu_frame_write_source_id(uint8_t *buf, size_t cap, uint64_t win, uint16_t idx) {
+    if (!buf || win >= (1ull << 62)) return FECGPU_ERR_INVALID_ARG;
+    const size_t n = (size_t)fecgpu_frame_source_id_len(win, idx);
+    if (cap < n) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    uint8_t *p = varint_put(buf, FECGPU_FRAME_SOURCE_ID);
+    p = varint_put(p, win);
+    p = varint_put(p, idx);
+    return (ssize_t)(p - buf);
+}
+
+ssize_t fecgpu_frame_repair_len(uint64_t win, uint16_t k, uint16_t r, uint16_t idx, size_t sym_len) {
+    return (ssize_t)(varint_len(FECGPU_FRAME_REPAIR) + varint_len(win) + varint_len(k) + varint_len(r) +
+                     varint_len(idx) + varint_len(sym_len) + sym_len);
+}
+
+ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16_t k, uint16_t r,
+                                  uint16_t idx, const uint8_t *sym, size_t sym_len) {
+    if (!buf || (!sym && sym_len) || win >= (1ull << 62) || idx >= r || k == 0 || r == 0)
+        return FECGPU_ERR_INVALID_ARG;
+    const size_t n = (size_t)fecgpu_frame_repair_len(win, k, r, idx, sym_len);
+    if (cap < n) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    uint8_t *p = varint_put(buf, FECGPU_FRAME_REPAIR);
+    p = varint_put(p, win);
+    p = varint_put(p, k);
+    p = varint_put(p, r);
+    p = varint_put(p, idx);
+    p = varint_put(p, sym_len);
+    if (sym_len) std::memcpy(p, sym, sym_len);
+    return (ssize_t)(p + sym_len - buf);
+}
+
+ssize_t fecgpu_frame_parse(const uint8_t *buf, size_t len, fecgpu_frame *out) {
+    if (!buf || !out) return FECGPU_ERR_INVALID_ARG;
+    std::memset(out, 0, sizeof(*out));
+    size_t pos = 0, n;
+    uint64_t v;
+#define GET(dst)                                              \
+    do {                                                      \
+        n = varint_get(buf + pos, len - pos, &v);             \
+        if (!n) return FECGPU_ERR_BUFFER_TOO_SHORT;           \
+        pos += n;                                             \
+        dst = v;                                              \
+    } while (0)
+    uint64_t type;
+    GET(type);
+    if (type != FECGPU_FRAME_SOURCE_ID && type != FECGPU_FRAME_REPAIR) return FECGPU_ERR_INVALID_ARG;
+    out->type = type;
+    GET(out->win);
+    if (type == FECGPU_FRAME_SOURCE_ID) {
+        uint64_t idx;
+        GET(idx);
+        if (idx > 0xFFFF) return FECGPU_ERR_INVALID_ARG;
+        out->idx = (uint16_t)idx;
+        return (ssize_t)pos;
+    }
+    uint64_t k, r, idx, sl;
+    GET(k);
+    GET(r);
+    GET(idx);
+    GET(sl);
+#undef GET
+    if (k == 0 || r == 0 || k > 0xFFFF || r > 0xFFFF || idx >= r) return FECGPU_ERR_INVALID_ARG;
+    if (sl > len - pos) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    out->k = (uint16_t)k;
+    out->r = (uint16_t)r;
+    out->idx = (uint16_t)idx;
+    out->payload = buf + pos;
+    out->payload_len = sl;
+    return (ssize_t)(pos + sl);
+}
+
+}  // extern "C"

@@ -48,7 +48,10 @@ EXPORTS = (
     "fecgpu_decoder_new", "fecgpu_decoder_free", "fecgpu_decoder_add_source",
     "fecgpu_decoder_add_repair", "fecgpu_decoder_flush", "fecgpu_decoder_recovered",
     "fecgpu_decoder_release",
+    "fecgpu_frame_source_id_len", "fecgpu_frame_write_source_id", "fecgpu_frame_repair_len",
+    "fecgpu_frame_write_repair", "fecgpu_frame_parse",
 )
+FRAME_SOURCE_ID, FRAME_REPAIR = 0xFEC0, 0xFEC1
 
 
 class FecError(RuntimeError):
@@ -69,6 +72,18 @@ class fecgpu_code(ctypes.Structure):
         ("k", ctypes.c_uint16),
         ("r", ctypes.c_uint16),
         ("poly", ctypes.c_uint32),
+    ]
+
+
+class fecgpu_frame(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_uint64),
+        ("win", ctypes.c_uint64),
+        ("k", ctypes.c_uint16),
+        ("r", ctypes.c_uint16),
+        ("idx", ctypes.c_uint16),
+        ("payload", ctypes.c_void_p),
+        ("payload_len", ctypes.c_size_t),
     ]
 
 
@@ -126,6 +141,14 @@ def _lib():
             "fecgpu_decoder_flush": (sz, [vp]),
             "fecgpu_decoder_recovered": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
             "fecgpu_decoder_release": (sz, [vp, u64]),
+            "fecgpu_frame_source_id_len": (sz, [u64, ctypes.c_uint16]),
+            "fecgpu_frame_write_source_id": (sz, [vp, ctypes.c_size_t, u64, ctypes.c_uint16]),
+            "fecgpu_frame_repair_len": (sz, [u64, ctypes.c_uint16, ctypes.c_uint16,
+                                             ctypes.c_uint16, ctypes.c_size_t]),
+            "fecgpu_frame_write_repair": (sz, [vp, ctypes.c_size_t, u64, ctypes.c_uint16,
+                                               ctypes.c_uint16, ctypes.c_uint16, vp,
+                                               ctypes.c_size_t]),
+            "fecgpu_frame_parse": (sz, [vp, ctypes.c_size_t, ctypes.POINTER(fecgpu_frame)]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -370,6 +393,35 @@ class Decoder:
             self.close()
         except Exception:
             pass
+
+
+def frame_source_id(win: int, idx: int) -> bytes:
+    """SOURCE_ID frame bytes (fecgpu_frame_write_source_id)."""
+    n = _check(_lib().fecgpu_frame_source_id_len(win, idx), "fecgpu_frame_source_id_len")
+    buf = ctypes.create_string_buffer(n)
+    m = _check(_lib().fecgpu_frame_write_source_id(buf, n, win, idx), "fecgpu_frame_write_source_id")
+    return buf.raw[:m]
+
+
+def frame_repair(win: int, k: int, r: int, idx: int, sym: bytes) -> bytes:
+    """REPAIR frame bytes (fecgpu_frame_write_repair)."""
+    n = _check(_lib().fecgpu_frame_repair_len(win, k, r, idx, len(sym)), "fecgpu_frame_repair_len")
+    buf = ctypes.create_string_buffer(n)
+    m = _check(_lib().fecgpu_frame_write_repair(buf, n, win, k, r, idx, sym, len(sym)),
+               "fecgpu_frame_write_repair")
+    return buf.raw[:m]
+
+
+def frame_parse(data: bytes):
+    """-> (consumed, dict) or raises FecError (fecgpu_frame_parse)."""
+    f = fecgpu_frame()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    n = _check(_lib().fecgpu_frame_parse(buf, len(data), ctypes.byref(f)), "fecgpu_frame_parse")
+    out = {"type": f.type, "win": f.win, "idx": f.idx}
+    if f.type == FRAME_REPAIR:
+        off = f.payload - ctypes.addressof(buf)
+        out.update(k=f.k, r=f.r, payload=bytes(data[off:off + f.payload_len]))
+    return n, out
 
 
 def round_up(x: int, m: int) -> int:

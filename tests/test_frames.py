@@ -1,0 +1,64 @@
+"""FEC frame wire format: QUIC varint SOURCE_ID and REPAIR
+frames through the C ABI (host-only code in libfecgpu.so, runs on CPU).
+The fec branch's own frame layout is not mounted: wire parity is unpinned."""
+import pytest
+
+import fecgpu
+
+
+@pytest.mark.parametrize("win", [0, 63, 64, 16383, 16384, (1 << 30) - 1, 1 << 30, (1 << 62) - 1])
+@pytest.mark.parametrize("idx", [0, 63, 64, 1000])
+def test_source_id_round_trip(win, idx):
+    b = fecgpu.frame_source_id(win, idx)
+    n, f = fecgpu.frame_parse(b + b"trailing")
+    assert n == len(b)
+    assert f == {"type": fecgpu.FRAME_SOURCE_ID, "win": win, "idx": idx}
+
+
+def test_varint_sizes_follow_rfc9000():
+    # type 0xfec0 needs a 4-byte varint; window/index 1,2,4,8 bytes at the boundaries
+    assert len(fecgpu.frame_source_id(0, 0)) == 4 + 1 + 1
+    assert len(fecgpu.frame_source_id(64, 0)) == 4 + 2 + 1
+    assert len(fecgpu.frame_source_id(1 << 14, 0)) == 4 + 4 + 1
+    assert len(fecgpu.frame_source_id(1 << 30, 0)) == 4 + 8 + 1
+    # RFC 9000 A.1 example: 0x25 encodes 37 in one byte; 151288809941952652 in 8 bytes
+    b = fecgpu.frame_source_id(151288809941952652, 37)
+    assert b[4:12] == bytes.fromhex("c2197c5eff14e88c") and b[12] == 0x25
+
+
+@pytest.mark.parametrize("sym_len", [0, 1, 1200, 9002, 70000])
+def test_repair_round_trip(sym_len):
+    sym = bytes((i * 7 + 3) & 0xFF for i in range(sym_len))
+    b = fecgpu.frame_repair(123456, 32, 8, 7, sym)
+    n, f = fecgpu.frame_parse(b)
+    assert n == len(b)
+    assert f["type"] == fecgpu.FRAME_REPAIR and f["win"] == 123456
+    assert (f["k"], f["r"], f["idx"]) == (32, 8, 7)
+    assert f["payload"] == sym
+
+
+def test_parse_errors():
+    b = fecgpu.frame_repair(5, 4, 2, 1, b"x" * 100)
+    for cut in (0, 1, 3, 5, 9, len(b) - 1):
+        with pytest.raises(fecgpu.FecError) as e:
+            fecgpu.frame_parse(b[:cut])
+        assert e.value.code == fecgpu.ERR_BUFFER_TOO_SHORT
+    with pytest.raises(fecgpu.FecError) as e:
+        fecgpu.frame_parse(bytes([0x01, 0x00, 0x00]))  # unknown frame type
+    assert e.value.code == fecgpu.ERR_INVALID_ARG
+    with pytest.raises(fecgpu.FecError) as e:
+        fecgpu.frame_repair(5, 4, 2, 2, b"x")  # repair index >= r
+    assert e.value.code == fecgpu.ERR_INVALID_ARG
+
+
+def test_stream_of_frames():
+    frames = [fecgpu.frame_source_id(w, i) for w in range(3) for i in range(4)]
+    frames += [fecgpu.frame_repair(w, 4, 1, 0, bytes([w]) * 50) for w in range(3)]
+    blob = b"".join(frames)
+    pos, seen = 0, []
+    while pos < len(blob):
+        n, f = fecgpu.frame_parse(blob[pos:])
+        seen.append(f)
+        pos += n
+    assert len(seen) == len(frames)
+    assert [f["payload"] for f in seen if f["type"] == fecgpu.FRAME_REPAIR] == [bytes([w]) * 50 for w in range(3)]

@@ -30,7 +30,20 @@ def _stream(nbytes, seed):
         for i in range((nbytes + (1 << 16) - 1) >> 16))
 
 
-def _run(ctx, code, data, mtu, loss, seed, batch=256, vary=False):
+def _wire_source(w, i, p, framed):
+    """Sender side: the packet as it goes on the wire (SOURCE_ID frame + payload)."""
+    return fecgpu.frame_source_id(w, i) + p if framed else (w, i, p)
+
+
+def _recv_source(wire, framed):
+    if not framed:
+        return wire
+    n, f = fecgpu.frame_parse(wire)
+    assert f["type"] == fecgpu.FRAME_SOURCE_ID
+    return f["win"], f["idx"], wire[n:]
+
+
+def _run(ctx, code, data, mtu, loss, seed, batch=256, vary=False, framed=False):
     rng = np.random.default_rng(seed)
     pkts, pos = [], 0
     while pos < len(data):
@@ -44,8 +57,10 @@ def _run(ctx, code, data, mtu, loss, seed, batch=256, vary=False):
     for p, lost in zip(pkts, lost_src):
         w, i = enc.add_source(p)
         ids.append((w, i))
+        wire = _wire_source(w, i, p, framed)
         if not lost:
-            assert dec.add_source(w, i, p) == 0
+            rw, ri, rp = _recv_source(wire, framed)
+            assert dec.add_source(rw, ri, rp) == 0
     last = enc.close_window() if len(pkts) % code.k else ids[-1][0]
     enc.flush()
     nwin = ids[-1][0] + 1
@@ -59,6 +74,10 @@ def _run(ctx, code, data, mtu, loss, seed, batch=256, vary=False):
         for i in range(code.r):
             rep = enc.repair(w, i)
             assert rep is not None
+            if framed:  # REPAIR frame on the wire, parsed by the receiver
+                _, f = fecgpu.frame_parse(fecgpu.frame_repair(w, code.k, code.r, i, rep))
+                assert (f["win"], f["idx"], f["k"], f["r"]) == (w, i, code.k, code.r)
+                rep = f["payload"]
             if not rep_lost[w, i]:
                 assert dec.add_repair(w, i, rep) == 0
     dec.flush()
@@ -94,7 +113,7 @@ def _run(ctx, code, data, mtu, loss, seed, batch=256, vary=False):
 def test_loopsim_xor_k4r1_10MB(ctx):
     data = _stream(10 * 1024 * 1024, 11)
     code = fecgpu.Code("xor", 4, 1, "lenprefix")
-    n, missing = _run(ctx, code, data, 1200, 0.02, 3)
+    n, missing = _run(ctx, code, data, 1200, 0.02, 3, framed=True)
     assert n == (len(data) + 1199) // 1200
     assert missing < n * 0.01
 
