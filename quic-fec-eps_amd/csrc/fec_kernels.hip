@@ -46,21 +46,28 @@ __constant__ GfTables c_gf = make_gf_tables();
 
 // ------------------------------------------------------------ helpers ---
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Symbol data is always in global memory.  Pointers that pass through LDS
+// (group-mode window bases) are generic to the compiler and would become
+// flat_load/flat_store, which count against lgkmcnt as well as vmcnt and force
+// conservative waits on LDS traffic; the explicit address space keeps them
+// global_load_dwordx4 / global_store_dwordx4.
+typedef __attribute__((address_space(1))) const u32x4 *gptr_c;
+typedef __attribute__((address_space(1))) u32x4 *gptr;
 
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
 #if FECGPU_NT
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    const u32x4 v = __builtin_nontemporal_load((gptr_c)(p));
 #else
-    const u32x4 v = *reinterpret_cast<const u32x4 *>(p);
+    const u32x4 v = *(gptr_c)(p);
 #endif
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
     const u32x4 x = {v.x, v.y, v.z, v.w};
 #if FECGPU_NT
-    __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
+    __builtin_nontemporal_store(x, (gptr)(p));
 #else
-    *reinterpret_cast<u32x4 *>(p) = x;
+    *(gptr)(p) = x;
 #endif
 }
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
@@ -378,10 +385,34 @@ __global__ __launch_bounds__(kBlock) void gf_encode_kernel(BatchArgs a) {
 template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
     if constexpr (FLAT) {
-        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t w, uint32_t col) {
-            const uint32_t bad = xor_decode_slot<R>(a, p, stride, a.present[w]);
-            if (col == 0) a.status[w] = (uint8_t)bad;
-        });
+        // for_flat_slots with the next slot's present mask loaded one iteration
+        // ahead: the plan (and so the data loads) never waits on that load.
+        const uint32_t ncol = a.ncol;
+        const uint64_t total = a.nwin * ncol;
+        XcdRange xr = xcd_range((total + kBlock - 1) / kBlock, a.nx);
+        if (xr.cur >= xr.hi) return;
+        uint64_t s = xr.cur * kBlock + threadIdx.x;
+        uint64_t w = s / ncol;
+        uint32_t col = (uint32_t)(s - w * ncol);
+        const uint64_t wbytes = (uint64_t)(a.k + a.r) * a.stride;
+        uint64_t pres = a.present[min(w, a.nwin - 1)];
+        for (; xr.cur < xr.hi; xr.cur += xr.step) {
+            const uint64_t s_now = s, w_now = w, p_now = pres;
+            const uint32_t col_now = col;
+            s += xr.step * kBlock;
+            col += a.step_col;
+            w += a.step_win;
+            if (col >= ncol) {
+                col -= ncol;
+                w++;
+            }
+            pres = a.present[min(w, a.nwin - 1)];  // prefetch for the next iteration
+            if (s_now < total) {
+                const uint32_t bad =
+                    xor_decode_slot<R>(a, a.win + w_now * wbytes + col_now * 16u, a.stride, p_now);
+                if (col_now == 0) a.status[w_now] = (uint8_t)bad;
+            }
+        }
     } else {
         __shared__ GroupLds g;
         __shared__ uint64_t s_pres[kMaxWpb];
