@@ -35,6 +35,9 @@
 // HBM efficient), r = 8 with 8 (its long VALU phase needs more loads queued).
 #define FECGPU_GF_U (R <= 4 ? 2 : 8)
 #endif
+#ifndef FECGPU_ENC_SGPR
+#define FECGPU_ENC_SGPR 0  // GF encode tables via scalar loads instead of LDS (A/B knob)
+#endif
 #ifndef FECGPU_PIPE
 #define FECGPU_PIPE 0  // register double-buffered input loads in the GF bodies (A/B: no gain,
                        // costs VGPRs / occupancy on decode; profiles/r01 notes)
@@ -164,7 +167,12 @@ __device__ __forceinline__ void for_flat_slots(const BatchArgs &a, Body &&body) 
     uint32_t col = (uint32_t)(s - w * ncol);
     const uint64_t wbytes = (uint64_t)(a.k + a.r) * a.stride;
     for (; xr.cur < xr.hi; xr.cur += xr.step) {
-        if (s < total) body(a.win + w * wbytes + col * 16u, a.stride, w, col);
+        // uniform control flow: lanes past the end work on the last slot and
+        // skip their stores (keeps wave-uniform table reads scalar)
+        const bool valid = s < total;
+        const uint64_t wv = valid ? w : a.nwin - 1;
+        const uint32_t cv = valid ? col : ncol - 1;
+        body(a.win + wv * wbytes + cv * 16u, a.stride, wv, cv, valid);
         s += xr.step * kBlock;
         col += a.step_col;
         w += a.step_win;
@@ -184,15 +192,20 @@ struct GroupLds {
     uint32_t ncol[kMaxWpb];
 };
 
-// Streams the flattened columns of the current group: body(base_of_column, stride, wl).
+// Streams the flattened columns of the current group:
+// body(base_of_column, stride, wl, valid).  Passes are block-uniform; lanes
+// past the end re-use the last slot with valid = false (stores skipped).
 template <class Body>
 __device__ __forceinline__ void for_group_slots(const GroupLds &g, int nb, Body &&body) {
     const uint32_t total = g.pfx[nb];
     int wl = 0;
-    for (uint32_t s = threadIdx.x; s < total; s += kBlock) {
-        while (s >= g.pfx[wl + 1]) wl++;
-        const uint32_t col = s - g.pfx[wl];
-        body(reinterpret_cast<uint8_t *>(g.base[wl]) + col * 16u, g.stride[wl], wl);
+    for (uint32_t s0 = 0; s0 < total; s0 += kBlock) {
+        const uint32_t s = s0 + threadIdx.x;
+        const bool valid = s < total;
+        const uint32_t sv = valid ? s : total - 1;
+        while (sv >= g.pfx[wl + 1]) wl++;
+        const uint32_t col = sv - g.pfx[wl];
+        body(reinterpret_cast<uint8_t *>(g.base[wl]) + col * 16u, g.stride[wl], wl, valid);
     }
 }
 
@@ -211,7 +224,7 @@ __device__ __forceinline__ void group_geometry(const BatchArgs &a, GroupLds &g, 
 // XOR encode (a4): R_g = xor of S_j, j = g (mod r).  All loads of a slot are
 // issued before the xors (8 x 16 B in flight per lane at k = 8).
 template <int R>
-__device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, int k) {
+__device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, int k, bool valid) {
     constexpr int STEP = R * ((FECGPU_XOR_LOADS + R - 1) / R);
     uint4 acc[R];
 #pragma unroll
@@ -225,8 +238,10 @@ __device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, 
         for (int t = 0; t < STEP; t++)
             if (j0 + t < k) acc[t % R] = xor4(acc[t % R], v[t]);
     }
+    if (valid) {
 #pragma unroll
-    for (int g = 0; g < R; g++) st16(base + (size_t)(k + g) * stride, acc[g]);
+        for (int g = 0; g < R; g++) st16(base + (size_t)(k + g) * stride, acc[g]);
+    }
 }
 
 // Software-pipelined GF multiply-accumulate over k inputs of one slot:
@@ -234,9 +249,9 @@ __device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, 
 // a time into one of two register buffers while the other is multiplied, so
 // every wave keeps U 16-B loads in flight through the VALU phase.
 // `addr(q)` gives input q's column address, tables are [q][m] in LDS.
-template <int R, int U, class Addr>
+template <int R, int U, class Addr, class TabP, class TcP>
 __device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne, Addr &&addr,
-                                                 const uint4 *tab, const uint32_t *tc) {
+                                                 TabP tab, TcP tc) {
     uint4 va[U], vb[U];
     auto load = [&](uint4(&v)[U], int q0) {
 #pragma unroll
@@ -247,7 +262,8 @@ __device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne,
         for (int t = 0; t < U; t++) {
             if (q0 + t < k) {
                 const Split sp = split(v[t]);
-                const int row = (q0 + t) * R;
+                // wave-uniform row index (lets uniform table reads become scalar loads)
+                const int row = __builtin_amdgcn_readfirstlane((q0 + t) * R);
 #pragma unroll
                 for (int m = 0; m < R; m++)
                     if (m < ne) gmac(acc[m], sp, tab[row + m], tc[row + m]);
@@ -273,16 +289,18 @@ __device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne,
 }
 
 // GF encode (a5): R_i = sum_j C[i][j] * S_j, tables [j][i] in LDS (broadcast reads).
-template <int R>
-__device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, int k,
-                                               const uint4 *tab, const uint32_t *tc) {
+template <int R, class TabP, class TcP>
+__device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, int k, TabP tab,
+                                               TcP tc, bool valid) {
     constexpr int U = FECGPU_GF_U;
     uint4 acc[R];
 #pragma unroll
     for (int m = 0; m < R; m++) acc[m] = zero4();
     gf_mac_pipelined<R, U>(acc, k, R, [&](int q) { return base + (uint32_t)q * stride; }, tab, tc);
+    if (valid) {
 #pragma unroll
-    for (int m = 0; m < R; m++) st16(base + (size_t)(k + m) * stride, acc[m]);
+        for (int m = 0; m < R; m++) st16(base + (size_t)(k + m) * stride, acc[m]);
+    }
 }
 
 // XOR decode (a6/a8), planned inline from the window's present mask: every
@@ -291,7 +309,7 @@ __device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, i
 // Returns the window status (1 if some source stays missing).
 template <int R>
 __device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t *base,
-                                                    uint32_t stride, uint64_t pres) {
+                                                    uint32_t stride, uint64_t pres, bool valid) {
     const int k = a.k;
     const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
     const uint64_t miss = ~pres & kmask;
@@ -318,7 +336,7 @@ __device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t 
 #pragma unroll
             for (int t = 0; t < 8; t++) acc = xor4(acc, v[t]);
         }
-        st16(base + (size_t)m * stride, acc);
+        if (valid) st16(base + (size_t)m * stride, acc);
     }
     return bad;
 }
@@ -327,8 +345,8 @@ __device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t 
 template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
     if constexpr (FLAT) {
-        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t) {
-            xor_encode_slot<R>(p, stride, a.k);
+        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t, bool valid) {
+            xor_encode_slot<R>(p, stride, a.k, valid);
         });
     } else {
         __shared__ GroupLds g;
@@ -340,8 +358,8 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
             __syncthreads();
             if (threadIdx.x < 64) block_prefix(g.pfx, (int)threadIdx.x < nb ? g.ncol[threadIdx.x] : 0u, threadIdx.x);
             __syncthreads();
-            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int) {
-                xor_encode_slot<R>(p, stride, a.k);
+            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int, bool valid) {
+                xor_encode_slot<R>(p, stride, a.k, valid);
             });
             __syncthreads();
         }
@@ -350,8 +368,22 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
 
 template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void gf_encode_kernel(BatchArgs a) {
-    extern __shared__ uint4 dyn[];
     const int k = a.k;
+#if FECGPU_ENC_SGPR
+    // kernel-uniform tables read through the constant address space with a
+    // wave-uniform index, i.e. scalar loads into SGPRs: no LDS traffic or
+    // latency in the multiply loop
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(4))) const uint4 *cptr4;
+    typedef __attribute__((address_space(4))) const uint32_t *cptr1;
+#else
+    typedef const uint4 *cptr4;
+    typedef const uint32_t *cptr1;
+#endif
+    const cptr4 tab = (cptr4)a.enc_ab;
+    const cptr1 tc = (cptr1)a.enc_c;
+#else
+    extern __shared__ uint4 dyn[];
     uint4 *tab = dyn;
     uint32_t *tc = reinterpret_cast<uint32_t *>(dyn + k * R);
     for (int i = threadIdx.x; i < k * R; i += kBlock) {
@@ -359,9 +391,10 @@ __global__ __launch_bounds__(kBlock) void gf_encode_kernel(BatchArgs a) {
         tc[i] = a.enc_c[i];
     }
     __syncthreads();
+#endif
     if constexpr (FLAT) {
-        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t) {
-            gf_encode_slot<R>(p, stride, k, tab, tc);
+        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t, bool valid) {
+            gf_encode_slot<R>(p, stride, k, tab, tc, valid);
         });
     } else {
         __shared__ GroupLds g;
@@ -373,8 +406,8 @@ __global__ __launch_bounds__(kBlock) void gf_encode_kernel(BatchArgs a) {
             __syncthreads();
             if (threadIdx.x < 64) block_prefix(g.pfx, (int)threadIdx.x < nb ? g.ncol[threadIdx.x] : 0u, threadIdx.x);
             __syncthreads();
-            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int) {
-                gf_encode_slot<R>(p, stride, k, tab, tc);
+            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int, bool valid) {
+                gf_encode_slot<R>(p, stride, k, tab, tc, valid);
             });
             __syncthreads();
         }
@@ -407,11 +440,12 @@ __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
                 w++;
             }
             pres = a.present[min(w, a.nwin - 1)];  // prefetch for the next iteration
-            if (s_now < total) {
-                const uint32_t bad =
-                    xor_decode_slot<R>(a, a.win + w_now * wbytes + col_now * 16u, a.stride, p_now);
-                if (col_now == 0) a.status[w_now] = (uint8_t)bad;
-            }
+            const bool valid = s_now < total;
+            const uint64_t wv = valid ? w_now : a.nwin - 1;
+            const uint32_t cv = valid ? col_now : ncol - 1;
+            const uint32_t bad = xor_decode_slot<R>(a, a.win + wv * wbytes + cv * 16u, a.stride,
+                                                    valid ? p_now : a.present[wv], valid);
+            if (valid && col_now == 0) a.status[w_now] = (uint8_t)bad;
         }
     } else {
         __shared__ GroupLds g;
@@ -443,8 +477,8 @@ __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
                 block_prefix(g.pfx, n, t);
             }
             __syncthreads();
-            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int wl) {
-                (void)xor_decode_slot<R>(a, p, stride, s_pres[wl]);
+            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int wl, bool valid) {
+                (void)xor_decode_slot<R>(a, p, stride, s_pres[wl], valid);
             });
             __syncthreads();
         }
@@ -577,8 +611,8 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
         __syncthreads();
         if (tid < 64) block_prefix(g.pfx, (tid < nb && s_ne[tid]) ? g.ncol[tid] : 0u, tid);
         __syncthreads();
-        for_group_slots(g, nb, [&](uint8_t *base, uint32_t stride, int wl) {
-            const int ne = s_ne[wl];
+        for_group_slots(g, nb, [&](uint8_t *base, uint32_t stride, int wl, bool valid) {
+            const int ne = valid ? (int)s_ne[wl] : 0;
             const uint8_t *region = regions + (size_t)wl * a.win_lds;
             const uint4 *tab = reinterpret_cast<const uint4 *>(region);
             const uint32_t *tc = reinterpret_cast<const uint32_t *>(region + k * R * 16);
