@@ -167,12 +167,9 @@ __device__ __forceinline__ void for_flat_slots(const BatchArgs &a, Body &&body) 
     uint32_t col = (uint32_t)(s - w * ncol);
     const uint64_t wbytes = (uint64_t)(a.k + a.r) * a.stride;
     for (; xr.cur < xr.hi; xr.cur += xr.step) {
-        // uniform control flow: lanes past the end work on the last slot and
-        // skip their stores (keeps wave-uniform table reads scalar)
-        const bool valid = s < total;
-        const uint64_t wv = valid ? w : a.nwin - 1;
-        const uint32_t cv = valid ? col : ncol - 1;
-        body(a.win + wv * wbytes + cv * 16u, a.stride, wv, cv, valid);
+        // lanes past the end skip the body (measured faster than running a
+        // clamped dummy slot to keep control flow uniform: scripts/ab.py, r01)
+        if (s < total) body(a.win + w * wbytes + col * 16u, a.stride, w, col, true);
         s += xr.step * kBlock;
         col += a.step_col;
         w += a.step_win;
@@ -193,19 +190,15 @@ struct GroupLds {
 };
 
 // Streams the flattened columns of the current group:
-// body(base_of_column, stride, wl, valid).  Passes are block-uniform; lanes
-// past the end re-use the last slot with valid = false (stores skipped).
+// body(base_of_column, stride, wl, valid = true).
 template <class Body>
 __device__ __forceinline__ void for_group_slots(const GroupLds &g, int nb, Body &&body) {
     const uint32_t total = g.pfx[nb];
     int wl = 0;
-    for (uint32_t s0 = 0; s0 < total; s0 += kBlock) {
-        const uint32_t s = s0 + threadIdx.x;
-        const bool valid = s < total;
-        const uint32_t sv = valid ? s : total - 1;
-        while (sv >= g.pfx[wl + 1]) wl++;
-        const uint32_t col = sv - g.pfx[wl];
-        body(reinterpret_cast<uint8_t *>(g.base[wl]) + col * 16u, g.stride[wl], wl, valid);
+    for (uint32_t s = threadIdx.x; s < total; s += kBlock) {
+        while (s >= g.pfx[wl + 1]) wl++;
+        const uint32_t col = s - g.pfx[wl];
+        body(reinterpret_cast<uint8_t *>(g.base[wl]) + col * 16u, g.stride[wl], wl, true);
     }
 }
 
@@ -440,12 +433,11 @@ __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
                 w++;
             }
             pres = a.present[min(w, a.nwin - 1)];  // prefetch for the next iteration
-            const bool valid = s_now < total;
-            const uint64_t wv = valid ? w_now : a.nwin - 1;
-            const uint32_t cv = valid ? col_now : ncol - 1;
-            const uint32_t bad = xor_decode_slot<R>(a, a.win + wv * wbytes + cv * 16u, a.stride,
-                                                    valid ? p_now : a.present[wv], valid);
-            if (valid && col_now == 0) a.status[w_now] = (uint8_t)bad;
+            if (s_now < total) {
+                const uint32_t bad = xor_decode_slot<R>(a, a.win + w_now * wbytes + col_now * 16u,
+                                                        a.stride, p_now, true);
+                if (col_now == 0) a.status[w_now] = (uint8_t)bad;
+            }
         }
     } else {
         __shared__ GroupLds g;

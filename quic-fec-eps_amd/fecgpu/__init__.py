@@ -109,7 +109,7 @@ def _lib():
         L = ctypes.CDLL(LIB_PATH)
         vp, u32, u64, i32, sz = (ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int,
                                  ctypes.c_ssize_t)
-        cp = ctypes.POINTER(fecgpu_code)
+        cp = vp  # const fecgpu_code * (byref of any fecgpu_code layout)
         sigs = {
             "fecgpu_abi_version": (i32, []),
             "fecgpu_strerror": (ctypes.c_char_p, [sz]),
