@@ -35,6 +35,22 @@
 // HBM efficient), r = 8 with 8 (its long VALU phase needs more loads queued).
 #define FECGPU_GF_U (R <= 4 ? 2 : 8)
 #endif
+#ifndef FECGPU_XDEC_ALL
+#define FECGPU_XDEC_ALL 0  // XOR decode: all recoverable groups in one row pass (A/B knob)
+#endif
+#ifndef FECGPU_NT_STORE
+// Nontemporal stores for repairs / recovered symbols (written once, not read
+// back by the kernel): +2.8% on cfg2, neutral on cfg3/cfg4 (scripts/ab.py, r01).
+#define FECGPU_NT_STORE 1
+#endif
+#ifndef FECGPU_GF_MINW
+#define FECGPU_GF_MINW 0  // >0: ask for at least this many waves per SIMD on GF kernels
+#endif
+#if FECGPU_GF_MINW > 0
+#define GF_WAVES __attribute__((amdgpu_waves_per_eu(FECGPU_GF_MINW, 8)))
+#else
+#define GF_WAVES
+#endif
 #ifndef FECGPU_ENC_SGPR
 #define FECGPU_ENC_SGPR 0  // GF encode tables via scalar loads instead of LDS (A/B knob)
 #endif
@@ -67,7 +83,7 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
     const u32x4 x = {v.x, v.y, v.z, v.w};
-#if FECGPU_NT
+#if FECGPU_NT || FECGPU_NT_STORE
     __builtin_nontemporal_store(x, (gptr)(p));
 #else
     *(gptr)(p) = x;
@@ -307,6 +323,44 @@ __device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t 
     const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
     const uint64_t miss = ~pres & kmask;
     uint32_t bad = 0;
+#if FECGPU_XDEC_ALL
+    // one pass over the window's rows for every recoverable group at once:
+    // row j feeds accumulator j mod r (the encode structure), rows of groups
+    // with nothing to rebuild and the missing rows themselves are not loaded
+    uint32_t recm = 0;
+    int mrow[R];
+#pragma unroll
+    for (int g = 0; g < R; g++) {
+        const uint64_t mg = miss & a.gmask[g];
+        mrow[g] = (int)__ffsll((unsigned long long)mg) - 1;
+        if (!mg) continue;
+        if (((mg & (mg - 1)) == 0) && ((pres >> (k + g)) & 1)) recm |= 1u << g;
+        else bad = 1;
+    }
+    if (!recm) return bad;
+    constexpr int STEP = R * ((8 + R - 1) / R);
+    uint4 acc[R];
+#pragma unroll
+    for (int g = 0; g < R; g++)
+        acc[g] = ((recm >> g) & 1) ? ld16(base + (size_t)(k + g) * stride) : zero4();
+    for (int j0 = 0; j0 < k; j0 += STEP) {
+        uint4 v[STEP];
+#pragma unroll
+        for (int t = 0; t < STEP; t++) {
+            const int j = j0 + t;
+            const bool need = j < k && ((recm >> (t % R)) & 1) && ((pres >> j) & 1);
+            v[t] = need ? ld16(base + (size_t)j * stride) : zero4();
+        }
+#pragma unroll
+        for (int t = 0; t < STEP; t++) acc[t % R] = xor4(acc[t % R], v[t]);
+    }
+    if (valid) {
+#pragma unroll
+        for (int g = 0; g < R; g++)
+            if ((recm >> g) & 1) st16(base + (size_t)mrow[g] * stride, acc[g]);
+    }
+    return bad;
+#endif
 #pragma unroll
     for (int g = 0; g < R; g++) {
         const uint64_t gm = a.gmask[g];
@@ -360,7 +414,7 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
 }
 
 template <int R, bool FLAT>
-__global__ __launch_bounds__(kBlock) void gf_encode_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kBlock) GF_WAVES void gf_encode_kernel(BatchArgs a) {
     const int k = a.k;
 #if FECGPU_ENC_SGPR
     // kernel-uniform tables read through the constant address space with a
@@ -581,7 +635,7 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, int lane, uint8_t *regio
 }
 
 template <int R>
-__global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kBlock) GF_WAVES void gf_decode_kernel(BatchArgs a) {
     extern __shared__ uint4 dyn[];
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];

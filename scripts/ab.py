@@ -42,12 +42,15 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--bpc", type=int, default=0)
     args = ap.parse_args()
-    libs = args.libs.split(",")
+    # entries: path[@bpc] — the same library may appear with different knobs
+    entries = args.libs.split(",")
+    libs = [e.split("@")[0] for e in entries]
     mods = [load_variant(p, str(i)) for i, p in enumerate(libs)]
     ctxs = [m.Context() for m in mods]
-    if args.bpc:
-        for c in ctxs:
-            c.set_tuning("blocks_per_cu", args.bpc)
+    for c, e in zip(ctxs, entries):
+        bpc = int(e.split("@")[1]) if "@" in e else args.bpc
+        if bpc:
+            c.set_tuning("blocks_per_cu", bpc)
     cfg = workloads.CONFIGS[args.config]
     b = workloads.Batch.allocate(cfg, cfg.nwin_per_gpu, torch.device("cuda"))
     b.synthesize(ctxs[0], 0)
@@ -74,7 +77,7 @@ def main():
             res[i]["decode"].append(timed(lambda: b.decode(c)))
     # the buffer must still decode correctly with the last variant
     ver = b.verify(ctxs[-1], 0)
-    for i, p in enumerate(libs):
+    for i, p in enumerate(entries):
         e = statistics.median(res[i]["encode"])
         d = statistics.median(res[i]["decode"])
         print(json.dumps({"lib": os.path.basename(p), "config": args.config,
