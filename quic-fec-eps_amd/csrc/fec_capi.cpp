@@ -323,7 +323,6 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
     if (rc) return rc;
     if (decode && (!present || !status)) return FECGPU_ERR_INVALID_ARG;
     if (nwin == 0) return 0;
-    const int k = code->k, r = code->r, scheme = (int)code->scheme;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
     // host pointers, uniform layout: chunked copy/compute pipeline

@@ -51,6 +51,20 @@
 #else
 #define GF_WAVES
 #endif
+#ifndef FECGPU_GFD_MINW
+#define FECGPU_GFD_MINW 0  // >0: GF decode at r <= 4 asks for this many waves per SIMD
+#endif
+#if FECGPU_GFD_MINW > 0
+#define GFD_WAVES __attribute__((amdgpu_waves_per_eu(R <= 4 ? FECGPU_GFD_MINW : 1, 8)))
+#else
+#define GFD_WAVES GF_WAVES
+#endif
+#ifndef FECGPU_PLAN_GJ
+#define FECGPU_PLAN_GJ 0  // GF decode plan by Gauss-Jordan instead of the closed form (A/B knob)
+#endif
+#ifndef FECGPU_DEC_PLANONLY
+#define FECGPU_DEC_PLANONLY 0  // measurement aid: GF decode plans only, no data pass
+#endif
 #ifndef FECGPU_ENC_SGPR
 #define FECGPU_ENC_SGPR 0  // GF encode tables via scalar loads instead of LDS (A/B knob)
 #endif
@@ -531,11 +545,95 @@ __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
     }
 }
 
-// GF plan (a6/a7) by one wave: choose the first e present repairs, invert the
-// e x e Cauchy submatrix by Gauss-Jordan (lane = (row, col) of [A | I],
-// exchanges by cross-lane shuffles), fold the inverse into one decode matrix
-// D (e x k inputs: received sources then chosen repairs) and write D's
-// byte-permute tables into the window's LDS region.
+// GF plan (a6/a7) by one wave, closed form.  Missing sources m_0..m_{e-1},
+// the first e present repairs with points x_t = k + sel_t; the system is the
+// Cauchy matrix A[t][u] = 1/(x_t ^ m_u).  Its inverse folded
+// into the decode matrix D (e x k inputs z_q: received sources, then the
+// chosen repairs) has a closed form — with
+//   A_u = sum_t log(x_t ^ m_u) - sum_{v != u} log(m_u ^ m_v)      (lane u)
+//   K_q = sum_v log(z_q ^ m_v) - sum_{t: x_t != z_q} log(x_t ^ z_q) (lane q)
+// every entry is  log D[u][q] = A_u + K_q - log(z_q ^ m_u)  (mod 255).
+// (g(z) = sum_t Ainv[u][t] / (x_t ^ z) is the rational function that is 1 at
+// m_u, 0 at the other m_v and has poles at the x_t; D[u][j] = g(j) for a
+// received source j and D[u][t] = its residue at x_t.)  All lookups are
+// independent: two LDS round trips instead of an e-step elimination chain.
+template <int R>
+__device__ void plan_gf(const BatchArgs &a, uint64_t w, uint64_t pres, int lane, uint8_t *region,
+                        const uint8_t *ex, const uint8_t *lg, uint8_t &ne_out) {
+    const int k = a.k, r = a.r;
+    uint4 *tab = reinterpret_cast<uint4 *>(region);
+    uint32_t *tc = reinterpret_cast<uint32_t *>(region + k * R * 16);
+    uint8_t *insym = region + k * R * 20;
+    uint8_t *outsym = insym + 64;
+    const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
+    const uint64_t miss = ~pres & kmask;
+    const uint64_t rep = (pres >> k) & ((1ull << r) - 1);
+    const int e = __popcll(miss);
+    if (e == 0 || __popcll(rep) < e || e > R) {
+        if (lane == 0) {
+            ne_out = 0;
+            a.status[w] = (e == 0) ? 0 : 1;
+        }
+        return;
+    }
+    // wave-uniform m_v and x_t (pres is uniform: SGPR bit scans)
+    int mv[R], xt[R];
+    {
+        uint64_t mm = miss, rr = rep;
+#pragma unroll
+        for (int v = 0; v < R; v++) {
+            mv[v] = (int)__ffsll((unsigned long long)mm) - 1;
+            xt[v] = k + (int)__ffsll((unsigned long long)rr) - 1;
+            mm &= mm - 1;
+            rr &= rr - 1;
+        }
+    }
+    const int kr = k - e;
+    // input list: received sources ascending, then the chosen repairs
+    if (lane < k && ((pres >> lane) & 1)) insym[__popcll(pres & kmask & ((1ull << lane) - 1))] = (uint8_t)lane;
+    int my_m = 0, my_x = 0;
+#pragma unroll
+    for (int v = 0; v < R; v++) {
+        if (lane == v) { my_m = mv[v]; my_x = xt[v]; }
+    }
+    if (lane < e) {
+        insym[kr + lane] = (uint8_t)my_x;
+        outsym[lane] = (uint8_t)my_m;
+    }
+    WAVE_SYNC();
+    const int zq = (lane < k) ? (int)insym[lane] : 0;
+    int K = 0, A = 0;
+#pragma unroll
+    for (int v = 0; v < R; v++) {
+        if (v < e) {
+            const uint32_t dz = (uint32_t)(zq ^ mv[v]), dx = (uint32_t)(xt[v] ^ zq);
+            const uint32_t ax = (uint32_t)(xt[v] ^ my_m), am = (uint32_t)(my_m ^ mv[v]);
+            K += (int)lg[dz & 255] - (dx ? (int)lg[dx & 255] : 0);
+            A += (int)lg[ax & 255] - (am ? (int)lg[am & 255] : 0);
+        }
+    }
+    // D[u][q] for idx = u*k + q; every __shfl with the whole wave active
+    for (int base = 0; base < e * k; base += 64) {
+        const int idx = base + lane;
+        const int du = idx / k, dq = idx - du * k;
+        const int Au = __shfl(A, du & 63, 64);
+        const int Kq = __shfl(K, dq & 63, 64);
+        const int z = __shfl(zq, dq & 63, 64);
+        const int mu = __shfl(my_m, du & 63, 64);
+        if (idx < e * k) {
+            const int lgd = Au + Kq - (int)lg[(z ^ mu) & 255] + 255 * 4 * kMaxR;
+            const CoefTab ct = make_coef_tab(ex[lgd % 255]);
+            tab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+            tc[dq * R + du] = ct.c;
+        }
+    }
+    if (lane == 0) {
+        ne_out = (uint8_t)e;
+        a.status[w] = 0;
+    }
+}
+
+// The previous Gauss-Jordan plan, kept as an A/B knob (FECGPU_PLAN_GJ=1).
 __device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t *ex, const uint8_t *lg, uint32_t x,
                                                uint32_t y) {
     return (x && y) ? ex[lg[x] + lg[y]] : 0u;
@@ -545,8 +643,8 @@ __device__ __forceinline__ uint32_t gf_inv_lds(const uint8_t *ex, const uint8_t 
 }
 
 template <int R>
-__device__ void plan_gf(const BatchArgs &a, uint64_t w, int lane, uint8_t *region,
-                        const uint8_t *ex, const uint8_t *lg, uint8_t &ne_out) {
+__device__ void plan_gf_gj(const BatchArgs &a, uint64_t w, int lane, uint8_t *region,
+                           const uint8_t *ex, const uint8_t *lg, uint8_t &ne_out) {
     const int k = a.k, r = a.r;
     uint4 *tab = reinterpret_cast<uint4 *>(region);
     uint32_t *tc = reinterpret_cast<uint32_t *>(region + k * R * 16);
@@ -635,7 +733,7 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, int lane, uint8_t *regio
 }
 
 template <int R>
-__global__ __launch_bounds__(kBlock) GF_WAVES void gf_decode_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a) {
     extern __shared__ uint4 dyn[];
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
@@ -652,11 +750,27 @@ __global__ __launch_bounds__(kBlock) GF_WAVES void gf_decode_kernel(BatchArgs a)
         const uint64_t w0 = xr.cur * a.wpb;
         const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
         group_geometry(a, g, w0, nb);
+#if FECGPU_PLAN_GJ
         for (int wl = wave; wl < nb; wl += kBlock / 64)
-            plan_gf<R>(a, w0 + wl, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log, s_ne[wl]);
+            plan_gf_gj<R>(a, w0 + wl, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log, s_ne[wl]);
+#else
+        {
+            // this wave plans windows wave, wave + 4, ...: their masks in one load
+            constexpr int NW = kBlock / 64;
+            const int wl_l = wave + NW * lane;
+            const uint64_t pl = (wl_l < nb) ? a.present[w0 + wl_l] : 0ull;
+            for (int i = 0, wl = wave; wl < nb; i++, wl += NW) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl, i);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pl >> 32), i);
+                plan_gf<R>(a, w0 + wl, ((uint64_t)hi << 32) | lo, lane, regions + (size_t)wl * a.win_lds,
+                           s_exp, s_log, s_ne[wl]);
+            }
+        }
+#endif
         __syncthreads();
         if (tid < 64) block_prefix(g.pfx, (tid < nb && s_ne[tid]) ? g.ncol[tid] : 0u, tid);
         __syncthreads();
+        if (FECGPU_DEC_PLANONLY) continue;
         for_group_slots(g, nb, [&](uint8_t *base, uint32_t stride, int wl, bool valid) {
             const int ne = valid ? (int)s_ne[wl] : 0;
             const uint8_t *region = regions + (size_t)wl * a.win_lds;

@@ -42,15 +42,17 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--bpc", type=int, default=0)
     args = ap.parse_args()
-    # entries: path[@bpc] — the same library may appear with different knobs
+    # entries: path[@bpc] or path@key=val:key=val (fecgpu_ctx_set_tuning keys);
+    # the same library may appear several times with different knobs
     entries = args.libs.split(",")
     libs = [e.split("@")[0] for e in entries]
     mods = [load_variant(p, str(i)) for i, p in enumerate(libs)]
     ctxs = [m.Context() for m in mods]
     for c, e in zip(ctxs, entries):
-        bpc = int(e.split("@")[1]) if "@" in e else args.bpc
-        if bpc:
-            c.set_tuning("blocks_per_cu", bpc)
+        knobs = e.split("@")[1] if "@" in e else (str(args.bpc) if args.bpc else "")
+        for kv in filter(None, knobs.split(":")):
+            key, val = kv.split("=") if "=" in kv else ("blocks_per_cu", kv)
+            c.set_tuning(key, int(val))
     cfg = workloads.CONFIGS[args.config]
     b = workloads.Batch.allocate(cfg, cfg.nwin_per_gpu, torch.device("cuda"))
     b.synthesize(ctxs[0], 0)
