@@ -15,8 +15,9 @@
 //
 // GF(2^8) multiply (DESIGN.md §GF multiply): a coefficient c becomes three
 // byte tables over 3+3+2 bits of the data byte, so c*x for four packed bytes
-// is 3 v_perm_b32 + 3 v_xor; the bit-field split of the data (5 VALU per
-// dword) is shared by every output.
+// is 3 v_perm_b32, accumulated with gfx950's 3-input v_bitop3_b32 (1.5-2 ops
+// per product); the bit-field split of the data (5 VALU per dword) is shared
+// by every output.
 #include "fec_internal.h"
 
 #ifndef FECGPU_NT
@@ -43,13 +44,16 @@
 // back by the kernel): +2.8% on cfg2, neutral on cfg3/cfg4 (scripts/ab.py, r01).
 #define FECGPU_NT_STORE 1
 #endif
-#ifndef FECGPU_GF_MINW
-#define FECGPU_GF_MINW 0  // >0: ask for at least this many waves per SIMD on GF kernels
+#ifndef FECGPU_GFE_MINW_HI
+// GF encode at r > 4 (VALU-bound, paired rows): ask for at least this many
+// waves per SIMD.  3 trades a few spilled registers for occupancy and ran
+// 7% faster than the unconstrained 2 waves on cfg4 (scripts/ab.py, r01).
+#define FECGPU_GFE_MINW_HI 3
 #endif
-#if FECGPU_GF_MINW > 0
-#define GF_WAVES __attribute__((amdgpu_waves_per_eu(FECGPU_GF_MINW, 8)))
+#if FECGPU_GFE_MINW_HI > 0
+#define GFE_WAVES __attribute__((amdgpu_waves_per_eu(R > 4 ? FECGPU_GFE_MINW_HI : 1, 8)))
 #else
-#define GF_WAVES
+#define GFE_WAVES
 #endif
 #ifndef FECGPU_GFD_MINW
 #define FECGPU_GFD_MINW 0  // >0: GF decode at r <= 4 asks for this many waves per SIMD
@@ -57,7 +61,7 @@
 #if FECGPU_GFD_MINW > 0
 #define GFD_WAVES __attribute__((amdgpu_waves_per_eu(R <= 4 ? FECGPU_GFD_MINW : 1, 8)))
 #else
-#define GFD_WAVES GF_WAVES
+#define GFD_WAVES
 #endif
 #ifndef FECGPU_PLAN_GJ
 #define FECGPU_PLAN_GJ 0  // GF decode plan by Gauss-Jordan instead of the closed form (A/B knob)
@@ -124,16 +128,55 @@ __device__ __forceinline__ Split split(uint4 v) {
     return s;
 }
 
-__device__ __forceinline__ uint32_t gmul4(const Split &s, int i, uint4 ab, uint32_t tc) {
-    return __builtin_amdgcn_perm(ab.y, ab.x, s.a[i]) ^ __builtin_amdgcn_perm(ab.w, ab.z, s.b[i]) ^
-           __builtin_amdgcn_perm(tc, tc, s.c[i]);
+#ifndef FECGPU_BITOP3
+#define FECGPU_BITOP3 1  // gfx950 v_bitop3_b32 (3-input XOR) in the GF multiply-accumulate
+#endif
+#ifndef FECGPU_GF_PAIR
+// Fold two input rows per xor3 chain (1.5 instead of 2 ops per product, but
+// two rows' splits and tables live at once): 0 never, 1 encode at r > 4,
+// 2 every encode (default: cfg4 encode -14% time, cfg3 -1%), 3 encode and
+// decode: pairing in decode cost 12% on cfg3 through register pressure
+// (scripts/ab.py, r01).
+#define FECGPU_GF_PAIR 2
+#endif
+#define GF_PAIR_ENC(R) (FECGPU_BITOP3 && (FECGPU_GF_PAIR >= 2 || (FECGPU_GF_PAIR == 1 && (R) > 4)))
+#define GF_PAIR_DEC (FECGPU_BITOP3 && FECGPU_GF_PAIR >= 3)
+
+// a ^ b ^ c in one gfx950 VALU op (truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if FECGPU_BITOP3
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
 }
 
+// acc ^= c*x for the 4 dwords of a column: 3 perm + 2 VALU per dword
+__device__ __forceinline__ uint32_t gmac1(uint32_t acc, const Split &s, int i, uint4 ab, uint32_t tc) {
+    return xor3(acc, __builtin_amdgcn_perm(ab.y, ab.x, s.a[i]), __builtin_amdgcn_perm(ab.w, ab.z, s.b[i])) ^
+           __builtin_amdgcn_perm(tc, tc, s.c[i]);
+}
 __device__ __forceinline__ void gmac(uint4 &acc, const Split &s, uint4 ab, uint32_t tc) {
-    acc.x ^= gmul4(s, 0, ab, tc);
-    acc.y ^= gmul4(s, 1, ab, tc);
-    acc.z ^= gmul4(s, 2, ab, tc);
-    acc.w ^= gmul4(s, 3, ab, tc);
+    acc.x = gmac1(acc.x, s, 0, ab, tc);
+    acc.y = gmac1(acc.y, s, 1, ab, tc);
+    acc.z = gmac1(acc.z, s, 2, ab, tc);
+    acc.w = gmac1(acc.w, s, 3, ab, tc);
+}
+
+// acc ^= c0*x0 ^ c1*x1 (two input rows): 6 perm + 3 xor3 per dword
+__device__ __forceinline__ uint32_t gmac2_1(uint32_t acc, const Split &s0, const Split &s1, int i,
+                                            uint4 ab0, uint32_t tc0, uint4 ab1, uint32_t tc1) {
+    uint32_t t = xor3(acc, __builtin_amdgcn_perm(ab0.y, ab0.x, s0.a[i]),
+                      __builtin_amdgcn_perm(ab0.w, ab0.z, s0.b[i]));
+    t = xor3(t, __builtin_amdgcn_perm(tc0, tc0, s0.c[i]), __builtin_amdgcn_perm(ab1.y, ab1.x, s1.a[i]));
+    return xor3(t, __builtin_amdgcn_perm(ab1.w, ab1.z, s1.b[i]), __builtin_amdgcn_perm(tc1, tc1, s1.c[i]));
+}
+__device__ __forceinline__ void gmac2(uint4 &acc, const Split &s0, const Split &s1, uint4 ab0,
+                                      uint32_t tc0, uint4 ab1, uint32_t tc1) {
+    acc.x = gmac2_1(acc.x, s0, s1, 0, ab0, tc0, ab1, tc1);
+    acc.y = gmac2_1(acc.y, s0, s1, 1, ab0, tc0, ab1, tc1);
+    acc.z = gmac2_1(acc.z, s0, s1, 2, ab0, tc0, ab1, tc1);
+    acc.w = gmac2_1(acc.w, s0, s1, 3, ab0, tc0, ab1, tc1);
 }
 
 __device__ __forceinline__ void win_geom(const BatchArgs &a, uint64_t w, uint64_t &base,
@@ -272,7 +315,7 @@ __device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, 
 // a time into one of two register buffers while the other is multiplied, so
 // every wave keeps U 16-B loads in flight through the VALU phase.
 // `addr(q)` gives input q's column address, tables are [q][m] in LDS.
-template <int R, int U, class Addr, class TabP, class TcP>
+template <int R, int U, bool PAIR, class Addr, class TabP, class TcP>
 __device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne, Addr &&addr,
                                                  TabP tab, TcP tc) {
     uint4 va[U], vb[U];
@@ -281,9 +324,22 @@ __device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne,
         for (int t = 0; t < U; t++) v[t] = ld16(addr(min(q0 + t, k - 1)));  // past k: unused re-read
     };
     auto mul = [&](const uint4(&v)[U], int q0) {
+        int t0 = 0;
+        // PAIR: rows in pairs, one xor3 chain folds both rows' lookups
+#pragma unroll
+        for (int t = 0; t + 1 < U; t += 2) {
+            if (PAIR && q0 + t + 1 < k) {
+                const Split s0 = split(v[t]), s1 = split(v[t + 1]);
+                const int row = __builtin_amdgcn_readfirstlane((q0 + t) * R);
+#pragma unroll
+                for (int m = 0; m < R; m++)
+                    if (m < ne) gmac2(acc[m], s0, s1, tab[row + m], tc[row + m], tab[row + R + m], tc[row + R + m]);
+                t0 = t + 2;
+            }
+        }
 #pragma unroll
         for (int t = 0; t < U; t++) {
-            if (q0 + t < k) {
+            if (t >= t0 && q0 + t < k) {
                 const Split sp = split(v[t]);
                 // wave-uniform row index (lets uniform table reads become scalar loads)
                 const int row = __builtin_amdgcn_readfirstlane((q0 + t) * R);
@@ -319,7 +375,7 @@ __device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, i
     uint4 acc[R];
 #pragma unroll
     for (int m = 0; m < R; m++) acc[m] = zero4();
-    gf_mac_pipelined<R, U>(acc, k, R, [&](int q) { return base + (uint32_t)q * stride; }, tab, tc);
+    gf_mac_pipelined<R, U, GF_PAIR_ENC(R)>(acc, k, R, [&](int q) { return base + (uint32_t)q * stride; }, tab, tc);
     if (valid) {
 #pragma unroll
         for (int m = 0; m < R; m++) st16(base + (size_t)(k + m) * stride, acc[m]);
@@ -428,7 +484,7 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
 }
 
 template <int R, bool FLAT>
-__global__ __launch_bounds__(kBlock) GF_WAVES void gf_encode_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a) {
     const int k = a.k;
 #if FECGPU_ENC_SGPR
     // kernel-uniform tables read through the constant address space with a
@@ -781,7 +837,7 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
             uint4 acc[R];
 #pragma unroll
             for (int m = 0; m < R; m++) acc[m] = zero4();
-            gf_mac_pipelined<R, U>(acc, k, ne,
+            gf_mac_pipelined<R, U, GF_PAIR_DEC>(acc, k, ne,
                                    [&](int q) { return base + (uint32_t)insym[q] * stride; }, tab, tc);
 #pragma unroll
             for (int m = 0; m < R; m++)
