@@ -54,6 +54,7 @@ for s in "$@"; do
         probe) step probe 300 ./scripts/stream_probe ;;
         layout) step layout 300 ./scripts/layout_probe ;;
         readp) step readp 300 ./scripts/read_probe ;;
+        valu) step valu 300 ./scripts/valu_probe ;;
         sweep*)  # sweepN: blocks-per-CU sweep of config N, default lib + every variant lib
             c=${s#sweep}
             step sweep${c}_base 400 python scripts/sweep.py --config $c
