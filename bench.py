@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--grid-mult", type=int, default=0, help="tuning: persistent grid multiplier")
     ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
     ap.add_argument("--bpc", type=int, default=0, help="tuning: persistent workgroups per CU")
+    ap.add_argument("--host-direct", type=int, default=-1,
+                    help="tuning (config 5/6): kernels write outputs to mapped host memory, bit 0 encode, bit 1 decode")
+    ap.add_argument("--host-chunk-mb", type=int, default=0, help="tuning (config 5/6): pipeline chunk size")
     return ap.parse_args()
 
 
@@ -140,6 +143,10 @@ def main():
         ctx.set_tuning("wpb", args.wpb)
     if args.bpc:
         ctx.set_tuning("blocks_per_cu", args.bpc)
+    if args.host_direct >= 0:
+        ctx.set_tuning("host_direct", args.host_direct)
+    if args.host_chunk_mb:
+        ctx.set_tuning("host_chunk_mb", args.host_chunk_mb)
     if cfg.host:  # config 5: host buffers, PCIe-inclusive (never the headline value)
         batch = workloads.HostBatch.allocate(cfg, nwin, dev)
         log(f"rank {rank}: {cfg.name}, windows [{w0}, {w0 + nwin}), "

@@ -94,11 +94,18 @@ ssize_t     fecgpu_code_check(const fecgpu_code *code);
 ssize_t fecgpu_ctx_new(const int *devs, int ndev, fecgpu_ctx **out);
 void    fecgpu_ctx_free(fecgpu_ctx *ctx);
 /* Pinned (page-locked) host memory for FECGPU_F_HOST_PTRS buffers: with it the
- * host-pointer batches overlap H2D copies, kernels and D2H copies. */
+ * host-pointer batches overlap H2D copies, kernels and D2H copies, and the
+ * kernels store repairs / recovered sources straight into the (device-mapped)
+ * host windows, so only changed rows cross PCIe device->host. */
 ssize_t fecgpu_host_alloc(size_t bytes, void **out);
 void    fecgpu_host_free(void *p);
 /* Launch tuning knobs (0 = automatic): "grid_mult" (persistent grid =
- * resident workgroups x value), "wpb" (windows per workgroup, group mode). */
+ * resident workgroups x value), "blocks_per_cu" (persistent grid = CUs x
+ * value), "wpb" (windows per workgroup, group mode); host pipeline:
+ * "host_direct" (bit 0 encode, bit 1 decode: kernels write outputs into
+ * mapped pinned host windows instead of D2H copies; bit 2: they also read the
+ * windows over PCIe instead of H2D copies; default 6 = decode zero-copy),
+ * "host_chunk_mb" (pipeline chunk, default 128). */
 ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value);
 
 /* ---- batch entry points (hot path) ---------------------------------- */

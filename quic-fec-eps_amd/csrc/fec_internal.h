@@ -35,6 +35,10 @@ struct BatchArgs {
     int k, r;
     int wpb;                   // group mode: windows per workgroup
     uint32_t win_lds;          // GF decode: LDS bytes per window region
+    // Written symbols (repairs, recovered sources) go to p + out_delta for an
+    // input address p: 0 in place; the host pipeline points it at the caller's
+    // pinned host windows so outputs cross PCIe straight from the kernel.
+    uint64_t out_delta;
 };
 
 struct LaunchPlan {

@@ -36,6 +36,9 @@
 // HBM efficient), r = 8 with 8 (its long VALU phase needs more loads queued).
 #define FECGPU_GF_U (R <= 4 ? 2 : 8)
 #endif
+#ifndef FECGPU_GFD_U
+#define FECGPU_GFD_U FECGPU_GF_U  // GF decode: input rows loaded per batch
+#endif
 #ifndef FECGPU_XDEC_ALL
 #define FECGPU_XDEC_ALL 0  // XOR decode: all recoverable groups in one row pass (A/B knob)
 #endif
@@ -290,7 +293,8 @@ __device__ __forceinline__ void group_geometry(const BatchArgs &a, GroupLds &g, 
 // XOR encode (a4): R_g = xor of S_j, j = g (mod r).  All loads of a slot are
 // issued before the xors (8 x 16 B in flight per lane at k = 8).
 template <int R>
-__device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, int k, bool valid) {
+__device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, int k, bool valid,
+                                                uint64_t od) {
     constexpr int STEP = R * ((FECGPU_XOR_LOADS + R - 1) / R);
     uint4 acc[R];
 #pragma unroll
@@ -306,7 +310,7 @@ __device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, 
     }
     if (valid) {
 #pragma unroll
-        for (int g = 0; g < R; g++) st16(base + (size_t)(k + g) * stride, acc[g]);
+        for (int g = 0; g < R; g++) st16(base + od + (size_t)(k + g) * stride, acc[g]);
     }
 }
 
@@ -370,7 +374,7 @@ __device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne,
 // GF encode (a5): R_i = sum_j C[i][j] * S_j, tables [j][i] in LDS (broadcast reads).
 template <int R, class TabP, class TcP>
 __device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, int k, TabP tab,
-                                               TcP tc, bool valid) {
+                                               TcP tc, bool valid, uint64_t od) {
     constexpr int U = FECGPU_GF_U;
     uint4 acc[R];
 #pragma unroll
@@ -378,7 +382,7 @@ __device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, i
     gf_mac_pipelined<R, U, GF_PAIR_ENC(R)>(acc, k, R, [&](int q) { return base + (uint32_t)q * stride; }, tab, tc);
     if (valid) {
 #pragma unroll
-        for (int m = 0; m < R; m++) st16(base + (size_t)(k + m) * stride, acc[m]);
+        for (int m = 0; m < R; m++) st16(base + od + (size_t)(k + m) * stride, acc[m]);
     }
 }
 
@@ -427,7 +431,7 @@ __device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t 
     if (valid) {
 #pragma unroll
         for (int g = 0; g < R; g++)
-            if ((recm >> g) & 1) st16(base + (size_t)mrow[g] * stride, acc[g]);
+            if ((recm >> g) & 1) st16(base + a.out_delta + (size_t)mrow[g] * stride, acc[g]);
     }
     return bad;
 #endif
@@ -453,7 +457,7 @@ __device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t 
 #pragma unroll
             for (int t = 0; t < 8; t++) acc = xor4(acc, v[t]);
         }
-        if (valid) st16(base + (size_t)m * stride, acc);
+        if (valid) st16(base + a.out_delta + (size_t)m * stride, acc);
     }
     return bad;
 }
@@ -463,7 +467,7 @@ template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
     if constexpr (FLAT) {
         for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t, bool valid) {
-            xor_encode_slot<R>(p, stride, a.k, valid);
+            xor_encode_slot<R>(p, stride, a.k, valid, a.out_delta);
         });
     } else {
         __shared__ GroupLds g;
@@ -476,7 +480,7 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
             if (threadIdx.x < 64) block_prefix(g.pfx, (int)threadIdx.x < nb ? g.ncol[threadIdx.x] : 0u, threadIdx.x);
             __syncthreads();
             for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int, bool valid) {
-                xor_encode_slot<R>(p, stride, a.k, valid);
+                xor_encode_slot<R>(p, stride, a.k, valid, a.out_delta);
             });
             __syncthreads();
         }
@@ -511,7 +515,7 @@ __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a
 #endif
     if constexpr (FLAT) {
         for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t, bool valid) {
-            gf_encode_slot<R>(p, stride, k, tab, tc, valid);
+            gf_encode_slot<R>(p, stride, k, tab, tc, valid, a.out_delta);
         });
     } else {
         __shared__ GroupLds g;
@@ -524,7 +528,7 @@ __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a
             if (threadIdx.x < 64) block_prefix(g.pfx, (int)threadIdx.x < nb ? g.ncol[threadIdx.x] : 0u, threadIdx.x);
             __syncthreads();
             for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int, bool valid) {
-                gf_encode_slot<R>(p, stride, k, tab, tc, valid);
+                gf_encode_slot<R>(p, stride, k, tab, tc, valid, a.out_delta);
             });
             __syncthreads();
         }
@@ -795,7 +799,7 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
     __shared__ uint8_t s_log[256];
     __shared__ GroupLds g;
     __shared__ uint8_t s_ne[kMaxWpb];
-    constexpr int U = FECGPU_GF_U;
+    constexpr int U = FECGPU_GFD_U;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
     uint8_t *regions = reinterpret_cast<uint8_t *>(dyn);
     for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
@@ -841,7 +845,7 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
                                    [&](int q) { return base + (uint32_t)insym[q] * stride; }, tab, tc);
 #pragma unroll
             for (int m = 0; m < R; m++)
-                if (m < ne) st16(base + (size_t)outsym[m] * stride, acc[m]);
+                if (m < ne) st16(base + a.out_delta + (size_t)outsym[m] * stride, acc[m]);
         });
         __syncthreads();
     }

@@ -227,11 +227,18 @@ class HostBatch:
         return self.nwin * self.cfg.k * self.cfg.L
 
     def algorithmic_bytes(self) -> dict:
-        """PCIe bytes per call: encode sends k rows, returns r rows; decode sends
-        whole windows + masks, returns k rows + status."""
+        """PCIe bytes each call must move: encode sends k source rows and returns
+        r repair rows; decode needs the k present rows that solve the window
+        (received sources + as many repairs as erasures) plus the mask, and
+        returns the e recovered rows plus status.  (The pipeline sends whole
+        windows, k + r rows, on the way in.)"""
+        import numpy as np
         c, n = self.cfg, self.nwin
+        kmask = np.uint64((1 << c.k) - 1)
+        miss = (~self.present) & kmask
+        e = int(sum(int(((miss >> np.uint64(j)) & np.uint64(1)).sum()) for j in range(c.k)))
         return {"encode": n * (c.k + c.r) * c.stride,
-                "decode": n * ((c.k + c.r) * c.stride + 8 + c.k * c.stride + 1)}
+                "decode": n * (c.k * c.stride + 8 + 1) + e * c.stride}
 
     def verify(self, ctx: Context, w0: int) -> dict:
         import numpy as np

@@ -39,7 +39,10 @@ for s in "$@"; do
         bench2) step bench2 600 python bench.py --config 2 --steps 20 --warmup 3 ;;
         bench3) step bench3 600 python bench.py --config 3 --steps 10 --warmup 2 --cpu-seconds 10 ;;
         bench4) step bench4 600 python bench.py --config 4 --steps 5 --warmup 1 --cpu-seconds 10 ;;
+        bench5) step bench5 600 python bench.py --config 5 --steps 10 --warmup 2 --cpu-seconds 0 ;;
+        bench6) step bench6 600 python bench.py --config 6 --steps 10 --warmup 2 --cpu-seconds 0 ;;
         prof2) prof prof2 2 ;;
+        prof5) prof prof5 5 ;;
         prof3) prof prof3 3 ;;
         prof4) prof prof4 4 ;;
         pmc2r) pmc pmc2r 2 FETCH_SIZE ;;

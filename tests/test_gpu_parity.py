@@ -216,10 +216,13 @@ def test_host_pointer_mode(ctx):
     _cmp_emitted(h, od, S, "host decode")
 
 
-@pytest.mark.parametrize("cfgid", [5, 6])
-def test_pinned_host_pipeline_matches_device_path(ctx, cfgid):
+@pytest.mark.parametrize("cfgid,direct", [(5, 6), (6, 6), (5, 0), (6, 0), (6, 3), (5, 7), (6, 7)])
+def test_pinned_host_pipeline_matches_device_path(ctx, cfgid, direct):
     """FECGPU_F_HOST_PTRS over pinned memory, > 3 pipeline chunks (slot reuse): repairs
-    and recovered sources equal the device-resident path on the same windows."""
+    and recovered sources equal the device-resident path on the same windows, with
+    the kernels storing straight into the mapped host windows (direct bit 0 encode,
+    bit 1 decode), reading them too (bit 2), and with H2D/D2H copies only (0)."""
+    ctx.set_tuning("host_direct", direct)
     cfg = WL.CONFIGS[cfgid]
     nwin = 40000  # 480 MB of windows -> 8 chunks of 64 MB
     hb = WL.HostBatch.allocate(cfg, nwin, torch.device("cuda"))
@@ -233,6 +236,7 @@ def test_pinned_host_pipeline_matches_device_path(ctx, cfgid):
     torch.cuda.synchronize()
     assert np.array_equal(hb.buf.array, db.win.cpu().numpy())
     res = hb.verify(ctx, 77)
+    ctx.set_tuning("host_direct", 6)
     assert res["ok"] and res["unrecoverable"] == 0, res
     hb.buf.close()
 
