@@ -241,6 +241,43 @@ def test_pinned_host_pipeline_matches_device_path(ctx, cfgid, direct):
     hb.buf.close()
 
 
+@pytest.mark.parametrize("scheme,k,r", [("gf256", 32, 8), ("xor", 8, 2)])
+@pytest.mark.parametrize("direct", [0, 6, 7])
+def test_pinned_host_mixed_mtu_vs_oracle(ctx, scheme, k, r, direct):
+    """Host pipeline on per-window symbol lengths (mixed MTU, LENPREFIX, i.i.d.
+    erasures), 1 MiB chunks so the 3 staging slots are reused many times: encode and
+    decode through pinned host windows equal the oracle, for copies only, zero-copy
+    decode, and zero-copy + direct stores on both sides."""
+    nwin = 150
+    S = O.sym_lens(1, SEED, 0, nwin, k, 0)
+    stride = O.round_up(int(S.max()), 16)
+    wins = O.make_windows(1, SEED, 0, nwin, k, r, 0, stride)
+    present = O.presents(2, SEED, 0, nwin, _scheme(scheme), k, r)
+    oe, od, os_ = oracle_run(scheme, k, r, wins, S, present)
+    code = fecgpu.Code(scheme, k, r)
+    buf = fecgpu.PinnedBuffer(wins.nbytes)
+    h = buf.array.reshape(wins.shape)
+    h[:] = wins
+    ctx.set_tuning("host_direct", direct)
+    ctx.set_tuning("host_chunk_mb", 1)
+    try:
+        ctx.encode_batch(code, h, nwin=nwin, stride=stride, sym_len=S, flags=fecgpu.F_HOST_PTRS)
+        enc = h.copy()
+        O.erase(h, present, k, r, fill=0xAB)  # the oracle_run poison
+        st = np.full(nwin, 9, np.uint8)
+        ctx.decode_batch(code, h, present, st, nwin=nwin, stride=stride, sym_len=S,
+                         flags=fecgpu.F_HOST_PTRS)
+        dec = h.copy()
+    finally:
+        ctx.set_tuning("host_direct", 6)
+        ctx.set_tuning("host_chunk_mb", 128)
+        del h
+        buf.close()  # no view of the freed pages may outlive this (pytest reprs locals)
+    _cmp_emitted(enc, oe, S, "host encode")
+    assert np.array_equal(st, os_), np.nonzero(st != os_)
+    _cmp_emitted(dec, od, S, "host decode")
+
+
 def test_zero_windows_and_errors(ctx):
     code = fecgpu.Code("gf256", 4, 2)
     d = torch.zeros(4096, dtype=torch.uint8, device="cuda")
