@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--bpc", type=int, default=0)
+    ap.add_argument("--alt", action="store_true",
+                    help="also time alternating encode/decode pairs (the bench's step)")
     args = ap.parse_args()
     # entries: path[@bpc] or path@key=val:key=val (fecgpu_ctx_set_tuning keys);
     # the same library may appear several times with different knobs
@@ -59,7 +61,7 @@ def main():
     b.make_erasures(ctxs[0], 0)
     alg = b.algorithmic_bytes()
     src = b.source_bytes()
-    res = [{"encode": [], "decode": []} for _ in libs]
+    res = [{"encode": [], "decode": [], "pair": []} for _ in libs]
 
     def timed(fn):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -77,6 +79,8 @@ def main():
         for i, c in enumerate(ctxs):
             res[i]["encode"].append(timed(lambda: b.encode(c)))
             res[i]["decode"].append(timed(lambda: b.decode(c)))
+            if args.alt:
+                res[i]["pair"].append(timed(lambda: (b.encode(c), b.decode(c))))
     # the buffer must still decode correctly with the last variant
     ver = b.verify(ctxs[-1], 0)
     for i, p in enumerate(entries):
@@ -88,7 +92,8 @@ def main():
                           "dec_min": round(min(res[i]["decode"]), 4),
                           "enc_TBps": round(alg["encode"] / e / 1e9, 3),
                           "dec_TBps": round(alg["decode"] / d / 1e9, 3),
-                          "src_GBps": round(src / (e + d) / 1e6, 1), "verify_ok": ver["ok"]}),
+                          "src_GBps": round(src / (e + d) / 1e6, 1), "verify_ok": ver["ok"],
+                          **({"pair_ms": round(statistics.median(res[i]["pair"]), 4)} if args.alt else {})}),
               flush=True)
 
 
