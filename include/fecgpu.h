@@ -19,8 +19,10 @@
  * Batch layout (A.4): window w is (k + r) symbols, sources 0..k-1 then
  * repairs k..k+r-1.  With win_off == NULL window w starts at
  * win + w*(k+r)*stride and every symbol occupies `stride` bytes (multiple of
- * 16, >= S).  With win_off != NULL window w starts at win + win_off[w] and
- * its symbol stride is round_up(S_w, 16).  S_w = sym_len[w], or sym_len_all
+ * 16, >= S).  With win_off != NULL window w starts at win + win_off[w]
+ * (64-bit wrap-around add, so offsets may reach below `win`) and its symbol
+ * stride is `stride` when nonzero (S_w is clamped to it), else
+ * round_up(S_w, 16) (windows packed).  S_w = sym_len[w], or sym_len_all
  * when sym_len == NULL.  Bytes [S_w, stride) of a symbol are padding: the
  * kernels compute on whole 16-byte columns, so padding of written symbols
  * holds the code applied to the inputs' padding (zero in, zero out).
@@ -132,9 +134,12 @@ ssize_t fecgpu_decode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *w
  * (§3 call stacks A/B).  The sender appends every
  * protected payload as a source symbol and reads repair symbols back; the
  * receiver files sources and repairs by (window, index) and reads recovered
- * packets back.  Complete windows are queued and run through the batch
- * entry points above (host pointers, ragged layout) `batch` windows at a
- * time.  All buffers are host memory. */
+ * packets back.  Symbols are written once, straight into pinned host
+ * windows the GPU maps (no staging copies): the sender fills `batch` windows
+ * and launches their encode asynchronously while it fills the next ones; the
+ * receiver files symbols into a pool of window slots and a flush decodes every
+ * decodable window in one zero-copy launch (ragged layout, fixed pitch).
+ * Caller buffers are plain host memory. */
 typedef struct fecgpu_encoder fecgpu_encoder;
 typedef struct fecgpu_decoder fecgpu_decoder;
 

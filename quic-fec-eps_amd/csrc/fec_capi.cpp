@@ -283,6 +283,9 @@ ssize_t validate_batch(const fecgpu_code *code, const void *win, const uint32_t 
     if (!win_off) {
         if (stride == 0 || (stride & 15)) return FECGPU_ERR_INVALID_ARG;
         if (!sym_len && sym_len_all > stride) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    } else if (stride) {  // ragged with a fixed symbol pitch
+        if (stride & 15) return FECGPU_ERR_INVALID_ARG;
+        if (!sym_len && sym_len_all > stride) return FECGPU_ERR_BUFFER_TOO_SHORT;
     }
     if (!sym_len && sym_len_all == 0) return FECGPU_ERR_INVALID_ARG;
     if ((reinterpret_cast<uintptr_t>(win) & 15) != 0) return FECGPU_ERR_INVALID_ARG;
@@ -321,7 +324,7 @@ size_t host_window_bytes(const fecgpu_code *code, const uint64_t *win_off, const
     size_t mx = 0;
     for (uint64_t w = 0; w < nwin; w++) {
         const uint32_t S = sym_len ? sym_len[w] : sym_len_all;
-        mx = std::max(mx, (size_t)win_off[w] + (size_t)n * ((S + 15u) & ~15u));
+        mx = std::max(mx, (size_t)win_off[w] + (size_t)n * (stride ? stride : ((S + 15u) & ~15u)));
     }
     return mx;
 }
@@ -389,6 +392,7 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
     a.nwin = nwin;
     a.S_all = sym_len_all;
     a.stride = stride;
+    a.off_stride = win_off ? stride : 0;
     rc = launch_device(ctx, code, decode, a, s);
     if (rc) return rc;
 
@@ -579,6 +583,24 @@ ssize_t run_host_pipelined(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode
 }
 
 }  // namespace
+
+namespace fecgpu {
+
+ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
+                     hipStream_t s) {
+    if (!ctx || !a.win) return FECGPU_ERR_INVALID_ARG;
+    ssize_t rc = fecgpu_code_check(code);
+    if (rc) return rc;
+    if (a.nwin == 0) return 0;
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != ctx->devs[0]) HIP_TRY(hipSetDevice(ctx->devs[0]), "hipSetDevice");
+    rc = launch_device(ctx, code, decode, a, s);
+    if (prev != ctx->devs[0]) (void)hipSetDevice(prev);
+    return rc;
+}
+
+}  // namespace fecgpu
 
 extern "C" {
 

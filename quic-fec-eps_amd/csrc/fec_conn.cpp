@@ -1,104 +1,223 @@
 // fec_conn.cpp — per-connection encoder / decoder objects of the C ABI
 // (include/fecgpu.h, "per-packet API"; SURVEY.md §8b item 2, §3 call stacks
-// A and B).
+// A and B, §8f-2/f-3).
 //
 // These are the calls a QUIC Connection makes one packet at a time: the
 // sender appends each protected payload as a source symbol and reads repair
 // symbols back; the receiver files sources and repairs by (window, index) and
-// reads recovered packets back.  Both sides queue complete windows and hand
-// them to the GPU hot path in batches (fecgpu_encode_batch /
-// fecgpu_decode_batch with FECGPU_F_HOST_PTRS, ragged window layout), so a
-// connection pays one H2D/kernel/D2H round trip per `batch` windows, not per
-// packet.  Framing: FIXED — every packet of a window
-// has the same length, symbol = packet; LENPREFIX — symbol = u16be(len) ||
-// payload || zero pad to S = 2 + max len of the window.
+// reads recovered packets back.  Framing: FIXED —
+// every packet of a window has the same length, symbol = packet; LENPREFIX —
+// symbol = u16be(len) || payload || zero pad to S = 2 + max len of the window.
+//
+// Zero-copy design.  Every symbol is written exactly once, by the add call,
+// into pinned host memory that the GPU maps, at its final place in a window
+// of (k + r) rows of a fixed pitch `stride` = round_up(max symbol, 16):
+//   sender   — a ring of batch buffers of `batch` windows each.  Closing the
+//              last window of a buffer launches its encode (uniform layout,
+//              per-window S) on the encoder's stream and the sender moves on
+//              to the next buffer; the kernel reads the sources and writes
+//              the repairs over PCIe.  A buffer is recycled once every one of
+//              its windows has been released.
+//   receiver — a pool of window slots.  flush() collects the windows that can
+//              recover something and decodes them in one launch over the pool
+//              (ragged layout with a fixed pitch: slot offsets from the first
+//              chunk, 64-bit wrap-around), the kernel writing recovered rows
+//              in place.  No staging buffers, no H2D / D2H copies.
+#include <hip/hip_runtime.h>
+
 #include <algorithm>
 #include <cstring>
 #include <deque>
-#include <map>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/fecgpu.h"
+#include "fec_internal.h"
+
+using fecgpu::BatchArgs;
 
 namespace {
 
 inline uint32_t rup16(uint32_t x) { return (x + 15u) & ~15u; }
+inline bool is_lenprefix(const fecgpu_code &c) { return c.framing == FECGPU_FRAMING_LENPREFIX; }
 
-struct EncWin {
-    uint64_t id = 0;
-    uint32_t S = 0;
-    std::vector<uint8_t> sym;  // (k + r) * rup16(S): sources then repairs
+// Pinned host block mapped into the device's address space.
+struct Pinned {
+    uint8_t *host = nullptr, *dev = nullptr;
+    size_t bytes = 0;
 };
 
-struct DecWin {
-    uint32_t S = 0;                       // known once a repair (or FIXED source) arrives
-    uint64_t present = 0;                 // bit i: symbol i held (received or recovered)
-    std::vector<std::vector<uint8_t>> src;  // framed source symbols (length S once known)
-    std::vector<std::vector<uint8_t>> rep;
-    std::vector<uint32_t> plen;           // payload length per source (LENPREFIX: from prefix)
+ssize_t pinned_alloc(size_t bytes, Pinned &p) {
+    void *h = nullptr, *d = nullptr;
+    if (hipHostMalloc(&h, bytes, hipHostMallocDefault) != hipSuccess) return FECGPU_ERR_DEVICE;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+        (void)hipHostFree(h);
+        return FECGPU_ERR_DEVICE;
+    }
+    p.host = static_cast<uint8_t *>(h);
+    p.dev = static_cast<uint8_t *>(d);
+    p.bytes = bytes;
+    return 0;
+}
+
+void pinned_free(Pinned &p) {
+    if (p.host) (void)hipHostFree(p.host);
+    p = Pinned{};
+}
+
+// Makes `dev` the current device for the guard's scope.
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DevGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
 };
 
-bool is_lenprefix(const fecgpu_code &c) { return c.framing == FECGPU_FRAMING_LENPREFIX; }
+int ctx_device() {
+    int d = 0;
+    (void)hipGetDevice(&d);
+    return d;
+}
+
+// ------------------------------------------------------------ encoder ---
+struct EncBatch {
+    Pinned mem;               // batch x (k + r) x stride window bytes, then S[batch]
+    uint32_t *S = nullptr;    // host view of the per-window symbol lengths
+    uint32_t *S_dev = nullptr;
+    hipEvent_t done = nullptr;
+    uint64_t first = 0;       // window id of slot 0
+    uint32_t nwin = 0;        // closed windows
+    uint32_t live = 0;        // closed and not released
+    bool launched = false;
+    std::vector<uint8_t> released;
+};
 
 }  // namespace
 
 struct fecgpu_encoder {
-    fecgpu_ctx *ctx;
-    fecgpu_code code;
-    uint32_t max_len, batch;
+    fecgpu_ctx *ctx = nullptr;
+    fecgpu_code code{};
+    uint32_t max_len = 0, batch = 0, stride = 0;
+    size_t wbytes = 0;
+    int dev = 0;
+    hipStream_t stream = nullptr;
     uint64_t next_win = 0;
-    std::vector<std::vector<uint8_t>> open;  // payloads of the open window
-    std::deque<EncWin> pending;              // closed, not yet encoded
-    std::map<uint64_t, EncWin> done;         // encoded, repairs readable
-};
-
-struct fecgpu_decoder {
-    fecgpu_ctx *ctx;
-    fecgpu_code code;
-    uint32_t max_len, batch;
-    std::map<uint64_t, DecWin> wins;
-    uint64_t dirty = 0;  // windows changed since the last flush
+    int open_n = 0;           // sources in the open window
+    uint32_t open_max = 0;
+    uint32_t open_len[FECGPU_MAX_K] = {};
+    EncBatch *cur = nullptr;  // being filled (its windows [first, first + nwin) closed)
+    std::deque<EncBatch *> active;  // window order: launched batches, then cur
+    std::vector<EncBatch *> spare;
+    std::vector<EncBatch *> all;
 };
 
 namespace {
 
-// Pack windows into one ragged host batch (win_off layout) and run the hot path.
-ssize_t run_host_batch(fecgpu_ctx *ctx, const fecgpu_code &code, bool decode,
-                       std::vector<uint8_t> &buf, std::vector<uint64_t> &off,
-                       std::vector<uint32_t> &len, std::vector<uint64_t> &pres,
-                       std::vector<uint8_t> &status) {
-    const uint64_t n = off.size();
-    if (n == 0) return 0;
-    if (decode)
-        return fecgpu_decode_batch(ctx, &code, buf.data(), off.data(), len.data(), 0, 0, n,
-                                   pres.data(), status.data(), FECGPU_F_HOST_PTRS, nullptr);
-    return fecgpu_encode_batch(ctx, &code, buf.data(), off.data(), len.data(), 0, 0, n,
-                               FECGPU_F_HOST_PTRS, nullptr);
+ssize_t enc_take_batch(fecgpu_encoder *e) {
+    EncBatch *b = nullptr;
+    if (!e->spare.empty()) {
+        b = e->spare.back();
+        e->spare.pop_back();
+        if (b->done) (void)hipEventSynchronize(b->done);  // the GPU is done with it
+    } else {
+        b = new EncBatch();
+        const size_t wb = (size_t)e->batch * e->wbytes;
+        ssize_t rc = pinned_alloc(wb + (size_t)e->batch * 4, b->mem);
+        if (rc) {
+            delete b;
+            return rc;
+        }
+        b->S = reinterpret_cast<uint32_t *>(b->mem.host + wb);
+        b->S_dev = reinterpret_cast<uint32_t *>(b->mem.dev + wb);
+        if (hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess) {
+            pinned_free(b->mem);
+            delete b;
+            return FECGPU_ERR_DEVICE;
+        }
+        b->released.assign(e->batch, 0);
+        e->all.push_back(b);
+    }
+    b->first = e->next_win;
+    b->nwin = 0;
+    b->live = 0;
+    b->launched = false;
+    std::fill(b->released.begin(), b->released.end(), 0);
+    e->cur = b;
+    e->active.push_back(b);
+    return 0;
 }
 
-void close_window(fecgpu_encoder *e) {
-    const int k = e->code.k, r = e->code.r;
-    const bool lp = is_lenprefix(e->code);
-    uint32_t mx = 0;
-    for (auto &p : e->open) mx = std::max<uint32_t>(mx, (uint32_t)p.size());
-    EncWin w;
-    w.id = e->next_win++;
-    w.S = lp ? 2 + mx : std::max<uint32_t>(mx, 1);
-    const uint32_t st = rup16(w.S);
-    w.sym.assign((size_t)(k + r) * st, 0);
-    for (int j = 0; j < (int)e->open.size(); j++) {
-        uint8_t *s = w.sym.data() + (size_t)j * st;
-        const auto &p = e->open[j];
-        if (lp) {
-            s[0] = (uint8_t)(p.size() >> 8);
-            s[1] = (uint8_t)p.size();
-            std::memcpy(s + 2, p.data(), p.size());
-        } else {
-            std::memcpy(s, p.data(), p.size());
-        }
+// Encode the current batch's closed windows on the encoder's stream (async).
+ssize_t enc_launch(fecgpu_encoder *e) {
+    EncBatch *b = e->cur;
+    if (!b || b->nwin == 0) return 0;
+    BatchArgs a{};
+    a.win = b->mem.dev;
+    a.sym_len = b->S_dev;
+    a.stride = e->stride;
+    a.nwin = b->nwin;
+    ssize_t rc = fecgpu::launch_batch(e->ctx, &e->code, false, a, e->stream);
+    if (rc) return rc;
+    DevGuard g(e->dev);
+    if (hipEventRecord(b->done, e->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
+    b->launched = true;
+    e->cur = nullptr;
+    if (b->live == 0) {  // every window already released (never read): recycle
+        e->active.pop_back();
+        e->spare.push_back(b);
     }
-    e->open.clear();
-    e->pending.push_back(std::move(w));
+    return (ssize_t)b->nwin;
+}
+
+uint8_t *enc_row(fecgpu_encoder *e, EncBatch *b, uint32_t slot, int row) {
+    return b->mem.host + (size_t)slot * e->wbytes + (size_t)row * e->stride;
+}
+
+ssize_t enc_close(fecgpu_encoder *e) {
+    const int k = e->code.k;
+    const bool lp = is_lenprefix(e->code);
+    EncBatch *b = e->cur;
+    const uint32_t slot = b->nwin;
+    if (!lp && e->open_n < k) {  // FIXED: missing sources are zero packets of length L
+        const uint32_t L = e->open_len[0];
+        for (int j = e->open_n; j < k; j++) e->open_len[j] = L;
+    }
+    const uint32_t S = lp ? 2 + e->open_max : std::max<uint32_t>(e->open_max, 1);
+    const uint32_t S16 = rup16(S);
+    for (int j = 0; j < k; j++) {
+        uint8_t *row = enc_row(e, b, slot, j);
+        uint32_t used = 0;
+        if (j < e->open_n) used = lp ? 2 + e->open_len[j] : e->open_len[j];
+        // zero padding of the symbol (and of its last 16-byte column)
+        std::memset(row + used, 0, S16 - used);
+    }
+    b->S[slot] = S;
+    b->nwin++;
+    b->live++;
+    e->next_win++;
+    e->open_n = 0;
+    e->open_max = 0;
+    if (b->nwin == e->batch) {
+        ssize_t rc = enc_launch(e);
+        if (rc < 0) return rc;
+    }
+    return 0;
+}
+
+EncBatch *enc_find(fecgpu_encoder *e, uint64_t win, uint32_t &slot) {
+    // active batches cover increasing, contiguous window ranges
+    auto it = std::upper_bound(e->active.begin(), e->active.end(), win,
+                               [](uint64_t w, const EncBatch *b) { return w < b->first; });
+    if (it == e->active.begin()) return nullptr;
+    EncBatch *b = *(it - 1);
+    if (win >= b->first + b->nwin) return nullptr;
+    slot = (uint32_t)(win - b->first);
+    return b;
 }
 
 }  // namespace
@@ -116,121 +235,194 @@ ssize_t fecgpu_encoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t ma
     e->code = *code;
     e->max_len = max_len;
     e->batch = batch;
+    e->stride = rup16(max_len + (is_lenprefix(*code) ? 2 : 0));
+    e->wbytes = (size_t)(code->k + code->r) * e->stride;
+    e->dev = ctx_device();
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return FECGPU_ERR_DEVICE;
+    }
     *out = e;
     return 0;
 }
 
-void fecgpu_encoder_free(fecgpu_encoder *enc) { delete enc; }
-
-ssize_t fecgpu_encoder_flush(fecgpu_encoder *e) {
-    if (!e) return FECGPU_ERR_INVALID_ARG;
-    const int n = e->code.k + e->code.r;
-    std::vector<uint64_t> off, pres;
-    std::vector<uint32_t> len;
-    std::vector<uint8_t> buf, status;
-    uint64_t pos = 0;
-    for (auto &w : e->pending) {
-        off.push_back(pos);
-        len.push_back(w.S);
-        pos += (uint64_t)n * rup16(w.S);
+void fecgpu_encoder_free(fecgpu_encoder *e) {
+    if (!e) return;
+    DevGuard g(e->dev);
+    (void)hipStreamSynchronize(e->stream);
+    for (EncBatch *b : e->all) {
+        if (b->done) (void)hipEventDestroy(b->done);
+        pinned_free(b->mem);
+        delete b;
     }
-    buf.resize(pos);
-    for (size_t i = 0; i < e->pending.size(); i++)
-        std::memcpy(buf.data() + off[i], e->pending[i].sym.data(), e->pending[i].sym.size());
-    ssize_t rc = run_host_batch(e->ctx, e->code, false, buf, off, len, pres, status);
-    if (rc < 0) return rc;
-    const ssize_t nw = (ssize_t)e->pending.size();
-    for (size_t i = 0; i < e->pending.size(); i++) {
-        EncWin &w = e->pending[i];
-        std::memcpy(w.sym.data(), buf.data() + off[i], w.sym.size());
-        const uint64_t id = w.id;
-        e->done[id] = std::move(w);
-    }
-    e->pending.clear();
-    return nw;
+    (void)hipStreamDestroy(e->stream);
+    delete e;
 }
 
 ssize_t fecgpu_encoder_add_source(fecgpu_encoder *e, const uint8_t *pkt, size_t len,
                                   uint64_t *win, uint16_t *idx) {
     if (!e || (!pkt && len)) return FECGPU_ERR_INVALID_ARG;
     if (len > e->max_len) return FECGPU_ERR_BUFFER_TOO_SHORT;
-    if (!is_lenprefix(e->code)) {
+    const bool lp = is_lenprefix(e->code);
+    if (!lp) {
         if (len == 0) return FECGPU_ERR_INVALID_ARG;
-        if (!e->open.empty() && e->open[0].size() != len) return FECGPU_ERR_INVALID_ARG;
+        if (e->open_n && e->open_len[0] != len) return FECGPU_ERR_INVALID_ARG;
+    }
+    if (!e->cur) {
+        ssize_t rc = enc_take_batch(e);
+        if (rc) return rc;
+    }
+    uint8_t *row = enc_row(e, e->cur, e->cur->nwin, e->open_n);
+    if (lp) {
+        row[0] = (uint8_t)(len >> 8);
+        row[1] = (uint8_t)len;
+        if (len) std::memcpy(row + 2, pkt, len);
+    } else {
+        std::memcpy(row, pkt, len);
     }
     if (win) *win = e->next_win;
-    if (idx) *idx = (uint16_t)e->open.size();
-    e->open.emplace_back(pkt, pkt + len);
-    if ((int)e->open.size() == e->code.k) {
-        close_window(e);
-        if (e->pending.size() >= e->batch) {
-            ssize_t rc = fecgpu_encoder_flush(e);
-            if (rc < 0) return rc;
-        }
+    if (idx) *idx = (uint16_t)e->open_n;
+    e->open_len[e->open_n++] = (uint32_t)len;
+    e->open_max = std::max<uint32_t>(e->open_max, (uint32_t)len);
+    if (e->open_n == e->code.k) {
+        ssize_t rc = enc_close(e);
+        if (rc < 0) return rc;
     }
     return 0;
 }
 
 ssize_t fecgpu_encoder_close_window(fecgpu_encoder *e) {
     if (!e) return FECGPU_ERR_INVALID_ARG;
-    if (e->open.empty()) return FECGPU_ERR_DONE;
-    const size_t L = e->open[0].size();
-    while ((int)e->open.size() < e->code.k)
-        e->open.emplace_back(is_lenprefix(e->code) ? 0 : L, 0);  // zero padding symbols
-    close_window(e);
-    return (ssize_t)(e->next_win - 1);
+    if (e->open_n == 0) return FECGPU_ERR_DONE;
+    const uint64_t id = e->next_win;
+    ssize_t rc = enc_close(e);  // missing sources become empty (zero) packets
+    return rc < 0 ? rc : (ssize_t)id;
+}
+
+ssize_t fecgpu_encoder_flush(fecgpu_encoder *e) {
+    if (!e) return FECGPU_ERR_INVALID_ARG;
+    ssize_t n = enc_launch(e);
+    if (n < 0) return n;
+    DevGuard g(e->dev);
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
+    return n;
 }
 
 ssize_t fecgpu_encoder_repair(fecgpu_encoder *e, uint64_t win, uint16_t i, uint8_t *out,
                               size_t cap) {
     if (!e || i >= e->code.r) return FECGPU_ERR_INVALID_ARG;
-    auto it = e->done.find(win);
-    if (it == e->done.end()) return win <= e->next_win ? FECGPU_ERR_DONE : FECGPU_ERR_INVALID_ARG;
-    const EncWin &w = it->second;
-    if (!out || cap < w.S) return FECGPU_ERR_BUFFER_TOO_SHORT;
-    std::memcpy(out, w.sym.data() + (size_t)(e->code.k + i) * rup16(w.S), w.S);
-    return (ssize_t)w.S;
+    uint32_t slot = 0;
+    EncBatch *b = enc_find(e, win, slot);
+    if (!b || b->released[slot]) return win <= e->next_win ? FECGPU_ERR_DONE : FECGPU_ERR_INVALID_ARG;
+    if (!b->launched) return FECGPU_ERR_DONE;  // not encoded yet
+    if (hipEventQuery(b->done) != hipSuccess) {
+        DevGuard g(e->dev);
+        if (hipEventSynchronize(b->done) != hipSuccess) return FECGPU_ERR_DEVICE;
+    }
+    const uint32_t S = b->S[slot];
+    if (!out || cap < S) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    std::memcpy(out, enc_row(e, b, slot, e->code.k + i), S);
+    return (ssize_t)S;
 }
 
 ssize_t fecgpu_encoder_release(fecgpu_encoder *e, uint64_t win) {
     if (!e) return FECGPU_ERR_INVALID_ARG;
-    return e->done.erase(win) ? 0 : FECGPU_ERR_DONE;
-}
-
-// ------------------------------------------------------------- decoder ---
-
-ssize_t fecgpu_decoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t max_len,
-                           uint32_t batch, fecgpu_decoder **out) {
-    if (!ctx || !out || max_len == 0 || batch == 0) return FECGPU_ERR_INVALID_ARG;
-    ssize_t rc = fecgpu_code_check(code);
-    if (rc) return rc;
-    if (is_lenprefix(*code) && max_len > 65535) return FECGPU_ERR_INVALID_ARG;
-    auto *d = new fecgpu_decoder();
-    d->ctx = ctx;
-    d->code = *code;
-    d->max_len = max_len;
-    d->batch = batch;
-    *out = d;
+    uint32_t slot = 0;
+    EncBatch *b = enc_find(e, win, slot);
+    if (!b || !b->launched || b->released[slot]) return FECGPU_ERR_DONE;
+    b->released[slot] = 1;
+    if (--b->live == 0) {
+        e->active.erase(std::find(e->active.begin(), e->active.end(), b));
+        e->spare.push_back(b);
+    }
     return 0;
 }
 
-void fecgpu_decoder_free(fecgpu_decoder *d) { delete d; }
+}  // extern "C"
 
-static DecWin &dwin(fecgpu_decoder *d, uint64_t win) {
-    DecWin &w = d->wins[win];
-    if (w.src.empty()) {
-        w.src.resize(d->code.k);
-        w.rep.resize(d->code.r);
-        w.plen.assign(d->code.k, 0);
+// ------------------------------------------------------------ decoder ---
+namespace {
+
+struct DecSlot {
+    uint64_t win = 0;
+    uint64_t present = 0;  // bit i: symbol i held (received or recovered)
+    uint32_t S = 0;        // known once a repair (or FIXED source) arrives
+    bool used = false;
+    bool cand = false;     // touched since the last flush
+};
+
+constexpr uint32_t kSlotsPerChunk = 256;
+
+}  // namespace
+
+struct fecgpu_decoder {
+    fecgpu_ctx *ctx = nullptr;
+    fecgpu_code code{};
+    uint32_t max_len = 0, batch = 0, stride = 0;
+    size_t wbytes = 0;
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    std::vector<Pinned> chunks;        // kSlotsPerChunk windows each
+    std::vector<DecSlot> slots;
+    std::vector<uint32_t> plen;        // [slot * k + j] payload length
+    std::vector<uint32_t> free_slots;
+    std::unordered_map<uint64_t, uint32_t> map;
+    std::vector<uint32_t> cand;
+    Pinned arg;                        // flush arrays: off, S, present, status
+    size_t arg_cap = 0;
+    uint64_t dirty = 0;
+};
+
+namespace {
+
+uint8_t *dec_row(fecgpu_decoder *d, uint32_t s, int row) {
+    return d->chunks[s / kSlotsPerChunk].host + (size_t)(s % kSlotsPerChunk) * d->wbytes +
+           (size_t)row * d->stride;
+}
+uint64_t dec_dev_addr(fecgpu_decoder *d, uint32_t s) {
+    return reinterpret_cast<uint64_t>(d->chunks[s / kSlotsPerChunk].dev) +
+           (uint64_t)(s % kSlotsPerChunk) * d->wbytes;
+}
+
+ssize_t dec_slot(fecgpu_decoder *d, uint64_t win, uint32_t &out) {
+    auto it = d->map.find(win);
+    if (it != d->map.end()) {
+        out = it->second;
+        return 0;
     }
-    return w;
+    if (d->free_slots.empty()) {
+        Pinned p;
+        ssize_t rc = pinned_alloc((size_t)kSlotsPerChunk * d->wbytes, p);
+        if (rc) return rc;
+        const uint32_t base = (uint32_t)d->slots.size();
+        d->chunks.push_back(p);
+        d->slots.resize(base + kSlotsPerChunk);
+        d->plen.resize((size_t)(base + kSlotsPerChunk) * d->code.k, 0);
+        for (uint32_t i = kSlotsPerChunk; i-- > 0;) d->free_slots.push_back(base + i);
+    }
+    const uint32_t s = d->free_slots.back();
+    d->free_slots.pop_back();
+    DecSlot &w = d->slots[s];
+    w = DecSlot{};
+    w.win = win;
+    w.used = true;
+    d->map.emplace(win, s);
+    out = s;
+    return 0;
+}
+
+void dec_touch(fecgpu_decoder *d, uint32_t s) {
+    if (!d->slots[s].cand) {
+        d->slots[s].cand = true;
+        d->cand.push_back(s);
+    }
 }
 
 // decodable now: some missing source can be recovered by the next flush
-static bool decodable(const fecgpu_code &c, const DecWin &w) {
+bool decodable(const fecgpu_code &c, const DecSlot &w) {
     const int k = c.k, r = c.r;
     if (w.S == 0) return false;
-    const uint64_t kmask = (1ull << k) - 1;
+    const uint64_t kmask = (k >= 64) ? ~0ull : (1ull << k) - 1;
     const uint64_t miss = ~w.present & kmask;
     if (!miss) return false;
     if (c.scheme == FECGPU_SCHEME_GF256)
@@ -243,60 +435,129 @@ static bool decodable(const fecgpu_code &c, const DecWin &w) {
     return false;
 }
 
+}  // namespace
+
+extern "C" {
+
+ssize_t fecgpu_decoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t max_len,
+                           uint32_t batch, fecgpu_decoder **out) {
+    if (!ctx || !out || max_len == 0 || batch == 0) return FECGPU_ERR_INVALID_ARG;
+    ssize_t rc = fecgpu_code_check(code);
+    if (rc) return rc;
+    if (is_lenprefix(*code) && max_len > 65535) return FECGPU_ERR_INVALID_ARG;
+    auto *d = new fecgpu_decoder();
+    d->ctx = ctx;
+    d->code = *code;
+    d->max_len = max_len;
+    d->batch = batch;
+    d->stride = rup16(max_len + (is_lenprefix(*code) ? 2 : 0));
+    d->wbytes = (size_t)(code->k + code->r) * d->stride;
+    d->dev = ctx_device();
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete d;
+        return FECGPU_ERR_DEVICE;
+    }
+    *out = d;
+    return 0;
+}
+
+void fecgpu_decoder_free(fecgpu_decoder *d) {
+    if (!d) return;
+    DevGuard g(d->dev);
+    (void)hipStreamSynchronize(d->stream);
+    for (Pinned &p : d->chunks) pinned_free(p);
+    pinned_free(d->arg);
+    (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
 ssize_t fecgpu_decoder_flush(fecgpu_decoder *d) {
     if (!d) return FECGPU_ERR_INVALID_ARG;
-    const int k = d->code.k, r = d->code.r, n = k + r;
+    const int k = d->code.k, r = d->code.r;
     const bool lp = is_lenprefix(d->code);
-    std::vector<uint64_t> ids, off, pres;
-    std::vector<uint32_t> len;
-    uint64_t pos = 0;
-    for (auto &kv : d->wins) {
-        if (!decodable(d->code, kv.second)) continue;
-        ids.push_back(kv.first);
-        off.push_back(pos);
-        len.push_back(kv.second.S);
-        pres.push_back(kv.second.present);
-        pos += (uint64_t)n * rup16(kv.second.S);
+    std::vector<uint32_t> sel;
+    for (uint32_t s : d->cand) {
+        DecSlot &w = d->slots[s];
+        if (!w.cand) continue;  // released (or a duplicate entry) since
+        w.cand = false;
+        if (w.used && decodable(d->code, w)) sel.push_back(s);
     }
-    std::vector<uint8_t> buf(pos, 0), status(ids.size(), 0);
-    for (size_t i = 0; i < ids.size(); i++) {
-        DecWin &w = d->wins[ids[i]];
-        const uint32_t st = rup16(w.S);
-        for (int j = 0; j < k; j++)
-            if ((w.present >> j) & 1) std::memcpy(buf.data() + off[i] + (size_t)j * st, w.src[j].data(), w.S);
-        for (int t = 0; t < r; t++)
-            if ((w.present >> (k + t)) & 1)
-                std::memcpy(buf.data() + off[i] + (size_t)(k + t) * st, w.rep[t].data(), w.S);
+    d->cand.clear();
+    d->dirty = 0;
+    if (sel.empty()) return 0;
+    DevGuard g(d->dev);
+    const size_t n = sel.size();
+    // per-window arguments in pinned memory the kernel reads directly
+    const size_t o_len = (n * 8 + 255) & ~size_t(255), o_pres = o_len + ((n * 4 + 255) & ~size_t(255));
+    const size_t o_stat = o_pres + n * 8, need = o_stat + n;
+    if (d->arg_cap < need) {
+        pinned_free(d->arg);
+        d->arg_cap = 0;
+        ssize_t rc = pinned_alloc(std::max(need, (size_t)64 << 10) * 2, d->arg);
+        if (rc) return rc;
+        d->arg_cap = d->arg.bytes;
     }
-    ssize_t rc = run_host_batch(d->ctx, d->code, true, buf, off, len, pres, status);
-    if (rc < 0) return rc;
+    uint64_t *off = reinterpret_cast<uint64_t *>(d->arg.host);
+    uint32_t *len = reinterpret_cast<uint32_t *>(d->arg.host + o_len);
+    uint64_t *pres = reinterpret_cast<uint64_t *>(d->arg.host + o_pres);
+    uint8_t *status = d->arg.host + o_stat;
+    const uint64_t base = reinterpret_cast<uint64_t>(d->chunks[0].dev);
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t s = sel[i];
+        const DecSlot &w = d->slots[s];
+        if (lp) {  // zero padding of the received sources up to S (A.3)
+            const uint32_t S16 = rup16(w.S);
+            for (int j = 0; j < k; j++)
+                if ((w.present >> j) & 1) {
+                    const uint32_t used = 2 + d->plen[(size_t)s * k + j];
+                    std::memset(dec_row(d, s, j) + used, 0, S16 - used);
+                }
+        }
+        off[i] = dec_dev_addr(d, s) - base;  // wraps for chunks below the first
+        len[i] = w.S;
+        pres[i] = w.present;
+        status[i] = 0xFF;
+    }
+    BatchArgs a{};
+    a.win = d->chunks[0].dev;
+    a.win_off = reinterpret_cast<const uint64_t *>(d->arg.dev);
+    a.sym_len = reinterpret_cast<const uint32_t *>(d->arg.dev + o_len);
+    a.present = reinterpret_cast<const uint64_t *>(d->arg.dev + o_pres);
+    a.status = d->arg.dev + o_stat;
+    a.stride = d->stride;
+    a.off_stride = d->stride;
+    a.nwin = n;
+    ssize_t rc = fecgpu::launch_batch(d->ctx, &d->code, true, a, d->stream);
+    if (rc) return rc;
+    if (hipStreamSynchronize(d->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
     ssize_t recovered = 0;
-    for (size_t i = 0; i < ids.size(); i++) {
-        DecWin &w = d->wins[ids[i]];
-        const uint32_t st = rup16(w.S);
-        const uint64_t kmask = (1ull << k) - 1;
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t s = sel[i];
+        DecSlot &w = d->slots[s];
+        uint64_t got_mask = 0;
         for (int j = 0; j < k; j++) {
             if ((w.present >> j) & 1) continue;
             // XOR windows recover group by group; a source is valid iff its group was solvable
             bool got = status[i] == FECGPU_STATUS_OK;
             if (!got && d->code.scheme == FECGPU_SCHEME_XOR) {
-                const int g = j % r;
+                const int grp = j % r;
                 int nm = 0;
-                for (int x = g; x < k; x += r) nm += !((w.present >> x) & 1);
-                got = nm == 1 && ((w.present >> (k + g)) & 1);
+                for (int x = grp; x < k; x += r) nm += !((w.present >> x) & 1);
+                got = nm == 1 && ((w.present >> (k + grp)) & 1);
             }
             if (!got) continue;
-            const uint8_t *s = buf.data() + off[i] + (size_t)j * st;
-            w.src[j].assign(s, s + w.S);
-            w.plen[j] = lp ? (((uint32_t)s[0] << 8) | s[1]) : w.S;
-            if (lp && w.plen[j] + 2 > w.S) w.plen[j] = w.S - 2;  // corrupt prefix: clamp
+            uint32_t pl = w.S;
+            if (lp) {
+                const uint8_t *row = dec_row(d, s, j);
+                pl = ((uint32_t)row[0] << 8) | row[1];
+                if (pl + 2 > w.S) pl = w.S - 2;  // corrupt prefix: clamp
+            }
+            d->plen[(size_t)s * k + j] = pl;
+            got_mask |= 1ull << j;
             recovered++;
         }
-        for (int j = 0; j < k; j++)
-            if (!w.src[j].empty()) w.present |= 1ull << j;
-        (void)kmask;
+        w.present |= got_mask;
     }
-    d->dirty = 0;
     return recovered;
 }
 
@@ -304,27 +565,25 @@ ssize_t fecgpu_decoder_add_source(fecgpu_decoder *d, uint64_t win, uint16_t idx,
                                   size_t len) {
     if (!d || idx >= d->code.k || (!pkt && len)) return FECGPU_ERR_INVALID_ARG;
     if (len > d->max_len) return FECGPU_ERR_BUFFER_TOO_SHORT;
-    DecWin &w = dwin(d, win);
+    uint32_t s = 0;
+    ssize_t rc = dec_slot(d, win, s);
+    if (rc) return rc;
+    DecSlot &w = d->slots[s];
     if ((w.present >> idx) & 1) return FECGPU_ERR_DONE;  // duplicate
-    const bool lp = is_lenprefix(d->code);
-    std::vector<uint8_t> sym;
-    if (lp) {
-        sym.assign(2 + len, 0);
-        sym[0] = (uint8_t)(len >> 8);
-        sym[1] = (uint8_t)len;
-        if (len) std::memcpy(sym.data() + 2, pkt, len);
+    uint8_t *row = dec_row(d, s, idx);
+    if (is_lenprefix(d->code)) {
+        if (w.S && 2 + len > w.S) return FECGPU_ERR_INVALID_ARG;
+        row[0] = (uint8_t)(len >> 8);
+        row[1] = (uint8_t)len;
+        if (len) std::memcpy(row + 2, pkt, len);
     } else {
         if (w.S && len != w.S) return FECGPU_ERR_INVALID_ARG;
-        sym.assign(pkt, pkt + len);
+        std::memcpy(row, pkt, len);
         w.S = (uint32_t)len;
     }
-    if (w.S) {
-        if (sym.size() > w.S) return FECGPU_ERR_INVALID_ARG;
-        sym.resize(w.S, 0);
-    }
-    w.src[idx] = std::move(sym);
-    w.plen[idx] = (uint32_t)len;
+    d->plen[(size_t)s * d->code.k + idx] = (uint32_t)len;
     w.present |= 1ull << idx;
+    dec_touch(d, s);
     if (++d->dirty >= (uint64_t)d->batch * d->code.k) return fecgpu_decoder_flush(d) < 0 ? FECGPU_ERR_DEVICE : 0;
     return 0;
 }
@@ -333,21 +592,22 @@ ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *d, uint64_t win, uint16_t idx,
                                   size_t len) {
     if (!d || idx >= d->code.r || !sym || len == 0) return FECGPU_ERR_INVALID_ARG;
     if (len > (size_t)d->max_len + (is_lenprefix(d->code) ? 2 : 0)) return FECGPU_ERR_BUFFER_TOO_SHORT;
-    DecWin &w = dwin(d, win);
+    uint32_t s = 0;
+    ssize_t rc = dec_slot(d, win, s);
+    if (rc) return rc;
+    DecSlot &w = d->slots[s];
     const int k = d->code.k;
     if ((w.present >> (k + idx)) & 1) return FECGPU_ERR_DONE;
     if (w.S && w.S != len) return FECGPU_ERR_INVALID_ARG;
     if (!w.S) {
-        // LENPREFIX: the repair length fixes S; pad sources received so far
-        for (int j = 0; j < k; j++) {
-            if (!((w.present >> j) & 1)) continue;
-            if (w.src[j].size() > len) return FECGPU_ERR_INVALID_ARG;
-            w.src[j].resize(len, 0);
-        }
+        // LENPREFIX: the repair length fixes S; sources received so far must fit
+        for (int j = 0; j < k; j++)
+            if (((w.present >> j) & 1) && 2 + d->plen[(size_t)s * k + j] > len) return FECGPU_ERR_INVALID_ARG;
         w.S = (uint32_t)len;
     }
-    w.rep[idx].assign(sym, sym + len);
+    std::memcpy(dec_row(d, s, k + idx), sym, len);
     w.present |= 1ull << (k + idx);
+    dec_touch(d, s);
     if (++d->dirty >= (uint64_t)d->batch * d->code.k) return fecgpu_decoder_flush(d) < 0 ? FECGPU_ERR_DEVICE : 0;
     return 0;
 }
@@ -355,19 +615,25 @@ ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *d, uint64_t win, uint16_t idx,
 ssize_t fecgpu_decoder_recovered(fecgpu_decoder *d, uint64_t win, uint16_t idx, uint8_t *out,
                                  size_t cap) {
     if (!d || idx >= d->code.k) return FECGPU_ERR_INVALID_ARG;
-    auto it = d->wins.find(win);
-    if (it == d->wins.end() || !((it->second.present >> idx) & 1)) return FECGPU_ERR_DONE;
-    const DecWin &w = it->second;
-    const uint32_t n = w.plen[idx];
+    auto it = d->map.find(win);
+    if (it == d->map.end() || !((d->slots[it->second].present >> idx) & 1)) return FECGPU_ERR_DONE;
+    const uint32_t s = it->second;
+    const uint32_t n = d->plen[(size_t)s * d->code.k + idx];
     if (cap < n || (!out && n)) return FECGPU_ERR_BUFFER_TOO_SHORT;
-    const uint8_t *s = w.src[idx].data() + (is_lenprefix(d->code) ? 2 : 0);
-    if (n) std::memcpy(out, s, n);
+    if (n) std::memcpy(out, dec_row(d, s, idx) + (is_lenprefix(d->code) ? 2 : 0), n);
     return (ssize_t)n;
 }
 
 ssize_t fecgpu_decoder_release(fecgpu_decoder *d, uint64_t win) {
     if (!d) return FECGPU_ERR_INVALID_ARG;
-    return d->wins.erase(win) ? 0 : FECGPU_ERR_DONE;
+    auto it = d->map.find(win);
+    if (it == d->map.end()) return FECGPU_ERR_DONE;
+    DecSlot &w = d->slots[it->second];
+    w.used = false;
+    w.cand = false;
+    d->free_slots.push_back(it->second);
+    d->map.erase(it);
+    return 0;
 }
 
 }  // extern "C"

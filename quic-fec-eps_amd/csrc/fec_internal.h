@@ -6,6 +6,7 @@
 
 #include <algorithm>
 
+#include "../../include/fecgpu.h"
 #include "fec_spec.h"
 
 namespace fecgpu {
@@ -39,6 +40,9 @@ struct BatchArgs {
     // input address p: 0 in place; the host pipeline points it at the caller's
     // pinned host windows so outputs cross PCIe straight from the kernel.
     uint64_t out_delta;
+    // ragged layout (win_off): symbol pitch of every window; 0 = packed
+    // round_up(S_w, 16)
+    uint32_t off_stride;
 };
 
 struct LaunchPlan {
@@ -55,6 +59,14 @@ struct LaunchPlan {
 inline uint32_t gf_dec_win_lds(int k, int R) { return (uint32_t)(k * R * 20 + 80 + 15) & ~15u; }
 
 hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s);
+
+// Library-internal entry (fec_conn.cpp): plan and launch one batch whose
+// pointers the device can address (device memory or mapped pinned host
+// memory) on `s`, on the ctx's device; asynchronous.  Geometry fields of `a`
+// (win, win_off, sym_len, S_all, stride, off_stride, nwin, present, status)
+// are the caller's; the rest is filled in.
+ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
+                     hipStream_t s);
 hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s);
 
 struct SynthArgs {

@@ -186,8 +186,14 @@ __device__ __forceinline__ void win_geom(const BatchArgs &a, uint64_t w, uint64_
                                          uint32_t &stride, uint32_t &S) {
     S = a.sym_len ? a.sym_len[w] : a.S_all;
     if (a.win_off) {
+        // 64-bit wrap-around add: offsets may point below `win` (pooled windows)
         base = reinterpret_cast<uint64_t>(a.win) + a.win_off[w];
-        stride = (S + 15u) & ~15u;
+        if (a.off_stride) {
+            stride = a.off_stride;
+            S = min(S, stride);  // a symbol never spills into the next row
+        } else {
+            stride = (S + 15u) & ~15u;
+        }
     } else {
         base = reinterpret_cast<uint64_t>(a.win) + w * (uint64_t)(a.k + a.r) * a.stride;
         stride = a.stride;
