@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--grid-mult", type=int, default=0, help="tuning: persistent grid multiplier")
     ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
     ap.add_argument("--bpc", type=int, default=0, help="tuning: persistent workgroups per CU")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1: nccl (= RCCL, one rank per GPU) or gloo (rehearsal: ranks may "
+                         "share a GPU; the reductions run on the host)")
     ap.add_argument("--event-every", type=int, default=4,
                     help="bracket encode/decode with HIP events on every Nth timed step (0 = never): "
                          "each timestamped event costs ~3 us of GPU time, so sampling keeps the "
@@ -131,8 +134,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":  # RCCL: one rank per GPU
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:  # rehearsal of the N>1 path with ranks sharing the box's GPUs
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -212,7 +219,7 @@ def main():
         dec_ms = sum(b.elapsed_time(c) for _, b, c in ev.values()) / len(ev)
 
     log(f"timed {args.steps} steps: {elapsed:.4f} s (encode {enc_ms:.3f} ms, decode {dec_ms:.3f} ms)")
-    elapsed, tot = shard.reduce_run(elapsed, src_bytes, dev)
+    elapsed, tot = shard.reduce_run(elapsed, src_bytes, dev if args.dist_backend == "nccl" else None)
     total_src = float(tot) * args.steps
     value = total_src / elapsed / 1e9
 

@@ -41,6 +41,9 @@ for s in "$@"; do
         bench4) step bench4 600 python bench.py --config 4 --steps 5 --warmup 1 --cpu-seconds 10 ;;
         bench5) step bench5 600 python bench.py --config 5 --steps 10 --warmup 2 --cpu-seconds 0 ;;
         bench6) step bench6 600 python bench.py --config 6 --steps 10 --warmup 2 --cpu-seconds 0 ;;
+        dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                   --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 \
+                   --dist-backend gloo ;;  # N>1 rehearsal: 2 ranks share the box's GPU
         prof2) prof prof2 2 ;;
         prof5) prof prof5 5 ;;
         prof3) prof prof3 3 ;;
