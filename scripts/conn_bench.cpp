@@ -6,8 +6,15 @@
 // reports packets/s and GB/s of payload for each side.
 //   build: g++ -O2 -std=c++17 -o scripts/conn_bench scripts/conn_bench.cpp
 //          -Lquic-fec-eps_amd/lib -lfecgpu -Wl,-rpath,'$ORIGIN/../quic-fec-eps_amd/lib'
-//   run  : scripts/conn_bench <xor|gf256> k r mtu MB loss batch [vary]
+//   run  : scripts/conn_bench <xor|gf256> k r mtu MB loss batch [vary [reorder [dup]]]
+//          vary: LENPREFIX lengths 1..mtu; reorder: symbols arrive shuffled within
+//          blocks of that many windows; dup: fraction of symbols delivered twice.
+// Exit status 3 if a delivered packet differs or the number of unrecovered
+// packets differs from what the loss pattern allows (MDS count for GF, one
+// loss per group with its repair for XOR).
+#include <algorithm>
 #include <chrono>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -45,6 +52,8 @@ int main(int argc, char **argv) {
     const double loss = atof(argv[6]);
     const uint32_t batch = (uint32_t)atoi(argv[7]);
     const bool vary = argc > 8 && atoi(argv[8]);
+    const uint32_t reorder = argc > 9 ? (uint32_t)atoi(argv[9]) : 0;
+    const double dup = argc > 10 ? atof(argv[10]) : 0.0;
     fecgpu_code code{};
     code.scheme = gf ? FECGPU_SCHEME_GF256 : FECGPU_SCHEME_XOR;
     code.matrix = FECGPU_MATRIX_CAUCHY;
@@ -131,7 +140,7 @@ int main(int argc, char **argv) {
     auto t2 = std::chrono::steady_clock::now();
     size_t recovered = 0, missing = 0, bad = 0;
     std::vector<uint8_t> out(mtu);
-    size_t p = 0, q = 0;
+    size_t p = 0, q = 0;  // next packet to file / to deliver
     uint64_t w_done = w_first;  // windows delivered and released
     // hand lost packets of windows < upto to the application, release them
     auto deliver = [&](uint64_t upto) {
@@ -145,19 +154,79 @@ int main(int argc, char **argv) {
         }
         for (; w_done < upto; w_done++) (void)fecgpu_decoder_release(dec, w_done);
     };
-    for (uint64_t w = w_first; w <= w_last; w++) {
-        for (; p < npk && pw[p] == w; p++)
-            if (!lost[p]) CK(fecgpu_decoder_add_source(dec, w, pi[p], &data[off[p]], len[p]));
-        for (int i = 0; i < r; i++) {
-            const size_t s = (w - w_first) * r + i;
-            if (!replost[s]) CK(fecgpu_decoder_add_repair(dec, w, (uint16_t)i, &reps[s * smax], replen[s]));
+    // the sender's short last window: its padding sources are known-empty/zero
+    const int last_n = (int)pi[npk - 1] + 1;
+    std::vector<uint8_t> zpad(mtu, 0);
+    // symbol events: (window, index); index < k source (packet number p), >= k repair
+    struct Ev { uint64_t w; uint32_t i; size_t p; };
+    std::vector<Ev> evs;
+    auto feed = [&](const Ev &e) {
+        ssize_t rc;
+        if (e.i < (uint32_t)k) {
+            if (e.p == SIZE_MAX)
+                rc = fecgpu_decoder_add_source(dec, e.w, (uint16_t)e.i, zpad.data(), vary ? 0 : len[npk - 1]);
+            else
+                rc = fecgpu_decoder_add_source(dec, e.w, (uint16_t)e.i, &data[off[e.p]], len[e.p]);
+        } else {
+            const size_t s = (e.w - w_first) * r + (e.i - k);
+            rc = fecgpu_decoder_add_repair(dec, e.w, (uint16_t)(e.i - k), &reps[s * smax], replen[s]);
+        }
+        if (rc != FECGPU_ERR_DONE) CK(rc);  // DONE: a duplicate
+    };
+    const uint32_t blk = reorder ? reorder : 1;
+    for (uint64_t w0 = w_first; w0 <= w_last; w0 += blk) {
+        evs.clear();
+        const uint64_t w1 = std::min<uint64_t>(w_last + 1, w0 + blk);
+        for (uint64_t w = w0; w < w1; w++) {
+            for (; p < npk && pw[p] == w; p++)
+                if (!lost[p]) evs.push_back({w, pi[p], p});
+            if (w == w_last)
+                for (int i = last_n; i < k; i++) evs.push_back({w, (uint32_t)i, SIZE_MAX});
+            for (int i = 0; i < r; i++)
+                if (!replost[(w - w_first) * r + i]) evs.push_back({w, (uint32_t)(k + i), 0});
+        }
+        if (reorder)
+            for (size_t i = evs.size(); i > 1; i--) {
+                ch = sm64(ch);
+                std::swap(evs[i - 1], evs[ch % i]);
+            }
+        for (const Ev &e : evs) {
+            feed(e);
+            if (dup > 0) {
+                ch = sm64(ch);
+                if ((double)(ch >> 11) * 0x1.0p-53 < dup) feed(e);
+            }
         }
         // auto-flushes run every batch*k symbols; windows 3 batches back are final
-        if (w >= w_first + 3 * (uint64_t)batch && (w - w_first) % batch == 0) deliver(w - 3 * (uint64_t)batch);
+        const uint64_t lag = 3 * (uint64_t)batch + blk;
+        if (w1 > w_first + lag) deliver(w1 - lag);
     }
     CK(fecgpu_decoder_flush(dec));
     deliver(w_last + 1);
     auto t3 = std::chrono::steady_clock::now();
+
+    // what the loss pattern allows
+    size_t expect_missing = 0;
+    for (size_t a = 0, b = 0; a < npk; a = b) {
+        const uint64_t w = pw[a];
+        while (b < npk && pw[b] == w) b++;
+        std::vector<int> lo(k, 0);
+        for (size_t t = a; t < b; t++) lo[pi[t]] = lost[t];
+        int nl = 0;
+        for (int j = 0; j < k; j++) nl += lo[j];
+        const uint8_t *rl = &replost[(w - w_first) * r];
+        if (gf) {
+            int rp = 0;
+            for (int i = 0; i < r; i++) rp += !rl[i];
+            if (nl > rp) expect_missing += nl;
+        } else {
+            for (int g = 0; g < r; g++) {
+                int ng = 0;
+                for (int j = g; j < k; j += r) ng += lo[j];
+                if (!(ng == 1 && !rl[g])) expect_missing += ng;
+            }
+        }
+    }
 
     const double ts = std::chrono::duration<double>(t1 - t0).count();
     const double tr = std::chrono::duration<double>(t3 - t2).count();
@@ -166,12 +235,13 @@ int main(int argc, char **argv) {
     printf("{\"what\": \"per-connection encoder/decoder (C ABI, packet by packet)\", "
            "\"scheme\": \"%s\", \"k\": %d, \"r\": %d, \"mtu\": %u, \"vary\": %d, \"batch\": %u, "
            "\"bytes\": %zu, \"packets\": %zu, \"loss\": %.3f, \"lost\": %zu, \"recovered\": %zu, "
-           "\"unrecovered\": %zu, \"corrupt\": %zu, \"send_s\": %.4f, \"recv_s\": %.4f, "
+           "\"unrecovered\": %zu, \"expected_unrecovered\": %zu, \"reorder\": %u, \"dup\": %.3f, "
+           "\"corrupt\": %zu, \"send_s\": %.4f, \"recv_s\": %.4f, "
            "\"send_Mpps\": %.3f, \"recv_Mpps\": %.3f, \"send_GBps\": %.3f, \"recv_GBps\": %.3f}\n",
            gf ? "gf256" : "xor", k, r, mtu, (int)vary, batch, total, npk, loss, lost_n, recovered,
-           missing, bad, ts, tr, npk / ts / 1e6, npk / tr / 1e6, total / ts / 1e9, total / tr / 1e9);
+           missing, expect_missing, reorder, dup, bad, ts, tr, npk / ts / 1e6, npk / tr / 1e6, total / ts / 1e9, total / tr / 1e9);
     fecgpu_encoder_free(enc);
     fecgpu_decoder_free(dec);
     fecgpu_ctx_free(ctx);
-    return bad ? 3 : 0;
+    return (bad || missing != expect_missing) ? 3 : 0;
 }

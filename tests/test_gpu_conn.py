@@ -6,6 +6,8 @@ and the receiver; every packet of every recoverable window must come back
 byte-identical.  (The reference runs this over quiche client<->server on
 loopback; Rust quiche is not available here.)
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -143,3 +145,28 @@ def test_conn_errors(ctx):
     dec = fecgpu.Decoder(ctx, code, max_len=100, batch=4)
     assert dec.add_source(0, 5, b"z" * 10) == fecgpu.ERR_INVALID_ARG  # idx >= k
     assert dec.recovered(0, 1) is None
+
+
+CONN_BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts", "conn_bench")
+
+
+@pytest.mark.parametrize("args", [
+    ["xor", "8", "2", "1200", "48", "0.05", "64"],
+    ["xor", "4", "1", "1000", "16", "0.03", "16", "0", "64", "0.02"],       # reordered + duplicates
+    ["gf256", "16", "4", "1200", "48", "0.08", "128", "1", "33", "0.01"],   # LENPREFIX, reordered
+    ["gf256", "32", "8", "9000", "64", "0.12", "16", "1"],                   # mixed lengths, deep loss
+    ["gf256", "5", "3", "333", "4", "0.2", "3", "0", "7", "0.05"],           # FIXED, short last window
+], ids=["xor-k8r2", "xor-k4r1-reorder-dup", "gf-k16r4-lp-reorder", "gf-k32r8-lp", "gf-k5r3-fixed"])
+def test_native_conn_driver(args):
+    """scripts/conn_bench (C++, per packet through the C ABI): encoder buffers recycle,
+    decoder slots are reused, symbols may arrive reordered and duplicated; every
+    delivered packet is byte-identical and exactly the packets the loss pattern
+    allows are recovered (exit 3 otherwise)."""
+    import json
+    import subprocess
+    assert os.path.exists(CONN_BENCH), "build first: make -C scripts"
+    r = subprocess.run([CONN_BENCH, *args], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["corrupt"] == 0 and res["unrecovered"] == res["expected_unrecovered"]
+    assert res["recovered"] + res["unrecovered"] == res["lost"]
