@@ -439,6 +439,9 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
     // flat slot space when every window has the same geometry (GF decode
     // always plans per window in LDS, so it always runs in group mode)
     p.flat = !win_off && !sym_len && !(decode && scheme == FECGPU_SCHEME_GF256);
+#ifdef FECGPU_FORCE_GROUP
+    p.flat = false;  // A/B knob: group mode for every kernel
+#endif
     a.ncol = (sym_len_all + 15u) >> 4;
     if (!decode) {
         if (scheme == FECGPU_SCHEME_GF256) {

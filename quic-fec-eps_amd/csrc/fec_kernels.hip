@@ -37,7 +37,11 @@
 #define FECGPU_GF_U (R <= 4 ? 2 : 8)
 #endif
 #ifndef FECGPU_GFD_U
-#define FECGPU_GFD_U FECGPU_GF_U  // GF decode: input rows loaded per batch
+// GF decode: input rows loaded per batch.  8 at every r: decode's input rows
+// come through an LDS index (received sources, chosen repairs), so a deeper
+// batch hides that extra latency; cfg3 decode -1.7% vs 2 (scripts/ab.py, r01),
+// cfg4 unchanged (already 8).
+#define FECGPU_GFD_U 8
 #endif
 #ifndef FECGPU_XDEC_ALL
 #define FECGPU_XDEC_ALL 0  // XOR decode: all recoverable groups in one row pass (A/B knob)
