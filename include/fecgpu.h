@@ -119,6 +119,15 @@ ssize_t fecgpu_encode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *w
                             uint32_t sym_len_all, uint32_t stride, uint64_t nwin,
                             uint32_t flags, void *stream);
 
+/* Repair generation with the sender's split layout (SURVEY §8b "encode_batch(
+ * ctx, code, src, repair, sym_len, nwin, flags, stream)", A.4): sources of
+ * window w in src[w][k][stride], repairs written to repair[w][r][stride]
+ * (sources are only read).  Device pointers only (FECGPU_F_HOST_PTRS returns
+ * FECGPU_ERR_UNSUPPORTED).  Returns nwin or a negative error. */
+ssize_t fecgpu_encode_split(fecgpu_ctx *ctx, const fecgpu_code *code, const uint8_t *src,
+                            uint8_t *repair, const uint32_t *sym_len, uint32_t sym_len_all,
+                            uint32_t stride, uint64_t nwin, uint32_t flags, void *stream);
+
 /* Recovery: present[w] bit i = symbol i received.
  * Missing sources are recovered in place; status[w] = FECGPU_STATUS_*.
  * Symbols whose bit is clear are never read.  XOR recovers every group with

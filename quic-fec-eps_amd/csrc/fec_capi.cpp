@@ -418,6 +418,7 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
     const uint32_t sym_len_all = a.S_all, stride = a.stride;
     a.k = k;
     a.r = r;
+    if (!a.wpitch) a.wpitch = (uint64_t)(k + r) * stride;
     for (int g = 0; g < kMaxR; g++) {
         uint64_t m = 0;
         if (g < r)
@@ -613,6 +614,34 @@ ssize_t fecgpu_encode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *w
                             uint32_t flags, void *stream) {
     return run_batch(ctx, code, false, win, win_off, sym_len, sym_len_all, stride, nwin, nullptr,
                      nullptr, flags, stream);
+}
+
+ssize_t fecgpu_encode_split(fecgpu_ctx *ctx, const fecgpu_code *code, const uint8_t *src,
+                            uint8_t *repair, const uint32_t *sym_len, uint32_t sym_len_all,
+                            uint32_t stride, uint64_t nwin, uint32_t flags, void *stream) {
+    if (!ctx || !repair) return FECGPU_ERR_INVALID_ARG;
+    ssize_t rc = validate_batch(code, src, sym_len, sym_len_all, stride, nullptr);
+    if (rc) return rc;
+    if ((reinterpret_cast<uintptr_t>(repair) & 15) != 0) return FECGPU_ERR_INVALID_ARG;
+    if (flags & FECGPU_F_HOST_PTRS) return FECGPU_ERR_UNSUPPORTED;  // device pointers only
+    if (nwin == 0) return 0;
+    const uint64_t k = code->k, r = code->r;
+    BatchArgs a{};
+    // sources of window w at src + w*k*stride; its repair m lands at
+    // repair + w*r*stride + m*stride = (source base) + (k + m)*stride + delta_w
+    a.win = const_cast<uint8_t *>(src);  // never written: encode stores only repairs
+    a.wpitch = k * stride;
+    a.out_delta = reinterpret_cast<uint64_t>(repair) - reinterpret_cast<uint64_t>(src) - k * stride;
+    a.out_wdelta = (r - k) * (uint64_t)stride;  // wraps when r < k
+    a.sym_len = sym_len;
+    a.nwin = nwin;
+    a.S_all = sym_len_all;
+    a.stride = stride;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    rc = launch_device(ctx, code, false, a, s);
+    if (rc) return rc;
+    if (flags & FECGPU_F_SYNC) HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+    return (ssize_t)nwin;
 }
 
 ssize_t fecgpu_decode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *win,

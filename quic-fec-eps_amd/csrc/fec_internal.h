@@ -40,6 +40,8 @@ struct BatchArgs {
     // input address p: 0 in place; the host pipeline points it at the caller's
     // pinned host windows so outputs cross PCIe straight from the kernel.
     uint64_t out_delta;
+    uint64_t out_wdelta;       // encode: + w * out_wdelta (split source / repair arrays)
+    uint64_t wpitch;           // uniform layout: bytes from window w to w + 1 (0: (k + r) * stride)
     // ragged layout (win_off): symbol pitch of every window; 0 = packed
     // round_up(S_w, 16)
     uint32_t off_stride;

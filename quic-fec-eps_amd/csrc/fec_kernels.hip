@@ -199,7 +199,7 @@ __device__ __forceinline__ void win_geom(const BatchArgs &a, uint64_t w, uint64_
             stride = (S + 15u) & ~15u;
         }
     } else {
-        base = reinterpret_cast<uint64_t>(a.win) + w * (uint64_t)(a.k + a.r) * a.stride;
+        base = reinterpret_cast<uint64_t>(a.win) + w * a.wpitch;
         stride = a.stride;
     }
 }
@@ -251,7 +251,7 @@ __device__ __forceinline__ void for_flat_slots(const BatchArgs &a, Body &&body) 
     uint64_t s = xr.cur * kBlock + threadIdx.x;
     uint64_t w = s / ncol;
     uint32_t col = (uint32_t)(s - w * ncol);
-    const uint64_t wbytes = (uint64_t)(a.k + a.r) * a.stride;
+    const uint64_t wbytes = a.wpitch;
     for (; xr.cur < xr.hi; xr.cur += xr.step) {
         // lanes past the end skip the body (measured faster than running a
         // clamped dummy slot to keep control flow uniform: scripts/ab.py, r01)
@@ -476,8 +476,8 @@ __device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t 
 template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
     if constexpr (FLAT) {
-        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t, bool valid) {
-            xor_encode_slot<R>(p, stride, a.k, valid, a.out_delta);
+        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t w, uint32_t, bool valid) {
+            xor_encode_slot<R>(p, stride, a.k, valid, a.out_delta + w * a.out_wdelta);
         });
     } else {
         __shared__ GroupLds g;
@@ -489,8 +489,8 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
             __syncthreads();
             if (threadIdx.x < 64) block_prefix(g.pfx, (int)threadIdx.x < nb ? g.ncol[threadIdx.x] : 0u, threadIdx.x);
             __syncthreads();
-            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int, bool valid) {
-                xor_encode_slot<R>(p, stride, a.k, valid, a.out_delta);
+            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int wl, bool valid) {
+                xor_encode_slot<R>(p, stride, a.k, valid, a.out_delta + (w0 + wl) * a.out_wdelta);
             });
             __syncthreads();
         }
@@ -524,8 +524,8 @@ __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a
     __syncthreads();
 #endif
     if constexpr (FLAT) {
-        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t, uint32_t, bool valid) {
-            gf_encode_slot<R>(p, stride, k, tab, tc, valid, a.out_delta);
+        for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t w, uint32_t, bool valid) {
+            gf_encode_slot<R>(p, stride, k, tab, tc, valid, a.out_delta + w * a.out_wdelta);
         });
     } else {
         __shared__ GroupLds g;
@@ -537,8 +537,8 @@ __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a
             __syncthreads();
             if (threadIdx.x < 64) block_prefix(g.pfx, (int)threadIdx.x < nb ? g.ncol[threadIdx.x] : 0u, threadIdx.x);
             __syncthreads();
-            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int, bool valid) {
-                gf_encode_slot<R>(p, stride, k, tab, tc, valid, a.out_delta);
+            for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int wl, bool valid) {
+                gf_encode_slot<R>(p, stride, k, tab, tc, valid, a.out_delta + (w0 + wl) * a.out_wdelta);
             });
             __syncthreads();
         }
@@ -558,7 +558,7 @@ __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
         uint64_t s = xr.cur * kBlock + threadIdx.x;
         uint64_t w = s / ncol;
         uint32_t col = (uint32_t)(s - w * ncol);
-        const uint64_t wbytes = (uint64_t)(a.k + a.r) * a.stride;
+        const uint64_t wbytes = a.wpitch;
         uint64_t pres = a.present[min(w, a.nwin - 1)];
         for (; xr.cur < xr.hi; xr.cur += xr.step) {
             const uint64_t s_now = s, w_now = w, p_now = pres;

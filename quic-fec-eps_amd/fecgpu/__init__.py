@@ -40,7 +40,7 @@ EXPORTS = (
     "fecgpu_abi_version", "fecgpu_strerror", "fecgpu_last_error", "fecgpu_code_check",
     "fecgpu_ctx_new", "fecgpu_ctx_free", "fecgpu_ctx_set_tuning",
     "fecgpu_host_alloc", "fecgpu_host_free",
-    "fecgpu_encode_batch", "fecgpu_decode_batch",
+    "fecgpu_encode_batch", "fecgpu_encode_split", "fecgpu_decode_batch",
     "fecgpu_synth_batch", "fecgpu_erasure_batch", "fecgpu_digest_batch",
     "fecgpu_encoder_new", "fecgpu_encoder_free", "fecgpu_encoder_add_source",
     "fecgpu_encoder_close_window", "fecgpu_encoder_flush", "fecgpu_encoder_repair",
@@ -121,6 +121,7 @@ def _lib():
             "fecgpu_host_alloc": (sz, [ctypes.c_size_t, ctypes.POINTER(vp)]),
             "fecgpu_host_free": (None, [vp]),
             "fecgpu_encode_batch": (sz, [vp, cp, vp, vp, vp, u32, u32, u64, u32, vp]),
+            "fecgpu_encode_split": (sz, [vp, cp, vp, vp, vp, u32, u32, u64, u32, vp]),
             "fecgpu_decode_batch": (sz, [vp, cp, vp, vp, vp, u32, u32, u64, vp, vp, u32, vp]),
             "fecgpu_synth_batch": (sz, [vp, cp, i32, u64, u64, vp, vp, u32, u32, u64, vp]),
             "fecgpu_erasure_batch": (sz, [vp, cp, i32, u64, u64, vp, u64, vp]),
@@ -258,6 +259,13 @@ class Context:
             self._h, ctypes.byref(code.c), _ptr(win), _ptr(win_off), _ptr(sym_len),
             sym_len_all, stride, nwin, flags, _stream(stream) if not flags & F_HOST_PTRS else None),
             "fecgpu_encode_batch")
+
+    def encode_split(self, code: Code, src, repair, *, nwin: int, stride: int, sym_len=None,
+                     sym_len_all: int = 0, flags: int = 0, stream=None) -> int:
+        """Sources src[w][k][stride] -> repairs repair[w][r][stride] (device memory)."""
+        return _check(_lib().fecgpu_encode_split(
+            self._h, ctypes.byref(code.c), _ptr(src), _ptr(repair), _ptr(sym_len), sym_len_all,
+            stride, nwin, flags, _stream(stream)), "fecgpu_encode_split")
 
     def decode_batch(self, code: Code, win, present, status, *, nwin: int, stride: int,
                      sym_len=None, sym_len_all: int = 0, win_off=None, flags: int = 0,

@@ -278,6 +278,27 @@ def test_pinned_host_mixed_mtu_vs_oracle(ctx, scheme, k, r, direct):
     _cmp_emitted(dec, od, S, "host decode")
 
 
+@pytest.mark.parametrize("scheme,k,r,wl,L", [("xor", 8, 2, 0, 1200), ("gf256", 16, 4, 0, 1200),
+                                              ("gf256", 32, 8, 1, 0), ("xor", 5, 3, 1, 0),
+                                              ("gf256", 4, 7, 0, 100)])
+def test_encode_split_layout_vs_oracle(ctx, scheme, k, r, wl, L):
+    """fecgpu_encode_split (SURVEY §8b form: src[W][k][stride] in, repair[W][r][stride]
+    out) equals the oracle's repairs and leaves the sources untouched (r > k too)."""
+    nwin = 37
+    S = O.sym_lens(wl, SEED, 0, nwin, k, L)
+    stride = O.round_up(int(S.max()), 16)
+    wins = O.make_windows(wl, SEED, 0, nwin, k, r, L, stride)
+    oe, _, _ = oracle_run(scheme, k, r, wins, S, np.full(nwin, (1 << (k + r)) - 1, np.uint64))
+    src = torch.from_numpy(np.ascontiguousarray(wins[:, :k])).cuda()
+    rep = torch.full((nwin, r, stride), 0x77, dtype=torch.uint8, device="cuda")
+    kw = dict(sym_len_all=int(S[0])) if wl == 0 else dict(sym_len=torch.from_numpy(S.astype(np.int32)).cuda())
+    ctx.encode_split(fecgpu.Code(scheme, k, r), src, rep, nwin=nwin, stride=stride, **kw)
+    torch.cuda.synchronize()
+    got = np.concatenate([src.cpu().numpy(), rep.cpu().numpy()], axis=1)
+    assert np.array_equal(got[:, :k], wins[:, :k])
+    _cmp_emitted(got, oe, S, "encode_split")
+
+
 def test_zero_windows_and_errors(ctx):
     code = fecgpu.Code("gf256", 4, 2)
     d = torch.zeros(4096, dtype=torch.uint8, device="cuda")
