@@ -201,6 +201,7 @@ __device__ __forceinline__ void win_geom(const BatchArgs &a, uint64_t w, uint64_
     } else {
         base = reinterpret_cast<uint64_t>(a.win) + w * a.wpitch;
         stride = a.stride;
+        S = min(S, stride);  // a bad sym_len[w] (device data, unchecked) stays in its rows
     }
 }
 
@@ -947,7 +948,7 @@ __global__ __launch_bounds__(kBlock) void digest_kernel(DigestArgs a) {
     __shared__ uint64_t s_red[kBlock / 64];
     const uint64_t wi = blockIdx.x;
     const int tid = threadIdx.x, n = a.k + a.r;
-    const uint32_t S = a.sym_len ? a.sym_len[wi] : a.S_all;
+    const uint32_t S = min(a.sym_len ? a.sym_len[wi] : a.S_all, a.stride);
     const uint32_t nw = (S + 7u) >> 3;
     const uint8_t *win = a.win + wi * (uint64_t)n * a.stride;
     uint64_t d = 0;
