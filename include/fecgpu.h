@@ -188,6 +188,27 @@ ssize_t fecgpu_decoder_recovered(fecgpu_decoder *dec, uint64_t win, uint16_t idx
                                  size_t cap);
 ssize_t fecgpu_decoder_release(fecgpu_decoder *dec, uint64_t win);
 
+/* Scheduling policy: bounds the time a packet waits for its
+ * repairs / its recovery, on the caller's clock.  The Connection calls
+ * *_tick(now_us) from its timer (and may call it on every packet); add calls
+ * stamp windows with the latest `now_us` seen.  0 disables a timeout.
+ *   window_timeout_us: the sender closes its open window this long after the
+ *       window's first packet (missing sources become empty packets);
+ *   batch_timeout_us : a partly filled batch is launched this long after its
+ *       first window closed (sender), a flush runs this long after the first
+ *       symbol filed since the last flush (receiver).
+ * tick returns the number of windows launched (sender) or sources recovered
+ * (receiver), or a negative error. */
+typedef struct fecgpu_policy {
+    uint64_t window_timeout_us;
+    uint64_t batch_timeout_us;
+} fecgpu_policy;
+
+ssize_t fecgpu_encoder_set_policy(fecgpu_encoder *enc, const fecgpu_policy *policy);
+ssize_t fecgpu_encoder_tick(fecgpu_encoder *enc, uint64_t now_us);
+ssize_t fecgpu_decoder_set_policy(fecgpu_decoder *dec, const fecgpu_policy *policy);
+ssize_t fecgpu_decoder_tick(fecgpu_decoder *dec, uint64_t now_us);
+
 /* ---- FEC frames on the wire --------------------
  * QUIC varint-coded frames (RFC 9000 §16 integers):
  *   SOURCE_ID: type | window | index                    (next to a source payload)

@@ -330,7 +330,7 @@ size_t host_window_bytes(const fecgpu_code *code, const uint64_t *win_off, const
 }
 
 ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
-                      hipStream_t s);
+                      hipStream_t s, bool remote = false);
 ssize_t run_host_pipelined(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
                            const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
                            uint64_t nwin, const uint64_t *present, uint8_t *status);
@@ -410,7 +410,7 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
 
 // Plan and launch one batch whose pointers are all device pointers.
 ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
-                      hipStream_t s) {
+                      hipStream_t s, bool remote) {
     ssize_t rc = 0;
     const int k = code->k, r = code->r, scheme = (int)code->scheme;
     const uint32_t *sym_len = a.sym_len;
@@ -462,6 +462,12 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         } else {
             p.wpb = choose_wpb(ncol, 0, 0);
         }
+    }
+    if (remote) {  // PCIe-latency bound: as many workgroups as windows
+        p.remote = true;
+        p.flat = false;
+        p.wpb = 1;
+        if (p.win_lds) p.lds_bytes = p.win_lds;
     }
     if (ctx->wpb_override > 0 && !p.flat) {
         p.wpb = std::min(ctx->wpb_override, kMaxWpb);
@@ -563,7 +569,7 @@ ssize_t run_host_pipelined(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode
         a.S_all = sym_len_all;
         a.stride = stride;
         if (hdev && !zc) a.out_delta = reinterpret_cast<uint64_t>(hdev + w0 * wbytes) - reinterpret_cast<uint64_t>(d);
-        ssize_t rc = launch_device(ctx, code, decode, a, hp.comp);
+        ssize_t rc = launch_device(ctx, code, decode, a, hp.comp, zc);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(hp.comp_done[sl], hp.comp), "record");
         HIP_TRY(hipStreamWaitEvent(hp.d2h, hp.comp_done[sl], 0), "wait");
@@ -591,7 +597,7 @@ ssize_t run_host_pipelined(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode
 namespace fecgpu {
 
 ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
-                     hipStream_t s) {
+                     hipStream_t s, bool remote) {
     if (!ctx || !a.win) return FECGPU_ERR_INVALID_ARG;
     ssize_t rc = fecgpu_code_check(code);
     if (rc) return rc;
@@ -599,7 +605,7 @@ ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Batc
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev), "hipGetDevice");
     if (prev != ctx->devs[0]) HIP_TRY(hipSetDevice(ctx->devs[0]), "hipSetDevice");
-    rc = launch_device(ctx, code, decode, a, s);
+    rc = launch_device(ctx, code, decode, a, s, remote);
     if (prev != ctx->devs[0]) (void)hipSetDevice(prev);
     return rc;
 }

@@ -111,6 +111,10 @@ struct fecgpu_encoder {
     uint32_t open_max = 0;
     uint32_t open_len[FECGPU_MAX_K] = {};
     EncBatch *cur = nullptr;  // being filled (its windows [first, first + nwin) closed)
+    fecgpu_policy policy{};
+    uint64_t now = 0;         // latest caller clock (tick)
+    uint64_t open_t = 0;      // when the open window got its first packet
+    uint64_t cur_t = 0;       // when cur's first window closed
     std::deque<EncBatch *> active;  // window order: launched batches, then cur
     std::vector<EncBatch *> spare;
     std::vector<EncBatch *> all;
@@ -161,7 +165,7 @@ ssize_t enc_launch(fecgpu_encoder *e) {
     a.sym_len = b->S_dev;
     a.stride = e->stride;
     a.nwin = b->nwin;
-    ssize_t rc = fecgpu::launch_batch(e->ctx, &e->code, false, a, e->stream);
+    ssize_t rc = fecgpu::launch_batch(e->ctx, &e->code, false, a, e->stream, true);
     if (rc) return rc;
     DevGuard g(e->dev);
     if (hipEventRecord(b->done, e->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
@@ -197,15 +201,13 @@ ssize_t enc_close(fecgpu_encoder *e) {
         std::memset(row + used, 0, S16 - used);
     }
     b->S[slot] = S;
+    if (b->nwin == 0) e->cur_t = e->now;
     b->nwin++;
     b->live++;
     e->next_win++;
     e->open_n = 0;
     e->open_max = 0;
-    if (b->nwin == e->batch) {
-        ssize_t rc = enc_launch(e);
-        if (rc < 0) return rc;
-    }
+    if (b->nwin == e->batch) return enc_launch(e);  // windows launched, or an error
     return 0;
 }
 
@@ -282,6 +284,7 @@ ssize_t fecgpu_encoder_add_source(fecgpu_encoder *e, const uint8_t *pkt, size_t 
     }
     if (win) *win = e->next_win;
     if (idx) *idx = (uint16_t)e->open_n;
+    if (e->open_n == 0) e->open_t = e->now;
     e->open_len[e->open_n++] = (uint32_t)len;
     e->open_max = std::max<uint32_t>(e->open_max, (uint32_t)len);
     if (e->open_n == e->code.k) {
@@ -306,6 +309,30 @@ ssize_t fecgpu_encoder_flush(fecgpu_encoder *e) {
     DevGuard g(e->dev);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
     return n;
+}
+
+ssize_t fecgpu_encoder_set_policy(fecgpu_encoder *e, const fecgpu_policy *p) {
+    if (!e || !p) return FECGPU_ERR_INVALID_ARG;
+    e->policy = *p;
+    return 0;
+}
+
+ssize_t fecgpu_encoder_tick(fecgpu_encoder *e, uint64_t now_us) {
+    if (!e) return FECGPU_ERR_INVALID_ARG;
+    e->now = std::max(e->now, now_us);
+    ssize_t launched = 0;
+    const uint64_t wt = e->policy.window_timeout_us, bt = e->policy.batch_timeout_us;
+    if (wt && e->open_n && e->now - e->open_t >= wt) {
+        ssize_t rc = enc_close(e);  // may launch a now-full batch
+        if (rc < 0) return rc;
+        launched += rc;
+    }
+    if (bt && e->cur && e->cur->nwin && e->now - e->cur_t >= bt) {
+        ssize_t rc = enc_launch(e);
+        if (rc < 0) return rc;
+        launched += rc;
+    }
+    return launched;
 }
 
 ssize_t fecgpu_encoder_repair(fecgpu_encoder *e, uint64_t win, uint16_t i, uint8_t *out,
@@ -371,6 +398,9 @@ struct fecgpu_decoder {
     Pinned arg;                        // flush arrays: off, S, present, status
     size_t arg_cap = 0;
     uint64_t dirty = 0;
+    fecgpu_policy policy{};
+    uint64_t now = 0;                  // latest caller clock (tick)
+    uint64_t dirty_t = 0;              // when the first symbol since the last flush was filed
 };
 
 namespace {
@@ -412,6 +442,7 @@ ssize_t dec_slot(fecgpu_decoder *d, uint64_t win, uint32_t &out) {
 }
 
 void dec_touch(fecgpu_decoder *d, uint32_t s) {
+    if (d->dirty == 0) d->dirty_t = d->now;
     if (!d->slots[s].cand) {
         d->slots[s].cand = true;
         d->cand.push_back(s);
@@ -527,7 +558,7 @@ ssize_t fecgpu_decoder_flush(fecgpu_decoder *d) {
     a.stride = d->stride;
     a.off_stride = d->stride;
     a.nwin = n;
-    ssize_t rc = fecgpu::launch_batch(d->ctx, &d->code, true, a, d->stream);
+    ssize_t rc = fecgpu::launch_batch(d->ctx, &d->code, true, a, d->stream, true);
     if (rc) return rc;
     if (hipStreamSynchronize(d->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
     ssize_t recovered = 0;
@@ -609,6 +640,20 @@ ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *d, uint64_t win, uint16_t idx,
     w.present |= 1ull << (k + idx);
     dec_touch(d, s);
     if (++d->dirty >= (uint64_t)d->batch * d->code.k) return fecgpu_decoder_flush(d) < 0 ? FECGPU_ERR_DEVICE : 0;
+    return 0;
+}
+
+ssize_t fecgpu_decoder_set_policy(fecgpu_decoder *d, const fecgpu_policy *p) {
+    if (!d || !p) return FECGPU_ERR_INVALID_ARG;
+    d->policy = *p;
+    return 0;
+}
+
+ssize_t fecgpu_decoder_tick(fecgpu_decoder *d, uint64_t now_us) {
+    if (!d) return FECGPU_ERR_INVALID_ARG;
+    d->now = std::max(d->now, now_us);
+    const uint64_t bt = d->policy.batch_timeout_us;
+    if (bt && d->dirty && d->now - d->dirty_t >= bt) return fecgpu_decoder_flush(d);
     return 0;
 }
 

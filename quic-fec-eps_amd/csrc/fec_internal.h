@@ -54,6 +54,8 @@ struct LaunchPlan {
     uint32_t win_lds;    // per-window region (GF decode)
     int grid_mult;       // resident blocks x grid_mult (tuning; 0 = automatic)
     int blocks_per_cu;   // persistent grid of CUs x blocks_per_cu (tuning; 0 = automatic)
+    bool remote;         // windows in mapped host memory: one window per workgroup and
+                         // deep load batches (PCIe latency, small batches)
 };
 
 // Per-window LDS region of the GF decode kernel: tables [k][R] uint4 + [k][R] u32,
@@ -68,7 +70,7 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
 // (win, win_off, sym_len, S_all, stride, off_stride, nwin, present, status)
 // are the caller's; the rest is filled in.
 ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
-                     hipStream_t s);
+                     hipStream_t s, bool remote = false);
 hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s);
 
 struct SynthArgs {

@@ -383,10 +383,10 @@ __device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne,
 }
 
 // GF encode (a5): R_i = sum_j C[i][j] * S_j, tables [j][i] in LDS (broadcast reads).
-template <int R, class TabP, class TcP>
+template <int R, int UO, class TabP, class TcP>
 __device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, int k, TabP tab,
                                                TcP tc, bool valid, uint64_t od) {
-    constexpr int U = FECGPU_GF_U;
+    constexpr int U = UO ? UO : FECGPU_GF_U;
     uint4 acc[R];
 #pragma unroll
     for (int m = 0; m < R; m++) acc[m] = zero4();
@@ -498,7 +498,9 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
     }
 }
 
-template <int R, bool FLAT>
+// UO: input rows per load batch (0 = FECGPU_GF_U); 8 for windows in mapped
+// host memory, where each batch of loads is a PCIe round trip.
+template <int R, bool FLAT, int UO = 0>
 __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a) {
     const int k = a.k;
 #if FECGPU_ENC_SGPR
@@ -526,7 +528,7 @@ __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a
 #endif
     if constexpr (FLAT) {
         for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t w, uint32_t, bool valid) {
-            gf_encode_slot<R>(p, stride, k, tab, tc, valid, a.out_delta + w * a.out_wdelta);
+            gf_encode_slot<R, UO>(p, stride, k, tab, tc, valid, a.out_delta + w * a.out_wdelta);
         });
     } else {
         __shared__ GroupLds g;
@@ -539,7 +541,7 @@ __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a
             if (threadIdx.x < 64) block_prefix(g.pfx, (int)threadIdx.x < nb ? g.ncol[threadIdx.x] : 0u, threadIdx.x);
             __syncthreads();
             for_group_slots(g, nb, [&](uint8_t *p, uint32_t stride, int wl, bool valid) {
-                gf_encode_slot<R>(p, stride, k, tab, tc, valid, a.out_delta + (w0 + wl) * a.out_wdelta);
+                gf_encode_slot<R, UO>(p, stride, k, tab, tc, valid, a.out_delta + (w0 + wl) * a.out_wdelta);
             });
             __syncthreads();
         }
@@ -1048,6 +1050,7 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
         else DISPATCH_R(a.r, launch(xor_encode_kernel<RR, false>, a, p, s, false))
     }
     if (flat) DISPATCH_R(a.r, launch(gf_encode_kernel<RR, true>, a, p, s, true))
+    else if (p.remote) DISPATCH_R(a.r, launch(gf_encode_kernel<RR, false, 8>, a, p, s, false))
     else DISPATCH_R(a.r, launch(gf_encode_kernel<RR, false>, a, p, s, false))
 }
 

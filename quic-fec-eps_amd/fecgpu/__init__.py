@@ -48,6 +48,8 @@ EXPORTS = (
     "fecgpu_decoder_new", "fecgpu_decoder_free", "fecgpu_decoder_add_source",
     "fecgpu_decoder_add_repair", "fecgpu_decoder_flush", "fecgpu_decoder_recovered",
     "fecgpu_decoder_release",
+    "fecgpu_encoder_set_policy", "fecgpu_encoder_tick", "fecgpu_decoder_set_policy",
+    "fecgpu_decoder_tick",
     "fecgpu_frame_source_id_len", "fecgpu_frame_write_source_id", "fecgpu_frame_repair_len",
     "fecgpu_frame_write_repair", "fecgpu_frame_parse",
 )
@@ -88,6 +90,11 @@ class fecgpu_frame(ctypes.Structure):
 
 
 _L = None
+
+
+class _Policy(ctypes.Structure):
+    """fecgpu_policy (include/fecgpu.h)."""
+    _fields_ = [("window_timeout_us", ctypes.c_uint64), ("batch_timeout_us", ctypes.c_uint64)]
 
 
 def _lib():
@@ -142,6 +149,10 @@ def _lib():
             "fecgpu_decoder_flush": (sz, [vp]),
             "fecgpu_decoder_recovered": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
             "fecgpu_decoder_release": (sz, [vp, u64]),
+            "fecgpu_encoder_set_policy": (sz, [vp, ctypes.POINTER(_Policy)]),
+            "fecgpu_encoder_tick": (sz, [vp, u64]),
+            "fecgpu_decoder_set_policy": (sz, [vp, ctypes.POINTER(_Policy)]),
+            "fecgpu_decoder_tick": (sz, [vp, u64]),
             "fecgpu_frame_source_id_len": (sz, [u64, ctypes.c_uint16]),
             "fecgpu_frame_write_source_id": (sz, [vp, ctypes.c_size_t, u64, ctypes.c_uint16]),
             "fecgpu_frame_repair_len": (sz, [u64, ctypes.c_uint16, ctypes.c_uint16,
@@ -350,6 +361,14 @@ class Encoder:
     def release(self, win: int) -> int:
         return _lib().fecgpu_encoder_release(self._h, win)
 
+    def set_policy(self, window_timeout_us: int = 0, batch_timeout_us: int = 0) -> None:
+        p = _Policy(window_timeout_us, batch_timeout_us)
+        _check(_lib().fecgpu_encoder_set_policy(self._h, ctypes.byref(p)), "fecgpu_encoder_set_policy")
+
+    def tick(self, now_us: int) -> int:
+        """Windows launched by the policy at `now_us`."""
+        return _check(_lib().fecgpu_encoder_tick(self._h, now_us), "fecgpu_encoder_tick")
+
     def close(self):
         if self._h:
             _lib().fecgpu_encoder_free(self._h)
@@ -390,6 +409,14 @@ class Decoder:
 
     def release(self, win: int) -> int:
         return _lib().fecgpu_decoder_release(self._h, win)
+
+    def set_policy(self, window_timeout_us: int = 0, batch_timeout_us: int = 0) -> None:
+        p = _Policy(window_timeout_us, batch_timeout_us)
+        _check(_lib().fecgpu_decoder_set_policy(self._h, ctypes.byref(p)), "fecgpu_decoder_set_policy")
+
+    def tick(self, now_us: int) -> int:
+        """Sources recovered by a policy flush at `now_us`."""
+        return _check(_lib().fecgpu_decoder_tick(self._h, now_us), "fecgpu_decoder_tick")
 
     def close(self):
         if self._h:

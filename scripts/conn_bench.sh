@@ -8,3 +8,5 @@ run xor 8 2 1200 512 0.05 256
 run xor 8 2 1200 512 0.05 4096
 run gf256 16 4 1200 512 0.05 1024
 run gf256 32 8 9000 512 0.10 256 1    # LENPREFIX, lengths 1..9000
+timeout -k 10 120 ./scripts/latency_bench xor 8 2 1200 || exit $?
+timeout -k 10 120 ./scripts/latency_bench gf256 16 4 1200 || exit $?

@@ -170,3 +170,35 @@ def test_native_conn_driver(args):
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["corrupt"] == 0 and res["unrecovered"] == res["expected_unrecovered"]
     assert res["recovered"] + res["unrecovered"] == res["lost"]
+
+
+def test_policy_timeouts(ctx):
+    """Scheduling policy: on the caller's clock, a window closes
+    window_timeout_us after its first packet and a partly filled batch launches
+    batch_timeout_us after its first window closed; the receiver flushes
+    batch_timeout_us after the first symbol filed since its last flush."""
+    code = fecgpu.Code("gf256", 8, 2, "lenprefix")
+    enc = fecgpu.Encoder(ctx, code, max_len=1200, batch=64)
+    enc.set_policy(window_timeout_us=100, batch_timeout_us=50)
+    assert enc.tick(1000) == 0
+    pkts = [bytes([i]) * (100 + i) for i in range(3)]
+    for p in pkts:
+        assert enc.add_source(p)[0] == 0
+    assert enc.tick(1099) == 0 and enc.repair(0, 0) is None     # window still open
+    assert enc.tick(1100) == 0 and enc.repair(0, 0) is None     # closed, batch not due
+    assert enc.tick(1149) == 0
+    assert enc.tick(1150) == 1                                   # batch launched
+    rep = [enc.repair(0, i) for i in range(2)]
+    assert all(r is not None and len(r) == 2 + 102 for r in rep)
+    w, i = enc.add_source(b"x" * 10)                             # next window opens at 1150
+    assert (w, i) == (1, 0)
+    dec = fecgpu.Decoder(ctx, code, max_len=1200, batch=64)
+    dec.set_policy(batch_timeout_us=30)
+    assert dec.tick(5000) == 0
+    assert dec.add_source(0, 1, pkts[1]) == 0
+    for j in range(3, 8):                                        # the padded, empty sources
+        assert dec.add_source(0, j, b"") == 0
+    assert dec.add_repair(0, 0, rep[0]) == 0 and dec.add_repair(0, 1, rep[1]) == 0
+    assert dec.tick(5029) == 0 and dec.recovered(0, 0) is None   # flush not due yet
+    assert dec.tick(5030) == 2                                   # flushed: sources 0 and 2 back
+    assert dec.recovered(0, 0) == pkts[0] and dec.recovered(0, 2) == pkts[2]
