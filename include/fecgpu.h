@@ -60,7 +60,11 @@ enum fecgpu_error {
 };
 
 enum fecgpu_scheme { FECGPU_SCHEME_XOR = 0, FECGPU_SCHEME_GF256 = 1 };
-enum fecgpu_matrix { FECGPU_MATRIX_CAUCHY = 0 };
+/* GF(2^8) parity rows: CAUCHY C[i][j] = inv((k+i) ^ j) (ISA-L cauchy1 layout);
+ * VANDERMONDE = rows k.. of V * inv(V[0..k)), V[i][j] = i^j (points 0..k+r-1):
+ * the systematic matrix of Backblaze JavaReedSolomon, klauspost/reedsolomon
+ * and the Rust crate reed-solomon-erasure. */
+enum fecgpu_matrix { FECGPU_MATRIX_CAUCHY = 0, FECGPU_MATRIX_VANDERMONDE = 1 };
 enum fecgpu_framing { FECGPU_FRAMING_FIXED = 0, FECGPU_FRAMING_LENPREFIX = 1 };
 
 /* per-window decode status */

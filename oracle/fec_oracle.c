@@ -64,6 +64,66 @@ void orc_cauchy(int k, int r, uint8_t *C) {
         for (int j = 0; j < k; j++) C[i * k + j] = orc_gf_inv((uint8_t)((k + i) ^ j));
 }
 
+/* Gauss-Jordan inverse of an n x n matrix (n <= 64) with row pivoting;
+ * returns 0 if singular. */
+static int gf_invert64(int n, const uint8_t *A, uint8_t *Ainv) {
+    static __thread uint8_t M[64][128];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < 2 * n; j++)
+            M[i][j] = j < n ? A[i * n + j] : (uint8_t)(j - n == i);
+    for (int c = 0; c < n; c++) {
+        int p = -1;
+        for (int i = c; i < n; i++)
+            if (M[i][c]) { p = i; break; }
+        if (p < 0) return 0;
+        if (p != c)
+            for (int j = 0; j < 2 * n; j++) { uint8_t t = M[c][j]; M[c][j] = M[p][j]; M[p][j] = t; }
+        const uint8_t iv = orc_gf_inv(M[c][c]);
+        for (int j = 0; j < 2 * n; j++) M[c][j] = orc_gf_mul(M[c][j], iv);
+        for (int i = 0; i < n; i++) {
+            if (i == c || !M[i][c]) continue;
+            const uint8_t f = M[i][c];
+            for (int j = 0; j < 2 * n; j++) M[i][j] ^= orc_gf_mul(f, M[c][j]);
+        }
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) Ainv[i * n + j] = M[i][n + j];
+    return 1;
+}
+
+/* a^n in the field, with 0^0 = 1 (Backblaze Galois.exp) */
+static uint8_t gf_pow(uint8_t a, int n) {
+    if (n == 0) return 1;
+    if (a == 0) return 0;
+    return orc_gf_exp((orc_gf_log(a) * n) % 255);
+}
+
+/* Systematic Vandermonde generator (FECGPU_MATRIX_VANDERMONDE): the (k+r) x k
+ * Vandermonde matrix V[i][j] = i^j (points 0..k+r-1) times the inverse of its
+ * top k x k block; rows k.. of the product are the parity rows P[r][k].  The
+ * construction of Backblaze's JavaReedSolomon (ReedSolomon.buildMatrix), the
+ * default matrix of klauspost/reedsolomon and of the Rust crate
+ * reed-solomon-erasure; pinned by their published 5+5 known answer
+ * (tests/test_oracle_field.py::test_vandermonde_kat).  MDS (distinct points). */
+void orc_vandermonde(int k, int r, uint8_t *P) {
+    static __thread uint8_t top[64 * 64], inv[64 * 64];
+    for (int i = 0; i < k; i++)
+        for (int j = 0; j < k; j++) top[i * k + j] = gf_pow((uint8_t)i, j);
+    (void)gf_invert64(k, top, inv);  /* distinct points: never singular */
+    for (int i = 0; i < r; i++)
+        for (int j = 0; j < k; j++) {
+            uint8_t v = 0;
+            for (int t = 0; t < k; t++) v ^= orc_gf_mul(gf_pow((uint8_t)(k + i), t), inv[t * k + j]);
+            P[i * k + j] = v;
+        }
+}
+
+/* parity rows of the scheme's generator (GF schemes) */
+void orc_matrix(int scheme, int k, int r, uint8_t *C) {
+    if (scheme == ORC_GF256_VDM) orc_vandermonde(k, r, C);
+    else orc_cauchy(k, r, C);
+}
+
 /* ---------------------------------------------------------------- A.5 --- */
 uint64_t orc_sm64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -134,7 +194,7 @@ uint64_t orc_present(int erasure, uint64_t seed, uint64_t w, int scheme, int k, 
         return p;
     }
     uint64_t p = all;
-    if (scheme == ORC_GF256) {
+    if (scheme != ORC_XOR) {
         int perm[64];
         for (int j = 0; j < k; j++) perm[j] = j;
         int e = r < k ? r : k;
@@ -171,7 +231,7 @@ void orc_encode(int scheme, int k, int r, uint32_t S, uint32_t stride, uint8_t *
     }
     /* a5: R_i = sum_j C[i][j] * S_j */
     uint8_t C[64 * 64];
-    orc_cauchy(k, r, C);
+    orc_matrix(scheme, k, r, C);
     for (int i = 0; i < r; i++) {
         uint8_t *R = win + (size_t)(k + i) * stride;
         memset(R, 0, S);
@@ -240,7 +300,7 @@ int orc_decode(int scheme, int k, int r, uint32_t S, uint32_t stride, uint64_t p
         if ((present >> (k + i)) & 1) sel[nrep++] = i;
     if (nrep < e || e > 16) return ORC_UNRECOVERABLE;
     uint8_t C[64 * 64], A[16 * 16], Ai[16 * 16];
-    orc_cauchy(k, r, C);
+    orc_matrix(scheme, k, r, C);
     for (int t = 0; t < e; t++)
         for (int u = 0; u < e; u++) A[t * e + u] = C[sel[t] * k + miss[u]];
     if (!gf_invert(e, A, Ai)) return ORC_UNRECOVERABLE;

@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-enum { ORC_XOR = 0, ORC_GF256 = 1 };
+/* schemes: XOR groups, GF(2^8) Cauchy rows, GF(2^8) systematic Vandermonde rows */
+enum { ORC_XOR = 0, ORC_GF256 = 1, ORC_GF256_VDM = 2 };
 enum { ORC_FIXED = 0, ORC_LENPREFIX = 1 };
 enum { ORC_OK = 0, ORC_UNRECOVERABLE = 1 };
 
@@ -41,6 +42,10 @@ uint8_t orc_gf_exp(int i);
 int     orc_gf_log(uint8_t a);
 /* A.2 matrix: C[i*k + j] = inv((k + i) ^ j) */
 void    orc_cauchy(int k, int r, uint8_t *C);
+/* systematic Vandermonde parity rows P[i*k + j] (Backblaze construction) */
+void    orc_vandermonde(int k, int r, uint8_t *P);
+/* parity rows of a GF scheme (ORC_GF256 -> Cauchy, ORC_GF256_VDM -> Vandermonde) */
+void    orc_matrix(int scheme, int k, int r, uint8_t *C);
 
 /* A.5 PRNG / workload */
 uint64_t orc_sm64(uint64_t x);

@@ -51,13 +51,43 @@ def cauchy(k: int, r: int) -> np.ndarray:
     return np.array([[_INV[(k + i) ^ j] for j in range(k)] for i in range(r)], np.uint8)
 
 
+def _gj_inverse(A: np.ndarray) -> np.ndarray:
+    """Gauss-Jordan inverse over GF(2^8) (row pivoting) through the product table."""
+    n = A.shape[0]
+    M = np.concatenate([A.astype(np.uint8), np.eye(n, dtype=np.uint8)], axis=1)
+    for c in range(n):
+        piv = next(i for i in range(c, n) if M[i, c])
+        M[[c, piv]] = M[[piv, c]]
+        M[c] = _MUL[_INV[M[c, c]]][M[c]]
+        for i in range(n):
+            if i != c and M[i, c]:
+                M[i] ^= _MUL[M[i, c]][M[c]]
+    return M[:, n:].copy()
+
+
+def vandermonde(k: int, r: int) -> np.ndarray:
+    """Systematic Vandermonde parity rows: V[i][j] = i^j (i < k+r, powers by
+    repeated table multiplication, 0^0 = 1) times inv(V[:k]); rows k.. (the
+    Backblaze JavaReedSolomon / klauspost / reed-solomon-erasure matrix)."""
+    V = np.zeros((k + r, k), np.uint8)
+    for i in range(k + r):
+        x = 1
+        for j in range(k):
+            V[i, j] = x
+            x = int(_MUL[x][i])
+    return matmul(V[k:], _gj_inverse(V[:k]))
+
+
 def generator(scheme: str, k: int, r: int) -> np.ndarray:
-    """Systematic (k+r) x k generator: identity on top, repair rows below."""
+    """Systematic (k+r) x k generator: identity on top, repair rows below.
+    scheme: "xor", "gf" (Cauchy rows) or "gf-vdm" (systematic Vandermonde)."""
     G = np.zeros((k + r, k), np.uint8)
     G[:k] = np.eye(k, dtype=np.uint8)
     if scheme == "xor":
         for g in range(r):
             G[k + g, g::r] = 1
+    elif scheme == "gf-vdm":
+        G[k:] = vandermonde(k, r)
     else:
         G[k:] = cauchy(k, r)
     return G
@@ -112,7 +142,7 @@ def decode(scheme: str, k: int, r: int, sym: np.ndarray, present: int):
     if len(reps) < len(missing):
         return src, False
     rows = [j for j in range(k) if (present >> j) & 1] + reps[: len(missing)]
-    G = generator("gf", k, r)
+    G = generator(scheme, k, r)
     A = np.concatenate([G[rows], sym[rows]], axis=1).astype(np.uint8)  # k x (k+L)
     n = k
     for c in range(n):
@@ -190,7 +220,7 @@ def present(erasure: int, seed: int, w: int, scheme: str, k: int, r: int) -> int
             if (sm64((sera + ((w << 8) | i)) & M64) & 0xFFFFFFFF) < P10:
                 p &= ~(1 << i)
         return p
-    if scheme == "gf":
+    if scheme != "xor":
         perm = list(range(k))
         for t in range(min(r, k)):
             u = t + sm64((sera + ((w << 8) | t)) & M64) % (k - t)

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
 _lib = None
 
-XOR, GF256 = 0, 1
+XOR, GF256, GF256_VDM = 0, 1, 2     # GF256: Cauchy rows; GF256_VDM: systematic Vandermonde
 FIXED_WL, MIXED_WL = 0, 1            # workloads
 ERA_NONE, ERA_EXACT, ERA_IID = 0, 1, 2
 OK, UNRECOVERABLE = 0, 1
@@ -42,6 +42,8 @@ def lib():
             "orc_gf_exp": (u8, [i32]),
             "orc_gf_log": (i32, [u8]),
             "orc_cauchy": (None, [i32, i32, vp]),
+            "orc_vandermonde": (None, [i32, i32, vp]),
+            "orc_matrix": (None, [i32, i32, i32, vp]),
             "orc_sm64": (u64, [u64]),
             "orc_pkt_len": (u32, [i32, u64, u64, i32, i32, u32]),
             "orc_sym_len": (u32, [i32, u64, u64, i32, u32]),
@@ -80,6 +82,13 @@ def cauchy(k: int, r: int) -> np.ndarray:
     C = np.zeros((r, k), np.uint8)
     lib().orc_cauchy(k, r, _p(C))
     return C
+
+
+def vandermonde(k: int, r: int) -> np.ndarray:
+    """Parity rows of the systematic Vandermonde generator (Backblaze construction)."""
+    P = np.zeros((r, k), np.uint8)
+    lib().orc_vandermonde(k, r, _p(P))
+    return P
 
 
 def sm64(x: int) -> int:

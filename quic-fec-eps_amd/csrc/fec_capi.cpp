@@ -47,7 +47,54 @@ uint8_t host_gf_inv(uint8_t a) {
 struct EncTables {
     uint4 *ab = nullptr;
     uint32_t *c = nullptr;
+    uint8_t *coef = nullptr;  // parity rows P[r][k] (non-Cauchy matrices: the decode plan reads them)
 };
+
+uint8_t host_gf_pow(uint8_t a, int n) {  // a^n, 0^0 = 1
+    static constexpr GfTables t = make_gf_tables();
+    if (n == 0) return 1;
+    if (a == 0) return 0;
+    return t.exp[(t.log[a] * n) % 255];
+}
+
+// Parity rows P[i*k + j] of the code's systematic generator:
+// Cauchy C[i][j] = inv((k+i) ^ j), or the systematic Vandermonde matrix —
+// V[i][j] = i^j over points 0..k+r-1 times the inverse of its top k x k block
+// (Backblaze JavaReedSolomon / klauspost / reed-solomon-erasure construction).
+void host_parity_rows(const fecgpu_code *code, std::vector<uint8_t> &P) {
+    const int k = code->k, r = code->r;
+    P.assign((size_t)r * k, 0);
+    if (code->matrix == FECGPU_MATRIX_CAUCHY) {
+        for (int i = 0; i < r; i++)
+            for (int j = 0; j < k; j++) P[(size_t)i * k + j] = host_gf_inv((uint8_t)((k + i) ^ j));
+        return;
+    }
+    // Gauss-Jordan inverse of the top block (distinct points: never singular)
+    std::vector<uint8_t> M((size_t)k * 2 * k);
+    for (int i = 0; i < k; i++)
+        for (int j = 0; j < 2 * k; j++)
+            M[(size_t)i * 2 * k + j] = j < k ? host_gf_pow((uint8_t)i, j) : (uint8_t)(j - k == i);
+    for (int c = 0; c < k; c++) {
+        int piv = c;
+        while (!M[(size_t)piv * 2 * k + c]) piv++;
+        if (piv != c)
+            for (int j = 0; j < 2 * k; j++) std::swap(M[(size_t)piv * 2 * k + j], M[(size_t)c * 2 * k + j]);
+        const uint8_t iv = host_gf_inv(M[(size_t)c * 2 * k + c]);
+        for (int j = 0; j < 2 * k; j++) M[(size_t)c * 2 * k + j] = host_gf_mul(M[(size_t)c * 2 * k + j], iv);
+        for (int i = 0; i < k; i++) {
+            const uint8_t f = M[(size_t)i * 2 * k + c];
+            if (i == c || !f) continue;
+            for (int j = 0; j < 2 * k; j++) M[(size_t)i * 2 * k + j] ^= host_gf_mul(f, M[(size_t)c * 2 * k + j]);
+        }
+    }
+    for (int i = 0; i < r; i++)
+        for (int j = 0; j < k; j++) {
+            uint8_t v = 0;
+            for (int t = 0; t < k; t++)
+                v ^= host_gf_mul(host_gf_pow((uint8_t)(k + i), t), M[(size_t)t * 2 * k + k + j]);
+            P[(size_t)i * k + j] = v;
+        }
+}
 
 constexpr int kPipeSlots = 3;
 
@@ -64,8 +111,8 @@ struct HostPipe {
 struct fecgpu_ctx {
     std::vector<int> devs;
     std::mutex mu;
-    // (device, k, r) -> Cauchy encode tables on that device
-    std::map<std::tuple<int, int, int>, EncTables> enc;
+    // (device, k, r, matrix) -> encode tables (and parity rows) on that device
+    std::map<std::tuple<int, int, int, int>, EncTables> enc;
     // host-pointer staging per device
     std::map<int, std::pair<void *, size_t>> stage;
     std::map<int, HostPipe> pipes;
@@ -111,7 +158,8 @@ ssize_t fecgpu_code_check(const fecgpu_code *code) {
     if (code->k + code->r > FECGPU_MAX_K) return FECGPU_ERR_UNSUPPORTED;
     if (code->r > FECGPU_MAX_R) return FECGPU_ERR_UNSUPPORTED;
     if (code->scheme == FECGPU_SCHEME_XOR && code->r > code->k) return FECGPU_ERR_INVALID_ARG;
-    if (code->scheme == FECGPU_SCHEME_GF256 && code->matrix != FECGPU_MATRIX_CAUCHY)
+    if (code->scheme == FECGPU_SCHEME_GF256 && code->matrix != FECGPU_MATRIX_CAUCHY &&
+        code->matrix != FECGPU_MATRIX_VANDERMONDE)
         return FECGPU_ERR_UNSUPPORTED;
     if (code->poly != 0 && code->poly != 0x11D) return FECGPU_ERR_UNSUPPORTED;
     return 0;
@@ -182,6 +230,7 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
         (void)hipSetDevice(std::get<0>(kv.first));
         (void)hipFree(kv.second.ab);
         (void)hipFree(kv.second.c);
+        if (kv.second.coef) (void)hipFree(kv.second.coef);
     }
     for (auto &kv : ctx->stage) {
         (void)hipSetDevice(kv.first);
@@ -222,23 +271,26 @@ void fecgpu_host_free(void *p) {
 
 namespace {
 
-// Cauchy tables for (k, r) on the current device, built once per ctx.
-ssize_t get_enc_tables(fecgpu_ctx *ctx, int k, int r, EncTables &out) {
+// Encode tables for the code's parity rows on the current device, built once
+// per ctx (and, for non-Cauchy matrices, the raw rows for the decode plan).
+ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out) {
+    const int k = code->k, r = code->r;
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    auto key = std::make_tuple(dev, k, r);
+    auto key = std::make_tuple(dev, k, r, (int)code->matrix);
     auto it = ctx->enc.find(key);
     if (it != ctx->enc.end()) {
         out = it->second;
         return 0;
     }
+    std::vector<uint8_t> P;
+    host_parity_rows(code, P);
     std::vector<uint4> ab((size_t)k * r);
     std::vector<uint32_t> cc((size_t)k * r);
     for (int j = 0; j < k; j++)
         for (int i = 0; i < r; i++) {
-            const uint8_t coef = host_gf_inv((uint8_t)((k + i) ^ j));  // A.2 Cauchy
-            const CoefTab t = make_coef_tab(coef);
+            const CoefTab t = make_coef_tab(P[(size_t)i * k + j]);
             ab[(size_t)j * r + i] = make_uint4(t.a_lo, t.a_hi, t.b_lo, t.b_hi);
             cc[(size_t)j * r + i] = t.c;
         }
@@ -247,6 +299,10 @@ ssize_t get_enc_tables(fecgpu_ctx *ctx, int k, int r, EncTables &out) {
     HIP_TRY(hipMalloc(&t.c, cc.size() * sizeof(uint32_t)), "hipMalloc");
     HIP_TRY(hipMemcpy(t.ab, ab.data(), ab.size() * sizeof(uint4), hipMemcpyHostToDevice), "hipMemcpy");
     HIP_TRY(hipMemcpy(t.c, cc.data(), cc.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy");
+    if (code->matrix != FECGPU_MATRIX_CAUCHY) {
+        HIP_TRY(hipMalloc(&t.coef, P.size()), "hipMalloc");
+        HIP_TRY(hipMemcpy(t.coef, P.data(), P.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    }
     ctx->enc[key] = t;
     out = t;
     return 0;
@@ -447,7 +503,7 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
     if (!decode) {
         if (scheme == FECGPU_SCHEME_GF256) {
             EncTables t;
-            rc = get_enc_tables(ctx, k, r, t);
+            rc = get_enc_tables(ctx, code, t);
             if (rc) return rc;
             a.enc_ab = t.ab;
             a.enc_c = t.c;
@@ -456,6 +512,12 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         p.wpb = choose_wpb(ncol, 0, 0);
     } else {
         if (scheme == FECGPU_SCHEME_GF256) {
+            if (code->matrix != FECGPU_MATRIX_CAUCHY) {  // the plan reads the parity rows
+                EncTables t;
+                rc = get_enc_tables(ctx, code, t);
+                if (rc) return rc;
+                a.coef = t.coef;
+            }
             p.win_lds = gf_dec_win_lds(k, r);
             p.wpb = choose_wpb(ncol, p.win_lds, 40 * 1024);
             p.lds_bytes = p.win_lds * (uint32_t)p.wpb;

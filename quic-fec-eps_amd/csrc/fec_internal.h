@@ -25,6 +25,7 @@ struct BatchArgs {
     uint8_t *status;           // decode
     const uint4 *enc_ab;       // encode tables [k][r] (TA lo/hi, TB lo/hi)
     const uint32_t *enc_c;     // encode tables [k][r] (TC)
+    const uint8_t *coef;       // GF decode: parity rows P[r][k] of a non-Cauchy matrix (null: Cauchy)
     uint64_t nwin;
     uint64_t gmask[kMaxR];     // XOR: members of group g (bit j)
     uint64_t step_win;         // flat mode: (grid threads) / ncol

@@ -805,6 +805,96 @@ __device__ void plan_gf_gj(const BatchArgs &a, uint64_t w, int lane, uint8_t *re
     }
 }
 
+// General-matrix plan (FECGPU_MATRIX_VANDERMONDE and any other systematic MDS
+// generator): the parity rows P[r][k] sit in LDS; A[t][u] = P[sel_t][m_u] is
+// inverted by wave-parallel Gauss-Jordan (no pivoting: every square
+// submatrix of an MDS code's parity rows is nonsingular, so are the leading
+// minors), then folded into the decode matrix D like the Cauchy plans.
+template <int R>
+__device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int lane, uint8_t *region,
+                            const uint8_t *ex, const uint8_t *lg, const uint8_t *P, uint8_t &ne_out) {
+    const int k = a.k, r = a.r;
+    uint4 *tab = reinterpret_cast<uint4 *>(region);
+    uint32_t *tc = reinterpret_cast<uint32_t *>(region + k * R * 16);
+    uint8_t *insym = region + k * R * 20;
+    uint8_t *outsym = insym + 64;
+    const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
+    const uint64_t miss = ~pres & kmask;
+    const uint64_t rep = (pres >> k) & ((1ull << r) - 1);
+    const int e = __popcll(miss);
+    if (e == 0 || __popcll(rep) < e || e > R) {
+        if (lane == 0) {
+            ne_out = 0;
+            a.status[w] = (e == 0) ? 0 : 1;
+        }
+        return;
+    }
+    uint64_t mm = miss, rr = rep;
+    for (int i = 0; i < lane && i < e; i++) { mm &= mm - 1; rr &= rr - 1; }
+    const int my_m = (int)__ffsll((unsigned long long)mm) - 1;  // valid for lane < e
+    const int my_sel = (int)__ffsll((unsigned long long)rr) - 1;
+    if (lane < k && ((pres >> lane) & 1)) insym[__popcll(pres & kmask & ((1ull << lane) - 1))] = (uint8_t)lane;
+    if (lane < e) {
+        insym[k - e + lane] = (uint8_t)(k + my_sel);
+        outsym[lane] = (uint8_t)my_m;
+    }
+    // [A | I], lane = t*8 + u; every __shfl with the whole wave active
+    const int t = lane >> 3, u = lane & 7;
+    const int sel_t = __shfl(my_sel, t & 7, 64);
+    const int m_u = __shfl(my_m, u, 64);
+    const bool valid = (t < e) && (u < e);
+    uint32_t xl = valid ? P[sel_t * k + m_u] : 0u;
+    uint32_t xr = (valid && t == u) ? 1u : 0u;
+    bool singular = false;
+    for (int c = 0; c < e; c++) {
+        const uint32_t piv = __shfl(xl, c * 8 + c, 64);
+        if (piv == 0) { singular = true; break; }
+        const uint32_t ip = gf_inv_lds(ex, lg, piv);
+        if (t == c) {
+            xl = gf_mul_lds(ex, lg, xl, ip);
+            xr = gf_mul_lds(ex, lg, xr, ip);
+        }
+        const uint32_t f = __shfl(xl, (t & 7) * 8 + c, 64);
+        const uint32_t rl = __shfl(xl, c * 8 + u, 64);
+        const uint32_t rq = __shfl(xr, c * 8 + u, 64);
+        if (t != c && valid) {
+            xl ^= gf_mul_lds(ex, lg, f, rl);
+            xr ^= gf_mul_lds(ex, lg, f, rq);
+        }
+    }
+    if (singular) {
+        if (lane == 0) { ne_out = 0; a.status[w] = 1; }
+        return;
+    }
+    WAVE_SYNC();
+    // D[u][q] for idx = u*k + q; Ainv[u][t] = xr of lane u*8 + t
+    const int kr = k - e;
+    for (int base = 0; base < e * k; base += 64) {
+        const int idx = base + lane;
+        const int du = idx / k, dq = idx - du * k;
+        const bool live = idx < e * k;
+        const bool is_src = dq < kr;
+        const uint32_t j = (live && is_src) ? insym[dq] : 0u;
+        uint32_t csrc = 0;
+        for (int tt = 0; tt < e; tt++) {
+            const uint32_t ai = __shfl(xr, ((du & 7) * 8 + tt) & 63, 64);
+            const int st = __shfl(my_sel, tt, 64);
+            if (is_src) csrc ^= gf_mul_lds(ex, lg, ai, P[st * k + j]);
+        }
+        const uint32_t crep = __shfl(xr, ((du & 7) * 8 + (is_src ? 0 : dq - kr)) & 63, 64);
+        const uint32_t c = is_src ? csrc : crep;
+        if (live) {
+            const CoefTab ct = make_coef_tab(c);
+            tab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+            tc[dq * R + du] = ct.c;
+        }
+    }
+    if (lane == 0) {
+        ne_out = (uint8_t)e;
+        a.status[w] = 0;
+    }
+}
+
 template <int R>
 __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a) {
     extern __shared__ uint4 dyn[];
@@ -812,11 +902,14 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
     __shared__ uint8_t s_log[256];
     __shared__ GroupLds g;
     __shared__ uint8_t s_ne[kMaxWpb];
+    __shared__ uint8_t s_coef[kMaxR * kMaxK];  // general-matrix codes: parity rows P[r][k]
     constexpr int U = FECGPU_GFD_U;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
     uint8_t *regions = reinterpret_cast<uint8_t *>(dyn);
     for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
     for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
+    if (a.coef)
+        for (int i = tid; i < a.r * k; i += kBlock) s_coef[i] = a.coef[i];
     __syncthreads();
     for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi;
          xr.cur += xr.step) {
@@ -835,8 +928,13 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
             for (int i = 0, wl = wave; wl < nb; i++, wl += NW) {
                 const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl, i);
                 const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pl >> 32), i);
-                plan_gf<R>(a, w0 + wl, ((uint64_t)hi << 32) | lo, lane, regions + (size_t)wl * a.win_lds,
-                           s_exp, s_log, s_ne[wl]);
+                const uint64_t pw = ((uint64_t)hi << 32) | lo;
+                if (a.coef)  // wave-uniform: one code per launch
+                    plan_gf_mat<R>(a, w0 + wl, pw, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log,
+                                   s_coef, s_ne[wl]);
+                else
+                    plan_gf<R>(a, w0 + wl, pw, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log,
+                               s_ne[wl]);
             }
         }
 #endif

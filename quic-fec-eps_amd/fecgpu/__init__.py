@@ -27,7 +27,7 @@ LIB_PATH = os.environ.get("FECGPU_LIB") or os.path.join(os.path.dirname(_HERE), 
 ERR_DONE, ERR_BUFFER_TOO_SHORT, ERR_INVALID_ARG = -1, -2, -3
 ERR_UNSUPPORTED, ERR_DEVICE, ERR_UNRECOVERABLE = -4, -5, -6
 SCHEME_XOR, SCHEME_GF256 = 0, 1
-MATRIX_CAUCHY = 0
+MATRIX_CAUCHY, MATRIX_VANDERMONDE = 0, 1
 FRAMING_FIXED, FRAMING_LENPREFIX = 0, 1
 STATUS_OK, STATUS_UNRECOVERABLE = 0, 1
 F_HOST_PTRS, F_SYNC = 1, 2
@@ -180,15 +180,18 @@ _lib()  # fail loudly at import when the native library is missing
 
 @dataclass(frozen=True)
 class Code:
-    """fecgpu_code: scheme 'xor' | 'gf256', k sources, r repairs per window."""
+    """fecgpu_code: scheme 'xor' | 'gf256', k sources, r repairs per window;
+    GF matrix 'cauchy' (default) | 'vandermonde'."""
     scheme: str
     k: int
     r: int
     framing: str = "fixed"
+    matrix: str = "cauchy"
 
     @property
     def c(self) -> fecgpu_code:
-        return fecgpu_code(SCHEME_XOR if self.scheme == "xor" else SCHEME_GF256, MATRIX_CAUCHY,
+        return fecgpu_code(SCHEME_XOR if self.scheme == "xor" else SCHEME_GF256,
+                           MATRIX_VANDERMONDE if self.matrix == "vandermonde" else MATRIX_CAUCHY,
                            FRAMING_FIXED if self.framing == "fixed" else FRAMING_LENPREFIX,
                            self.k, self.r, 0x11D)
 

@@ -29,6 +29,10 @@ CASES = [
     ("gf_k10r7_L33_iid", "gf", 10, 7, 33, 2, 8, 100),
     ("gf_k32r8_L48_iid", "gf", 32, 8, 48, 2, 4, 1 << 20),
     ("gf_k56r8_L16_exact", "gf", 56, 8, 16, 1, 2, 9),
+    # systematic Vandermonde rows (FECGPU_MATRIX_VANDERMONDE), scheme id 2
+    ("vdm_k5r5_L24_iid", "gf-vdm", 5, 5, 24, 2, 8, 40),
+    ("vdm_k16r4_L64_exact", "gf-vdm", 16, 4, 64, 1, 4, 7),
+    ("vdm_k32r8_L40_iid", "gf-vdm", 32, 8, 40, 2, 4, 1 << 21),
 ]
 
 
@@ -56,11 +60,15 @@ def make(name, scheme, k, r, L, erasure, nwin, w0):
         dec[i] = out
     np.savez_compressed(os.path.join(HERE, name + ".npz"), src=src, repair=rep, present=pres,
                         status=status, decoded=dec,
-                        meta=np.array([0 if scheme == "xor" else 1, k, r, L, erasure, nwin, w0,
-                                       SEED], np.int64))
+                        meta=np.array([{"xor": 0, "gf": 1, "gf-vdm": 2}[scheme], k, r, L, erasure,
+                                       nwin, w0, SEED], np.int64))
 
 
 if __name__ == "__main__":
+    # optional names: regenerate only those fixtures (others keep their bytes)
+    want = set(sys.argv[1:])
     for c in CASES:
+        if want and c[0] not in want:
+            continue
         make(*c)
         print("wrote", c[0])

@@ -57,7 +57,8 @@ def test_header_compiles_as_c():
     (1, 4, 0, 0, 0, 0, fecgpu.ERR_INVALID_ARG),
     (2, 4, 1, 0, 0, 0, fecgpu.ERR_INVALID_ARG),    # unknown scheme
     (1, 4, 1, 2, 0, 0, fecgpu.ERR_INVALID_ARG),    # unknown framing
-    (1, 4, 1, 0, 1, 0, fecgpu.ERR_UNSUPPORTED),    # Vandermonde not built
+    (1, 4, 1, 0, 1, 0, 0),                         # systematic Vandermonde
+    (1, 4, 1, 0, 2, 0, fecgpu.ERR_UNSUPPORTED),    # unknown matrix
     (1, 4, 1, 0, 0, 0x11B, fecgpu.ERR_UNSUPPORTED),
 ])
 def test_code_check(scheme, k, r, framing, matrix, poly, want):

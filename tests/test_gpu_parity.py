@@ -47,11 +47,11 @@ def _cmp_emitted(a: np.ndarray, b: np.ndarray, S: np.ndarray, what: str):
             raise AssertionError(f"{what}: window {w} differs at (sym, byte) {bad[:5].tolist()}")
 
 
-def gpu_run(ctx, scheme, k, r, wins, S, present, uniform: bool, poison=0xAB):
+def gpu_run(ctx, scheme, k, r, wins, S, present, uniform: bool, poison=0xAB, matrix="cauchy"):
     """Encode on the GPU, poison erased symbols, decode on the GPU.
     Returns (encoded, decoded, status) as numpy."""
     nwin, n, stride = wins.shape
-    code = fecgpu.Code(scheme, k, r)
+    code = fecgpu.Code(scheme, k, r, matrix=matrix)
     d = torch.from_numpy(wins.copy()).cuda()
     sl = torch.from_numpy(S.astype(np.int32)).cuda()
     kw = dict(sym_len=None, sym_len_all=int(S[0])) if uniform else dict(sym_len=sl)
@@ -142,11 +142,12 @@ def test_golden_fixtures(ctx, path):
     z = np.load(path)
     scheme_id, k, r, L, era, nwin, w0, seed = (int(x) for x in z["meta"])
     scheme = "xor" if scheme_id == 0 else "gf256"
+    matrix = "vandermonde" if scheme_id == 2 else "cauchy"
     stride = O.round_up(L, 16)
     wins = np.zeros((nwin, k + r, stride), np.uint8)
     wins[:, :k, :L] = z["src"]
     S = np.full(nwin, L, np.uint32)
-    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, z["present"], uniform=True)
+    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, z["present"], uniform=True, matrix=matrix)
     assert np.array_equal(ge[:, k:, :L], z["repair"])
     assert np.array_equal(gs, z["status"])
     ok = z["status"] == 0
@@ -297,6 +298,81 @@ def test_encode_split_layout_vs_oracle(ctx, scheme, k, r, wl, L):
     got = np.concatenate([src.cpu().numpy(), rep.cpu().numpy()], axis=1)
     assert np.array_equal(got[:, :k], wins[:, :k])
     _cmp_emitted(got, oe, S, "encode_split")
+
+
+VDM_CASES = [(5, 5, 0, 2, 1, 9), (8, 2, 0, 1200, 1, 64), (16, 4, 0, 1200, 2, 64),
+             (32, 8, 1, 0, 2, 12), (56, 8, 0, 64, 1, 9), (3, 7, 0, 33, 2, 40)]
+
+
+@pytest.mark.parametrize("k,r,wl,L,era,nwin", VDM_CASES)
+def test_vandermonde_matrix_vs_oracle(ctx, k, r, wl, L, era, nwin):
+    """FECGPU_MATRIX_VANDERMONDE (systematic Vandermonde rows, decode through the
+    general-matrix Gauss-Jordan plan) vs the oracle: repairs, status and recovered
+    bytes."""
+    S = O.sym_lens(wl, SEED, 0, nwin, k, L)
+    stride = O.round_up(int(S.max()), 16)
+    wins = O.make_windows(wl, SEED, 0, nwin, k, r, L, stride)
+    present = O.presents(era, SEED, 0, nwin, O.GF256_VDM, k, r)
+    code = fecgpu.Code("gf256", k, r, matrix="vandermonde")
+    d = torch.from_numpy(wins.copy()).cuda()
+    kw = dict(sym_len_all=int(S[0])) if wl == 0 else dict(sym_len=torch.from_numpy(S.astype(np.int32)).cuda())
+    ctx.encode_batch(code, d, nwin=nwin, stride=stride, **kw)
+    torch.cuda.synchronize()
+    ge = d.cpu().numpy()
+    oe = wins.copy()
+    O.encode_batch(O.GF256_VDM, k, r, S, oe, 4)
+    _cmp_emitted(ge, oe, S, "vdm encode")
+    od = oe.copy()
+    O.erase(od, present, k, r, fill=0xAB)
+    os_ = O.decode_batch(O.GF256_VDM, k, r, S, od, present, 4)
+    mask = torch.from_numpy(np.array([[(int(p) >> i) & 1 for i in range(k + r)] for p in present],
+                                     dtype=bool)).cuda()
+    d[~mask] = 0xAB
+    st = torch.full((nwin,), 7, dtype=torch.uint8, device="cuda")
+    ctx.decode_batch(code, d, torch.from_numpy(present.astype(np.int64)).cuda(), st, nwin=nwin,
+                     stride=stride, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), os_)
+    _cmp_emitted(d.cpu().numpy(), od, S, "vdm decode")
+
+
+def test_vandermonde_kat_on_gpu(ctx):
+    """The published 5+5 known answer through the GPU encode."""
+    code = fecgpu.Code("gf256", 5, 5, matrix="vandermonde")
+    win = np.zeros((1, 10, 16), np.uint8)
+    win[0, :5, :2] = [[0, 1], [4, 5], [2, 3], [6, 7], [8, 9]]
+    d = torch.from_numpy(win).cuda()
+    ctx.encode_batch(code, d, nwin=1, stride=16, sym_len_all=2)
+    torch.cuda.synchronize()
+    assert d.cpu().numpy()[0, 5:, :2].tolist() == [[12, 13], [10, 11], [14, 15], [90, 91], [94, 95]]
+
+
+@pytest.mark.parametrize("k,r", [(4, 3), (5, 5), (6, 2)])
+def test_vandermonde_every_erasure_pattern(ctx, k, r):
+    n = k + r
+    nwin = 1 << n
+    wins = np.repeat(O.make_windows(0, SEED, 3, 1, k, r, 40, 48), nwin, axis=0)
+    S = np.full(nwin, 40, np.uint32)
+    present = np.arange(nwin, dtype=np.uint64)
+    code = fecgpu.Code("gf256", k, r, matrix="vandermonde")
+    d = torch.from_numpy(wins.copy()).cuda()
+    ctx.encode_batch(code, d, nwin=nwin, stride=48, sym_len_all=40)
+    torch.cuda.synchronize()
+    enc = d.cpu().numpy()
+    mask = torch.from_numpy(np.array([[(p >> i) & 1 for i in range(n)] for p in range(nwin)],
+                                     dtype=bool)).cuda()
+    d[~mask] = 0x3C
+    st = torch.full((nwin,), 7, dtype=torch.uint8, device="cuda")
+    ctx.decode_batch(code, d, torch.from_numpy(present.astype(np.int64)).cuda(), st, nwin=nwin,
+                     stride=48, sym_len_all=40)
+    torch.cuda.synchronize()
+    got, st = d.cpu().numpy(), st.cpu().numpy()
+    for p in range(nwin):
+        miss = sum(1 for j in range(k) if not (p >> j) & 1)
+        reps = sum(1 for i in range(r) if (p >> (k + i)) & 1)
+        assert st[p] == (0 if miss <= reps else 1), p
+        if st[p] == 0:
+            assert np.array_equal(got[p, :k, :40], enc[p, :k, :40]), p
 
 
 def test_zero_windows_and_errors(ctx):

@@ -19,10 +19,10 @@ def O(oracle_lib):
 
 
 def sid(O, s):
-    return O.XOR if s == "xor" else O.GF256
+    return {"xor": O.XOR, "gf": O.GF256, "gf-vdm": O.GF256_VDM}[s]
 
 
-@pytest.mark.parametrize("scheme", ["xor", "gf"])
+@pytest.mark.parametrize("scheme", ["xor", "gf", "gf-vdm"])
 @pytest.mark.parametrize("wl,L,k,r,era", [(0, 100, 8, 2, 1), (1, 0, 6, 3, 2), (0, 64, 16, 4, 1),
                                            (1, 0, 4, 1, 2), (0, 1, 3, 3, 1), (0, 31, 12, 5, 2)])
 def test_c_oracle_matches_numpy(O, scheme, wl, L, k, r, era):
@@ -73,7 +73,8 @@ def test_c_oracle_reproduces_golden(O, path):
 
 
 @pytest.mark.parametrize("scheme,k,r", [("gf", 4, 3), ("gf", 6, 2), ("xor", 6, 3), ("xor", 5, 2),
-                                        ("gf", 1, 1), ("xor", 1, 1)])
+                                        ("gf", 1, 1), ("xor", 1, 1), ("gf-vdm", 4, 3),
+                                        ("gf-vdm", 5, 5), ("gf-vdm", 7, 2), ("gf-vdm", 1, 1)])
 def test_every_erasure_pattern(O, scheme, k, r):
     n = k + r
     L = 24
@@ -86,7 +87,7 @@ def test_every_erasure_pattern(O, scheme, k, r):
     st = O.decode_batch(sid(O, scheme), k, r, np.full(nwin, L, np.uint32), wins, pres)
     for p in range(nwin):
         miss = [j for j in range(k) if not (p >> j) & 1]
-        if scheme == "gf":
+        if scheme != "xor":  # MDS
             reps = sum(1 for i in range(r) if (p >> (k + i)) & 1)
             expect_ok = len(miss) <= reps
         else:

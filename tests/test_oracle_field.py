@@ -93,3 +93,37 @@ def test_cauchy_is_mds(O):
                     for i in range(e):
                         if i != c and M[i, c]:
                             M[i] ^= N.mul_table()[M[i, c]][M[c]]
+
+
+def test_vandermonde_kat(oracle_lib):
+    """FECGPU_MATRIX_VANDERMONDE pinned by the published known answer of the
+    libraries that define it (Backblaze JavaReedSolomon's construction; the 5+5
+    one-encode test of klauspost/reedsolomon and of the Rust crate
+    reed-solomon-erasure): data {0,1},{4,5},{2,3},{6,7},{8,9} -> parity
+    {12,13},{10,11},{14,15},{90,91},{94,95}.  C oracle and numpy restatement."""
+    import numpy as np
+    import np_oracle as N
+    src = np.array([[0, 1], [4, 5], [2, 3], [6, 7], [8, 9]], np.uint8)
+    want = [[12, 13], [10, 11], [14, 15], [90, 91], [94, 95]]
+    assert N.encode("gf-vdm", 5, 5, src).tolist() == want
+    win = np.zeros((1, 10, 16), np.uint8)
+    win[0, :5, :2] = src
+    oracle_lib.encode_batch(oracle_lib.GF256_VDM, 5, 5, np.array([2], np.uint32), win)
+    assert win[0, 5:, :2].tolist() == want
+    for k, r in [(5, 5), (8, 2), (16, 4), (32, 8), (56, 8), (3, 7)]:
+        assert np.array_equal(N.vandermonde(k, r), oracle_lib.vandermonde(k, r))
+
+
+@pytest.mark.parametrize("k,r", [(4, 4), (6, 3), (5, 5), (10, 2)])
+def test_vandermonde_parity_rows_are_mds(oracle_lib, k, r):
+    """Every square submatrix of the parity rows is nonsingular (systematic MDS),
+    which is also why the GPU decode plan needs no pivoting for this matrix."""
+    import itertools
+    import numpy as np
+    import np_oracle as N
+    P = oracle_lib.vandermonde(k, r)
+    for e in range(1, min(k, r) + 1):
+        for rows in itertools.combinations(range(r), e):
+            for cols in itertools.combinations(range(k), e):
+                A = P[np.ix_(rows, cols)]
+                N._gj_inverse(A)  # raises StopIteration if singular
