@@ -34,7 +34,10 @@
 // GF bodies: input rows loaded per batch.  Swept on the box (scripts/sweep.py):
 // r = 4 runs best with 2 rows in flight per lane (fewer bytes in flight keep
 // HBM efficient), r = 8 with 8 (its long VALU phase needs more loads queued).
-#define FECGPU_GF_U (R <= 4 ? 2 : 8)
+#ifndef FECGPU_GF_U_HI
+#define FECGPU_GF_U_HI 8
+#endif
+#define FECGPU_GF_U (R <= 4 ? 2 : FECGPU_GF_U_HI)
 #endif
 #ifndef FECGPU_GFD_U
 // GF decode: input rows loaded per batch.  8 at every r: decode's input rows
