@@ -525,6 +525,16 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
             p.wpb = choose_wpb(ncol, 0, 0);
         }
     }
+    // Per-window lengths (group mode): a group's last pass is partly idle by
+    // half a pass on average, so give each group >= 16 passes at the longest
+    // window (cfg4 encode: 5 -> 8 windows per group, -4 %, scripts/ab.py r01).
+    if (sym_len && !win_off && ncol && !p.flat) {
+        const int want = (int)((16u * kBlock + ncol - 1) / ncol);
+        int cap = kMaxWpb;
+        if (p.win_lds) cap = std::max(1, (int)((40u << 10) / p.win_lds));
+        p.wpb = std::max(p.wpb, std::min(want, cap));
+        if (p.win_lds) p.lds_bytes = p.win_lds * (uint32_t)p.wpb;
+    }
     if (remote) {  // PCIe-latency bound: as many workgroups as windows
         p.remote = true;
         p.flat = false;
@@ -533,7 +543,10 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
     }
     if (ctx->wpb_override > 0 && !p.flat) {
         p.wpb = std::min(ctx->wpb_override, kMaxWpb);
-        if (p.win_lds) p.lds_bytes = p.win_lds * (uint32_t)p.wpb;
+        if (p.win_lds) {  // per-window decode regions must fit the workgroup's LDS
+            p.wpb = std::max(1, std::min<int>(p.wpb, (int)((96u << 10) / p.win_lds)));
+            p.lds_bytes = p.win_lds * (uint32_t)p.wpb;
+        }
     }
     a.wpb = p.wpb;
     a.win_lds = p.win_lds;
