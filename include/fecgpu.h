@@ -75,6 +75,7 @@ enum fecgpu_status { FECGPU_STATUS_OK = 0, FECGPU_STATUS_UNRECOVERABLE = 1 };
 
 #define FECGPU_MAX_K 64
 #define FECGPU_MAX_R 8
+#define FECGPU_MAX_SYMBOL (1u << 24) /* symbol length / pitch limit (QUIC packets are < 64 KiB) */
 
 typedef struct fecgpu_code {
     uint32_t scheme;  /* enum fecgpu_scheme */

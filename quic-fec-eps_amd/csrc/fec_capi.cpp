@@ -344,6 +344,7 @@ ssize_t validate_batch(const fecgpu_code *code, const void *win, const uint32_t 
         if (!sym_len && sym_len_all > stride) return FECGPU_ERR_BUFFER_TOO_SHORT;
     }
     if (!sym_len && sym_len_all == 0) return FECGPU_ERR_INVALID_ARG;
+    if (stride > FECGPU_MAX_SYMBOL || sym_len_all > FECGPU_MAX_SYMBOL) return FECGPU_ERR_UNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(win) & 15) != 0) return FECGPU_ERR_INVALID_ARG;
     return 0;
 }

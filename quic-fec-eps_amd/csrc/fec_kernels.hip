@@ -199,6 +199,7 @@ __device__ __forceinline__ void win_geom(const BatchArgs &a, uint64_t w, uint64_
             stride = a.off_stride;
             S = min(S, stride);  // a symbol never spills into the next row
         } else {
+            S = min(S, (uint32_t)FECGPU_MAX_SYMBOL);  // keeps group prefix sums in 32 bits
             stride = (S + 15u) & ~15u;
         }
     } else {

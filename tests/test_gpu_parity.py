@@ -388,6 +388,9 @@ def test_zero_windows_and_errors(ctx):
     with pytest.raises(fecgpu.FecError) as e:
         ctx.encode_batch(fecgpu.Code("gf256", 60, 9), d, nwin=1, stride=64, sym_len_all=10)
     assert e.value.code == fecgpu.ERR_UNSUPPORTED
+    with pytest.raises(fecgpu.FecError) as e:  # pitch over FECGPU_MAX_SYMBOL (16 MiB)
+        ctx.encode_batch(code, d, nwin=1, stride=1 << 25, sym_len_all=10)
+    assert e.value.code == fecgpu.ERR_UNSUPPORTED
 
 
 # ------------------------------------------------ workload generators ---
