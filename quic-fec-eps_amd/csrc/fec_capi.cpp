@@ -11,6 +11,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -100,6 +101,7 @@ constexpr int kPipeSlots = 3;
 
 // Streams, events and device staging slots of the host-pointer pipeline.
 struct HostPipe {
+    int dev = 0;
     hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
     hipEvent_t h2d_done[kPipeSlots] = {}, comp_done[kPipeSlots] = {}, d2h_done[kPipeSlots] = {};
     uint8_t *slot[kPipeSlots] = {};
@@ -115,6 +117,7 @@ struct fecgpu_ctx {
     std::map<std::tuple<int, int, int, int>, EncTables> enc;
     // host-pointer staging per device
     std::map<int, std::pair<void *, size_t>> stage;
+    // host-pointer pipelines, one per entry of devs (keyed by that index)
     std::map<int, HostPipe> pipes;
     // tuning knobs (fecgpu_ctx_set_tuning): 0 = automatic
     int grid_mult = 0;
@@ -238,7 +241,7 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
     }
     for (auto &kv : ctx->pipes) {
         HostPipe &hp = kv.second;
-        (void)hipSetDevice(kv.first);
+        (void)hipSetDevice(hp.dev);
         if (hp.h2d) (void)hipStreamSynchronize(hp.d2h);
         for (int i = 0; i < kPipeSlots; i++) {
             if (hp.slot[i]) (void)hipFree(hp.slot[i]);
@@ -388,9 +391,44 @@ size_t host_window_bytes(const fecgpu_code *code, const uint64_t *win_off, const
 
 ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
                       hipStream_t s, bool remote = false);
-ssize_t run_host_pipelined(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
-                           const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
-                           uint64_t nwin, const uint64_t *present, uint8_t *status);
+ssize_t run_host_pipelined(fecgpu_ctx *ctx, int di, const fecgpu_code *code, bool decode,
+                           uint8_t *win, const uint32_t *sym_len, uint32_t sym_len_all,
+                           uint32_t stride, uint64_t nwin, const uint64_t *present,
+                           uint8_t *status);
+
+// Host-pointer batch over every device of the ctx: contiguous window ranges
+// [d*n/D, (d+1)*n/D), one host thread per device, each with its own pipeline
+// (windows are independent, nothing is exchanged).
+ssize_t run_host_multi(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
+                       const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
+                       uint64_t nwin, const uint64_t *present, uint8_t *status) {
+    const int nd = (int)ctx->devs.size();
+    if (nd == 1)
+        return run_host_pipelined(ctx, 0, code, decode, win, sym_len, sym_len_all, stride, nwin,
+                                  present, status);
+    for (int d = 0; d < nd; d++) ctx->pipes[d].dev = ctx->devs[d];  // create entries up front
+    const size_t wbytes = (size_t)(code->k + code->r) * stride;
+    std::vector<ssize_t> rcs(nd, 0);
+    std::vector<std::string> errs(nd);
+    auto part = [&](int d) {
+        const uint64_t lo = nwin * d / nd, hi = nwin * (d + 1) / nd;
+        if (hi > lo)
+            rcs[d] = run_host_pipelined(ctx, d, code, decode, win + lo * wbytes,
+                                        sym_len ? sym_len + lo : nullptr, sym_len_all, stride, hi - lo,
+                                        present ? present + lo : nullptr, status ? status + lo : nullptr);
+        if (rcs[d] < 0) errs[d] = g_last_error;  // thread_local: carry it back
+    };
+    std::vector<std::thread> th;
+    for (int d = 1; d < nd; d++) th.emplace_back(part, d);
+    part(0);
+    for (auto &t : th) t.join();
+    for (int d = 0; d < nd; d++)
+        if (rcs[d] < 0) {
+            g_last_error = errs[d];
+            return rcs[d];
+        }
+    return (ssize_t)nwin;
+}
 
 ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
                   const uint64_t *win_off, const uint32_t *sym_len, uint32_t sym_len_all,
@@ -403,10 +441,10 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
     if (nwin == 0) return 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
-    // host pointers, uniform layout: chunked copy/compute pipeline
+    // host pointers, uniform layout: chunked copy/compute pipeline on every device
     if ((flags & FECGPU_F_HOST_PTRS) && !win_off)
-        return run_host_pipelined(ctx, code, decode, win, sym_len, sym_len_all, stride, nwin,
-                                  present, status);
+        return run_host_multi(ctx, code, decode, win, sym_len, sym_len_all, stride, nwin, present,
+                              status);
     // host pointers, ragged layout: stage everything once, synchronously
     HostStage hs;
     int prev_dev = -1;
@@ -569,16 +607,18 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
 // store their outputs (repairs / recovered sources) straight into them over
 // PCIe instead: decode then moves e rows per window device->host instead of
 // k, and the D2H direction carries only the bytes that changed.
-ssize_t run_host_pipelined(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
-                           const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
-                           uint64_t nwin, const uint64_t *present, uint8_t *status) {
+ssize_t run_host_pipelined(fecgpu_ctx *ctx, int di, const fecgpu_code *code, bool decode,
+                           uint8_t *win, const uint32_t *sym_len, uint32_t sym_len_all,
+                           uint32_t stride, uint64_t nwin, const uint64_t *present,
+                           uint8_t *status) {
     const int k = code->k, r = code->r;
     const size_t wbytes = (size_t)(k + r) * stride;
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev), "hipGetDevice");
-    const int dev = ctx->devs[0];
+    const int dev = ctx->devs[di];
     HIP_TRY(hipSetDevice(dev), "hipSetDevice");
-    HostPipe &hp = ctx->pipes[dev];
+    HostPipe &hp = ctx->pipes[di];
+    hp.dev = dev;
     const uint64_t cw_max = std::max<uint64_t>(1, ((uint64_t)ctx->host_chunk_mb << 20) / wbytes);
     const size_t need = cw_max * wbytes;
     const size_t o_len = (need + 255) & ~size_t(255);

@@ -375,6 +375,43 @@ def test_vandermonde_every_erasure_pattern(ctx, k, r):
             assert np.array_equal(got[p, :k, :40], enc[p, :k, :40]), p
 
 
+@pytest.mark.parametrize("devs", [[0, 0], [0, 0, 0]])
+def test_multi_device_ctx_host_batches(ctx, devs):
+    """A ctx over several devices splits host-pointer batches into contiguous
+    window ranges, one host thread and pipeline per device (the one-GPU box lists
+    device 0 several times): same repairs, status and recovered bytes as the
+    oracle, for uniform and per-window lengths."""
+    multi = fecgpu.Context(devs)
+    try:
+        for scheme, k, r, wl, L, era in (("xor", 8, 2, 0, 1200, 1), ("gf256", 32, 8, 1, 0, 2)):
+            nwin = 61
+            S = O.sym_lens(wl, SEED, 5, nwin, k, L)
+            stride = O.round_up(int(S.max()), 16)
+            wins = O.make_windows(wl, SEED, 5, nwin, k, r, L, stride)
+            present = O.presents(era, SEED, 5, nwin, _scheme(scheme), k, r)
+            oe, od, os_ = oracle_run(scheme, k, r, wins, S, present)
+            code = fecgpu.Code(scheme, k, r)
+            buf = fecgpu.PinnedBuffer(wins.nbytes)
+            h = buf.array.reshape(wins.shape)
+            h[:] = wins
+            kw = dict(sym_len_all=L) if wl == 0 else dict(sym_len=S)
+            multi.set_tuning("host_chunk_mb", 1)
+            multi.encode_batch(code, h, nwin=nwin, stride=stride, flags=fecgpu.F_HOST_PTRS, **kw)
+            enc = h.copy()
+            O.erase(h, present, k, r, fill=0xAB)
+            st = np.full(nwin, 9, np.uint8)
+            multi.decode_batch(code, h, present, st, nwin=nwin, stride=stride,
+                               flags=fecgpu.F_HOST_PTRS, **kw)
+            dec = h.copy()
+            del h
+            buf.close()
+            _cmp_emitted(enc, oe, S, f"multi encode {scheme}")
+            assert np.array_equal(st, os_)
+            _cmp_emitted(dec, od, S, f"multi decode {scheme}")
+    finally:
+        multi.close()
+
+
 def test_zero_windows_and_errors(ctx):
     code = fecgpu.Code("gf256", 4, 2)
     d = torch.zeros(4096, dtype=torch.uint8, device="cuda")
