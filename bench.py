@@ -86,8 +86,9 @@ def log(msg: str) -> None:
 
 
 def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
-    """Time the CPU oracle (oracle/fec_oracle.c, kind "port") on a bounded
-    sample of the same workload: same packets, same erasure stream."""
+    """Time the CPU codec (oracle/fec_cpu_simd.c: the oracle's contract with
+    AVX2 nibble tables / GFNI affine products, ISA-L style; kind "port") on a
+    bounded sample of the same workload: same packets, same erasure stream."""
     sys.path.insert(0, os.path.join(_ROOT, "oracle"))
     import oracle as O  # test/baseline infrastructure only
 
@@ -102,8 +103,8 @@ def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
         wins, S, pres, src = O.make_batch(cfg.workload, workloads.SEED, 0, nw, scheme, cfg.erasure,
                                           cfg.k, cfg.r, cfg.L, cfg.stride, threads)
         t0 = time.perf_counter()
-        O.encode_batch(scheme, cfg.k, cfg.r, S, wins, threads)
-        O.decode_batch(scheme, cfg.k, cfg.r, S, wins, pres, threads)
+        O.encode_batch_simd(scheme, cfg.k, cfg.r, S, wins, threads)
+        O.decode_batch_simd(scheme, cfg.k, cfg.r, S, wins, pres, threads)
         return time.perf_counter() - t0, src
 
     nw = 4 * threads
@@ -124,6 +125,8 @@ def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
             break
     dt, src = tot_dt, tot_src
     return {"value": round(src / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "codec": f"oracle/fec_cpu_simd.c ({O.SIMD_NAMES[O.simd_level()]}; equal outputs to the "
+                     f"scalar oracle: tests/test_oracle_simd.py)",
             "sample": f"{nw} windows of {cfg.name} (encode+decode, same packets and erasures), "
                       f"{dt:.1f} s on {threads} host threads"}
 

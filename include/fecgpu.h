@@ -96,8 +96,10 @@ const char *fecgpu_last_error(void);
 ssize_t     fecgpu_code_check(const fecgpu_code *code);
 
 /* ctx over devs[0..ndev-1] (NULL/0 = current device).  Batches with device
- * pointers run on the device of the pointers; host-pointer batches are split
- * over the ctx's devices. */
+ * pointers run on the current device (the one the pointers live on);
+ * host-pointer batches with the uniform layout are split into contiguous
+ * window ranges, one host thread and copy/compute pipeline per listed device
+ * (windows are independent: nothing is exchanged between devices). */
 ssize_t fecgpu_ctx_new(const int *devs, int ndev, fecgpu_ctx **out);
 void    fecgpu_ctx_free(fecgpu_ctx *ctx);
 /* Pinned (page-locked) host memory for FECGPU_F_HOST_PTRS buffers: with it the

@@ -1,0 +1,366 @@
+/*
+ * fec_cpu_simd.c — the CPU baseline codec (BASELINE.md "CPU baseline plan"):
+ * the same coding contract as fec_oracle.c, vectorised
+ * the way a tuned CPU FEC library is (ISA-L style):
+ *   level 1  AVX2: GF(2^8) products by split-nibble tables (vpshufb), several
+ *            repair / recovered rows accumulated per pass over an input row;
+ *   level 2  AVX2 + GFNI: one vgf2p8affineqb per product (the multiply-by-c
+ *            bit matrix; GFNI's own field polynomial is not used);
+ *   level 0  scalar (fec_oracle.c's byte loops).
+ * TEST / BASELINE INFRASTRUCTURE ONLY: bench.py's cpu_baseline leg times it
+ * and tests/test_oracle_simd.py checks it against the scalar oracle.  The
+ * product (libfecgpu.so) never links it.
+ */
+#include <immintrin.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fec_oracle.h"
+
+static int g_level = -1;  /* -1: detect */
+
+int orc_simd_detect(void) {
+    __builtin_cpu_init();
+    if (!__builtin_cpu_supports("avx2")) return 0;
+    return __builtin_cpu_supports("gfni") ? 2 : 1;
+}
+
+int orc_simd_level(void) { return g_level < 0 ? orc_simd_detect() : g_level; }
+
+/* force a level (tests); -1 restores detection.  Clamped to what the CPU has. */
+void orc_simd_set_level(int level) {
+    const int hw = orc_simd_detect();
+    g_level = level < 0 ? -1 : (level > hw ? hw : level);
+}
+
+/* ------------------------------------------------------------ tables --- */
+static uint8_t LG[256], EX[512];  /* local log / exp tables (0x11D, generator 2) */
+
+static void tables_init(void) {
+    if (EX[0]) return;
+    int x = 1;
+    for (int i = 0; i < 255; i++) {
+        EX[i] = EX[i + 255] = (uint8_t)x;
+        LG[x] = (uint8_t)i;
+        x <<= 1;
+        if (x & 0x100) x ^= 0x11D;
+    }
+    EX[510] = EX[0];
+}
+
+static inline uint8_t gmul(uint8_t a, uint8_t b) { return (a && b) ? EX[LG[a] + LG[b]] : 0; }
+static inline uint8_t ginv(uint8_t a) { return EX[255 - LG[a]]; }
+
+/* 8x8 bit-matrix transpose of the bytes of x (Hacker's Delight transpose8) */
+static inline uint64_t transpose8(uint64_t x) {
+    uint64_t t;
+    t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+    x = x ^ t ^ (t << 7);
+    t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+    x = x ^ t ^ (t << 14);
+    t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+    x = x ^ t ^ (t << 28);
+    return x;
+}
+/* per coefficient: 32-B low-nibble and high-nibble product tables (the 16-B
+ * table twice, one per AVX2 lane) and the GFNI 8x8 bit matrix */
+typedef struct {
+    uint8_t lo[32], hi[32];
+    uint64_t gfni;
+} coef_t;
+
+static void coef_make(uint8_t c, coef_t *t) {
+    uint8_t p[8];  /* c * 2^b: the product is linear in the bits of x */
+    p[0] = c;
+    for (int b = 1; b < 8; b++) p[b] = (uint8_t)((p[b - 1] << 1) ^ ((p[b - 1] & 0x80) ? 0x1D : 0));
+    t->lo[0] = t->hi[0] = 0;
+    for (int x = 1; x < 16; x++) {
+        const int b = __builtin_ctz(x);
+        t->lo[x] = (uint8_t)(t->lo[x & (x - 1)] ^ p[b]);
+        t->hi[x] = (uint8_t)(t->hi[x & (x - 1)] ^ p[b + 4]);
+    }
+    memcpy(t->lo + 16, t->lo, 16);
+    memcpy(t->hi + 16, t->hi, 16);
+    /* vgf2p8affineqb: result bit i = parity(qword byte (7 - i) & x), so byte
+     * 7 - i holds row i = sum_b bit_i(c * 2^b) << b: the transpose of the
+     * matrix whose byte b is c * 2^b, bytes reversed */
+    uint64_t m = 0;
+    for (int b = 0; b < 8; b++) m |= (uint64_t)p[b] << (8 * b);
+    t->gfni = __builtin_bswap64(transpose8(m));
+}
+
+/* out[m] = sum_j tab[j * nout + m] * in[j] over bytes [0, n) for nout <= 8;
+ * always inlined into a switch on nout so the accumulators stay in registers */
+__attribute__((target("avx2"), always_inline)) static inline void dot_avx2_n(
+    int nin, const uint8_t *const *in, const int nout, uint8_t *const *out, const coef_t *tab,
+    uint32_t n) {
+    const __m256i mask = _mm256_set1_epi8(0x0f);
+    uint32_t p = 0;
+    for (; p + 32 <= n; p += 32) {
+        __m256i acc[8];
+        for (int m = 0; m < nout; m++) acc[m] = _mm256_setzero_si256();
+        for (int j = 0; j < nin; j++) {
+            const __m256i d = _mm256_loadu_si256((const __m256i *)(in[j] + p));
+            const __m256i lo = _mm256_and_si256(d, mask);
+            const __m256i hi = _mm256_and_si256(_mm256_srli_epi64(d, 4), mask);
+            const coef_t *t = tab + (size_t)j * nout;
+            for (int m = 0; m < nout; m++) {
+                const __m256i pl = _mm256_shuffle_epi8(_mm256_loadu_si256((const __m256i *)t[m].lo), lo);
+                const __m256i ph = _mm256_shuffle_epi8(_mm256_loadu_si256((const __m256i *)t[m].hi), hi);
+                acc[m] = _mm256_xor_si256(acc[m], _mm256_xor_si256(pl, ph));
+            }
+        }
+        for (int m = 0; m < nout; m++) _mm256_storeu_si256((__m256i *)(out[m] + p), acc[m]);
+    }
+    for (; p < n; p++)  /* tail bytes */
+        for (int m = 0; m < nout; m++) {
+            uint8_t v = 0;
+            for (int j = 0; j < nin; j++) v ^= (uint8_t)(tab[(size_t)j * nout + m].lo[in[j][p] & 15] ^
+                                                         tab[(size_t)j * nout + m].hi[in[j][p] >> 4]);
+            out[m][p] = v;
+        }
+}
+
+__attribute__((target("avx2,gfni"), always_inline)) static inline void dot_gfni_n(
+    int nin, const uint8_t *const *in, const int nout, uint8_t *const *out, const coef_t *tab,
+    uint32_t n) {
+    uint32_t p = 0;
+    for (; p + 32 <= n; p += 32) {
+        __m256i acc[8];
+        for (int m = 0; m < nout; m++) acc[m] = _mm256_setzero_si256();
+        for (int j = 0; j < nin; j++) {
+            const __m256i d = _mm256_loadu_si256((const __m256i *)(in[j] + p));
+            const coef_t *t = tab + (size_t)j * nout;
+            for (int m = 0; m < nout; m++)
+                acc[m] = _mm256_xor_si256(
+                    acc[m], _mm256_gf2p8affine_epi64_epi8(d, _mm256_set1_epi64x((long long)t[m].gfni), 0));
+        }
+        for (int m = 0; m < nout; m++) _mm256_storeu_si256((__m256i *)(out[m] + p), acc[m]);
+    }
+    for (; p < n; p++)
+        for (int m = 0; m < nout; m++) {
+            uint8_t v = 0;
+            for (int j = 0; j < nin; j++) v ^= (uint8_t)(tab[(size_t)j * nout + m].lo[in[j][p] & 15] ^
+                                                         tab[(size_t)j * nout + m].hi[in[j][p] >> 4]);
+            out[m][p] = v;
+        }
+}
+
+static void dot_scalar(int nin, const uint8_t *const *in, int nout, uint8_t *const *out,
+                       const coef_t *tab, uint32_t n) {
+    for (uint32_t p = 0; p < n; p++)
+        for (int m = 0; m < nout; m++) {
+            uint8_t v = 0;
+            for (int j = 0; j < nin; j++) v ^= (uint8_t)(tab[(size_t)j * nout + m].lo[in[j][p] & 15] ^
+                                                         tab[(size_t)j * nout + m].hi[in[j][p] >> 4]);
+            out[m][p] = v;
+        }
+}
+
+#define DOT_SWITCH(FN)                                                   \
+    switch (nout) {                                                      \
+        case 1: FN(nin, in, 1, out, tab, n); break;                      \
+        case 2: FN(nin, in, 2, out, tab, n); break;                      \
+        case 3: FN(nin, in, 3, out, tab, n); break;                      \
+        case 4: FN(nin, in, 4, out, tab, n); break;                      \
+        case 5: FN(nin, in, 5, out, tab, n); break;                      \
+        case 6: FN(nin, in, 6, out, tab, n); break;                      \
+        case 7: FN(nin, in, 7, out, tab, n); break;                      \
+        default: FN(nin, in, 8, out, tab, n); break;                     \
+    }
+
+__attribute__((target("avx2"))) static void dot_avx2(int nin, const uint8_t *const *in, int nout,
+                                                     uint8_t *const *out, const coef_t *tab,
+                                                     uint32_t n) {
+    DOT_SWITCH(dot_avx2_n)
+}
+
+__attribute__((target("avx2,gfni"))) static void dot_gfni(int nin, const uint8_t *const *in, int nout,
+                                                          uint8_t *const *out, const coef_t *tab,
+                                                          uint32_t n) {
+    DOT_SWITCH(dot_gfni_n)
+}
+
+static void dot(int level, int nin, const uint8_t *const *in, int nout, uint8_t *const *out,
+                const coef_t *tab, uint32_t n) {
+    if (level >= 2) dot_gfni(nin, in, nout, out, tab, n);
+    else if (level == 1) dot_avx2(nin, in, nout, out, tab, n);
+    else dot_scalar(nin, in, nout, out, tab, n);
+}
+
+/* dst ^= src over n bytes (XOR scheme) */
+__attribute__((target("avx2"))) static void xor_into_avx2(uint8_t *dst, const uint8_t *src, uint32_t n) {
+    uint32_t p = 0;
+    for (; p + 32 <= n; p += 32)
+        _mm256_storeu_si256((__m256i *)(dst + p),
+                            _mm256_xor_si256(_mm256_loadu_si256((const __m256i *)(dst + p)),
+                                             _mm256_loadu_si256((const __m256i *)(src + p))));
+    for (; p < n; p++) dst[p] ^= src[p];
+}
+
+static void xor_into(int level, uint8_t *dst, const uint8_t *src, uint32_t n) {
+    if (level >= 1) xor_into_avx2(dst, src, n);
+    else for (uint32_t p = 0; p < n; p++) dst[p] ^= src[p];
+}
+
+/* ----------------------------------------------------------- windows --- */
+static void encode_window(int level, int scheme, int k, int r, const coef_t *tab, uint32_t S,
+                          uint32_t stride, uint8_t *win) {
+    if (scheme == ORC_XOR) {
+        for (int g = 0; g < r; g++) {
+            uint8_t *R = win + (size_t)(k + g) * stride;
+            memcpy(R, win + (size_t)g * stride, S);
+            for (int j = g + r; j < k; j += r) xor_into(level, R, win + (size_t)j * stride, S);
+        }
+        return;
+    }
+    const uint8_t *in[64];
+    uint8_t *out[8];
+    for (int j = 0; j < k; j++) in[j] = win + (size_t)j * stride;
+    for (int i = 0; i < r; i++) out[i] = win + (size_t)(k + i) * stride;
+    dot(level, k, in, r, out, tab, S);
+}
+
+/* GF(2^8) inverse of an e x e matrix (e <= 8) by Gauss-Jordan; 0 if singular */
+static int inv_small(int e, uint8_t *A, uint8_t *Ai) {
+    uint8_t M[8][16];
+    for (int i = 0; i < e; i++)
+        for (int j = 0; j < 2 * e; j++) M[i][j] = j < e ? A[i * e + j] : (uint8_t)(j - e == i);
+    for (int c = 0; c < e; c++) {
+        int p = c;
+        while (p < e && !M[p][c]) p++;
+        if (p == e) return 0;
+        if (p != c)
+            for (int j = 0; j < 2 * e; j++) { uint8_t t = M[c][j]; M[c][j] = M[p][j]; M[p][j] = t; }
+        const uint8_t iv = ginv(M[c][c]);
+        for (int j = 0; j < 2 * e; j++) M[c][j] = gmul(M[c][j], iv);
+        for (int i = 0; i < e; i++) {
+            if (i == c || !M[i][c]) continue;
+            const uint8_t f = M[i][c];
+            for (int j = 0; j < 2 * e; j++) M[i][j] ^= gmul(f, M[c][j]);
+        }
+    }
+    for (int i = 0; i < e; i++)
+        for (int j = 0; j < e; j++) Ai[i * e + j] = M[i][e + j];
+    return 1;
+}
+
+static int decode_window(int level, int scheme, int k, int r, const uint8_t *C, uint32_t S,
+                         uint32_t stride, uint64_t present, uint8_t *win) {
+    if (scheme == ORC_XOR) {
+        int status = ORC_OK;
+        for (int g = 0; g < r; g++) {
+            int miss = -1, nmiss = 0;
+            for (int j = g; j < k; j += r)
+                if (!((present >> j) & 1)) { miss = j; nmiss++; }
+            if (nmiss == 0) continue;
+            if (nmiss > 1 || !((present >> (k + g)) & 1)) { status = ORC_UNRECOVERABLE; continue; }
+            uint8_t *out = win + (size_t)miss * stride;
+            memcpy(out, win + (size_t)(k + g) * stride, S);
+            for (int j = g; j < k; j += r)
+                if (j != miss) xor_into(level, out, win + (size_t)j * stride, S);
+        }
+        return status;
+    }
+    int miss[64], sel[8], e = 0, nrep = 0;
+    for (int j = 0; j < k; j++)
+        if (!((present >> j) & 1)) miss[e++] = j;
+    if (e == 0) return ORC_OK;
+    for (int i = 0; i < r && nrep < e; i++)
+        if ((present >> (k + i)) & 1) sel[nrep++] = i;
+    if (nrep < e || e > 8) return ORC_UNRECOVERABLE;
+    /* A[t][u] = C[sel_t][miss_u]; recovered_u = sum_t Ainv[u][t] (R_sel_t + sum_j C[sel_t][j] S_j)
+     * folded into one dot product over the k inputs (received sources, chosen repairs) */
+    uint8_t A[64], Ai[64];
+    for (int t = 0; t < e; t++)
+        for (int u = 0; u < e; u++) A[t * e + u] = C[sel[t] * k + miss[u]];
+    if (!inv_small(e, A, Ai)) return ORC_UNRECOVERABLE;
+    const uint8_t *in[64];
+    uint8_t *out[8];
+    coef_t tab[64 * 8];
+    int q = 0;
+    for (int j = 0; j < k; j++) {
+        if (!((present >> j) & 1)) continue;
+        for (int u = 0; u < e; u++) {
+            uint8_t c = 0;
+            for (int t = 0; t < e; t++) c ^= gmul(Ai[u * e + t], C[sel[t] * k + j]);
+            coef_make(c, &tab[q * e + u]);
+        }
+        in[q++] = win + (size_t)j * stride;
+    }
+    for (int t = 0; t < e; t++) {
+        for (int u = 0; u < e; u++) coef_make(Ai[u * e + t], &tab[q * e + u]);
+        in[q++] = win + (size_t)(k + sel[t]) * stride;
+    }
+    for (int u = 0; u < e; u++) out[u] = win + (size_t)miss[u] * stride;
+    dot(level, q, in, e, out, tab, S);
+    return ORC_OK;
+}
+
+/* -------------------------------------------------------------- batch --- */
+typedef struct {
+    int op, level, scheme, k, r;
+    const uint32_t *S;
+    uint32_t stride;
+    uint64_t lo, hi;
+    const uint64_t *present;
+    uint8_t *status, *wins;
+    const coef_t *tab;
+    const uint8_t *C;
+} sjob_t;
+
+static void *run_sjob(void *p) {
+    sjob_t *j = (sjob_t *)p;
+    const size_t wbytes = (size_t)(j->k + j->r) * j->stride;
+    for (uint64_t w = j->lo; w < j->hi; w++) {
+        uint8_t *win = j->wins + w * wbytes;
+        if (j->op == 0)
+            encode_window(j->level, j->scheme, j->k, j->r, j->tab, j->S[w], j->stride, win);
+        else
+            j->status[w] = (uint8_t)decode_window(j->level, j->scheme, j->k, j->r, j->C, j->S[w],
+                                                  j->stride, j->present[w], win);
+    }
+    return NULL;
+}
+
+static void run_sbatch(int op, int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                       uint64_t nwin, const uint64_t *present, uint8_t *status, uint8_t *wins,
+                       int nthreads) {
+    uint8_t C[64 * 64];
+    coef_t *tab = NULL;
+    tables_init();
+    if (scheme != ORC_XOR) {
+        orc_matrix(scheme, k, r, C);
+        tab = (coef_t *)malloc(sizeof(coef_t) * (size_t)k * r);
+        for (int j = 0; j < k; j++)
+            for (int i = 0; i < r; i++) coef_make(C[i * k + j], &tab[(size_t)j * r + i]);
+    }
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    sjob_t jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        sjob_t x = {op, orc_simd_level(), scheme, k, r, S, stride,
+                    nwin * (uint64_t)t / (uint64_t)nthreads, nwin * (uint64_t)(t + 1) / (uint64_t)nthreads,
+                    present, status, wins, tab, C};
+        jobs[t] = x;
+        if (nthreads == 1) run_sjob(&jobs[t]);
+        else pthread_create(&th[t], NULL, run_sjob, &jobs[t]);
+    }
+    if (nthreads > 1)
+        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(tab);
+}
+
+void orc_encode_batch_simd(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                           uint64_t nwin, uint8_t *wins, int nthreads) {
+    run_sbatch(0, scheme, k, r, S, stride, nwin, NULL, NULL, wins, nthreads);
+}
+
+void orc_decode_batch_simd(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                           uint64_t nwin, const uint64_t *present, uint8_t *status, uint8_t *wins,
+                           int nthreads) {
+    run_sbatch(1, scheme, k, r, S, stride, nwin, present, status, wins, nthreads);
+}

@@ -76,6 +76,18 @@ void orc_decode_batch(int scheme, int k, int r, const uint32_t *S, uint32_t stri
                       uint64_t nwin, const uint64_t *present, uint8_t *status, uint8_t *wins,
                       int nthreads);
 
+/* CPU baseline codec (fec_cpu_simd.c): same contract and outputs,
+ * AVX2 split-nibble tables or GFNI affine products; level 0 scalar, 1 AVX2,
+ * 2 AVX2+GFNI (detected; set_level(-1) restores detection) */
+int  orc_simd_detect(void);
+int  orc_simd_level(void);
+void orc_simd_set_level(int level);
+void orc_encode_batch_simd(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                           uint64_t nwin, uint8_t *wins, int nthreads);
+void orc_decode_batch_simd(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                           uint64_t nwin, const uint64_t *present, uint8_t *status, uint8_t *wins,
+                           int nthreads);
+
 /* parallel fill of nwin windows + S + present masks; returns source-packet bytes */
 uint64_t orc_make_batch(int workload, uint64_t seed, uint64_t w0, uint64_t nwin, int scheme,
                         int erasure, int k, int r, uint32_t L, uint32_t stride, uint8_t *wins,

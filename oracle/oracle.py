@@ -56,6 +56,11 @@ def lib():
             "orc_decode_batch": (None, [i32, i32, i32, vp, u32, u64, vp, vp, vp, i32]),
             "orc_make_batch": (u64, [i32, u64, u64, u64, i32, i32, i32, i32, u32, u32, vp, vp, vp,
                                      i32]),
+            "orc_simd_detect": (i32, []),
+            "orc_simd_level": (i32, []),
+            "orc_simd_set_level": (None, [i32]),
+            "orc_encode_batch_simd": (None, [i32, i32, i32, vp, u32, u64, vp, i32]),
+            "orc_decode_batch_simd": (None, [i32, i32, i32, vp, u32, u64, vp, vp, vp, i32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -158,6 +163,39 @@ def erase(wins: np.ndarray, present: np.ndarray, k: int, r: int, fill: int = 0) 
 
 def window_digest(k: int, r: int, S: int, win: np.ndarray) -> int:
     return lib().orc_window_digest(k, r, S, win.shape[-1], _p(np.ascontiguousarray(win)))
+
+
+SIMD_NAMES = {0: "scalar", 1: "AVX2 vpshufb nibble tables", 2: "AVX2+GFNI vgf2p8affineqb"}
+
+
+def simd_detect() -> int:
+    """CPU baseline codec level this CPU supports (fec_cpu_simd.c)."""
+    return lib().orc_simd_detect()
+
+
+def simd_level() -> int:
+    return lib().orc_simd_level()
+
+
+def simd_set_level(level: int) -> None:
+    lib().orc_simd_set_level(level)
+
+
+def encode_batch_simd(scheme: int, k: int, r: int, S: np.ndarray, wins: np.ndarray, nthreads: int = 1):
+    nwin, _, stride = wins.shape
+    S = np.ascontiguousarray(S, np.uint32)
+    lib().orc_encode_batch_simd(scheme, k, r, _p(S), stride, nwin, _p(wins), nthreads)
+
+
+def decode_batch_simd(scheme: int, k: int, r: int, S: np.ndarray, wins: np.ndarray,
+                      present: np.ndarray, nthreads: int = 1) -> np.ndarray:
+    nwin, _, stride = wins.shape
+    S = np.ascontiguousarray(S, np.uint32)
+    present = np.ascontiguousarray(present, np.uint64)
+    status = np.zeros(nwin, np.uint8)
+    lib().orc_decode_batch_simd(scheme, k, r, _p(S), stride, nwin, _p(present), _p(status),
+                                _p(wins), nthreads)
+    return status
 
 
 def batch_digest(k: int, r: int, S: np.ndarray, wins: np.ndarray, w0: int = 0) -> int:
