@@ -115,7 +115,7 @@ def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
     # scale to ~seconds of work; repeat the capped sample if it is still short
     per_win = dt / nw
     nw = min(max_nw, max(nw, int(seconds / per_win)))
-    reps = min(20, max(1, int(seconds / (per_win * nw) + 0.5)))
+    reps = min(1000, max(1, int(seconds / (per_win * nw) + 0.5)))
     tot_dt, tot_src = 0.0, 0
     for _ in range(reps):
         dt, src = run(nw)
