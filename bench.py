@@ -228,6 +228,12 @@ def main():
 
     verify = None if args.no_verify else batch.verify(ctx, w0)
     log(f"verify: {verify}")
+    # run digest of every rank's encoded windows, gathered over RCCL (8 B per
+    # rank over xGMI: the path's only collective, outside the timed region)
+    digest = None
+    if verify is not None and not cfg.host:
+        digest = shard.gather_digest(batch.digest(ctx, w0),
+                                     dev if args.dist_backend == "nccl" else None)
 
     if rank == 0:
         dom = "decode" if dec_ms > enc_ms else "encode"
@@ -282,6 +288,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "verify": verify,
+            "digest": None if digest is None else f"{digest:016x}",
         }
         print(json.dumps(line), flush=True)
     if world > 1:

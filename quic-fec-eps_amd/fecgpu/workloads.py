@@ -148,6 +148,17 @@ class Batch:
         return {"encode": enc, "decode": dec}
 
     # --------------------------------------------------------- verification ---
+    def digest(self, ctx: Context, w0: int) -> int:
+        """Run digest of the encoded windows: sources and
+        repairs, order- and shard-invariant (XOR over global window ids)."""
+        c = self.cfg
+        self.encode(ctx)
+        d = torch.zeros(1, dtype=torch.int64, device=self.win.device)
+        ctx.digest_batch(c.code, self.win, d, nwin=self.nwin, stride=c.stride, w0=w0,
+                         **self._len_args())
+        torch.cuda.synchronize()
+        return int(d.item()) & (2**64 - 1)
+
     def verify(self, ctx: Context, w0: int, chunk: int = 8192) -> dict:
         """Poison every erased symbol, decode once, and compare each window's
         sources with a copy taken before poisoning (all on device)."""
