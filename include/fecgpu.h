@@ -181,13 +181,17 @@ ssize_t fecgpu_encoder_release(fecgpu_encoder *enc, uint64_t win);
 ssize_t fecgpu_decoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t max_len,
                            uint32_t batch, fecgpu_decoder **out);
 void    fecgpu_decoder_free(fecgpu_decoder *dec);
-/* File a received source packet / repair symbol (repair length = S). */
+/* File a received source packet / repair symbol (repair length = S).  Every
+ * batch*k filed symbols an automatic flush is launched without waiting; its
+ * windows complete when a later call touches them (add, recovered, release),
+ * at the next flush, or at a tick once the GPU is done. */
 ssize_t fecgpu_decoder_add_source(fecgpu_decoder *dec, uint64_t win, uint16_t idx,
                                   const uint8_t *pkt, size_t len);
 ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *dec, uint64_t win, uint16_t idx,
                                   const uint8_t *sym, size_t len);
-/* Decode every window that can now recover a missing source; returns the
- * number of source packets recovered. */
+/* Decode every window that can now recover a missing source and wait for
+ * it; returns the number of source packets recovered (including those of an
+ * automatic flush completed here). */
 ssize_t fecgpu_decoder_flush(fecgpu_decoder *dec);
 /* Copy source packet idx of window win (received or recovered, de-framed);
  * returns its length, FECGPU_ERR_DONE if it is not available. */

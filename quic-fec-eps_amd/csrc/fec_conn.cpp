@@ -23,6 +23,13 @@
 //              (ragged layout with a fixed pitch: slot offsets from the first
 //              chunk, 64-bit wrap-around), the kernel writing recovered rows
 //              in place.  No staging buffers, no H2D / D2H copies.
+//              The automatic flush (every batch*k filed symbols) does not
+//              wait: its windows are marked in flight and the next call that
+//              touches one of them (or the next flush) completes it, so the
+//              receiver keeps filing packets while the GPU decodes.  The
+//              window that triggered it stays open for the next flush (its
+//              remaining repairs are likely still arriving).  fecgpu_decoder_
+//              flush() and tick() complete everything before returning.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -376,6 +383,7 @@ struct DecSlot {
     uint32_t S = 0;        // known once a repair (or FIXED source) arrives
     bool used = false;
     bool cand = false;     // touched since the last flush
+    bool inflight = false; // in the launched, not yet completed decode
 };
 
 constexpr uint32_t kSlotsPerChunk = 256;
@@ -401,6 +409,9 @@ struct fecgpu_decoder {
     fecgpu_policy policy{};
     uint64_t now = 0;                  // latest caller clock (tick)
     uint64_t dirty_t = 0;              // when the first symbol since the last flush was filed
+    std::vector<uint32_t> sel;         // windows of the launched decode (in arg order)
+    bool pending = false;              // a launched decode awaits completion
+    hipEvent_t done = nullptr;         // recorded after the pending decode
 };
 
 namespace {
@@ -488,6 +499,11 @@ ssize_t fecgpu_decoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t ma
         delete d;
         return FECGPU_ERR_DEVICE;
     }
+    if (hipEventCreateWithFlags(&d->done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(d->stream);
+        delete d;
+        return FECGPU_ERR_DEVICE;
+    }
     *out = d;
     return 0;
 }
@@ -498,73 +514,33 @@ void fecgpu_decoder_free(fecgpu_decoder *d) {
     (void)hipStreamSynchronize(d->stream);
     for (Pinned &p : d->chunks) pinned_free(p);
     pinned_free(d->arg);
+    (void)hipEventDestroy(d->done);
     (void)hipStreamDestroy(d->stream);
     delete d;
 }
 
-ssize_t fecgpu_decoder_flush(fecgpu_decoder *d) {
-    if (!d) return FECGPU_ERR_INVALID_ARG;
+}  // extern "C"
+
+namespace {
+
+// Completes the pending decode: waits for it and marks what it recovered.
+// Returns the number of recovered sources (0 if nothing was pending).
+ssize_t dec_complete(fecgpu_decoder *d) {
+    if (!d->pending) return 0;
+    d->pending = false;
     const int k = d->code.k, r = d->code.r;
     const bool lp = is_lenprefix(d->code);
-    std::vector<uint32_t> sel;
-    for (uint32_t s : d->cand) {
-        DecSlot &w = d->slots[s];
-        if (!w.cand) continue;  // released (or a duplicate entry) since
-        w.cand = false;
-        if (w.used && decodable(d->code, w)) sel.push_back(s);
-    }
-    d->cand.clear();
-    d->dirty = 0;
-    if (sel.empty()) return 0;
     DevGuard g(d->dev);
-    const size_t n = sel.size();
-    // per-window arguments in pinned memory the kernel reads directly
-    const size_t o_len = (n * 8 + 255) & ~size_t(255), o_pres = o_len + ((n * 4 + 255) & ~size_t(255));
-    const size_t o_stat = o_pres + n * 8, need = o_stat + n;
-    if (d->arg_cap < need) {
-        pinned_free(d->arg);
-        d->arg_cap = 0;
-        ssize_t rc = pinned_alloc(std::max(need, (size_t)64 << 10) * 2, d->arg);
-        if (rc) return rc;
-        d->arg_cap = d->arg.bytes;
-    }
-    uint64_t *off = reinterpret_cast<uint64_t *>(d->arg.host);
-    uint32_t *len = reinterpret_cast<uint32_t *>(d->arg.host + o_len);
-    uint64_t *pres = reinterpret_cast<uint64_t *>(d->arg.host + o_pres);
-    uint8_t *status = d->arg.host + o_stat;
-    const uint64_t base = reinterpret_cast<uint64_t>(d->chunks[0].dev);
-    for (size_t i = 0; i < n; i++) {
-        const uint32_t s = sel[i];
-        const DecSlot &w = d->slots[s];
-        if (lp) {  // zero padding of the received sources up to S (A.3)
-            const uint32_t S16 = rup16(w.S);
-            for (int j = 0; j < k; j++)
-                if ((w.present >> j) & 1) {
-                    const uint32_t used = 2 + d->plen[(size_t)s * k + j];
-                    std::memset(dec_row(d, s, j) + used, 0, S16 - used);
-                }
-        }
-        off[i] = dec_dev_addr(d, s) - base;  // wraps for chunks below the first
-        len[i] = w.S;
-        pres[i] = w.present;
-        status[i] = 0xFF;
-    }
-    BatchArgs a{};
-    a.win = d->chunks[0].dev;
-    a.win_off = reinterpret_cast<const uint64_t *>(d->arg.dev);
-    a.sym_len = reinterpret_cast<const uint32_t *>(d->arg.dev + o_len);
-    a.present = reinterpret_cast<const uint64_t *>(d->arg.dev + o_pres);
-    a.status = d->arg.dev + o_stat;
-    a.stride = d->stride;
-    a.off_stride = d->stride;
-    a.nwin = n;
-    ssize_t rc = fecgpu::launch_batch(d->ctx, &d->code, true, a, d->stream, true);
-    if (rc) return rc;
-    if (hipStreamSynchronize(d->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
+    const hipError_t e = hipEventSynchronize(d->done);
+    const size_t n = d->sel.size();
+    const size_t o_stat = d->arg_cap / 2;  // see dec_launch
+    const uint8_t *status = d->arg.host + o_stat;
     ssize_t recovered = 0;
     for (size_t i = 0; i < n; i++) {
-        const uint32_t s = sel[i];
+        const uint32_t s = d->sel[i];
         DecSlot &w = d->slots[s];
+        w.inflight = false;
+        if (e != hipSuccess) continue;
         uint64_t got_mask = 0;
         for (int j = 0; j < k; j++) {
             if ((w.present >> j) & 1) continue;
@@ -589,7 +565,122 @@ ssize_t fecgpu_decoder_flush(fecgpu_decoder *d) {
         }
         w.present |= got_mask;
     }
-    return recovered;
+    d->sel.clear();
+    return e == hipSuccess ? recovered : FECGPU_ERR_DEVICE;
+}
+
+// A call about to read or write slot s first completes a decode that owns it.
+ssize_t dec_ready(fecgpu_decoder *d, uint32_t s) {
+    return d->slots[s].inflight ? dec_complete(d) : 0;
+}
+
+// Launches one decode over the candidate windows that can recover something
+// (all but `keep`, which stays a candidate).  The caller completes any
+// pending decode first.  Returns the number of windows launched.
+ssize_t dec_launch(fecgpu_decoder *d, uint32_t keep) {
+    const int k = d->code.k;
+    const bool lp = is_lenprefix(d->code);
+    std::vector<uint32_t> &sel = d->sel;
+    sel.clear();
+    bool kept = false;
+    for (uint32_t s : d->cand) {
+        DecSlot &w = d->slots[s];
+        if (!w.cand) continue;  // released (or a duplicate entry) since
+        if (s == keep) {
+            kept = true;
+            continue;
+        }
+        w.cand = false;
+        if (w.used && decodable(d->code, w)) sel.push_back(s);
+    }
+    d->cand.clear();
+    d->dirty = 0;
+    if (kept) {
+        d->cand.push_back(keep);
+        d->dirty = 1;
+        d->dirty_t = d->now;
+    }
+    if (sel.empty()) return 0;
+    DevGuard g(d->dev);
+    const size_t n = sel.size();
+    // per-window arguments in pinned memory the kernel reads directly; the
+    // status bytes live in the upper half so dec_complete finds them at arg_cap/2
+    const size_t o_len = (n * 8 + 255) & ~size_t(255), o_pres = o_len + ((n * 4 + 255) & ~size_t(255));
+    const size_t need = o_pres + n * 8;
+    if (d->arg_cap / 2 < std::max(need, n)) {
+        pinned_free(d->arg);
+        d->arg_cap = 0;
+        ssize_t rc = pinned_alloc(std::max(need, (size_t)64 << 10) * 2, d->arg);
+        if (rc) {
+            for (uint32_t s : sel) d->slots[s].inflight = false;
+            sel.clear();
+            return rc;
+        }
+        d->arg_cap = d->arg.bytes;
+    }
+    const size_t o_stat = d->arg_cap / 2;
+    uint64_t *off = reinterpret_cast<uint64_t *>(d->arg.host);
+    uint32_t *len = reinterpret_cast<uint32_t *>(d->arg.host + o_len);
+    uint64_t *pres = reinterpret_cast<uint64_t *>(d->arg.host + o_pres);
+    uint8_t *status = d->arg.host + o_stat;
+    const uint64_t base = reinterpret_cast<uint64_t>(d->chunks[0].dev);
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t s = sel[i];
+        DecSlot &w = d->slots[s];
+        if (lp) {  // zero padding of the received sources up to S (A.3)
+            const uint32_t S16 = rup16(w.S);
+            for (int j = 0; j < k; j++)
+                if ((w.present >> j) & 1) {
+                    const uint32_t used = 2 + d->plen[(size_t)s * k + j];
+                    std::memset(dec_row(d, s, j) + used, 0, S16 - used);
+                }
+        }
+        off[i] = dec_dev_addr(d, s) - base;  // wraps for chunks below the first
+        len[i] = w.S;
+        pres[i] = w.present;
+        status[i] = 0xFF;
+        w.inflight = true;
+    }
+    BatchArgs a{};
+    a.win = d->chunks[0].dev;
+    a.win_off = reinterpret_cast<const uint64_t *>(d->arg.dev);
+    a.sym_len = reinterpret_cast<const uint32_t *>(d->arg.dev + o_len);
+    a.present = reinterpret_cast<const uint64_t *>(d->arg.dev + o_pres);
+    a.status = d->arg.dev + o_stat;
+    a.stride = d->stride;
+    a.off_stride = d->stride;
+    a.nwin = n;
+    ssize_t rc = fecgpu::launch_batch(d->ctx, &d->code, true, a, d->stream, true);
+    if (rc == 0 && hipEventRecord(d->done, d->stream) != hipSuccess) rc = FECGPU_ERR_DEVICE;
+    if (rc) {
+        for (uint32_t s : sel) d->slots[s].inflight = false;
+        sel.clear();
+        return rc;
+    }
+    d->pending = true;
+    return (ssize_t)n;
+}
+
+// The automatic flush after `batch`*k filed symbols: launch without waiting.
+ssize_t dec_auto_flush(fecgpu_decoder *d, uint32_t s) {
+    if (++d->dirty < (uint64_t)d->batch * d->code.k) return 0;
+    ssize_t rc = dec_complete(d);
+    if (rc >= 0) rc = dec_launch(d, s);
+    return rc < 0 ? FECGPU_ERR_DEVICE : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+ssize_t fecgpu_decoder_flush(fecgpu_decoder *d) {
+    if (!d) return FECGPU_ERR_INVALID_ARG;
+    ssize_t before = dec_complete(d);
+    if (before < 0) return before;
+    ssize_t rc = dec_launch(d, UINT32_MAX);
+    if (rc <= 0) return rc < 0 ? rc : before;
+    rc = dec_complete(d);
+    return rc < 0 ? rc : before + rc;
 }
 
 ssize_t fecgpu_decoder_add_source(fecgpu_decoder *d, uint64_t win, uint16_t idx, const uint8_t *pkt,
@@ -599,6 +690,7 @@ ssize_t fecgpu_decoder_add_source(fecgpu_decoder *d, uint64_t win, uint16_t idx,
     uint32_t s = 0;
     ssize_t rc = dec_slot(d, win, s);
     if (rc) return rc;
+    if (dec_ready(d, s) < 0) return FECGPU_ERR_DEVICE;
     DecSlot &w = d->slots[s];
     if ((w.present >> idx) & 1) return FECGPU_ERR_DONE;  // duplicate
     uint8_t *row = dec_row(d, s, idx);
@@ -615,8 +707,7 @@ ssize_t fecgpu_decoder_add_source(fecgpu_decoder *d, uint64_t win, uint16_t idx,
     d->plen[(size_t)s * d->code.k + idx] = (uint32_t)len;
     w.present |= 1ull << idx;
     dec_touch(d, s);
-    if (++d->dirty >= (uint64_t)d->batch * d->code.k) return fecgpu_decoder_flush(d) < 0 ? FECGPU_ERR_DEVICE : 0;
-    return 0;
+    return dec_auto_flush(d, s);
 }
 
 ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *d, uint64_t win, uint16_t idx, const uint8_t *sym,
@@ -626,6 +717,7 @@ ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *d, uint64_t win, uint16_t idx,
     uint32_t s = 0;
     ssize_t rc = dec_slot(d, win, s);
     if (rc) return rc;
+    if (dec_ready(d, s) < 0) return FECGPU_ERR_DEVICE;
     DecSlot &w = d->slots[s];
     const int k = d->code.k;
     if ((w.present >> (k + idx)) & 1) return FECGPU_ERR_DONE;
@@ -639,8 +731,7 @@ ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *d, uint64_t win, uint16_t idx,
     std::memcpy(dec_row(d, s, k + idx), sym, len);
     w.present |= 1ull << (k + idx);
     dec_touch(d, s);
-    if (++d->dirty >= (uint64_t)d->batch * d->code.k) return fecgpu_decoder_flush(d) < 0 ? FECGPU_ERR_DEVICE : 0;
-    return 0;
+    return dec_auto_flush(d, s);
 }
 
 ssize_t fecgpu_decoder_set_policy(fecgpu_decoder *d, const fecgpu_policy *p) {
@@ -654,6 +745,8 @@ ssize_t fecgpu_decoder_tick(fecgpu_decoder *d, uint64_t now_us) {
     d->now = std::max(d->now, now_us);
     const uint64_t bt = d->policy.batch_timeout_us;
     if (bt && d->dirty && d->now - d->dirty_t >= bt) return fecgpu_decoder_flush(d);
+    // an automatic flush that has finished by now is completed here
+    if (d->pending && hipEventQuery(d->done) != hipErrorNotReady) return dec_complete(d);
     return 0;
 }
 
@@ -661,8 +754,10 @@ ssize_t fecgpu_decoder_recovered(fecgpu_decoder *d, uint64_t win, uint16_t idx, 
                                  size_t cap) {
     if (!d || idx >= d->code.k) return FECGPU_ERR_INVALID_ARG;
     auto it = d->map.find(win);
-    if (it == d->map.end() || !((d->slots[it->second].present >> idx) & 1)) return FECGPU_ERR_DONE;
+    if (it == d->map.end()) return FECGPU_ERR_DONE;
     const uint32_t s = it->second;
+    if (dec_ready(d, s) < 0) return FECGPU_ERR_DEVICE;
+    if (!((d->slots[s].present >> idx) & 1)) return FECGPU_ERR_DONE;
     const uint32_t n = d->plen[(size_t)s * d->code.k + idx];
     if (cap < n || (!out && n)) return FECGPU_ERR_BUFFER_TOO_SHORT;
     if (n) std::memcpy(out, dec_row(d, s, idx) + (is_lenprefix(d->code) ? 2 : 0), n);
@@ -673,6 +768,7 @@ ssize_t fecgpu_decoder_release(fecgpu_decoder *d, uint64_t win) {
     if (!d) return FECGPU_ERR_INVALID_ARG;
     auto it = d->map.find(win);
     if (it == d->map.end()) return FECGPU_ERR_DONE;
+    if (dec_ready(d, it->second) < 0) return FECGPU_ERR_DEVICE;
     DecSlot &w = d->slots[it->second];
     w.used = false;
     w.cand = false;

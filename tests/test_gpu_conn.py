@@ -202,3 +202,34 @@ def test_policy_timeouts(ctx):
     assert dec.tick(5029) == 0 and dec.recovered(0, 0) is None   # flush not due yet
     assert dec.tick(5030) == 2                                   # flushed: sources 0 and 2 back
     assert dec.recovered(0, 0) == pkts[0] and dec.recovered(0, 2) == pkts[2]
+
+
+def test_async_auto_flush(ctx):
+    """The automatic flush (every batch*k filed symbols) launches without waiting:
+    a window in flight completes when it is next touched; the window whose symbol
+    triggered the flush stays open and is decoded by the next flush."""
+    code = fecgpu.Code("xor", 4, 1, "fixed")
+    enc = fecgpu.Encoder(ctx, code, max_len=64, batch=2)
+    pkts = [bytes([7 * n + 1]) * 64 for n in range(8)]
+    for p in pkts:
+        enc.add_source(p)
+    enc.flush()
+    reps = [enc.repair(w, 0) for w in range(2)]
+    dec = fecgpu.Decoder(ctx, code, max_len=64, batch=2)     # auto flush every 8 symbols
+    for w in range(2):
+        for i in range(3):                                  # source 3 of each window is lost
+            assert dec.add_source(w, i, pkts[4 * w + i]) == 0
+        assert dec.add_repair(w, 0, reps[w]) == 0           # 8th symbol: window 0 launched
+    assert dec.recovered(0, 3) == pkts[3]                   # completes the in-flight decode
+    assert dec.recovered(1, 3) is None                      # the triggering window waits
+    assert dec.add_source(1, 0, pkts[4]) == fecgpu.ERR_DONE  # duplicate, still detected
+    assert dec.flush() == 1
+    assert dec.recovered(1, 3) == pkts[7]
+    # a window in flight released before completion, and flush counting pending results
+    for w in range(2, 4):
+        for i in (0, 2, 3):
+            assert dec.add_source(w, i, pkts[i]) == 0
+        assert dec.add_repair(w, 0, reps[0]) == 0           # window 2 launched at the 8th
+    assert dec.release(2) == 0
+    assert dec.flush() == 1                                 # window 3 (window 2 was released)
+    assert dec.recovered(3, 1) == pkts[1]
