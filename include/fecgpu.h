@@ -114,7 +114,9 @@ void    fecgpu_host_free(void *p);
  * "host_direct" (bit 0 encode, bit 1 decode: kernels write outputs into
  * mapped pinned host windows instead of D2H copies; bit 2: they also read the
  * windows over PCIe instead of H2D copies; default 6 = decode zero-copy),
- * "host_chunk_mb" (pipeline chunk, default 128). */
+ * "host_chunk_mb" (pipeline chunk, default 128); "bitslice" (1 default: GF
+ * encode of a code with a compiled bit-sliced kernel — Cauchy rows, r = 8,
+ * k in {16, 24, 32} — uses it; 0: the table multiply for every code). */
 ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value);
 
 /* ---- batch entry points (hot path) ---------------------------------- */

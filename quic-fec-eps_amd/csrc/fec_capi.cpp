@@ -131,6 +131,8 @@ struct fecgpu_ctx {
     // way and its DMA copies beat kernel PCIe traffic (11.8 vs 12.5 ms).
     int host_direct = 6;
     int host_chunk_mb = 128;
+    // GF encode by the bit-sliced kernel where the code has one (DESIGN.md §GF bit-slicing)
+    int bitslice = 1;
 };
 
 extern "C" {
@@ -215,6 +217,11 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
     if (!std::strcmp(key, "host_chunk_mb")) {
         if (value < 1 || value > 4096) return FECGPU_ERR_INVALID_ARG;
         ctx->host_chunk_mb = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "bitslice")) {
+        if (value < 0 || value > 1) return FECGPU_ERR_INVALID_ARG;
+        ctx->bitslice = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "wpb")) {
@@ -573,6 +580,17 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         if (p.win_lds) cap = std::max(1, (int)((40u << 10) / p.win_lds));
         p.wpb = std::max(p.wpb, std::min(want, cap));
         if (p.win_lds) p.lds_bytes = p.win_lds * (uint32_t)p.wpb;
+    }
+    if (!decode && scheme == FECGPU_SCHEME_GF256 && !remote && ctx->bitslice &&
+        bitslice_supported(k, r, (int)code->matrix)) {
+        // column pairs in group mode; no tables.  Groups of >= 8 passes at the
+        // longest window (a lane's unit is k sources x 32 B of heavy XOR work,
+        // so a partly idle last pass costs more than in the table kernels).
+        p.bitslice = true;
+        p.flat = false;
+        p.lds_bytes = 0;
+        const uint32_t units = ncol ? (ncol + 1) / 2 : (uint32_t)((stride >> 4) + 1) / 2;
+        p.wpb = units ? std::max(1, std::min<int>(kMaxWpb, (int)((8u * kBlock + units - 1) / units))) : kMaxWpb;
     }
     if (remote) {  // PCIe-latency bound: as many workgroups as windows
         p.remote = true;

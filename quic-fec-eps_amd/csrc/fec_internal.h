@@ -57,7 +57,11 @@ struct LaunchPlan {
     int blocks_per_cu;   // persistent grid of CUs x blocks_per_cu (tuning; 0 = automatic)
     bool remote;         // windows in mapped host memory: one window per workgroup and
                          // deep load batches (PCIe latency, small batches)
+    bool bitslice;       // GF encode by the bit-sliced kernel (compile-time matrix)
 };
+
+// GF encode of (k, r, matrix) has a compiled bit-sliced kernel.
+bool bitslice_supported(int k, int r, int matrix);
 
 // Per-window LDS region of the GF decode kernel: tables [k][R] uint4 + [k][R] u32,
 // input symbol list (64 B), output symbol list (16 B).

@@ -20,6 +20,8 @@
 // by every output.
 #include "fec_internal.h"
 
+#include <utility>
+
 #ifndef FECGPU_NT
 #define FECGPU_NT 0  // nontemporal (streaming) loads/stores; A/B build knob
 #endif
@@ -549,6 +551,217 @@ __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a
             });
             __syncthreads();
         }
+    }
+}
+
+// ================================================ bit-sliced GF encode ===
+// GF encode for codes whose matrix is known at compile time (DESIGN.md §GF
+// bit-slicing).  Multiplying by a constant c is linear over GF(2): output bit
+// p of c*x is the XOR of the input bits q for which bit p of c*2^q is set.  A
+// lane takes 32 byte positions of a window (two 16-B columns, A = u and
+// B = u + half the columns, so loads stay coalesced), transposes each source's
+// 8 dwords into 8 bit planes (plane q = bit q of the 32 bytes, in a fixed
+// lane order), and every output plane becomes a compile-time XOR of input
+// planes.  Per source the 15 XOR combinations of planes 0-3 and of planes
+// 4-7 are formed once (those used), so an output plane costs one 3-input XOR.
+// No v_perm, no tables: ~150 VALU ops per source and 32 bytes at r = 8
+// against ~450 v_perm-weighted cycles for the table multiply.  Bytes are the
+// same as the table multiply's (tests/test_gpu_parity.py).
+namespace bs {
+
+constexpr GfTables kGf = make_gf_tables();
+
+constexpr uint8_t gmul(uint8_t a, uint8_t b) {
+    return (a && b) ? kGf.exp[kGf.log[a] + kGf.log[b]] : 0;
+}
+
+// masks[j][i][p]: input planes of source j feeding output plane p of repair i
+template <int K, int R>
+struct Masks {
+    uint8_t m[K][R][8];
+    constexpr Masks() : m{} {
+        for (int j = 0; j < K; j++)
+            for (int i = 0; i < R; i++) {
+                const uint8_t c = kGf.exp[255 - kGf.log[(uint8_t)((K + i) ^ j)]];  // Cauchy (A.2)
+                for (int q = 0; q < 8; q++) {
+                    const uint8_t col = gmul(c, (uint8_t)(1u << q));
+                    for (int p = 0; p < 8; p++)
+                        if ((col >> p) & 1) m[j][i][p] |= (uint8_t)(1u << q);
+                }
+            }
+    }
+};
+
+// (m & x) | (~m & y) as one v_bitop3_b32 (truth table of S0 ? S1 : S2 over
+// S0 = 0xF0, S1 = 0xCC, S2 = 0xAA).  The intrinsic keeps the optimiser from
+// distributing the planes' XORs through the selects, which multiplies live
+// values (masked halves of every plane) and spills.
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) {
+    return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA);
+}
+
+// 8 x 8 bit transpose in every byte lane of d[0..7] (rows = dwords, columns =
+// bits of the byte): three block-swap stages, 2 shifts + 2 selects per pair.
+// An involution, so the same call turns output planes back into bytes.
+__device__ __forceinline__ void tr8(uint32_t (&d)[8]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t x = d[i], y = d[i + 4];
+        d[i] = bsel(0xF0F0F0F0u, y << 4, x);
+        d[i + 4] = bsel(0x0F0F0F0Fu, x >> 4, y);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        if (i & 2) continue;
+        const uint32_t x = d[i], y = d[i + 2];
+        d[i] = bsel(0xCCCCCCCCu, y << 2, x);
+        d[i + 2] = bsel(0x33333333u, x >> 2, y);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        const uint32_t x = d[i], y = d[i + 1];
+        d[i] = bsel(0xAAAAAAAAu, y << 1, x);
+        d[i + 1] = bsel(0x55555555u, x >> 1, y);
+    }
+}
+
+template <int K, int R>
+inline constexpr Masks<K, R> kMasks{};
+
+// a ^ b through the bitop3 intrinsic (S0 ^ S1 = 0xF0 ^ 0xCC): opaque to the
+// reassociation pass, which otherwise flattens every output plane into one
+// XOR over all sources' planes, undoes the shared combinations and keeps
+// planes of many sources live at once
+__device__ __forceinline__ uint32_t oxor(uint32_t a, uint32_t b) {
+#if FECGPU_BS_VOP2
+    return a ^ b;
+#else
+    return __builtin_amdgcn_bitop3_b32(a, b, b, 0x3C);
+#endif
+}
+
+// output plane IP % 8 of repair IP / 8 takes source J's planes (compile time)
+template <int K, int R, int J, int IP>
+__device__ __forceinline__ void plane(uint32_t (&acc)[R][8], const uint32_t (&lo)[16], const uint32_t (&hi)[16]) {
+    constexpr int m = kMasks<K, R>.m[J][IP / 8][IP % 8], l = m & 15, h = m >> 4;
+    uint32_t &v = acc[IP / 8][IP % 8];
+    if constexpr (J == 0) v = l && h ? oxor(lo[l], hi[h]) : (l ? lo[l] : hi[h]);
+    else if constexpr (l && h) v = xor3(v, lo[l], hi[h]);
+    else if constexpr (l) v = oxor(v, lo[l]);
+    else if constexpr (h) v = oxor(v, hi[h]);
+}
+
+// acc ^= source J's contribution to every repair, from its planes x
+template <int K, int R, int J, int... IP>
+__device__ __forceinline__ void source(const uint32_t (&x)[8], uint32_t (&acc)[R][8],
+                                       std::integer_sequence<int, IP...>) {
+    uint32_t lo[16], hi[16];
+    lo[0] = hi[0] = 0;
+#pragma unroll
+    for (int s = 1; s < 16; s++) {
+        const int b = __builtin_ctz(s), rest = s & (s - 1);
+        lo[s] = rest ? oxor(lo[rest], x[b]) : x[b];
+        hi[s] = rest ? oxor(hi[rest], x[4 + b]) : x[4 + b];
+    }
+    (plane<K, R, J, IP>(acc, lo, hi), ...);
+    // pin the accumulators here: otherwise IR sinking moves every repair's XOR
+    // chain down to its store, past all later sources, and keeps their planes live
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int p = 0; p < 8; p++) asm volatile("" : "+v"(acc[i][p]));
+}
+
+template <int T>
+__device__ __forceinline__ void load_src(const uint8_t *pa, const uint8_t *pb, uint32_t stride,
+                                         uint32_t (&x)[8]) {
+    const uint4 va = ld16(pa + T * stride), vb = ld16(pb + T * stride);
+    x[0] = va.x; x[1] = va.y; x[2] = va.z; x[3] = va.w;
+    x[4] = vb.x; x[5] = vb.y; x[6] = vb.z; x[7] = vb.w;
+}
+
+// one batch of sources J0 + T (pa / pb point at source J0): all loads first,
+// then transposes and XORs
+template <int K, int R, int J0, int... T>
+__device__ __forceinline__ void batch(const uint8_t *pa, const uint8_t *pb, uint32_t stride,
+                                      uint32_t (&acc)[R][8], std::integer_sequence<int, T...>) {
+    uint32_t x[sizeof...(T)][8];
+    (load_src<T>(pa, pb, stride, x[T]), ...);
+    ((tr8(x[T]), source<K, R, J0 + T>(x[T], acc, std::make_integer_sequence<int, R * 8>{}),
+      __builtin_amdgcn_sched_barrier(0)), ...);
+}
+
+template <int K, int R, int U, int J0>
+__device__ __forceinline__ void sources(const uint8_t *pa, const uint8_t *pb, uint32_t stride,
+                                        uint32_t (&acc)[R][8]) {
+    if constexpr (J0 < K) {
+        batch<K, R, J0>(pa, pb, stride, acc, std::make_integer_sequence<int, ((K - J0) < U ? (K - J0) : U)>{});
+#if FECGPU_BS_SYNC
+        __syncthreads();  // keeps the workgroup's waves in one stretch of code
+#endif
+        // advance opaquely, so the compiler does not keep K addresses live at once
+        pa += U * stride;
+        pb += U * stride;
+        asm volatile("" : "+v"(pa), "+v"(pb));
+        sources<K, R, U, J0 + U>(pa, pb, stride, acc);
+    }
+}
+
+}  // namespace bs
+
+#ifndef FECGPU_BS_U
+#define FECGPU_BS_U 8  // bit-sliced encode: sources loaded per batch (8 > 4 > 2 by 1-3 %, r01)
+#endif
+#ifndef FECGPU_BS_SYNC
+// bit-sliced encode: workgroup barrier after every batch, keeping the waves of a
+// workgroup in one stretch of the long straight-line code (+1-3 %, r01)
+#define FECGPU_BS_SYNC 1
+#endif
+#ifndef FECGPU_BS_VOP2
+#define FECGPU_BS_VOP2 0  // bit-sliced encode: plain (VOP2) XORs for combinations and single terms
+#endif
+
+// Group mode over column pairs: window wl of the group has h = ceil(ncol / 2)
+// units; unit u covers columns u and u + h (the second absent when odd).
+template <int K, int R>
+__global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
+    __shared__ GroupLds g;
+    for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+        const uint64_t w0 = xr.cur * a.wpb;
+        const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
+        group_geometry(a, g, w0, nb);
+        __syncthreads();
+        if (threadIdx.x < 64)
+            block_prefix(g.pfx, (int)threadIdx.x < nb ? (g.ncol[threadIdx.x] + 1u) >> 1 : 0u, threadIdx.x);
+        __syncthreads();
+        const uint32_t total = g.pfx[nb];
+        int wl = 0;
+        // workgroup-uniform trip count (lanes past the end redo the last unit
+        // without storing), so a barrier inside the unit is safe
+        for (uint32_t s0 = 0; s0 < total; s0 += kBlock) {
+            const bool live = s0 + threadIdx.x < total;
+            const uint32_t s = live ? s0 + threadIdx.x : total - 1;
+            while (s >= g.pfx[wl + 1]) wl++;
+            const uint32_t u = s - g.pfx[wl], h = g.pfx[wl + 1] - g.pfx[wl];
+            // without a second column B repeats A: same inputs, same outputs, so
+            // its stores rewrite A's bytes with equal values (no branch)
+            const bool has_b = u + h < g.ncol[wl];
+            const uint32_t stride = g.stride[wl];
+            uint8_t *pa = reinterpret_cast<uint8_t *>(g.base[wl]) + u * 16u;
+            uint8_t *pb = has_b ? pa + h * 16u : pa;
+            uint32_t acc[R][8];
+            bs::sources<K, R, FECGPU_BS_U, 0>(pa, pb, stride, acc);
+            const uint64_t od = a.out_delta + (w0 + wl) * a.out_wdelta;
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                bs::tr8(acc[i]);
+                if (live) {
+                    st16(pa + od + (size_t)(K + i) * stride, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
+                    st16(pb + od + (size_t)(K + i) * stride, make_uint4(acc[i][4], acc[i][5], acc[i][6], acc[i][7]));
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -1144,8 +1357,31 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
         default: return hipErrorInvalidValue;   \
     }
 
+// Codes with a bit-sliced encode (Cauchy rows, compiled in).  r = 8 and
+// k >= 16 only: there the table multiply is VALU-bound and the bit-sliced
+// kernel 1.1-1.4x faster; at r <= 4 (and k = 8, r = 8) the table kernel is
+// memory-bound and, at higher occupancy, 5-12 % faster (scripts/bs_probe.py, r01).
+#ifndef FECGPU_BS_CODES
+#define FECGPU_BS_CODES(X) X(16, 8) X(24, 8) X(32, 8)
+#endif
+
+bool bitslice_supported(int k, int r, int matrix) {
+    if (matrix != FECGPU_MATRIX_CAUCHY) return false;
+#define FECGPU_BS_HAS(K_, R_) if (k == K_ && r == R_) return true;
+    FECGPU_BS_CODES(FECGPU_BS_HAS)
+#undef FECGPU_BS_HAS
+    return false;
+}
+
 hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
+    if (p.bitslice) {
+#define FECGPU_BS_LAUNCH(K_, R_) \
+        if (a.k == K_ && a.r == R_) return launch(gf_encode_bs_kernel<K_, R_>, a, p, s, false);
+        FECGPU_BS_CODES(FECGPU_BS_LAUNCH)
+#undef FECGPU_BS_LAUNCH
+        return hipErrorInvalidValue;
+    }
     const bool flat = p.flat;
     if (scheme == 0) {
         if (flat) DISPATCH_R(a.r, launch(xor_encode_kernel<RR, true>, a, p, s, true))

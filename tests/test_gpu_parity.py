@@ -497,3 +497,80 @@ def test_linearity_full_size(ctx):
     a.view[:, :cfg.k] ^= bsrc
     a.encode(ctx)
     assert torch.equal(a.view[:, cfg.k:], ra ^ rb)
+
+
+BS_CODES = [(16, 8), (24, 8), (32, 8), (8, 8), (16, 4)]  # (8, 8), (16, 4): table kernel (not compiled)
+
+
+@pytest.fixture(scope="module")
+def ctx_tables():
+    """A second context with the bit-sliced encode switched off (table multiply)."""
+    c = fecgpu.Context()
+    c.set_tuning("bitslice", 0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("k,r", BS_CODES)
+@pytest.mark.parametrize("wl,L,nwin", [(0, 1200, 70), (1, 0, 9), (0, 16, 33), (0, 1, 5), (0, 9000, 6)])
+def test_bitslice_encode_vs_oracle(ctx, ctx_tables, k, r, wl, L, nwin):
+    """The bit-sliced GF encode (compile-time Cauchy rows, DESIGN.md §GF bit-slicing)
+    emits the oracle's repairs for every compiled code: odd column counts (1200 B:
+    75 columns, the last unit without a second column), one column (16 B), S = 1,
+    per-window lengths (mixed MTU, LENPREFIX) and 9000-B symbols; and the same
+    bytes as the table-multiply kernel."""
+    S = O.sym_lens(wl, SEED + k, 0, nwin, k, L)
+    stride = O.round_up(int(S.max()), 16) + (16 if wl == 0 else 0)
+    wins = O.make_windows(wl, SEED + k, 0, nwin, k, r, L, stride)
+    oe = wins.copy()
+    O.encode_batch(O.GF256, k, r, S, oe, 4)
+    code = fecgpu.Code("gf256", k, r)
+    outs = []
+    for c in (ctx, ctx_tables):
+        d = torch.from_numpy(wins.copy()).cuda()
+        kw = dict(sym_len_all=int(S[0])) if wl == 0 else dict(sym_len=torch.from_numpy(S.astype(np.int32)).cuda())
+        c.encode_batch(code, d, nwin=nwin, stride=stride, **kw)
+        torch.cuda.synchronize()
+        outs.append(d.cpu().numpy())
+    _cmp_emitted(outs[0], oe, S, "bit-sliced encode")
+    _cmp_emitted(outs[1], oe, S, "table encode")
+
+
+@pytest.mark.parametrize("k,r", [(16, 8), (32, 8)])
+def test_bitslice_ragged_and_split(ctx, k, r):
+    """Bit-sliced encode through the ragged (win_off) and split (src / repair arrays) layouts."""
+    nwin = 11
+    rng = np.random.default_rng(k)
+    S = rng.integers(1, 2000, nwin).astype(np.uint32)
+    strides = [O.round_up(int(s), 16) for s in S]
+    offs, pos = [], 0
+    for w in range(nwin):
+        pos += 16 * int(rng.integers(0, 3))
+        offs.append(pos)
+        pos += (k + r) * strides[w]
+    buf = np.zeros(pos + 64, np.uint8)
+    ref = []
+    for w in range(nwin):
+        win = np.zeros((k + r, strides[w]), np.uint8)
+        win[:k, :S[w]] = rng.integers(0, 256, (k, int(S[w])), dtype=np.uint8)
+        buf[offs[w]:offs[w] + win.size] = win.ravel()
+        O.encode_batch(O.GF256, k, r, np.array([S[w]], np.uint32), win[None], 1)
+        ref.append(win)
+    d = torch.from_numpy(buf).cuda()
+    ctx.encode_batch(fecgpu.Code("gf256", k, r), d, nwin=nwin, stride=0,
+                     sym_len=torch.from_numpy(S.astype(np.int32)).cuda(),
+                     win_off=torch.tensor(offs, dtype=torch.int64).cuda())
+    out = d.cpu().numpy()
+    for w in range(nwin):
+        got = out[offs[w]:offs[w] + ref[w].size].reshape(ref[w].shape)
+        assert np.array_equal(got[:, :S[w]], ref[w][:, :S[w]]), w
+    # split layout, uniform S
+    Su = np.full(nwin, 1100, np.uint32)
+    wins = O.make_windows(0, SEED, 0, nwin, k, r, 1100, 1104)
+    oe = wins.copy()
+    O.encode_batch(O.GF256, k, r, Su, oe, 2)
+    src = torch.from_numpy(np.ascontiguousarray(wins[:, :k])).cuda()
+    rep = torch.full((nwin, r, 1104), 0x55, dtype=torch.uint8, device="cuda")
+    ctx.encode_split(fecgpu.Code("gf256", k, r), src, rep, nwin=nwin, stride=1104, sym_len_all=1100)
+    torch.cuda.synchronize()
+    assert np.array_equal(rep.cpu().numpy()[:, :, :1100], oe[:, k:, :1100])
