@@ -34,8 +34,8 @@ pmc() {  # name config counters...
 for s in "$@"; do
     case $s in
         smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        pytest) step pytest 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
-        pytest-x) step pytest 1100 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+        pytest) step pytest 1100 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+        pytest-x) step pytest 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         bench2) step bench2 600 python bench.py --config 2 --steps 20 --warmup 3 ;;
         bench3) step bench3 600 python bench.py --config 3 --steps 10 --warmup 2 --cpu-seconds 10 ;;
         bench4) step bench4 600 python bench.py --config 4 --steps 5 --warmup 1 --cpu-seconds 10 ;;
