@@ -1360,7 +1360,7 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
 // Codes with a bit-sliced encode (Cauchy rows, compiled in).  r = 8 and
 // k >= 16 only: there the table multiply is VALU-bound and the bit-sliced
 // kernel 1.1-1.4x faster; at r <= 4 (and k = 8, r = 8) the table kernel is
-// memory-bound and, at higher occupancy, 5-12 % faster (scripts/bs_probe.py, r01).
+// memory-bound and, at higher occupancy, 8-12 % faster (profiles/r01_bs_r4_and_alternation.txt).
 #ifndef FECGPU_BS_CODES
 #define FECGPU_BS_CODES(X) X(16, 8) X(24, 8) X(32, 8)
 #endif
