@@ -244,6 +244,12 @@ ssize_t fecgpu_frame_write_source_id(uint8_t *buf, size_t cap, uint64_t win, uin
 ssize_t fecgpu_frame_repair_len(uint64_t win, uint16_t k, uint16_t r, uint16_t idx, size_t sym_len);
 ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16_t k, uint16_t r,
                                   uint16_t idx, const uint8_t *sym, size_t sym_len);
+/* REPAIR frame header only (every field up to and including length): the
+ * symbol bytes follow from the caller's own buffer, e.g. as a second iovec of
+ * a gather send straight from the pinned window row (zero-copy, §8f-4).
+ * Returns the header length. */
+ssize_t fecgpu_frame_write_repair_header(uint8_t *buf, size_t cap, uint64_t win, uint16_t k,
+                                         uint16_t r, uint16_t idx, size_t sym_len);
 /* Parse one frame at buf; returns bytes consumed or a negative error
  * (BUFFER_TOO_SHORT on truncation, INVALID_ARG on an unknown type or bad field). */
 ssize_t fecgpu_frame_parse(const uint8_t *buf, size_t len, fecgpu_frame *out);

@@ -65,11 +65,11 @@ ssize_t fecgpu_frame_repair_len(uint64_t win, uint16_t k, uint16_t r, uint16_t i
                      varint_len(idx) + varint_len(sym_len) + sym_len);
 }
 
-ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16_t k, uint16_t r,
-                                  uint16_t idx, const uint8_t *sym, size_t sym_len) {
-    if (!buf || (!sym && sym_len) || win >= (1ull << 62) || idx >= r || k == 0 || r == 0)
+ssize_t fecgpu_frame_write_repair_header(uint8_t *buf, size_t cap, uint64_t win, uint16_t k,
+                                         uint16_t r, uint16_t idx, size_t sym_len) {
+    if (!buf || win >= (1ull << 62) || idx >= r || k == 0 || r == 0 || sym_len >= (1ull << 62))
         return FECGPU_ERR_INVALID_ARG;
-    const size_t n = (size_t)fecgpu_frame_repair_len(win, k, r, idx, sym_len);
+    const size_t n = (size_t)fecgpu_frame_repair_len(win, k, r, idx, sym_len) - sym_len;
     if (cap < n) return FECGPU_ERR_BUFFER_TOO_SHORT;
     uint8_t *p = varint_put(buf, FECGPU_FRAME_REPAIR);
     p = varint_put(p, win);
@@ -77,8 +77,17 @@ ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16
     p = varint_put(p, r);
     p = varint_put(p, idx);
     p = varint_put(p, sym_len);
-    if (sym_len) std::memcpy(p, sym, sym_len);
-    return (ssize_t)(p + sym_len - buf);
+    return (ssize_t)(p - buf);
+}
+
+ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16_t k, uint16_t r,
+                                  uint16_t idx, const uint8_t *sym, size_t sym_len) {
+    if (!buf || (!sym && sym_len)) return FECGPU_ERR_INVALID_ARG;
+    const ssize_t h = fecgpu_frame_write_repair_header(buf, cap, win, k, r, idx, sym_len);
+    if (h < 0) return h;
+    if (cap - (size_t)h < sym_len) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    if (sym_len) std::memcpy(buf + h, sym, sym_len);
+    return h + (ssize_t)sym_len;
 }
 
 ssize_t fecgpu_frame_parse(const uint8_t *buf, size_t len, fecgpu_frame *out) {

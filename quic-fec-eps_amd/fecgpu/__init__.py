@@ -51,7 +51,7 @@ EXPORTS = (
     "fecgpu_encoder_set_policy", "fecgpu_encoder_tick", "fecgpu_decoder_set_policy",
     "fecgpu_decoder_tick",
     "fecgpu_frame_source_id_len", "fecgpu_frame_write_source_id", "fecgpu_frame_repair_len",
-    "fecgpu_frame_write_repair", "fecgpu_frame_parse",
+    "fecgpu_frame_write_repair", "fecgpu_frame_write_repair_header", "fecgpu_frame_parse",
 )
 FRAME_SOURCE_ID, FRAME_REPAIR = 0xFEC0, 0xFEC1
 
@@ -160,6 +160,8 @@ def _lib():
             "fecgpu_frame_write_repair": (sz, [vp, ctypes.c_size_t, u64, ctypes.c_uint16,
                                                ctypes.c_uint16, ctypes.c_uint16, vp,
                                                ctypes.c_size_t]),
+            "fecgpu_frame_write_repair_header": (sz, [vp, ctypes.c_size_t, u64, ctypes.c_uint16,
+                                                      ctypes.c_uint16, ctypes.c_uint16, ctypes.c_size_t]),
             "fecgpu_frame_parse": (sz, [vp, ctypes.c_size_t, ctypes.POINTER(fecgpu_frame)]),
         }
         for name, (res, args) in sigs.items():
@@ -447,6 +449,15 @@ def frame_repair(win: int, k: int, r: int, idx: int, sym: bytes) -> bytes:
     buf = ctypes.create_string_buffer(n)
     m = _check(_lib().fecgpu_frame_write_repair(buf, n, win, k, r, idx, sym, len(sym)),
                "fecgpu_frame_write_repair")
+    return buf.raw[:m]
+
+
+def frame_repair_header(win: int, k: int, r: int, idx: int, sym_len: int) -> bytes:
+    """REPAIR frame header without the symbol bytes (fecgpu_frame_write_repair_header):
+    header + symbol == frame_repair(...), so the symbol can be sent from its own buffer."""
+    buf = ctypes.create_string_buffer(32)
+    m = _check(_lib().fecgpu_frame_write_repair_header(buf, 32, win, k, r, idx, sym_len),
+               "fecgpu_frame_write_repair_header")
     return buf.raw[:m]
 
 

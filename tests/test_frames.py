@@ -37,6 +37,25 @@ def test_repair_round_trip(sym_len):
     assert f["payload"] == sym
 
 
+@pytest.mark.parametrize("win,sym_len", [(0, 0), (1, 1200), (70000, 9002), ((1 << 62) - 1, 70000)])
+def test_repair_header_gather_equals_frame(win, sym_len):
+    """Header + symbol bytes from a separate buffer (gather send) == the whole frame."""
+    sym = bytes((i * 13 + 1) & 0xFF for i in range(sym_len))
+    h = fecgpu.frame_repair_header(win, 16, 4, 3, sym_len)
+    assert h + sym == fecgpu.frame_repair(win, 16, 4, 3, sym)
+    n, f = fecgpu.frame_parse(h + sym)
+    assert n == len(h) + sym_len and f["payload"] == sym
+
+
+def test_repair_header_errors():
+    with pytest.raises(fecgpu.FecError):
+        fecgpu.frame_repair_header(1, 16, 4, 4, 10)  # idx >= r
+    with pytest.raises(fecgpu.FecError):
+        fecgpu.frame_repair_header(1 << 62, 16, 4, 0, 10)
+    buf = fecgpu.ctypes.create_string_buffer(4)
+    assert fecgpu._lib().fecgpu_frame_write_repair_header(buf, 4, 1, 16, 4, 0, 1200) == -2
+
+
 def test_parse_errors():
     b = fecgpu.frame_repair(5, 4, 2, 1, b"x" * 100)
     for cut in (0, 1, 3, 5, 9, len(b) - 1):

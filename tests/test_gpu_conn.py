@@ -172,6 +172,30 @@ def test_native_conn_driver(args):
     assert res["recovered"] + res["unrecovered"] == res["lost"]
 
 
+UDP_RING = os.path.join(os.path.dirname(CONN_BENCH), "udp_ring")
+
+
+@pytest.mark.parametrize("args", [
+    ["xor", "8", "2", "1200", "200000", "0.03", "256"],
+    ["gf256", "16", "4", "1200", "100003", "0.08", "128"],   # short last window
+    ["xor", "4", "1", "1000", "10485", "0.02", "16"],        # config-1 shape: 10 MB, XOR k4 r1
+], ids=["xor-k8r2", "gf-k16r4-short-last", "xor-k4r1-10MB"])
+def test_udp_ring_driver(args):
+    """scripts/udp_ring (C++): real UDP loopback sockets -> recvmmsg straight into pinned
+    window rows -> GPU encode -> SOURCE_ID / REPAIR frames sent as gather sends from
+    the rows -> seeded loss -> recvmmsg -> decoder -> in-order delivery.  Every packet is
+    delivered byte-identical or is one the loss pattern cannot recover (exit 3 otherwise)."""
+    import json
+    import subprocess
+    assert os.path.exists(UDP_RING), "build first: make -C scripts"
+    r = subprocess.run([UDP_RING, *args], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["corrupt"] == 0 and res["unrecovered"] == res["expected_unrecovered"]
+    assert res["delivered"] + res["unrecovered"] == res["packets"]
+    assert res["recovered"] + res["unrecovered"] == res["lost"]
+
+
 def test_policy_timeouts(ctx):
     """Scheduling policy: on the caller's clock, a window closes
     window_timeout_us after its first packet and a partly filled batch launches
