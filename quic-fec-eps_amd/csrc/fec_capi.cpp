@@ -20,6 +20,10 @@
 
 using namespace fecgpu;
 
+#ifndef FECGPU_CHECK
+#define FECGPU_CHECK 0  // bounds-checked debug build (fec_kernels.hip); lib/libfecgpu_check.so
+#endif
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -133,6 +137,9 @@ struct fecgpu_ctx {
     int host_chunk_mb = 128;
     // GF encode by the bit-sliced kernel where the code has one (DESIGN.md §GF bit-slicing)
     int bitslice = 1;
+    // FECGPU_CHECK builds: bytes taken off the end of every checked range, so a
+    // test can see the checker fire on a correct kernel ("check_shrink")
+    int check_shrink = 0;
 };
 
 extern "C" {
@@ -217,6 +224,12 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
     if (!std::strcmp(key, "host_chunk_mb")) {
         if (value < 1 || value > 4096) return FECGPU_ERR_INVALID_ARG;
         ctx->host_chunk_mb = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "check_shrink")) {
+        if (!FECGPU_CHECK) return FECGPU_ERR_UNSUPPORTED;  // release build: nothing is checked
+        if (value < 0 || value > (1 << 20)) return FECGPU_ERR_INVALID_ARG;
+        ctx->check_shrink = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "bitslice")) {
@@ -510,6 +523,56 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
     return (ssize_t)nwin;
 }
 
+#if FECGPU_CHECK
+// The byte ranges a launch's symbol accesses may touch (BatchArgs::chk): the
+// windows it reads (and writes in place), and the output rows when they are
+// redirected (split repairs, outputs into mapped host windows).  Ragged
+// windows are located from win_off (copied back: a debug build may wait).
+ssize_t set_check_ranges(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
+                         hipStream_t s) {
+    const uint64_t k = code->k, r = code->r, n = a.nwin, base = reinterpret_cast<uint64_t>(a.win);
+    const bool redirected = a.out_delta || a.out_wdelta;
+    uint64_t lo = base, len;
+    if (!a.win_off) {
+        // in-place encode writes rows k..k+r-1 of the last window; redirected reads stop at row k
+        len = (n - 1) * a.wpitch + ((!decode && redirected) ? k : k + r) * a.stride;
+    } else {
+        std::vector<uint64_t> off(n);
+        std::vector<uint32_t> sl(a.sym_len && !a.off_stride ? n : 0);
+        HIP_TRY(hipMemcpyAsync(off.data(), a.win_off, n * 8, hipMemcpyDefault, s), "check: win_off");
+        if (!sl.empty()) HIP_TRY(hipMemcpyAsync(sl.data(), a.sym_len, n * 4, hipMemcpyDefault, s), "check: sym_len");
+        HIP_TRY(hipStreamSynchronize(s), "check: sync");
+        int64_t mn = INT64_MAX, mx = INT64_MIN;
+        for (uint64_t w = 0; w < n; w++) {
+            uint64_t st = a.off_stride;
+            if (!st) {
+                const uint64_t S = std::min<uint64_t>(sl.empty() ? a.S_all : sl[w], FECGPU_MAX_SYMBOL);
+                st = (S + 15) & ~uint64_t(15);
+            }
+            const int64_t o = (int64_t)off[w];
+            mn = std::min(mn, o);
+            mx = std::max(mx, o + (int64_t)((k + r) * st));
+        }
+        lo = base + (uint64_t)mn;
+        len = (uint64_t)(mx - mn);
+    }
+    a.chk = ChkRange{};
+    a.chk.lo[0] = lo;
+    a.chk.n[0] = len;
+    if (redirected) {
+        if (decode) {  // recovered sources: rows 0..k-1 at + out_delta
+            a.chk.lo[1] = lo + a.out_delta;
+            a.chk.n[1] = len;
+        } else {       // repairs: rows k..k+r-1 at + out_delta + w * out_wdelta
+            a.chk.lo[1] = lo + a.out_delta + k * a.stride;
+            a.chk.n[1] = (n - 1) * (a.wpitch + a.out_wdelta) + r * a.stride;
+        }
+    }
+    for (int i = 0; i < 2; i++) a.chk.n[i] -= std::min<uint64_t>(a.chk.n[i], (uint64_t)ctx->check_shrink);
+    return 0;
+}
+#endif
+
 // Plan and launch one batch whose pointers are all device pointers.
 ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
                       hipStream_t s, bool remote) {
@@ -608,8 +671,27 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
     a.wpb = p.wpb;
     a.win_lds = p.win_lds;
 
+#if FECGPU_CHECK
+    rc = set_check_ranges(ctx, code, decode, a, s);
+    if (rc) return rc;
+#endif
     hipError_t e = decode ? launch_decode(scheme, a, p, s) : launch_encode(scheme, a, p, s);
     if (e != hipSuccess) return dev_err(e, decode ? "decode launch" : "encode launch");
+#if FECGPU_CHECK
+    HIP_TRY(hipStreamSynchronize(s), "check: sync");
+    uint64_t nbad = 0, first = 0;
+    HIP_TRY(take_bounds_faults(&nbad, &first), "check: read faults");
+    if (nbad) {
+        char msg[256];
+        snprintf(msg, sizeof msg,
+                 "bounds check: %s kernel made %llu symbol accesses outside its windows "
+                 "(first at %#llx; windows [%#llx, +%llu))",
+                 decode ? "decode" : "encode", (unsigned long long)nbad, (unsigned long long)first,
+                 (unsigned long long)a.chk.lo[0], (unsigned long long)a.chk.n[0]);
+        g_last_error = msg;
+        return FECGPU_ERR_DEVICE;
+    }
+#endif
     return rc;
 }
 

@@ -17,6 +17,12 @@ constexpr int kMaxK = 64;
 constexpr int kMaxR = 8;
 
 // Geometry + decode inputs of one batch, passed by value as the kernel argument.
+// Byte ranges [lo, lo + n) that symbol loads / stores of one launch may touch
+// (FECGPU_CHECK builds; lo is an address, n == 0 = range unused).
+struct ChkRange {
+    uint64_t lo[2], n[2];
+};
+
 struct BatchArgs {
     uint8_t *win;
     const uint64_t *win_off;   // nullable: ragged windows
@@ -46,6 +52,7 @@ struct BatchArgs {
     // ragged layout (win_off): symbol pitch of every window; 0 = packed
     // round_up(S_w, 16)
     uint32_t off_stride;
+    ChkRange chk;              // FECGPU_CHECK builds: where this launch's symbols lie
 };
 
 struct LaunchPlan {
@@ -77,6 +84,11 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
 ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
                      hipStream_t s, bool remote = false);
 hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s);
+
+// FECGPU_CHECK builds: symbol accesses outside their launch's ChkRange since
+// the last call (count, first offending address), then resets the record.
+// Release builds: always {0, 0}.
+hipError_t take_bounds_faults(uint64_t *count, uint64_t *first);
 
 struct SynthArgs {
     uint8_t *win;

@@ -84,6 +84,14 @@
 #ifndef FECGPU_ENC_SGPR
 #define FECGPU_ENC_SGPR 0  // GF encode tables via scalar loads instead of LDS (A/B knob)
 #endif
+#ifndef FECGPU_CHECK
+// Bounds-checked debug build (GPU AddressSanitizer is not available
+// on this pool): every symbol load / store is checked against the byte ranges
+// the host computed for the launch (BatchArgs::chk); an access outside them is
+// not performed (loads return zero) and is recorded for the host, which fails
+// the call with FECGPU_ERR_DEVICE.  Built as lib/libfecgpu_check.so.
+#define FECGPU_CHECK 0
+#endif
 #ifndef FECGPU_PIPE
 #define FECGPU_PIPE 0  // register double-buffered input loads in the GF bodies (A/B: no gain,
                        // costs VGPRs / occupancy on decode; profiles/r01 notes)
@@ -103,7 +111,36 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 *gptr_c;
 typedef __attribute__((address_space(1))) u32x4 *gptr;
 
+#if FECGPU_CHECK
+__shared__ ChkRange s_chk;                   // the launch's ranges (copied by CHK_PROLOGUE)
+__device__ unsigned long long g_chk_bad[2];  // faulting accesses, first address
+
+__device__ __forceinline__ bool chk_ok(const uint8_t *p) {
+    const uint64_t x = reinterpret_cast<uint64_t>(p);
+    bool ok = false;
+#pragma unroll
+    for (int i = 0; i < 2; i++) ok |= s_chk.n[i] >= 16 && x - s_chk.lo[i] <= s_chk.n[i] - 16;
+    if (!ok) {
+        atomicAdd(&g_chk_bad[0], 1ull);
+        atomicCAS(&g_chk_bad[1], 0ull, (unsigned long long)x);
+    }
+    return ok;
+}
+#define CHK_PROLOGUE(a)                      \
+    do {                                     \
+        if (threadIdx.x == 0) s_chk = (a).chk; \
+        __syncthreads();                     \
+    } while (0)
+#else
+#define CHK_PROLOGUE(a) \
+    do {                \
+    } while (0)
+#endif
+
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+#if FECGPU_CHECK
+    if (!chk_ok(p)) return make_uint4(0, 0, 0, 0);
+#endif
 #if FECGPU_NT
     const u32x4 v = __builtin_nontemporal_load((gptr_c)(p));
 #else
@@ -112,6 +149,9 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
+#if FECGPU_CHECK
+    if (!chk_ok(p)) return;
+#endif
     const u32x4 x = {v.x, v.y, v.z, v.w};
 #if FECGPU_NT || FECGPU_NT_STORE
     __builtin_nontemporal_store(x, (gptr)(p));
@@ -482,6 +522,7 @@ __device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t 
 // ============================================================ encode ===
 template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
+    CHK_PROLOGUE(a);
     if constexpr (FLAT) {
         for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t w, uint32_t, bool valid) {
             xor_encode_slot<R>(p, stride, a.k, valid, a.out_delta + w * a.out_wdelta);
@@ -508,6 +549,7 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
 // host memory, where each batch of loads is a PCIe round trip.
 template <int R, bool FLAT, int UO = 0>
 __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a) {
+    CHK_PROLOGUE(a);
     const int k = a.k;
 #if FECGPU_ENC_SGPR
     // kernel-uniform tables read through the constant address space with a
@@ -725,6 +767,7 @@ __device__ __forceinline__ void sources(const uint8_t *pa, const uint8_t *pb, ui
 // units; unit u covers columns u and u + h (the second absent when odd).
 template <int K, int R>
 __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
+    CHK_PROLOGUE(a);
     __shared__ GroupLds g;
     for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
         const uint64_t w0 = xr.cur * a.wpb;
@@ -768,6 +811,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
 // ============================================================ decode ===
 template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
+    CHK_PROLOGUE(a);
     if constexpr (FLAT) {
         // for_flat_slots with the next slot's present mask loaded one iteration
         // ahead: the plan (and so the data loads) never waits on that load.
@@ -1114,6 +1158,7 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
 
 template <int R>
 __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a) {
+    CHK_PROLOGUE(a);
     extern __shared__ uint4 dyn[];
     __shared__ uint8_t s_exp[512];
     __shared__ uint8_t s_log[256];
@@ -1399,6 +1444,24 @@ hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
         else DISPATCH_R(a.r, launch(xor_decode_kernel<RR, false>, a, p, s, false))
     }
     DISPATCH_R(a.r, launch(gf_decode_kernel<RR>, a, p, s, false))
+}
+
+hipError_t take_bounds_faults(uint64_t *count, uint64_t *first) {
+    *count = *first = 0;
+#if FECGPU_CHECK
+    unsigned long long v[2] = {0, 0};
+    hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_chk_bad), sizeof(v));
+    if (e != hipSuccess) return e;
+    *count = v[0];
+    *first = v[1];
+    if (v[0]) {
+        const unsigned long long z[2] = {0, 0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_chk_bad), z, sizeof(z));
+    }
+    return e;
+#else
+    return hipSuccess;
+#endif
 }
 
 hipError_t launch_synth(const SynthArgs &a, hipStream_t s) {

@@ -1,0 +1,256 @@
+"""Bounds-checked debug build (GPU AddressSanitizer is not available
+on this pool, so lib/libfecgpu_check.so, built with FECGPU_CHECK=1, checks every
+symbol load / store of every batch kernel against the byte ranges of the launch's
+windows and fails the call with FECGPU_ERR_DEVICE when one falls outside).
+
+The layouts and codes of the parity suite run on that build: their outputs equal
+the oracle's AND no kernel touched a byte outside its windows.  check_shrink
+takes bytes off the end of the checked ranges, so the checker is seen to fire.
+"""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import fecgpu  # noqa: E402
+import oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "quic-fec-eps_amd")
+CHECK_LIB = os.path.join(PKG, "lib", "libfecgpu_check.so")
+SEED = 97531
+
+
+def _load_check_module():
+    """A second copy of the fecgpu package bound to the bounds-checked library."""
+    assert os.path.exists(CHECK_LIB), "build first: make -C quic-fec-eps_amd"
+    os.environ["FECGPU_LIB"] = CHECK_LIB
+    try:
+        spec = importlib.util.spec_from_file_location("fecgpu_check", os.path.join(PKG, "fecgpu", "__init__.py"))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[spec.name] = mod
+        spec.loader.exec_module(mod)
+    finally:
+        del os.environ["FECGPU_LIB"]
+    assert mod.LIB_PATH == CHECK_LIB
+    return mod
+
+
+@pytest.fixture(scope="module")
+def chk():
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    O.build()
+    m = _load_check_module()
+    c = m.Context()
+    yield m, c
+    c.close()
+
+
+def _scheme(s):
+    return O.XOR if s == "xor" else O.GF256
+
+
+def _oracle(scheme, k, r, wins, S, present, poison=0xAB):
+    enc = wins.copy()
+    O.encode_batch(_scheme(scheme), k, r, S, enc, 4)
+    dec = enc.copy()
+    O.erase(dec, present, k, r, fill=poison)
+    st = O.decode_batch(_scheme(scheme), k, r, S, dec, present, 4)
+    return enc, dec, st
+
+
+def _emitted_equal(a, b, S):
+    return all(np.array_equal(a[w, :, :int(S[w])], b[w, :, :int(S[w])]) for w in range(a.shape[0]))
+
+
+CASES = [
+    # scheme, k, r, workload, L, erasure, nwin: flat and group modes, per-window S,
+    # tiny and large symbols, r > k, the bit-sliced codes
+    ("xor", 8, 2, 0, 1200, 1, 64),
+    ("xor", 5, 3, 0, 17, 2, 64),
+    ("xor", 8, 2, 1, 0, 2, 12),
+    ("gf256", 16, 4, 0, 1200, 1, 64),
+    ("gf256", 32, 8, 1, 0, 2, 12),
+    ("gf256", 32, 8, 0, 1200, 2, 40),
+    ("gf256", 16, 8, 0, 16, 1, 33),
+    ("gf256", 1, 1, 0, 1, 1, 5),
+    ("gf256", 56, 8, 0, 64, 1, 9),
+    ("gf256", 3, 5, 0, 16, 1, 8),
+]
+
+
+@pytest.mark.parametrize("scheme,k,r,wl,L,era,nwin", CASES)
+def test_checked_encode_decode_vs_oracle(chk, scheme, k, r, wl, L, era, nwin):
+    """Windows in a tensor of exactly nwin x (k + r) x stride bytes: every access of
+    encode and decode stays inside (else the call raises) and the bytes equal the oracle."""
+    m, ctx = chk
+    S = O.sym_lens(wl, SEED, 0, nwin, k, L)
+    stride = O.round_up(int(S.max()), 16)
+    wins = O.make_windows(wl, SEED, 0, nwin, k, r, L, stride)
+    present = O.presents(era, SEED, 0, nwin, _scheme(scheme), k, r)
+    oe, od, os_ = _oracle(scheme, k, r, wins, S, present)
+    code = m.Code(scheme, k, r)
+    d = torch.from_numpy(wins.copy()).cuda()
+    kw = dict(sym_len_all=int(S[0])) if wl == 0 else dict(sym_len=torch.from_numpy(S.astype(np.int32)).cuda())
+    ctx.encode_batch(code, d, nwin=nwin, stride=stride, **kw)
+    torch.cuda.synchronize()
+    enc = d.cpu().numpy()
+    assert _emitted_equal(enc, oe, S)
+    mask = torch.from_numpy(np.array([[(int(p) >> i) & 1 for i in range(k + r)] for p in present], bool)).cuda()
+    d[~mask] = 0xAB
+    st = torch.full((nwin,), 7, dtype=torch.uint8, device="cuda")
+    ctx.decode_batch(code, d, torch.from_numpy(present.astype(np.int64)).cuda(), st, nwin=nwin,
+                     stride=stride, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), os_)
+    assert _emitted_equal(d.cpu().numpy(), od, S)
+
+
+@pytest.mark.parametrize("pitch", [0, 320])
+def test_checked_ragged_layout(chk, pitch):
+    """win_off windows, packed (pitch 0: stride round_up(S_w, 16)) or fixed pitch,
+    at scattered offsets with gaps: the checked range is derived from win_off."""
+    m, ctx = chk
+    k, r, nwin = 6, 3, 17
+    rng = np.random.default_rng(11)
+    S = rng.integers(1, 300, nwin).astype(np.uint32)
+    strides = [pitch or O.round_up(int(s), 16) for s in S]
+    offs, pos = [], 0
+    for w in range(nwin):
+        pos += 16 * int(rng.integers(0, 4))
+        offs.append(pos)
+        pos += (k + r) * strides[w]
+    for scheme in ("gf256", "xor"):
+        buf = np.zeros(pos, np.uint8)
+        for w in range(nwin):
+            win = np.zeros((k + r, strides[w]), np.uint8)
+            win[:k, :S[w]] = rng.integers(0, 256, (k, int(S[w])), dtype=np.uint8)
+            buf[offs[w]:offs[w] + win.size] = win.ravel()
+        present = O.presents(1, SEED, 0, nwin, _scheme(scheme), k, r)
+        d = torch.from_numpy(buf).cuda()
+        off_t = torch.tensor(offs, dtype=torch.int64).cuda()
+        sl = torch.from_numpy(S.astype(np.int32)).cuda()
+        code = m.Code(scheme, k, r)
+        ctx.encode_batch(code, d, nwin=nwin, stride=pitch, sym_len=sl, win_off=off_t)
+        enc = d.cpu().numpy()
+        for w in range(nwin):
+            for i in range(k + r):
+                if not (int(present[w]) >> i) & 1:
+                    a = offs[w] + i * strides[w]
+                    d[a:a + strides[w]] = 0xCD
+        st = torch.zeros(nwin, dtype=torch.uint8, device="cuda")
+        ctx.decode_batch(code, d, torch.from_numpy(present.astype(np.int64)).cuda(), st,
+                         nwin=nwin, stride=pitch, sym_len=sl, win_off=off_t)
+        out = d.cpu().numpy()
+        assert int(st.sum().item()) == 0
+        for w in range(nwin):
+            o = np.frombuffer(enc[offs[w]:offs[w] + (k + r) * strides[w]].tobytes(), np.uint8)
+            o = o.reshape(k + r, strides[w]).copy()
+            ref = o.copy()
+            O.encode_batch(_scheme(scheme), k, r, np.array([S[w]], np.uint32), ref[None], 1)
+            assert np.array_equal(o[:, :S[w]], ref[:, :S[w]]), (scheme, w)
+            rec = out[offs[w]:offs[w] + o.size].reshape(o.shape)
+            assert np.array_equal(rec[:k, :S[w]], ref[:k, :S[w]]), (scheme, w)
+
+
+@pytest.mark.parametrize("scheme,k,r,wl,L", [("xor", 8, 2, 0, 1200), ("gf256", 16, 4, 0, 1200),
+                                              ("gf256", 32, 8, 1, 0), ("gf256", 4, 7, 0, 100)])
+def test_checked_encode_split(chk, scheme, k, r, wl, L):
+    """Split layout: sources read only inside src, repairs written only inside repair."""
+    m, ctx = chk
+    nwin = 37
+    S = O.sym_lens(wl, SEED, 0, nwin, k, L)
+    stride = O.round_up(int(S.max()), 16)
+    wins = O.make_windows(wl, SEED, 0, nwin, k, r, L, stride)
+    oe, _, _ = _oracle(scheme, k, r, wins, S, np.full(nwin, (1 << (k + r)) - 1, np.uint64))
+    src = torch.from_numpy(np.ascontiguousarray(wins[:, :k])).cuda()
+    rep = torch.full((nwin, r, stride), 0x77, dtype=torch.uint8, device="cuda")
+    kw = dict(sym_len_all=int(S[0])) if wl == 0 else dict(sym_len=torch.from_numpy(S.astype(np.int32)).cuda())
+    ctx.encode_split(m.Code(scheme, k, r), src, rep, nwin=nwin, stride=stride, **kw)
+    torch.cuda.synchronize()
+    got = np.concatenate([src.cpu().numpy(), rep.cpu().numpy()], axis=1)
+    assert np.array_equal(got[:, :k], wins[:, :k])
+    assert _emitted_equal(got, oe, S)
+
+
+@pytest.mark.parametrize("direct", [0, 6, 7])
+def test_checked_host_pipeline(chk, direct):
+    """Pinned host windows through the chunked pipeline (staging slots reused, outputs
+    stored into the mapped host windows for direct != 0): each launch's range is its
+    chunk."""
+    m, ctx = chk
+    k, r, nwin = 32, 8, 120
+    S = O.sym_lens(1, SEED, 0, nwin, k, 0)
+    stride = O.round_up(int(S.max()), 16)
+    wins = O.make_windows(1, SEED, 0, nwin, k, r, 0, stride)
+    present = O.presents(2, SEED, 0, nwin, O.GF256, k, r)
+    oe, od, os_ = _oracle("gf256", k, r, wins, S, present)
+    buf = m.PinnedBuffer(wins.nbytes)
+    h = buf.array.reshape(wins.shape)
+    h[:] = wins
+    ctx.set_tuning("host_direct", direct)
+    ctx.set_tuning("host_chunk_mb", 1)
+    try:
+        code = m.Code("gf256", k, r)
+        ctx.encode_batch(code, h, nwin=nwin, stride=stride, sym_len=S, flags=m.F_HOST_PTRS)
+        enc = h.copy()
+        O.erase(h, present, k, r, fill=0xAB)
+        st = np.full(nwin, 9, np.uint8)
+        ctx.decode_batch(code, h, present, st, nwin=nwin, stride=stride, sym_len=S, flags=m.F_HOST_PTRS)
+        dec = h.copy()
+    finally:
+        ctx.set_tuning("host_direct", 6)
+        ctx.set_tuning("host_chunk_mb", 128)
+        del h
+        buf.close()
+    assert _emitted_equal(enc, oe, S)
+    assert np.array_equal(st, os_)
+    assert _emitted_equal(dec, od, S)
+
+
+@pytest.mark.parametrize("scheme,k,r,L", [("xor", 8, 2, 1200), ("gf256", 16, 4, 1200), ("gf256", 32, 8, 1200)])
+def test_checker_fires_when_the_range_is_short(chk, scheme, k, r, L):
+    """check_shrink=16 hides the last 16-byte column of the batch from the checker:
+    the kernel's (correct) access to it must be reported as a fault."""
+    m, ctx = chk
+    nwin = 8
+    wins = O.make_windows(0, SEED, 0, nwin, k, r, L, L)
+    d = torch.from_numpy(wins).cuda()
+    code = m.Code(scheme, k, r)
+    ctx.set_tuning("check_shrink", 16)
+    try:
+        with pytest.raises(m.FecError, match="bounds check"):
+            ctx.encode_batch(code, d, nwin=nwin, stride=L, sym_len_all=L)
+    finally:
+        ctx.set_tuning("check_shrink", 0)
+    ctx.encode_batch(code, d, nwin=nwin, stride=L, sym_len_all=L)  # and clean again
+
+
+@pytest.mark.parametrize("scheme,k,r,framing,mtu,loss,batch,vary", [
+    ("xor", 4, 1, "lenprefix", 1200, 0.03, 16, False),
+    ("gf256", 16, 4, "lenprefix", 1350, 0.08, 32, True),
+    ("gf256", 8, 3, "fixed", 1000, 0.1, 8, False),
+])
+def test_checked_per_connection(chk, scheme, k, r, framing, mtu, loss, batch, vary):
+    """Per-connection encoder / decoder on the checked build: their launches run on
+    windows in mapped pinned memory (remote plan, ragged fixed-pitch decode of
+    pooled slots with offsets that wrap below the base)."""
+    from test_gpu_conn import _run, _stream
+    m, ctx = chk
+    data = _stream(600 * 1000, 21)
+    _run(ctx, m.Code(scheme, k, r, framing), data, mtu, loss, 9, batch=batch, vary=vary, m=m)
+
+
+def test_release_build_has_no_checker():
+    ctx = fecgpu.Context()
+    try:
+        with pytest.raises(fecgpu.FecError) as e:
+            ctx.set_tuning("check_shrink", 16)
+        assert e.value.code == fecgpu.ERR_UNSUPPORTED
+    finally:
+        ctx.close()

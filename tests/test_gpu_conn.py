@@ -45,15 +45,16 @@ def _recv_source(wire, framed):
     return f["win"], f["idx"], wire[n:]
 
 
-def _run(ctx, code, data, mtu, loss, seed, batch=256, vary=False, framed=False):
+def _run(ctx, code, data, mtu, loss, seed, batch=256, vary=False, framed=False, m=fecgpu):
+    """m: the fecgpu module (a copy bound to another library build may be passed)."""
     rng = np.random.default_rng(seed)
     pkts, pos = [], 0
     while pos < len(data):
         n = mtu if not vary else int(rng.integers(1, mtu + 1))
         pkts.append(data[pos:pos + n])
         pos += n
-    enc = fecgpu.Encoder(ctx, code, max_len=mtu, batch=batch)
-    dec = fecgpu.Decoder(ctx, code, max_len=mtu, batch=batch)
+    enc = m.Encoder(ctx, code, max_len=mtu, batch=batch)
+    dec = m.Decoder(ctx, code, max_len=mtu, batch=batch)
     ids = []
     lost_src = rng.random(len(pkts)) < loss
     for p, lost in zip(pkts, lost_src):
