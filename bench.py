@@ -252,6 +252,7 @@ def main():
             "value": round(value, 3),
             "unit": "GB/s",
             "n_gpus": world,
+            "value_per_gpu": round(value / world, 3),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
