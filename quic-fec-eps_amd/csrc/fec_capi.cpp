@@ -23,6 +23,9 @@ using namespace fecgpu;
 #ifndef FECGPU_CHECK
 #define FECGPU_CHECK 0  // bounds-checked debug build (fec_kernels.hip); lib/libfecgpu_check.so
 #endif
+#ifndef FECGPU_BS_FLAT
+#define FECGPU_BS_FLAT 1  // fec_kernels.hip: bit-sliced encode in a flat unit space on uniform windows
+#endif
 
 namespace {
 
@@ -137,6 +140,8 @@ struct fecgpu_ctx {
     int host_chunk_mb = 128;
     // GF encode by the bit-sliced kernel where the code has one (DESIGN.md §GF bit-slicing)
     int bitslice = 1;
+    // bit-sliced encode in group mode: passes per group at the longest window
+    int bs_passes = 8;
     // FECGPU_CHECK builds: bytes taken off the end of every checked range, so a
     // test can see the checker fire on a correct kernel ("check_shrink")
     int check_shrink = 0;
@@ -230,6 +235,11 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         if (!FECGPU_CHECK) return FECGPU_ERR_UNSUPPORTED;  // release build: nothing is checked
         if (value < 0 || value > (1 << 20)) return FECGPU_ERR_INVALID_ARG;
         ctx->check_shrink = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "bs_passes")) {
+        if (value < 1 || value > 256) return FECGPU_ERR_INVALID_ARG;
+        ctx->bs_passes = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "bitslice")) {
@@ -650,10 +660,13 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         // longest window (a lane's unit is k sources x 32 B of heavy XOR work,
         // so a partly idle last pass costs more than in the table kernels).
         p.bitslice = true;
+#if !FECGPU_BS_FLAT
         p.flat = false;
+#endif
         p.lds_bytes = 0;
         const uint32_t units = ncol ? (ncol + 1) / 2 : (uint32_t)((stride >> 4) + 1) / 2;
-        p.wpb = units ? std::max(1, std::min<int>(kMaxWpb, (int)((8u * kBlock + units - 1) / units))) : kMaxWpb;
+        const uint32_t want = (uint32_t)ctx->bs_passes * kBlock;
+        p.wpb = units ? std::max(1, std::min<int>(kMaxWpb, (int)((want + units - 1) / units))) : kMaxWpb;
     }
     if (remote) {  // PCIe-latency bound: as many workgroups as windows
         p.remote = true;

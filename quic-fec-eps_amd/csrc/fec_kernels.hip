@@ -763,48 +763,100 @@ __device__ __forceinline__ void sources(const uint8_t *pa, const uint8_t *pb, ui
 #define FECGPU_BS_VOP2 0  // bit-sliced encode: plain (VOP2) XORs for combinations and single terms
 #endif
 
-// Group mode over column pairs: window wl of the group has h = ceil(ncol / 2)
-// units; unit u covers columns u and u + h (the second absent when odd).
+#ifndef FECGPU_BS_FLAT
+// bit-sliced encode on uniform windows: one flat unit space over all windows
+// (no groups, so no partly idle last pass per group) instead of group mode:
+// S = 1200 k32 r8 3.84 -> 4.60 TB/s, k16 r8 4.01 -> 4.30
+// (profiles/r01_bs_layout.txt)
+#define FECGPU_BS_FLAT 1
+#endif
+#ifndef FECGPU_BS_ADJ
+// bit-sliced encode: a unit is two adjacent columns (2u, 2u + 1) instead of
+// u and u + h (A/B knob; 10-25 % slower: each load instruction then touches
+// every other 16 B of 2 KiB, profiles/r01_bs_layout.txt)
+#define FECGPU_BS_ADJ 0
+#endif
+
+namespace bs {
+
+// The two 16-B columns of unit u of a window with ncol columns (h = ceil(ncol / 2)
+// units).  Without a second column B repeats A: same inputs, same outputs, so
+// its stores rewrite A's bytes with equal values (no branch).
+__device__ __forceinline__ void unit_cols(uint8_t *base, uint32_t u, uint32_t h, uint32_t ncol,
+                                          uint8_t *&pa, uint8_t *&pb) {
+#if FECGPU_BS_ADJ
+    pa = base + u * 32u;
+    pb = 2 * u + 1 < ncol ? pa + 16 : pa;
+#else
+    pa = base + u * 16u;
+    pb = u + h < ncol ? pa + h * 16u : pa;
+#endif
+}
+
+// one unit: every source's planes into the R x 8 output planes, then stores
 template <int K, int R>
+__device__ __forceinline__ void unit(uint8_t *pa, uint8_t *pb, uint32_t stride, bool live, uint64_t od) {
+    uint32_t acc[R][8];
+    sources<K, R, FECGPU_BS_U, 0>(pa, pb, stride, acc);
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        tr8(acc[i]);
+        if (live) {
+            st16(pa + od + (size_t)(K + i) * stride, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
+            st16(pb + od + (size_t)(K + i) * stride, make_uint4(acc[i][4], acc[i][5], acc[i][6], acc[i][7]));
+        }
+    }
+}
+
+}  // namespace bs
+
+// Units of h = ceil(ncol / 2) per window, each two 16-B columns (bs::unit_cols).
+//   FLAT : uniform windows; units numbered over the whole batch, 256-unit chunks
+//          split over the XCDs and walked by a persistent grid.
+//   group: per-window S / ragged windows; a workgroup streams the units of
+//          `wpb` windows at a time (prefix sums in LDS).
+// Trip counts are workgroup-uniform (lanes past the end redo the last unit
+// without storing), so the barriers inside a unit are safe.
+template <int K, int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
-    __shared__ GroupLds g;
-    for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
-        const uint64_t w0 = xr.cur * a.wpb;
-        const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
-        group_geometry(a, g, w0, nb);
-        __syncthreads();
-        if (threadIdx.x < 64)
-            block_prefix(g.pfx, (int)threadIdx.x < nb ? (g.ncol[threadIdx.x] + 1u) >> 1 : 0u, threadIdx.x);
-        __syncthreads();
-        const uint32_t total = g.pfx[nb];
-        int wl = 0;
-        // workgroup-uniform trip count (lanes past the end redo the last unit
-        // without storing), so a barrier inside the unit is safe
-        for (uint32_t s0 = 0; s0 < total; s0 += kBlock) {
-            const bool live = s0 + threadIdx.x < total;
-            const uint32_t s = live ? s0 + threadIdx.x : total - 1;
-            while (s >= g.pfx[wl + 1]) wl++;
-            const uint32_t u = s - g.pfx[wl], h = g.pfx[wl + 1] - g.pfx[wl];
-            // without a second column B repeats A: same inputs, same outputs, so
-            // its stores rewrite A's bytes with equal values (no branch)
-            const bool has_b = u + h < g.ncol[wl];
-            const uint32_t stride = g.stride[wl];
-            uint8_t *pa = reinterpret_cast<uint8_t *>(g.base[wl]) + u * 16u;
-            uint8_t *pb = has_b ? pa + h * 16u : pa;
-            uint32_t acc[R][8];
-            bs::sources<K, R, FECGPU_BS_U, 0>(pa, pb, stride, acc);
-            const uint64_t od = a.out_delta + (w0 + wl) * a.out_wdelta;
-#pragma unroll
-            for (int i = 0; i < R; i++) {
-                bs::tr8(acc[i]);
-                if (live) {
-                    st16(pa + od + (size_t)(K + i) * stride, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
-                    st16(pb + od + (size_t)(K + i) * stride, make_uint4(acc[i][4], acc[i][5], acc[i][6], acc[i][7]));
-                }
-            }
+    if constexpr (FLAT) {
+        const uint32_t ncol = a.ncol, h = (ncol + 1) >> 1;
+        const uint64_t total = a.nwin * h;
+        for (XcdRange xr = xcd_range((total + kBlock - 1) / kBlock, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+            uint64_t s = xr.cur * kBlock + threadIdx.x;
+            const bool live = s < total;
+            if (!live) s = total - 1;
+            const uint64_t w = s / h;
+            const uint32_t u = (uint32_t)(s - w * h);
+            uint8_t *pa, *pb;
+            bs::unit_cols(a.win + w * a.wpitch, u, h, ncol, pa, pb);
+            bs::unit<K, R>(pa, pb, a.stride, live, a.out_delta + w * a.out_wdelta);
         }
-        __syncthreads();
+        return;
+    } else {
+        __shared__ GroupLds g;
+        for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+            const uint64_t w0 = xr.cur * a.wpb;
+            const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
+            group_geometry(a, g, w0, nb);
+            __syncthreads();
+            if (threadIdx.x < 64)
+                block_prefix(g.pfx, (int)threadIdx.x < nb ? (g.ncol[threadIdx.x] + 1u) >> 1 : 0u, threadIdx.x);
+            __syncthreads();
+            const uint32_t total = g.pfx[nb];
+            int wl = 0;
+            for (uint32_t s0 = 0; s0 < total; s0 += kBlock) {
+                const bool live = s0 + threadIdx.x < total;
+                const uint32_t s = live ? s0 + threadIdx.x : total - 1;
+                while (s >= g.pfx[wl + 1]) wl++;
+                uint8_t *pa, *pb;
+                bs::unit_cols(reinterpret_cast<uint8_t *>(g.base[wl]), s - g.pfx[wl], g.pfx[wl + 1] - g.pfx[wl],
+                              g.ncol[wl], pa, pb);
+                bs::unit<K, R>(pa, pb, g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -1345,12 +1397,16 @@ int resident_blocks(const void *fn, uint32_t lds) {
     return cus * per;
 }
 
+// chunks != 0: the kernel walks that many work units of its own (a flat unit
+// space other than 16-B slots) on a persistent grid, like flat mode.
 template <class K>
-hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, bool flat) {
+hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, bool flat,
+                  uint64_t chunks = 0) {
     const void *fn = reinterpret_cast<const void *>(kernel);
     // work units: 256-slot chunks (flat) or window groups
-    const uint64_t want = flat ? (a.nwin * a.ncol + kBlock - 1) / kBlock
-                               : (a.nwin + a.wpb - 1) / a.wpb;
+    const uint64_t want = chunks ? chunks
+                          : flat ? (a.nwin * a.ncol + kBlock - 1) / kBlock
+                                 : (a.nwin + a.wpb - 1) / a.wpb;
     // Flat mode: persistent, 2 x resident workgroups (measured best on cfg2/cfg3).
     // Group mode: one workgroup per group unless a multiplier is forced — the
     // dispatcher's dynamic assignment balances uneven windows better than a
@@ -1361,7 +1417,7 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         grid = std::min<uint64_t>(want, (uint64_t)cus * (uint64_t)p.blocks_per_cu);
-    } else if (flat || p.grid_mult > 0) {
+    } else if (flat || chunks || p.grid_mult > 0) {
         const int mult = p.grid_mult > 0 ? p.grid_mult : 2;
         grid = std::min<uint64_t>(want, (uint64_t)resident_blocks(fn, p.lds_bytes) * (uint64_t)mult);
     }
@@ -1421,8 +1477,11 @@ bool bitslice_supported(int k, int r, int matrix) {
 hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     if (p.bitslice) {
-#define FECGPU_BS_LAUNCH(K_, R_) \
-        if (a.k == K_ && a.r == R_) return launch(gf_encode_bs_kernel<K_, R_>, a, p, s, false);
+#define FECGPU_BS_LAUNCH(K_, R_)                                                                  \
+        if (a.k == K_ && a.r == R_)                                                               \
+            return p.flat ? launch(gf_encode_bs_kernel<K_, R_, true>, a, p, s, false,             \
+                                   (a.nwin * ((a.ncol + 1) / 2) + kBlock - 1) / kBlock)             \
+                          : launch(gf_encode_bs_kernel<K_, R_, false>, a, p, s, false);
         FECGPU_BS_CODES(FECGPU_BS_LAUNCH)
 #undef FECGPU_BS_LAUNCH
         return hipErrorInvalidValue;
