@@ -42,8 +42,10 @@ PCIE_PEAK_GBS = 126.0  # PCIe Gen5 x16, 63 GB/s per direction (spec), both direc
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # one cfg2 step is ~0.3 ms: 200 steps keep the timed region (~60 ms) well
+    # above barrier / launch jitter across ranks, and still finish in seconds
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, choices=sorted(workloads.CONFIGS))
     ap.add_argument("--nwin", type=int, default=0, help="windows per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,

@@ -197,6 +197,29 @@ def test_udp_ring_driver(args):
     assert res["recovered"] + res["unrecovered"] == res["lost"]
 
 
+@pytest.mark.parametrize("args", [
+    ["conn_bench_asan", "gf256", "32", "8", "9000", "16", "0.12", "16", "1"],
+    ["conn_bench_asan", "xor", "4", "1", "1000", "8", "0.03", "16", "0", "64", "0.02"],
+    ["conn_bench_asan", "gf256", "5", "3", "333", "2", "0.2", "3", "0", "7", "0.05"],
+    ["udp_ring_asan", "gf256", "16", "4", "1200", "50003", "0.08", "128"],
+], ids=["conn-gf-k32r8-lp", "conn-xor-reorder-dup", "conn-gf-short-last", "udp-gf-k16r4"])
+def test_native_drivers_under_asan(args):
+    """The per-connection objects, pools, frames and pinned rings under host
+    AddressSanitizer + UBSan (lib/asan/libfecgpu.so: host code instrumented, kernels
+    the release ones; GPU ASan is not available on this pool).  Any report aborts."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(CONN_BENCH), args[0])
+    assert os.path.exists(exe), "build first: make -C scripts"
+    env = dict(os.environ,
+               # quarantine off: ROCm's ASan runtime otherwise recycles one of its device
+               # allocator's chunks in the HSA runtime's exit-time finalizer and trips a CHECK
+               ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0:halt_on_error=1:quarantine_size_mb=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe, *args[1:]], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
+
+
 def test_policy_timeouts(ctx):
     """Scheduling policy: on the caller's clock, a window closes
     window_timeout_us after its first packet and a partly filled batch launches
