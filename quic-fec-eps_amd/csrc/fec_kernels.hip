@@ -752,7 +752,12 @@ __device__ __forceinline__ void sources(const uint8_t *pa, const uint8_t *pb, ui
 }  // namespace bs
 
 #ifndef FECGPU_BS_U
-#define FECGPU_BS_U 8  // bit-sliced encode: sources loaded per batch (8 > 4 > 2 by 1-3 %, r01)
+#define FECGPU_BS_U 8  // bit-sliced encode, group mode: sources loaded per batch (8 > 4 > 2 by 1-3 % on cfg4, r01)
+#endif
+#ifndef FECGPU_BS_U_FLAT
+// bit-sliced encode, flat mode: sources loaded per batch (2 > 4 > 8: k32 r8
+// 4.72 / 4.60 / 4.59 TB/s at S = 1200, profiles/r01_bs_layout.txt)
+#define FECGPU_BS_U_FLAT 2
 #endif
 #ifndef FECGPU_BS_SYNC
 // bit-sliced encode: workgroup barrier after every batch, keeping the waves of a
@@ -793,11 +798,12 @@ __device__ __forceinline__ void unit_cols(uint8_t *base, uint32_t u, uint32_t h,
 #endif
 }
 
-// one unit: every source's planes into the R x 8 output planes, then stores
-template <int K, int R>
+// one unit: every source's planes into the R x 8 output planes (U sources
+// loaded per batch), then stores
+template <int K, int R, int U>
 __device__ __forceinline__ void unit(uint8_t *pa, uint8_t *pb, uint32_t stride, bool live, uint64_t od) {
     uint32_t acc[R][8];
-    sources<K, R, FECGPU_BS_U, 0>(pa, pb, stride, acc);
+    sources<K, R, U, 0>(pa, pb, stride, acc);
 #pragma unroll
     for (int i = 0; i < R; i++) {
         tr8(acc[i]);
@@ -831,7 +837,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
             const uint32_t u = (uint32_t)(s - w * h);
             uint8_t *pa, *pb;
             bs::unit_cols(a.win + w * a.wpitch, u, h, ncol, pa, pb);
-            bs::unit<K, R>(pa, pb, a.stride, live, a.out_delta + w * a.out_wdelta);
+            bs::unit<K, R, FECGPU_BS_U_FLAT>(pa, pb, a.stride, live, a.out_delta + w * a.out_wdelta);
         }
         return;
     } else {
@@ -853,7 +859,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
                 uint8_t *pa, *pb;
                 bs::unit_cols(reinterpret_cast<uint8_t *>(g.base[wl]), s - g.pfx[wl], g.pfx[wl + 1] - g.pfx[wl],
                               g.ncol[wl], pa, pb);
-                bs::unit<K, R>(pa, pb, g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
+                bs::unit<K, R, FECGPU_BS_U>(pa, pb, g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
             }
             __syncthreads();
         }
