@@ -36,7 +36,7 @@ for s in "$@"; do
         smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
         pytest) step pytest 1100 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         pytest-x) step pytest 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
-        bench2) step bench2 600 python bench.py --config 2 --steps 20 --warmup 3 ;;
+        bench2) step bench2 600 python bench.py ;;
         bench3) step bench3 600 python bench.py --config 3 --steps 10 --warmup 2 --cpu-seconds 10 ;;
         bench4) step bench4 600 python bench.py --config 4 --steps 5 --warmup 1 --cpu-seconds 10 ;;
         bench5) step bench5 600 python bench.py --config 5 --steps 10 --warmup 2 --cpu-seconds 0 ;;
@@ -44,7 +44,8 @@ for s in "$@"; do
         dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 \
                    --dist-backend gloo ;;  # N>1 rehearsal: 2 ranks share the box's GPU
-        prof2) prof prof2 2 ;;
+        prof2) step prof2 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof2 -o run -- \
+                   python bench.py ;;  # the driver's default command, as is
         prof5) prof prof5 5 ;;
         prof3) prof prof3 3 ;;
         prof4) prof prof4 4 ;;
