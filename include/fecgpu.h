@@ -115,8 +115,8 @@ void    fecgpu_host_free(void *p);
  * mapped pinned host windows instead of D2H copies; bit 2: they also read the
  * windows over PCIe instead of H2D copies; default 6 = decode zero-copy),
  * "host_chunk_mb" (pipeline chunk, default 128); "bitslice" (1 default: GF
- * encode of a code with a compiled bit-sliced kernel — Cauchy rows, r = 8,
- * k in {16, 24, 32} — uses it; 0: the table multiply for every code);
+ * encode of a code with a compiled bit-sliced kernel — Cauchy or Vandermonde
+ * rows, r = 8, k in {16, 24, 32} — uses it; 0: the table multiply for every code);
  * "bs_passes" (bit-sliced encode on per-window lengths: 256-unit passes per
  * window group at the longest window, default 8). */
 ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value);

@@ -660,6 +660,7 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         // longest window (a lane's unit is k sources x 32 B of heavy XOR work,
         // so a partly idle last pass costs more than in the table kernels).
         p.bitslice = true;
+        p.matrix = (int)code->matrix;
 #if !FECGPU_BS_FLAT
         p.flat = false;
 #endif

@@ -65,6 +65,7 @@ struct LaunchPlan {
     bool remote;         // windows in mapped host memory: one window per workgroup and
                          // deep load batches (PCIe latency, small batches)
     bool bitslice;       // GF encode by the bit-sliced kernel (compile-time matrix)
+    int matrix;          // bitslice: the code's matrix (fecgpu_matrix)
 };
 
 // GF encode of (k, r, matrix) has a compiled bit-sliced kernel.

@@ -618,13 +618,15 @@ constexpr uint8_t gmul(uint8_t a, uint8_t b) {
 }
 
 // masks[j][i][p]: input planes of source j feeding output plane p of repair i
-template <int K, int R>
+// (M: the code's matrix, fecgpu_matrix)
+template <int K, int R, int M>
 struct Masks {
     uint8_t m[K][R][8];
     constexpr Masks() : m{} {
+        constexpr ParityRows<K, R, M> P{};
         for (int j = 0; j < K; j++)
             for (int i = 0; i < R; i++) {
-                const uint8_t c = kGf.exp[255 - kGf.log[(uint8_t)((K + i) ^ j)]];  // Cauchy (A.2)
+                const uint8_t c = P.p[i][j];
                 for (int q = 0; q < 8; q++) {
                     const uint8_t col = gmul(c, (uint8_t)(1u << q));
                     for (int p = 0; p < 8; p++)
@@ -667,8 +669,8 @@ __device__ __forceinline__ void tr8(uint32_t (&d)[8]) {
     }
 }
 
-template <int K, int R>
-inline constexpr Masks<K, R> kMasks{};
+template <int K, int R, int M>
+inline constexpr Masks<K, R, M> kMasks{};
 
 // a ^ b through the bitop3 intrinsic (S0 ^ S1 = 0xF0 ^ 0xCC): opaque to the
 // reassociation pass, which otherwise flattens every output plane into one
@@ -683,9 +685,9 @@ __device__ __forceinline__ uint32_t oxor(uint32_t a, uint32_t b) {
 }
 
 // output plane IP % 8 of repair IP / 8 takes source J's planes (compile time)
-template <int K, int R, int J, int IP>
+template <int K, int R, int M, int J, int IP>
 __device__ __forceinline__ void plane(uint32_t (&acc)[R][8], const uint32_t (&lo)[16], const uint32_t (&hi)[16]) {
-    constexpr int m = kMasks<K, R>.m[J][IP / 8][IP % 8], l = m & 15, h = m >> 4;
+    constexpr int m = kMasks<K, R, M>.m[J][IP / 8][IP % 8], l = m & 15, h = m >> 4;
     uint32_t &v = acc[IP / 8][IP % 8];
     if constexpr (J == 0) v = l && h ? oxor(lo[l], hi[h]) : (l ? lo[l] : hi[h]);
     else if constexpr (l && h) v = xor3(v, lo[l], hi[h]);
@@ -694,7 +696,7 @@ __device__ __forceinline__ void plane(uint32_t (&acc)[R][8], const uint32_t (&lo
 }
 
 // acc ^= source J's contribution to every repair, from its planes x
-template <int K, int R, int J, int... IP>
+template <int K, int R, int M, int J, int... IP>
 __device__ __forceinline__ void source(const uint32_t (&x)[8], uint32_t (&acc)[R][8],
                                        std::integer_sequence<int, IP...>) {
     uint32_t lo[16], hi[16];
@@ -705,7 +707,7 @@ __device__ __forceinline__ void source(const uint32_t (&x)[8], uint32_t (&acc)[R
         lo[s] = rest ? oxor(lo[rest], x[b]) : x[b];
         hi[s] = rest ? oxor(hi[rest], x[4 + b]) : x[4 + b];
     }
-    (plane<K, R, J, IP>(acc, lo, hi), ...);
+    (plane<K, R, M, J, IP>(acc, lo, hi), ...);
     // pin the accumulators here: otherwise IR sinking moves every repair's XOR
     // chain down to its store, past all later sources, and keeps their planes live
 #pragma unroll
@@ -724,20 +726,20 @@ __device__ __forceinline__ void load_src(const uint8_t *pa, const uint8_t *pb, u
 
 // one batch of sources J0 + T (pa / pb point at source J0): all loads first,
 // then transposes and XORs
-template <int K, int R, int J0, int... T>
+template <int K, int R, int M, int J0, int... T>
 __device__ __forceinline__ void batch(const uint8_t *pa, const uint8_t *pb, uint32_t stride,
                                       uint32_t (&acc)[R][8], std::integer_sequence<int, T...>) {
     uint32_t x[sizeof...(T)][8];
     (load_src<T>(pa, pb, stride, x[T]), ...);
-    ((tr8(x[T]), source<K, R, J0 + T>(x[T], acc, std::make_integer_sequence<int, R * 8>{}),
+    ((tr8(x[T]), source<K, R, M, J0 + T>(x[T], acc, std::make_integer_sequence<int, R * 8>{}),
       __builtin_amdgcn_sched_barrier(0)), ...);
 }
 
-template <int K, int R, int U, int J0>
+template <int K, int R, int M, int U, int J0>
 __device__ __forceinline__ void sources(const uint8_t *pa, const uint8_t *pb, uint32_t stride,
                                         uint32_t (&acc)[R][8]) {
     if constexpr (J0 < K) {
-        batch<K, R, J0>(pa, pb, stride, acc, std::make_integer_sequence<int, ((K - J0) < U ? (K - J0) : U)>{});
+        batch<K, R, M, J0>(pa, pb, stride, acc, std::make_integer_sequence<int, ((K - J0) < U ? (K - J0) : U)>{});
 #if FECGPU_BS_SYNC
         __syncthreads();  // keeps the workgroup's waves in one stretch of code
 #endif
@@ -745,7 +747,7 @@ __device__ __forceinline__ void sources(const uint8_t *pa, const uint8_t *pb, ui
         pa += U * stride;
         pb += U * stride;
         asm volatile("" : "+v"(pa), "+v"(pb));
-        sources<K, R, U, J0 + U>(pa, pb, stride, acc);
+        sources<K, R, M, U, J0 + U>(pa, pb, stride, acc);
     }
 }
 
@@ -800,10 +802,10 @@ __device__ __forceinline__ void unit_cols(uint8_t *base, uint32_t u, uint32_t h,
 
 // one unit: every source's planes into the R x 8 output planes (U sources
 // loaded per batch), then stores
-template <int K, int R, int U>
+template <int K, int R, int M, int U>
 __device__ __forceinline__ void unit(uint8_t *pa, uint8_t *pb, uint32_t stride, bool live, uint64_t od) {
     uint32_t acc[R][8];
-    sources<K, R, U, 0>(pa, pb, stride, acc);
+    sources<K, R, M, U, 0>(pa, pb, stride, acc);
 #pragma unroll
     for (int i = 0; i < R; i++) {
         tr8(acc[i]);
@@ -823,7 +825,7 @@ __device__ __forceinline__ void unit(uint8_t *pa, uint8_t *pb, uint32_t stride, 
 //          `wpb` windows at a time (prefix sums in LDS).
 // Trip counts are workgroup-uniform (lanes past the end redo the last unit
 // without storing), so the barriers inside a unit are safe.
-template <int K, int R, bool FLAT>
+template <int K, int R, int M, bool FLAT>
 __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
     if constexpr (FLAT) {
@@ -837,7 +839,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
             const uint32_t u = (uint32_t)(s - w * h);
             uint8_t *pa, *pb;
             bs::unit_cols(a.win + w * a.wpitch, u, h, ncol, pa, pb);
-            bs::unit<K, R, FECGPU_BS_U_FLAT>(pa, pb, a.stride, live, a.out_delta + w * a.out_wdelta);
+            bs::unit<K, R, M, FECGPU_BS_U_FLAT>(pa, pb, a.stride, live, a.out_delta + w * a.out_wdelta);
         }
         return;
     } else {
@@ -859,7 +861,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
                 uint8_t *pa, *pb;
                 bs::unit_cols(reinterpret_cast<uint8_t *>(g.base[wl]), s - g.pfx[wl], g.pfx[wl + 1] - g.pfx[wl],
                               g.ncol[wl], pa, pb);
-                bs::unit<K, R, FECGPU_BS_U>(pa, pb, g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
+                bs::unit<K, R, M, FECGPU_BS_U>(pa, pb, g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
             }
             __syncthreads();
         }
@@ -1464,7 +1466,7 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
         default: return hipErrorInvalidValue;   \
     }
 
-// Codes with a bit-sliced encode (Cauchy rows, compiled in).  r = 8 and
+// Codes with a bit-sliced encode (Cauchy and Vandermonde rows, compiled in).  r = 8 and
 // k >= 16 only: there the table multiply is VALU-bound and the bit-sliced
 // kernel 1.1-1.4x faster; at r <= 4 (and k = 8, r = 8) the table kernel is
 // memory-bound and, at higher occupancy, 8-12 % faster (profiles/r01_bs_r4_and_alternation.txt).
@@ -1473,7 +1475,7 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
 #endif
 
 bool bitslice_supported(int k, int r, int matrix) {
-    if (matrix != FECGPU_MATRIX_CAUCHY) return false;
+    if (matrix != FECGPU_MATRIX_CAUCHY && matrix != FECGPU_MATRIX_VANDERMONDE) return false;
 #define FECGPU_BS_HAS(K_, R_) if (k == K_ && r == R_) return true;
     FECGPU_BS_CODES(FECGPU_BS_HAS)
 #undef FECGPU_BS_HAS
@@ -1483,13 +1485,17 @@ bool bitslice_supported(int k, int r, int matrix) {
 hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     if (p.bitslice) {
-#define FECGPU_BS_LAUNCH(K_, R_)                                                                  \
-        if (a.k == K_ && a.r == R_)                                                               \
-            return p.flat ? launch(gf_encode_bs_kernel<K_, R_, true>, a, p, s, false,             \
+#define FECGPU_BS_LAUNCH_M(K_, R_, M_)                                                            \
+        if (a.k == K_ && a.r == R_ && p.matrix == M_)                                             \
+            return p.flat ? launch(gf_encode_bs_kernel<K_, R_, M_, true>, a, p, s, false,         \
                                    (a.nwin * ((a.ncol + 1) / 2) + kBlock - 1) / kBlock)             \
-                          : launch(gf_encode_bs_kernel<K_, R_, false>, a, p, s, false);
+                          : launch(gf_encode_bs_kernel<K_, R_, M_, false>, a, p, s, false);
+#define FECGPU_BS_LAUNCH(K_, R_)                                 \
+        FECGPU_BS_LAUNCH_M(K_, R_, FECGPU_MATRIX_CAUCHY)         \
+        FECGPU_BS_LAUNCH_M(K_, R_, FECGPU_MATRIX_VANDERMONDE)
         FECGPU_BS_CODES(FECGPU_BS_LAUNCH)
 #undef FECGPU_BS_LAUNCH
+#undef FECGPU_BS_LAUNCH_M
         return hipErrorInvalidValue;
     }
     const bool flat = p.flat;

@@ -37,6 +37,55 @@ constexpr GfTables make_gf_tables() {
     return t;
 }
 
+// ---------------------------------------------------------------- A.2 ----
+// Parity rows P[i][j] (i < R, j < K) of the systematic generator, computed at
+// compile time for the bit-sliced kernels (same construction as the host's
+// host_parity_rows): matrix 0 = Cauchy inv((K+i) ^ j); matrix 1 = systematic
+// Vandermonde, rows K.. of V * inv(V[0..K)) with V[i][j] = i^j.
+template <int K, int R, int M>
+struct ParityRows {
+    uint8_t p[R][K];
+    static constexpr uint8_t mul(const GfTables &t, uint8_t a, uint8_t b) {
+        return (a && b) ? t.exp[t.log[a] + t.log[b]] : 0;
+    }
+    static constexpr uint8_t pw(const GfTables &t, uint8_t a, int n) {
+        return n == 0 ? 1 : a == 0 ? 0 : t.exp[(t.log[a] * n) % 255];
+    }
+    constexpr ParityRows() : p{} {
+        const GfTables t = make_gf_tables();
+        if (M == 0) {
+            for (int i = 0; i < R; i++)
+                for (int j = 0; j < K; j++) p[i][j] = t.exp[255 - t.log[(uint8_t)((K + i) ^ j)]];
+            return;
+        }
+        uint8_t a[K][2 * K] = {};  // [V_top | I] -> [I | inv(V_top)]
+        for (int i = 0; i < K; i++)
+            for (int j = 0; j < 2 * K; j++) a[i][j] = j < K ? pw(t, (uint8_t)i, j) : (uint8_t)(j - K == i);
+        for (int c = 0; c < K; c++) {
+            int piv = c;
+            while (!a[piv][c]) piv++;
+            for (int j = 0; j < 2 * K; j++) {
+                const uint8_t x = a[piv][j];
+                a[piv][j] = a[c][j];
+                a[c][j] = x;
+            }
+            const uint8_t iv = t.exp[255 - t.log[a[c][c]]];
+            for (int j = 0; j < 2 * K; j++) a[c][j] = mul(t, a[c][j], iv);
+            for (int i = 0; i < K; i++) {
+                const uint8_t f = a[i][c];
+                if (i == c || !f) continue;
+                for (int j = 0; j < 2 * K; j++) a[i][j] ^= mul(t, f, a[c][j]);
+            }
+        }
+        for (int i = 0; i < R; i++)
+            for (int j = 0; j < K; j++) {
+                uint8_t v = 0;
+                for (int q = 0; q < K; q++) v ^= mul(t, pw(t, (uint8_t)(K + i), q), a[q][K + j]);
+                p[i][j] = v;
+            }
+    }
+};
+
 // multiply by x (=2) in GF(2^8)/0x11D, one byte in the low 8 bits
 FEC_HD uint32_t gf_xtime(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x1Du : 0u)) & 0xFFu; }
 

@@ -511,20 +511,21 @@ def ctx_tables():
     c.close()
 
 
+@pytest.mark.parametrize("matrix", ["cauchy", "vandermonde"])
 @pytest.mark.parametrize("k,r", BS_CODES)
 @pytest.mark.parametrize("wl,L,nwin", [(0, 1200, 70), (1, 0, 9), (0, 16, 33), (0, 1, 5), (0, 9000, 6)])
-def test_bitslice_encode_vs_oracle(ctx, ctx_tables, k, r, wl, L, nwin):
-    """The bit-sliced GF encode (compile-time Cauchy rows, DESIGN.md §GF bit-slicing)
-    emits the oracle's repairs for every compiled code: odd column counts (1200 B:
-    75 columns, the last unit without a second column), one column (16 B), S = 1,
-    per-window lengths (mixed MTU, LENPREFIX) and 9000-B symbols; and the same
-    bytes as the table-multiply kernel."""
+def test_bitslice_encode_vs_oracle(ctx, ctx_tables, k, r, wl, L, nwin, matrix):
+    """The bit-sliced GF encode (compile-time parity rows, Cauchy or systematic
+    Vandermonde, DESIGN.md §GF bit-slicing) emits the oracle's repairs for every
+    compiled code: odd column counts (1200 B: 75 columns, the last unit without a
+    second column), one column (16 B), S = 1, per-window lengths (mixed MTU,
+    LENPREFIX) and 9000-B symbols; and the same bytes as the table-multiply kernel."""
     S = O.sym_lens(wl, SEED + k, 0, nwin, k, L)
     stride = O.round_up(int(S.max()), 16) + (16 if wl == 0 else 0)
     wins = O.make_windows(wl, SEED + k, 0, nwin, k, r, L, stride)
     oe = wins.copy()
-    O.encode_batch(O.GF256, k, r, S, oe, 4)
-    code = fecgpu.Code("gf256", k, r)
+    O.encode_batch(O.GF256 if matrix == "cauchy" else O.GF256_VDM, k, r, S, oe, 4)
+    code = fecgpu.Code("gf256", k, r, matrix=matrix)
     outs = []
     for c in (ctx, ctx_tables):
         d = torch.from_numpy(wins.copy()).cuda()
