@@ -430,6 +430,41 @@ def test_zero_windows_and_errors(ctx):
     assert e.value.code == fecgpu.ERR_UNSUPPORTED
 
 
+@pytest.mark.parametrize("scheme,k,r,L", [("xor", 8, 2, 1200), ("gf256", 16, 4, 1200),
+                                          ("gf256", 32, 8, 1200), ("gf256", 32, 8, 9000),
+                                          ("xor", 1, 1, 16), ("gf256", 64 - 8, 8, 33)])
+@pytest.mark.parametrize("uniform", [True, False])
+def test_single_window(ctx, scheme, k, r, L, uniform):
+    """One window: the tiny-grid paths (fewer work units than XCD regions) of the
+    flat, group and bit-sliced kernels, encode and decode vs the oracle."""
+    S = np.full(1, L, np.uint32)
+    stride = O.round_up(L, 16)
+    wins = O.make_windows(0, SEED + 3, 0, 1, k, r, L, stride)
+    present = O.presents(1, SEED + 3, 0, 1, _scheme(scheme), k, r)
+    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, present, uniform)
+    oe, od, os_ = oracle_run(scheme, k, r, wins, S, present)
+    _cmp_emitted(ge, oe, S, "encode")
+    assert np.array_equal(gs, os_)
+    _cmp_emitted(gd, od, S, "decode")
+
+
+@pytest.mark.parametrize("scheme,k,r", [("xor", 4, 2), ("gf256", 4, 2), ("gf256", 16, 8)])
+def test_megabyte_symbols(ctx, scheme, k, r):
+    """Symbols far above any MTU (1 MiB + 5 B, 3 windows): 64-bit window offsets,
+    long column loops, the last partial 16-B column."""
+    L = (1 << 20) + 5
+    stride = O.round_up(L, 16)
+    nwin = 3
+    S = np.full(nwin, L, np.uint32)
+    wins = O.make_windows(0, SEED + 5, 0, nwin, k, r, L, stride)
+    present = O.presents(1, SEED + 5, 0, nwin, _scheme(scheme), k, r)
+    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, present, True)
+    oe, od, os_ = oracle_run(scheme, k, r, wins, S, present)
+    _cmp_emitted(ge, oe, S, "encode")
+    assert np.array_equal(gs, os_)
+    _cmp_emitted(gd, od, S, "decode")
+
+
 # ------------------------------------------------ workload generators ---
 @pytest.mark.parametrize("cfgid", [2, 3, 4])
 def test_synth_erasure_digest_vs_oracle(ctx, cfgid):
