@@ -465,6 +465,42 @@ def test_megabyte_symbols(ctx, scheme, k, r):
     _cmp_emitted(gd, od, S, "decode")
 
 
+def _random_cases(n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        scheme = ["xor", "gf256", "gf256"][int(rng.integers(0, 3))]
+        k = int(rng.integers(1, 57))
+        r = int(rng.integers(1, min(8, 64 - k, k if scheme == "xor" else 8) + 1))
+        matrix = "vandermonde" if scheme == "gf256" and rng.random() < 0.3 else "cauchy"
+        out.append((scheme, matrix, k, r, int(rng.integers(1, 3001)), int(rng.integers(1, 41)),
+                    bool(rng.random() < 0.5), int(rng.integers(1, 3))))
+    return out
+
+
+@pytest.mark.parametrize("scheme,matrix,k,r,L,nwin,uniform,era", _random_cases(40, 2026))
+def test_random_shapes_vs_oracle(ctx, scheme, matrix, k, r, L, nwin, uniform, era):
+    """Seeded random codes and shapes (k 1..56, r 1..8, S 1..3000, 1..40 windows, both
+    matrices, uniform or per-window S, exact-r or i.i.d. erasures) vs the oracle."""
+    sid = _scheme(scheme) if matrix == "cauchy" else O.GF256_VDM
+    rng = np.random.default_rng(k * 1000 + L)
+    S = np.full(nwin, L, np.uint32) if uniform else rng.integers(1, L + 1, nwin).astype(np.uint32)
+    stride = O.round_up(int(S.max()), 16)
+    wins = np.zeros((nwin, k + r, stride), np.uint8)
+    for w in range(nwin):
+        wins[w, :k, :S[w]] = rng.integers(0, 256, (k, int(S[w])), dtype=np.uint8)
+    present = O.presents(era, SEED + k, 0, nwin, sid, k, r)
+    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, present, uniform, matrix=matrix)
+    oe = wins.copy()
+    O.encode_batch(sid, k, r, S, oe, 4)
+    od = oe.copy()
+    O.erase(od, present, k, r, fill=0xAB)
+    os_ = O.decode_batch(sid, k, r, S, od, present, 4)
+    _cmp_emitted(ge, oe, S, "encode")
+    assert np.array_equal(gs, os_)
+    _cmp_emitted(gd, od, S, "decode")
+
+
 # ------------------------------------------------ workload generators ---
 @pytest.mark.parametrize("cfgid", [2, 3, 4])
 def test_synth_erasure_digest_vs_oracle(ctx, cfgid):
