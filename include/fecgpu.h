@@ -118,7 +118,9 @@ void    fecgpu_host_free(void *p);
  * encode of a code with a compiled bit-sliced kernel — Cauchy or Vandermonde
  * rows, r = 8, k in {16, 24, 32} — uses it; 0: the table multiply for every code);
  * "bs_passes" (bit-sliced encode on per-window lengths: 256-unit passes per
- * window group at the longest window, default 8). */
+ * window group at the longest window, default 8); "conn_streams" (streams per
+ * device shared round robin by the encoders / decoders created afterwards,
+ * default 4, 1..64). */
 ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value);
 
 /* ---- batch entry points (hot path) ---------------------------------- */
@@ -159,7 +161,9 @@ ssize_t fecgpu_decode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *w
  * and launches their encode asynchronously while it fills the next ones; the
  * receiver files symbols into a pool of window slots and a flush decodes every
  * decodable window in one zero-copy launch (ragged layout, fixed pitch).
- * Caller buffers are plain host memory. */
+ * Caller buffers are plain host memory.  Objects launch on a small pool of
+ * streams owned by their ctx (not one stream per connection), so they must be
+ * freed before the ctx, and used from the ctx's thread. */
 typedef struct fecgpu_encoder fecgpu_encoder;
 typedef struct fecgpu_decoder fecgpu_decoder;
 

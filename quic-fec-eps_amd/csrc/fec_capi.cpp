@@ -140,6 +140,12 @@ struct fecgpu_ctx {
     int host_chunk_mb = 128;
     // GF encode by the bit-sliced kernel where the code has one (DESIGN.md §GF bit-slicing)
     int bitslice = 1;
+    // per-connection encoders / decoders launch on a small pool of streams per
+    // device owned by the ctx (round robin), not one stream per object: a
+    // server holds thousands of connections, the GPU has few hardware queues
+    int conn_nstreams = 4;
+    uint32_t conn_rr = 0;
+    std::map<int, std::vector<hipStream_t>> conn_streams;
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
     // FECGPU_CHECK builds: bytes taken off the end of every checked range, so a
@@ -242,6 +248,11 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         ctx->bs_passes = (int)value;
         return 0;
     }
+    if (!std::strcmp(key, "conn_streams")) {
+        if (value < 1 || value > 64) return FECGPU_ERR_INVALID_ARG;
+        ctx->conn_nstreams = (int)value;  // objects created from now on
+        return 0;
+    }
     if (!std::strcmp(key, "bitslice")) {
         if (value < 0 || value > 1) return FECGPU_ERR_INVALID_ARG;
         ctx->bitslice = (int)value;
@@ -268,6 +279,13 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
     for (auto &kv : ctx->stage) {
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second.first);
+    }
+    for (auto &kv : ctx->conn_streams) {
+        (void)hipSetDevice(kv.first);
+        for (hipStream_t st : kv.second) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
     }
     for (auto &kv : ctx->pipes) {
         HostPipe &hp = kv.second;
@@ -838,6 +856,26 @@ ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Batc
     rc = launch_device(ctx, code, decode, a, s, remote);
     if (prev != ctx->devs[0]) (void)hipSetDevice(prev);
     return rc;
+}
+
+}  // namespace fecgpu
+
+namespace fecgpu {
+
+// A stream of the ctx's per-connection pool on the current device (created on
+// first use, round robin; freed with the ctx).
+ssize_t ctx_conn_stream(fecgpu_ctx *ctx, int dev, hipStream_t *out) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::vector<hipStream_t> &v = ctx->conn_streams[dev];
+    if ((int)v.size() < ctx->conn_nstreams) {
+        hipStream_t st = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+        v.push_back(st);
+        *out = st;
+        return 0;
+    }
+    *out = v[ctx->conn_rr++ % v.size()];
+    return 0;
 }
 
 }  // namespace fecgpu

@@ -112,7 +112,8 @@ struct fecgpu_encoder {
     uint32_t max_len = 0, batch = 0, stride = 0;
     size_t wbytes = 0;
     int dev = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // of the ctx's pool
+    hipEvent_t last_done = nullptr; // recorded after the latest launched batch
     uint64_t next_win = 0;
     int open_n = 0;           // sources in the open window
     uint32_t open_max = 0;
@@ -176,6 +177,7 @@ ssize_t enc_launch(fecgpu_encoder *e) {
     if (rc) return rc;
     DevGuard g(e->dev);
     if (hipEventRecord(b->done, e->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
+    e->last_done = b->done;
     b->launched = true;
     e->cur = nullptr;
     if (b->live == 0) {  // every window already released (never read): recycle
@@ -247,9 +249,10 @@ ssize_t fecgpu_encoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t ma
     e->stride = rup16(max_len + (is_lenprefix(*code) ? 2 : 0));
     e->wbytes = (size_t)(code->k + code->r) * e->stride;
     e->dev = ctx_device();
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    rc = fecgpu::ctx_conn_stream(ctx, e->dev, &e->stream);  // shared, owned by the ctx
+    if (rc) {
         delete e;
-        return FECGPU_ERR_DEVICE;
+        return rc;
     }
     *out = e;
     return 0;
@@ -258,13 +261,12 @@ ssize_t fecgpu_encoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t ma
 void fecgpu_encoder_free(fecgpu_encoder *e) {
     if (!e) return;
     DevGuard g(e->dev);
-    (void)hipStreamSynchronize(e->stream);
+    if (e->last_done) (void)hipEventSynchronize(e->last_done);  // its launches, in stream order
     for (EncBatch *b : e->all) {
         if (b->done) (void)hipEventDestroy(b->done);
         pinned_free(b->mem);
         delete b;
     }
-    (void)hipStreamDestroy(e->stream);
     delete e;
 }
 
@@ -314,7 +316,9 @@ ssize_t fecgpu_encoder_flush(fecgpu_encoder *e) {
     ssize_t n = enc_launch(e);
     if (n < 0) return n;
     DevGuard g(e->dev);
-    if (hipStreamSynchronize(e->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
+    // the stream is shared with other connections: wait for this encoder's
+    // last launch only (its earlier ones precede it on the same stream)
+    if (e->last_done && hipEventSynchronize(e->last_done) != hipSuccess) return FECGPU_ERR_DEVICE;
     return n;
 }
 
@@ -495,12 +499,12 @@ ssize_t fecgpu_decoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t ma
     d->stride = rup16(max_len + (is_lenprefix(*code) ? 2 : 0));
     d->wbytes = (size_t)(code->k + code->r) * d->stride;
     d->dev = ctx_device();
-    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+    rc = fecgpu::ctx_conn_stream(ctx, d->dev, &d->stream);  // shared, owned by the ctx
+    if (rc) {
         delete d;
-        return FECGPU_ERR_DEVICE;
+        return rc;
     }
     if (hipEventCreateWithFlags(&d->done, hipEventDisableTiming) != hipSuccess) {
-        (void)hipStreamDestroy(d->stream);
         delete d;
         return FECGPU_ERR_DEVICE;
     }
@@ -511,11 +515,10 @@ ssize_t fecgpu_decoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t ma
 void fecgpu_decoder_free(fecgpu_decoder *d) {
     if (!d) return;
     DevGuard g(d->dev);
-    (void)hipStreamSynchronize(d->stream);
+    if (d->pending) (void)hipEventSynchronize(d->done);  // its launch (the stream is shared)
     for (Pinned &p : d->chunks) pinned_free(p);
     pinned_free(d->arg);
     (void)hipEventDestroy(d->done);
-    (void)hipStreamDestroy(d->stream);
     delete d;
 }
 

@@ -91,6 +91,9 @@ hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
 // Release builds: always {0, 0}.
 hipError_t take_bounds_faults(uint64_t *count, uint64_t *first);
 
+// Per-connection objects launch on a stream of the ctx's pool (fec_capi.cpp).
+ssize_t ctx_conn_stream(fecgpu_ctx *ctx, int dev, hipStream_t *out);
+
 struct SynthArgs {
     uint8_t *win;
     uint32_t *sym_len;

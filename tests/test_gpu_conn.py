@@ -220,6 +220,34 @@ def test_native_drivers_under_asan(args):
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
 
 
+@pytest.mark.parametrize("nstreams", [4, 1])
+def test_many_connections_share_streams(nstreams):
+    """A server's worth of connections on one ctx: 400 encoder / decoder pairs (800
+    objects) launch on the ctx's pool of `nstreams` streams, interleaved window by
+    window; every lost packet comes back from its own connection's decoder."""
+    c = fecgpu.Context()
+    c.set_tuning("conn_streams", nstreams)
+    code = fecgpu.Code("gf256", 4, 2)
+    n = 400
+    encs = [fecgpu.Encoder(c, code, max_len=64, batch=1) for _ in range(n)]
+    decs = [fecgpu.Decoder(c, code, max_len=64, batch=1) for _ in range(n)]
+    pk = [[bytes([(i * 7 + j * 13 + t) & 0xFF for t in range(64)]) for j in range(4)] for i in range(n)]
+    ids = [[encs[i].add_source(p) for p in pk[i]] for i in range(n)]  # batch=1: launches per window
+    for i in range(n):
+        w = ids[i][0][0]
+        for j in (0, 3):  # sources 1 and 2 lost
+            assert decs[i].add_source(w, j, pk[i][j]) == 0
+        for t in range(2):
+            assert decs[i].add_repair(w, t, encs[i].repair(w, t)) == 0
+    for i in range(n):
+        decs[i].flush()
+        w = ids[i][0][0]
+        assert decs[i].recovered(w, 1) == pk[i][1] and decs[i].recovered(w, 2) == pk[i][2], i
+    for o in encs + decs:
+        o.close()
+    c.close()
+
+
 def test_policy_timeouts(ctx):
     """Scheduling policy: on the caller's clock, a window closes
     window_timeout_us after its first packet and a partly filled batch launches
