@@ -390,7 +390,9 @@ struct DecSlot {
     bool inflight = false; // in the launched, not yet completed decode
 };
 
-constexpr uint32_t kSlotsPerChunk = 256;
+// window slots per pinned chunk of the decoder's pool: 4 batches, 16..256
+// (a low-rate connection with small batches keeps a small footprint)
+uint32_t dec_chunk_slots(uint32_t batch) { return std::min<uint32_t>(256, std::max<uint32_t>(16, 4 * batch)); }
 
 }  // namespace
 
@@ -401,7 +403,8 @@ struct fecgpu_decoder {
     size_t wbytes = 0;
     int dev = 0;
     hipStream_t stream = nullptr;
-    std::vector<Pinned> chunks;        // kSlotsPerChunk windows each
+    uint32_t chunk_slots = 256;        // windows per pinned chunk (dec_chunk_slots)
+    std::vector<Pinned> chunks;        // chunk_slots windows each
     std::vector<DecSlot> slots;
     std::vector<uint32_t> plen;        // [slot * k + j] payload length
     std::vector<uint32_t> free_slots;
@@ -421,12 +424,12 @@ struct fecgpu_decoder {
 namespace {
 
 uint8_t *dec_row(fecgpu_decoder *d, uint32_t s, int row) {
-    return d->chunks[s / kSlotsPerChunk].host + (size_t)(s % kSlotsPerChunk) * d->wbytes +
+    return d->chunks[s / d->chunk_slots].host + (size_t)(s % d->chunk_slots) * d->wbytes +
            (size_t)row * d->stride;
 }
 uint64_t dec_dev_addr(fecgpu_decoder *d, uint32_t s) {
-    return reinterpret_cast<uint64_t>(d->chunks[s / kSlotsPerChunk].dev) +
-           (uint64_t)(s % kSlotsPerChunk) * d->wbytes;
+    return reinterpret_cast<uint64_t>(d->chunks[s / d->chunk_slots].dev) +
+           (uint64_t)(s % d->chunk_slots) * d->wbytes;
 }
 
 ssize_t dec_slot(fecgpu_decoder *d, uint64_t win, uint32_t &out) {
@@ -437,13 +440,13 @@ ssize_t dec_slot(fecgpu_decoder *d, uint64_t win, uint32_t &out) {
     }
     if (d->free_slots.empty()) {
         Pinned p;
-        ssize_t rc = pinned_alloc((size_t)kSlotsPerChunk * d->wbytes, p);
+        ssize_t rc = pinned_alloc((size_t)d->chunk_slots * d->wbytes, p);
         if (rc) return rc;
         const uint32_t base = (uint32_t)d->slots.size();
         d->chunks.push_back(p);
-        d->slots.resize(base + kSlotsPerChunk);
-        d->plen.resize((size_t)(base + kSlotsPerChunk) * d->code.k, 0);
-        for (uint32_t i = kSlotsPerChunk; i-- > 0;) d->free_slots.push_back(base + i);
+        d->slots.resize(base + d->chunk_slots);
+        d->plen.resize((size_t)(base + d->chunk_slots) * d->code.k, 0);
+        for (uint32_t i = d->chunk_slots; i-- > 0;) d->free_slots.push_back(base + i);
     }
     const uint32_t s = d->free_slots.back();
     d->free_slots.pop_back();
@@ -498,6 +501,7 @@ ssize_t fecgpu_decoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t ma
     d->batch = batch;
     d->stride = rup16(max_len + (is_lenprefix(*code) ? 2 : 0));
     d->wbytes = (size_t)(code->k + code->r) * d->stride;
+    d->chunk_slots = dec_chunk_slots(batch);
     d->dev = ctx_device();
     rc = fecgpu::ctx_conn_stream(ctx, d->dev, &d->stream);  // shared, owned by the ctx
     if (rc) {
