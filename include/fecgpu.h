@@ -120,7 +120,8 @@ void    fecgpu_host_free(void *p);
  * "bs_passes" (bit-sliced encode on per-window lengths: 256-unit passes per
  * window group at the longest window, default 8); "conn_streams" (streams per
  * device shared round robin by the encoders / decoders created afterwards,
- * default 4, 1..64). */
+ * default 4, 1..64); "pinned_cache_mb" (pinned blocks that freed encoders /
+ * decoders leave cached in the ctx for the next ones, default 1024). */
 ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value);
 
 /* ---- batch entry points (hot path) ---------------------------------- */

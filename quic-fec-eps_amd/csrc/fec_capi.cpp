@@ -146,6 +146,10 @@ struct fecgpu_ctx {
     int conn_nstreams = 4;
     uint32_t conn_rr = 0;
     std::map<int, std::vector<hipStream_t>> conn_streams;
+    // pinned blocks freed by per-connection objects, by size, for the next ones
+    std::multimap<size_t, void *> pinned_cache;
+    size_t pinned_cached = 0;
+    size_t pinned_cache_cap = (size_t)1 << 30;
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
     // FECGPU_CHECK builds: bytes taken off the end of every checked range, so a
@@ -248,6 +252,18 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         ctx->bs_passes = (int)value;
         return 0;
     }
+    if (!std::strcmp(key, "pinned_cache_mb")) {
+        if (value < 0 || value > (1 << 20)) return FECGPU_ERR_INVALID_ARG;
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ctx->pinned_cache_cap = (size_t)value << 20;
+        while (ctx->pinned_cached > ctx->pinned_cache_cap) {  // shrink now
+            auto it = ctx->pinned_cache.begin();
+            ctx->pinned_cached -= it->first;
+            (void)hipHostFree(it->second);
+            ctx->pinned_cache.erase(it);
+        }
+        return 0;
+    }
     if (!std::strcmp(key, "conn_streams")) {
         if (value < 1 || value > 64) return FECGPU_ERR_INVALID_ARG;
         ctx->conn_nstreams = (int)value;  // objects created from now on
@@ -280,6 +296,7 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second.first);
     }
+    for (auto &kv : ctx->pinned_cache) (void)hipHostFree(kv.second);
     for (auto &kv : ctx->conn_streams) {
         (void)hipSetDevice(kv.first);
         for (hipStream_t st : kv.second) {
@@ -876,6 +893,32 @@ ssize_t ctx_conn_stream(fecgpu_ctx *ctx, int dev, hipStream_t *out) {
     }
     *out = v[ctx->conn_rr++ % v.size()];
     return 0;
+}
+
+
+ssize_t ctx_pinned_get(fecgpu_ctx *ctx, size_t bytes, void **host) {
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        auto it = ctx->pinned_cache.find(bytes);
+        if (it != ctx->pinned_cache.end()) {
+            *host = it->second;
+            ctx->pinned_cached -= bytes;
+            ctx->pinned_cache.erase(it);
+            return 0;
+        }
+    }
+    HIP_TRY(hipHostMalloc(host, bytes, hipHostMallocDefault), "hipHostMalloc");
+    return 0;
+}
+
+void ctx_pinned_put(fecgpu_ctx *ctx, void *host, size_t bytes) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->pinned_cached + bytes <= ctx->pinned_cache_cap) {
+        ctx->pinned_cache.emplace(bytes, host);
+        ctx->pinned_cached += bytes;
+        return;
+    }
+    (void)hipHostFree(host);
 }
 
 }  // namespace fecgpu

@@ -54,11 +54,14 @@ struct Pinned {
     size_t bytes = 0;
 };
 
-ssize_t pinned_alloc(size_t bytes, Pinned &p) {
+// Pinned blocks come from the ctx's cache of blocks freed by earlier objects
+// (connection churn would otherwise pin and unpin pages per connection).
+ssize_t pinned_alloc(fecgpu_ctx *ctx, size_t bytes, Pinned &p) {
     void *h = nullptr, *d = nullptr;
-    if (hipHostMalloc(&h, bytes, hipHostMallocDefault) != hipSuccess) return FECGPU_ERR_DEVICE;
+    ssize_t rc = fecgpu::ctx_pinned_get(ctx, bytes, &h);
+    if (rc) return rc;
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
-        (void)hipHostFree(h);
+        fecgpu::ctx_pinned_put(ctx, h, bytes);
         return FECGPU_ERR_DEVICE;
     }
     p.host = static_cast<uint8_t *>(h);
@@ -67,8 +70,8 @@ ssize_t pinned_alloc(size_t bytes, Pinned &p) {
     return 0;
 }
 
-void pinned_free(Pinned &p) {
-    if (p.host) (void)hipHostFree(p.host);
+void pinned_free(fecgpu_ctx *ctx, Pinned &p) {
+    if (p.host) fecgpu::ctx_pinned_put(ctx, p.host, p.bytes);
     p = Pinned{};
 }
 
@@ -139,7 +142,7 @@ ssize_t enc_take_batch(fecgpu_encoder *e) {
     } else {
         b = new EncBatch();
         const size_t wb = (size_t)e->batch * e->wbytes;
-        ssize_t rc = pinned_alloc(wb + (size_t)e->batch * 4, b->mem);
+        ssize_t rc = pinned_alloc(e->ctx, wb + (size_t)e->batch * 4, b->mem);
         if (rc) {
             delete b;
             return rc;
@@ -147,7 +150,7 @@ ssize_t enc_take_batch(fecgpu_encoder *e) {
         b->S = reinterpret_cast<uint32_t *>(b->mem.host + wb);
         b->S_dev = reinterpret_cast<uint32_t *>(b->mem.dev + wb);
         if (hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess) {
-            pinned_free(b->mem);
+            pinned_free(e->ctx, b->mem);
             delete b;
             return FECGPU_ERR_DEVICE;
         }
@@ -264,7 +267,7 @@ void fecgpu_encoder_free(fecgpu_encoder *e) {
     if (e->last_done) (void)hipEventSynchronize(e->last_done);  // its launches, in stream order
     for (EncBatch *b : e->all) {
         if (b->done) (void)hipEventDestroy(b->done);
-        pinned_free(b->mem);
+        pinned_free(e->ctx, b->mem);
         delete b;
     }
     delete e;
@@ -440,7 +443,7 @@ ssize_t dec_slot(fecgpu_decoder *d, uint64_t win, uint32_t &out) {
     }
     if (d->free_slots.empty()) {
         Pinned p;
-        ssize_t rc = pinned_alloc((size_t)d->chunk_slots * d->wbytes, p);
+        ssize_t rc = pinned_alloc(d->ctx, (size_t)d->chunk_slots * d->wbytes, p);
         if (rc) return rc;
         const uint32_t base = (uint32_t)d->slots.size();
         d->chunks.push_back(p);
@@ -520,8 +523,8 @@ void fecgpu_decoder_free(fecgpu_decoder *d) {
     if (!d) return;
     DevGuard g(d->dev);
     if (d->pending) (void)hipEventSynchronize(d->done);  // its launch (the stream is shared)
-    for (Pinned &p : d->chunks) pinned_free(p);
-    pinned_free(d->arg);
+    for (Pinned &p : d->chunks) pinned_free(d->ctx, p);
+    pinned_free(d->ctx, d->arg);
     (void)hipEventDestroy(d->done);
     delete d;
 }
@@ -615,9 +618,9 @@ ssize_t dec_launch(fecgpu_decoder *d, uint32_t keep) {
     const size_t o_len = (n * 8 + 255) & ~size_t(255), o_pres = o_len + ((n * 4 + 255) & ~size_t(255));
     const size_t need = o_pres + n * 8;
     if (d->arg_cap / 2 < std::max(need, n)) {
-        pinned_free(d->arg);
+        pinned_free(d->ctx, d->arg);
         d->arg_cap = 0;
-        ssize_t rc = pinned_alloc(std::max(need, (size_t)64 << 10) * 2, d->arg);
+        ssize_t rc = pinned_alloc(d->ctx, std::max(need, (size_t)64 << 10) * 2, d->arg);
         if (rc) {
             for (uint32_t s : sel) d->slots[s].inflight = false;
             sel.clear();

@@ -94,6 +94,12 @@ hipError_t take_bounds_faults(uint64_t *count, uint64_t *first);
 // Per-connection objects launch on a stream of the ctx's pool (fec_capi.cpp).
 ssize_t ctx_conn_stream(fecgpu_ctx *ctx, int dev, hipStream_t *out);
 
+// Pinned host blocks for per-connection objects: a block of exactly `bytes`
+// from the ctx's cache of freed blocks, else a new hipHostMalloc; put returns
+// it to the cache (up to "pinned_cache_mb"), else frees it.
+ssize_t ctx_pinned_get(fecgpu_ctx *ctx, size_t bytes, void **host);
+void ctx_pinned_put(fecgpu_ctx *ctx, void *host, size_t bytes);
+
 struct SynthArgs {
     uint8_t *win;
     uint32_t *sym_len;

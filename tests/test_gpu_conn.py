@@ -248,6 +248,38 @@ def test_many_connections_share_streams(nstreams):
     c.close()
 
 
+def test_connection_churn_reuses_pinned_blocks():
+    """300 short-lived connections one after another (open, one window each way,
+    close): every lost packet is recovered, and with the ctx's pinned-block cache the
+    churn costs less than pinning and unpinning fresh memory per connection."""
+    import time
+    code = fecgpu.Code("gf256", 16, 4)
+    pk = [bytes([(j * 31 + t) & 0xFF for t in range(1200)]) for j in range(16)]
+    times = {}
+    for cache_mb in (1024, 0):
+        c = fecgpu.Context()
+        c.set_tuning("pinned_cache_mb", cache_mb)
+        t0 = time.perf_counter()
+        for i in range(300):
+            enc = fecgpu.Encoder(c, code, max_len=1200, batch=8)
+            dec = fecgpu.Decoder(c, code, max_len=1200, batch=8)
+            ids = [enc.add_source(p) for p in pk]
+            enc.flush()
+            w = ids[0][0]
+            for j in range(4, 16):
+                assert dec.add_source(w, j, pk[j]) == 0
+            for t in range(4):
+                assert dec.add_repair(w, t, enc.repair(w, t)) == 0
+            dec.flush()
+            assert all(dec.recovered(w, j) == pk[j] for j in range(4)), i
+            enc.close()
+            dec.close()
+        times[cache_mb] = time.perf_counter() - t0
+        c.close()
+    print(f"300 connections: {times[1024]:.3f} s with the pinned cache, {times[0]:.3f} s without")
+    assert times[1024] < times[0] * 1.1
+
+
 def test_policy_timeouts(ctx):
     """Scheduling policy: on the caller's clock, a window closes
     window_timeout_us after its first packet and a partly filled batch launches
