@@ -202,6 +202,11 @@ ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *dec, uint64_t win, uint16_t id
  * it; returns the number of source packets recovered (including those of an
  * automatic flush completed here). */
 ssize_t fecgpu_decoder_flush(fecgpu_decoder *dec);
+/* fecgpu_decoder_flush for n decoders in ONE launch, waiting for it: a server
+ * that flushes many connections at once pays one kernel, not n.  The decoders
+ * must share ctx, code and max_len (INVALID_ARG otherwise, or if one is listed
+ * twice).  Returns the number of source packets recovered over all of them. */
+ssize_t fecgpu_decoder_flush_many(fecgpu_decoder *const *decs, size_t n);
 /* Copy source packet idx of window win (received or recovered, de-framed);
  * returns its length, FECGPU_ERR_DONE if it is not available. */
 ssize_t fecgpu_decoder_recovered(fecgpu_decoder *dec, uint64_t win, uint16_t idx, uint8_t *out,

@@ -533,24 +533,18 @@ void fecgpu_decoder_free(fecgpu_decoder *d) {
 
 namespace {
 
-// Completes the pending decode: waits for it and marks what it recovered.
-// Returns the number of recovered sources (0 if nothing was pending).
-ssize_t dec_complete(fecgpu_decoder *d) {
-    if (!d->pending) return 0;
-    d->pending = false;
+// Marks what a decode recovered in the windows of d->sel, whose status bytes
+// are status[0 .. |sel|) (ok: the launch completed).  Returns the number of
+// recovered sources.
+ssize_t dec_apply(fecgpu_decoder *d, const uint8_t *status, bool ok) {
     const int k = d->code.k, r = d->code.r;
     const bool lp = is_lenprefix(d->code);
-    DevGuard g(d->dev);
-    const hipError_t e = hipEventSynchronize(d->done);
-    const size_t n = d->sel.size();
-    const size_t o_stat = d->arg_cap / 2;  // see dec_launch
-    const uint8_t *status = d->arg.host + o_stat;
     ssize_t recovered = 0;
-    for (size_t i = 0; i < n; i++) {
+    for (size_t i = 0; i < d->sel.size(); i++) {
         const uint32_t s = d->sel[i];
         DecSlot &w = d->slots[s];
         w.inflight = false;
-        if (e != hipSuccess) continue;
+        if (!ok) continue;
         uint64_t got_mask = 0;
         for (int j = 0; j < k; j++) {
             if ((w.present >> j) & 1) continue;
@@ -576,7 +570,18 @@ ssize_t dec_complete(fecgpu_decoder *d) {
         w.present |= got_mask;
     }
     d->sel.clear();
-    return e == hipSuccess ? recovered : FECGPU_ERR_DEVICE;
+    return recovered;
+}
+
+// Completes the pending decode: waits for it and marks what it recovered.
+// Returns the number of recovered sources (0 if nothing was pending).
+ssize_t dec_complete(fecgpu_decoder *d) {
+    if (!d->pending) return 0;
+    d->pending = false;
+    DevGuard g(d->dev);
+    const hipError_t e = hipEventSynchronize(d->done);
+    const ssize_t rec = dec_apply(d, d->arg.host + d->arg_cap / 2, e == hipSuccess);  // see dec_args
+    return e == hipSuccess ? rec : FECGPU_ERR_DEVICE;
 }
 
 // A call about to read or write slot s first completes a decode that owns it.
@@ -584,12 +589,9 @@ ssize_t dec_ready(fecgpu_decoder *d, uint32_t s) {
     return d->slots[s].inflight ? dec_complete(d) : 0;
 }
 
-// Launches one decode over the candidate windows that can recover something
-// (all but `keep`, which stays a candidate).  The caller completes any
-// pending decode first.  Returns the number of windows launched.
-ssize_t dec_launch(fecgpu_decoder *d, uint32_t keep) {
-    const int k = d->code.k;
-    const bool lp = is_lenprefix(d->code);
+// The candidate windows that can recover something now go to d->sel (all but
+// `keep`, which stays a candidate).  Returns |sel|.
+size_t dec_select(fecgpu_decoder *d, uint32_t keep) {
     std::vector<uint32_t> &sel = d->sel;
     sel.clear();
     bool kept = false;
@@ -610,34 +612,49 @@ ssize_t dec_launch(fecgpu_decoder *d, uint32_t keep) {
         d->dirty = 1;
         d->dirty_t = d->now;
     }
-    if (sel.empty()) return 0;
-    DevGuard g(d->dev);
-    const size_t n = sel.size();
-    // per-window arguments in pinned memory the kernel reads directly; the
-    // status bytes live in the upper half so dec_complete finds them at arg_cap/2
-    const size_t o_len = (n * 8 + 255) & ~size_t(255), o_pres = o_len + ((n * 4 + 255) & ~size_t(255));
-    const size_t need = o_pres + n * 8;
+    return sel.size();
+}
+
+// Per-window launch arguments for n windows in d's pinned argument block, which
+// the kernel reads directly: win_off, sym_len, present, and the status bytes
+// in the upper half (dec_complete finds them at arg_cap / 2).
+struct DecArgs {
+    uint64_t *off;
+    uint32_t *len;
+    uint64_t *pres;
+    uint8_t *status;
+    size_t o_len, o_pres, o_stat;
+};
+
+ssize_t dec_args(fecgpu_decoder *d, size_t n, DecArgs &a) {
+    a.o_len = (n * 8 + 255) & ~size_t(255);
+    a.o_pres = a.o_len + ((n * 4 + 255) & ~size_t(255));
+    const size_t need = a.o_pres + n * 8;
     if (d->arg_cap / 2 < std::max(need, n)) {
         pinned_free(d->ctx, d->arg);
         d->arg_cap = 0;
         ssize_t rc = pinned_alloc(d->ctx, std::max(need, (size_t)64 << 10) * 2, d->arg);
-        if (rc) {
-            for (uint32_t s : sel) d->slots[s].inflight = false;
-            sel.clear();
-            return rc;
-        }
+        if (rc) return rc;
         d->arg_cap = d->arg.bytes;
     }
-    const size_t o_stat = d->arg_cap / 2;
-    uint64_t *off = reinterpret_cast<uint64_t *>(d->arg.host);
-    uint32_t *len = reinterpret_cast<uint32_t *>(d->arg.host + o_len);
-    uint64_t *pres = reinterpret_cast<uint64_t *>(d->arg.host + o_pres);
-    uint8_t *status = d->arg.host + o_stat;
-    const uint64_t base = reinterpret_cast<uint64_t>(d->chunks[0].dev);
-    for (size_t i = 0; i < n; i++) {
-        const uint32_t s = sel[i];
+    a.o_stat = d->arg_cap / 2;
+    a.off = reinterpret_cast<uint64_t *>(d->arg.host);
+    a.len = reinterpret_cast<uint32_t *>(d->arg.host + a.o_len);
+    a.pres = reinterpret_cast<uint64_t *>(d->arg.host + a.o_pres);
+    a.status = d->arg.host + a.o_stat;
+    return 0;
+}
+
+// Fills argument rows [i0, i0 + |d->sel|) for d's selected windows, as
+// offsets from `base` (64-bit wrap: any pinned chunk of any decoder), and
+// zero-pads their received LENPREFIX sources (A.3).
+void dec_fill(fecgpu_decoder *d, uint64_t base, size_t i0, const DecArgs &a) {
+    const int k = d->code.k;
+    const bool lp = is_lenprefix(d->code);
+    for (size_t i = 0; i < d->sel.size(); i++) {
+        const uint32_t s = d->sel[i];
         DecSlot &w = d->slots[s];
-        if (lp) {  // zero padding of the received sources up to S (A.3)
+        if (lp) {
             const uint32_t S16 = rup16(w.S);
             for (int j = 0; j < k; j++)
                 if ((w.present >> j) & 1) {
@@ -645,26 +662,53 @@ ssize_t dec_launch(fecgpu_decoder *d, uint32_t keep) {
                     std::memset(dec_row(d, s, j) + used, 0, S16 - used);
                 }
         }
-        off[i] = dec_dev_addr(d, s) - base;  // wraps for chunks below the first
-        len[i] = w.S;
-        pres[i] = w.present;
-        status[i] = 0xFF;
+        a.off[i0 + i] = dec_dev_addr(d, s) - base;
+        a.len[i0 + i] = w.S;
+        a.pres[i0 + i] = w.present;
+        a.status[i0 + i] = 0xFF;
         w.inflight = true;
     }
+}
+
+// Launches the decode of n argument rows on d's stream and records d->done.
+ssize_t dec_launch_args(fecgpu_decoder *d, uint64_t base, size_t n, const DecArgs &da) {
     BatchArgs a{};
-    a.win = d->chunks[0].dev;
+    a.win = reinterpret_cast<uint8_t *>(base);
     a.win_off = reinterpret_cast<const uint64_t *>(d->arg.dev);
-    a.sym_len = reinterpret_cast<const uint32_t *>(d->arg.dev + o_len);
-    a.present = reinterpret_cast<const uint64_t *>(d->arg.dev + o_pres);
-    a.status = d->arg.dev + o_stat;
+    a.sym_len = reinterpret_cast<const uint32_t *>(d->arg.dev + da.o_len);
+    a.present = reinterpret_cast<const uint64_t *>(d->arg.dev + da.o_pres);
+    a.status = d->arg.dev + da.o_stat;
     a.stride = d->stride;
     a.off_stride = d->stride;
     a.nwin = n;
     ssize_t rc = fecgpu::launch_batch(d->ctx, &d->code, true, a, d->stream, true);
     if (rc == 0 && hipEventRecord(d->done, d->stream) != hipSuccess) rc = FECGPU_ERR_DEVICE;
+    return rc;
+}
+
+void dec_unselect(fecgpu_decoder *d) {
+    for (uint32_t s : d->sel) d->slots[s].inflight = false;
+    d->sel.clear();
+}
+
+// Launches one decode over the candidate windows that can recover something
+// (all but `keep`, which stays a candidate).  The caller completes any
+// pending decode first.  Returns the number of windows launched.
+ssize_t dec_launch(fecgpu_decoder *d, uint32_t keep) {
+    const size_t n = dec_select(d, keep);
+    if (n == 0) return 0;
+    DevGuard g(d->dev);
+    DecArgs a;
+    ssize_t rc = dec_args(d, n, a);
     if (rc) {
-        for (uint32_t s : sel) d->slots[s].inflight = false;
-        sel.clear();
+        d->sel.clear();
+        return rc;
+    }
+    const uint64_t base = reinterpret_cast<uint64_t>(d->chunks[0].dev);
+    dec_fill(d, base, 0, a);
+    rc = dec_launch_args(d, base, n, a);
+    if (rc) {
+        dec_unselect(d);
         return rc;
     }
     d->pending = true;
@@ -691,6 +735,50 @@ ssize_t fecgpu_decoder_flush(fecgpu_decoder *d) {
     if (rc <= 0) return rc < 0 ? rc : before;
     rc = dec_complete(d);
     return rc < 0 ? rc : before + rc;
+}
+
+ssize_t fecgpu_decoder_flush_many(fecgpu_decoder *const *decs, size_t n) {
+    if (!decs || n == 0) return FECGPU_ERR_INVALID_ARG;
+    fecgpu_decoder *d0 = decs[0];
+    for (size_t i = 0; i < n; i++) {
+        const fecgpu_decoder *d = decs[i];
+        if (!d || !d0 || d->ctx != d0->ctx || d->dev != d0->dev || d->stride != d0->stride ||
+            std::memcmp(&d->code, &d0->code, sizeof(fecgpu_code)) != 0)
+            return FECGPU_ERR_INVALID_ARG;
+        for (size_t j = 0; j < i; j++)
+            if (decs[j] == d) return FECGPU_ERR_INVALID_ARG;  // listed twice
+    }
+    ssize_t before = 0;
+    for (size_t i = 0; i < n; i++) {  // automatic flushes still in flight
+        const ssize_t rc = dec_complete(decs[i]);
+        if (rc < 0) return rc;
+        before += rc;
+    }
+    size_t total = 0;
+    uint64_t base = 0;
+    for (size_t i = 0; i < n; i++) {
+        total += dec_select(decs[i], UINT32_MAX);
+        if (!base && !decs[i]->chunks.empty()) base = reinterpret_cast<uint64_t>(decs[i]->chunks[0].dev);
+    }
+    if (total == 0) return before;
+    DevGuard g(d0->dev);
+    DecArgs a;
+    ssize_t rc = dec_args(d0, total, a);
+    if (rc) {
+        for (size_t i = 0; i < n; i++) decs[i]->sel.clear();
+        return rc;
+    }
+    std::vector<size_t> at(n);
+    for (size_t i = 0, i0 = 0; i < n; i0 += decs[i]->sel.size(), i++) {
+        at[i] = i0;
+        dec_fill(decs[i], base, i0, a);
+    }
+    rc = dec_launch_args(d0, base, total, a);  // one launch for every decoder
+    const bool ok = rc == 0 && hipEventSynchronize(d0->done) == hipSuccess;
+    ssize_t rec = 0;
+    for (size_t i = 0; i < n; i++) rec += dec_apply(decs[i], a.status + at[i], ok);
+    if (rc) return rc;
+    return ok ? before + rec : FECGPU_ERR_DEVICE;
 }
 
 ssize_t fecgpu_decoder_add_source(fecgpu_decoder *d, uint64_t win, uint16_t idx, const uint8_t *pkt,

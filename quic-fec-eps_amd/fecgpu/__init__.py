@@ -46,7 +46,8 @@ EXPORTS = (
     "fecgpu_encoder_close_window", "fecgpu_encoder_flush", "fecgpu_encoder_repair",
     "fecgpu_encoder_release",
     "fecgpu_decoder_new", "fecgpu_decoder_free", "fecgpu_decoder_add_source",
-    "fecgpu_decoder_add_repair", "fecgpu_decoder_flush", "fecgpu_decoder_recovered",
+    "fecgpu_decoder_add_repair", "fecgpu_decoder_flush", "fecgpu_decoder_flush_many",
+    "fecgpu_decoder_recovered",
     "fecgpu_decoder_release",
     "fecgpu_encoder_set_policy", "fecgpu_encoder_tick", "fecgpu_decoder_set_policy",
     "fecgpu_decoder_tick",
@@ -147,6 +148,7 @@ def _lib():
             "fecgpu_decoder_add_source": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
             "fecgpu_decoder_add_repair": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
             "fecgpu_decoder_flush": (sz, [vp]),
+            "fecgpu_decoder_flush_many": (sz, [ctypes.POINTER(vp), ctypes.c_size_t]),
             "fecgpu_decoder_recovered": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
             "fecgpu_decoder_release": (sz, [vp, u64]),
             "fecgpu_encoder_set_policy": (sz, [vp, ctypes.POINTER(_Policy)]),
@@ -433,6 +435,13 @@ class Decoder:
             self.close()
         except Exception:
             pass
+
+
+def decoder_flush_many(decs) -> int:
+    """fecgpu_decoder_flush_many: flush several decoders (same ctx, code, max_len)
+    in one launch; returns the sources recovered over all of them."""
+    arr = (ctypes.c_void_p * len(decs))(*[d._h.value for d in decs])
+    return _check(_lib().fecgpu_decoder_flush_many(arr, len(decs)), "fecgpu_decoder_flush_many")
 
 
 def frame_source_id(win: int, idx: int) -> bytes:

@@ -246,6 +246,35 @@ def test_checked_per_connection(chk, scheme, k, r, framing, mtu, loss, batch, va
     _run(ctx, m.Code(scheme, k, r, framing), data, mtu, loss, 9, batch=batch, vary=vary, m=m)
 
 
+def test_checked_flush_many(chk):
+    """fecgpu_decoder_flush_many on the checked build: one launch over windows of 20
+    decoders' separate pinned pools (offsets from one base, wrapping)."""
+    m, _ = chk
+    c = m.Context()
+    code = m.Code("gf256", 8, 2, "lenprefix")
+    rng = np.random.default_rng(3)
+    encs = [m.Encoder(c, code, max_len=700, batch=2) for _ in range(20)]
+    decs = [m.Decoder(c, code, max_len=700, batch=64) for _ in range(20)]
+    sent = []
+    for e, d in zip(encs, decs):
+        pk = [rng.integers(0, 256, int(rng.integers(1, 701)), dtype=np.uint8).tobytes() for _ in range(24)]
+        ids = [e.add_source(p) for p in pk]
+        e.flush()
+        for (w, j), p in zip(ids, pk):
+            if j not in (2, 5):
+                assert d.add_source(w, j, p) == 0
+        for w in {w for w, _ in ids}:
+            for t in range(2):
+                assert d.add_repair(w, t, e.repair(w, t)) == 0
+        sent.append((ids, pk))
+    assert m.decoder_flush_many(decs) == 20 * 3 * 2
+    for d, (ids, pk) in zip(decs, sent):
+        assert all(d.recovered(w, j) == p for (w, j), p in zip(ids, pk))
+    for o in encs + decs:
+        o.close()
+    c.close()
+
+
 def test_release_build_has_no_checker():
     ctx = fecgpu.Context()
     try:

@@ -280,6 +280,64 @@ def test_connection_churn_reuses_pinned_blocks():
     assert times[1024] < times[0] * 1.1
 
 
+@pytest.mark.parametrize("scheme,framing", [("gf256", "fixed"), ("xor", "fixed"), ("gf256", "lenprefix")])
+def test_flush_many_one_launch_for_all_connections(scheme, framing):
+    """fecgpu_decoder_flush_many: 200 connections' decoders flushed by one launch
+    recover exactly what 200 separate flushes recover, faster."""
+    import time
+    c = fecgpu.Context()
+    k, r, n = 8, 2, 200
+    code = fecgpu.Code(scheme, k, r, framing)
+    rng = np.random.default_rng(5)
+
+    def setup():
+        encs = [fecgpu.Encoder(c, code, max_len=1200, batch=4) for _ in range(n)]
+        decs = [fecgpu.Decoder(c, code, max_len=1200, batch=64) for _ in range(n)]
+        sent = []
+        for i in range(n):
+            pk = [rng.integers(0, 256, 1200 if framing == "fixed" else int(rng.integers(1, 1201)),
+                               dtype=np.uint8).tobytes() for _ in range(2 * k)]
+            ids = [encs[i].add_source(p) for p in pk]
+            encs[i].flush()
+            lost = {0, 3} if scheme == "gf256" else {0, 1}  # XOR: one per group
+            for (w, j), p in zip(ids, pk):
+                if j not in lost:
+                    assert decs[i].add_source(w, j, p) == 0
+            for w in {w for w, _ in ids}:
+                for t in range(r):
+                    assert decs[i].add_repair(w, t, encs[i].repair(w, t)) == 0
+            sent.append((ids, pk, lost))
+        return encs, decs, sent
+
+    def check(decs, sent):
+        for d, (ids, pk, lost) in zip(decs, sent):
+            for (w, j), p in zip(ids, pk):
+                assert d.recovered(w, j) == p
+
+    encs, decs, sent = setup()
+    t0 = time.perf_counter()
+    got_many = fecgpu.decoder_flush_many(decs)
+    t_many = time.perf_counter() - t0
+    check(decs, sent)
+    encs2, decs2, sent2 = setup()
+    t0 = time.perf_counter()
+    got_each = sum(d.flush() for d in decs2)
+    t_each = time.perf_counter() - t0
+    check(decs2, sent2)
+    assert got_many == got_each == n * 2 * 2
+    print(f"{scheme}/{framing}: 200 decoders, one launch {t_many * 1e3:.2f} ms, "
+          f"200 launches {t_each * 1e3:.2f} ms")
+    assert t_many < t_each
+    with pytest.raises(fecgpu.FecError):  # listed twice
+        fecgpu.decoder_flush_many([decs[0], decs[0]])
+    other = fecgpu.Decoder(c, fecgpu.Code(scheme, k, r, framing), max_len=600, batch=4)
+    with pytest.raises(fecgpu.FecError):  # different max_len
+        fecgpu.decoder_flush_many([decs[0], other])
+    for o in encs + decs + encs2 + decs2 + [other]:
+        o.close()
+    c.close()
+
+
 def test_policy_timeouts(ctx):
     """Scheduling policy: on the caller's clock, a window closes
     window_timeout_us after its first packet and a partly filled batch launches
