@@ -181,6 +181,10 @@ ssize_t fecgpu_encoder_add_source(fecgpu_encoder *enc, const uint8_t *pkt, size_
 ssize_t fecgpu_encoder_close_window(fecgpu_encoder *enc);
 /* Encode every queued window now; returns the number encoded. */
 ssize_t fecgpu_encoder_flush(fecgpu_encoder *enc);
+/* fecgpu_encoder_flush for n encoders in ONE launch, waiting for it (same
+ * ctx, code and max_len; INVALID_ARG otherwise, or if one is listed twice).
+ * Returns the number of windows encoded. */
+ssize_t fecgpu_encoder_flush_many(fecgpu_encoder *const *encs, size_t n);
 /* Copy repair i of window win (S bytes); FECGPU_ERR_DONE until encoded. */
 ssize_t fecgpu_encoder_repair(fecgpu_encoder *enc, uint64_t win, uint16_t i, uint8_t *out,
                               size_t cap);

@@ -325,6 +325,77 @@ ssize_t fecgpu_encoder_flush(fecgpu_encoder *e) {
     return n;
 }
 
+ssize_t fecgpu_encoder_flush_many(fecgpu_encoder *const *encs, size_t n) {
+    if (!encs || n == 0) return FECGPU_ERR_INVALID_ARG;
+    fecgpu_encoder *e0 = encs[0];
+    for (size_t i = 0; i < n; i++) {
+        const fecgpu_encoder *e = encs[i];
+        if (!e || !e0 || e->ctx != e0->ctx || e->dev != e0->dev || e->stride != e0->stride ||
+            std::memcmp(&e->code, &e0->code, sizeof(fecgpu_code)) != 0)
+            return FECGPU_ERR_INVALID_ARG;
+        for (size_t j = 0; j < i; j++)
+            if (encs[j] == e) return FECGPU_ERR_INVALID_ARG;  // listed twice
+    }
+    // every encoder's queued windows, as ragged windows (fixed pitch) of one launch
+    uint64_t total = 0, base = 0;
+    for (size_t i = 0; i < n; i++)
+        if (encs[i]->cur && encs[i]->cur->nwin) {
+            total += encs[i]->cur->nwin;
+            if (!base) base = reinterpret_cast<uint64_t>(encs[i]->cur->mem.dev);
+        }
+    DevGuard g(e0->dev);
+    if (total) {
+        const size_t o_len = (total * 8 + 255) & ~size_t(255);
+        size_t bytes = (size_t)64 << 10;  // power-of-two sizes: the ctx cache finds it next time
+        while (bytes < o_len + total * 4) bytes <<= 1;
+        Pinned arg;
+        ssize_t rc = pinned_alloc(e0->ctx, bytes, arg);
+        if (rc) return rc;
+        uint64_t *off = reinterpret_cast<uint64_t *>(arg.host);
+        uint32_t *len = reinterpret_cast<uint32_t *>(arg.host + o_len);
+        uint64_t i0 = 0;
+        for (size_t i = 0; i < n; i++) {
+            const EncBatch *b = encs[i]->cur;
+            if (!b) continue;
+            for (uint32_t w = 0; w < b->nwin; w++, i0++) {
+                off[i0] = reinterpret_cast<uint64_t>(b->mem.dev) + (uint64_t)w * e0->wbytes - base;
+                len[i0] = b->S[w];
+            }
+        }
+        BatchArgs a{};
+        a.win = reinterpret_cast<uint8_t *>(base);
+        a.win_off = reinterpret_cast<const uint64_t *>(arg.dev);
+        a.sym_len = reinterpret_cast<const uint32_t *>(arg.dev + o_len);
+        a.stride = e0->stride;
+        a.off_stride = e0->stride;
+        a.nwin = total;
+        rc = fecgpu::launch_batch(e0->ctx, &e0->code, false, a, e0->stream, true);  // one launch
+        if (rc == 0) {
+            // no per-batch events: this call waits for the stream before it
+            // returns, so every batch is complete before anyone looks at it
+            // (an event record per batch cost ~5 us each on the host)
+            for (size_t i = 0; i < n; i++) {
+                fecgpu_encoder *e = encs[i];
+                EncBatch *b = e->cur;
+                if (!b || !b->nwin) continue;
+                b->launched = true;
+                e->cur = nullptr;
+                if (b->live == 0) {  // every window already released: recycle
+                    e->active.pop_back();
+                    e->spare.push_back(b);
+                }
+            }
+        }
+        if (hipStreamSynchronize(e0->stream) != hipSuccess && rc == 0) rc = FECGPU_ERR_DEVICE;
+        pinned_free(e0->ctx, arg);
+        if (rc) return rc;
+    }
+    for (size_t i = 0; i < n; i++)  // launches of earlier batches, possibly on other streams
+        if (encs[i]->last_done && hipEventSynchronize(encs[i]->last_done) != hipSuccess)
+            return FECGPU_ERR_DEVICE;
+    return (ssize_t)total;
+}
+
 ssize_t fecgpu_encoder_set_policy(fecgpu_encoder *e, const fecgpu_policy *p) {
     if (!e || !p) return FECGPU_ERR_INVALID_ARG;
     e->policy = *p;

@@ -47,6 +47,7 @@ EXPORTS = (
     "fecgpu_encoder_release",
     "fecgpu_decoder_new", "fecgpu_decoder_free", "fecgpu_decoder_add_source",
     "fecgpu_decoder_add_repair", "fecgpu_decoder_flush", "fecgpu_decoder_flush_many",
+    "fecgpu_encoder_flush_many",
     "fecgpu_decoder_recovered",
     "fecgpu_decoder_release",
     "fecgpu_encoder_set_policy", "fecgpu_encoder_tick", "fecgpu_decoder_set_policy",
@@ -149,6 +150,7 @@ def _lib():
             "fecgpu_decoder_add_repair": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
             "fecgpu_decoder_flush": (sz, [vp]),
             "fecgpu_decoder_flush_many": (sz, [ctypes.POINTER(vp), ctypes.c_size_t]),
+            "fecgpu_encoder_flush_many": (sz, [ctypes.POINTER(vp), ctypes.c_size_t]),
             "fecgpu_decoder_recovered": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
             "fecgpu_decoder_release": (sz, [vp, u64]),
             "fecgpu_encoder_set_policy": (sz, [vp, ctypes.POINTER(_Policy)]),
@@ -435,6 +437,13 @@ class Decoder:
             self.close()
         except Exception:
             pass
+
+
+def encoder_flush_many(encs) -> int:
+    """fecgpu_encoder_flush_many: encode every queued window of several encoders
+    (same ctx, code, max_len) in one launch; returns the windows encoded."""
+    arr = (ctypes.c_void_p * len(encs))(*[e._h.value for e in encs])
+    return _check(_lib().fecgpu_encoder_flush_many(arr, len(encs)), "fecgpu_encoder_flush_many")
 
 
 def decoder_flush_many(decs) -> int:

@@ -268,6 +268,15 @@ def test_checked_flush_many(chk):
                 assert d.add_repair(w, t, e.repair(w, t)) == 0
         sent.append((ids, pk))
     assert m.decoder_flush_many(decs) == 20 * 3 * 2
+    e2 = [m.Encoder(c, code, max_len=700, batch=64) for _ in range(20)]  # queued, not launched
+    for e, (ids, pk) in zip(e2, sent):
+        for p in pk:
+            e.add_source(p)
+    assert m.encoder_flush_many(e2) == 20 * 3
+    for e, ee, (ids, pk) in zip(e2, encs, sent):
+        for w in {w for w, _ in ids}:
+            assert [e.repair(w, t) for t in range(2)] == [ee.repair(w, t) for t in range(2)]
+        e.close()
     for d, (ids, pk) in zip(decs, sent):
         assert all(d.recovered(w, j) == p for (w, j), p in zip(ids, pk))
     for o in encs + decs:
