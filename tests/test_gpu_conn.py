@@ -202,7 +202,10 @@ def test_udp_ring_driver(args):
     ["conn_bench_asan", "xor", "4", "1", "1000", "8", "0.03", "16", "0", "64", "0.02"],
     ["conn_bench_asan", "gf256", "5", "3", "333", "2", "0.2", "3", "0", "7", "0.05"],
     ["udp_ring_asan", "gf256", "16", "4", "1200", "50003", "0.08", "128"],
-], ids=["conn-gf-k32r8-lp", "conn-xor-reorder-dup", "conn-gf-short-last", "udp-gf-k16r4"])
+    ["many_conn_asan", "gf256", "16", "4", "1200", "60", "5", "0.1", "3"],
+    ["many_conn_asan", "xor", "8", "2", "700", "60", "5", "0.05", "2"],
+], ids=["conn-gf-k32r8-lp", "conn-xor-reorder-dup", "conn-gf-short-last", "udp-gf-k16r4",
+        "many-gf-k16r4", "many-xor-k8r2"])
 def test_native_drivers_under_asan(args):
     """The per-connection objects, pools, frames and pinned rings under host
     AddressSanitizer + UBSan (lib/asan/libfecgpu.so: host code instrumented, kernels
@@ -372,6 +375,25 @@ def test_encoder_flush_many(scheme, framing):
     print(f"{scheme}/{framing}: 200 encoders, one launch {t[0] * 1e3:.2f} ms, 200 launches {t[1] * 1e3:.2f} ms")
     assert t[0] < t[1]
     c.close()
+
+
+@pytest.mark.parametrize("args", [["gf256", "16", "4", "1200", "300", "4", "0.1", "3"],
+                                  ["xor", "8", "2", "1200", "300", "4", "0.05", "2"],
+                                  ["gf256", "32", "8", "9000", "40", "2", "0.12", "2"]],
+                         ids=["gf-k16r4", "xor-k8r2", "gf-k32r8-9000"])
+def test_native_many_connections(args):
+    """scripts/many_conn (C++): hundreds of connections per ctx, senders and receivers
+    flushed with the *_flush_many calls, connections closed and reopened each round;
+    every lost packet recovered exactly as the loss pattern allows."""
+    import json
+    import subprocess
+    exe = os.path.join(os.path.dirname(CONN_BENCH), "many_conn")
+    assert os.path.exists(exe), "build first: make -C scripts"
+    r = subprocess.run([exe, *args], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["corrupt"] == 0 and res["unrecovered"] == res["expected_unrecovered"]
+    assert res["recovered"] + res["unrecovered"] == res["lost"] > 0
 
 
 def test_policy_timeouts(ctx):
