@@ -29,6 +29,19 @@ def test_header_declarations_are_exported():
     assert sorted(fecgpu.EXPORTS) == names
 
 
+def test_integration_binding_matches_header():
+    """INTEGRATION.md's Rust extern block binds only header functions, and
+    every header function is either bound or named as an unbound helper."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = re.search(r"```rust\n(.*?)```", doc, flags=re.S).group(1)
+    bound = set(re.findall(r"pub fn (fecgpu_[a-z_0-9]+)\(", block))
+    names = set(declared())
+    assert bound <= names, sorted(bound - names)
+    rest = doc[doc.index("```", doc.index("```rust") + 3):]
+    for n in sorted(names - bound):
+        assert f"`{n}`" in rest, f"{n} neither bound nor named in INTEGRATION.md"
+
+
 def test_exports_are_c_symbols():
     out = subprocess.run(["nm", "-D", "--defined-only", fecgpu.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout
