@@ -14,9 +14,11 @@ Workloads (BASELINE.json configs):
                         exactly r sources erased per window
   --config 4          : GF(2^8) k=32 r=8, mixed MTU 1200/9000 LENPREFIX,
                         131,072 windows per GPU (1M over 8), i.i.d. 10% erasures
-Multi-GPU: one process per GPU (torchrun), windows sharded by rank with no
-data-path collective (weak scaling); RCCL only carries the barrier and the
-max-over-ranks time reduction.
+Multi-GPU: one process per GPU, windows sharded by rank with no data-path
+collective (weak scaling); RCCL only carries the barrier, the max-over-ranks
+time reduction and the 8-byte digest all-gather.  `--gpus N` launched without
+WORLD_SIZE (plain `python bench.py --gpus N`) starts the N ranks itself: a
+torch.distributed.run child, spawned before this process touches the GPU.
 """
 from __future__ import annotations
 
@@ -87,6 +89,18 @@ def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def host_share() -> int:
+    """Host threads for the CPU baseline: every core this process may run on
+    (sched_getaffinity), bounded by the CPU share the GPU pool grants one GPU's
+    job (OMP_NUM_THREADS, 16 on the box: its nproc / cpu_count show the whole
+    machine, whose other cores belong to other GPUs' jobs)."""
+    n = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
 def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
     """Time the CPU codec (oracle/fec_cpu_simd.c: the oracle's contract with
     AVX2 nibble tables / GFNI affine products, ISA-L style; kind "port") on a
@@ -95,8 +109,9 @@ def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
     import oracle as O  # test/baseline infrastructure only
 
     O.lib()
+    aff = len(os.sched_getaffinity(0))
     if threads <= 0:
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        threads = host_share()
     scheme = O.XOR if cfg.scheme == "xor" else O.GF256
     win_bytes = (cfg.k + cfg.r) * cfg.stride
     max_nw = max(threads, (2 << 30) // win_bytes)  # sample buffer <= 2 GiB
@@ -127,17 +142,48 @@ def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
             break
     dt, src = tot_dt, tot_src
     return {"value": round(src / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "host_cores": {"affinity": aff, "cpu_count": os.cpu_count(), "used": threads,
+                           "share_env": os.environ.get("OMP_NUM_THREADS")},
             "codec": f"oracle/fec_cpu_simd.c ({O.SIMD_NAMES[O.simd_level()]}; equal outputs to the "
                      f"scalar oracle: tests/test_oracle_simd.py)",
             "sample": f"{nw} windows of {cfg.name} (encode+decode, same packets and erasures), "
                       f"{dt:.1f} s on {threads} host threads"}
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: run N ranks (one per GPU) through a
+    torch.distributed.run child and return its exit code.  Called before anything
+    touches the GPU (device_count() does not initialise it on this image), and
+    the child is a separate process, never an exec of this one."""
+    import socket
+    import subprocess
+    if args.dist_backend == "nccl":
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            log(f"--gpus {args.gpus} needs {args.gpus} GPUs (one rank per GPU over RCCL); "
+                f"{ndev} visible (use --dist-backend gloo for a shared-GPU rehearsal)")
+            return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a mislabelled run")
+        sys.exit(2)
+    log(f"rank {rank}/{world} (local {local}) starting, backend "
+        f"{args.dist_backend if world > 1 else 'none'}")
     if world > 1:
         if args.dist_backend == "nccl":  # RCCL: one rank per GPU
             torch.cuda.set_device(local)
@@ -254,6 +300,11 @@ def main():
             "value": round(value, 3),
             "unit": "GB/s",
             "n_gpus": world,
+            "ranks": world,
+            "gpus_used": min(world, torch.cuda.device_count()),
+            "rehearsal": (None if world <= torch.cuda.device_count() else
+                          f"{world} ranks share {torch.cuda.device_count()} GPU(s) ({args.dist_backend}): "
+                          f"exercises the N>1 path, not a multi-GPU measurement"),
             "value_per_gpu": round(value / world, 3),
             "steps": args.steps,
             "warmup": args.warmup,

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define FECGPU_ABI_VERSION 1
+#define FECGPU_ABI_VERSION 2  /* 2: REPAIR frames carry nsrc; decoder limits / recovered queue */
 
 /* errors (mirror quiche's QUICHE_ERR_DONE = -1, QUICHE_ERR_BUFFER_TOO_SHORT = -2 style) */
 enum fecgpu_error {
@@ -57,6 +57,7 @@ enum fecgpu_error {
     FECGPU_ERR_UNSUPPORTED = -4,      /* valid but not implemented (e.g. r > 8) */
     FECGPU_ERR_DEVICE = -5,           /* HIP error or no GPU */
     FECGPU_ERR_UNRECOVERABLE = -6,    /* too many erasures in a window */
+    FECGPU_ERR_LIMIT = -7,            /* decoder: open-window limit reached (release windows) */
 };
 
 enum fecgpu_scheme { FECGPU_SCHEME_XOR = 0, FECGPU_SCHEME_GF256 = 1 };
@@ -185,6 +186,11 @@ ssize_t fecgpu_encoder_flush(fecgpu_encoder *enc);
  * ctx, code and max_len; INVALID_ARG otherwise, or if one is listed twice).
  * Returns the number of windows encoded. */
 ssize_t fecgpu_encoder_flush_many(fecgpu_encoder *const *encs, size_t n);
+/* Number of real sources (1..k) of closed window win: k unless the window was
+ * closed early (close_window, window timeout), whose padding sources never go
+ * on the wire.  Carried in the REPAIR frame (nsrc).  FECGPU_ERR_DONE if win is
+ * not closed yet or released. */
+ssize_t fecgpu_encoder_window_sources(fecgpu_encoder *enc, uint64_t win);
 /* Copy repair i of window win (S bytes); FECGPU_ERR_DONE until encoded. */
 ssize_t fecgpu_encoder_repair(fecgpu_encoder *enc, uint64_t win, uint16_t i, uint8_t *out,
                               size_t cap);
@@ -202,9 +208,21 @@ ssize_t fecgpu_decoder_add_source(fecgpu_decoder *dec, uint64_t win, uint16_t id
                                   const uint8_t *pkt, size_t len);
 ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *dec, uint64_t win, uint16_t idx,
                                   const uint8_t *sym, size_t len);
+/* A REPAIR frame's nsrc < k: sources nsrc..k-1 of window win are padding
+ * (empty / zero packets the sender never sent), so they count as received.
+ * Idempotent; INVALID_ARG if a source >= nsrc was filed or nsrc differs from
+ * an earlier call.  recovered() returns FECGPU_ERR_DONE for padding indices. */
+ssize_t fecgpu_decoder_set_window_sources(fecgpu_decoder *dec, uint64_t win, uint16_t nsrc);
+/* At most max_windows windows open (filed and not released) per decoder
+ * (default 4096; 0 = no limit): a symbol of a further window is rejected with
+ * FECGPU_ERR_LIMIT and nothing is pinned for it, so a peer cannot make the
+ * receiver pin memory without bound.  The Connection releases delivered
+ * windows (fecgpu_decoder_release) to make room. */
+ssize_t fecgpu_decoder_set_max_windows(fecgpu_decoder *dec, uint64_t max_windows);
 /* Decode every window that can now recover a missing source and wait for
- * it; returns the number of source packets recovered (including those of an
- * automatic flush completed here). */
+ * it; returns the number of source packets recovered since the last flush or
+ * tick returned, including those of automatic flushes completed in between
+ * (inside add / recovered / release calls). */
 ssize_t fecgpu_decoder_flush(fecgpu_decoder *dec);
 /* fecgpu_decoder_flush for n decoders in ONE launch, waiting for it: a server
  * that flushes many connections at once pays one kernel, not n.  The decoders
@@ -215,6 +233,12 @@ ssize_t fecgpu_decoder_flush_many(fecgpu_decoder *const *decs, size_t n);
  * returns its length, FECGPU_ERR_DONE if it is not available. */
 ssize_t fecgpu_decoder_recovered(fecgpu_decoder *dec, uint64_t win, uint16_t idx, uint8_t *out,
                                  size_t cap);
+/* Recovered packets in the order they were recovered: *win / *idx of the
+ * oldest one not yet returned (skipping windows released since); returns 0,
+ * or FECGPU_ERR_DONE when there is none.  Lets a Connection deliver recovered
+ * packets without scanning its windows.  The queue holds at most
+ * max(4096, k x max_windows) entries (oldest dropped first). */
+ssize_t fecgpu_decoder_next_recovered(fecgpu_decoder *dec, uint64_t *win, uint16_t *idx);
 ssize_t fecgpu_decoder_release(fecgpu_decoder *dec, uint64_t win);
 
 /* Scheduling policy: bounds the time a packet waits for its
@@ -241,7 +265,8 @@ ssize_t fecgpu_decoder_tick(fecgpu_decoder *dec, uint64_t now_us);
 /* ---- FEC frames on the wire --------------------
  * QUIC varint-coded frames (RFC 9000 §16 integers):
  *   SOURCE_ID: type | window | index                    (next to a source payload)
- *   REPAIR   : type | window | k | r | index | length | symbol bytes
+ *   REPAIR   : type | window | k | r | nsrc | index | length | symbol bytes
+ * nsrc = real sources of the window (fecgpu_encoder_window_sources), 1..k.
  * Frame types sit in QUIC's extension space.  Host-only, no device calls. */
 #define FECGPU_FRAME_SOURCE_ID 0xfec0u
 #define FECGPU_FRAME_REPAIR 0xfec1u
@@ -253,19 +278,21 @@ typedef struct fecgpu_frame {
     uint16_t idx;            /* source index (SOURCE_ID) or repair index (REPAIR) */
     const uint8_t *payload;  /* REPAIR: points into the parsed buffer */
     size_t payload_len;
+    uint16_t nsrc;           /* REPAIR: real sources of the window, 1..k */
 } fecgpu_frame;
 
 ssize_t fecgpu_frame_source_id_len(uint64_t win, uint16_t idx);
 ssize_t fecgpu_frame_write_source_id(uint8_t *buf, size_t cap, uint64_t win, uint16_t idx);
-ssize_t fecgpu_frame_repair_len(uint64_t win, uint16_t k, uint16_t r, uint16_t idx, size_t sym_len);
+ssize_t fecgpu_frame_repair_len(uint64_t win, uint16_t k, uint16_t r, uint16_t nsrc, uint16_t idx,
+                                size_t sym_len);
 ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16_t k, uint16_t r,
-                                  uint16_t idx, const uint8_t *sym, size_t sym_len);
+                                  uint16_t nsrc, uint16_t idx, const uint8_t *sym, size_t sym_len);
 /* REPAIR frame header only (every field up to and including length): the
  * symbol bytes follow from the caller's own buffer, e.g. as a second iovec of
  * a gather send straight from the pinned window row (zero-copy, §8f-4).
  * Returns the header length. */
 ssize_t fecgpu_frame_write_repair_header(uint8_t *buf, size_t cap, uint64_t win, uint16_t k,
-                                         uint16_t r, uint16_t idx, size_t sym_len);
+                                         uint16_t r, uint16_t nsrc, uint16_t idx, size_t sym_len);
 /* Parse one frame at buf; returns bytes consumed or a negative error
  * (BUFFER_TOO_SHORT on truncation, INVALID_ARG on an unknown type or bad field). */
 ssize_t fecgpu_frame_parse(const uint8_t *buf, size_t len, fecgpu_frame *out);

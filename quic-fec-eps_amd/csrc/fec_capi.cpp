@@ -169,6 +169,7 @@ const char *fecgpu_strerror(ssize_t err) {
         case FECGPU_ERR_UNSUPPORTED: return "unsupported";
         case FECGPU_ERR_DEVICE: return "device error";
         case FECGPU_ERR_UNRECOVERABLE: return "unrecoverable";
+        case FECGPU_ERR_LIMIT: return "limit reached";
         default: return err >= 0 ? "ok" : "unknown error";
     }
 }
@@ -862,16 +863,18 @@ ssize_t run_host_pipelined(fecgpu_ctx *ctx, int di, const fecgpu_code *code, boo
 namespace fecgpu {
 
 ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
-                     hipStream_t s, bool remote) {
+                     hipStream_t s, bool remote, int dev) {
     if (!ctx || !a.win) return FECGPU_ERR_INVALID_ARG;
     ssize_t rc = fecgpu_code_check(code);
     if (rc) return rc;
     if (a.nwin == 0) return 0;
+    // the object's own device: its stream, pinned windows and tables live there
+    const int d = dev >= 0 ? dev : ctx->devs[0];
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev), "hipGetDevice");
-    if (prev != ctx->devs[0]) HIP_TRY(hipSetDevice(ctx->devs[0]), "hipSetDevice");
+    if (prev != d) HIP_TRY(hipSetDevice(d), "hipSetDevice");
     rc = launch_device(ctx, code, decode, a, s, remote);
-    if (prev != ctx->devs[0]) (void)hipSetDevice(prev);
+    if (prev != d) (void)hipSetDevice(prev);
     return rc;
 }
 

@@ -105,6 +105,7 @@ struct EncBatch {
     uint32_t live = 0;        // closed and not released
     bool launched = false;
     std::vector<uint8_t> released;
+    std::vector<uint16_t> nsrc;  // real sources per window (k unless closed early)
 };
 
 }  // namespace
@@ -155,6 +156,7 @@ ssize_t enc_take_batch(fecgpu_encoder *e) {
             return FECGPU_ERR_DEVICE;
         }
         b->released.assign(e->batch, 0);
+        b->nsrc.assign(e->batch, 0);
         e->all.push_back(b);
     }
     b->first = e->next_win;
@@ -176,7 +178,7 @@ ssize_t enc_launch(fecgpu_encoder *e) {
     a.sym_len = b->S_dev;
     a.stride = e->stride;
     a.nwin = b->nwin;
-    ssize_t rc = fecgpu::launch_batch(e->ctx, &e->code, false, a, e->stream, true);
+    ssize_t rc = fecgpu::launch_batch(e->ctx, &e->code, false, a, e->stream, true, e->dev);
     if (rc) return rc;
     DevGuard g(e->dev);
     if (hipEventRecord(b->done, e->stream) != hipSuccess) return FECGPU_ERR_DEVICE;
@@ -213,6 +215,7 @@ ssize_t enc_close(fecgpu_encoder *e) {
         std::memset(row + used, 0, S16 - used);
     }
     b->S[slot] = S;
+    b->nsrc[slot] = (uint16_t)e->open_n;
     if (b->nwin == 0) e->cur_t = e->now;
     b->nwin++;
     b->live++;
@@ -281,6 +284,12 @@ ssize_t fecgpu_encoder_add_source(fecgpu_encoder *e, const uint8_t *pkt, size_t 
     if (!lp) {
         if (len == 0) return FECGPU_ERR_INVALID_ARG;
         if (e->open_n && e->open_len[0] != len) return FECGPU_ERR_INVALID_ARG;
+    }
+    if (e->cur && e->cur->nwin >= e->batch) {
+        // a full batch whose launch failed earlier: launch it before taking
+        // a new source (never index a slot past the batch)
+        ssize_t rc = enc_launch(e);
+        if (rc < 0) return rc;
     }
     if (!e->cur) {
         ssize_t rc = enc_take_batch(e);
@@ -369,7 +378,7 @@ ssize_t fecgpu_encoder_flush_many(fecgpu_encoder *const *encs, size_t n) {
         a.stride = e0->stride;
         a.off_stride = e0->stride;
         a.nwin = total;
-        rc = fecgpu::launch_batch(e0->ctx, &e0->code, false, a, e0->stream, true);  // one launch
+        rc = fecgpu::launch_batch(e0->ctx, &e0->code, false, a, e0->stream, true, e0->dev);  // one launch
         if (rc == 0) {
             // no per-batch events: this call waits for the stream before it
             // returns, so every batch is complete before anyone looks at it
@@ -420,6 +429,14 @@ ssize_t fecgpu_encoder_tick(fecgpu_encoder *e, uint64_t now_us) {
     return launched;
 }
 
+ssize_t fecgpu_encoder_window_sources(fecgpu_encoder *e, uint64_t win) {
+    if (!e) return FECGPU_ERR_INVALID_ARG;
+    uint32_t slot = 0;
+    EncBatch *b = enc_find(e, win, slot);
+    if (!b || b->released[slot]) return FECGPU_ERR_DONE;
+    return (ssize_t)b->nsrc[slot];
+}
+
 ssize_t fecgpu_encoder_repair(fecgpu_encoder *e, uint64_t win, uint16_t i, uint8_t *out,
                               size_t cap) {
     if (!e || i >= e->code.r) return FECGPU_ERR_INVALID_ARG;
@@ -459,6 +476,7 @@ struct DecSlot {
     uint64_t win = 0;
     uint64_t present = 0;  // bit i: symbol i held (received or recovered)
     uint32_t S = 0;        // known once a repair (or FIXED source) arrives
+    uint16_t nsrc = 0;     // real sources (REPAIR frame nsrc); 0 = not told (k)
     bool used = false;
     bool cand = false;     // touched since the last flush
     bool inflight = false; // in the launched, not yet completed decode
@@ -493,6 +511,9 @@ struct fecgpu_decoder {
     std::vector<uint32_t> sel;         // windows of the launched decode (in arg order)
     bool pending = false;              // a launched decode awaits completion
     hipEvent_t done = nullptr;         // recorded after the pending decode
+    uint64_t max_windows = 4096;       // open-window limit (0 = none)
+    ssize_t rec_acc = 0;               // recovered since flush / tick last returned
+    std::deque<std::pair<uint64_t, uint16_t>> rec_q;  // recovered (win, idx), oldest first
 };
 
 namespace {
@@ -512,6 +533,8 @@ ssize_t dec_slot(fecgpu_decoder *d, uint64_t win, uint32_t &out) {
         out = it->second;
         return 0;
     }
+    // a peer controls the window ids it sends: bound what it can make us pin
+    if (d->max_windows && d->map.size() >= d->max_windows) return FECGPU_ERR_LIMIT;
     if (d->free_slots.empty()) {
         Pinned p;
         ssize_t rc = pinned_alloc(d->ctx, (size_t)d->chunk_slots * d->wbytes, p);
@@ -637,11 +660,24 @@ ssize_t dec_apply(fecgpu_decoder *d, const uint8_t *status, bool ok) {
             d->plen[(size_t)s * k + j] = pl;
             got_mask |= 1ull << j;
             recovered++;
+            d->rec_q.emplace_back(w.win, (uint16_t)j);
         }
         w.present |= got_mask;
     }
     d->sel.clear();
+    // the queue is for callers that poll it; bounded for those that do not
+    const size_t qcap = std::max<size_t>(4096, (size_t)k * (d->max_windows ? d->max_windows : d->slots.size()));
+    while (d->rec_q.size() > qcap) d->rec_q.pop_front();
+    d->rec_acc += recovered;
     return recovered;
+}
+
+// Recovered count since the last flush / tick returned (every completed
+// decode adds to it, whichever call completed it), and reset it.
+ssize_t dec_take(fecgpu_decoder *d) {
+    const ssize_t n = d->rec_acc;
+    d->rec_acc = 0;
+    return n;
 }
 
 // Completes the pending decode: waits for it and marks what it recovered.
@@ -725,14 +761,18 @@ void dec_fill(fecgpu_decoder *d, uint64_t base, size_t i0, const DecArgs &a) {
     for (size_t i = 0; i < d->sel.size(); i++) {
         const uint32_t s = d->sel[i];
         DecSlot &w = d->slots[s];
+        const uint32_t S16 = rup16(w.S);
+        const int nsrc = w.nsrc ? w.nsrc : k;
         if (lp) {
-            const uint32_t S16 = rup16(w.S);
-            for (int j = 0; j < k; j++)
+            for (int j = 0; j < nsrc; j++)
                 if ((w.present >> j) & 1) {
                     const uint32_t used = 2 + d->plen[(size_t)s * k + j];
                     std::memset(dec_row(d, s, j) + used, 0, S16 - used);
                 }
         }
+        // padding sources of a window closed early: empty (LENPREFIX) / zero
+        // (FIXED) packets, i.e. all-zero rows, as the sender encoded them
+        for (int j = nsrc; j < k; j++) std::memset(dec_row(d, s, j), 0, S16);
         a.off[i0 + i] = dec_dev_addr(d, s) - base;
         a.len[i0 + i] = w.S;
         a.pres[i0 + i] = w.present;
@@ -752,7 +792,7 @@ ssize_t dec_launch_args(fecgpu_decoder *d, uint64_t base, size_t n, const DecArg
     a.stride = d->stride;
     a.off_stride = d->stride;
     a.nwin = n;
-    ssize_t rc = fecgpu::launch_batch(d->ctx, &d->code, true, a, d->stream, true);
+    ssize_t rc = fecgpu::launch_batch(d->ctx, &d->code, true, a, d->stream, true, d->dev);
     if (rc == 0 && hipEventRecord(d->done, d->stream) != hipSuccess) rc = FECGPU_ERR_DEVICE;
     return rc;
 }
@@ -789,7 +829,7 @@ ssize_t dec_launch(fecgpu_decoder *d, uint32_t keep) {
 // The automatic flush after `batch`*k filed symbols: launch without waiting.
 ssize_t dec_auto_flush(fecgpu_decoder *d, uint32_t s) {
     if (++d->dirty < (uint64_t)d->batch * d->code.k) return 0;
-    ssize_t rc = dec_complete(d);
+    ssize_t rc = dec_complete(d);  // its recovered count stays in rec_acc
     if (rc >= 0) rc = dec_launch(d, s);
     return rc < 0 ? FECGPU_ERR_DEVICE : 0;
 }
@@ -800,12 +840,15 @@ extern "C" {
 
 ssize_t fecgpu_decoder_flush(fecgpu_decoder *d) {
     if (!d) return FECGPU_ERR_INVALID_ARG;
-    ssize_t before = dec_complete(d);
-    if (before < 0) return before;
-    ssize_t rc = dec_launch(d, UINT32_MAX);
-    if (rc <= 0) return rc < 0 ? rc : before;
-    rc = dec_complete(d);
-    return rc < 0 ? rc : before + rc;
+    ssize_t rc = dec_complete(d);
+    if (rc < 0) return rc;
+    rc = dec_launch(d, UINT32_MAX);
+    if (rc < 0) return rc;
+    if (rc > 0) {
+        rc = dec_complete(d);
+        if (rc < 0) return rc;
+    }
+    return dec_take(d);
 }
 
 ssize_t fecgpu_decoder_flush_many(fecgpu_decoder *const *decs, size_t n) {
@@ -819,11 +862,14 @@ ssize_t fecgpu_decoder_flush_many(fecgpu_decoder *const *decs, size_t n) {
         for (size_t j = 0; j < i; j++)
             if (decs[j] == d) return FECGPU_ERR_INVALID_ARG;  // listed twice
     }
-    ssize_t before = 0;
+    auto take_all = [&]() {
+        ssize_t t = 0;
+        for (size_t i = 0; i < n; i++) t += dec_take(decs[i]);
+        return t;
+    };
     for (size_t i = 0; i < n; i++) {  // automatic flushes still in flight
         const ssize_t rc = dec_complete(decs[i]);
         if (rc < 0) return rc;
-        before += rc;
     }
     size_t total = 0;
     uint64_t base = 0;
@@ -831,7 +877,7 @@ ssize_t fecgpu_decoder_flush_many(fecgpu_decoder *const *decs, size_t n) {
         total += dec_select(decs[i], UINT32_MAX);
         if (!base && !decs[i]->chunks.empty()) base = reinterpret_cast<uint64_t>(decs[i]->chunks[0].dev);
     }
-    if (total == 0) return before;
+    if (total == 0) return take_all();
     DevGuard g(d0->dev);
     DecArgs a;
     ssize_t rc = dec_args(d0, total, a);
@@ -846,10 +892,9 @@ ssize_t fecgpu_decoder_flush_many(fecgpu_decoder *const *decs, size_t n) {
     }
     rc = dec_launch_args(d0, base, total, a);  // one launch for every decoder
     const bool ok = rc == 0 && hipEventSynchronize(d0->done) == hipSuccess;
-    ssize_t rec = 0;
-    for (size_t i = 0; i < n; i++) rec += dec_apply(decs[i], a.status + at[i], ok);
+    for (size_t i = 0; i < n; i++) (void)dec_apply(decs[i], a.status + at[i], ok);
     if (rc) return rc;
-    return ok ? before + rec : FECGPU_ERR_DEVICE;
+    return ok ? take_all() : FECGPU_ERR_DEVICE;
 }
 
 ssize_t fecgpu_decoder_add_source(fecgpu_decoder *d, uint64_t win, uint16_t idx, const uint8_t *pkt,
@@ -861,6 +906,7 @@ ssize_t fecgpu_decoder_add_source(fecgpu_decoder *d, uint64_t win, uint16_t idx,
     if (rc) return rc;
     if (dec_ready(d, s) < 0) return FECGPU_ERR_DEVICE;
     DecSlot &w = d->slots[s];
+    if (w.nsrc && idx >= w.nsrc) return FECGPU_ERR_INVALID_ARG;  // a padding index
     if ((w.present >> idx) & 1) return FECGPU_ERR_DONE;  // duplicate
     uint8_t *row = dec_row(d, s, idx);
     if (is_lenprefix(d->code)) {
@@ -893,7 +939,7 @@ ssize_t fecgpu_decoder_add_repair(fecgpu_decoder *d, uint64_t win, uint16_t idx,
     if (w.S && w.S != len) return FECGPU_ERR_INVALID_ARG;
     if (!w.S) {
         // LENPREFIX: the repair length fixes S; sources received so far must fit
-        for (int j = 0; j < k; j++)
+        for (int j = 0; j < (w.nsrc ? w.nsrc : k); j++)
             if (((w.present >> j) & 1) && 2 + d->plen[(size_t)s * k + j] > len) return FECGPU_ERR_INVALID_ARG;
         w.S = (uint32_t)len;
     }
@@ -915,8 +961,57 @@ ssize_t fecgpu_decoder_tick(fecgpu_decoder *d, uint64_t now_us) {
     const uint64_t bt = d->policy.batch_timeout_us;
     if (bt && d->dirty && d->now - d->dirty_t >= bt) return fecgpu_decoder_flush(d);
     // an automatic flush that has finished by now is completed here
-    if (d->pending && hipEventQuery(d->done) != hipErrorNotReady) return dec_complete(d);
+    if (d->pending && hipEventQuery(d->done) != hipErrorNotReady) {
+        const ssize_t rc = dec_complete(d);
+        if (rc < 0) return rc;
+    }
+    return dec_take(d);
+}
+
+ssize_t fecgpu_decoder_set_window_sources(fecgpu_decoder *d, uint64_t win, uint16_t nsrc) {
+    if (!d || nsrc == 0 || nsrc > d->code.k) return FECGPU_ERR_INVALID_ARG;
+    uint32_t s = 0;
+    ssize_t rc = dec_slot(d, win, s);
+    if (rc) return rc;
+    if (dec_ready(d, s) < 0) return FECGPU_ERR_DEVICE;
+    DecSlot &w = d->slots[s];
+    const int k = d->code.k;
+    if (w.nsrc) return w.nsrc == nsrc ? 0 : FECGPU_ERR_INVALID_ARG;
+    if (nsrc == k) {
+        w.nsrc = nsrc;
+        return 0;
+    }
+    const uint64_t kmask = (k >= 64) ? ~0ull : (1ull << k) - 1;
+    const uint64_t pad = kmask & ~((1ull << nsrc) - 1);
+    if (w.present & pad) return FECGPU_ERR_INVALID_ARG;  // a source filed at a padding index
+    w.nsrc = nsrc;
+    w.present |= pad;
+    for (int j = nsrc; j < k; j++) d->plen[(size_t)s * k + j] = 0;
+    dec_touch(d, s);
     return 0;
+}
+
+ssize_t fecgpu_decoder_set_max_windows(fecgpu_decoder *d, uint64_t max_windows) {
+    if (!d) return FECGPU_ERR_INVALID_ARG;
+    d->max_windows = max_windows;
+    return 0;
+}
+
+ssize_t fecgpu_decoder_next_recovered(fecgpu_decoder *d, uint64_t *win, uint16_t *idx) {
+    if (!d || !win || !idx) return FECGPU_ERR_INVALID_ARG;
+    // a finished automatic flush contributes without the caller flushing
+    if (d->pending && hipEventQuery(d->done) != hipErrorNotReady && dec_complete(d) < 0)
+        return FECGPU_ERR_DEVICE;
+    while (!d->rec_q.empty()) {
+        const auto [w, j] = d->rec_q.front();
+        d->rec_q.pop_front();
+        auto it = d->map.find(w);
+        if (it == d->map.end() || !((d->slots[it->second].present >> j) & 1)) continue;  // released
+        *win = w;
+        *idx = j;
+        return 0;
+    }
+    return FECGPU_ERR_DONE;
 }
 
 ssize_t fecgpu_decoder_recovered(fecgpu_decoder *d, uint64_t win, uint16_t idx, uint8_t *out,
@@ -927,6 +1022,7 @@ ssize_t fecgpu_decoder_recovered(fecgpu_decoder *d, uint64_t win, uint16_t idx, 
     const uint32_t s = it->second;
     if (dec_ready(d, s) < 0) return FECGPU_ERR_DEVICE;
     if (!((d->slots[s].present >> idx) & 1)) return FECGPU_ERR_DONE;
+    if (d->slots[s].nsrc && idx >= d->slots[s].nsrc) return FECGPU_ERR_DONE;  // padding, not a packet
     const uint32_t n = d->plen[(size_t)s * d->code.k + idx];
     if (cap < n || (!out && n)) return FECGPU_ERR_BUFFER_TOO_SHORT;
     if (n) std::memcpy(out, dec_row(d, s, idx) + (is_lenprefix(d->code) ? 2 : 0), n);

@@ -5,10 +5,15 @@
 // own encoding, written in QUIC's idiom: every integer is a QUIC
 // variable-length integer (RFC 9000 §16) and a frame is
 //   SOURCE_ID: type | window | index
-//   REPAIR   : type | window | k | r | index | length | repair symbol bytes
-// with frame types in the reserved-for-extensions space.  A Connection puts a
-// SOURCE_ID frame next to each protected payload and carries repair symbols
-// in REPAIR frames; the receiver parses both and feeds fecgpu_decoder_*.
+//   REPAIR   : type | window | k | r | nsrc | index | length | repair symbol bytes
+// with frame types in the reserved-for-extensions space.  nsrc is the number
+// of real sources of the window (1..k): a window closed early (close_window,
+// window timeout) is padded with empty sources that never go on the wire, and
+// the receiver marks indices >= nsrc as present and empty
+// (fecgpu_decoder_set_window_sources) instead of counting them as lost.  A
+// Connection puts a SOURCE_ID frame next to each protected payload and carries
+// repair symbols in REPAIR frames; the receiver parses both and feeds
+// fecgpu_decoder_*.
 // Pure host code: no device calls.
 #include <cstring>
 
@@ -60,30 +65,33 @@ ssize_t fecgpu_frame_write_source_id(uint8_t *buf, size_t cap, uint64_t win, uin
     return (ssize_t)(p - buf);
 }
 
-ssize_t fecgpu_frame_repair_len(uint64_t win, uint16_t k, uint16_t r, uint16_t idx, size_t sym_len) {
+ssize_t fecgpu_frame_repair_len(uint64_t win, uint16_t k, uint16_t r, uint16_t nsrc, uint16_t idx,
+                                size_t sym_len) {
     return (ssize_t)(varint_len(FECGPU_FRAME_REPAIR) + varint_len(win) + varint_len(k) + varint_len(r) +
-                     varint_len(idx) + varint_len(sym_len) + sym_len);
+                     varint_len(nsrc) + varint_len(idx) + varint_len(sym_len) + sym_len);
 }
 
 ssize_t fecgpu_frame_write_repair_header(uint8_t *buf, size_t cap, uint64_t win, uint16_t k,
-                                         uint16_t r, uint16_t idx, size_t sym_len) {
-    if (!buf || win >= (1ull << 62) || idx >= r || k == 0 || r == 0 || sym_len >= (1ull << 62))
+                                         uint16_t r, uint16_t nsrc, uint16_t idx, size_t sym_len) {
+    if (!buf || win >= (1ull << 62) || idx >= r || k == 0 || r == 0 || nsrc == 0 || nsrc > k ||
+        sym_len >= (1ull << 62))
         return FECGPU_ERR_INVALID_ARG;
-    const size_t n = (size_t)fecgpu_frame_repair_len(win, k, r, idx, sym_len) - sym_len;
+    const size_t n = (size_t)fecgpu_frame_repair_len(win, k, r, nsrc, idx, sym_len) - sym_len;
     if (cap < n) return FECGPU_ERR_BUFFER_TOO_SHORT;
     uint8_t *p = varint_put(buf, FECGPU_FRAME_REPAIR);
     p = varint_put(p, win);
     p = varint_put(p, k);
     p = varint_put(p, r);
+    p = varint_put(p, nsrc);
     p = varint_put(p, idx);
     p = varint_put(p, sym_len);
     return (ssize_t)(p - buf);
 }
 
 ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16_t k, uint16_t r,
-                                  uint16_t idx, const uint8_t *sym, size_t sym_len) {
+                                  uint16_t nsrc, uint16_t idx, const uint8_t *sym, size_t sym_len) {
     if (!buf || (!sym && sym_len)) return FECGPU_ERR_INVALID_ARG;
-    const ssize_t h = fecgpu_frame_write_repair_header(buf, cap, win, k, r, idx, sym_len);
+    const ssize_t h = fecgpu_frame_write_repair_header(buf, cap, win, k, r, nsrc, idx, sym_len);
     if (h < 0) return h;
     if (cap - (size_t)h < sym_len) return FECGPU_ERR_BUFFER_TOO_SHORT;
     if (sym_len) std::memcpy(buf + h, sym, sym_len);
@@ -114,16 +122,19 @@ ssize_t fecgpu_frame_parse(const uint8_t *buf, size_t len, fecgpu_frame *out) {
         out->idx = (uint16_t)idx;
         return (ssize_t)pos;
     }
-    uint64_t k, r, idx, sl;
+    uint64_t k, r, nsrc, idx, sl;
     GET(k);
     GET(r);
+    GET(nsrc);
     GET(idx);
     GET(sl);
 #undef GET
-    if (k == 0 || r == 0 || k > 0xFFFF || r > 0xFFFF || idx >= r) return FECGPU_ERR_INVALID_ARG;
+    if (k == 0 || r == 0 || k > 0xFFFF || r > 0xFFFF || idx >= r || nsrc == 0 || nsrc > k)
+        return FECGPU_ERR_INVALID_ARG;
     if (sl > len - pos) return FECGPU_ERR_BUFFER_TOO_SHORT;
     out->k = (uint16_t)k;
     out->r = (uint16_t)r;
+    out->nsrc = (uint16_t)nsrc;
     out->idx = (uint16_t)idx;
     out->payload = buf + pos;
     out->payload_len = sl;

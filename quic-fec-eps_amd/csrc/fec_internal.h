@@ -81,9 +81,10 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
 // pointers the device can address (device memory or mapped pinned host
 // memory) on `s`, on the ctx's device; asynchronous.  Geometry fields of `a`
 // (win, win_off, sym_len, S_all, stride, off_stride, nwin, present, status)
-// are the caller's; the rest is filled in.
+// are the caller's; the rest is filled in.  dev: the device `s` belongs to
+// (-1: the ctx's first device).
 ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
-                     hipStream_t s, bool remote = false);
+                     hipStream_t s, bool remote = false, int dev = -1);
 hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s);
 
 // FECGPU_CHECK builds: symbol accesses outside their launch's ChkRange since

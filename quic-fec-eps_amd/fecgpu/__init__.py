@@ -25,7 +25,7 @@ LIB_PATH = os.environ.get("FECGPU_LIB") or os.path.join(os.path.dirname(_HERE), 
 
 # enums of include/fecgpu.h
 ERR_DONE, ERR_BUFFER_TOO_SHORT, ERR_INVALID_ARG = -1, -2, -3
-ERR_UNSUPPORTED, ERR_DEVICE, ERR_UNRECOVERABLE = -4, -5, -6
+ERR_UNSUPPORTED, ERR_DEVICE, ERR_UNRECOVERABLE, ERR_LIMIT = -4, -5, -6, -7
 SCHEME_XOR, SCHEME_GF256 = 0, 1
 MATRIX_CAUCHY, MATRIX_VANDERMONDE = 0, 1
 FRAMING_FIXED, FRAMING_LENPREFIX = 0, 1
@@ -48,8 +48,9 @@ EXPORTS = (
     "fecgpu_decoder_new", "fecgpu_decoder_free", "fecgpu_decoder_add_source",
     "fecgpu_decoder_add_repair", "fecgpu_decoder_flush", "fecgpu_decoder_flush_many",
     "fecgpu_encoder_flush_many",
-    "fecgpu_decoder_recovered",
-    "fecgpu_decoder_release",
+    "fecgpu_decoder_recovered", "fecgpu_decoder_next_recovered",
+    "fecgpu_decoder_release", "fecgpu_encoder_window_sources",
+    "fecgpu_decoder_set_window_sources", "fecgpu_decoder_set_max_windows",
     "fecgpu_encoder_set_policy", "fecgpu_encoder_tick", "fecgpu_decoder_set_policy",
     "fecgpu_decoder_tick",
     "fecgpu_frame_source_id_len", "fecgpu_frame_write_source_id", "fecgpu_frame_repair_len",
@@ -88,6 +89,7 @@ class fecgpu_frame(ctypes.Structure):
         ("idx", ctypes.c_uint16),
         ("payload", ctypes.c_void_p),
         ("payload_len", ctypes.c_size_t),
+        ("nsrc", ctypes.c_uint16),
     ]
 
 
@@ -153,19 +155,25 @@ def _lib():
             "fecgpu_encoder_flush_many": (sz, [ctypes.POINTER(vp), ctypes.c_size_t]),
             "fecgpu_decoder_recovered": (sz, [vp, u64, ctypes.c_uint16, vp, ctypes.c_size_t]),
             "fecgpu_decoder_release": (sz, [vp, u64]),
+            "fecgpu_decoder_next_recovered": (sz, [vp, ctypes.POINTER(ctypes.c_uint64),
+                                                   ctypes.POINTER(ctypes.c_uint16)]),
+            "fecgpu_encoder_window_sources": (sz, [vp, u64]),
+            "fecgpu_decoder_set_window_sources": (sz, [vp, u64, ctypes.c_uint16]),
+            "fecgpu_decoder_set_max_windows": (sz, [vp, u64]),
             "fecgpu_encoder_set_policy": (sz, [vp, ctypes.POINTER(_Policy)]),
             "fecgpu_encoder_tick": (sz, [vp, u64]),
             "fecgpu_decoder_set_policy": (sz, [vp, ctypes.POINTER(_Policy)]),
             "fecgpu_decoder_tick": (sz, [vp, u64]),
             "fecgpu_frame_source_id_len": (sz, [u64, ctypes.c_uint16]),
             "fecgpu_frame_write_source_id": (sz, [vp, ctypes.c_size_t, u64, ctypes.c_uint16]),
-            "fecgpu_frame_repair_len": (sz, [u64, ctypes.c_uint16, ctypes.c_uint16,
+            "fecgpu_frame_repair_len": (sz, [u64, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16,
                                              ctypes.c_uint16, ctypes.c_size_t]),
             "fecgpu_frame_write_repair": (sz, [vp, ctypes.c_size_t, u64, ctypes.c_uint16,
-                                               ctypes.c_uint16, ctypes.c_uint16, vp,
+                                               ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16, vp,
                                                ctypes.c_size_t]),
             "fecgpu_frame_write_repair_header": (sz, [vp, ctypes.c_size_t, u64, ctypes.c_uint16,
-                                                      ctypes.c_uint16, ctypes.c_uint16, ctypes.c_size_t]),
+                                                      ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16,
+                                                      ctypes.c_size_t]),
             "fecgpu_frame_parse": (sz, [vp, ctypes.c_size_t, ctypes.POINTER(fecgpu_frame)]),
         }
         for name, (res, args) in sigs.items():
@@ -370,6 +378,11 @@ class Encoder:
     def release(self, win: int) -> int:
         return _lib().fecgpu_encoder_release(self._h, win)
 
+    def window_sources(self, win: int) -> int | None:
+        """Real sources of closed window `win` (the REPAIR frame's nsrc), None if unknown."""
+        n = _lib().fecgpu_encoder_window_sources(self._h, win)
+        return None if n == ERR_DONE else _check(n, "fecgpu_encoder_window_sources")
+
     def set_policy(self, window_timeout_us: int = 0, batch_timeout_us: int = 0) -> None:
         p = _Policy(window_timeout_us, batch_timeout_us)
         _check(_lib().fecgpu_encoder_set_policy(self._h, ctypes.byref(p)), "fecgpu_encoder_set_policy")
@@ -419,6 +432,28 @@ class Decoder:
     def release(self, win: int) -> int:
         return _lib().fecgpu_decoder_release(self._h, win)
 
+    def set_window_sources(self, win: int, nsrc: int) -> int:
+        """A REPAIR frame's nsrc: sources nsrc..k-1 of `win` are padding, not losses."""
+        return _lib().fecgpu_decoder_set_window_sources(self._h, win, nsrc)
+
+    def set_max_windows(self, n: int) -> None:
+        _check(_lib().fecgpu_decoder_set_max_windows(self._h, n), "fecgpu_decoder_set_max_windows")
+
+    def next_recovered(self) -> tuple[int, int] | None:
+        """(win, idx) of the oldest recovered packet not yet returned, or None."""
+        w, i = ctypes.c_uint64(), ctypes.c_uint16()
+        rc = _lib().fecgpu_decoder_next_recovered(self._h, ctypes.byref(w), ctypes.byref(i))
+        if rc == ERR_DONE:
+            return None
+        _check(rc, "fecgpu_decoder_next_recovered")
+        return w.value, i.value
+
+    def drain_recovered(self) -> list[tuple[int, int]]:
+        out = []
+        while (x := self.next_recovered()) is not None:
+            out.append(x)
+        return out
+
     def set_policy(self, window_timeout_us: int = 0, batch_timeout_us: int = 0) -> None:
         p = _Policy(window_timeout_us, batch_timeout_us)
         _check(_lib().fecgpu_decoder_set_policy(self._h, ctypes.byref(p)), "fecgpu_decoder_set_policy")
@@ -461,20 +496,24 @@ def frame_source_id(win: int, idx: int) -> bytes:
     return buf.raw[:m]
 
 
-def frame_repair(win: int, k: int, r: int, idx: int, sym: bytes) -> bytes:
-    """REPAIR frame bytes (fecgpu_frame_write_repair)."""
-    n = _check(_lib().fecgpu_frame_repair_len(win, k, r, idx, len(sym)), "fecgpu_frame_repair_len")
+def frame_repair(win: int, k: int, r: int, idx: int, sym: bytes, nsrc: int | None = None) -> bytes:
+    """REPAIR frame bytes (fecgpu_frame_write_repair); nsrc = the window's real
+    sources (default k: a full window)."""
+    ns = k if nsrc is None else nsrc
+    n = _check(_lib().fecgpu_frame_repair_len(win, k, r, ns, idx, len(sym)), "fecgpu_frame_repair_len")
     buf = ctypes.create_string_buffer(n)
-    m = _check(_lib().fecgpu_frame_write_repair(buf, n, win, k, r, idx, sym, len(sym)),
+    m = _check(_lib().fecgpu_frame_write_repair(buf, n, win, k, r, ns, idx, sym, len(sym)),
                "fecgpu_frame_write_repair")
     return buf.raw[:m]
 
 
-def frame_repair_header(win: int, k: int, r: int, idx: int, sym_len: int) -> bytes:
+def frame_repair_header(win: int, k: int, r: int, idx: int, sym_len: int,
+                        nsrc: int | None = None) -> bytes:
     """REPAIR frame header without the symbol bytes (fecgpu_frame_write_repair_header):
     header + symbol == frame_repair(...), so the symbol can be sent from its own buffer."""
-    buf = ctypes.create_string_buffer(32)
-    m = _check(_lib().fecgpu_frame_write_repair_header(buf, 32, win, k, r, idx, sym_len),
+    buf = ctypes.create_string_buffer(40)
+    m = _check(_lib().fecgpu_frame_write_repair_header(buf, 40, win, k, r, k if nsrc is None else nsrc,
+                                                       idx, sym_len),
                "fecgpu_frame_write_repair_header")
     return buf.raw[:m]
 
@@ -487,7 +526,7 @@ def frame_parse(data: bytes):
     out = {"type": f.type, "win": f.win, "idx": f.idx}
     if f.type == FRAME_REPAIR:
         off = f.payload - ctypes.addressof(buf)
-        out.update(k=f.k, r=f.r, payload=bytes(data[off:off + f.payload_len]))
+        out.update(k=f.k, r=f.r, nsrc=f.nsrc, payload=bytes(data[off:off + f.payload_len]))
     return n, out
 
 

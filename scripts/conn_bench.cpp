@@ -105,9 +105,13 @@ int main(int argc, char **argv) {
     const uint64_t nw_max = (npk + k - 1) / k + 1;
     std::vector<uint8_t> reps(nw_max * (size_t)r * smax);
     std::vector<uint32_t> replen(nw_max * (size_t)r);
+    std::vector<uint16_t> wnsrc(nw_max);  // the REPAIR frames' nsrc (real sources per window)
     uint64_t w_sent = 0;  // windows whose repairs were read and released
     auto send_repairs = [&](uint64_t upto) {
         for (; w_sent < upto; w_sent++) {
+            const ssize_t ns = fecgpu_encoder_window_sources(enc, w_sent + 1);
+            CK(ns);
+            wnsrc[w_sent] = (uint16_t)ns;
             for (int i = 0; i < r; i++) {
                 const size_t s = w_sent * r + i;
                 ssize_t n = fecgpu_encoder_repair(enc, w_sent + 1, (uint16_t)i, &reps[s * smax], smax);
@@ -154,21 +158,19 @@ int main(int argc, char **argv) {
         }
         for (; w_done < upto; w_done++) (void)fecgpu_decoder_release(dec, w_done);
     };
-    // the sender's short last window: its padding sources are known-empty/zero
-    const int last_n = (int)pi[npk - 1] + 1;
-    std::vector<uint8_t> zpad(mtu, 0);
     // symbol events: (window, index); index < k source (packet number p), >= k repair
     struct Ev { uint64_t w; uint32_t i; size_t p; };
     std::vector<Ev> evs;
     auto feed = [&](const Ev &e) {
         ssize_t rc;
         if (e.i < (uint32_t)k) {
-            if (e.p == SIZE_MAX)
-                rc = fecgpu_decoder_add_source(dec, e.w, (uint16_t)e.i, zpad.data(), vary ? 0 : len[npk - 1]);
-            else
-                rc = fecgpu_decoder_add_source(dec, e.w, (uint16_t)e.i, &data[off[e.p]], len[e.p]);
+            rc = fecgpu_decoder_add_source(dec, e.w, (uint16_t)e.i, &data[off[e.p]], len[e.p]);
         } else {
             const size_t s = (e.w - w_first) * r + (e.i - k);
+            // a REPAIR frame of a window closed early names its real sources:
+            // the padding indices are not losses (fec_frame.cpp)
+            const uint16_t ns = wnsrc[e.w - w_first];
+            if (ns < k) CK(fecgpu_decoder_set_window_sources(dec, e.w, ns));
             rc = fecgpu_decoder_add_repair(dec, e.w, (uint16_t)(e.i - k), &reps[s * smax], replen[s]);
         }
         if (rc != FECGPU_ERR_DONE) CK(rc);  // DONE: a duplicate
@@ -180,8 +182,6 @@ int main(int argc, char **argv) {
         for (uint64_t w = w0; w < w1; w++) {
             for (; p < npk && pw[p] == w; p++)
                 if (!lost[p]) evs.push_back({w, pi[p], p});
-            if (w == w_last)
-                for (int i = last_n; i < k; i++) evs.push_back({w, (uint32_t)i, SIZE_MAX});
             for (int i = 0; i < r; i++)
                 if (!replost[(w - w_first) * r + i]) evs.push_back({w, (uint32_t)(k + i), 0});
         }

@@ -329,7 +329,8 @@ int main(int argc, char **argv) {
                         row = buf[b] + wl * wbytes + (size_t)i * stride;
                     } else {
                         const int ri = i - nsrc;
-                        hl = fecgpu_frame_write_repair_header(h, 32, w, (uint16_t)k, (uint16_t)r, (uint16_t)ri, L);
+                        hl = fecgpu_frame_write_repair_header(h, 32, w, (uint16_t)k, (uint16_t)r, (uint16_t)nsrc,
+                                                              (uint16_t)ri, L);
                         row = buf[b] + wl * wbytes + (size_t)(k + ri) * stride;
                     }
                     CK(hl);
@@ -379,10 +380,6 @@ int main(int argc, char **argv) {
                 (void)fecgpu_decoder_release(dec, w_next);
             }
         };
-        // the short last window's padding sources are known to be empty
-        const int last_n = (int)(npk - (nwin - 1) * k);
-        std::vector<uint8_t> zero(L, 0);
-        for (int i = last_n; i < k; i++) CK(fecgpu_decoder_add_source(dec, nwin, (uint16_t)i, zero.data(), L));
         bool fin = false;
         for (;;) {
             if (fin && enc_done.load(std::memory_order_acquire) && got == enc_sent.load(std::memory_order_acquire)) break;
@@ -409,6 +406,9 @@ int main(int argc, char **argv) {
                     CK(fecgpu_decoder_add_source(dec, f.win, f.idx, d + h, L));
                     slot(f.win, f.idx) = 1;
                 } else {
+                    // the short last window's REPAIR frames carry nsrc < k: its
+                    // padding sources never go on the wire and are not losses
+                    if (f.nsrc < k) CK(fecgpu_decoder_set_window_sources(dec, f.win, f.nsrc));
                     CK(fecgpu_decoder_add_repair(dec, f.win, f.idx, f.payload, f.payload_len));
                 }
                 w_max = std::max<uint64_t>(w_max, f.win);

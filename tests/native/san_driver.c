@@ -52,7 +52,7 @@ static void frames(void) {
     for (size_t i = 0; i < sizeof sym; i++) sym[i] = (uint8_t)next();
     for (size_t w = 0; w < sizeof wins / sizeof wins[0]; w++) {
         for (size_t len = 0; len < sizeof sym; len += 97) {
-            ssize_t m = fecgpu_frame_write_repair(buf, sizeof buf, wins[w], 32, 8, 5, sym, len);
+            ssize_t m = fecgpu_frame_write_repair(buf, sizeof buf, wins[w], 32, 8, 17, 5, sym, len);
             CHECK(m > 0);
             for (ssize_t cut = 0; cut <= m; cut++) {
                 /* a heap copy of exactly `cut` bytes: the parser may not read past it */
@@ -61,7 +61,7 @@ static void frames(void) {
                 fecgpu_frame f;
                 ssize_t rc = fecgpu_frame_parse(t, (size_t)cut, &f);
                 if (cut < m) CHECK(rc < 0);
-                else CHECK(rc == m && f.win == wins[w] && f.payload_len == len &&
+                else CHECK(rc == m && f.win == wins[w] && f.nsrc == 17 && f.payload_len == len &&
                            !memcmp(f.payload, sym, len));
                 free(t);
             }

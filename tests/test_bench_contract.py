@@ -55,3 +55,45 @@ def test_cfg2_traffic_close_to_algorithmic(bench):
     t, _ = bench.pmc_traffic(2, "encode")
     alg = 65536 * 10 * 1200
     assert 1.0 <= t / alg < 1.1
+
+
+def test_gpus_flag_launches_n_ranks(bench):
+    """`python bench.py --gpus N` (the driver's form, no launcher) must
+    run N ranks, one per GPU.  On this GPU-less host the ranks stop at the first
+    device call, but both must have started with WORLD_SIZE = 2."""
+    import subprocess
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "1", "--dist-backend", "gloo", "--cpu-seconds", "0"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert "launching 2 ranks" in r.stderr
+    assert "rank 0/2" in r.stderr and "rank 1/2" in r.stderr, r.stderr[-3000:]
+
+
+def test_gpus_flag_refuses_without_enough_gpus(bench):
+    """RCCL runs one rank per GPU: --gpus 4 with fewer visible GPUs is an error,
+    not a run on GPU 0 labelled n_gpus 4."""
+    import subprocess
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 2 and "needs 4 GPUs" in r.stderr
+
+
+def test_world_size_must_match_gpus(bench):
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 2 and "refusing" in r.stderr
+
+
+def test_host_share_bounds_threads(bench, monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.host_share() == min(3, len(os.sched_getaffinity(0)))
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.host_share() == len(os.sched_getaffinity(0))

@@ -33,8 +33,32 @@ def test_repair_round_trip(sym_len):
     n, f = fecgpu.frame_parse(b)
     assert n == len(b)
     assert f["type"] == fecgpu.FRAME_REPAIR and f["win"] == 123456
-    assert (f["k"], f["r"], f["idx"]) == (32, 8, 7)
+    assert (f["k"], f["r"], f["idx"], f["nsrc"]) == (32, 8, 7, 32)
     assert f["payload"] == sym
+
+
+@pytest.mark.parametrize("nsrc", [1, 5, 31, 32])
+def test_repair_nsrc_round_trip(nsrc):
+    """A window closed early carries its real source count (padding
+    sources are not on the wire, so the receiver must learn which indices exist)."""
+    b = fecgpu.frame_repair(77, 32, 8, 2, b"abc", nsrc=nsrc)
+    n, f = fecgpu.frame_parse(b)
+    assert n == len(b) and f["nsrc"] == nsrc and f["payload"] == b"abc"
+    # layout: type(4) | win(2: 77 >= 64) | k | r | nsrc | idx | len | bytes, all varints
+    assert b[4:6] == bytes([0x40, 77]) and b[6:11] == bytes([32, 8, nsrc, 2, 3])
+
+
+@pytest.mark.parametrize("nsrc", [0, 33])
+def test_repair_nsrc_out_of_range(nsrc):
+    with pytest.raises(fecgpu.FecError) as e:
+        fecgpu.frame_repair(1, 32, 8, 0, b"x", nsrc=nsrc)
+    assert e.value.code == fecgpu.ERR_INVALID_ARG
+    # and a parsed frame with nsrc > k is rejected
+    good = fecgpu.frame_repair(1, 32, 8, 0, b"x", nsrc=32)
+    bad = good[:7] + bytes([33]) + good[8:]
+    with pytest.raises(fecgpu.FecError) as e:
+        fecgpu.frame_parse(bad)
+    assert e.value.code == fecgpu.ERR_INVALID_ARG
 
 
 @pytest.mark.parametrize("win,sym_len", [(0, 0), (1, 1200), (70000, 9002), ((1 << 62) - 1, 70000)])
@@ -53,7 +77,7 @@ def test_repair_header_errors():
     with pytest.raises(fecgpu.FecError):
         fecgpu.frame_repair_header(1 << 62, 16, 4, 0, 10)
     buf = fecgpu.ctypes.create_string_buffer(4)
-    assert fecgpu._lib().fecgpu_frame_write_repair_header(buf, 4, 1, 16, 4, 0, 1200) == -2
+    assert fecgpu._lib().fecgpu_frame_write_repair_header(buf, 4, 1, 16, 4, 16, 0, 1200) == -2
 
 
 def test_parse_errors():

@@ -292,3 +292,38 @@ def test_release_build_has_no_checker():
         assert e.value.code == fecgpu.ERR_UNSUPPORTED
     finally:
         ctx.close()
+
+
+def test_checked_encoder_failed_launch_recovers(chk):
+    """when the launch of a full batch fails, the encoder must not file
+    the next source past the end of that batch.  check_shrink makes the launch fail
+    (bounds check); add_source retries it and keeps failing without writing out of
+    bounds; once the checker is relaxed the same batch launches and every repair
+    matches the oracle."""
+    import np_oracle as N
+    m, ctx = chk
+    code = m.Code("gf256", 4, 2, "fixed")
+    pk = [bytes([(13 * n + t) & 0xFF for t in range(256)]) for n in range(16)]
+    enc = m.Encoder(ctx, code, max_len=256, batch=2)
+    for p in pk[:4]:
+        enc.add_source(p)                           # window 0 closed, batch not full
+    ctx.set_tuning("check_shrink", 16)
+    try:
+        for p in pk[4:7]:
+            enc.add_source(p)
+        with pytest.raises(m.FecError, match="bounds check"):
+            enc.add_source(pk[7])                   # closes window 1: the launch fails
+        for _ in range(3):                          # retried, never filed past the batch
+            with pytest.raises(m.FecError, match="bounds check"):
+                enc.add_source(pk[8])
+        assert enc.repair(0, 0) is None             # not encoded
+    finally:
+        ctx.set_tuning("check_shrink", 0)
+    assert enc.add_source(pk[8]) == (2, 0)          # launches batch 0, starts window 2
+    for p in pk[9:12]:
+        enc.add_source(p)
+    enc.flush()
+    for w in range(3):
+        ref = N.encode("gf", 4, 2, np.frombuffer(b"".join(pk[4 * w:4 * w + 4]), np.uint8).reshape(4, 256))
+        assert [enc.repair(w, i) for i in range(2)] == [ref[i].tobytes() for i in range(2)], w
+    enc.close()

@@ -528,10 +528,12 @@ def test_synth_erasure_digest_vs_oracle(ctx, cfgid):
 
 
 # --------------------------------------------------- full BASELINE sizes ---
-@pytest.mark.parametrize("cfgid,nwin", [(2, 65536), (3, 262144), (4, 16384)])
+@pytest.mark.parametrize("cfgid,nwin", [(2, 65536), (3, 262144), (4, 131072)])
 def test_full_size_roundtrip(ctx, cfgid, nwin):
     """Every window: encode -> poison erased -> decode == original sources, status as
-    predicted from the masks; 32 sampled windows bit-exact vs the oracle."""
+    predicted from the masks; 64 sampled windows bit-exact vs the oracle.  cfg4 runs
+    its real per-GPU shard (1M windows / 8 GPUs = 131,072 windows, 47 GB + a 38 GB
+    saved copy of the sources in HBM)."""
     cfg = WL.CONFIGS[cfgid]
     b = WL.Batch.allocate(cfg, nwin, torch.device("cuda"))
     b.synthesize(ctx, 0)
@@ -539,7 +541,7 @@ def test_full_size_roundtrip(ctx, cfgid, nwin):
     b.encode(ctx)
     torch.cuda.synchronize()
     rng = np.random.default_rng(cfgid)
-    sample = np.sort(rng.choice(nwin, 32, replace=False))
+    sample = np.sort(rng.choice(nwin, 64, replace=False))
     enc = b.view[torch.from_numpy(sample).cuda()].cpu().numpy()
     res = b.verify(ctx, 0)
     assert res["ok"], res
