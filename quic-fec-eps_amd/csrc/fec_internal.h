@@ -71,9 +71,14 @@ struct LaunchPlan {
 // GF encode of (k, r, matrix) has a compiled bit-sliced kernel.
 bool bitslice_supported(int k, int r, int matrix);
 
-// Per-window LDS region of the GF decode kernel: tables [k][R] uint4 + [k][R] u32,
-// input symbol list (64 B), output symbol list (16 B).
-inline uint32_t gf_dec_win_lds(int k, int R) { return (uint32_t)(k * R * 20 + 80 + 15) & ~15u; }
+// Per-window LDS region of the GF decode kernel (fec_kernels.hip DecRegion):
+// tables [k][R] uint4 (TA/TB) + [k][round_up(R, 4)] u32 (TC), input row byte
+// offsets [round_up(k, 8)] u32, output row byte offsets [8] u32, input symbol
+// list (64 B), output symbol list (16 B).
+inline uint32_t gf_dec_win_lds(int k, int R) {
+    const uint32_t r4 = (uint32_t)(R + 3) & ~3u, k8 = (uint32_t)(k + 7) & ~7u;
+    return ((uint32_t)k * R * 16 + (uint32_t)k * r4 * 4 + k8 * 4 + 32 + 80 + 15) & ~15u;
+}
 
 hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s);
 

@@ -939,6 +939,43 @@ __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
     }
 }
 
+// Per-window LDS region of the GF decode (size: gf_dec_win_lds).  The decode
+// matrix D (e x k, entry [u][q] = coefficient of input q in missing source u)
+// as multiply tables: ab[q][u] (TA/TB, one ds_read_b128) and tc[q][u] (TC,
+// rows padded to 4 so a row's TC entries are one ds_read_b128).  roff[q] is
+// input q's row offset in the window (received sources ascending, then the
+// chosen repairs; padded with row 0, so a load batch never clamps), ooff[u]
+// the output row of missing source u.  Entries for u >= e are stale: they
+// feed only accumulators that are never stored.
+template <int R>
+struct DecRegion {
+    static constexpr int R4 = (R + 3) & ~3;
+    uint4 *ab;
+    uint32_t *tc, *roff, *ooff;
+    uint8_t *insym, *outsym;
+    __device__ __forceinline__ DecRegion(uint8_t *region, int k) {
+        ab = reinterpret_cast<uint4 *>(region);
+        tc = reinterpret_cast<uint32_t *>(region + k * R * 16);
+        roff = tc + k * R4;
+        ooff = roff + ((k + 7) & ~7);
+        insym = reinterpret_cast<uint8_t *>(ooff + 8);
+        outsym = insym + 64;
+    }
+};
+
+// Row offsets of a planned window from its symbol lists (every lane of the
+// wave; the lists were written before the plan's last wave sync).
+template <int R>
+__device__ __forceinline__ void plan_offsets(const BatchArgs &a, uint64_t w, int lane,
+                                             const DecRegion<R> &rg, int e) {
+    uint64_t base;
+    uint32_t stride, S;
+    win_geom(a, w, base, stride, S);
+    const int k = a.k;
+    if (lane < ((k + 7) & ~7)) rg.roff[lane] = lane < k ? (uint32_t)rg.insym[lane] * stride : 0u;
+    if (lane < 8) rg.ooff[lane] = lane < e ? (uint32_t)rg.outsym[lane] * stride : 0u;
+}
+
 // GF plan (a6/a7) by one wave, closed form.  Missing sources m_0..m_{e-1},
 // the first e present repairs with points x_t = k + sel_t; the system is the
 // Cauchy matrix A[t][u] = 1/(x_t ^ m_u).  Its inverse folded
@@ -955,10 +992,8 @@ template <int R>
 __device__ void plan_gf(const BatchArgs &a, uint64_t w, uint64_t pres, int lane, uint8_t *region,
                         const uint8_t *ex, const uint8_t *lg, uint8_t &ne_out) {
     const int k = a.k, r = a.r;
-    uint4 *tab = reinterpret_cast<uint4 *>(region);
-    uint32_t *tc = reinterpret_cast<uint32_t *>(region + k * R * 16);
-    uint8_t *insym = region + k * R * 20;
-    uint8_t *outsym = insym + 64;
+    const DecRegion<R> rg(region, k);
+    uint8_t *insym = rg.insym, *outsym = rg.outsym;
     const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
     const uint64_t miss = ~pres & kmask;
     const uint64_t rep = (pres >> k) & ((1ull << r) - 1);
@@ -1017,10 +1052,11 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, uint64_t pres, int lane,
         if (idx < e * k) {
             const int lgd = Au + Kq - (int)lg[(z ^ mu) & 255] + 255 * 4 * kMaxR;
             const CoefTab ct = make_coef_tab(ex[lgd % 255]);
-            tab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
-            tc[dq * R + du] = ct.c;
+            rg.ab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+            rg.tc[dq * DecRegion<R>::R4 + du] = ct.c;
         }
     }
+    plan_offsets<R>(a, w, lane, rg, e);
     if (lane == 0) {
         ne_out = (uint8_t)e;
         a.status[w] = 0;
@@ -1040,10 +1076,8 @@ template <int R>
 __device__ void plan_gf_gj(const BatchArgs &a, uint64_t w, int lane, uint8_t *region,
                            const uint8_t *ex, const uint8_t *lg, uint8_t &ne_out) {
     const int k = a.k, r = a.r;
-    uint4 *tab = reinterpret_cast<uint4 *>(region);
-    uint32_t *tc = reinterpret_cast<uint32_t *>(region + k * R * 16);
-    uint8_t *insym = region + k * R * 20;
-    uint8_t *outsym = insym + 64;
+    const DecRegion<R> rg(region, k);
+    uint8_t *insym = rg.insym, *outsym = rg.outsym;
     const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
     const uint64_t pres = a.present[w];
     const uint64_t miss = ~pres & kmask;
@@ -1116,10 +1150,11 @@ __device__ void plan_gf_gj(const BatchArgs &a, uint64_t w, int lane, uint8_t *re
         const uint32_t c = is_src ? csrc : crep;
         if (live) {
             const CoefTab ct = make_coef_tab(c);
-            tab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
-            tc[dq * R + du] = ct.c;
+            rg.ab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+            rg.tc[dq * DecRegion<R>::R4 + du] = ct.c;
         }
     }
+    plan_offsets<R>(a, w, lane, rg, e);
     if (lane == 0) {
         ne_out = (uint8_t)e;
         a.status[w] = 0;
@@ -1135,10 +1170,8 @@ template <int R>
 __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int lane, uint8_t *region,
                             const uint8_t *ex, const uint8_t *lg, const uint8_t *P, uint8_t &ne_out) {
     const int k = a.k, r = a.r;
-    uint4 *tab = reinterpret_cast<uint4 *>(region);
-    uint32_t *tc = reinterpret_cast<uint32_t *>(region + k * R * 16);
-    uint8_t *insym = region + k * R * 20;
-    uint8_t *outsym = insym + 64;
+    const DecRegion<R> rg(region, k);
+    uint8_t *insym = rg.insym, *outsym = rg.outsym;
     const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
     const uint64_t miss = ~pres & kmask;
     const uint64_t rep = (pres >> k) & ((1ull << r) - 1);
@@ -1206,13 +1239,87 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
         const uint32_t c = is_src ? csrc : crep;
         if (live) {
             const CoefTab ct = make_coef_tab(c);
-            tab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
-            tc[dq * R + du] = ct.c;
+            rg.ab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+            rg.tc[dq * DecRegion<R>::R4 + du] = ct.c;
         }
     }
+    plan_offsets<R>(a, w, lane, rg, e);
     if (lane == 0) {
         ne_out = (uint8_t)e;
         a.status[w] = 0;
+    }
+}
+
+// GF decode of one slot for NE outputs (wave-uniform): acc[u] = sum_q D[u][q]
+// * in_q over the k inputs, U rows loaded per batch; output u is stored when
+// u < ne (this lane's window).
+template <int R, int NE>
+__device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t out_delta,
+                                         const DecRegion<R> &rg) {
+    constexpr int U = FECGPU_GFD_U, R4 = DecRegion<R>::R4;
+    static_assert(U == 4 || U == 8, "row offsets are read 4 at a time, padded to 8 rows");
+    uint4 acc[NE];
+#pragma unroll
+    for (int m = 0; m < NE; m++) acc[m] = zero4();
+    for (int q0 = 0; q0 < k; q0 += U) {
+        uint4 v[U];
+        uint32_t ro[U];
+#pragma unroll
+        for (int t = 0; t < U; t += 4) {  // roff is padded to a multiple of 8 rows
+            const uint4 o = *reinterpret_cast<const uint4 *>(rg.roff + q0 + t);
+            ro[t] = o.x; ro[t + 1] = o.y; ro[t + 2] = o.z; ro[t + 3] = o.w;
+        }
+#pragma unroll
+        for (int t = 0; t < U; t++) v[t] = ld16(base + ro[t]);
+        int t0 = 0;
+#if GF_PAIR_DEC
+#pragma unroll
+        for (int t = 0; t + 1 < U; t += 2) {
+            if (q0 + t + 1 < k) {
+                const Split s0 = split(v[t]), s1 = split(v[t + 1]);
+                const int q = q0 + t;
+                uint32_t c0[R4], c1[R4];
+#pragma unroll
+                for (int j = 0; j < (NE + 3) / 4; j++) {
+                    const uint4 x = *reinterpret_cast<const uint4 *>(rg.tc + q * R4 + 4 * j);
+                    const uint4 y = *reinterpret_cast<const uint4 *>(rg.tc + (q + 1) * R4 + 4 * j);
+                    c0[4 * j] = x.x; c0[4 * j + 1] = x.y; c0[4 * j + 2] = x.z; c0[4 * j + 3] = x.w;
+                    c1[4 * j] = y.x; c1[4 * j + 1] = y.y; c1[4 * j + 2] = y.z; c1[4 * j + 3] = y.w;
+                }
+#pragma unroll
+                for (int m = 0; m < NE; m++)
+                    gmac2(acc[m], s0, s1, rg.ab[q * R + m], c0[m], rg.ab[(q + 1) * R + m], c1[m]);
+                t0 = t + 2;
+            }
+        }
+#endif
+#pragma unroll
+        for (int t = 0; t < U; t++) {
+            if (t >= t0 && q0 + t < k) {
+                const int q = q0 + t;
+                const Split sp = split(v[t]);
+                uint32_t c[R4];
+#pragma unroll
+                for (int j = 0; j < (NE + 3) / 4; j++) {
+                    const uint4 x = *reinterpret_cast<const uint4 *>(rg.tc + q * R4 + 4 * j);
+                    c[4 * j] = x.x; c[4 * j + 1] = x.y; c[4 * j + 2] = x.z; c[4 * j + 3] = x.w;
+                }
+#pragma unroll
+                for (int m = 0; m < NE; m++) gmac(acc[m], sp, rg.ab[q * R + m], c[m]);
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < NE; m++)
+        if (m < ne) st16(base + out_delta + rg.ooff[m], acc[m]);
+}
+
+template <int R, int NE = R>
+__device__ __forceinline__ void dec_dispatch(int nw, uint8_t *base, int k, int ne, uint64_t out_delta,
+                                             const DecRegion<R> &rg) {
+    if constexpr (NE >= 1) {
+        if (nw == NE) dec_slot<R, NE>(base, k, ne, out_delta, rg);
+        else dec_dispatch<R, NE - 1>(nw, base, k, ne, out_delta, rg);
     }
 }
 
@@ -1224,8 +1331,8 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
     __shared__ uint8_t s_log[256];
     __shared__ GroupLds g;
     __shared__ uint8_t s_ne[kMaxWpb];
+    __shared__ uint8_t s_perm[kMaxWpb];        // group windows, descending e
     __shared__ uint8_t s_coef[kMaxR * kMaxK];  // general-matrix codes: parity rows P[r][k]
-    constexpr int U = FECGPU_GFD_U;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
     uint8_t *regions = reinterpret_cast<uint8_t *>(dyn);
     for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
@@ -1261,25 +1368,40 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
         }
 #endif
         __syncthreads();
-        if (tid < 64) block_prefix(g.pfx, (tid < nb && s_ne[tid]) ? g.ncol[tid] : 0u, tid);
+        if (tid < 64) {
+            // Windows in descending order of e (ties by index): a wave's first
+            // active lane then holds the largest e among its lanes, so the
+            // multiply runs for that many outputs, wave-uniform (no per-product
+            // exec masking); lanes of windows with smaller e accumulate extra
+            // outputs from stale table rows and do not store them.
+            const int t = tid;
+            const int ne_t = t < nb ? (int)s_ne[t] : -1;
+            const uint64_t below = (1ull << t) - 1;
+            int rank = 0;
+#pragma unroll
+            for (int v = R; v >= 0; v--) {
+                const uint64_t b = __ballot(ne_t == v);  // whole wave active
+                if (v > ne_t) rank += __popcll(b);
+                else if (v == ne_t) rank += __popcll(b & below);
+            }
+            if (t < nb) s_perm[rank] = (uint8_t)t;
+            WAVE_SYNC();
+            const int wl = t < nb ? (int)s_perm[t] : 0;
+            block_prefix(g.pfx, (t < nb && s_ne[wl]) ? g.ncol[wl] : 0u, t);
+        }
         __syncthreads();
         if (FECGPU_DEC_PLANONLY) continue;
-        for_group_slots(g, nb, [&](uint8_t *base, uint32_t stride, int wl, bool valid) {
-            const int ne = valid ? (int)s_ne[wl] : 0;
-            const uint8_t *region = regions + (size_t)wl * a.win_lds;
-            const uint4 *tab = reinterpret_cast<const uint4 *>(region);
-            const uint32_t *tc = reinterpret_cast<const uint32_t *>(region + k * R * 16);
-            const uint8_t *insym = region + k * R * 20;
-            const uint8_t *outsym = insym + 64;
-            uint4 acc[R];
-#pragma unroll
-            for (int m = 0; m < R; m++) acc[m] = zero4();
-            gf_mac_pipelined<R, U, GF_PAIR_DEC>(acc, k, ne,
-                                   [&](int q) { return base + (uint32_t)insym[q] * stride; }, tab, tc);
-#pragma unroll
-            for (int m = 0; m < R; m++)
-                if (m < ne) st16(base + a.out_delta + (size_t)outsym[m] * stride, acc[m]);
-        });
+        const uint32_t total = g.pfx[nb];
+        int i = 0;
+        for (uint32_t s = tid; s < total; s += kBlock) {
+            while (s >= g.pfx[i + 1]) i++;
+            const int wl = s_perm[i];
+            const int ne = s_ne[wl];
+            const int nw = __builtin_amdgcn_readfirstlane(ne);  // max e over the wave's lanes
+            uint8_t *base = reinterpret_cast<uint8_t *>(g.base[wl]) + (s - g.pfx[i]) * 16u;
+            const DecRegion<R> rg(regions + (size_t)wl * a.win_lds, k);
+            dec_dispatch<R>(nw, base, k, ne, a.out_delta, rg);
+        }
         __syncthreads();
     }
 }
