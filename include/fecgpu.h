@@ -47,7 +47,8 @@
 extern "C" {
 #endif
 
-#define FECGPU_ABI_VERSION 2  /* 2: REPAIR frames carry nsrc; decoder limits / recovered queue */
+#define FECGPU_ABI_VERSION 3  /* 2: REPAIR frames carry nsrc; decoder limits / recovered queue;
+                                 3: fecgpu_code.rlc_key / rlc_dt, FECGPU_MATRIX_RLC */
 
 /* errors (mirror quiche's QUICHE_ERR_DONE = -1, QUICHE_ERR_BUFFER_TOO_SHORT = -2 style) */
 enum fecgpu_error {
@@ -64,8 +65,14 @@ enum fecgpu_scheme { FECGPU_SCHEME_XOR = 0, FECGPU_SCHEME_GF256 = 1 };
 /* GF(2^8) parity rows: CAUCHY C[i][j] = inv((k+i) ^ j) (ISA-L cauchy1 layout);
  * VANDERMONDE = rows k.. of V * inv(V[0..k)), V[i][j] = i^j (points 0..k+r-1):
  * the systematic matrix of Backblaze JavaReedSolomon, klauspost/reedsolomon
- * and the Rust crate reed-solomon-erasure. */
-enum fecgpu_matrix { FECGPU_MATRIX_CAUCHY = 0, FECGPU_MATRIX_VANDERMONDE = 1 };
+ * and the Rust crate reed-solomon-erasure.
+ * RLC = random linear code of RFC 8681 (Sliding Window RLC FEC schemes, m = 8)
+ * in block form: parity row i holds the coefficients that RFC 8681 §3.6
+ * generate_coding_coefficients(repair_key = rlc_key + i, cc_nb = k, dt =
+ * rlc_dt) draws from the RFC 8682 TinyMT32 PRNG.  Not MDS: a window whose
+ * present repairs leave the missing sources' system singular is reported
+ * unrecoverable (decode uses every present repair, pivoting). */
+enum fecgpu_matrix { FECGPU_MATRIX_CAUCHY = 0, FECGPU_MATRIX_VANDERMONDE = 1, FECGPU_MATRIX_RLC = 2 };
 enum fecgpu_framing { FECGPU_FRAMING_FIXED = 0, FECGPU_FRAMING_LENPREFIX = 1 };
 
 /* per-window decode status */
@@ -85,6 +92,10 @@ typedef struct fecgpu_code {
     uint16_t k;       /* source symbols per window, 1..64 */
     uint16_t r;       /* repair symbols per window, 1..8, k + r <= 64, XOR: r <= k */
     uint32_t poly;    /* field polynomial, 0x11D (0 = default) */
+    uint16_t rlc_key; /* MATRIX_RLC: repair_key of parity row 0 (row i: rlc_key + i mod 2^16) */
+    uint8_t rlc_dt;   /* MATRIX_RLC: RFC 8681 density threshold DT, 0..15 (15 = dense:
+                         every coefficient nonzero; else nonzero w.p. (DT + 1) / 16) */
+    uint8_t reserved; /* 0 */
 } fecgpu_code;
 
 typedef struct fecgpu_ctx fecgpu_ctx;
@@ -95,6 +106,10 @@ const char *fecgpu_strerror(ssize_t err);
 const char *fecgpu_last_error(void);
 /* 0 if the code is valid and supported, else a negative error */
 ssize_t     fecgpu_code_check(const fecgpu_code *code);
+/* The code's parity rows P[i*k + j] (i < r, j < k: repair i = sum_j P[i][j] *
+ * source j over GF(2^8); XOR: 1 where j mod r == i) into out[0 .. r*k).  Host
+ * only, no device.  Returns r*k, or BUFFER_TOO_SHORT / the code_check error. */
+ssize_t     fecgpu_code_parity_rows(const fecgpu_code *code, uint8_t *out, size_t cap);
 
 /* ctx over devs[0..ndev-1] (NULL/0 = current device).  Batches with device
  * pointers run on the current device (the one the pointers live on);

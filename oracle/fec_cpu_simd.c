@@ -264,13 +264,10 @@ static int decode_window(int level, int scheme, int k, int r, const uint8_t *C, 
         }
         return status;
     }
-    int miss[64], sel[8], e = 0, nrep = 0;
-    for (int j = 0; j < k; j++)
-        if (!((present >> j) & 1)) miss[e++] = j;
+    int miss[64], sel[64];
+    const int e = orc_select_rows(k, r, C, present, miss, sel);
     if (e == 0) return ORC_OK;
-    for (int i = 0; i < r && nrep < e; i++)
-        if ((present >> (k + i)) & 1) sel[nrep++] = i;
-    if (nrep < e || e > 8) return ORC_UNRECOVERABLE;
+    if (e < 0 || e > 8) return ORC_UNRECOVERABLE;
     /* A[t][u] = C[sel_t][miss_u]; recovered_u = sum_t Ainv[u][t] (R_sel_t + sum_j C[sel_t][j] S_j)
      * folded into one dot product over the k inputs (received sources, chosen repairs) */
     uint8_t A[64], Ai[64];

@@ -118,10 +118,115 @@ void orc_vandermonde(int k, int r, uint8_t *P) {
         }
 }
 
-/* parity rows of the scheme's generator (GF schemes) */
+/* RFC 8682 TinyMT32, parameter set mat1 = 0x8f7011ee, mat2 = 0xfc78ff1f,
+ * tmat = 0x3793fdff, restated from the RFC's reference code (tinymt32_init,
+ * next_state, temper).  Pinned by the RFC's seed-1 output list
+ * (tests/test_rlc_spec.py).  FECGPU_MATRIX_RLC, SURVEY.md Appendix A.2
+ * "seeded RLC" / Appendix B q6. */
+typedef struct { uint32_t st[4]; } tmt_t;
+
+static void tmt_next(tmt_t *t) {
+    uint32_t y = t->st[3];
+    uint32_t x = (t->st[0] & 0x7fffffffu) ^ t->st[1] ^ t->st[2];
+    x ^= x << 1;
+    y ^= (y >> 1) ^ x;
+    t->st[0] = t->st[1];
+    t->st[1] = t->st[2];
+    t->st[2] = x ^ (y << 10);
+    t->st[3] = y;
+    if (y & 1) {
+        t->st[1] ^= 0x8f7011eeu;
+        t->st[2] ^= 0xfc78ff1fu;
+    }
+}
+
+static uint32_t tmt_u32(tmt_t *t) {
+    tmt_next(t);
+    uint32_t t0 = t->st[3];
+    uint32_t t1 = t->st[0] + (t->st[2] >> 8);
+    t0 ^= t1;
+    if (t1 & 1) t0 ^= 0x3793fdffu;
+    return t0;
+}
+
+static void tmt_init(tmt_t *t, uint32_t seed) {
+    t->st[0] = seed;
+    t->st[1] = 0x8f7011eeu;
+    t->st[2] = 0xfc78ff1fu;
+    t->st[3] = 0x3793fdffu;
+    for (uint32_t i = 1; i < 8; i++)
+        t->st[i & 3] ^= i + 1812433253u * (t->st[(i - 1) & 3] ^ (t->st[(i - 1) & 3] >> 30));
+    if ((t->st[0] & 0x7fffffffu) == 0 && t->st[1] == 0 && t->st[2] == 0 && t->st[3] == 0) {
+        t->st[0] = 'T'; t->st[1] = 'I'; t->st[2] = 'N'; t->st[3] = 'Y';
+    }
+    for (int i = 0; i < 8; i++) tmt_next(t);
+}
+
+void orc_tinymt32(uint32_t seed, int n, uint32_t *out) {
+    tmt_t t;
+    tmt_init(&t, seed);
+    for (int i = 0; i < n; i++) out[i] = tmt_u32(&t);
+}
+
+/* RFC 8681 §3.6 generate_coding_coefficients() for m = 8: rand16() = u32 &
+ * 0xF, rand256() = u32 & 0xFF; dt = 15: every coefficient a nonzero
+ * rand256(); else coefficient i is nonzero iff rand16() <= dt. */
+int orc_rlc_coefs(uint32_t key, int n, int dt, uint8_t *cc) {
+    if (dt < 0 || dt > 15) return -1;
+    tmt_t t;
+    tmt_init(&t, key & 0xFFFFu);
+    for (int i = 0; i < n; i++) {
+        cc[i] = 0;
+        if (dt == 15 || (int)(tmt_u32(&t) & 0xFu) <= dt) {
+            do cc[i] = (uint8_t)(tmt_u32(&t) & 0xFFu); while (cc[i] == 0);
+        }
+    }
+    return 0;
+}
+
+/* parity rows of the scheme's generator (GF schemes); RLC: row i from
+ * repair_key key0 + i (ORC_RLC(key0, dt)) */
 void orc_matrix(int scheme, int k, int r, uint8_t *C) {
+    if (ORC_KIND(scheme) == ORC_GF256_RLC) {
+        for (int i = 0; i < r; i++)
+            orc_rlc_coefs((uint32_t)(ORC_RLC_KEY(scheme) + i), k, ORC_RLC_DT(scheme), C + i * k);
+        return;
+    }
     if (scheme == ORC_GF256_VDM) orc_vandermonde(k, r, C);
     else orc_cauchy(k, r, C);
+}
+
+/* a6/a7: the missing sources miss[0..e) and e present repairs sel[0..e) whose
+ * rows restricted to the missing columns are independent, chosen greedily in
+ * repair order (for an MDS matrix: the first e present repairs).  Returns e,
+ * or -1 if the present repairs have rank < e (unrecoverable). */
+int orc_select_rows(int k, int r, const uint8_t *C, uint64_t present, int *miss, int *sel) {
+    int e = 0, n = 0;
+    for (int j = 0; j < k; j++)
+        if (!((present >> j) & 1)) miss[e++] = j;
+    if (e == 0) return 0;
+    if (e > 16) return -1;
+    uint8_t basis[16][16];
+    int pivc[16];
+    for (int i = 0; i < r && n < e; i++) {
+        if (!((present >> (k + i)) & 1)) continue;
+        uint8_t v[16];
+        for (int u = 0; u < e; u++) v[u] = C[i * k + miss[u]];
+        for (int b = 0; b < n; b++) {
+            const uint8_t f = v[pivc[b]];
+            if (!f) continue;
+            for (int u = 0; u < e; u++) v[u] ^= orc_gf_mul(f, basis[b][u]);
+        }
+        int pc = -1;
+        for (int u = 0; u < e; u++)
+            if (v[u]) { pc = u; break; }
+        if (pc < 0) continue;  /* dependent on the rows chosen so far */
+        const uint8_t iv = orc_gf_inv(v[pc]);
+        for (int u = 0; u < e; u++) basis[n][u] = orc_gf_mul(v[u], iv);
+        pivc[n] = pc;
+        sel[n++] = i;
+    }
+    return n == e ? e : -1;
 }
 
 /* ---------------------------------------------------------------- A.5 --- */
@@ -291,16 +396,14 @@ int orc_decode(int scheme, int k, int r, uint32_t S, uint32_t stride, uint64_t p
         }
         return status;
     }
-    /* a7: MDS solve with the first e present repairs */
-    int miss[64], e = 0, sel[64], nrep = 0;
-    for (int j = 0; j < k; j++)
-        if (!((present >> j) & 1)) miss[e++] = j;
-    if (e == 0) return ORC_OK;
-    for (int i = 0; i < r; i++)
-        if ((present >> (k + i)) & 1) sel[nrep++] = i;
-    if (nrep < e || e > 16) return ORC_UNRECOVERABLE;
+    /* a7: solve with e present repairs independent on the missing columns
+     * (an MDS matrix: the first e present) */
+    int miss[64], sel[64];
     uint8_t C[64 * 64], A[16 * 16], Ai[16 * 16];
     orc_matrix(scheme, k, r, C);
+    const int e = orc_select_rows(k, r, C, present, miss, sel);
+    if (e == 0) return ORC_OK;
+    if (e < 0) return ORC_UNRECOVERABLE;
     for (int t = 0; t < e; t++)
         for (int u = 0; u < e; u++) A[t * e + u] = C[sel[t] * k + miss[u]];
     if (!gf_invert(e, A, Ai)) return ORC_UNRECOVERABLE;

@@ -30,8 +30,14 @@
 extern "C" {
 #endif
 
-/* schemes: XOR groups, GF(2^8) Cauchy rows, GF(2^8) systematic Vandermonde rows */
-enum { ORC_XOR = 0, ORC_GF256 = 1, ORC_GF256_VDM = 2 };
+/* schemes: XOR groups, GF(2^8) Cauchy rows, GF(2^8) systematic Vandermonde
+ * rows, GF(2^8) RFC 8681 random linear code rows (ORC_RLC(key0, dt): row i
+ * from repair_key key0 + i at density threshold dt) */
+enum { ORC_XOR = 0, ORC_GF256 = 1, ORC_GF256_VDM = 2, ORC_GF256_RLC = 3 };
+#define ORC_RLC(key0, dt) (ORC_GF256_RLC | ((dt) << 4) | ((int)(key0) << 8))
+#define ORC_KIND(s) ((s) & 0xF)
+#define ORC_RLC_DT(s) (((s) >> 4) & 0xF)
+#define ORC_RLC_KEY(s) (((s) >> 8) & 0xFFFF)
 enum { ORC_FIXED = 0, ORC_LENPREFIX = 1 };
 enum { ORC_OK = 0, ORC_UNRECOVERABLE = 1 };
 
@@ -44,8 +50,16 @@ int     orc_gf_log(uint8_t a);
 void    orc_cauchy(int k, int r, uint8_t *C);
 /* systematic Vandermonde parity rows P[i*k + j] (Backblaze construction) */
 void    orc_vandermonde(int k, int r, uint8_t *P);
-/* parity rows of a GF scheme (ORC_GF256 -> Cauchy, ORC_GF256_VDM -> Vandermonde) */
+/* parity rows of a GF scheme (ORC_GF256 -> Cauchy, ORC_GF256_VDM -> Vandermonde,
+ * ORC_RLC(key0, dt) -> RFC 8681 coefficients) */
 void    orc_matrix(int scheme, int k, int r, uint8_t *C);
+/* RFC 8682 TinyMT32 outputs 1..n after tinymt32_init(seed) */
+void    orc_tinymt32(uint32_t seed, int n, uint32_t *out);
+/* RFC 8681 §3.6 generate_coding_coefficients, m = 8; -1 if dt > 15 */
+int     orc_rlc_coefs(uint32_t key, int n, int dt, uint8_t *cc);
+/* missing sources and e independent present repairs (greedy in repair order);
+ * returns e (0: nothing missing) or -1 if the present repairs have rank < e */
+int     orc_select_rows(int k, int r, const uint8_t *C, uint64_t present, int *miss, int *sel);
 
 /* A.5 PRNG / workload */
 uint64_t orc_sm64(uint64_t x);

@@ -78,14 +78,84 @@ def vandermonde(k: int, r: int) -> np.ndarray:
     return matmul(V[k:], _gj_inverse(V[:k]))
 
 
+class TinyMT32:
+    """RFC 8682 TinyMT32 (mat1 0x8f7011ee, mat2 0xfc78ff1f, tmat 0x3793fdff),
+    restated in Python from the RFC's description: 127-bit state of four
+    words, 8 pre-loop steps after seeding, tempered output."""
+    MAT1, MAT2, TMAT = 0x8F7011EE, 0xFC78FF1F, 0x3793FDFF
+
+    def __init__(self, seed: int):
+        st = [seed & 0xFFFFFFFF, self.MAT1, self.MAT2, self.TMAT]
+        for i in range(1, 8):
+            prev = st[(i - 1) & 3]
+            st[i & 3] ^= (i + 1812433253 * (prev ^ (prev >> 30))) & 0xFFFFFFFF
+        if (st[0] & 0x7FFFFFFF) == 0 and st[1] == st[2] == st[3] == 0:
+            st = [ord(c) for c in "TINY"]
+        self.st = st
+        for _ in range(8):
+            self._next()
+
+    def _next(self):
+        s0, s1, s2, s3 = self.st
+        x = (s0 & 0x7FFFFFFF) ^ s1 ^ s2
+        x = (x ^ (x << 1)) & 0xFFFFFFFF
+        y = s3 ^ (s3 >> 1) ^ x
+        n1, n2 = s2, (x ^ (y << 10)) & 0xFFFFFFFF
+        if y & 1:
+            n1 ^= self.MAT1
+            n2 ^= self.MAT2
+        self.st = [s1, n1, n2, y]
+
+    def u32(self) -> int:
+        self._next()
+        s0, _, s2, s3 = self.st
+        t1 = (s0 + (s2 >> 8)) & 0xFFFFFFFF
+        return (s3 ^ t1 ^ (self.TMAT if t1 & 1 else 0)) & 0xFFFFFFFF
+
+
+def rlc_coefs(key: int, n: int, dt: int) -> np.ndarray:
+    """RFC 8681 §3.6 generate_coding_coefficients(repair_key, n, dt, m = 8)."""
+    assert 0 <= dt <= 15
+    t = TinyMT32(key & 0xFFFF)
+    cc = np.zeros(n, np.uint8)
+    for i in range(n):
+        if dt == 15 or (t.u32() & 0xF) <= dt:
+            c = 0
+            while c == 0:
+                c = t.u32() & 0xFF
+            cc[i] = c
+    return cc
+
+
+def parse_rlc(scheme: str):
+    """"rlc:KEY:DT" -> (key, dt), else None."""
+    if not scheme.startswith("rlc:"):
+        return None
+    _, key, dt = scheme.split(":")
+    return int(key), int(dt)
+
+
+def scheme_id(scheme: str) -> int:
+    """The C oracle's scheme integer (fec_oracle.h, ORC_RLC for RLC)."""
+    rl = parse_rlc(scheme)
+    if rl:
+        return 3 | (rl[1] << 4) | (rl[0] << 8)
+    return {"xor": 0, "gf": 1, "gf-vdm": 2}[scheme]
+
+
 def generator(scheme: str, k: int, r: int) -> np.ndarray:
     """Systematic (k+r) x k generator: identity on top, repair rows below.
-    scheme: "xor", "gf" (Cauchy rows) or "gf-vdm" (systematic Vandermonde)."""
+    scheme: "xor", "gf" (Cauchy rows), "gf-vdm" (systematic Vandermonde) or
+    "rlc:KEY:DT" (RFC 8681 coefficients, row i from repair_key KEY + i)."""
     G = np.zeros((k + r, k), np.uint8)
     G[:k] = np.eye(k, dtype=np.uint8)
+    rl = parse_rlc(scheme)
     if scheme == "xor":
         for g in range(r):
             G[k + g, g::r] = 1
+    elif rl:
+        for i in range(r):
+            G[k + i] = rlc_coefs(rl[0] + i, k, rl[1])
     elif scheme == "gf-vdm":
         G[k:] = vandermonde(k, r)
     else:
@@ -141,6 +211,8 @@ def decode(scheme: str, k: int, r: int, sym: np.ndarray, present: int):
     reps = [k + i for i in range(r) if (present >> (k + i)) & 1]
     if len(reps) < len(missing):
         return src, False
+    if parse_rlc(scheme):
+        return _solve_all_rows(generator(scheme, k, r), sym, present, k, r)
     rows = [j for j in range(k) if (present >> j) & 1] + reps[: len(missing)]
     G = generator(scheme, k, r)
     A = np.concatenate([G[rows], sym[rows]], axis=1).astype(np.uint8)  # k x (k+L)
@@ -153,6 +225,29 @@ def decode(scheme: str, k: int, r: int, sym: np.ndarray, present: int):
             if i != c and A[i, c]:
                 A[i] ^= _MUL[A[i, c]][A[c]]
     return A[:, k:k + L].copy(), True
+
+
+def _solve_all_rows(G: np.ndarray, sym: np.ndarray, present: int, k: int, r: int):
+    """Random linear code (not MDS): Gaussian elimination of EVERY received row
+    of the generator (sources and repairs) against the k unknowns; recoverable
+    iff that system has rank k.  Row-echelon with pivot search over all rows,
+    then back substitution."""
+    L = sym.shape[1]
+    rows = [i for i in range(k + r) if (present >> i) & 1]
+    A = np.concatenate([G[rows], sym[rows]], axis=1).astype(np.uint8)
+    m, piv_rows = A.shape[0], []
+    for c in range(k):
+        piv = next((i for i in range(len(piv_rows), m) if A[i, c]), None)
+        if piv is None:
+            return sym[:k].copy(), False
+        t = len(piv_rows)
+        A[[t, piv]] = A[[piv, t]]
+        A[t] = _MUL[_INV[A[t, c]]][A[t]]
+        for i in range(m):
+            if i != t and A[i, c]:
+                A[i] ^= _MUL[A[i, c]][A[t]]
+        piv_rows.append(t)
+    return A[:k, k:k + L].copy(), True
 
 
 # ------------------------------------------------------------ workloads ---

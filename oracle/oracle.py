@@ -17,6 +17,16 @@ _LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
 _lib = None
 
 XOR, GF256, GF256_VDM = 0, 1, 2     # GF256: Cauchy rows; GF256_VDM: systematic Vandermonde
+
+
+def RLC(key0: int, dt: int) -> int:
+    """Scheme id of the RFC 8681 random linear code rows (fec_oracle.h ORC_RLC):
+    parity row i from repair_key key0 + i at density threshold dt."""
+    return 3 | (dt << 4) | (key0 << 8)
+
+
+def scheme_kind(scheme: int) -> int:
+    return scheme & 0xF
 FIXED_WL, MIXED_WL = 0, 1            # workloads (DESIGN.md §Workloads)
 ERA_NONE, ERA_EXACT, ERA_IID = 0, 1, 2
 OK, UNRECOVERABLE = 0, 1
@@ -44,6 +54,8 @@ def lib():
             "orc_cauchy": (None, [i32, i32, vp]),
             "orc_vandermonde": (None, [i32, i32, vp]),
             "orc_matrix": (None, [i32, i32, i32, vp]),
+            "orc_tinymt32": (None, [u32, i32, vp]),
+            "orc_rlc_coefs": (i32, [u32, i32, i32, vp]),
             "orc_sm64": (u64, [u64]),
             "orc_pkt_len": (u32, [i32, u64, u64, i32, i32, u32]),
             "orc_sym_len": (u32, [i32, u64, u64, i32, u32]),
@@ -94,6 +106,27 @@ def vandermonde(k: int, r: int) -> np.ndarray:
     P = np.zeros((r, k), np.uint8)
     lib().orc_vandermonde(k, r, _p(P))
     return P
+
+
+def matrix(scheme: int, k: int, r: int) -> np.ndarray:
+    """Parity rows [r, k] of a GF scheme id."""
+    P = np.zeros((r, k), np.uint8)
+    lib().orc_matrix(scheme, k, r, _p(P))
+    return P
+
+
+def tinymt32(seed: int, n: int) -> list:
+    """RFC 8682 TinyMT32 outputs 1..n after tinymt32_init(seed)."""
+    out = np.zeros(n, np.uint32)
+    lib().orc_tinymt32(seed, n, _p(out))
+    return [int(x) for x in out]
+
+
+def rlc_coefs(key: int, n: int, dt: int) -> np.ndarray:
+    """RFC 8681 §3.6 coding coefficients (m = 8)."""
+    cc = np.zeros(n, np.uint8)
+    assert lib().orc_rlc_coefs(key, n, dt, _p(cc)) == 0
+    return cc
 
 
 def sm64(x: int) -> int:

@@ -66,12 +66,17 @@ uint8_t host_gf_pow(uint8_t a, int n) {  // a^n, 0^0 = 1
 }
 
 // Parity rows P[i*k + j] of the code's systematic generator:
-// Cauchy C[i][j] = inv((k+i) ^ j), or the systematic Vandermonde matrix —
+// Cauchy C[i][j] = inv((k+i) ^ j), the systematic Vandermonde matrix —
 // V[i][j] = i^j over points 0..k+r-1 times the inverse of its top k x k block
-// (Backblaze JavaReedSolomon / klauspost / reed-solomon-erasure construction).
+// (Backblaze JavaReedSolomon / klauspost / reed-solomon-erasure construction) —
+// or RFC 8681 RLC rows (fec_spec.h rlc_coefs).
 void host_parity_rows(const fecgpu_code *code, std::vector<uint8_t> &P) {
     const int k = code->k, r = code->r;
     P.assign((size_t)r * k, 0);
+    if (code->matrix == FECGPU_MATRIX_RLC) {  // RFC 8681 coefficients, one repair_key per row
+        for (int i = 0; i < r; i++) rlc_coefs((uint32_t)code->rlc_key + i, k, code->rlc_dt, &P[(size_t)i * k]);
+        return;
+    }
     if (code->matrix == FECGPU_MATRIX_CAUCHY) {
         for (int i = 0; i < r; i++)
             for (int j = 0; j < k; j++) P[(size_t)i * k + j] = host_gf_inv((uint8_t)((k + i) ^ j));
@@ -120,8 +125,8 @@ struct HostPipe {
 struct fecgpu_ctx {
     std::vector<int> devs;
     std::mutex mu;
-    // (device, k, r, matrix) -> encode tables (and parity rows) on that device
-    std::map<std::tuple<int, int, int, int>, EncTables> enc;
+    // (device, k, r, matrix, rlc_key, rlc_dt) -> encode tables (and parity rows) on that device
+    std::map<std::tuple<int, int, int, int, int, int>, EncTables> enc;
     // host-pointer staging per device
     std::map<int, std::pair<void *, size_t>> stage;
     // host-pointer pipelines, one per entry of devs (keyed by that index)
@@ -187,10 +192,28 @@ ssize_t fecgpu_code_check(const fecgpu_code *code) {
     if (code->r > FECGPU_MAX_R) return FECGPU_ERR_UNSUPPORTED;
     if (code->scheme == FECGPU_SCHEME_XOR && code->r > code->k) return FECGPU_ERR_INVALID_ARG;
     if (code->scheme == FECGPU_SCHEME_GF256 && code->matrix != FECGPU_MATRIX_CAUCHY &&
-        code->matrix != FECGPU_MATRIX_VANDERMONDE)
+        code->matrix != FECGPU_MATRIX_VANDERMONDE && code->matrix != FECGPU_MATRIX_RLC)
         return FECGPU_ERR_UNSUPPORTED;
+    if (code->scheme == FECGPU_SCHEME_GF256 && code->matrix == FECGPU_MATRIX_RLC && code->rlc_dt > 15)
+        return FECGPU_ERR_INVALID_ARG;
     if (code->poly != 0 && code->poly != 0x11D) return FECGPU_ERR_UNSUPPORTED;
     return 0;
+}
+
+ssize_t fecgpu_code_parity_rows(const fecgpu_code *code, uint8_t *out, size_t cap) {
+    ssize_t rc = fecgpu_code_check(code);
+    if (rc) return rc;
+    const size_t n = (size_t)code->k * code->r;
+    if (!out || cap < n) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    if (code->scheme == FECGPU_SCHEME_XOR) {
+        for (int i = 0; i < code->r; i++)
+            for (int j = 0; j < code->k; j++) out[(size_t)i * code->k + j] = (uint8_t)(j % code->r == i);
+        return (ssize_t)n;
+    }
+    std::vector<uint8_t> P;
+    host_parity_rows(code, P);
+    std::memcpy(out, P.data(), n);
+    return (ssize_t)n;
 }
 
 ssize_t fecgpu_ctx_new(const int *devs, int ndev, fecgpu_ctx **out) {
@@ -347,7 +370,9 @@ ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out)
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
     std::lock_guard<std::mutex> lk(ctx->mu);
-    auto key = std::make_tuple(dev, k, r, (int)code->matrix);
+    const bool rlc = code->matrix == FECGPU_MATRIX_RLC;
+    auto key = std::make_tuple(dev, k, r, (int)code->matrix, rlc ? (int)code->rlc_key : 0,
+                               rlc ? (int)code->rlc_dt : 0);
     auto it = ctx->enc.find(key);
     if (it != ctx->enc.end()) {
         out = it->second;

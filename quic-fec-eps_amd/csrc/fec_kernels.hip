@@ -1161,11 +1161,16 @@ __device__ void plan_gf_gj(const BatchArgs &a, uint64_t w, int lane, uint8_t *re
     }
 }
 
-// General-matrix plan (FECGPU_MATRIX_VANDERMONDE and any other systematic MDS
-// generator): the parity rows P[r][k] sit in LDS; A[t][u] = P[sel_t][m_u] is
-// inverted by wave-parallel Gauss-Jordan (no pivoting: every square
-// submatrix of an MDS code's parity rows is nonsingular, so are the leading
-// minors), then folded into the decode matrix D like the Cauchy plans.
+// General-matrix plan (FECGPU_MATRIX_VANDERMONDE, FECGPU_MATRIX_RLC, any
+// systematic generator): the parity rows P[r][k] sit in LDS.  The system of
+// EVERY present repair, A[t][u] = P[sel_t][m_u] (t < np <= 8 rows, u < e
+// columns), is reduced by wave-parallel Gauss-Jordan with pivot search: the
+// pivot of column c is the first row not yet used whose entry is nonzero, so
+// a random linear code (not MDS) recovers whenever its present repairs have
+// rank e, and is unrecoverable otherwise.  Row operations only ever add pivot
+// rows, so pivot row P_u of column u ends as x_u = sum_c T[P_u][P_c] * s_{P_c}
+// over the chosen repairs (T: the identity columns carried along), which is
+// folded into the decode matrix D like the Cauchy plans.
 template <int R>
 __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int lane, uint8_t *region,
                             const uint8_t *ex, const uint8_t *lg, const uint8_t *P, uint8_t &ne_out) {
@@ -1175,8 +1180,8 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
     const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
     const uint64_t miss = ~pres & kmask;
     const uint64_t rep = (pres >> k) & ((1ull << r) - 1);
-    const int e = __popcll(miss);
-    if (e == 0 || __popcll(rep) < e || e > R) {
+    const int e = __popcll(miss), np = __popcll(rep);
+    if (e == 0 || np < e || e > R) {
         if (lane == 0) {
             ne_out = 0;
             a.status[w] = (e == 0) ? 0 : 1;
@@ -1184,34 +1189,36 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
         return;
     }
     uint64_t mm = miss, rr = rep;
-    for (int i = 0; i < lane && i < e; i++) { mm &= mm - 1; rr &= rr - 1; }
-    const int my_m = (int)__ffsll((unsigned long long)mm) - 1;  // valid for lane < e
-    const int my_sel = (int)__ffsll((unsigned long long)rr) - 1;
+    for (int i = 0; i < lane && i < 8; i++) { mm &= mm - 1; rr &= rr - 1; }
+    const int my_m = (int)__ffsll((unsigned long long)mm) - 1;    // lane u < e: u-th missing source
+    const int my_sel = (int)__ffsll((unsigned long long)rr) - 1;  // lane t < np: t-th present repair
     if (lane < k && ((pres >> lane) & 1)) insym[__popcll(pres & kmask & ((1ull << lane) - 1))] = (uint8_t)lane;
-    if (lane < e) {
-        insym[k - e + lane] = (uint8_t)(k + my_sel);
-        outsym[lane] = (uint8_t)my_m;
-    }
-    // [A | I], lane = t*8 + u; every __shfl with the whole wave active
+    if (lane < e) outsym[lane] = (uint8_t)my_m;
+    // [A | I], lane = t*8 + u; every __shfl and ballot with the whole wave active
     const int t = lane >> 3, u = lane & 7;
-    const int sel_t = __shfl(my_sel, t & 7, 64);
+    const int sel_t = __shfl(my_sel, t, 64);
     const int m_u = __shfl(my_m, u, 64);
-    const bool valid = (t < e) && (u < e);
-    uint32_t xl = valid ? P[sel_t * k + m_u] : 0u;
-    uint32_t xr = (valid && t == u) ? 1u : 0u;
+    const bool row = t < np;
+    uint32_t xl = (row && u < e) ? P[sel_t * k + m_u] : 0u;
+    uint32_t xr = (row && t == u) ? 1u : 0u;
+    uint32_t used = 0;  // wave-uniform: rows already pivots
+    int my_piv = 0;     // lane c < e: pivot row of column c
     bool singular = false;
     for (int c = 0; c < e; c++) {
-        const uint32_t piv = __shfl(xl, c * 8 + c, 64);
-        if (piv == 0) { singular = true; break; }
-        const uint32_t ip = gf_inv_lds(ex, lg, piv);
-        if (t == c) {
+        const uint64_t cand = __ballot(row && u == c && !((used >> t) & 1) && xl != 0);
+        if (!cand) { singular = true; break; }
+        const int pr = (int)(__ffsll((unsigned long long)cand) - 1) >> 3;
+        used |= 1u << pr;
+        if (lane == c) my_piv = pr;
+        const uint32_t ip = gf_inv_lds(ex, lg, __shfl(xl, pr * 8 + c, 64));
+        if (t == pr) {
             xl = gf_mul_lds(ex, lg, xl, ip);
             xr = gf_mul_lds(ex, lg, xr, ip);
         }
-        const uint32_t f = __shfl(xl, (t & 7) * 8 + c, 64);
-        const uint32_t rl = __shfl(xl, c * 8 + u, 64);
-        const uint32_t rq = __shfl(xr, c * 8 + u, 64);
-        if (t != c && valid) {
+        const uint32_t f = __shfl(xl, t * 8 + c, 64);
+        const uint32_t rl = __shfl(xl, pr * 8 + u, 64);
+        const uint32_t rq = __shfl(xr, pr * 8 + u, 64);
+        if (t != pr && row) {
             xl ^= gf_mul_lds(ex, lg, f, rl);
             xr ^= gf_mul_lds(ex, lg, f, rq);
         }
@@ -1220,22 +1227,29 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
         if (lane == 0) { ne_out = 0; a.status[w] = 1; }
         return;
     }
-    WAVE_SYNC();
-    // D[u][q] for idx = u*k + q; Ainv[u][t] = xr of lane u*8 + t
     const int kr = k - e;
+    {
+        const int sel_piv = __shfl(my_sel, my_piv & 7, 64);  // lane c: repair chosen for column c
+        if (lane < e) insym[kr + lane] = (uint8_t)(k + sel_piv);
+    }
+    WAVE_SYNC();
+    // D[u][q] for idx = u*k + q; Ainv'[u][c] = T[P_u][P_c] = xr of lane P_u*8 + P_c
     for (int base = 0; base < e * k; base += 64) {
         const int idx = base + lane;
         const int du = idx / k, dq = idx - du * k;
         const bool live = idx < e * k;
         const bool is_src = dq < kr;
         const uint32_t j = (live && is_src) ? insym[dq] : 0u;
+        const int pu = __shfl(my_piv, du & 7, 64);
         uint32_t csrc = 0;
         for (int tt = 0; tt < e; tt++) {
-            const uint32_t ai = __shfl(xr, ((du & 7) * 8 + tt) & 63, 64);
-            const int st = __shfl(my_sel, tt, 64);
+            const int pt = __shfl(my_piv, tt, 64);
+            const uint32_t ai = __shfl(xr, (pu * 8 + pt) & 63, 64);
+            const int st = __shfl(my_sel, pt & 7, 64);
             if (is_src) csrc ^= gf_mul_lds(ex, lg, ai, P[st * k + j]);
         }
-        const uint32_t crep = __shfl(xr, ((du & 7) * 8 + (is_src ? 0 : dq - kr)) & 63, 64);
+        const int pc = __shfl(my_piv, (is_src ? 0 : dq - kr) & 7, 64);
+        const uint32_t crep = __shfl(xr, (pu * 8 + pc) & 63, 64);
         const uint32_t c = is_src ? csrc : crep;
         if (live) {
             const CoefTab ct = make_coef_tab(c);

@@ -86,6 +86,78 @@ struct ParityRows {
     }
 };
 
+// ------------------------------------------------- A.2 random linear codes --
+// RFC 8682 TinyMT32 (parameter set mat1 0x8f7011ee, mat2 0xfc78ff1f, tmat
+// 0x3793fdff) and RFC 8681 §3.6 generate_coding_coefficients(): the PRNG and
+// coefficient generator of the Sliding Window RLC FEC schemes, whose field
+// for m = 8 is GF(2^8)/0x11D as A.1.  Pinned by RFC 8682's seed-1 outputs
+// (tests/test_rlc_spec.py).  Used by FECGPU_MATRIX_RLC (block form: parity row
+// i = coefficients of repair_key rlc_key + i over the k sources) and by the
+// sliding-window encoder (one repair_key per repair symbol).
+struct Tinymt32 {
+    uint32_t s[4];
+};
+
+constexpr uint32_t kTmtMat1 = 0x8f7011eeu, kTmtMat2 = 0xfc78ff1fu, kTmtTmat = 0x3793fdffu;
+
+FEC_HD void tinymt32_next(Tinymt32 &t) {
+    uint32_t y = t.s[3];
+    uint32_t x = (t.s[0] & 0x7fffffffu) ^ t.s[1] ^ t.s[2];
+    x ^= x << 1;
+    y ^= (y >> 1) ^ x;
+    t.s[0] = t.s[1];
+    t.s[1] = t.s[2];
+    t.s[2] = x ^ (y << 10);
+    t.s[3] = y;
+    const uint32_t m = 0u - (y & 1u);
+    t.s[1] ^= m & kTmtMat1;
+    t.s[2] ^= m & kTmtMat2;
+}
+
+FEC_HD uint32_t tinymt32_u32(Tinymt32 &t) {
+    tinymt32_next(t);
+    uint32_t t0 = t.s[3];
+    const uint32_t t1 = t.s[0] + (t.s[2] >> 8);
+    t0 ^= t1;
+    if (t1 & 1u) t0 ^= kTmtTmat;
+    return t0;
+}
+
+FEC_HD void tinymt32_init(Tinymt32 &t, uint32_t seed) {
+    t.s[0] = seed;
+    t.s[1] = kTmtMat1;
+    t.s[2] = kTmtMat2;
+    t.s[3] = kTmtTmat;
+    for (uint32_t i = 1; i < 8; i++)
+        t.s[i & 3] ^= i + 1812433253u * (t.s[(i - 1) & 3] ^ (t.s[(i - 1) & 3] >> 30));
+    if ((t.s[0] & 0x7fffffffu) == 0 && t.s[1] == 0 && t.s[2] == 0 && t.s[3] == 0) {
+        t.s[0] = 'T';
+        t.s[1] = 'I';
+        t.s[2] = 'N';
+        t.s[3] = 'Y';
+    }
+    for (int i = 0; i < 8; i++) tinymt32_next(t);
+}
+
+// RFC 8681 §3.6 for m = 8: cc[0..n) of repair_key `key` at density threshold
+// dt (0..15; 15 = every coefficient nonzero, else each is nonzero with
+// probability (dt + 1) / 16).  Returns false for dt > 15.
+FEC_HD bool rlc_coefs(uint32_t key, int n, uint32_t dt, uint8_t *cc) {
+    if (dt > 15) return false;
+    Tinymt32 t;
+    tinymt32_init(t, key & 0xFFFFu);
+    for (int i = 0; i < n; i++) {
+        uint32_t c = 0;
+        if (dt == 15 || (tinymt32_u32(t) & 0xFu) <= dt) {
+            do {
+                c = tinymt32_u32(t) & 0xFFu;
+            } while (c == 0);
+        }
+        cc[i] = (uint8_t)c;
+    }
+    return true;
+}
+
 // multiply by x (=2) in GF(2^8)/0x11D, one byte in the low 8 bits
 FEC_HD uint32_t gf_xtime(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x1Du : 0u)) & 0xFFu; }
 

@@ -27,7 +27,8 @@ LIB_PATH = os.environ.get("FECGPU_LIB") or os.path.join(os.path.dirname(_HERE), 
 ERR_DONE, ERR_BUFFER_TOO_SHORT, ERR_INVALID_ARG = -1, -2, -3
 ERR_UNSUPPORTED, ERR_DEVICE, ERR_UNRECOVERABLE, ERR_LIMIT = -4, -5, -6, -7
 SCHEME_XOR, SCHEME_GF256 = 0, 1
-MATRIX_CAUCHY, MATRIX_VANDERMONDE = 0, 1
+MATRIX_CAUCHY, MATRIX_VANDERMONDE, MATRIX_RLC = 0, 1, 2
+_MATRIX_IDS = {"cauchy": MATRIX_CAUCHY, "vandermonde": MATRIX_VANDERMONDE, "rlc": MATRIX_RLC}
 FRAMING_FIXED, FRAMING_LENPREFIX = 0, 1
 STATUS_OK, STATUS_UNRECOVERABLE = 0, 1
 F_HOST_PTRS, F_SYNC = 1, 2
@@ -38,6 +39,7 @@ ERASURE_NONE, ERASURE_EXACT, ERASURE_IID = 0, 1, 2
 # every symbol include/fecgpu.h declares (tests check the library exports them)
 EXPORTS = (
     "fecgpu_abi_version", "fecgpu_strerror", "fecgpu_last_error", "fecgpu_code_check",
+    "fecgpu_code_parity_rows",
     "fecgpu_ctx_new", "fecgpu_ctx_free", "fecgpu_ctx_set_tuning",
     "fecgpu_host_alloc", "fecgpu_host_free",
     "fecgpu_encode_batch", "fecgpu_encode_split", "fecgpu_decode_batch",
@@ -77,6 +79,9 @@ class fecgpu_code(ctypes.Structure):
         ("k", ctypes.c_uint16),
         ("r", ctypes.c_uint16),
         ("poly", ctypes.c_uint32),
+        ("rlc_key", ctypes.c_uint16),
+        ("rlc_dt", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8),
     ]
 
 
@@ -126,6 +131,7 @@ def _lib():
             "fecgpu_strerror": (ctypes.c_char_p, [sz]),
             "fecgpu_last_error": (ctypes.c_char_p, []),
             "fecgpu_code_check": (sz, [cp]),
+            "fecgpu_code_parity_rows": (sz, [cp, vp, ctypes.c_size_t]),
             "fecgpu_ctx_new": (sz, [vp, i32, ctypes.POINTER(vp)]),
             "fecgpu_ctx_free": (None, [vp]),
             "fecgpu_ctx_set_tuning": (sz, [vp, ctypes.c_char_p, ctypes.c_int64]),
@@ -195,19 +201,22 @@ _lib()  # fail loudly at import when the native library is missing
 @dataclass(frozen=True)
 class Code:
     """fecgpu_code: scheme 'xor' | 'gf256', k sources, r repairs per window;
-    GF matrix 'cauchy' (default) | 'vandermonde'."""
+    GF matrix 'cauchy' (default) | 'vandermonde' | 'rlc' (RFC 8681 random
+    linear code: parity row i from repair_key rlc_key + i, density rlc_dt)."""
     scheme: str
     k: int
     r: int
     framing: str = "fixed"
     matrix: str = "cauchy"
+    rlc_key: int = 0
+    rlc_dt: int = 15
 
     @property
     def c(self) -> fecgpu_code:
         return fecgpu_code(SCHEME_XOR if self.scheme == "xor" else SCHEME_GF256,
-                           MATRIX_VANDERMONDE if self.matrix == "vandermonde" else MATRIX_CAUCHY,
+                           _MATRIX_IDS[self.matrix],
                            FRAMING_FIXED if self.framing == "fixed" else FRAMING_LENPREFIX,
-                           self.k, self.r, 0x11D)
+                           self.k, self.r, 0x11D, self.rlc_key, self.rlc_dt, 0)
 
     @property
     def scheme_id(self) -> int:
@@ -215,6 +224,14 @@ class Code:
 
     def check(self) -> int:
         return _lib().fecgpu_code_check(ctypes.byref(self.c))
+
+    def parity_rows(self):
+        """[r, k] u8 parity rows of the code (host only, fecgpu_code_parity_rows)."""
+        import numpy as np
+        out = np.zeros((self.r, self.k), np.uint8)
+        _check(_lib().fecgpu_code_parity_rows(ctypes.byref(self.c), out.ctypes.data, out.size),
+               "fecgpu_code_parity_rows")
+        return out
 
 
 def _check(rc: int, what: str) -> int:

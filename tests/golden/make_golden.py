@@ -33,6 +33,11 @@ CASES = [
     ("vdm_k5r5_L24_iid", "gf-vdm", 5, 5, 24, 2, 8, 40),
     ("vdm_k16r4_L64_exact", "gf-vdm", 16, 4, 64, 1, 4, 7),
     ("vdm_k32r8_L40_iid", "gf-vdm", 32, 8, 40, 2, 4, 1 << 21),
+    # RFC 8681 random linear code rows (FECGPU_MATRIX_RLC): "rlc:KEY:DT",
+    # scheme id 3 | DT << 4 | KEY << 8 (the C oracle's ORC_RLC)
+    ("rlc_k16r4_L64_exact_dt15", "rlc:1:15", 16, 4, 64, 1, 4, 3),
+    ("rlc_k10r6_L33_iid_dt7", "rlc:4660:7", 10, 6, 33, 2, 16, 50),
+    ("rlc_k6r6_L20_iid_dt1", "rlc:65535:1", 6, 6, 20, 2, 24, 7),
 ]
 
 
@@ -60,8 +65,8 @@ def make(name, scheme, k, r, L, erasure, nwin, w0):
         dec[i] = out
     np.savez_compressed(os.path.join(HERE, name + ".npz"), src=src, repair=rep, present=pres,
                         status=status, decoded=dec,
-                        meta=np.array([{"xor": 0, "gf": 1, "gf-vdm": 2}[scheme], k, r, L, erasure,
-                                       nwin, w0, SEED], np.int64))
+                        meta=np.array([N.scheme_id(scheme), k, r, L, erasure, nwin, w0, SEED],
+                                      np.int64))
 
 
 if __name__ == "__main__":

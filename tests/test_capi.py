@@ -71,12 +71,32 @@ def test_header_compiles_as_c():
     (2, 4, 1, 0, 0, 0, fecgpu.ERR_INVALID_ARG),    # unknown scheme
     (1, 4, 1, 2, 0, 0, fecgpu.ERR_INVALID_ARG),    # unknown framing
     (1, 4, 1, 0, 1, 0, 0),                         # systematic Vandermonde
-    (1, 4, 1, 0, 2, 0, fecgpu.ERR_UNSUPPORTED),    # unknown matrix
+    (1, 4, 1, 0, 2, 0, 0),                         # RFC 8681 RLC rows (dt 0: sparse)
+    (1, 4, 1, 0, 3, 0, fecgpu.ERR_UNSUPPORTED),    # unknown matrix
     (1, 4, 1, 0, 0, 0x11B, fecgpu.ERR_UNSUPPORTED),
 ])
 def test_code_check(scheme, k, r, framing, matrix, poly, want):
     c = fecgpu.fecgpu_code(scheme, matrix, framing, k, r, poly)
     assert fecgpu.lib().fecgpu_code_check(ctypes.byref(c)) == want
+
+
+def test_rlc_density_threshold_checked():
+    for dt, want in [(0, 0), (15, 0), (16, fecgpu.ERR_INVALID_ARG), (255, fecgpu.ERR_INVALID_ARG)]:
+        c = fecgpu.fecgpu_code(1, fecgpu.MATRIX_RLC, 0, 8, 2, 0, 7, dt, 0)
+        assert fecgpu.lib().fecgpu_code_check(ctypes.byref(c)) == want
+
+
+def test_parity_rows_host_only():
+    """fecgpu_code_parity_rows runs on the host (no device here) for every matrix."""
+    P = fecgpu.Code("xor", 6, 3).parity_rows()
+    assert P.tolist() == [[1, 0, 0, 1, 0, 0], [0, 1, 0, 0, 1, 0], [0, 0, 1, 0, 0, 1]]
+    P = fecgpu.Code("gf256", 16, 4).parity_rows()
+    assert P[0, :4].tolist() == [0xd8, 0x72, 0xc0, 0x58]   # SURVEY §4 T0 Cauchy row
+    c = fecgpu.Code("gf256", 8, 2).c
+    buf = (ctypes.c_uint8 * 15)()
+    assert fecgpu.lib().fecgpu_code_parity_rows(ctypes.byref(c), ctypes.cast(buf, ctypes.c_void_p), 15) \
+        == fecgpu.ERR_BUFFER_TOO_SHORT
+
 
 
 def test_null_and_invalid_args_before_device():
@@ -92,7 +112,7 @@ def test_null_and_invalid_args_before_device():
     assert L.fecgpu_ctx_new(None, 0, None) == fecgpu.ERR_INVALID_ARG
     assert L.fecgpu_strerror(fecgpu.ERR_UNRECOVERABLE) == b"unrecoverable"
     assert L.fecgpu_strerror(fecgpu.ERR_LIMIT) == b"limit reached"
-    assert L.fecgpu_abi_version() == 2
+    assert L.fecgpu_abi_version() == 3
 
 
 def test_no_cpu_fallback_without_gpu():

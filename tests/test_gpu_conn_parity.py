@@ -38,7 +38,17 @@ def ctx():
 def _oscheme(code):
     if code.scheme == "xor":
         return "xor"
+    if code.matrix == "rlc":
+        return f"rlc:{code.rlc_key}:{code.rlc_dt}"
     return "gf-vdm" if code.matrix == "vandermonde" else "gf"
+
+
+def _code(scheme, k, r, framing, matrix):
+    """matrix 'rlc:KEY:DT' -> the RFC 8681 RLC rows of repair_key KEY.., density DT."""
+    if matrix.startswith("rlc:"):
+        _, key, dt = matrix.split(":")
+        return fecgpu.Code(scheme, k, r, framing, "rlc", rlc_key=int(key), rlc_dt=int(dt))
+    return fecgpu.Code(scheme, k, r, framing, matrix)
 
 
 def frame_window(code, pkts):
@@ -85,13 +95,15 @@ CASES = [
     ("xor", 4, 1, "lenprefix", "cauchy", 1200, 15, 2, 4),
     ("xor", 8, 2, "fixed", "cauchy", 1200, 10, 5, 16),
     ("xor", 6, 3, "lenprefix", "cauchy", 700, 8, 4, 3),
+    ("gf256", 16, 4, "lenprefix", "rlc:0:15", 1350, 9, 5, 4),
+    ("gf256", 8, 4, "fixed", "rlc:4660:5", 1000, 12, 3, 4),
 ]
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-k{c[1]}r{c[2]}-{c[3]}-{c[4]}" for c in CASES])
 def test_encoder_repairs_match_oracle(ctx, case):
     scheme, k, r, framing, matrix, mtu, nwin, short_last, batch = case
-    code = fecgpu.Code(scheme, k, r, framing, matrix)
+    code = _code(scheme, k, r, framing, matrix)
     rng = np.random.default_rng(k * 100 + r)
     wins = _packets(rng, code, nwin, mtu, short_last)
     enc = fecgpu.Encoder(ctx, code, max_len=mtu, batch=batch)
@@ -120,7 +132,7 @@ def test_frames_only_receiver_matches_oracle(ctx, case):
     """Sender -> frames on the wire -> lossy channel -> frame_parse -> decoder.
     The receiver learns nothing out of band: short windows through REPAIR nsrc."""
     scheme, k, r, framing, matrix, mtu, nwin, short_last, batch = case
-    code = fecgpu.Code(scheme, k, r, framing, matrix)
+    code = _code(scheme, k, r, framing, matrix)
     rng = np.random.default_rng(7 * k + r)
     wins = _packets(rng, code, nwin, mtu, short_last)
     enc = fecgpu.Encoder(ctx, code, max_len=mtu, batch=batch)
@@ -168,14 +180,14 @@ def test_frames_only_receiver_matches_oracle(ctx, case):
         if not got_rep:  # no REPAIR frame arrived: the receiver cannot know nsrc
             for j in range(len(pk), k):
                 pres &= ~(1 << j)
-        out, _ = N.decode(_oscheme(code), k, r, full, pres)
+        out, ok_all = N.decode(_oscheme(code), k, r, full, pres)
         for j, p in enumerate(pk):
             q = dec.recovered(w, j)
             if (pres >> j) & 1:
                 assert q == p
                 continue
             # lost: the oracle recovers it iff the decoder does, with the same bytes
-            oracle_ok = _recoverable(code, pres, j)
+            oracle_ok = ok_all if code.matrix == "rlc" else _recoverable(code, pres, j)
             if oracle_ok:
                 exp = bytes(N.deframe(out[j])) if framing == "lenprefix" else out[j][:len(p)].tobytes()
                 assert exp == p

@@ -47,11 +47,12 @@ def _cmp_emitted(a: np.ndarray, b: np.ndarray, S: np.ndarray, what: str):
             raise AssertionError(f"{what}: window {w} differs at (sym, byte) {bad[:5].tolist()}")
 
 
-def gpu_run(ctx, scheme, k, r, wins, S, present, uniform: bool, poison=0xAB, matrix="cauchy"):
+def gpu_run(ctx, scheme, k, r, wins, S, present, uniform: bool, poison=0xAB, matrix="cauchy",
+            rlc=(0, 15)):
     """Encode on the GPU, poison erased symbols, decode on the GPU.
-    Returns (encoded, decoded, status) as numpy."""
+    Returns (encoded, decoded, status) as numpy.  rlc: (key, dt) of matrix 'rlc'."""
     nwin, n, stride = wins.shape
-    code = fecgpu.Code(scheme, k, r, matrix=matrix)
+    code = fecgpu.Code(scheme, k, r, matrix=matrix, rlc_key=rlc[0], rlc_dt=rlc[1])
     d = torch.from_numpy(wins.copy()).cuda()
     sl = torch.from_numpy(S.astype(np.int32)).cuda()
     kw = dict(sym_len=None, sym_len_all=int(S[0])) if uniform else dict(sym_len=sl)
@@ -68,12 +69,13 @@ def gpu_run(ctx, scheme, k, r, wins, S, present, uniform: bool, poison=0xAB, mat
     return enc, d.cpu().numpy(), status.cpu().numpy()
 
 
-def oracle_run(scheme, k, r, wins, S, present, poison=0xAB):
+def oracle_run(scheme, k, r, wins, S, present, poison=0xAB, oscheme=None):
+    osc = _scheme(scheme) if oscheme is None else oscheme
     enc = wins.copy()
-    O.encode_batch(_scheme(scheme), k, r, S, enc, 4)
+    O.encode_batch(osc, k, r, S, enc, 4)
     dec = enc.copy()
     O.erase(dec, present, k, r, fill=poison)
-    st = O.decode_batch(_scheme(scheme), k, r, S, dec, present, 4)
+    st = O.decode_batch(osc, k, r, S, dec, present, 4)
     return enc, dec, st
 
 
@@ -142,12 +144,13 @@ def test_golden_fixtures(ctx, path):
     z = np.load(path)
     scheme_id, k, r, L, era, nwin, w0, seed = (int(x) for x in z["meta"])
     scheme = "xor" if scheme_id == 0 else "gf256"
-    matrix = "vandermonde" if scheme_id == 2 else "cauchy"
+    matrix = {2: "vandermonde", 3: "rlc"}.get(scheme_id & 0xF, "cauchy")
+    rlc = ((scheme_id >> 8) & 0xFFFF, (scheme_id >> 4) & 0xF)
     stride = O.round_up(L, 16)
     wins = np.zeros((nwin, k + r, stride), np.uint8)
     wins[:, :k, :L] = z["src"]
     S = np.full(nwin, L, np.uint32)
-    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, z["present"], uniform=True, matrix=matrix)
+    ge, gd, gs = gpu_run(ctx, scheme, k, r, wins, S, z["present"], uniform=True, matrix=matrix, rlc=rlc)
     assert np.array_equal(ge[:, k:, :L], z["repair"])
     assert np.array_equal(gs, z["status"])
     ok = z["status"] == 0
@@ -648,3 +651,59 @@ def test_bitslice_ragged_and_split(ctx, k, r):
     ctx.encode_split(fecgpu.Code("gf256", k, r), src, rep, nwin=nwin, stride=1104, sym_len_all=1100)
     torch.cuda.synchronize()
     assert np.array_equal(rep.cpu().numpy()[:, :, :1100], oe[:, k:, :1100])
+
+
+# ---- FECGPU_MATRIX_RLC: RFC 8681 random linear code rows (tests/test_rlc_spec.py pins the
+# generator on CPU).  Not MDS: status is the rank of the present repairs on the missing
+# columns, which the plan finds by Gauss-Jordan with pivot search over every present repair.
+RLC_CASES = [
+    # k, r, key, dt, workload, L, erasure, nwin
+    (16, 4, 0, 15, 0, 1200, 1, 64),
+    (8, 2, 77, 15, 0, 1200, 2, 200),
+    (32, 8, 4660, 15, 1, 0, 2, 12),     # mixed MTU, LENPREFIX, i.i.d. erasures
+    (10, 6, 4660, 7, 0, 33, 2, 300),
+    (6, 6, 65535, 1, 0, 20, 2, 400),    # sparse: many singular windows
+    (12, 8, 9, 0, 0, 48, 2, 300),       # density 1/16
+    (56, 8, 65530, 3, 0, 64, 2, 40),    # repair keys wrap at 2^16
+    (1, 1, 5, 15, 0, 1, 1, 5),
+]
+
+
+@pytest.mark.parametrize("k,r,key,dt,wl,L,era,nwin", RLC_CASES)
+def test_rlc_encode_decode_vs_oracle(ctx, k, r, key, dt, wl, L, era, nwin):
+    S = O.sym_lens(wl, SEED, 0, nwin, k, L)
+    stride = O.round_up(int(S.max()), 16) + (16 if wl == 0 else 0)
+    wins = O.make_windows(wl, SEED, 0, nwin, k, r, L, stride)
+    osc = O.RLC(key, dt)
+    present = O.presents(era, SEED, 0, nwin, osc, k, r)
+    ge, gd, gs = gpu_run(ctx, "gf256", k, r, wins, S, present, uniform=(wl == 0), matrix="rlc",
+                         rlc=(key, dt))
+    oe, od, os_ = oracle_run("gf256", k, r, wins, S, present, oscheme=osc)
+    _cmp_emitted(ge, oe, S, "encode")
+    assert np.array_equal(gs, os_), np.argwhere(gs != os_)[:5].tolist()
+    _cmp_emitted(gd, od, S, "decode")
+    for w in range(nwin):
+        if gs[w] == 0:
+            s = int(S[w])
+            assert np.array_equal(gd[w, :k, :s], wins[w, :k, :s])
+
+
+@pytest.mark.parametrize("k,r,key,dt", [(4, 4, 3, 2), (5, 3, 77, 0), (4, 3, 9, 15), (3, 5, 1, 5)])
+def test_rlc_every_erasure_pattern(ctx, k, r, key, dt):
+    """All 2^(k+r) present masks: GPU status (pivoting plan over every present repair)
+    and bytes equal the oracle's (greedy independent repairs); recovered == original."""
+    n = k + r
+    nwin = 1 << n
+    L = 40
+    wins = O.make_windows(0, SEED, 11, 1, k, r, L, 48)
+    wins = np.repeat(wins, nwin, axis=0)
+    S = np.full(nwin, L, np.uint32)
+    present = np.arange(nwin, dtype=np.uint64)
+    osc = O.RLC(key, dt)
+    ge, gd, gs = gpu_run(ctx, "gf256", k, r, wins, S, present, uniform=True, matrix="rlc", rlc=(key, dt))
+    oe, od, os_ = oracle_run("gf256", k, r, wins, S, present, oscheme=osc)
+    _cmp_emitted(ge, oe, S, "encode")
+    assert np.array_equal(gs, os_)
+    _cmp_emitted(gd, od, S, "decode")
+    ok = gs == 0
+    assert np.array_equal(gd[ok, :k, :L], wins[ok, :k, :L])
