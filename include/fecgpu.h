@@ -333,6 +333,56 @@ ssize_t fecgpu_digest_batch(fecgpu_ctx *ctx, const fecgpu_code *code, const uint
                             const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
                             uint64_t w0, uint64_t nwin, uint64_t *digest, void *stream);
 
+/* ---- sliding-window random linear code (RFC 8681, m = 8) --------------
+ * SURVEY.md Appendix B q6 (window vs sliding-window coding).  Sources form a
+ * stream: src[i] is source symbol i of the batch (i < nsrc), `stride` bytes
+ * apart, S = sym_len bytes each (framing as A.3, done by the caller).  Repair
+ * symbol t is the GF(2^8) combination of the nss sources of its encoding
+ * window [fss, fss + nss) with the coefficients RFC 8681 §3.6 draws for
+ * (repair_key, nss, dt) from the RFC 8682 TinyMT32 PRNG: the REPAIR frame of
+ * RFC 8681 carries exactly these fields (repair_key, DT, NSS, FSS_ESI). */
+#define FECGPU_SW_MAX_WINDOW 255 /* nss limit (sources per encoding window) */
+#define FECGPU_SW_MAX_UNKNOWNS 64 /* decode: lost sources one linked system may hold */
+#define FECGPU_SW_MAX_EQUATIONS 96 /* decode: received repairs one linked system uses */
+
+typedef struct fecgpu_sw_repair {
+    uint64_t fss;        /* first source of the encoding window (index into the batch) */
+    uint16_t nss;        /* sources in the window, 1..FECGPU_SW_MAX_WINDOW */
+    uint16_t key;        /* RFC 8681 repair_key */
+    uint8_t  dt;         /* density threshold DT, 0..15 (15: every coefficient nonzero) */
+    uint8_t  reserved[3];
+} fecgpu_sw_repair;
+
+/* rep[t] (nrep rows of `stride` bytes) from the sources of hdr[t]'s window.
+ * src, rep and hdr are device pointers (FECGPU_F_HOST_PTRS: host memory,
+ * staged, synchronous).  max_window: the largest nss among the headers
+ * (1..FECGPU_SW_MAX_WINDOW; 0 = FECGPU_SW_MAX_WINDOW), which sizes the
+ * kernel's per-repair tables.  Device headers are not validated: a window
+ * reaching past nsrc or longer than max_window is clipped, dt > 15 counts as
+ * 15; host headers are checked (INVALID_ARG).  Returns nrep or a negative
+ * error. */
+ssize_t fecgpu_sw_encode(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_t *rep,
+                         const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t max_window,
+                         uint32_t sym_len, uint32_t stride, uint32_t flags, void *stream);
+
+/* Recovers lost sources in place.  The receiver's bookkeeping is host memory:
+ * src_present[i] / rep_present[t] nonzero = received, hdr[t] the repairs'
+ * headers (fss nondecreasing), src_status[i] out: 0 = present or recovered,
+ * 1 = still lost.  src / rep are device pointers (FECGPU_F_HOST_PTRS: host).
+ * Lost sources are split into linked systems (two lost sources are linked
+ * when a received repair's window holds both); each system is solved by
+ * Gauss-Jordan with pivot search over its received repairs on the GPU, and
+ * every lost source its repairs determine is recovered — also when the
+ * system as a whole is rank deficient.  A system of more than
+ * FECGPU_SW_MAX_UNKNOWNS lost sources stays lost (status 1); one with more
+ * than FECGPU_SW_MAX_EQUATIONS received repairs uses the first ones (in
+ * header order).  Synchronous on
+ * `stream`; returns the number of sources recovered, or a negative error. */
+ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_present, uint64_t nsrc,
+                         const uint8_t *rep, const uint8_t *rep_present,
+                         const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t sym_len,
+                         uint32_t stride, uint8_t *src_status, uint32_t flags, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

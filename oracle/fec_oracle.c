@@ -547,3 +547,104 @@ uint64_t orc_make_batch(int workload, uint64_t seed, uint64_t w0, uint64_t nwin,
     }
     return total;
 }
+
+/* ------------------------------------------ sliding-window RLC (RFC 8681) --- */
+/* a5 for the sliding-window scheme: repair t combines
+ * the nss_t sources of its encoding window with RFC 8681 §3.6 coefficients. */
+void orc_sw_encode(const uint8_t *src, uint64_t nsrc, uint32_t S, uint32_t stride,
+                   const orc_sw_repair *hdr, uint64_t nrep, uint8_t *rep) {
+    uint8_t cc[256];
+    (void)nsrc;
+    for (uint64_t t = 0; t < nrep; t++) {
+        uint8_t *out = rep + t * stride;
+        memset(out, 0, S);
+        orc_rlc_coefs(hdr[t].key, hdr[t].nss, hdr[t].dt, cc);
+        for (int j = 0; j < hdr[t].nss; j++) {
+            const uint8_t *s = src + (hdr[t].fss + (uint64_t)j) * stride;
+            for (uint32_t b = 0; b < S; b++) out[b] ^= orc_gf_mul(cc[j], s[b]);
+        }
+    }
+}
+
+/* a7 for the sliding-window scheme: unknowns = lost sources, equations = the
+ * received repairs whose windows hold at least one unknown, with right-hand
+ * side s_t = rep_t + sum over the window's received sources of cc * src.
+ * Gauss-Jordan with pivot search on [A | I]; a pivot column is determined iff
+ * its pivot row is zero on every free column, and then x = (I part) * s. */
+int64_t orc_sw_decode(uint8_t *src, const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep,
+                      const uint8_t *rep_present, const orc_sw_repair *hdr, uint64_t nrep,
+                      uint32_t S, uint32_t stride, uint8_t *status) {
+    int64_t e = 0;
+    for (uint64_t i = 0; i < nsrc; i++) {
+        status[i] = src_present[i] ? 0 : 1;
+        e += !src_present[i];
+    }
+    if (e == 0) return 0;
+    if (e > 4096) return -1;
+    int64_t *unk = malloc(sizeof(int64_t) * e), *col = malloc(sizeof(int64_t) * nsrc);
+    e = 0;
+    for (uint64_t i = 0; i < nsrc; i++) {
+        col[i] = -1;
+        if (!src_present[i]) { col[i] = e; unk[e++] = (int64_t)i; }
+    }
+    int64_t *eq = malloc(sizeof(int64_t) * (nrep ? nrep : 1)), p = 0;
+    uint8_t cc[256];
+    for (uint64_t t = 0; t < nrep; t++) {
+        if (!rep_present[t]) continue;
+        int any = 0;
+        for (int j = 0; j < hdr[t].nss; j++) any |= col[hdr[t].fss + j] >= 0;
+        if (any) eq[p++] = (int64_t)t;
+    }
+    const int64_t w = e + p;
+    uint8_t *M = calloc((size_t)p * w, 1), *s = calloc((size_t)p * S, 1);
+    for (int64_t q = 0; q < p; q++) {
+        const orc_sw_repair *h = &hdr[eq[q]];
+        orc_rlc_coefs(h->key, h->nss, h->dt, cc);
+        memcpy(s + q * S, rep + eq[q] * stride, S);
+        for (int j = 0; j < h->nss; j++) {
+            const uint64_t i = h->fss + j;
+            if (col[i] >= 0) { M[q * w + col[i]] = cc[j]; continue; }
+            for (uint32_t b = 0; b < S; b++) s[q * S + b] ^= orc_gf_mul(cc[j], src[i * stride + b]);
+        }
+        M[q * w + e + q] = 1;
+    }
+    int64_t *pivrow = malloc(sizeof(int64_t) * e), nused = 0;
+    char *isfree = calloc(e, 1);
+    for (int64_t c = 0; c < e; c++) {
+        int64_t pr = -1;
+        for (int64_t q = nused; q < p; q++)
+            if (M[q * w + c]) { pr = q; break; }
+        if (pr < 0) { isfree[c] = 1; pivrow[c] = -1; continue; }
+        if (pr != nused)
+            for (int64_t j = 0; j < w; j++) { uint8_t x = M[pr * w + j]; M[pr * w + j] = M[nused * w + j]; M[nused * w + j] = x; }
+        pr = nused++;
+        const uint8_t iv = orc_gf_inv(M[pr * w + c]);
+        for (int64_t j = 0; j < w; j++) M[pr * w + j] = orc_gf_mul(M[pr * w + j], iv);
+        for (int64_t q = 0; q < p; q++) {
+            const uint8_t f = M[q * w + c];
+            if (q == pr || !f) continue;
+            for (int64_t j = 0; j < w; j++) M[q * w + j] ^= orc_gf_mul(f, M[pr * w + j]);
+        }
+        pivrow[c] = pr;
+    }
+    int64_t rec = 0;
+    for (int64_t c = 0; c < e; c++) {
+        if (isfree[c]) continue;
+        const int64_t pr = pivrow[c];
+        int det = 1;
+        for (int64_t j = 0; j < e; j++)
+            if (isfree[j] && M[pr * w + j]) { det = 0; break; }
+        if (!det) continue;
+        uint8_t *out = src + unk[c] * stride;
+        memset(out, 0, S);
+        for (int64_t q = 0; q < p; q++) {
+            const uint8_t f = M[pr * w + e + q];
+            if (!f) continue;
+            for (uint32_t b = 0; b < S; b++) out[b] ^= orc_gf_mul(f, s[q * S + b]);
+        }
+        status[unk[c]] = 0;
+        rec++;
+    }
+    free(unk); free(col); free(eq); free(M); free(s); free(pivrow); free(isfree);
+    return rec;
+}

@@ -107,6 +107,27 @@ uint64_t orc_make_batch(int workload, uint64_t seed, uint64_t w0, uint64_t nwin,
                         int erasure, int k, int r, uint32_t L, uint32_t stride, uint8_t *wins,
                         uint32_t *S, uint64_t *present, int nthreads);
 
+/* ---- sliding-window RLC (RFC 8681, m = 8): fecgpu_sw_encode / _decode ----
+ * Same header layout as fecgpu_sw_repair. */
+typedef struct orc_sw_repair {
+    uint64_t fss;
+    uint16_t nss;
+    uint16_t key;
+    uint8_t  dt;
+    uint8_t  reserved[3];
+} orc_sw_repair;
+
+/* rep[t] = sum_{j < nss_t} cc_t[j] * src[fss_t + j] over bytes [0, S) */
+void    orc_sw_encode(const uint8_t *src, uint64_t nsrc, uint32_t S, uint32_t stride,
+                      const orc_sw_repair *hdr, uint64_t nrep, uint8_t *rep);
+/* Global Gauss-Jordan over every lost source (unknown) and every received
+ * repair that covers one; recovers each determined unknown in place;
+ * status[i] = 0 present / recovered, 1 lost.  Returns #recovered, or -1 if
+ * there are more than 4096 unknowns (a test-size oracle). */
+int64_t orc_sw_decode(uint8_t *src, const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep,
+                      const uint8_t *rep_present, const orc_sw_repair *hdr, uint64_t nrep,
+                      uint32_t S, uint32_t stride, uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -335,3 +335,74 @@ def deframe(sym: np.ndarray) -> np.ndarray:
     """a9: LENPREFIX symbol -> packet payload."""
     n = (int(sym[0]) << 8) | int(sym[1])
     return sym[2:2 + n]
+
+
+# ------------------------------------------------- sliding-window RLC ---
+def sw_encode(src: np.ndarray, hdr) -> np.ndarray:
+    """RFC 8681 sliding-window repairs: rep[t] = sum_j cc_t[j] * src[fss_t + j]
+    (hdr: iterable of (fss, nss, key, dt)); src [nsrc, L]."""
+    reps = []
+    for fss, nss, key, dt in hdr:
+        cc = rlc_coefs(key, nss, dt)
+        reps.append(matmul(cc[None, :], src[fss:fss + nss])[0])
+    return np.array(reps, np.uint8).reshape(len(reps), src.shape[1])
+
+
+def sw_decode(src: np.ndarray, src_present, rep: np.ndarray, rep_present, hdr):
+    """Recover what the received repairs determine, by elimination of the data
+    itself: rows [A | s] with s = rep + known-source terms (A: coefficients of
+    the lost sources), reduced to row echelon form with pivot search; a lost
+    source is determined iff its pivot row is zero on every free column.
+    -> (sources [nsrc, L], status per source: 0 present/recovered, 1 lost)."""
+    src = src.copy()
+    nsrc, L = src.shape
+    lost = [i for i in range(nsrc) if not src_present[i]]
+    col = {s: c for c, s in enumerate(lost)}
+    status = np.array([0 if src_present[i] else 1 for i in range(nsrc)], np.uint8)
+    e = len(lost)
+    rows = []
+    for t, (fss, nss, key, dt) in enumerate(hdr):
+        if not rep_present[t] or not any((fss + j) in col for j in range(nss)):
+            continue
+        cc = rlc_coefs(key, nss, dt)
+        a = np.zeros(e, np.uint8)
+        s = rep[t].copy()
+        for j in range(nss):
+            i = fss + j
+            if i in col:
+                a[col[i]] = cc[j]
+            elif cc[j]:
+                s ^= _MUL[cc[j]][src[i]]
+        rows.append(np.concatenate([a, s]))
+    if not rows or e == 0:
+        return src, status
+    M = np.array(rows, np.uint8)
+    pivots, r = {}, 0
+    for c in range(e):
+        piv = next((i for i in range(r, len(M)) if M[i, c]), None)
+        if piv is None:
+            continue
+        M[[r, piv]] = M[[piv, r]]
+        M[r] = _MUL[_INV[M[r, c]]][M[r]]
+        for i in range(len(M)):
+            if i != r and M[i, c]:
+                M[i] ^= _MUL[M[i, c]][M[r]]
+        pivots[c] = r
+        r += 1
+    free = [c for c in range(e) if c not in pivots]
+    for c, pr in pivots.items():
+        if all(M[pr, f] == 0 for f in free):
+            src[lost[c]] = M[pr, e:]
+            status[lost[c]] = 0
+    return src, status
+
+
+def sw_schedule(nsrc: int, k: int, W: int, key0: int = 0, dt: int = 15):
+    """A repair after every k sources over the last W (RFC 8681 sliding window):
+    repair t covers [max(0, (t+1)k - W), (t+1)k), repair_key key0 + t."""
+    hdr = []
+    for t in range(nsrc // k):
+        end = (t + 1) * k
+        fss = max(0, end - W)
+        hdr.append((fss, end - fss, (key0 + t) & 0xFFFF, dt))
+    return hdr

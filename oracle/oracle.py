@@ -56,6 +56,8 @@ def lib():
             "orc_matrix": (None, [i32, i32, i32, vp]),
             "orc_tinymt32": (None, [u32, i32, vp]),
             "orc_rlc_coefs": (i32, [u32, i32, i32, vp]),
+            "orc_sw_encode": (None, [vp, u64, u32, u32, vp, u64, vp]),
+            "orc_sw_decode": (ctypes.c_int64, [vp, vp, u64, vp, vp, vp, u64, u32, u32, vp]),
             "orc_sm64": (u64, [u64]),
             "orc_pkt_len": (u32, [i32, u64, u64, i32, i32, u32]),
             "orc_sym_len": (u32, [i32, u64, u64, i32, u32]),
@@ -127,6 +129,28 @@ def rlc_coefs(key: int, n: int, dt: int) -> np.ndarray:
     cc = np.zeros(n, np.uint8)
     assert lib().orc_rlc_coefs(key, n, dt, _p(cc)) == 0
     return cc
+
+
+SW_REPAIR_DTYPE = [("fss", "<u8"), ("nss", "<u2"), ("key", "<u2"), ("dt", "u1"), ("reserved", "u1", (3,))]
+
+
+def sw_encode(src: np.ndarray, hdr: np.ndarray, S: int) -> np.ndarray:
+    """Sliding-window RLC repairs [nrep, stride] of src [nsrc, stride] (headers SW_REPAIR_DTYPE)."""
+    nsrc, stride = src.shape
+    rep = np.zeros((len(hdr), stride), np.uint8)
+    src = np.ascontiguousarray(src)
+    lib().orc_sw_encode(_p(src), nsrc, S, stride, _p(hdr), len(hdr), _p(rep))
+    return rep
+
+
+def sw_decode(src: np.ndarray, src_present: np.ndarray, rep: np.ndarray, rep_present: np.ndarray,
+              hdr: np.ndarray, S: int):
+    """In place on src; -> (status per source, number recovered)."""
+    nsrc, stride = src.shape
+    st = np.zeros(nsrc, np.uint8)
+    n = lib().orc_sw_decode(_p(src), _p(src_present), nsrc, _p(rep), _p(rep_present), _p(hdr),
+                            len(hdr), S, stride, _p(st))
+    return st, int(n)
 
 
 def sm64(x: int) -> int:

@@ -160,6 +160,9 @@ struct fecgpu_ctx {
     // FECGPU_CHECK builds: bytes taken off the end of every checked range, so a
     // test can see the checker fire on a correct kernel ("check_shrink")
     int check_shrink = 0;
+    // sliding-window calls: device scratch slots and the last call's end event, per device
+    std::map<int, std::vector<std::pair<void *, size_t>>> sw_scratch;
+    std::map<int, hipEvent_t> sw_event;
 };
 
 extern "C" {
@@ -321,6 +324,16 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
         (void)hipFree(kv.second.first);
     }
     for (auto &kv : ctx->pinned_cache) (void)hipHostFree(kv.second);
+    for (auto &kv : ctx->sw_scratch) {
+        (void)hipSetDevice(kv.first);
+        (void)hipDeviceSynchronize();
+        for (auto &b : kv.second)
+            if (b.first) (void)hipFree(b.first);
+    }
+    for (auto &kv : ctx->sw_event) {
+        (void)hipSetDevice(kv.first);
+        (void)hipEventDestroy(kv.second);
+    }
     for (auto &kv : ctx->conn_streams) {
         (void)hipSetDevice(kv.first);
         for (hipStream_t st : kv.second) {
@@ -936,6 +949,51 @@ ssize_t ctx_pinned_get(fecgpu_ctx *ctx, size_t bytes, void **host) {
         }
     }
     HIP_TRY(hipHostMalloc(host, bytes, hipHostMallocDefault), "hipHostMalloc");
+    return 0;
+}
+
+ssize_t set_dev_error(hipError_t e, const char *what) { return dev_err(e, what); }
+
+int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget) {
+    return choose_wpb(ncol, lds_per_unit, lds_budget);
+}
+
+ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    std::vector<std::pair<void *, size_t>> &v = ctx->sw_scratch[dev];
+    if ((int)v.size() <= slot) v.resize(slot + 1, {nullptr, 0});
+    auto &b = v[slot];
+    if (b.second < bytes) {
+        const size_t want = std::max(bytes, b.second + b.second / 2);
+        if (b.first) HIP_TRY(hipFree(b.first), "hipFree");
+        b = {nullptr, 0};
+        HIP_TRY(hipMalloc(&b.first, want), "hipMalloc sw scratch");
+        b.second = want;
+    }
+    *p = b.first;
+    return 0;
+}
+
+ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    auto it = ctx->sw_event.find(dev);
+    if (it == ctx->sw_event.end()) {
+        hipEvent_t ev = nullptr;
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+        HIP_TRY(hipEventRecord(ev, s), "hipEventRecord");
+        ctx->sw_event[dev] = ev;
+        return 0;
+    }
+    HIP_TRY(hipStreamWaitEvent(s, it->second, 0), "hipStreamWaitEvent");
+    return 0;
+}
+
+ssize_t ctx_sw_end(fecgpu_ctx *ctx, hipStream_t s) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    HIP_TRY(hipEventRecord(ctx->sw_event[dev], s), "hipEventRecord");
     return 0;
 }
 

@@ -132,4 +132,100 @@ struct DigestArgs {
 };
 hipError_t launch_digest(const DigestArgs &a, hipStream_t s);
 
+// ---- sliding-window RLC (fecgpu_sw_*, fec_sw.cpp) ----------------------
+// A combine job makes nout <= R output rows, each a GF(2^8) combination of
+// nin contiguous input rows: repair generation (one output, the window's
+// sources), decode syndromes (one output, xor of the received repair) and
+// decode solves (up to 8 recovered sources from a system's syndromes).
+struct CombJob {
+    uint64_t in_off;    // input row q at in_base + in_off + q * stride
+    uint64_t coef_off;  // coefficient bytes [nout][nin] at coef + coef_off
+    uint64_t out_list;  // output u at out_base + outs[out_list + u]
+    uint64_t xor_off;   // kNoXor, or every output ^= the row at xor_base + xor_off
+    uint32_t nin, nout;
+};
+constexpr uint64_t kNoXor = ~0ull;
+constexpr int kSwMaxWindow = FECGPU_SW_MAX_WINDOW;
+constexpr int kSwMaxUnknowns = FECGPU_SW_MAX_UNKNOWNS;
+constexpr int kSwMaxEq = FECGPU_SW_MAX_EQUATIONS;
+constexpr uint32_t kSwCoefPitch = 256;  // coefficient bytes per repair job
+
+struct CombArgs {
+    const CombJob *jobs;
+    const uint8_t *coef;
+    const uint64_t *outs;
+    const uint8_t *in_base;
+    uint8_t *out_base;
+    const uint8_t *xor_base;
+    uint64_t njobs;
+    uint32_t ncol, stride;
+    int wpb, nin_max, nout_max;
+    uint32_t job_lds;
+    uint32_t nx;
+};
+// LDS bytes per job of comb_kernel<R> at nin_max inputs
+inline uint32_t comb_job_lds(int nin_max, int R) {
+    const uint32_t rt = R == 1 ? 1u : (uint32_t)(R + 3) & ~3u;
+    return ((uint32_t)nin_max * (16u * R + 4u * rt) + 8u * R + 8u + 15u) & ~15u;
+}
+hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
+
+// encode: job t = repair t (coefficients at coef + t * kSwCoefPitch, output rep row t)
+struct SwEncCoefArgs {
+    const fecgpu_sw_repair *hdr;
+    uint64_t nrep, nsrc;
+    uint32_t stride;
+    int max_window;
+    CombJob *jobs;
+    uint8_t *coef;
+    uint64_t *outs;
+};
+hipError_t launch_sw_enc_coef(const SwEncCoefArgs &a, hipStream_t s);
+
+// one linked system of a decode: lost sources unk[u_off ..+ e) (ascending),
+// received repairs eqh[q_off ..+ p) (their syndromes: scratch rows q_off..),
+// A [p][e] at amat + a_off, solve jobs jobs[j_off ..+ ceil(e / 8)] with
+// coefficients at coef + t_off ([round_up(e, 8)][p]) and outputs outs[o_off + d]
+struct SwComp {
+    uint64_t u_off, q_off, a_off, j_off, t_off, o_off;
+    uint32_t e, p;
+};
+struct SwSynArgs {  // thread per equation: syndrome coefficients and jobs, and A
+    const fecgpu_sw_repair *eqh;  // headers of the equations (compact copies)
+    const uint64_t *eqr;          // their repair indices
+    const uint32_t *eqc;          // their systems
+    const SwComp *comps;
+    const uint64_t *unk;
+    uint64_t neq;
+    uint32_t stride;
+    CombJob *jobs;
+    uint8_t *coef;
+    uint64_t *outs;
+    uint8_t *amat;
+};
+hipError_t launch_sw_syn(const SwSynArgs &a, hipStream_t s);
+struct SwPlanArgs {  // wave per system: Gauss-Jordan, solve jobs, per-unknown status
+    const SwComp *comps;
+    uint64_t ncomp;
+    const uint8_t *amat;
+    const uint64_t *unk;
+    uint32_t stride;
+    CombJob *jobs;
+    uint8_t *coef;
+    uint64_t *outs;
+    uint8_t *ustat;
+};
+hipError_t launch_sw_plan(const SwPlanArgs &a, hipStream_t s);
+
+// fec_capi.cpp services for fec_sw.cpp: the thread's FECGPU_ERR_DEVICE text,
+// the group-size choice of the block kernels, device scratch slots of the ctx
+// (current device, grown on demand, contents not kept), and the ordering of
+// sliding-window calls on one ctx (begin: `s` waits for the previous call's
+// end; end: records it), which share that scratch.
+ssize_t set_dev_error(hipError_t e, const char *what);
+int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget);
+ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p);
+ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);
+ssize_t ctx_sw_end(fecgpu_ctx *ctx, hipStream_t s);
+
 }  // namespace fecgpu

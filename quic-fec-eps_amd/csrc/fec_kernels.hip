@@ -1529,6 +1529,280 @@ __global__ __launch_bounds__(kBlock) void digest_kernel(DigestArgs a) {
     }
 }
 
+// ================================================ sliding-window RLC ===
+// RFC 8681 sliding-window random linear code (include/fecgpu.h fecgpu_sw_*).
+// Every data pass is a combine job (fec_internal.h CombJob): nout <= R outputs
+// over nin contiguous input rows, multiply tables built per job in LDS from
+// its coefficient bytes, the job's 16-B columns streamed by the workgroup like
+// the block kernels' group mode.  Coefficients come from the RFC 8682 PRNG on
+// the device (one lane per repair), the decode's linked systems are reduced
+// by one wave each (Gauss-Jordan with pivot search).
+
+// Per-job LDS region of comb_kernel<R>: tables [nin_max][R] uint4 (TA/TB),
+// [nin_max][RT] u32 (TC), output column-0 pointers [R], xor pointer.
+template <int R>
+struct CombRegion {
+    static constexpr int RT = R == 1 ? 1 : ((R + 3) & ~3);
+    uint4 *ab;
+    uint32_t *tc;
+    uint64_t *optr;  // [R] + xor pointer at optr[R]
+    __device__ __forceinline__ CombRegion(uint8_t *region, int nin_max) {
+        ab = reinterpret_cast<uint4 *>(region);
+        tc = reinterpret_cast<uint32_t *>(region + (size_t)nin_max * R * 16);
+        optr = reinterpret_cast<uint64_t *>(region + (size_t)nin_max * (16 * R + 4 * RT));
+    }
+};
+
+// One slot (job, 16-B column) for NE outputs (wave-uniform): acc[u] = sum_q
+// T[q][u] * in_q over the job's nin rows (8 loads in flight), optional xor
+// row, stores for u < ne (this lane's job).
+template <int R, int NE>
+__device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, int nin, int ne, uint32_t col,
+                                          const CombRegion<R> &rg) {
+    constexpr int U = 8, RT = CombRegion<R>::RT;
+    uint4 acc[NE];
+#pragma unroll
+    for (int m = 0; m < NE; m++) acc[m] = zero4();
+    for (int q0 = 0; q0 < nin; q0 += U) {
+        uint4 v[U];
+#pragma unroll
+        for (int t = 0; t < U; t++) v[t] = ld16(in + (uint32_t)min(q0 + t, nin - 1) * stride);
+#pragma unroll
+        for (int t = 0; t < U; t++) {
+            if (q0 + t < nin) {
+                const int q = q0 + t;
+                const Split sp = split(v[t]);
+#pragma unroll
+                for (int m = 0; m < NE; m++) gmac(acc[m], sp, rg.ab[q * R + m], rg.tc[q * RT + m]);
+            }
+        }
+    }
+    const uint64_t xp = rg.optr[R];
+    if (xp) acc[0] = xor4(acc[0], ld16(reinterpret_cast<const uint8_t *>(xp) + col * 16u));
+#pragma unroll
+    for (int m = 0; m < NE; m++)
+        if (m < ne) st16(reinterpret_cast<uint8_t *>(rg.optr[m]) + col * 16u, acc[m]);
+}
+
+template <int R, int NE = R>
+__device__ __forceinline__ void comb_dispatch(int nw, const uint8_t *in, uint32_t stride, int nin, int ne,
+                                              uint32_t col, const CombRegion<R> &rg) {
+    if constexpr (NE >= 1) {
+        if (nw == NE) comb_slot<R, NE>(in, stride, nin, ne, col, rg);
+        else comb_dispatch<R, NE - 1>(nw, in, stride, nin, ne, col, rg);
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
+    extern __shared__ uint4 dyn[];
+    __shared__ uint32_t s_pfx[kMaxWpb + 1];
+    __shared__ uint64_t s_in[kMaxWpb];
+    __shared__ uint32_t s_nin[kMaxWpb];
+    __shared__ uint8_t s_ne[kMaxWpb], s_perm[kMaxWpb];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint8_t *regions = reinterpret_cast<uint8_t *>(dyn);
+    constexpr int RT = CombRegion<R>::RT;
+    for (XcdRange xr = xcd_range((a.njobs + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+        const uint64_t j0 = xr.cur * a.wpb;
+        const int nb = (int)min((uint64_t)a.wpb, a.njobs - j0);
+        // plan: wave w builds the tables of jobs w, w + 4, ...
+        for (int jl = wave; jl < nb; jl += kBlock / 64) {
+            const CombJob J = a.jobs[j0 + jl];
+            const int nin = min((int)J.nin, a.nin_max), nout = min((int)J.nout, R);
+            const CombRegion<R> rg(regions + (size_t)jl * a.job_lds, a.nin_max);
+            const uint8_t *cf = a.coef + J.coef_off;
+            for (int i = lane; i < nout * nin; i += 64) {
+                const int u = i / nin, q = i - u * nin;
+                const CoefTab ct = make_coef_tab(cf[i]);
+                rg.ab[q * R + u] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+                rg.tc[q * RT + u] = ct.c;
+            }
+            if (lane < nout) rg.optr[lane] = reinterpret_cast<uint64_t>(a.out_base) + a.outs[J.out_list + lane];
+            if (lane == 0) {
+                rg.optr[R] = J.xor_off == kNoXor ? 0ull : reinterpret_cast<uint64_t>(a.xor_base) + J.xor_off;
+                s_in[jl] = reinterpret_cast<uint64_t>(a.in_base) + J.in_off;
+                s_nin[jl] = (uint32_t)nin;
+                s_ne[jl] = (uint8_t)nout;
+            }
+        }
+        __syncthreads();
+        if (tid < 64) {
+            // jobs in descending order of outputs (comb_slot runs the wave's largest)
+            const int t = tid;
+            const int ne_t = t < nb ? (int)s_ne[t] : -1;
+            const uint64_t below = (1ull << t) - 1;
+            int rank = 0;
+#pragma unroll
+            for (int v = R; v >= 0; v--) {
+                const uint64_t b = __ballot(ne_t == v);
+                if (v > ne_t) rank += __popcll(b);
+                else if (v == ne_t) rank += __popcll(b & below);
+            }
+            if (t < nb) s_perm[rank] = (uint8_t)t;
+            WAVE_SYNC();
+            const int jl = t < nb ? (int)s_perm[t] : 0;
+            block_prefix(s_pfx, (t < nb && s_ne[jl]) ? a.ncol : 0u, t);
+        }
+        __syncthreads();
+        const uint32_t total = s_pfx[nb];
+        int i = 0;
+        for (uint32_t s = tid; s < total; s += kBlock) {
+            while (s >= s_pfx[i + 1]) i++;
+            const int jl = s_perm[i];
+            const uint32_t col = s - s_pfx[i];
+            const int ne = s_ne[jl];
+            const int nw = __builtin_amdgcn_readfirstlane(ne);
+            const CombRegion<R> rg(regions + (size_t)jl * a.job_lds, a.nin_max);
+            comb_dispatch<R>(nw, reinterpret_cast<const uint8_t *>(s_in[jl]) + col * 16u, a.stride,
+                             (int)s_nin[jl], ne, col, rg);
+        }
+        __syncthreads();
+    }
+}
+
+// Encode: lane per repair — clip the window to the batch, draw its RFC 8681
+// coefficients, write its job (output: repair row t).
+__global__ __launch_bounds__(kBlock) void sw_enc_coef_kernel(SwEncCoefArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= a.nrep) return;
+    const fecgpu_sw_repair h = a.hdr[t];
+    const uint64_t fss = min(h.fss, a.nsrc);
+    const int nss = (int)min((uint64_t)min((int)h.nss, a.max_window), a.nsrc - fss);
+    uint8_t *cc = a.coef + t * kSwCoefPitch;
+    (void)rlc_coefs(h.key, nss, min((uint32_t)h.dt, 15u), cc);
+    CombJob J;
+    J.in_off = fss * a.stride;
+    J.coef_off = t * kSwCoefPitch;
+    J.out_list = t;
+    J.xor_off = kNoXor;
+    J.nin = (uint32_t)nss;
+    J.nout = 1;
+    a.jobs[t] = J;
+    a.outs[t] = t * a.stride;
+}
+
+// Decode, lane per equation g (a received repair of system c): coefficients
+// of its window with the system's lost sources zeroed (the syndrome job:
+// s_g = rep + sum of the received sources' terms, into scratch row g), and the
+// lost sources' coefficients into row g - q_off of the system's A [p][e].
+__global__ __launch_bounds__(kBlock) void sw_syn_kernel(SwSynArgs a) {
+    const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= a.neq) return;
+    const fecgpu_sw_repair h = a.eqh[g];
+    const SwComp c = a.comps[a.eqc[g]];
+    const uint64_t *U = a.unk + c.u_off;
+    uint8_t *cc = a.coef + g * kSwCoefPitch;
+    uint8_t *arow = a.amat + c.a_off + (g - c.q_off) * c.e;
+    const int nss = min((int)h.nss, kSwMaxWindow);
+    (void)rlc_coefs(h.key, nss, min((uint32_t)h.dt, 15u), cc);
+    for (uint32_t u = 0; u < c.e; u++) arow[u] = 0;
+    uint32_t u = 0;
+    for (int j = 0; j < nss; j++) {
+        const uint64_t i = h.fss + j;
+        while (u < c.e && U[u] < i) u++;
+        if (u < c.e && U[u] == i) {
+            arow[u] = cc[j];
+            cc[j] = 0;
+        }
+    }
+    CombJob J;
+    J.in_off = h.fss * a.stride;
+    J.coef_off = g * kSwCoefPitch;
+    J.out_list = g;
+    J.xor_off = a.eqr[g] * a.stride;
+    J.nin = (uint32_t)nss;
+    J.nout = 1;
+    a.jobs[g] = J;
+    a.outs[g] = g * a.stride;
+}
+
+// Decode, wave per linked system: Gauss-Jordan with pivot search on [A | I]
+// (p <= 96 rows, e <= 64 unknowns; row pitch 160 in LDS).  Column c with no
+// pivot is free; unknown c is determined iff its pivot row is zero on every
+// free column, and then x_c = sum_t M[P_c][e + t] * s_t.  Writes the solve
+// jobs (8 determined unknowns each, inputs = the system's syndrome rows), their
+// coefficient rows and output rows, and every unknown's status.
+constexpr int kSwPitch = kSwMaxUnknowns + kSwMaxEq;
+__global__ __launch_bounds__(kBlock) void sw_plan_kernel(SwPlanArgs a) {
+    extern __shared__ uint4 dyn[];
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ int8_t s_piv[kBlock / 64][kSwMaxUnknowns];  // pivot row of column c, -1 free
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
+    for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
+    __syncthreads();
+    const uint64_t ci = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+    if (ci >= a.ncomp) return;  // no block-wide barrier below
+    const SwComp c = a.comps[ci];
+    const int e = (int)c.e, p = (int)c.p, W = e + p;
+    uint8_t *M = reinterpret_cast<uint8_t *>(dyn) + (size_t)wave * kSwMaxEq * kSwPitch;
+    int8_t *piv = s_piv[wave];
+    const uint8_t *A = a.amat + c.a_off;
+    for (int q = 0; q < p; q++)
+        for (int j = lane; j < W; j += 64) M[q * kSwPitch + j] = j < e ? A[q * e + j] : (uint8_t)(j - e == q);
+    WAVE_SYNC();
+    uint64_t used0 = 0, used1 = 0;  // wave-uniform: rows 0..63, 64..95 already pivots
+    for (int col = 0; col < e; col++) {
+        const bool c0 = lane < p && !((used0 >> lane) & 1) && M[lane * kSwPitch + col] != 0;
+        const bool c1 = lane + 64 < p && !((used1 >> lane) & 1) && M[(lane + 64) * kSwPitch + col] != 0;
+        const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
+        int pr = -1;
+        if (b0) pr = (int)__ffsll((unsigned long long)b0) - 1;
+        else if (b1) pr = 64 + (int)__ffsll((unsigned long long)b1) - 1;
+        if (lane == 0) piv[col] = (int8_t)pr;
+        if (pr < 0) continue;  // free column (uniform)
+        if (pr < 64) used0 |= 1ull << pr;
+        else used1 |= 1ull << (pr - 64);
+        uint8_t *P = M + pr * kSwPitch;
+        const uint32_t iv = gf_inv_lds(s_exp, s_log, P[col]);
+        WAVE_SYNC();
+        for (int j = lane; j < W; j += 64) P[j] = (uint8_t)gf_mul_lds(s_exp, s_log, P[j], iv);
+        WAVE_SYNC();
+        for (int q = lane; q < p; q += 64) {
+            if (q == pr) continue;
+            uint8_t *row = M + q * kSwPitch;
+            const uint32_t f = row[col];
+            if (!f) continue;
+            for (int j = 0; j < W; j++) row[j] ^= (uint8_t)gf_mul_lds(s_exp, s_log, f, P[j]);
+        }
+        WAVE_SYNC();
+    }
+    WAVE_SYNC();
+    // determined unknowns (lane c), compacted in column order
+    bool det = false;
+    int prc = -1;
+    if (lane < e) {
+        prc = piv[lane];
+        det = prc >= 0;
+        for (int j = 0; j < e && det; j++)
+            if (piv[j] < 0 && M[prc * kSwPitch + j]) det = false;
+    }
+    const uint64_t dm = __ballot(det);
+    const int ndet = __popcll(dm);
+    if (lane < e) {
+        a.ustat[c.u_off + lane] = det ? 0 : 1;
+        if (det) {
+            const int d = __popcll(dm & ((1ull << lane) - 1));
+            uint8_t *cf = a.coef + c.t_off + (uint64_t)d * p;
+            for (int t = 0; t < p; t++) cf[t] = M[prc * kSwPitch + e + t];
+            a.outs[c.o_off + d] = a.unk[c.u_off + lane] * a.stride;
+        }
+    }
+    const int njob = (e + 7) / 8;
+    if (lane < njob) {
+        CombJob J;
+        J.in_off = c.q_off * a.stride;
+        J.coef_off = c.t_off + (uint64_t)lane * 8 * p;
+        J.out_list = c.o_off + (uint64_t)lane * 8;
+        J.xor_off = kNoXor;
+        J.nin = (uint32_t)p;
+        J.nout = (uint32_t)max(0, min(8, ndet - 8 * lane));
+        a.jobs[c.j_off + lane] = J;
+    }
+}
+
 // ========================================================== launchers ===
 namespace {
 
@@ -1681,6 +1955,40 @@ hipError_t launch_erasure(const EraseArgs &a, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     hipLaunchKernelGGL(erasure_kernel, dim3((unsigned)((a.nwin + kBlock - 1) / kBlock)), dim3(kBlock),
                        0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_comb(CombArgs a, int R, hipStream_t s) {
+    if (a.njobs == 0) return hipSuccess;
+    const uint64_t groups = (a.njobs + a.wpb - 1) / a.wpb;
+    a.nx = groups >= 8 ? 8 : 1;
+    const uint64_t grid = (groups + a.nx - 1) / a.nx * a.nx;  // one group per workgroup
+    const uint32_t lds = a.job_lds * (uint32_t)a.wpb;
+    switch (R) {
+        case 1: hipLaunchKernelGGL(comb_kernel<1>, dim3((unsigned)grid), dim3(kBlock), lds, s, a); break;
+        case 8: hipLaunchKernelGGL(comb_kernel<8>, dim3((unsigned)grid), dim3(kBlock), lds, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_sw_enc_coef(const SwEncCoefArgs &a, hipStream_t s) {
+    if (a.nrep == 0) return hipSuccess;
+    hipLaunchKernelGGL(sw_enc_coef_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sw_syn(const SwSynArgs &a, hipStream_t s) {
+    if (a.neq == 0) return hipSuccess;
+    hipLaunchKernelGGL(sw_syn_kernel, dim3((unsigned)((a.neq + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sw_plan(const SwPlanArgs &a, hipStream_t s) {
+    if (a.ncomp == 0) return hipSuccess;
+    constexpr int per = kBlock / 64;
+    const uint32_t lds = (uint32_t)per * kSwMaxEq * kSwPitch;
+    hipLaunchKernelGGL(sw_plan_kernel, dim3((unsigned)((a.ncomp + per - 1) / per)), dim3(kBlock), lds, s, a);
     return hipGetLastError();
 }
 

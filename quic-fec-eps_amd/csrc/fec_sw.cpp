@@ -1,0 +1,322 @@
+// fec_sw.cpp — sliding-window random linear code entry points (include/fecgpu.h
+// fecgpu_sw_encode / fecgpu_sw_decode; RFC 8681 with m = 8; SURVEY.md Appendix
+// B q6).  Host side: argument checks, staging, the decode's split of the lost
+// sources into linked systems, and the launches of fec_kernels.hip's
+// sliding-window kernels.  No CPU fallback: every symbol byte is computed on
+// the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/fecgpu.h"
+#include "fec_internal.h"
+
+using namespace fecgpu;
+
+namespace {
+
+#define SW_TRY(expr, what)                                      \
+    do {                                                        \
+        hipError_t e_ = (expr);                                 \
+        if (e_ != hipSuccess) return set_dev_error(e_, what);   \
+    } while (0)
+#define RC_TRY(expr)               \
+    do {                           \
+        ssize_t r_ = (expr);       \
+        if (r_ < 0) return r_;     \
+    } while (0)
+
+constexpr uint32_t kCombBudget = 40u << 10;  // LDS of one combine workgroup's job tables
+constexpr int kSwSolveOut = 8;               // recovered sources per solve job
+
+ssize_t check_geometry(uint32_t sym_len, uint32_t stride, const void *a, const void *b) {
+    if (stride == 0 || (stride & 15) || sym_len == 0 || sym_len > stride) return FECGPU_ERR_INVALID_ARG;
+    if (stride > FECGPU_MAX_SYMBOL) return FECGPU_ERR_UNSUPPORTED;
+    if ((reinterpret_cast<uintptr_t>(a) & 15) || (reinterpret_cast<uintptr_t>(b) & 15))
+        return FECGPU_ERR_INVALID_ARG;
+    return 0;
+}
+
+bool header_ok(const fecgpu_sw_repair &h, uint64_t nsrc) {
+    return h.nss >= 1 && h.nss <= kSwMaxWindow && h.dt <= 15 && h.fss <= nsrc && nsrc - h.fss >= h.nss;
+}
+
+// One combine launch (fec_internal.h CombJob) over njobs jobs.
+ssize_t run_comb(const CombJob *jobs, uint64_t njobs, const uint8_t *coef, const uint64_t *outs,
+                 const uint8_t *in_base, uint8_t *out_base, const uint8_t *xor_base, uint32_t S,
+                 uint32_t stride, int R, int nin_max, hipStream_t s) {
+    CombArgs a{};
+    a.jobs = jobs;
+    a.coef = coef;
+    a.outs = outs;
+    a.in_base = in_base;
+    a.out_base = out_base;
+    a.xor_base = xor_base;
+    a.njobs = njobs;
+    a.ncol = (S + 15u) >> 4;
+    a.stride = stride;
+    a.nin_max = std::max(1, nin_max);
+    a.nout_max = R;
+    a.job_lds = comb_job_lds(a.nin_max, R);
+    a.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(a.ncol, a.job_lds, kCombBudget)));
+    SW_TRY(launch_comb(a, R, s), "sliding-window combine launch");
+    return 0;
+}
+
+ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_t *rep,
+                      const fecgpu_sw_repair *hdr, uint64_t nrep, int max_window, uint32_t S,
+                      uint32_t stride, hipStream_t s) {
+    void *pj = nullptr, *pc = nullptr, *po = nullptr;
+    RC_TRY(ctx_sw_scratch(ctx, 0, nrep * sizeof(CombJob), &pj));
+    RC_TRY(ctx_sw_scratch(ctx, 1, nrep * kSwCoefPitch, &pc));
+    RC_TRY(ctx_sw_scratch(ctx, 2, nrep * sizeof(uint64_t), &po));
+    SwEncCoefArgs ca{};
+    ca.hdr = hdr;
+    ca.nrep = nrep;
+    ca.nsrc = nsrc;
+    ca.stride = stride;
+    ca.max_window = max_window;
+    ca.jobs = static_cast<CombJob *>(pj);
+    ca.coef = static_cast<uint8_t *>(pc);
+    ca.outs = static_cast<uint64_t *>(po);
+    SW_TRY(launch_sw_enc_coef(ca, s), "sliding-window coefficient launch");
+    return run_comb(ca.jobs, nrep, ca.coef, ca.outs, src, rep, nullptr, S, stride, 1, max_window, s);
+}
+
+// Host arrays of a decode's linked systems (see fecgpu_sw_decode).
+struct SwPlan {
+    std::vector<SwComp> comps;
+    std::vector<uint64_t> unk, eqr;
+    std::vector<uint32_t> eqc;
+    std::vector<fecgpu_sw_repair> eqh;
+    uint64_t amat = 0, nsolve = 0, tcoef = 0;
+    int max_nss = 1, max_p = 1;
+};
+
+// Lost sources, ascending, split into linked systems: consecutive lost sources
+// a < b are linked iff a received repair's window holds both, i.e. some
+// received repair with fss <= a ends past b (windows are intervals, so this
+// links every pair a repair holds).  Each system's equations are the received
+// repairs whose windows hold one of its lost sources (the first kSwMaxEq).
+// Systems of more than kSwMaxUnknowns lost sources, or with no equation, are
+// left out (their sources stay lost).
+void sw_build_plan(const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep_present,
+                   const fecgpu_sw_repair *hdr, uint64_t nrep, SwPlan &P) {
+    std::vector<uint64_t> lost;
+    for (uint64_t i = 0; i < nsrc; i++)
+        if (!src_present[i]) lost.push_back(i);
+    std::vector<uint64_t> pr;  // received repairs, fss ascending (headers are sorted)
+    for (uint64_t t = 0; t < nrep; t++)
+        if (rep_present[t]) pr.push_back(t);
+    size_t ip = 0;
+    uint64_t max_end = 0;
+    size_t start = 0;
+    for (size_t x = 0; x < lost.size(); x++) {
+        while (ip < pr.size() && hdr[pr[ip]].fss <= lost[x]) {
+            max_end = std::max(max_end, hdr[pr[ip]].fss + hdr[pr[ip]].nss);
+            ip++;
+        }
+        if (x + 1 < lost.size() && max_end > lost[x + 1]) continue;
+        // system = lost[start .. x]
+        const uint64_t *U = lost.data() + start;
+        const size_t e = x + 1 - start;
+        start = x + 1;
+        if (e > (size_t)kSwMaxUnknowns) continue;
+        const uint64_t lo = U[0] > (uint64_t)kSwMaxWindow ? U[0] - kSwMaxWindow : 0;
+        auto it = std::lower_bound(pr.begin(), pr.end(), lo,
+                                   [&](uint64_t t, uint64_t v) { return hdr[t].fss < v; });
+        std::vector<uint64_t> eq;
+        for (; it != pr.end() && hdr[*it].fss <= U[e - 1] && eq.size() < (size_t)kSwMaxEq; ++it) {
+            const fecgpu_sw_repair &h = hdr[*it];
+            const uint64_t *u = std::lower_bound(U, U + e, h.fss);
+            if (u != U + e && *u < h.fss + h.nss) eq.push_back(*it);
+        }
+        if (eq.empty()) continue;
+        SwComp c{};
+        c.u_off = P.unk.size();
+        c.q_off = P.eqr.size();
+        c.a_off = P.amat;
+        c.j_off = P.nsolve;
+        c.t_off = P.tcoef;  // relative; the syndrome coefficients go first
+        c.o_off = c.u_off;  // relative; the syndrome outputs go first
+        c.e = (uint32_t)e;
+        c.p = (uint32_t)eq.size();
+        P.amat += (uint64_t)c.e * c.p;
+        P.nsolve += (e + kSwSolveOut - 1) / kSwSolveOut;
+        P.tcoef += (uint64_t)((e + kSwSolveOut - 1) / kSwSolveOut * kSwSolveOut) * c.p;
+        P.max_p = std::max(P.max_p, (int)c.p);
+        const uint32_t ci = (uint32_t)P.comps.size();
+        for (size_t j = 0; j < e; j++) P.unk.push_back(U[j]);
+        for (uint64_t t : eq) {
+            P.eqr.push_back(t);
+            P.eqc.push_back(ci);
+            P.eqh.push_back(hdr[t]);
+            P.max_nss = std::max(P.max_nss, (int)hdr[t].nss);
+        }
+        P.comps.push_back(c);
+    }
+}
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Device part of a decode: src / rep device pointers, plan P on the host.
+ssize_t sw_decode_dev(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *rep, SwPlan &P, uint32_t S,
+                      uint32_t stride, std::vector<uint8_t> &ustat, hipStream_t s) {
+    const uint64_t neq = P.eqr.size(), nunk = P.unk.size(), ncomp = P.comps.size();
+    const uint64_t coef_syn = neq * kSwCoefPitch;
+    for (SwComp &c : P.comps) {
+        c.t_off += coef_syn;
+        c.o_off += neq;
+    }
+    // one metadata block: comps | unk | eqr | eqc | eqh, then amat, ustat, syndrome rows
+    const size_t o_unk = align256(ncomp * sizeof(SwComp));
+    const size_t o_eqr = o_unk + align256(nunk * 8);
+    const size_t o_eqc = o_eqr + align256(neq * 8);
+    const size_t o_eqh = o_eqc + align256(neq * 4);
+    const size_t o_amat = o_eqh + align256(neq * sizeof(fecgpu_sw_repair));
+    const size_t o_ust = o_amat + align256(P.amat);
+    const size_t o_syn = o_ust + align256(nunk);
+    const size_t total = o_syn + neq * (size_t)stride;
+    std::vector<uint8_t> meta(o_amat, 0);
+    std::memcpy(meta.data(), P.comps.data(), ncomp * sizeof(SwComp));
+    std::memcpy(meta.data() + o_unk, P.unk.data(), nunk * 8);
+    std::memcpy(meta.data() + o_eqr, P.eqr.data(), neq * 8);
+    std::memcpy(meta.data() + o_eqc, P.eqc.data(), neq * 4);
+    std::memcpy(meta.data() + o_eqh, P.eqh.data(), neq * sizeof(fecgpu_sw_repair));
+    void *pm = nullptr, *pj = nullptr, *pc = nullptr, *po = nullptr;
+    RC_TRY(ctx_sw_scratch(ctx, 6, total, &pm));
+    RC_TRY(ctx_sw_scratch(ctx, 0, (neq + P.nsolve) * sizeof(CombJob), &pj));
+    RC_TRY(ctx_sw_scratch(ctx, 1, coef_syn + P.tcoef, &pc));
+    RC_TRY(ctx_sw_scratch(ctx, 2, (neq + nunk) * sizeof(uint64_t), &po));
+    uint8_t *m = static_cast<uint8_t *>(pm);
+    SW_TRY(hipMemcpyAsync(m, meta.data(), meta.size(), hipMemcpyHostToDevice, s), "H2D sw plan");
+    CombJob *jobs = static_cast<CombJob *>(pj);
+    uint8_t *coef = static_cast<uint8_t *>(pc);
+    uint64_t *outs = static_cast<uint64_t *>(po);
+    uint8_t *synd = m + o_syn;
+
+    SwSynArgs ya{};
+    ya.eqh = reinterpret_cast<const fecgpu_sw_repair *>(m + o_eqh);
+    ya.eqr = reinterpret_cast<const uint64_t *>(m + o_eqr);
+    ya.eqc = reinterpret_cast<const uint32_t *>(m + o_eqc);
+    ya.comps = reinterpret_cast<const SwComp *>(m);
+    ya.unk = reinterpret_cast<const uint64_t *>(m + o_unk);
+    ya.neq = neq;
+    ya.stride = stride;
+    ya.jobs = jobs;
+    ya.coef = coef;
+    ya.outs = outs;
+    ya.amat = m + o_amat;
+    SW_TRY(launch_sw_syn(ya, s), "sliding-window syndrome coefficient launch");
+    RC_TRY(run_comb(jobs, neq, coef, outs, src, synd, rep, S, stride, 1, P.max_nss, s));
+
+    SwPlanArgs pa{};
+    pa.comps = ya.comps;
+    pa.ncomp = ncomp;
+    pa.amat = m + o_amat;
+    pa.unk = ya.unk;
+    pa.stride = stride;
+    pa.jobs = jobs + neq;
+    pa.coef = coef;
+    pa.outs = outs;
+    pa.ustat = m + o_ust;
+    SW_TRY(launch_sw_plan(pa, s), "sliding-window plan launch");
+    RC_TRY(run_comb(jobs + neq, P.nsolve, coef, outs, synd, src, nullptr, S, stride, kSwSolveOut,
+                    P.max_p, s));
+    ustat.resize(nunk);
+    SW_TRY(hipMemcpyAsync(ustat.data(), m + o_ust, nunk, hipMemcpyDeviceToHost, s), "D2H sw status");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+ssize_t fecgpu_sw_encode(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_t *rep,
+                         const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t max_window,
+                         uint32_t sym_len, uint32_t stride, uint32_t flags, void *stream) {
+    if (!ctx) return FECGPU_ERR_INVALID_ARG;
+    if (nrep == 0) return 0;
+    if (!src || !rep || !hdr || nsrc == 0) return FECGPU_ERR_INVALID_ARG;
+    if (max_window > (uint32_t)kSwMaxWindow) return FECGPU_ERR_INVALID_ARG;
+    RC_TRY(check_geometry(sym_len, stride, src, rep));
+    int mw = max_window ? (int)max_window : kSwMaxWindow;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (flags & FECGPU_F_HOST_PTRS) {
+        int hmax = 1;
+        for (uint64_t t = 0; t < nrep; t++) {
+            if (!header_ok(hdr[t], nsrc) || hdr[t].nss > mw) return FECGPU_ERR_INVALID_ARG;
+            hmax = std::max(hmax, (int)hdr[t].nss);
+        }
+        RC_TRY(ctx_sw_begin(ctx, s));
+        void *ds = nullptr, *dr = nullptr, *dh = nullptr;
+        RC_TRY(ctx_sw_scratch(ctx, 3, nsrc * stride, &ds));
+        RC_TRY(ctx_sw_scratch(ctx, 4, nrep * stride, &dr));
+        RC_TRY(ctx_sw_scratch(ctx, 5, nrep * sizeof(fecgpu_sw_repair), &dh));
+        SW_TRY(hipMemcpyAsync(ds, src, nsrc * stride, hipMemcpyHostToDevice, s), "H2D sw sources");
+        SW_TRY(hipMemcpyAsync(dh, hdr, nrep * sizeof(fecgpu_sw_repair), hipMemcpyHostToDevice, s), "H2D sw headers");
+        RC_TRY(sw_encode_dev(ctx, static_cast<uint8_t *>(ds), nsrc, static_cast<uint8_t *>(dr),
+                             static_cast<fecgpu_sw_repair *>(dh), nrep, hmax, sym_len, stride, s));
+        SW_TRY(hipMemcpyAsync(rep, dr, nrep * stride, hipMemcpyDeviceToHost, s), "D2H sw repairs");
+        RC_TRY(ctx_sw_end(ctx, s));
+        SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+        return (ssize_t)nrep;
+    }
+    RC_TRY(ctx_sw_begin(ctx, s));
+    RC_TRY(sw_encode_dev(ctx, src, nsrc, rep, hdr, nrep, mw, sym_len, stride, s));
+    RC_TRY(ctx_sw_end(ctx, s));
+    if (flags & FECGPU_F_SYNC) SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+    return (ssize_t)nrep;
+}
+
+ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_present, uint64_t nsrc,
+                         const uint8_t *rep, const uint8_t *rep_present,
+                         const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t sym_len,
+                         uint32_t stride, uint8_t *src_status, uint32_t flags, void *stream) {
+    if (!ctx || !src || !src_present || !src_status || nsrc == 0) return FECGPU_ERR_INVALID_ARG;
+    if (nrep && (!rep || !rep_present || !hdr)) return FECGPU_ERR_INVALID_ARG;
+    RC_TRY(check_geometry(sym_len, stride, src, nrep ? rep : src));
+    for (uint64_t t = 0; t < nrep; t++) {
+        if (!header_ok(hdr[t], nsrc)) return FECGPU_ERR_INVALID_ARG;
+        if (t && hdr[t].fss < hdr[t - 1].fss) return FECGPU_ERR_INVALID_ARG;  // fss nondecreasing
+    }
+    uint64_t nlost = 0;
+    for (uint64_t i = 0; i < nsrc; i++) {
+        src_status[i] = src_present[i] ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
+        nlost += !src_present[i];
+    }
+    if (nlost == 0 || nrep == 0) return 0;
+    SwPlan P;
+    sw_build_plan(src_present, nsrc, rep_present, hdr, nrep, P);
+    if (P.comps.empty()) return 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    RC_TRY(ctx_sw_begin(ctx, s));
+    uint8_t *dsrc = src;
+    const uint8_t *drep = rep;
+    if (flags & FECGPU_F_HOST_PTRS) {
+        void *ds = nullptr, *dr = nullptr;
+        RC_TRY(ctx_sw_scratch(ctx, 3, nsrc * stride, &ds));
+        RC_TRY(ctx_sw_scratch(ctx, 4, nrep * stride, &dr));
+        SW_TRY(hipMemcpyAsync(ds, src, nsrc * stride, hipMemcpyHostToDevice, s), "H2D sw sources");
+        SW_TRY(hipMemcpyAsync(dr, rep, nrep * stride, hipMemcpyHostToDevice, s), "H2D sw repairs");
+        dsrc = static_cast<uint8_t *>(ds);
+        drep = static_cast<uint8_t *>(dr);
+    }
+    std::vector<uint8_t> ustat;
+    RC_TRY(sw_decode_dev(ctx, dsrc, drep, P, sym_len, stride, ustat, s));
+    if (flags & FECGPU_F_HOST_PTRS)
+        SW_TRY(hipMemcpyAsync(src, dsrc, nsrc * stride, hipMemcpyDeviceToHost, s), "D2H sw sources");
+    RC_TRY(ctx_sw_end(ctx, s));
+    SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+    ssize_t rec = 0;
+    for (size_t u = 0; u < P.unk.size(); u++)
+        if (ustat[u] == 0) {
+            src_status[P.unk[u]] = FECGPU_STATUS_OK;
+            rec++;
+        }
+    return rec;
+}
+
+}  // extern "C"

@@ -57,7 +57,11 @@ EXPORTS = (
     "fecgpu_decoder_tick",
     "fecgpu_frame_source_id_len", "fecgpu_frame_write_source_id", "fecgpu_frame_repair_len",
     "fecgpu_frame_write_repair", "fecgpu_frame_write_repair_header", "fecgpu_frame_parse",
+    "fecgpu_sw_encode", "fecgpu_sw_decode",
 )
+SW_MAX_WINDOW, SW_MAX_UNKNOWNS, SW_MAX_EQUATIONS = 255, 64, 96
+# fecgpu_sw_repair as a numpy dtype (16 bytes, the C layout)
+SW_REPAIR_DTYPE = [("fss", "<u8"), ("nss", "<u2"), ("key", "<u2"), ("dt", "u1"), ("reserved", "u1", (3,))]
 FRAME_SOURCE_ID, FRAME_REPAIR = 0xFEC0, 0xFEC1
 
 
@@ -181,6 +185,8 @@ def _lib():
                                                       ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16,
                                                       ctypes.c_size_t]),
             "fecgpu_frame_parse": (sz, [vp, ctypes.c_size_t, ctypes.POINTER(fecgpu_frame)]),
+            "fecgpu_sw_encode": (sz, [vp, vp, u64, vp, vp, u64, u32, u32, u32, u32, vp]),
+            "fecgpu_sw_decode": (sz, [vp, vp, vp, u64, vp, vp, vp, u64, u32, u32, vp, u32, vp]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -319,6 +325,22 @@ class Context:
             self._h, ctypes.byref(code.c), _ptr(win), _ptr(win_off), _ptr(sym_len),
             sym_len_all, stride, nwin, _ptr(present), _ptr(status), flags,
             _stream(stream) if not flags & F_HOST_PTRS else None), "fecgpu_decode_batch")
+
+    def sw_encode(self, src, rep, hdr, *, nsrc: int, nrep: int, sym_len: int, stride: int,
+                  max_window: int = 0, flags: int = 0, stream=None) -> int:
+        """Sliding-window RLC repairs (fecgpu_sw_encode): rep[t] from hdr[t]'s window of src."""
+        return _check(_lib().fecgpu_sw_encode(
+            self._h, _ptr(src), nsrc, _ptr(rep), _ptr(hdr), nrep, max_window, sym_len, stride, flags,
+            _stream(stream) if not flags & F_HOST_PTRS else None), "fecgpu_sw_encode")
+
+    def sw_decode(self, src, src_present, rep, rep_present, hdr, src_status, *, nsrc: int, nrep: int,
+                  sym_len: int, stride: int, flags: int = 0, stream=None) -> int:
+        """Sliding-window RLC recovery in place (fecgpu_sw_decode); src_present, rep_present,
+        hdr and src_status are host (numpy) arrays.  Returns the number recovered."""
+        return _check(_lib().fecgpu_sw_decode(
+            self._h, _ptr(src), _ptr(src_present), nsrc, _ptr(rep), _ptr(rep_present), _ptr(hdr),
+            nrep, sym_len, stride, _ptr(src_status), flags,
+            _stream(stream) if not flags & F_HOST_PTRS else None), "fecgpu_sw_decode")
 
     def synth_batch(self, code: Code, workload: int, seed: int, w0: int, win, sym_len, *,
                     L: int, stride: int, nwin: int, stream=None) -> int:
