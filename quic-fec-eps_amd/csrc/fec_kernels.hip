@@ -1271,17 +1271,22 @@ template <int R, int NE>
 __device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t out_delta,
                                          const DecRegion<R> &rg) {
     constexpr int U = FECGPU_GFD_U, R4 = DecRegion<R>::R4;
-    static_assert(U == 4 || U == 8, "row offsets are read 4 at a time, padded to 8 rows");
+    static_assert(U == 2 || U == 4 || U == 8, "row offsets are padded to 8 rows");
     uint4 acc[NE];
 #pragma unroll
     for (int m = 0; m < NE; m++) acc[m] = zero4();
     for (int q0 = 0; q0 < k; q0 += U) {
         uint4 v[U];
         uint32_t ro[U];
+        if constexpr (U >= 4) {
 #pragma unroll
-        for (int t = 0; t < U; t += 4) {  // roff is padded to a multiple of 8 rows
-            const uint4 o = *reinterpret_cast<const uint4 *>(rg.roff + q0 + t);
-            ro[t] = o.x; ro[t + 1] = o.y; ro[t + 2] = o.z; ro[t + 3] = o.w;
+            for (int t = 0; t < U; t += 4) {  // roff is padded to a multiple of 8 rows
+                const uint4 o = *reinterpret_cast<const uint4 *>(rg.roff + q0 + t);
+                ro[t] = o.x; ro[t + 1] = o.y; ro[t + 2] = o.z; ro[t + 3] = o.w;
+            }
+        } else {
+            const uint2 o = *reinterpret_cast<const uint2 *>(rg.roff + q0);
+            ro[0] = o.x; ro[1] = o.y;
         }
 #pragma unroll
         for (int t = 0; t < U; t++) v[t] = ld16(base + ro[t]);
@@ -1365,6 +1370,8 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
 #else
         {
             // this wave plans windows wave, wave + 4, ...: their masks in one load
+            // (prefetching the next group's masks in persistent workgroups did
+            // not pay: the default one-group-per-workgroup grid was faster, r02)
             constexpr int NW = kBlock / 64;
             const int wl_l = wave + NW * lane;
             const uint64_t pl = (wl_l < nb) ? a.present[w0 + wl_l] : 0ull;

@@ -23,7 +23,7 @@ step() {  # name timeout cmd...
 prof() {  # name config extra-args...
     local name=$1 cfg=$2; shift 2
     step "$name" 600 rocprofv3 --kernel-trace --stats -f csv -d "gpurun_out/$name" -o run -- \
-        python bench.py --config "$cfg" --steps 10 --warmup 2 --cpu-seconds 0 "$@"
+        python bench.py --config "$cfg" --steps 20 --warmup 10 --cpu-seconds 0 "$@"
 }
 pmc() {  # name config counters...
     local name=$1 cfg=$2; shift 2
