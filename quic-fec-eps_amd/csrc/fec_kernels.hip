@@ -1545,6 +1545,13 @@ __global__ __launch_bounds__(kBlock) void digest_kernel(DigestArgs a) {
 // the device (one lane per repair), the decode's linked systems are reduced
 // by one wave each (Gauss-Jordan with pivot search).
 
+#ifndef FECGPU_COMB_U
+// combine kernel: input rows loaded per batch.  One output (repairs,
+// syndromes): 16 (sliding-window encode k 8 W 32: 0.370 vs 0.387 ms at 8,
+// 0.466 at 4; profiles/r02_sw_ab.txt); solves (8 outputs, register-bound): 8.
+#define FECGPU_COMB_U (R == 1 ? 16 : 8)
+#endif
+
 // Per-job LDS region of comb_kernel<R>: tables [nin_max][R] uint4 (TA/TB),
 // [nin_max][RT] u32 (TC), output column-0 pointers [R], xor pointer.
 template <int R>
@@ -1566,7 +1573,7 @@ struct CombRegion {
 template <int R, int NE>
 __device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, int nin, int ne, uint32_t col,
                                           const CombRegion<R> &rg) {
-    constexpr int U = 8, RT = CombRegion<R>::RT;
+    constexpr int U = FECGPU_COMB_U, RT = CombRegion<R>::RT;
     uint4 acc[NE];
 #pragma unroll
     for (int m = 0; m < NE; m++) acc[m] = zero4();
