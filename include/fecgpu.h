@@ -48,7 +48,8 @@ extern "C" {
 #endif
 
 #define FECGPU_ABI_VERSION 3  /* 2: REPAIR frames carry nsrc; decoder limits / recovered queue;
-                                 3: fecgpu_code.rlc_key / rlc_dt, FECGPU_MATRIX_RLC */
+                                 3: fecgpu_code.rlc_key / rlc_dt, FECGPU_MATRIX_RLC, sliding-window
+                                    RLC (fecgpu_sw_*, SW frames, fecgpu_frame.key / dt) */
 
 /* errors (mirror quiche's QUICHE_ERR_DONE = -1, QUICHE_ERR_BUFFER_TOO_SHORT = -2 style) */
 enum fecgpu_error {
@@ -99,6 +100,7 @@ typedef struct fecgpu_code {
 } fecgpu_code;
 
 typedef struct fecgpu_ctx fecgpu_ctx;
+struct fecgpu_sw_repair;  /* sliding-window repair header, defined below */
 
 int         fecgpu_abi_version(void);
 const char *fecgpu_strerror(ssize_t err);
@@ -285,15 +287,22 @@ ssize_t fecgpu_decoder_tick(fecgpu_decoder *dec, uint64_t now_us);
  * Frame types sit in QUIC's extension space.  Host-only, no device calls. */
 #define FECGPU_FRAME_SOURCE_ID 0xfec0u
 #define FECGPU_FRAME_REPAIR 0xfec1u
+/* sliding-window code (RFC 8681 FEC payload IDs):
+ *   SW_SOURCE: type | esi                                  (next to a source payload)
+ *   SW_REPAIR: type | fss | nss | repair_key | dt | length | symbol bytes */
+#define FECGPU_FRAME_SW_SOURCE 0xfec2u
+#define FECGPU_FRAME_SW_REPAIR 0xfec3u
 
 typedef struct fecgpu_frame {
     uint64_t type;           /* FECGPU_FRAME_* */
-    uint64_t win;            /* window id */
+    uint64_t win;            /* window id; SW_SOURCE: esi; SW_REPAIR: fss */
     uint16_t k, r;           /* REPAIR: code shape */
     uint16_t idx;            /* source index (SOURCE_ID) or repair index (REPAIR) */
-    const uint8_t *payload;  /* REPAIR: points into the parsed buffer */
+    const uint8_t *payload;  /* REPAIR / SW_REPAIR: points into the parsed buffer */
     size_t payload_len;
-    uint16_t nsrc;           /* REPAIR: real sources of the window, 1..k */
+    uint16_t nsrc;           /* REPAIR: real sources of the window, 1..k; SW_REPAIR: nss */
+    uint16_t key;            /* SW_REPAIR: repair_key */
+    uint8_t dt;              /* SW_REPAIR: DT */
 } fecgpu_frame;
 
 ssize_t fecgpu_frame_source_id_len(uint64_t win, uint16_t idx);
@@ -308,6 +317,10 @@ ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16
  * Returns the header length. */
 ssize_t fecgpu_frame_write_repair_header(uint8_t *buf, size_t cap, uint64_t win, uint16_t k,
                                          uint16_t r, uint16_t nsrc, uint16_t idx, size_t sym_len);
+/* sliding-window frames (hdr->fss is the absolute ESI of the window's first source) */
+ssize_t fecgpu_frame_write_sw_source(uint8_t *buf, size_t cap, uint64_t esi);
+ssize_t fecgpu_frame_write_sw_repair(uint8_t *buf, size_t cap, const struct fecgpu_sw_repair *hdr,
+                                     const uint8_t *sym, size_t sym_len);
 /* Parse one frame at buf; returns bytes consumed or a negative error
  * (BUFFER_TOO_SHORT on truncation, INVALID_ARG on an unknown type or bad field). */
 ssize_t fecgpu_frame_parse(const uint8_t *buf, size_t len, fecgpu_frame *out);
@@ -382,6 +395,62 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
                          const uint8_t *rep, const uint8_t *rep_present,
                          const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t sym_len,
                          uint32_t stride, uint8_t *src_status, uint32_t flags, void *stream);
+
+/* ---- sliding-window per-connection objects ----------------------------
+ * The Connection's per-packet API for the sliding-window code (RFC 8681
+ * semantics: encoding symbol size E fixed per session, ADU framing as A.3).
+ * Sender: every protected payload gets the next ESI; after every `step`
+ * sources a repair over the last `window` sources is scheduled (repair_key =
+ * 0, 1, 2, ... mod 2^16); `batch` scheduled repairs are encoded in one
+ * asynchronous launch (the kernel reads the sources from pinned host memory
+ * the GPU maps; 4 launches' repairs held until read) and read back in order with
+ * fecgpu_sw_encoder_next_repair for SW_REPAIR frames.  Receiver: files
+ * sources by ESI and repairs by header, and a flush (automatic every `batch`
+ * received repairs) runs fecgpu_sw_decode over its live span.  Sources more
+ * than `span` behind the newest ESI are given up.  Objects must be freed
+ * before their ctx and used from its thread. */
+typedef struct fecgpu_sw_params {
+    uint32_t framing;     /* FECGPU_FRAMING_FIXED (payload = symbol) or _LENPREFIX */
+    uint32_t symbol_size; /* E bytes (LENPREFIX: 2 + the largest payload), <= 65537 */
+    uint16_t window;      /* W: sources per encoding window, 1..FECGPU_SW_MAX_WINDOW */
+    uint16_t step;        /* a repair after every `step` sources, >= 1 */
+    uint8_t  dt;          /* RFC 8681 DT, 0..15 */
+    uint8_t  reserved[3];
+    uint32_t batch;       /* repairs per encode launch / per automatic decoder flush, >= 1 */
+    uint32_t span;        /* receiver: sources kept behind the newest (0 = 16 x window) */
+} fecgpu_sw_params;
+
+typedef struct fecgpu_sw_encoder fecgpu_sw_encoder;
+typedef struct fecgpu_sw_decoder fecgpu_sw_decoder;
+
+ssize_t fecgpu_sw_encoder_new(fecgpu_ctx *ctx, const fecgpu_sw_params *p, fecgpu_sw_encoder **out);
+void    fecgpu_sw_encoder_free(fecgpu_sw_encoder *enc);
+/* Append a source payload; *esi receives its ESI.  FECGPU_ERR_LIMIT (nothing
+ * consumed) while every launch slot holds repairs not yet read. */
+ssize_t fecgpu_sw_encoder_add_source(fecgpu_sw_encoder *enc, const uint8_t *pkt, size_t len,
+                                     uint64_t *esi);
+/* Launch the scheduled repairs (when a launch slot is free) and wait for
+ * every launch; returns the number of repairs ready to read. */
+ssize_t fecgpu_sw_encoder_flush(fecgpu_sw_encoder *enc);
+/* The next encoded repair in order: header (absolute fss) and E bytes;
+ * FECGPU_ERR_DONE if none is ready yet. */
+ssize_t fecgpu_sw_encoder_next_repair(fecgpu_sw_encoder *enc, fecgpu_sw_repair *hdr, uint8_t *out,
+                                      size_t cap);
+
+ssize_t fecgpu_sw_decoder_new(fecgpu_ctx *ctx, const fecgpu_sw_params *p, fecgpu_sw_decoder **out);
+void    fecgpu_sw_decoder_free(fecgpu_sw_decoder *dec);
+ssize_t fecgpu_sw_decoder_add_source(fecgpu_sw_decoder *dec, uint64_t esi, const uint8_t *pkt,
+                                     size_t len);
+/* hdr->fss absolute; sym: E bytes */
+ssize_t fecgpu_sw_decoder_add_repair(fecgpu_sw_decoder *dec, const fecgpu_sw_repair *hdr,
+                                     const uint8_t *sym, size_t len);
+/* Decode now; returns the number of sources recovered (also queued for
+ * fecgpu_sw_decoder_next_recovered). */
+ssize_t fecgpu_sw_decoder_flush(fecgpu_sw_decoder *dec);
+/* Payload of source esi (received or recovered, de-framed); FECGPU_ERR_DONE
+ * if it is not available (lost, or given up). */
+ssize_t fecgpu_sw_decoder_recovered(fecgpu_sw_decoder *dec, uint64_t esi, uint8_t *out, size_t cap);
+ssize_t fecgpu_sw_decoder_next_recovered(fecgpu_sw_decoder *dec, uint64_t *esi);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,9 @@
 // Connection puts a SOURCE_ID frame next to each protected payload and carries
 // repair symbols in REPAIR frames; the receiver parses both and feeds
 // fecgpu_decoder_*.
+// Sliding-window frames carry RFC 8681's FEC payload IDs in the same idiom:
+//   SW_SOURCE: type | esi
+//   SW_REPAIR: type | fss | nss | repair_key | dt | length | repair symbol bytes
 // Pure host code: no device calls.
 #include <cstring>
 
@@ -98,6 +101,33 @@ ssize_t fecgpu_frame_write_repair(uint8_t *buf, size_t cap, uint64_t win, uint16
     return h + (ssize_t)sym_len;
 }
 
+ssize_t fecgpu_frame_write_sw_source(uint8_t *buf, size_t cap, uint64_t esi) {
+    if (!buf || esi >= (1ull << 62)) return FECGPU_ERR_INVALID_ARG;
+    const size_t n = varint_len(FECGPU_FRAME_SW_SOURCE) + varint_len(esi);
+    if (cap < n) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    uint8_t *p = varint_put(buf, FECGPU_FRAME_SW_SOURCE);
+    p = varint_put(p, esi);
+    return (ssize_t)(p - buf);
+}
+
+ssize_t fecgpu_frame_write_sw_repair(uint8_t *buf, size_t cap, const struct fecgpu_sw_repair *hdr,
+                                     const uint8_t *sym, size_t sym_len) {
+    if (!buf || !hdr || (!sym && sym_len) || hdr->fss >= (1ull << 62) || hdr->nss == 0 ||
+        hdr->nss > FECGPU_SW_MAX_WINDOW || hdr->dt > 15 || sym_len >= (1ull << 62))
+        return FECGPU_ERR_INVALID_ARG;
+    const size_t n = varint_len(FECGPU_FRAME_SW_REPAIR) + varint_len(hdr->fss) + varint_len(hdr->nss) +
+                     varint_len(hdr->key) + varint_len(hdr->dt) + varint_len(sym_len) + sym_len;
+    if (cap < n) return FECGPU_ERR_BUFFER_TOO_SHORT;
+    uint8_t *p = varint_put(buf, FECGPU_FRAME_SW_REPAIR);
+    p = varint_put(p, hdr->fss);
+    p = varint_put(p, hdr->nss);
+    p = varint_put(p, hdr->key);
+    p = varint_put(p, hdr->dt);
+    p = varint_put(p, sym_len);
+    if (sym_len) std::memcpy(p, sym, sym_len);
+    return (ssize_t)(p + sym_len - buf);
+}
+
 ssize_t fecgpu_frame_parse(const uint8_t *buf, size_t len, fecgpu_frame *out) {
     if (!buf || !out) return FECGPU_ERR_INVALID_ARG;
     std::memset(out, 0, sizeof(*out));
@@ -112,9 +142,27 @@ ssize_t fecgpu_frame_parse(const uint8_t *buf, size_t len, fecgpu_frame *out) {
     } while (0)
     uint64_t type;
     GET(type);
-    if (type != FECGPU_FRAME_SOURCE_ID && type != FECGPU_FRAME_REPAIR) return FECGPU_ERR_INVALID_ARG;
+    if (type != FECGPU_FRAME_SOURCE_ID && type != FECGPU_FRAME_REPAIR && type != FECGPU_FRAME_SW_SOURCE &&
+        type != FECGPU_FRAME_SW_REPAIR)
+        return FECGPU_ERR_INVALID_ARG;
     out->type = type;
     GET(out->win);
+    if (type == FECGPU_FRAME_SW_SOURCE) return (ssize_t)pos;
+    if (type == FECGPU_FRAME_SW_REPAIR) {
+        uint64_t nss, key, dt, sl;
+        GET(nss);
+        GET(key);
+        GET(dt);
+        GET(sl);
+        if (nss == 0 || nss > FECGPU_SW_MAX_WINDOW || key > 0xFFFF || dt > 15) return FECGPU_ERR_INVALID_ARG;
+        if (sl > len - pos) return FECGPU_ERR_BUFFER_TOO_SHORT;
+        out->nsrc = (uint16_t)nss;
+        out->key = (uint16_t)key;
+        out->dt = (uint8_t)dt;
+        out->payload = buf + pos;
+        out->payload_len = sl;
+        return (ssize_t)(pos + sl);
+    }
     if (type == FECGPU_FRAME_SOURCE_ID) {
         uint64_t idx;
         GET(idx);

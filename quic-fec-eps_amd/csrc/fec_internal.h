@@ -223,6 +223,12 @@ hipError_t launch_sw_plan(const SwPlanArgs &a, hipStream_t s);
 // sliding-window calls on one ctx (begin: `s` waits for the previous call's
 // end; end: records it), which share that scratch.
 ssize_t set_dev_error(hipError_t e, const char *what);
+// Sliding-window encode launches on `s` with caller-owned device scratch:
+// jobs (nrep x sizeof(CombJob)), coefficients (nrep x kSwCoefPitch), output
+// offsets (nrep x 8) (fec_sw.cpp; used by the per-connection encoder).
+ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
+                       uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *jobs,
+                       void *coef, void *outs, hipStream_t s);
 int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget);
 ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p);
 ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);

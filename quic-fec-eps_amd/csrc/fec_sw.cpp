@@ -65,13 +65,13 @@ ssize_t run_comb(const CombJob *jobs, uint64_t njobs, const uint8_t *coef, const
     return 0;
 }
 
-ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_t *rep,
-                      const fecgpu_sw_repair *hdr, uint64_t nrep, int max_window, uint32_t S,
-                      uint32_t stride, hipStream_t s) {
-    void *pj = nullptr, *pc = nullptr, *po = nullptr;
-    RC_TRY(ctx_sw_scratch(ctx, 0, nrep * sizeof(CombJob), &pj));
-    RC_TRY(ctx_sw_scratch(ctx, 1, nrep * kSwCoefPitch, &pc));
-    RC_TRY(ctx_sw_scratch(ctx, 2, nrep * sizeof(uint64_t), &po));
+}  // namespace
+
+namespace fecgpu {
+
+ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
+                       uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *pj, void *pc,
+                       void *po, hipStream_t s) {
     SwEncCoefArgs ca{};
     ca.hdr = hdr;
     ca.nrep = nrep;
@@ -83,6 +83,20 @@ ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_
     ca.outs = static_cast<uint64_t *>(po);
     SW_TRY(launch_sw_enc_coef(ca, s), "sliding-window coefficient launch");
     return run_comb(ca.jobs, nrep, ca.coef, ca.outs, src, rep, nullptr, S, stride, 1, max_window, s);
+}
+
+}  // namespace fecgpu
+
+namespace {
+
+ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_t *rep,
+                      const fecgpu_sw_repair *hdr, uint64_t nrep, int max_window, uint32_t S,
+                      uint32_t stride, hipStream_t s) {
+    void *pj = nullptr, *pc = nullptr, *po = nullptr;
+    RC_TRY(ctx_sw_scratch(ctx, 0, nrep * sizeof(CombJob), &pj));
+    RC_TRY(ctx_sw_scratch(ctx, 1, nrep * kSwCoefPitch, &pc));
+    RC_TRY(ctx_sw_scratch(ctx, 2, nrep * sizeof(uint64_t), &po));
+    return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s);
 }
 
 // Host arrays of a decode's linked systems (see fecgpu_sw_decode).

@@ -58,7 +58,14 @@ EXPORTS = (
     "fecgpu_frame_source_id_len", "fecgpu_frame_write_source_id", "fecgpu_frame_repair_len",
     "fecgpu_frame_write_repair", "fecgpu_frame_write_repair_header", "fecgpu_frame_parse",
     "fecgpu_sw_encode", "fecgpu_sw_decode",
+    "fecgpu_frame_write_sw_source", "fecgpu_frame_write_sw_repair",
+    "fecgpu_sw_encoder_new", "fecgpu_sw_encoder_free", "fecgpu_sw_encoder_add_source",
+    "fecgpu_sw_encoder_flush", "fecgpu_sw_encoder_next_repair",
+    "fecgpu_sw_decoder_new", "fecgpu_sw_decoder_free", "fecgpu_sw_decoder_add_source",
+    "fecgpu_sw_decoder_add_repair", "fecgpu_sw_decoder_flush", "fecgpu_sw_decoder_recovered",
+    "fecgpu_sw_decoder_next_recovered",
 )
+FRAME_SW_SOURCE, FRAME_SW_REPAIR = 0xFEC2, 0xFEC3
 SW_MAX_WINDOW, SW_MAX_UNKNOWNS, SW_MAX_EQUATIONS = 255, 64, 96
 # fecgpu_sw_repair as a numpy dtype (16 bytes, the C layout)
 SW_REPAIR_DTYPE = [("fss", "<u8"), ("nss", "<u2"), ("key", "<u2"), ("dt", "u1"), ("reserved", "u1", (3,))]
@@ -99,7 +106,20 @@ class fecgpu_frame(ctypes.Structure):
         ("payload", ctypes.c_void_p),
         ("payload_len", ctypes.c_size_t),
         ("nsrc", ctypes.c_uint16),
+        ("key", ctypes.c_uint16),
+        ("dt", ctypes.c_uint8),
     ]
+
+
+class fecgpu_sw_repair(ctypes.Structure):
+    _fields_ = [("fss", ctypes.c_uint64), ("nss", ctypes.c_uint16), ("key", ctypes.c_uint16),
+                ("dt", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 3)]
+
+
+class fecgpu_sw_params(ctypes.Structure):
+    _fields_ = [("framing", ctypes.c_uint32), ("symbol_size", ctypes.c_uint32), ("window", ctypes.c_uint16),
+                ("step", ctypes.c_uint16), ("dt", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 3),
+                ("batch", ctypes.c_uint32), ("span", ctypes.c_uint32)]
 
 
 _L = None
@@ -187,6 +207,21 @@ def _lib():
             "fecgpu_frame_parse": (sz, [vp, ctypes.c_size_t, ctypes.POINTER(fecgpu_frame)]),
             "fecgpu_sw_encode": (sz, [vp, vp, u64, vp, vp, u64, u32, u32, u32, u32, vp]),
             "fecgpu_sw_decode": (sz, [vp, vp, vp, u64, vp, vp, vp, u64, u32, u32, vp, u32, vp]),
+            "fecgpu_frame_write_sw_source": (sz, [vp, ctypes.c_size_t, u64]),
+            "fecgpu_frame_write_sw_repair": (sz, [vp, ctypes.c_size_t, ctypes.POINTER(fecgpu_sw_repair), vp,
+                                                  ctypes.c_size_t]),
+            "fecgpu_sw_encoder_new": (sz, [vp, ctypes.POINTER(fecgpu_sw_params), ctypes.POINTER(vp)]),
+            "fecgpu_sw_encoder_free": (None, [vp]),
+            "fecgpu_sw_encoder_add_source": (sz, [vp, vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]),
+            "fecgpu_sw_encoder_flush": (sz, [vp]),
+            "fecgpu_sw_encoder_next_repair": (sz, [vp, ctypes.POINTER(fecgpu_sw_repair), vp, ctypes.c_size_t]),
+            "fecgpu_sw_decoder_new": (sz, [vp, ctypes.POINTER(fecgpu_sw_params), ctypes.POINTER(vp)]),
+            "fecgpu_sw_decoder_free": (None, [vp]),
+            "fecgpu_sw_decoder_add_source": (sz, [vp, u64, vp, ctypes.c_size_t]),
+            "fecgpu_sw_decoder_add_repair": (sz, [vp, ctypes.POINTER(fecgpu_sw_repair), vp, ctypes.c_size_t]),
+            "fecgpu_sw_decoder_flush": (sz, [vp]),
+            "fecgpu_sw_decoder_recovered": (sz, [vp, u64, vp, ctypes.c_size_t]),
+            "fecgpu_sw_decoder_next_recovered": (sz, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -513,6 +548,119 @@ class Decoder:
             pass
 
 
+def sw_params(symbol_size: int, window: int, step: int, *, framing: str = "lenprefix", dt: int = 15,
+              batch: int = 16, span: int = 0) -> fecgpu_sw_params:
+    return fecgpu_sw_params(FRAMING_FIXED if framing == "fixed" else FRAMING_LENPREFIX, symbol_size, window,
+                            step, dt, (ctypes.c_uint8 * 3)(), batch, span)
+
+
+class SwEncoder:
+    """Per-connection sliding-window sender (fecgpu_sw_encoder_*)."""
+
+    def __init__(self, ctx: Context, params: fecgpu_sw_params):
+        self._ctx = ctx
+        self.params = params
+        self._h = ctypes.c_void_p()
+        _check(_lib().fecgpu_sw_encoder_new(ctx.handle, ctypes.byref(params), ctypes.byref(self._h)),
+               "fecgpu_sw_encoder_new")
+
+    def add_source(self, pkt: bytes) -> int:
+        """-> the packet's ESI; raises FecError(ERR_LIMIT) while repairs wait to be read."""
+        esi = ctypes.c_uint64()
+        _check(_lib().fecgpu_sw_encoder_add_source(self._h, pkt, len(pkt), ctypes.byref(esi)),
+               "fecgpu_sw_encoder_add_source")
+        return esi.value
+
+    def flush(self) -> int:
+        return _check(_lib().fecgpu_sw_encoder_flush(self._h), "fecgpu_sw_encoder_flush")
+
+    def next_repair(self):
+        """-> ((fss, nss, key, dt), symbol bytes) or None."""
+        h = fecgpu_sw_repair()
+        buf = ctypes.create_string_buffer(self.params.symbol_size)
+        n = _lib().fecgpu_sw_encoder_next_repair(self._h, ctypes.byref(h), buf, self.params.symbol_size)
+        if n == ERR_DONE:
+            return None
+        _check(n, "fecgpu_sw_encoder_next_repair")
+        return (h.fss, h.nss, h.key, h.dt), buf.raw[:n]
+
+    def close(self):
+        if self._h:
+            _lib().fecgpu_sw_encoder_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SwDecoder:
+    """Per-connection sliding-window receiver (fecgpu_sw_decoder_*)."""
+
+    def __init__(self, ctx: Context, params: fecgpu_sw_params):
+        self._ctx = ctx
+        self.params = params
+        self._h = ctypes.c_void_p()
+        _check(_lib().fecgpu_sw_decoder_new(ctx.handle, ctypes.byref(params), ctypes.byref(self._h)),
+               "fecgpu_sw_decoder_new")
+
+    def add_source(self, esi: int, pkt: bytes) -> int:
+        return _lib().fecgpu_sw_decoder_add_source(self._h, esi, pkt, len(pkt))
+
+    def add_repair(self, hdr, sym: bytes) -> int:
+        fss, nss, key, dt = hdr
+        h = fecgpu_sw_repair(fss, nss, key, dt)
+        return _check(_lib().fecgpu_sw_decoder_add_repair(self._h, ctypes.byref(h), sym, len(sym)),
+                      "fecgpu_sw_decoder_add_repair")
+
+    def flush(self) -> int:
+        return _check(_lib().fecgpu_sw_decoder_flush(self._h), "fecgpu_sw_decoder_flush")
+
+    def recovered(self, esi: int) -> bytes | None:
+        cap = self.params.symbol_size
+        buf = ctypes.create_string_buffer(cap)
+        n = _lib().fecgpu_sw_decoder_recovered(self._h, esi, buf, cap)
+        if n == ERR_DONE:
+            return None
+        n = _check(n, "fecgpu_sw_decoder_recovered")
+        return buf.raw[:n]
+
+    def drain_recovered(self) -> list[int]:
+        out, esi = [], ctypes.c_uint64()
+        while _lib().fecgpu_sw_decoder_next_recovered(self._h, ctypes.byref(esi)) == 0:
+            out.append(esi.value)
+        return out
+
+    def close(self):
+        if self._h:
+            _lib().fecgpu_sw_decoder_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def frame_sw_source(esi: int) -> bytes:
+    buf = ctypes.create_string_buffer(16)
+    n = _check(_lib().fecgpu_frame_write_sw_source(buf, 16, esi), "fecgpu_frame_write_sw_source")
+    return buf.raw[:n]
+
+
+def frame_sw_repair(hdr, sym: bytes) -> bytes:
+    fss, nss, key, dt = hdr
+    h = fecgpu_sw_repair(fss, nss, key, dt)
+    cap = len(sym) + 48
+    buf = ctypes.create_string_buffer(cap)
+    n = _check(_lib().fecgpu_frame_write_sw_repair(buf, cap, ctypes.byref(h), sym, len(sym)),
+               "fecgpu_frame_write_sw_repair")
+    return buf.raw[:n]
+
+
 def encoder_flush_many(encs) -> int:
     """fecgpu_encoder_flush_many: encode every queued window of several encoders
     (same ctx, code, max_len) in one launch; returns the windows encoded."""
@@ -566,6 +714,11 @@ def frame_parse(data: bytes):
     if f.type == FRAME_REPAIR:
         off = f.payload - ctypes.addressof(buf)
         out.update(k=f.k, r=f.r, nsrc=f.nsrc, payload=bytes(data[off:off + f.payload_len]))
+    elif f.type == FRAME_SW_SOURCE:
+        out.update(esi=f.win)
+    elif f.type == FRAME_SW_REPAIR:
+        off = f.payload - ctypes.addressof(buf)
+        out.update(hdr=(f.win, f.nsrc, f.key, f.dt), payload=bytes(data[off:off + f.payload_len]))
     return n, out
 
 

@@ -105,3 +105,32 @@ def test_stream_of_frames():
         pos += n
     assert len(seen) == len(frames)
     assert [f["payload"] for f in seen if f["type"] == fecgpu.FRAME_REPAIR] == [bytes([w]) * 50 for w in range(3)]
+
+
+@pytest.mark.parametrize("esi", [0, 63, 64, 1 << 20, (1 << 62) - 1])
+def test_sw_source_round_trip(esi):
+    b = fecgpu.frame_sw_source(esi)
+    n, f = fecgpu.frame_parse(b + b"payload")
+    assert n == len(b)
+    assert f["type"] == fecgpu.FRAME_SW_SOURCE and f["esi"] == esi
+
+
+@pytest.mark.parametrize("hdr", [(0, 1, 0, 15), (123456789, 32, 65535, 7), ((1 << 62) - 1, 255, 1, 0)])
+@pytest.mark.parametrize("sym_len", [0, 1, 1202])
+def test_sw_repair_round_trip(hdr, sym_len):
+    sym = bytes((i * 7) & 0xFF for i in range(sym_len))
+    b = fecgpu.frame_sw_repair(hdr, sym)
+    n, f = fecgpu.frame_parse(b + b"x")
+    assert n == len(b)
+    assert f["type"] == fecgpu.FRAME_SW_REPAIR and f["hdr"] == hdr and f["payload"] == sym
+    # RFC 8681 repair FEC payload ID fields, QUIC varints: type 0xfec3 is 4 bytes
+    assert b[:4] == bytes.fromhex("8000fec3")
+
+
+def test_sw_repair_errors():
+    for bad in [(0, 0, 0, 15), (0, 256, 0, 15), (0, 8, 0, 16), (1 << 62, 8, 0, 15)]:
+        with pytest.raises(fecgpu.FecError):
+            fecgpu.frame_sw_repair(bad, b"abc")
+    b = fecgpu.frame_sw_repair((5, 8, 9, 15), b"0123456789")
+    with pytest.raises(fecgpu.FecError):
+        fecgpu.frame_parse(b[:-1])   # truncated payload
