@@ -417,7 +417,9 @@ typedef struct fecgpu_sw_params {
     uint8_t  dt;          /* RFC 8681 DT, 0..15 */
     uint8_t  reserved[3];
     uint32_t batch;       /* repairs per encode launch / per automatic decoder flush, >= 1 */
-    uint32_t span;        /* receiver: sources kept behind the newest (0 = 16 x window) */
+    uint32_t span;        /* receiver: sources kept behind the newest (0 = 16 x window +
+                             2 x batch x step); repairs whose window starts before it are dropped
+                             (add_repair returns FECGPU_ERR_DONE) */
 } fecgpu_sw_params;
 
 typedef struct fecgpu_sw_encoder fecgpu_sw_encoder;

@@ -1617,6 +1617,17 @@ __global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint8_t *regions = reinterpret_cast<uint8_t *>(dyn);
     constexpr int RT = CombRegion<R>::RT;
+#if FECGPU_CHECK
+    // the checked build bounds the block kernels' symbol accesses; the
+    // sliding-window jobs address rows through their own tables: unchecked
+    if (tid == 0) {
+        s_chk.lo[0] = 0;
+        s_chk.n[0] = ~0ull;
+        s_chk.lo[1] = 0;
+        s_chk.n[1] = 0;
+    }
+    __syncthreads();
+#endif
     for (XcdRange xr = xcd_range((a.njobs + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
         const uint64_t j0 = xr.cur * a.wpb;
         const int nb = (int)min((uint64_t)a.wpb, a.njobs - j0);
