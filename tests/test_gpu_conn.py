@@ -206,8 +206,10 @@ def test_udp_ring_driver(args):
     ["udp_ring_asan", "gf256", "16", "4", "1200", "50003", "0.08", "128"],
     ["many_conn_asan", "gf256", "16", "4", "1200", "60", "5", "0.1", "3"],
     ["many_conn_asan", "xor", "8", "2", "700", "60", "5", "0.05", "2"],
+    ["sw_conn_bench_asan", "1202", "32", "8", "6", "0.05", "16"],
+    ["sw_conn_bench_asan", "302", "16", "4", "3", "0.1", "4", "128"],
 ], ids=["conn-gf-k32r8-lp", "conn-xor-reorder-dup", "conn-gf-short-last", "udp-gf-k16r4",
-        "many-gf-k16r4", "many-xor-k8r2"])
+        "many-gf-k16r4", "many-xor-k8r2", "sw-conn-W32", "sw-conn-W16-small-span"])
 def test_native_drivers_under_asan(args):
     """The per-connection objects, pools, frames and pinned rings under host
     AddressSanitizer + UBSan (lib/asan/libfecgpu.so: host code instrumented, kernels
