@@ -23,6 +23,7 @@ torch.distributed.run child, spawned before this process touches the GPU.
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, choices=sorted(workloads.CONFIGS))
     ap.add_argument("--nwin", type=int, default=0, help="windows per GPU (0 = config default)")
+    ap.add_argument("--matrix", default="cauchy", choices=["cauchy", "vandermonde", "rlc"],
+                    help="GF configs: parity rows (rlc: RFC 8681 random linear code, dense)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU work for the cpu_baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -112,7 +115,8 @@ def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
     aff = len(os.sched_getaffinity(0))
     if threads <= 0:
         threads = host_share()
-    scheme = O.XOR if cfg.scheme == "xor" else O.GF256
+    scheme = (O.XOR if cfg.scheme == "xor" else O.RLC(cfg.rlc_key, cfg.rlc_dt) if cfg.matrix == "rlc"
+              else O.GF256_VDM if cfg.matrix == "vandermonde" else O.GF256)
     win_bytes = (cfg.k + cfg.r) * cfg.stride
     max_nw = max(threads, (2 << 30) // win_bytes)  # sample buffer <= 2 GiB
 
@@ -196,6 +200,8 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     cfg = workloads.CONFIGS[args.config]
+    if args.matrix != "cauchy" and cfg.scheme != "xor":
+        cfg = dataclasses.replace(cfg, matrix=args.matrix, name=f"{cfg.name}-{args.matrix}")
     nwin = args.nwin or cfg.nwin_per_gpu
     w0, nwin = shard.weak_shard(rank, world, nwin)  # this rank's global window range
     ctx = fecgpu.Context()
@@ -287,7 +293,8 @@ def main():
         dom = "decode" if dec_ms > enc_ms else "encode"
         dom_ms = max(enc_ms, dec_ms)
         achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(args.config, dom) if nwin == cfg.nwin_per_gpu else (None, None)
+        traffic, traffic_src = (pmc_traffic(args.config, dom) if nwin == cfg.nwin_per_gpu and cfg.matrix == "cauchy"
+                                else (None, None))
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
             log("cpu baseline")
@@ -317,6 +324,7 @@ def main():
             "config": {
                 "workload": cfg.name,
                 "scheme": cfg.scheme, "k": cfg.k, "r": cfg.r,
+                **({"matrix": cfg.matrix} if cfg.scheme != "xor" else {}),
                 "windows_per_gpu": nwin, "packet_bytes": cfg.L if cfg.workload == 0 else "1200|9000 mixed",
                 "erasures": cfg.erasure_desc,
                 "parallelism": f"window-shard x{world}",

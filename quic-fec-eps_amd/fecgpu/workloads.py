@@ -28,11 +28,20 @@ class Config:
     erasure: int
     erasure_desc: str
     host: bool = False     # windows live in pinned host memory (config 5: PCIe inclusive)
+    matrix: str = "cauchy"  # GF parity rows: cauchy | vandermonde | rlc (bench.py --matrix)
+    rlc_key: int = 0
+    rlc_dt: int = 15
 
     @property
     def code(self) -> Code:
         return Code(self.scheme, self.k, self.r,
-                    "fixed" if self.workload == WORKLOAD_FIXED else "lenprefix")
+                    "fixed" if self.workload == WORKLOAD_FIXED else "lenprefix", self.matrix,
+                    self.rlc_key, self.rlc_dt)
+
+    @property
+    def mds(self) -> bool:
+        """Any e <= r erasures recoverable (every matrix but the random linear code)."""
+        return self.scheme == "xor" or self.matrix != "rlc"
 
     @property
     def stride(self) -> int:
@@ -182,13 +191,21 @@ class Batch:
             eq = ((v[s:s + chunk, :c.k] == saved[s:s + chunk]) | pad).flatten(1).all(1)
             mismatched += int((ok_status[s:s + chunk] & ~eq).sum().item())
         unrec = int((~ok_status).sum().item())
-        status_agree = bool(((~ok_status) == bad_expect).all().item())
+        if c.mds:
+            status_agree = bool(((~ok_status) == bad_expect).all().item())
+            rank_deficient = 0
+        else:  # RLC: every window an MDS code loses is lost, plus the rank-deficient ones
+            status_agree = bool((~ok_status | ~bad_expect).all().item())
+            rank_deficient = int((~ok_status & ~bad_expect).sum().item())
         del saved
         # restore the erased symbols so the buffer is reusable
         self.synthesize(ctx, w0)
-        return {"ok": mismatched == 0 and status_agree, "windows": self.nwin,
-                "mismatched_ok_windows": mismatched, "unrecoverable": unrec,
-                "status_matches_expected": status_agree}
+        out = {"ok": mismatched == 0 and status_agree, "windows": self.nwin,
+               "mismatched_ok_windows": mismatched, "unrecoverable": unrec,
+               "status_matches_expected": status_agree}
+        if not c.mds:
+            out["rank_deficient"] = rank_deficient
+        return out
 
 
 @dataclass
