@@ -56,6 +56,7 @@ struct EncTables {
     uint4 *ab = nullptr;
     uint32_t *c = nullptr;
     uint8_t *coef = nullptr;  // parity rows P[r][k] (non-Cauchy matrices: the decode plan reads them)
+    uint32_t *bs = nullptr;   // plane masks [k][r][8] (runtime bit-sliced encode)
 };
 
 uint8_t host_gf_pow(uint8_t a, int n) {  // a^n, 0^0 = 1
@@ -318,6 +319,7 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
         (void)hipFree(kv.second.ab);
         (void)hipFree(kv.second.c);
         if (kv.second.coef) (void)hipFree(kv.second.coef);
+        if (kv.second.bs) (void)hipFree(kv.second.bs);
     }
     for (auto &kv : ctx->stage) {
         (void)hipSetDevice(kv.first);
@@ -406,6 +408,33 @@ ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out)
     HIP_TRY(hipMalloc(&t.c, cc.size() * sizeof(uint32_t)), "hipMalloc");
     HIP_TRY(hipMemcpy(t.ab, ab.data(), ab.size() * sizeof(uint4), hipMemcpyHostToDevice), "hipMemcpy");
     HIP_TRY(hipMemcpy(t.c, cc.data(), cc.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy");
+    {
+        // (j, i, p): lo = the planes q < 4, hi = the planes q >= 4 (as bits
+        // q, q - 4) for which bit p of P[i][j] * 2^q is set; stored lo | hi << 8,
+        // or as two dwords lo, hi (fec_kernels.hip rbs::)
+        static constexpr GfTables g = make_gf_tables();
+        std::vector<uint32_t> m((size_t)k * r * 8 * kRbsPlaneDw, 0);
+        for (int j = 0; j < k; j++)
+            for (int i = 0; i < r; i++) {
+                const uint8_t c = P[(size_t)i * k + j];
+                for (int p = 0; p < 8; p++) {
+                    uint32_t lo = 0, hi = 0;
+                    for (int q = 0; q < 8; q++) {
+                        const uint8_t col = c ? g.exp[g.log[c] + q] : 0;
+                        if ((col >> p) & 1) (q < 4 ? lo : hi) |= 1u << (q & 3);
+                    }
+                    uint32_t *d = &m[(((size_t)j * r + i) * 8 + p) * kRbsPlaneDw];
+                    if (kRbsPlaneDw == 2) {
+                        d[0] = lo;
+                        d[kRbsPlaneDw - 1] = hi;
+                    } else {
+                        d[0] = lo | hi << 8;
+                    }
+                }
+            }
+        HIP_TRY(hipMalloc(&t.bs, m.size() * sizeof(uint32_t)), "hipMalloc");
+        HIP_TRY(hipMemcpy(t.bs, m.data(), m.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy");
+    }
     if (code->matrix != FECGPU_MATRIX_CAUCHY) {
         HIP_TRY(hipMalloc(&t.coef, P.size()), "hipMalloc");
         HIP_TRY(hipMemcpy(t.coef, P.data(), P.size(), hipMemcpyHostToDevice), "hipMemcpy");
@@ -700,6 +729,7 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
             if (rc) return rc;
             a.enc_ab = t.ab;
             a.enc_c = t.c;
+            a.enc_bs = t.bs;
             p.lds_bytes = (uint32_t)(k * r * 20);
         }
         p.wpb = choose_wpb(ncol, 0, 0);
@@ -735,6 +765,18 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         // so a partly idle last pass costs more than in the table kernels).
         p.bitslice = true;
         p.matrix = (int)code->matrix;
+#if !FECGPU_BS_FLAT
+        p.flat = false;
+#endif
+        p.lds_bytes = 0;
+        const uint32_t units = ncol ? (ncol + 1) / 2 : (uint32_t)((stride >> 4) + 1) / 2;
+        const uint32_t want = (uint32_t)ctx->bs_passes * kBlock;
+        p.wpb = units ? std::max(1, std::min<int>(kMaxWpb, (int)((want + units - 1) / units))) : kMaxWpb;
+    }
+    else if (!decode && scheme == FECGPU_SCHEME_GF256 && !remote && ctx->bitslice && r >= FECGPU_RBS_MIN_R) {
+        // no compiled masks for this code: the runtime-mask kernel, same unit
+        // space and group sizing
+        p.rbitslice = true;
 #if !FECGPU_BS_FLAT
         p.flat = false;
 #endif

@@ -32,6 +32,7 @@ struct BatchArgs {
     const uint4 *enc_ab;       // encode tables [k][r] (TA lo/hi, TB lo/hi)
     const uint32_t *enc_c;     // encode tables [k][r] (TC)
     const uint8_t *coef;       // GF decode: parity rows P[r][k] of a non-Cauchy matrix (null: Cauchy)
+    const uint32_t *enc_bs;    // runtime bit-sliced encode: plane indices [k][r][8][kRbsPlaneDw]
     uint64_t nwin;
     uint64_t gmask[kMaxR];     // XOR: members of group g (bit j)
     uint64_t step_win;         // flat mode: (grid threads) / ncol
@@ -66,7 +67,20 @@ struct LaunchPlan {
                          // deep load batches (PCIe latency, small batches)
     bool bitslice;       // GF encode by the bit-sliced kernel (compile-time matrix)
     int matrix;          // bitslice: the code's matrix (fecgpu_matrix)
+    bool rbitslice;      // GF encode by the runtime-mask bit-sliced kernel (any matrix)
 };
+
+// GF encode of r parity rows goes to the runtime-mask bit-sliced kernel
+// (fec_kernels.hip rbs::) when no compiled one exists: r >= this.
+#ifndef FECGPU_RBS_MIN_R
+#define FECGPU_RBS_MIN_R 5
+#endif
+#ifndef FECGPU_RBS_WIDE
+// runtime bit-sliced encode: 1 = a dword per plane index (lo, hi), loaded
+// straight into M0 with no unpacking; 0 = one dword per plane (lo | hi << 8)
+#define FECGPU_RBS_WIDE 1
+#endif
+constexpr int kRbsPlaneDw = FECGPU_RBS_WIDE ? 2 : 1;  // mask dwords per output plane
 
 // GF encode of (k, r, matrix) has a compiled bit-sliced kernel.
 bool bitslice_supported(int k, int r, int matrix);

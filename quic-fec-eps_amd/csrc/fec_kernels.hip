@@ -868,6 +868,230 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
     }
 }
 
+// ==================================== runtime-mask bit-sliced GF encode ===
+// The bit-sliced encode for a matrix known only at run time (RLC rows, and
+// every (k, r) without a compiled kernel): the same planes, combinations and
+// 3-input XORs as bs::, with each output plane's pick of lo[] / hi[] read from
+// a per-code mask table (a.enc_bs: byte (j, i, p) = lo | hi << 4, the input
+// planes of source j feeding plane p of repair i) through scalar loads.  The
+// wave-uniform index selects a combination by relative VGPR addressing
+// (s_set_gpr_idx_on / v_mov / off), so an output plane costs 3 VALU ops and a
+// few SALU ops where the table multiply spends 3 v_perm + XOR per dword and
+// repair.  Bytes equal the table multiply's (tests/test_gpu_parity.py).
+#ifndef FECGPU_RBS_U
+#define FECGPU_RBS_U 1  // runtime bit-sliced encode: sources loaded per batch (1 > 2 = 4 by 1-2 %, cfg4 rlc)
+#endif
+
+namespace rbs {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(4))) const uint32_t *cmask;
+#else
+typedef const uint32_t *cmask;
+#endif
+
+#ifndef FECGPU_RBS_FUSE
+// 1: the lo pick is the XOR's own indexed source operand (2 VALU per output
+// plane); 0: both picks by v_mov, then the XOR (3 VALU)
+#define FECGPU_RBS_FUSE 1
+#endif
+
+// a[q] ^= lo[d[q] & 0xff] ^ hi[d[q] >> 8] for four output planes q, where
+// d[q] (wave-uniform, SGPR) packs the plane's lo / hi indices.  Relative VGPR
+// addressing (s_set_gpr_idx_on / _idx / _off, M0[7:0] = index) needs each
+// table in consecutive registers, so lo / hi are pinned to v32-v47 / v48-v63 by
+// register constraints (the same registers in every block, so no copies), and
+// one asm block holds the picks and XORs: the compiler's own lowering of
+// lo[i] hoists every pick of a source ahead of the XORs and holds 128 of them
+// in VGPRs at once (251 VGPRs, 2 waves per SIMD).  Index mode stays on across
+// the block and only instructions whose source 0 is a table run in it.
+#define RBS_IN(A, N, R0) "{v" #R0 "}"(A[N])
+#if FECGPU_RBS_WIDE
+#define RBS_HI(Q) "s_set_gpr_idx_idx %[h" #Q "]\n\t"
+#define RBS_LO(Q) "s_set_gpr_idx_idx %[d" #Q "]\n\t"
+#else
+#define RBS_HI(Q) "s_lshr_b32 %[h], %[d" #Q "], 8\n\ts_set_gpr_idx_idx %[h]\n\t"
+#define RBS_LO(Q) "s_set_gpr_idx_idx %[d" #Q "]\n\t"
+#endif
+#ifndef FECGPU_RBS_PAIR
+#define FECGPU_RBS_PAIR 1  // 1: two planes' hi picks, then their lo picks + XORs (more distance per dependency)
+#endif
+#define RBS_PAIR(Q0, Q1)                                 \
+    RBS_HI(Q0) "v_mov_b32 %[t0], v48\n\t"                \
+    RBS_HI(Q1) "v_mov_b32 %[t1], v48\n\t"                \
+    RBS_LO(Q0) "v_bitop3_b32 %[a" #Q0 "], v32, %[a" #Q0 "], %[t0] bitop3:0x96\n\t" \
+    RBS_LO(Q1) "v_bitop3_b32 %[a" #Q1 "], v32, %[a" #Q1 "], %[t1] bitop3:0x96\n\t"
+#if FECGPU_RBS_FUSE
+#define RBS_PLANE(Q, T)                                  \
+    RBS_HI(Q)                                            \
+    "v_mov_b32 %[" #T "], v48\n\t"                       \
+    RBS_LO(Q)                                            \
+    "v_bitop3_b32 %[a" #Q "], v32, %[a" #Q "], %[" #T "] bitop3:0x96\n\t"
+#else
+#define RBS_PLANE(Q, T)                                  \
+    RBS_HI(Q)                                            \
+    "v_mov_b32 %[" #T "], v48\n\t"                       \
+    RBS_LO(Q)                                            \
+    "v_mov_b32 %[u], v32\n\t"                            \
+    "s_set_gpr_idx_off\n\t"                              \
+    "v_bitop3_b32 %[a" #Q "], %[u], %[a" #Q "], %[" #T "] bitop3:0x96\n\t" \
+    "s_set_gpr_idx_on %[d" #Q "], gpr_idx(SRC0)\n\t"
+#endif
+__device__ __forceinline__ void pick4(uint32_t &a0, uint32_t &a1, uint32_t &a2, uint32_t &a3,
+                                      const uint32_t (&d)[4], const uint32_t (&e)[4], const uint32_t (&lo)[16],
+                                      const uint32_t (&hi)[16]) {
+    uint32_t t0, t1, u, h;
+    asm("s_set_gpr_idx_on %[d0], gpr_idx(SRC0)\n\t"
+#if FECGPU_RBS_PAIR && FECGPU_RBS_FUSE
+        RBS_PAIR(0, 1) RBS_PAIR(2, 3)
+#else
+        RBS_PLANE(0, t0) RBS_PLANE(1, t1) RBS_PLANE(2, t0) RBS_PLANE(3, t1)
+#endif
+        "s_set_gpr_idx_off"
+        : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3), [t0] "=&v"(t0), [t1] "=&v"(t1),
+          [u] "=&v"(u), [h] "=&s"(h)
+        : [d0] "s"(d[0]), [d1] "s"(d[1]), [d2] "s"(d[2]), [d3] "s"(d[3]),
+          [h0] "s"(e[0]), [h1] "s"(e[1]), [h2] "s"(e[2]), [h3] "s"(e[3]),
+          RBS_IN(lo, 0, 32), RBS_IN(lo, 1, 33), RBS_IN(lo, 2, 34), RBS_IN(lo, 3, 35),
+          RBS_IN(lo, 4, 36), RBS_IN(lo, 5, 37), RBS_IN(lo, 6, 38), RBS_IN(lo, 7, 39),
+          RBS_IN(lo, 8, 40), RBS_IN(lo, 9, 41), RBS_IN(lo, 10, 42), RBS_IN(lo, 11, 43),
+          RBS_IN(lo, 12, 44), RBS_IN(lo, 13, 45), RBS_IN(lo, 14, 46), RBS_IN(lo, 15, 47),
+          RBS_IN(hi, 0, 48), RBS_IN(hi, 1, 49), RBS_IN(hi, 2, 50), RBS_IN(hi, 3, 51),
+          RBS_IN(hi, 4, 52), RBS_IN(hi, 5, 53), RBS_IN(hi, 6, 54), RBS_IN(hi, 7, 55),
+          RBS_IN(hi, 8, 56), RBS_IN(hi, 9, 57), RBS_IN(hi, 10, 58), RBS_IN(hi, 11, 59),
+          RBS_IN(hi, 12, 60), RBS_IN(hi, 13, 61), RBS_IN(hi, 14, 62), RBS_IN(hi, 15, 63));
+}
+#undef RBS_IN
+#undef RBS_PLANE
+#undef RBS_HI
+#undef RBS_LO
+#undef RBS_PAIR
+
+// acc ^= source planes x times the source's mask row mk ([R][8][kRbsPlaneDw] dwords)
+template <int R>
+__device__ __forceinline__ void source(const uint32_t (&x)[8], uint32_t (&acc)[R][8], cmask mk) {
+    uint32_t lo[16], hi[16];
+    lo[0] = hi[0] = 0;
+#pragma unroll
+    for (int s = 1; s < 16; s++) {
+        const int b = __builtin_ctz(s), rest = s & (s - 1);
+        lo[s] = rest ? bs::oxor(lo[rest], x[b]) : x[b];
+        hi[s] = rest ? bs::oxor(hi[rest], x[4 + b]) : x[4 + b];
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int w = 0; w < 2; w++) {
+            const cmask m = mk + (i * 8 + w * 4) * kRbsPlaneDw;
+            uint32_t d[4], e[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                d[q] = m[q * kRbsPlaneDw];
+                e[q] = m[q * kRbsPlaneDw + kRbsPlaneDw - 1];  // unused when packed
+            }
+            uint32_t(&c)[8] = acc[i];
+            pick4(c[w * 4], c[w * 4 + 1], c[w * 4 + 2], c[w * 4 + 3], d, e, lo, hi);
+        }
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int p = 0; p < 8; p++) asm volatile("" : "+v"(acc[i][p]));
+}
+
+template <int R, int U>
+__device__ __forceinline__ void unit(uint8_t *pa, uint8_t *pb, uint32_t stride, int k, cmask mk,
+                                     bool live, uint64_t od) {
+    uint32_t acc[R][8];
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int p = 0; p < 8; p++) acc[i][p] = 0;
+    const uint8_t *qa = pa, *qb = pb;
+    for (int j0 = 0; j0 < k; j0 += U) {
+        uint32_t x[U][8];
+#pragma unroll
+        for (int t = 0; t < U; t++) {
+            // past k (k % U != 0): reload the last source, masked out below
+            const uint32_t off = (uint32_t)min(t, k - 1 - j0) * stride;
+            const uint4 va = ld16(qa + off), vb = ld16(qb + off);
+            x[t][0] = va.x; x[t][1] = va.y; x[t][2] = va.z; x[t][3] = va.w;
+            x[t][4] = vb.x; x[t][5] = vb.y; x[t][6] = vb.z; x[t][7] = vb.w;
+        }
+#pragma unroll
+        for (int t = 0; t < U; t++) {
+            if (t == 0 || j0 + t < k) {  // uniform
+                bs::tr8(x[t]);
+                source<R>(x[t], acc, mk + (size_t)(j0 + t) * (R * 8 * kRbsPlaneDw));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        qa += U * stride;
+        qb += U * stride;
+        asm volatile("" : "+v"(qa), "+v"(qb));
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        bs::tr8(acc[i]);
+        if (live) {
+            st16(pa + od + (size_t)(k + i) * stride, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
+            st16(pb + od + (size_t)(k + i) * stride, make_uint4(acc[i][4], acc[i][5], acc[i][6], acc[i][7]));
+        }
+    }
+}
+
+}  // namespace rbs
+
+// Unit spaces as gf_encode_bs_kernel (flat over uniform windows, group mode
+// otherwise); the masks are the code's, R = its r.
+#ifndef FECGPU_RBS_MINW
+#define FECGPU_RBS_MINW 4  // runtime bit-sliced encode: waves per SIMD asked of the register allocator
+#endif
+template <int R, bool FLAT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FECGPU_RBS_MINW, 8)))
+void gf_encode_rbs_kernel(BatchArgs a) {
+    CHK_PROLOGUE(a);
+    const rbs::cmask mk = (rbs::cmask)a.enc_bs;
+    const int k = a.k;
+    if constexpr (FLAT) {
+        const uint32_t ncol = a.ncol, h = (ncol + 1) >> 1;
+        const uint64_t total = a.nwin * h;
+        for (XcdRange xr = xcd_range((total + kBlock - 1) / kBlock, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+            uint64_t s = xr.cur * kBlock + threadIdx.x;
+            const bool live = s < total;
+            if (!live) s = total - 1;
+            const uint64_t w = s / h;
+            const uint32_t u = (uint32_t)(s - w * h);
+            uint8_t *pa, *pb;
+            bs::unit_cols(a.win + w * a.wpitch, u, h, ncol, pa, pb);
+            rbs::unit<R, FECGPU_RBS_U>(pa, pb, a.stride, k, mk, live, a.out_delta + w * a.out_wdelta);
+        }
+    } else {
+        __shared__ GroupLds g;
+        for (XcdRange xr = xcd_range((a.nwin + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+            const uint64_t w0 = xr.cur * a.wpb;
+            const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
+            group_geometry(a, g, w0, nb);
+            __syncthreads();
+            if (threadIdx.x < 64)
+                block_prefix(g.pfx, (int)threadIdx.x < nb ? (g.ncol[threadIdx.x] + 1u) >> 1 : 0u, threadIdx.x);
+            __syncthreads();
+            const uint32_t total = g.pfx[nb];
+            int wl = 0;
+            for (uint32_t s0 = 0; s0 < total; s0 += kBlock) {
+                const bool live = s0 + threadIdx.x < total;
+                const uint32_t s = live ? s0 + threadIdx.x : total - 1;
+                while (s >= g.pfx[wl + 1]) wl++;
+                uint8_t *pa, *pb;
+                bs::unit_cols(reinterpret_cast<uint8_t *>(g.base[wl]), s - g.pfx[wl], g.pfx[wl + 1] - g.pfx[wl],
+                              g.ncol[wl], pa, pb);
+                rbs::unit<R, FECGPU_RBS_U>(pa, pb, g.stride[wl], k, mk, live,
+                                           a.out_delta + (w0 + wl) * a.out_wdelta);
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // ============================================================ decode ===
 template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void xor_decode_kernel(BatchArgs a) {
@@ -1932,6 +2156,18 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
 #undef FECGPU_BS_LAUNCH
 #undef FECGPU_BS_LAUNCH_M
         return hipErrorInvalidValue;
+    }
+    if (p.rbitslice) {
+        const uint64_t want = (a.nwin * ((a.ncol + 1) / 2) + kBlock - 1) / kBlock;
+        switch (a.r) {
+#define FECGPU_RBS_CASE(R_)                                                                        \
+            case R_:                                                                               \
+                return p.flat ? launch(gf_encode_rbs_kernel<R_, true>, a, p, s, false, want)       \
+                              : launch(gf_encode_rbs_kernel<R_, false>, a, p, s, false);
+            FECGPU_RBS_CASE(4) FECGPU_RBS_CASE(5) FECGPU_RBS_CASE(6) FECGPU_RBS_CASE(7) FECGPU_RBS_CASE(8)
+#undef FECGPU_RBS_CASE
+            default: return hipErrorInvalidValue;
+        }
     }
     const bool flat = p.flat;
     if (scheme == 0) {

@@ -49,6 +49,7 @@ for s in "$@"; do
         prof5) prof prof5 5 ;;
         prof3) prof prof3 3 ;;
         prof4) prof prof4 4 ;;
+        prof4rlc) prof prof4rlc 4 --matrix rlc ;;
         pmc2r) pmc pmc2r 2 FETCH_SIZE ;;
         pmc2w) pmc pmc2w 2 WRITE_SIZE ;;
         pmc3r) pmc pmc3r 3 FETCH_SIZE ;;

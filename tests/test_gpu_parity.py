@@ -575,7 +575,8 @@ def test_linearity_full_size(ctx):
     assert torch.equal(a.view[:, cfg.k:], ra ^ rb)
 
 
-BS_CODES = [(16, 8), (24, 8), (32, 8), (8, 8), (16, 4)]  # (8, 8), (16, 4): table kernel (not compiled)
+# (16|24|32, 8): compiled masks; r >= 5 otherwise: runtime masks (rbs); (16, 4): table kernel
+BS_CODES = [(16, 8), (24, 8), (32, 8), (8, 8), (16, 4), (1, 5), (13, 6), (45, 7), (56, 8)]
 
 
 @pytest.fixture(scope="module")
@@ -591,9 +592,9 @@ def ctx_tables():
 @pytest.mark.parametrize("k,r", BS_CODES)
 @pytest.mark.parametrize("wl,L,nwin", [(0, 1200, 70), (1, 0, 9), (0, 16, 33), (0, 1, 5), (0, 9000, 6)])
 def test_bitslice_encode_vs_oracle(ctx, ctx_tables, k, r, wl, L, nwin, matrix):
-    """The bit-sliced GF encode (compile-time parity rows, Cauchy or systematic
-    Vandermonde, DESIGN.md §GF bit-slicing) emits the oracle's repairs for every
-    compiled code: odd column counts (1200 B: 75 columns, the last unit without a
+    """The bit-sliced GF encodes (compile-time parity rows, Cauchy or systematic
+    Vandermonde, and runtime plane masks for the other codes with r >= 5,
+    DESIGN.md §GF bit-slicing) emit the oracle's repairs for every code: odd column counts (1200 B: 75 columns, the last unit without a
     second column), one column (16 B), S = 1, per-window lengths (mixed MTU,
     LENPREFIX) and 9000-B symbols; and the same bytes as the table-multiply kernel."""
     S = O.sym_lens(wl, SEED + k, 0, nwin, k, L)
@@ -613,7 +614,7 @@ def test_bitslice_encode_vs_oracle(ctx, ctx_tables, k, r, wl, L, nwin, matrix):
     _cmp_emitted(outs[1], oe, S, "table encode")
 
 
-@pytest.mark.parametrize("k,r", [(16, 8), (32, 8)])
+@pytest.mark.parametrize("k,r", [(16, 8), (32, 8), (8, 8), (20, 5)])
 def test_bitslice_ragged_and_split(ctx, k, r):
     """Bit-sliced encode through the ragged (win_off) and split (src / repair arrays) layouts."""
     nwin = 11
