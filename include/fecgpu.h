@@ -134,7 +134,10 @@ void    fecgpu_host_free(void *p);
  * windows over PCIe instead of H2D copies; default 6 = decode zero-copy),
  * "host_chunk_mb" (pipeline chunk, default 128); "bitslice" (1 default: GF
  * encode of a code with a compiled bit-sliced kernel — Cauchy or Vandermonde
- * rows, r = 8, k in {16, 24, 32} — uses it; 0: the table multiply for every code);
+ * rows, r = 8, k in {16, 24, 32} — uses it, and of any other code with r >= 5
+ * the runtime-mask bit-sliced kernel; 0: the table multiply for every code);
+ * "sw_group" (sliding-window encode: consecutive repairs per combine job, each
+ * source loaded once per group; 1, 2 or 4, default 4);
  * "bs_passes" (bit-sliced encode on per-window lengths: 256-unit passes per
  * window group at the longest window, default 8); "conn_streams" (streams per
  * device shared round robin by the encoders / decoders created afterwards,

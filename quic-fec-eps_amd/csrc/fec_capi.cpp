@@ -158,6 +158,7 @@ struct fecgpu_ctx {
     size_t pinned_cache_cap = (size_t)1 << 30;
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
+    int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4)
     // FECGPU_CHECK builds: bytes taken off the end of every checked range, so a
     // test can see the checker fire on a correct kernel ("check_shrink")
     int check_shrink = 0;
@@ -295,6 +296,11 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
     if (!std::strcmp(key, "conn_streams")) {
         if (value < 1 || value > 64) return FECGPU_ERR_INVALID_ARG;
         ctx->conn_nstreams = (int)value;  // objects created from now on
+        return 0;
+    }
+    if (!std::strcmp(key, "sw_group")) {
+        if (value != 1 && value != 2 && value != 4) return FECGPU_ERR_INVALID_ARG;
+        ctx->sw_group = (int)value;  // calls and objects created from now on
         return 0;
     }
     if (!std::strcmp(key, "bitslice")) {
@@ -999,6 +1005,8 @@ ssize_t set_dev_error(hipError_t e, const char *what) { return dev_err(e, what);
 int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget) {
     return choose_wpb(ncol, lds_per_unit, lds_budget);
 }
+
+int ctx_sw_group(const fecgpu_ctx *ctx) { return ctx->sw_group; }
 
 ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p) {
     int dev = 0;

@@ -172,6 +172,10 @@ struct CombArgs {
     uint8_t *out_base;
     const uint8_t *xor_base;
     uint64_t njobs;
+    // optional device count of further jobs after the first njobs (grouped
+    // encode's per-repair tail), at most extra_max; the grid covers the maximum
+    const uint32_t *extra;
+    uint64_t extra_max;
     uint32_t ncol, stride;
     int wpb, nin_max, nout_max;
     uint32_t job_lds;
@@ -180,21 +184,35 @@ struct CombArgs {
 // LDS bytes per job of comb_kernel<R> at nin_max inputs
 inline uint32_t comb_job_lds(int nin_max, int R) {
     const uint32_t rt = R == 1 ? 1u : (uint32_t)(R + 3) & ~3u;
-    return ((uint32_t)nin_max * (16u * R + 4u * rt) + 8u * R + 8u + 15u) & ~15u;
+    return ((uint32_t)nin_max * (16u * R + 4u * rt + 1u) + 8u * R + 8u + 15u) & ~15u;
 }
 hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
 
-// encode: job t = repair t (coefficients at coef + t * kSwCoefPitch, output rep row t)
+// encode: job t = repair t (coefficients at coef + t * kSwCoefPitch, output rep row t).
+// group > 1: the repairs t0 = g * group .. t0 + group - 1 share job g when
+// their windows fit in span_max sources together: one output per repair, the
+// union of their windows as input rows, zero coefficients outside each window
+// (at coef + t0 * kSwCoefPitch as [n][span]), so each source is loaded once
+// per group instead of once per repair.  The repairs of groups that do not
+// fit get one job each after the ngroups group jobs, counted in *tail
+// (zeroed by the caller; sw_enc_jobs(nrep, group) jobs of room).
 struct SwEncCoefArgs {
     const fecgpu_sw_repair *hdr;
     uint64_t nrep, nsrc;
     uint32_t stride;
     int max_window;
+    int group, span_max;
+    uint32_t *tail;
     CombJob *jobs;
     uint8_t *coef;
     uint64_t *outs;
 };
 hipError_t launch_sw_enc_coef(const SwEncCoefArgs &a, hipStream_t s);
+// job slots of an encode's scratch (group jobs, per-repair tail, and a
+// CombJob's room for the tail counter)
+inline uint64_t sw_enc_jobs(uint64_t nrep, int group) {
+    return group > 1 ? (nrep + group - 1) / group + nrep + 1 : nrep;
+}
 
 // one linked system of a decode: lost sources unk[u_off ..+ e) (ascending),
 // received repairs eqh[q_off ..+ p) (their syndromes: scratch rows q_off..),
@@ -238,11 +256,17 @@ hipError_t launch_sw_plan(const SwPlanArgs &a, hipStream_t s);
 // end; end: records it), which share that scratch.
 ssize_t set_dev_error(hipError_t e, const char *what);
 // Sliding-window encode launches on `s` with caller-owned device scratch:
-// jobs (nrep x sizeof(CombJob)), coefficients (nrep x kSwCoefPitch), output
-// offsets (nrep x 8) (fec_sw.cpp; used by the per-connection encoder).
+// jobs (sw_enc_jobs(nrep, group) x sizeof(CombJob)), coefficients (nrep x
+// kSwCoefPitch), output offsets (nrep x 8) (fec_sw.cpp; used by the
+// per-connection encoder).  group: repairs per combine job (SwEncCoefArgs);
+// hdr_host: a host-readable copy of hdr (nullable) that lets the launch skip
+// the per-repair tail when every group fits.
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *jobs,
-                       void *coef, void *outs, hipStream_t s);
+                       void *coef, void *outs, hipStream_t s, int group = 1,
+                       const fecgpu_sw_repair *hdr_host = nullptr);
+// the ctx's "sw_group" tuning (repairs per sliding-window encode job)
+int ctx_sw_group(const fecgpu_ctx *ctx);
 int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget);
 ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p);
 ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);

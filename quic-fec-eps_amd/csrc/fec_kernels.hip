@@ -1776,18 +1776,29 @@ __global__ __launch_bounds__(kBlock) void digest_kernel(DigestArgs a) {
 #define FECGPU_COMB_U (R == 1 ? 16 : 8)
 #endif
 
+#ifndef FECGPU_COMB_SKIP
+// combine kernel: skip the multiply-accumulates of zero coefficients (a
+// wave-uniform test per input row and output; grouped sliding-window encode
+// jobs are zero outside each repair's window)
+#define FECGPU_COMB_SKIP 1
+#endif
+
 // Per-job LDS region of comb_kernel<R>: tables [nin_max][R] uint4 (TA/TB),
-// [nin_max][RT] u32 (TC), output column-0 pointers [R], xor pointer.
+// [nin_max][RT] u32 (TC), output column-0 pointers [R], xor pointer, and per
+// input row the mask of outputs with a nonzero coefficient [nin_max] u8
+// (fec_internal.h comb_job_lds).
 template <int R>
 struct CombRegion {
     static constexpr int RT = R == 1 ? 1 : ((R + 3) & ~3);
     uint4 *ab;
     uint32_t *tc;
     uint64_t *optr;  // [R] + xor pointer at optr[R]
+    uint8_t *nz;
     __device__ __forceinline__ CombRegion(uint8_t *region, int nin_max) {
         ab = reinterpret_cast<uint4 *>(region);
         tc = reinterpret_cast<uint32_t *>(region + (size_t)nin_max * R * 16);
         optr = reinterpret_cast<uint64_t *>(region + (size_t)nin_max * (16 * R + 4 * RT));
+        nz = reinterpret_cast<uint8_t *>(optr + R + 1);
     }
 };
 
@@ -1796,7 +1807,7 @@ struct CombRegion {
 // row, stores for u < ne (this lane's job).
 template <int R, int NE>
 __device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, int nin, int ne, uint32_t col,
-                                          const CombRegion<R> &rg) {
+                                          const CombRegion<R> &rg, bool skip) {
     constexpr int U = FECGPU_COMB_U, RT = CombRegion<R>::RT;
     uint4 acc[NE];
 #pragma unroll
@@ -1809,9 +1820,28 @@ __device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, in
         for (int t = 0; t < U; t++) {
             if (q0 + t < nin) {
                 const int q = q0 + t;
+#if FECGPU_COMB_SKIP
+                // the wave's lanes may belong to different jobs: skip what no
+                // active lane needs.  With >= 64 columns per job a wave spans at
+                // most two jobs, its first and last active lanes'; otherwise no skip.
+                uint32_t nzm = 0xffu;
+                // only grouped encode jobs (R = 2, 4) have zero runs; single
+                // repairs, syndromes and solves are dense (+5 % time with the test)
+                if (R > 1 && R < 8 && skip) {
+                    const uint32_t z = rg.nz[q];
+                    const int last = 63 - __builtin_clzll(__builtin_amdgcn_read_exec());
+                    nzm = __builtin_amdgcn_readfirstlane(z) | __builtin_amdgcn_readlane(z, last);
+                }
+                if (!nzm) continue;
+                const Split sp = split(v[t]);
+#pragma unroll
+                for (int m = 0; m < NE; m++)
+                    if ((nzm >> m) & 1u) gmac(acc[m], sp, rg.ab[q * R + m], rg.tc[q * RT + m]);
+#else
                 const Split sp = split(v[t]);
 #pragma unroll
                 for (int m = 0; m < NE; m++) gmac(acc[m], sp, rg.ab[q * R + m], rg.tc[q * RT + m]);
+#endif
             }
         }
     }
@@ -1824,10 +1854,10 @@ __device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, in
 
 template <int R, int NE = R>
 __device__ __forceinline__ void comb_dispatch(int nw, const uint8_t *in, uint32_t stride, int nin, int ne,
-                                              uint32_t col, const CombRegion<R> &rg) {
+                                              uint32_t col, const CombRegion<R> &rg, bool skip) {
     if constexpr (NE >= 1) {
-        if (nw == NE) comb_slot<R, NE>(in, stride, nin, ne, col, rg);
-        else comb_dispatch<R, NE - 1>(nw, in, stride, nin, ne, col, rg);
+        if (nw == NE) comb_slot<R, NE>(in, stride, nin, ne, col, rg, skip);
+        else comb_dispatch<R, NE - 1>(nw, in, stride, nin, ne, col, rg, skip);
     }
 }
 
@@ -1852,9 +1882,10 @@ __global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
     }
     __syncthreads();
 #endif
-    for (XcdRange xr = xcd_range((a.njobs + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+    const uint64_t njobs = a.njobs + (a.extra ? (uint64_t)*a.extra : 0ull);
+    for (XcdRange xr = xcd_range((njobs + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
         const uint64_t j0 = xr.cur * a.wpb;
-        const int nb = (int)min((uint64_t)a.wpb, a.njobs - j0);
+        const int nb = (int)min((uint64_t)a.wpb, njobs - j0);
         // plan: wave w builds the tables of jobs w, w + 4, ...
         for (int jl = wave; jl < nb; jl += kBlock / 64) {
             const CombJob J = a.jobs[j0 + jl];
@@ -1866,6 +1897,11 @@ __global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
                 const CoefTab ct = make_coef_tab(cf[i]);
                 rg.ab[q * R + u] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
                 rg.tc[q * RT + u] = ct.c;
+            }
+            for (int q = lane; q < nin; q += 64) {
+                uint32_t m = 0;
+                for (int u = 0; u < nout; u++) m |= (cf[u * nin + q] != 0 ? 1u : 0u) << u;
+                rg.nz[q] = (uint8_t)m;
             }
             if (lane < nout) rg.optr[lane] = reinterpret_cast<uint64_t>(a.out_base) + a.outs[J.out_list + lane];
             if (lane == 0) {
@@ -1904,7 +1940,7 @@ __global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
             const int nw = __builtin_amdgcn_readfirstlane(ne);
             const CombRegion<R> rg(regions + (size_t)jl * a.job_lds, a.nin_max);
             comb_dispatch<R>(nw, reinterpret_cast<const uint8_t *>(s_in[jl]) + col * 16u, a.stride,
-                             (int)s_nin[jl], ne, col, rg);
+                             (int)s_nin[jl], ne, col, rg, a.ncol >= 64);
         }
         __syncthreads();
     }
@@ -1912,9 +1948,62 @@ __global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
 
 // Encode: lane per repair — clip the window to the batch, draw its RFC 8681
 // coefficients, write its job (output: repair row t).
+__device__ __forceinline__ void sw_enc_single(const SwEncCoefArgs &a, uint64_t t, uint64_t jt);
+
+// Grouped encode jobs (SwEncCoefArgs::group), lane per repair t of group
+// g = t / group: every lane of the group finds the union of its windows; its
+// row of the group's coefficients, or (group too wide) its own job in the tail.
+__device__ __forceinline__ void sw_enc_grouped(const SwEncCoefArgs &a, uint64_t t) {
+    const uint64_t g = t / (uint64_t)a.group, t0 = g * (uint64_t)a.group;
+    const uint64_t ngroups = (a.nrep + a.group - 1) / a.group;
+    const int n = (int)min((uint64_t)a.group, a.nrep - t0), u = (int)(t - t0);
+    uint64_t lo = ~0ull, hi = 0;
+    for (int v = 0; v < n; v++) {
+        const fecgpu_sw_repair h = a.hdr[t0 + v];
+        const uint64_t fss = min(h.fss, a.nsrc);
+        const uint64_t nss = min((uint64_t)min((int)h.nss, a.max_window), a.nsrc - fss);
+        lo = min(lo, fss);
+        hi = max(hi, fss + nss);
+    }
+    const uint64_t span = hi - lo;
+    if (span > (uint64_t)a.span_max || span * (uint64_t)n > (uint64_t)a.group * kSwCoefPitch) {
+        if (u == 0) {
+            CombJob E{};
+            E.xor_off = kNoXor;  // empty: nout = 0
+            a.jobs[g] = E;
+        }
+        sw_enc_single(a, t, ngroups + atomicAdd(a.tail, 1u));
+        return;
+    }
+    const fecgpu_sw_repair h = a.hdr[t];
+    const uint64_t fss = min(h.fss, a.nsrc);
+    const int nss = (int)min((uint64_t)min((int)h.nss, a.max_window), a.nsrc - fss);
+    uint8_t *row = a.coef + t0 * kSwCoefPitch + (uint64_t)u * span;
+    const int b = (int)(fss - lo);
+    for (int q = 0; q < b; q++) row[q] = 0;
+    (void)rlc_coefs(h.key, nss, min((uint32_t)h.dt, 15u), row + b);
+    for (int q = b + nss; q < (int)span; q++) row[q] = 0;
+    a.outs[t] = t * a.stride;
+    if (u == 0) {
+        CombJob J;
+        J.in_off = lo * a.stride;
+        J.coef_off = t0 * kSwCoefPitch;
+        J.out_list = t0;
+        J.xor_off = kNoXor;
+        J.nin = (uint32_t)span;
+        J.nout = (uint32_t)n;
+        a.jobs[g] = J;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void sw_enc_coef_kernel(SwEncCoefArgs a) {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (t >= a.nrep) return;
+    if (a.group > 1) sw_enc_grouped(a, t);
+    else sw_enc_single(a, t, t);
+}
+
+__device__ __forceinline__ void sw_enc_single(const SwEncCoefArgs &a, uint64_t t, uint64_t jt) {
     const fecgpu_sw_repair h = a.hdr[t];
     const uint64_t fss = min(h.fss, a.nsrc);
     const int nss = (int)min((uint64_t)min((int)h.nss, a.max_window), a.nsrc - fss);
@@ -1927,7 +2016,7 @@ __global__ __launch_bounds__(kBlock) void sw_enc_coef_kernel(SwEncCoefArgs a) {
     J.xor_off = kNoXor;
     J.nin = (uint32_t)nss;
     J.nout = 1;
-    a.jobs[t] = J;
+    a.jobs[jt] = J;
     a.outs[t] = t * a.stride;
 }
 
@@ -2220,13 +2309,16 @@ hipError_t launch_erasure(const EraseArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_comb(CombArgs a, int R, hipStream_t s) {
-    if (a.njobs == 0) return hipSuccess;
-    const uint64_t groups = (a.njobs + a.wpb - 1) / a.wpb;
+    const uint64_t nmax = a.njobs + (a.extra ? a.extra_max : 0);
+    if (nmax == 0) return hipSuccess;
+    const uint64_t groups = (nmax + a.wpb - 1) / a.wpb;
     a.nx = groups >= 8 ? 8 : 1;
     const uint64_t grid = (groups + a.nx - 1) / a.nx * a.nx;  // one group per workgroup
     const uint32_t lds = a.job_lds * (uint32_t)a.wpb;
     switch (R) {
         case 1: hipLaunchKernelGGL(comb_kernel<1>, dim3((unsigned)grid), dim3(kBlock), lds, s, a); break;
+        case 2: hipLaunchKernelGGL(comb_kernel<2>, dim3((unsigned)grid), dim3(kBlock), lds, s, a); break;
+        case 4: hipLaunchKernelGGL(comb_kernel<4>, dim3((unsigned)grid), dim3(kBlock), lds, s, a); break;
         case 8: hipLaunchKernelGGL(comb_kernel<8>, dim3((unsigned)grid), dim3(kBlock), lds, s, a); break;
         default: return hipErrorInvalidValue;
     }

@@ -43,10 +43,12 @@ bool header_ok(const fecgpu_sw_repair &h, uint64_t nsrc) {
     return h.nss >= 1 && h.nss <= kSwMaxWindow && h.dt <= 15 && h.fss <= nsrc && nsrc - h.fss >= h.nss;
 }
 
-// One combine launch (fec_internal.h CombJob) over njobs jobs.
+// One combine launch (fec_internal.h CombJob) over njobs jobs (plus *extra
+// more, at most extra_max, when extra is given).
 ssize_t run_comb(const CombJob *jobs, uint64_t njobs, const uint8_t *coef, const uint64_t *outs,
                  const uint8_t *in_base, uint8_t *out_base, const uint8_t *xor_base, uint32_t S,
-                 uint32_t stride, int R, int nin_max, hipStream_t s) {
+                 uint32_t stride, int R, int nin_max, hipStream_t s, const uint32_t *extra = nullptr,
+                 uint64_t extra_max = 0) {
     CombArgs a{};
     a.jobs = jobs;
     a.coef = coef;
@@ -55,6 +57,8 @@ ssize_t run_comb(const CombJob *jobs, uint64_t njobs, const uint8_t *coef, const
     a.out_base = out_base;
     a.xor_base = xor_base;
     a.njobs = njobs;
+    a.extra = extra;
+    a.extra_max = extra_max;
     a.ncol = (S + 15u) >> 4;
     a.stride = stride;
     a.nin_max = std::max(1, nin_max);
@@ -69,20 +73,57 @@ ssize_t run_comb(const CombJob *jobs, uint64_t njobs, const uint8_t *coef, const
 
 namespace fecgpu {
 
+// Repairs per group and the union span a group may cover: W + 3 steps for
+// 4 repairs at W / step = 4, so 2 * max_window keeps the overlapping stream
+// shapes grouped and the job tables small (comb_job_lds).
+int sw_span_max(int max_window) { return std::min<int>(kSwCoefPitch, 2 * std::max(1, max_window)); }
+
+// Host replica of sw_enc_group's fit test: every group's clipped windows span
+// at most span_max sources (then the per-repair tail is not launched).
+bool sw_groups_fit(const fecgpu_sw_repair *h, uint64_t nrep, uint64_t nsrc, int max_window, int group,
+                   int span_max) {
+    for (uint64_t t0 = 0; t0 < nrep; t0 += group) {
+        const int n = (int)std::min<uint64_t>(group, nrep - t0);
+        uint64_t lo = ~0ull, hi = 0;
+        for (int u = 0; u < n; u++) {
+            const uint64_t fss = std::min<uint64_t>(h[t0 + u].fss, nsrc);
+            const uint64_t nss = std::min<uint64_t>(std::min<int>(h[t0 + u].nss, max_window), nsrc - fss);
+            lo = std::min(lo, fss);
+            hi = std::max(hi, fss + nss);
+        }
+        if (hi - lo > (uint64_t)span_max || (hi - lo) * (uint64_t)n > (uint64_t)group * kSwCoefPitch)
+            return false;
+    }
+    return true;
+}
+
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *pj, void *pc,
-                       void *po, hipStream_t s) {
+                       void *po, hipStream_t s, int group, const fecgpu_sw_repair *hdr_host) {
     SwEncCoefArgs ca{};
     ca.hdr = hdr;
     ca.nrep = nrep;
     ca.nsrc = nsrc;
     ca.stride = stride;
     ca.max_window = max_window;
+    ca.group = nrep > 1 && group > 1 ? group : 1;
+    ca.span_max = sw_span_max(max_window);
     ca.jobs = static_cast<CombJob *>(pj);
     ca.coef = static_cast<uint8_t *>(pc);
     ca.outs = static_cast<uint64_t *>(po);
+    if (ca.group == 1) {
+        SW_TRY(launch_sw_enc_coef(ca, s), "sliding-window coefficient launch");
+        return run_comb(ca.jobs, nrep, ca.coef, ca.outs, src, rep, nullptr, S, stride, 1, max_window, s);
+    }
+    // the tail counter sits after the jobs (sw_enc_jobs leaves room); the host
+    // copy of the headers, when given, says whether a tail can occur at all
+    const uint64_t ngroups = (nrep + ca.group - 1) / ca.group;
+    const bool tail = !hdr_host || !sw_groups_fit(hdr_host, nrep, nsrc, max_window, ca.group, ca.span_max);
+    ca.tail = reinterpret_cast<uint32_t *>(ca.jobs + ngroups + nrep);
+    SW_TRY(hipMemsetAsync(ca.tail, 0, sizeof(uint32_t), s), "sliding-window tail reset");
     SW_TRY(launch_sw_enc_coef(ca, s), "sliding-window coefficient launch");
-    return run_comb(ca.jobs, nrep, ca.coef, ca.outs, src, rep, nullptr, S, stride, 1, max_window, s);
+    return run_comb(ca.jobs, ngroups, ca.coef, ca.outs, src, rep, nullptr, S, stride, ca.group,
+                    std::max(ca.span_max, max_window), s, tail ? ca.tail : nullptr, nrep);
 }
 
 }  // namespace fecgpu
@@ -91,12 +132,13 @@ namespace {
 
 ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_t *rep,
                       const fecgpu_sw_repair *hdr, uint64_t nrep, int max_window, uint32_t S,
-                      uint32_t stride, hipStream_t s) {
+                      uint32_t stride, hipStream_t s, const fecgpu_sw_repair *hdr_host = nullptr) {
     void *pj = nullptr, *pc = nullptr, *po = nullptr;
-    RC_TRY(ctx_sw_scratch(ctx, 0, nrep * sizeof(CombJob), &pj));
+    const int group = ctx_sw_group(ctx);
+    RC_TRY(ctx_sw_scratch(ctx, 0, sw_enc_jobs(nrep, group) * sizeof(CombJob), &pj));
     RC_TRY(ctx_sw_scratch(ctx, 1, nrep * kSwCoefPitch, &pc));
     RC_TRY(ctx_sw_scratch(ctx, 2, nrep * sizeof(uint64_t), &po));
-    return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s);
+    return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s, group, hdr_host);
 }
 
 // Host arrays of a decode's linked systems (see fecgpu_sw_decode).
@@ -272,7 +314,7 @@ ssize_t fecgpu_sw_encode(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uin
         SW_TRY(hipMemcpyAsync(ds, src, nsrc * stride, hipMemcpyHostToDevice, s), "H2D sw sources");
         SW_TRY(hipMemcpyAsync(dh, hdr, nrep * sizeof(fecgpu_sw_repair), hipMemcpyHostToDevice, s), "H2D sw headers");
         RC_TRY(sw_encode_dev(ctx, static_cast<uint8_t *>(ds), nsrc, static_cast<uint8_t *>(dr),
-                             static_cast<fecgpu_sw_repair *>(dh), nrep, hmax, sym_len, stride, s));
+                             static_cast<fecgpu_sw_repair *>(dh), nrep, hmax, sym_len, stride, s, hdr));
         SW_TRY(hipMemcpyAsync(rep, dr, nrep * stride, hipMemcpyDeviceToHost, s), "D2H sw repairs");
         RC_TRY(ctx_sw_end(ctx, s));
         SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");

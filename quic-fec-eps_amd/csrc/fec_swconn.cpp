@@ -77,6 +77,7 @@ struct fecgpu_sw_encoder {
     uint64_t cap = 0, base = 0, next = 0;
     std::vector<fecgpu_sw_repair> sched;  // scheduled, not launched (absolute fss)
     uint32_t key = 0;
+    int group = 1;  // repairs per combine job (ctx "sw_group")
     struct Slot {
         fecgpu_sw_repair *hdr = nullptr;  // pinned, fss relative to the base at launch
         uint8_t *rep = nullptr;           // pinned rows
@@ -125,7 +126,7 @@ ssize_t enc_launch(fecgpu_sw_encoder *e) {
         S.hdr[t].fss -= e->base;
     }
     const ssize_t rc = sw_encode_core(e->src, e->cap, S.rep, S.hdr, S.n, e->p.window, e->p.symbol_size, e->stride,
-                                      S.jobs, S.coef, S.outs, e->s);
+                                      S.jobs, S.coef, S.outs, e->s, e->group, S.hdr);
     if (rc < 0) return rc;
     SWC_TRY(hipEventRecord(S.ev, e->s), "hipEventRecord");
     S.used = true;
@@ -202,6 +203,7 @@ ssize_t fecgpu_sw_encoder_new(fecgpu_ctx *ctx, const fecgpu_sw_params *p, fecgpu
     auto *e = new fecgpu_sw_encoder();
     e->ctx = ctx;
     e->p = *p;
+    e->group = ctx_sw_group(ctx);
     e->stride = (p->symbol_size + 15u) & ~15u;
     e->cap = 4ull * (p->window + (uint64_t)p->batch * p->step);
     rc = [&]() -> ssize_t {
@@ -215,7 +217,7 @@ ssize_t fecgpu_sw_encoder_new(fecgpu_ctx *ctx, const fecgpu_sw_params *p, fecgpu
             rc = ctx_pinned_get(ctx, p->batch * (sizeof(fecgpu_sw_repair) + e->stride), reinterpret_cast<void **>(&S.hdr));
             if (rc) return rc;
             S.rep = reinterpret_cast<uint8_t *>(S.hdr + p->batch);
-            SWC_TRY(hipMalloc(&S.jobs, p->batch * sizeof(CombJob)), "hipMalloc");
+            SWC_TRY(hipMalloc(&S.jobs, sw_enc_jobs(p->batch, e->group) * sizeof(CombJob)), "hipMalloc");
             SWC_TRY(hipMalloc(&S.coef, p->batch * (size_t)kSwCoefPitch), "hipMalloc");
             SWC_TRY(hipMalloc(&S.outs, p->batch * sizeof(uint64_t)), "hipMalloc");
             SWC_TRY(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming), "hipEventCreate");

@@ -42,10 +42,13 @@ def main():
     ap.add_argument("--W", type=int, default=32)
     ap.add_argument("--loss", type=float, default=0.02)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--sw-group", type=int, default=0, help="tuning: repairs per encode job (0 = library default)")
     args = ap.parse_args()
     nsrc, L, k, W = args.nsrc, args.L, args.k, args.W
     stride = (L + 15) // 16 * 16
     ctx = fecgpu.Context()
+    if args.sw_group:
+        ctx.set_tuning("sw_group", args.sw_group)
     g = torch.Generator(device="cuda").manual_seed(1)
     src = torch.randint(0, 256, (nsrc, stride), dtype=torch.uint8, device="cuda", generator=g)
     hdr = schedule(nsrc, k, W)
@@ -88,7 +91,7 @@ def main():
     alg = (nsrc + nrep) * L
     print(json.dumps({
         "what": "sliding-window RLC (RFC 8681), device-resident symbols",
-        "nsrc": nsrc, "L": L, "k": k, "W": W, "nrep": nrep,
+        "nsrc": nsrc, "L": L, "k": k, "W": W, "nrep": nrep, "sw_group": args.sw_group or 4,
         "encode_ms": round(enc_ms, 4), "encode_src_GBps": round(nsrc * L / enc_ms / 1e6, 1),
         "encode_alg_TBps": round(alg / enc_ms / 1e9, 3),
         "loss": args.loss, "lost": nlost, "recovered": n, "verify_ok": verified,

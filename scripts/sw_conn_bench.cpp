@@ -9,7 +9,7 @@
 //          -Lquic-fec-eps_amd/lib -lfecgpu -Wl,-rpath,'$ORIGIN/../quic-fec-eps_amd/lib'
 //   run  : scripts/sw_conn_bench E W step MB loss batch [span]
 //          E: symbol size (LENPREFIX, payloads 1..E-2 bytes); a repair after every
-//          `step` sources over the last W.
+//          `step` sources over the last W.  SW_GROUP=1|2|4: the ctx's "sw_group".
 // Exit status 3 if a returned packet differs from the one sent.
 #include <chrono>
 #include <cstdint>
@@ -53,6 +53,7 @@ int main(int argc, char **argv) {
     const uint64_t seed = 0x5EEDFEC0;
     fecgpu_ctx *ctx = nullptr;
     CK(fecgpu_ctx_new(nullptr, 0, &ctx));
+    if (const char *g = getenv("SW_GROUP")) CK(fecgpu_ctx_set_tuning(ctx, "sw_group", atoi(g)));
     fecgpu_sw_params p{};
     p.framing = FECGPU_FRAMING_LENPREFIX;
     p.symbol_size = E;

@@ -113,6 +113,43 @@ def test_sw_encode_device_headers_are_clipped(ctx):
     assert not g[3, :L].any()   # empty window: zero repair
 
 
+@pytest.mark.parametrize("L", [300, 1200])   # < 64 / >= 64 columns: zero-skip off / on
+@pytest.mark.parametrize("group", [1, 2, 4])
+@pytest.mark.parametrize("host", [False, True], ids=["dev_hdr", "host_hdr"])
+def test_sw_encode_grouped_jobs(group, host, L):
+    """Grouped encode jobs (ctx "sw_group"): consecutive repairs share one combine
+    job over the union of their windows when it spans <= 2 * max_window sources,
+    else fall back to one job per repair (the tail; skipped when the host sees
+    the headers and every group fits).  A stream schedule with some repairs moved
+    far away (mixed fitting / non-fitting groups), a ragged last group, and one
+    with every group fitting: equal to the oracle."""
+    c = fecgpu.Context()
+    try:
+        c.set_tuning("sw_group", group)
+        nsrc, W = 700, 32
+        stride = O.round_up(L, 16)
+        src = stream(nsrc, L, stride, 11 + group)
+        base = N.sw_schedule(nsrc, 8, W, key0=100)
+        moved = list(base)
+        for t in range(5, len(moved), 9):   # some windows far from their group neighbours
+            fss, nss, key, dt = moved[t]
+            moved[t] = ((fss + 333) % (nsrc - nss), nss, key, dt)
+        for sched in (base, moved, base[:-3]):
+            hdr = hdr_array(sched)
+            o = O.sw_encode(src, hdr, L)
+            if host:
+                rep = np.zeros((len(hdr), stride), np.uint8)
+                c.sw_encode(src, rep, hdr, nsrc=nsrc, nrep=len(hdr), sym_len=L, stride=stride,
+                            max_window=W, flags=fecgpu.F_HOST_PTRS)
+            else:
+                rep = gpu_encode(c, src, hdr, L, W)
+            assert np.array_equal(rep[:, :L], o[:, :L])
+        with pytest.raises(fecgpu.FecError):
+            c.set_tuning("sw_group", 3)
+    finally:
+        c.close()
+
+
 LOSS = [("iid", 0.03), ("iid", 0.1), ("iid", 0.25), ("burst", 7), ("burst", 30), ("reps", 0.5)]
 
 
