@@ -165,6 +165,8 @@ struct fecgpu_ctx {
     // sliding-window calls: device scratch slots and the last call's end event, per device
     std::map<int, std::vector<std::pair<void *, size_t>>> sw_scratch;
     std::map<int, hipEvent_t> sw_event;
+    void *sw_host = nullptr;  // pinned staging of sliding-window decodes (ctx_sw_host)
+    size_t sw_host_bytes = 0;
 };
 
 extern "C" {
@@ -338,6 +340,7 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
         for (auto &b : kv.second)
             if (b.first) (void)hipFree(b.first);
     }
+    if (ctx->sw_host) (void)hipHostFree(ctx->sw_host);
     for (auto &kv : ctx->sw_event) {
         (void)hipSetDevice(kv.first);
         (void)hipEventDestroy(kv.second);
@@ -1022,6 +1025,19 @@ ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p) {
         b.second = want;
     }
     *p = b.first;
+    return 0;
+}
+
+ssize_t ctx_sw_host(fecgpu_ctx *ctx, size_t bytes, void **p) {
+    if (ctx->sw_host_bytes < bytes) {
+        const size_t want = std::max(bytes, ctx->sw_host_bytes + ctx->sw_host_bytes / 2);
+        if (ctx->sw_host) HIP_TRY(hipHostFree(ctx->sw_host), "hipHostFree");
+        ctx->sw_host = nullptr;
+        ctx->sw_host_bytes = 0;
+        HIP_TRY(hipHostMalloc(&ctx->sw_host, want, hipHostMallocDefault), "hipHostMalloc sw staging");
+        ctx->sw_host_bytes = want;
+    }
+    *p = ctx->sw_host;
     return 0;
 }
 

@@ -243,6 +243,7 @@ struct SwPlanArgs {  // wave per system: Gauss-Jordan, solve jobs, per-unknown s
     const uint64_t *unk;
     uint32_t stride;
     CombJob *jobs;
+    CombJob *syn_jobs;  // the syndrome jobs (equation g at syn_jobs[g]): emptied when no solve reads them
     uint8_t *coef;
     uint64_t *outs;
     uint8_t *ustat;
@@ -269,6 +270,9 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
 int ctx_sw_group(const fecgpu_ctx *ctx);
 int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget);
 ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p);
+// the ctx's pinned host staging block for sliding-window decodes (grown on
+// demand; a decode synchronizes before returning, so the next may reuse it)
+ssize_t ctx_sw_host(fecgpu_ctx *ctx, size_t bytes, void **p);
 ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);
 ssize_t ctx_sw_end(fecgpu_ctx *ctx, hipStream_t s);
 

@@ -2060,7 +2060,10 @@ __global__ __launch_bounds__(kBlock) void sw_syn_kernel(SwSynArgs a) {
 // pivot is free; unknown c is determined iff its pivot row is zero on every
 // free column, and then x_c = sum_t M[P_c][e + t] * s_t.  Writes the solve
 // jobs (8 determined unknowns each, inputs = the system's syndrome rows), their
-// coefficient rows and output rows, and every unknown's status.
+// coefficient rows and output rows, and every unknown's status, and empties
+// the syndrome jobs of equations no solve reads (only pivot rows can appear
+// in M[P_c][e + t]: a non-pivot row never enters a pivot row), so about one
+// syndrome per lost source is computed instead of one per received repair.
 constexpr int kSwPitch = kSwMaxUnknowns + kSwMaxEq;
 __global__ __launch_bounds__(kBlock) void sw_plan_kernel(SwPlanArgs a) {
     extern __shared__ uint4 dyn[];
@@ -2127,6 +2130,14 @@ __global__ __launch_bounds__(kBlock) void sw_plan_kernel(SwPlanArgs a) {
             for (int t = 0; t < p; t++) cf[t] = M[prc * kSwPitch + e + t];
             a.outs[c.o_off + d] = a.unk[c.u_off + lane] * a.stride;
         }
+    }
+    // syndromes no solve reads (non-pivot rows, undetermined unknowns' rows)
+    // are not computed: the plan runs before the syndrome pass
+    for (int q = lane; q < p; q += 64) {
+        bool need = false;
+        for (int col = 0; col < e && !need; col++)
+            need = ((dm >> col) & 1) && M[piv[col] * kSwPitch + e + q] != 0;
+        if (!need) a.syn_jobs[c.q_off + q].nout = 0;
     }
     const int njob = (e + 7) / 8;
     if (lane < njob) {

@@ -160,15 +160,32 @@ struct SwPlan {
 // left out (their sources stay lost).
 void sw_build_plan(const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep_present,
                    const fecgpu_sw_repair *hdr, uint64_t nrep, SwPlan &P) {
+    // lost sources: 8 flags at a time, skipping words with no zero byte
     std::vector<uint64_t> lost;
-    for (uint64_t i = 0; i < nsrc; i++)
+    uint64_t i = 0;
+    for (; i + 8 <= nsrc; i += 8) {
+        uint64_t v;
+        std::memcpy(&v, src_present + i, 8);
+        if (!((v - 0x0101010101010101ull) & ~v & 0x8080808080808080ull)) continue;
+        for (int b = 0; b < 8; b++)
+            if (!src_present[i + b]) lost.push_back(i + b);
+    }
+    for (; i < nsrc; i++)
         if (!src_present[i]) lost.push_back(i);
     std::vector<uint64_t> pr;  // received repairs, fss ascending (headers are sorted)
+    pr.reserve(nrep);
+    uint64_t wmax = 1;  // longest received window: a repair holding source i has fss > i - wmax
     for (uint64_t t = 0; t < nrep; t++)
-        if (rep_present[t]) pr.push_back(t);
+        if (rep_present[t]) {
+            pr.push_back(t);
+            wmax = std::max<uint64_t>(wmax, hdr[t].nss);
+        }
     size_t ip = 0;
     uint64_t max_end = 0;
     size_t start = 0;
+    std::vector<uint64_t> eq;  // one system's equations (reused)
+    size_t jp = 0;             // first received repair that can hold the next system's sources
+    P.unk.reserve(lost.size());
     for (size_t x = 0; x < lost.size(); x++) {
         while (ip < pr.size() && hdr[pr[ip]].fss <= lost[x]) {
             max_end = std::max(max_end, hdr[pr[ip]].fss + hdr[pr[ip]].nss);
@@ -180,14 +197,15 @@ void sw_build_plan(const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep
         const size_t e = x + 1 - start;
         start = x + 1;
         if (e > (size_t)kSwMaxUnknowns) continue;
-        const uint64_t lo = U[0] > (uint64_t)kSwMaxWindow ? U[0] - kSwMaxWindow : 0;
-        auto it = std::lower_bound(pr.begin(), pr.end(), lo,
-                                   [&](uint64_t t, uint64_t v) { return hdr[t].fss < v; });
-        std::vector<uint64_t> eq;
-        for (; it != pr.end() && hdr[*it].fss <= U[e - 1] && eq.size() < (size_t)kSwMaxEq; ++it) {
-            const fecgpu_sw_repair &h = hdr[*it];
-            const uint64_t *u = std::lower_bound(U, U + e, h.fss);
-            if (u != U + e && *u < h.fss + h.nss) eq.push_back(*it);
+        // systems come in ascending order, so the first candidate repair only
+        // moves forward (a sweep, not a search per system)
+        const uint64_t lo = U[0] >= wmax ? U[0] - wmax + 1 : 0;
+        while (jp < pr.size() && hdr[pr[jp]].fss < lo) jp++;
+        eq.clear();
+        for (size_t it = jp; it < pr.size() && hdr[pr[it]].fss <= U[e - 1] && eq.size() < (size_t)kSwMaxEq; ++it) {
+            const fecgpu_sw_repair &h = hdr[pr[it]];
+            const uint64_t *u = e == 1 ? U : std::lower_bound(U, U + e, h.fss);
+            if (u != U + e && *u >= h.fss && *u < h.fss + h.nss) eq.push_back(pr[it]);
         }
         if (eq.empty()) continue;
         SwComp c{};
@@ -219,7 +237,7 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // Device part of a decode: src / rep device pointers, plan P on the host.
 ssize_t sw_decode_dev(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *rep, SwPlan &P, uint32_t S,
-                      uint32_t stride, std::vector<uint8_t> &ustat, hipStream_t s) {
+                      uint32_t stride, const uint8_t **ustat, hipStream_t s) {
     const uint64_t neq = P.eqr.size(), nunk = P.unk.size(), ncomp = P.comps.size();
     const uint64_t coef_syn = neq * kSwCoefPitch;
     for (SwComp &c : P.comps) {
@@ -235,19 +253,23 @@ ssize_t sw_decode_dev(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *rep, SwPlan 
     const size_t o_ust = o_amat + align256(P.amat);
     const size_t o_syn = o_ust + align256(nunk);
     const size_t total = o_syn + neq * (size_t)stride;
-    std::vector<uint8_t> meta(o_amat, 0);
-    std::memcpy(meta.data(), P.comps.data(), ncomp * sizeof(SwComp));
-    std::memcpy(meta.data() + o_unk, P.unk.data(), nunk * 8);
-    std::memcpy(meta.data() + o_eqr, P.eqr.data(), neq * 8);
-    std::memcpy(meta.data() + o_eqc, P.eqc.data(), neq * 4);
-    std::memcpy(meta.data() + o_eqh, P.eqh.data(), neq * sizeof(fecgpu_sw_repair));
+    // the plan goes up from (and the statuses come back to) the ctx's pinned
+    // staging block: a pageable copy of ~2 MB was a third of the call
+    void *ph = nullptr;
+    RC_TRY(ctx_sw_host(ctx, o_amat + nunk, &ph));
+    uint8_t *meta = static_cast<uint8_t *>(ph);
+    std::memcpy(meta, P.comps.data(), ncomp * sizeof(SwComp));
+    std::memcpy(meta + o_unk, P.unk.data(), nunk * 8);
+    std::memcpy(meta + o_eqr, P.eqr.data(), neq * 8);
+    std::memcpy(meta + o_eqc, P.eqc.data(), neq * 4);
+    std::memcpy(meta + o_eqh, P.eqh.data(), neq * sizeof(fecgpu_sw_repair));
     void *pm = nullptr, *pj = nullptr, *pc = nullptr, *po = nullptr;
     RC_TRY(ctx_sw_scratch(ctx, 6, total, &pm));
     RC_TRY(ctx_sw_scratch(ctx, 0, (neq + P.nsolve) * sizeof(CombJob), &pj));
     RC_TRY(ctx_sw_scratch(ctx, 1, coef_syn + P.tcoef, &pc));
     RC_TRY(ctx_sw_scratch(ctx, 2, (neq + nunk) * sizeof(uint64_t), &po));
     uint8_t *m = static_cast<uint8_t *>(pm);
-    SW_TRY(hipMemcpyAsync(m, meta.data(), meta.size(), hipMemcpyHostToDevice, s), "H2D sw plan");
+    SW_TRY(hipMemcpyAsync(m, meta, o_amat, hipMemcpyHostToDevice, s), "H2D sw plan");
     CombJob *jobs = static_cast<CombJob *>(pj);
     uint8_t *coef = static_cast<uint8_t *>(pc);
     uint64_t *outs = static_cast<uint64_t *>(po);
@@ -266,7 +288,6 @@ ssize_t sw_decode_dev(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *rep, SwPlan 
     ya.outs = outs;
     ya.amat = m + o_amat;
     SW_TRY(launch_sw_syn(ya, s), "sliding-window syndrome coefficient launch");
-    RC_TRY(run_comb(jobs, neq, coef, outs, src, synd, rep, S, stride, 1, P.max_nss, s));
 
     SwPlanArgs pa{};
     pa.comps = ya.comps;
@@ -275,14 +296,16 @@ ssize_t sw_decode_dev(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *rep, SwPlan 
     pa.unk = ya.unk;
     pa.stride = stride;
     pa.jobs = jobs + neq;
+    pa.syn_jobs = jobs;
     pa.coef = coef;
     pa.outs = outs;
     pa.ustat = m + o_ust;
     SW_TRY(launch_sw_plan(pa, s), "sliding-window plan launch");
+    RC_TRY(run_comb(jobs, neq, coef, outs, src, synd, rep, S, stride, 1, P.max_nss, s));
     RC_TRY(run_comb(jobs + neq, P.nsolve, coef, outs, synd, src, nullptr, S, stride, kSwSolveOut,
                     P.max_p, s));
-    ustat.resize(nunk);
-    SW_TRY(hipMemcpyAsync(ustat.data(), m + o_ust, nunk, hipMemcpyDeviceToHost, s), "D2H sw status");
+    SW_TRY(hipMemcpyAsync(meta + o_amat, m + o_ust, nunk, hipMemcpyDeviceToHost, s), "D2H sw status");
+    *ustat = meta + o_amat;  // valid once the stream has completed
     return 0;
 }
 
@@ -360,8 +383,8 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
         dsrc = static_cast<uint8_t *>(ds);
         drep = static_cast<uint8_t *>(dr);
     }
-    std::vector<uint8_t> ustat;
-    RC_TRY(sw_decode_dev(ctx, dsrc, drep, P, sym_len, stride, ustat, s));
+    const uint8_t *ustat = nullptr;
+    RC_TRY(sw_decode_dev(ctx, dsrc, drep, P, sym_len, stride, &ustat, s));
     if (flags & FECGPU_F_HOST_PTRS)
         SW_TRY(hipMemcpyAsync(src, dsrc, nsrc * stride, hipMemcpyDeviceToHost, s), "D2H sw sources");
     RC_TRY(ctx_sw_end(ctx, s));
