@@ -433,9 +433,9 @@ ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out)
                         if ((col >> p) & 1) (q < 4 ? lo : hi) |= 1u << (q & 3);
                     }
                     uint32_t *d = &m[(((size_t)j * r + i) * 8 + p) * kRbsPlaneDw];
-                    if (kRbsPlaneDw == 2) {
-                        d[0] = lo;
-                        d[kRbsPlaneDw - 1] = hi;
+                    if (kRbsPlaneDw == 2) {  // four-column units index register pairs: 2 x index
+                        d[0] = lo * (kRbsCols / 2);
+                        d[kRbsPlaneDw - 1] = hi * (kRbsCols / 2);
                     } else {
                         d[0] = lo | hi << 8;
                     }

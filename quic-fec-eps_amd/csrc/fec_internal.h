@@ -80,7 +80,13 @@ struct LaunchPlan {
 // straight into M0 with no unpacking; 0 = one dword per plane (lo | hi << 8)
 #define FECGPU_RBS_WIDE 1
 #endif
-constexpr int kRbsPlaneDw = FECGPU_RBS_WIDE ? 2 : 1;  // mask dwords per output plane
+#ifndef FECGPU_RBS_COLS
+// runtime bit-sliced encode: 16-B columns per lane (2: 32 byte positions, 4:
+// 64, half the index-mode switches per byte; needs FECGPU_RBS_WIDE)
+#define FECGPU_RBS_COLS 4
+#endif
+constexpr int kRbsCols = FECGPU_RBS_COLS;
+constexpr int kRbsPlaneDw = FECGPU_RBS_WIDE || FECGPU_RBS_COLS == 4 ? 2 : 1;  // mask dwords per output plane
 
 // GF encode of (k, r, matrix) has a compiled bit-sliced kernel.
 bool bitslice_supported(int k, int r, int matrix);

@@ -972,6 +972,7 @@ template <int R>
 __device__ __forceinline__ void source(const uint32_t (&x)[8], uint32_t (&acc)[R][8], cmask mk) {
     uint32_t lo[16], hi[16];
     lo[0] = hi[0] = 0;
+    asm volatile("" : "+v"(lo[0]), "+v"(hi[0]));  // opaque zeros (no re-materialisation per block)
 #pragma unroll
     for (int s = 1; s < 16; s++) {
         const int b = __builtin_ctz(s), rest = s & (s - 1);
@@ -1041,29 +1042,188 @@ __device__ __forceinline__ void unit(uint8_t *pa, uint8_t *pb, uint32_t stride, 
 
 }  // namespace rbs
 
+// Four-column units (FECGPU_RBS_COLS = 4): a lane takes 64 byte positions,
+// so each output plane is a dword pair and one pair of index sets serves
+// 64 bytes instead of 32 (half the index-mode switches per byte, at ~240
+// VGPRs: 2 waves per SIMD).  lo / hi entries are pairs pinned at v32-v63 /
+// v64-v95 (entry s at v[32 + 2s : 33 + 2s]), so the table holds 2 x index.
+namespace rbs4 {
+
+using rbs::cmask;
+
+#define R4_IN(A, N, R0) "{v" #R0 "}"(A[N])
+#define R4_PAIR(Q0, Q1, TA, TB)                                                 \
+    "s_set_gpr_idx_idx %[h" #Q0 "]\n\t"                                        \
+    "v_mov_b64 v[" #TA ":" #TB "], v[64:65]\n\t"                               \
+    "s_set_gpr_idx_idx %[l" #Q0 "]\n\t"                                        \
+    "v_bitop3_b32 %[a" #Q0 "], v32, %[a" #Q0 "], v" #TA " bitop3:0x96\n\t"      \
+    "v_bitop3_b32 %[b" #Q0 "], v33, %[b" #Q0 "], v" #TB " bitop3:0x96\n\t"      \
+    "s_set_gpr_idx_idx %[h" #Q1 "]\n\t"                                        \
+    "v_mov_b64 v[" #TA ":" #TB "], v[64:65]\n\t"                               \
+    "s_set_gpr_idx_idx %[l" #Q1 "]\n\t"                                        \
+    "v_bitop3_b32 %[a" #Q1 "], v32, %[a" #Q1 "], v" #TA " bitop3:0x96\n\t"      \
+    "v_bitop3_b32 %[b" #Q1 "], v33, %[b" #Q1 "], v" #TB " bitop3:0x96\n\t"
+
+// planes q = 0..3 of one repair half: (a[q], b[q]) ^= lo[l[q]] ^ hi[h[q]]
+__device__ __forceinline__ void pick4(uint32_t (&a)[4], uint32_t (&b)[4], const uint32_t (&l)[4],
+                                      const uint32_t (&h)[4], const uint32_t (&lo)[32], const uint32_t (&hi)[32]) {
+    asm("s_set_gpr_idx_on %[h0], gpr_idx(SRC0)\n\t"
+        R4_PAIR(0, 1, 96, 97) R4_PAIR(2, 3, 98, 99)
+        "s_set_gpr_idx_off"
+        : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]),
+          [b0] "+v"(b[0]), [b1] "+v"(b[1]), [b2] "+v"(b[2]), [b3] "+v"(b[3])
+        : [l0] "s"(l[0]), [l1] "s"(l[1]), [l2] "s"(l[2]), [l3] "s"(l[3]),
+          [h0] "s"(h[0]), [h1] "s"(h[1]), [h2] "s"(h[2]), [h3] "s"(h[3]),
+          R4_IN(lo, 0, 32), R4_IN(lo, 1, 33), R4_IN(lo, 2, 34), R4_IN(lo, 3, 35),
+          R4_IN(lo, 4, 36), R4_IN(lo, 5, 37), R4_IN(lo, 6, 38), R4_IN(lo, 7, 39),
+          R4_IN(lo, 8, 40), R4_IN(lo, 9, 41), R4_IN(lo, 10, 42), R4_IN(lo, 11, 43),
+          R4_IN(lo, 12, 44), R4_IN(lo, 13, 45), R4_IN(lo, 14, 46), R4_IN(lo, 15, 47),
+          R4_IN(lo, 16, 48), R4_IN(lo, 17, 49), R4_IN(lo, 18, 50), R4_IN(lo, 19, 51),
+          R4_IN(lo, 20, 52), R4_IN(lo, 21, 53), R4_IN(lo, 22, 54), R4_IN(lo, 23, 55),
+          R4_IN(lo, 24, 56), R4_IN(lo, 25, 57), R4_IN(lo, 26, 58), R4_IN(lo, 27, 59),
+          R4_IN(lo, 28, 60), R4_IN(lo, 29, 61), R4_IN(lo, 30, 62), R4_IN(lo, 31, 63),
+          R4_IN(hi, 0, 64), R4_IN(hi, 1, 65), R4_IN(hi, 2, 66), R4_IN(hi, 3, 67),
+          R4_IN(hi, 4, 68), R4_IN(hi, 5, 69), R4_IN(hi, 6, 70), R4_IN(hi, 7, 71),
+          R4_IN(hi, 8, 72), R4_IN(hi, 9, 73), R4_IN(hi, 10, 74), R4_IN(hi, 11, 75),
+          R4_IN(hi, 12, 76), R4_IN(hi, 13, 77), R4_IN(hi, 14, 78), R4_IN(hi, 15, 79),
+          R4_IN(hi, 16, 80), R4_IN(hi, 17, 81), R4_IN(hi, 18, 82), R4_IN(hi, 19, 83),
+          R4_IN(hi, 20, 84), R4_IN(hi, 21, 85), R4_IN(hi, 22, 86), R4_IN(hi, 23, 87),
+          R4_IN(hi, 24, 88), R4_IN(hi, 25, 89), R4_IN(hi, 26, 90), R4_IN(hi, 27, 91),
+          R4_IN(hi, 28, 92), R4_IN(hi, 29, 93), R4_IN(hi, 30, 94), R4_IN(hi, 31, 95)
+        : "v96", "v97", "v98", "v99");
+}
+#undef R4_IN
+#undef R4_PAIR
+
+// acc ^= one source (planes xa of columns 0-1, xb of columns 2-3) times its
+// mask row mk ([R][8][2] dwords: lo, hi indices x 2)
+template <int R>
+__device__ __forceinline__ void source(const uint32_t (&xa)[8], const uint32_t (&xb)[8], uint32_t (&aa)[R][8],
+                                       uint32_t (&ab)[R][8], cmask mk) {
+    uint32_t lo[32], hi[32];
+    lo[0] = lo[1] = hi[0] = hi[1] = 0;
+    // opaque zeros: a constant is re-materialised into its pinned register
+    // before every asm block (4 v_mov per block)
+    asm volatile("" : "+v"(lo[0]), "+v"(lo[1]), "+v"(hi[0]), "+v"(hi[1]));
+#pragma unroll
+    for (int s = 1; s < 16; s++) {
+        const int b = __builtin_ctz(s), rest = s & (s - 1);
+        lo[2 * s] = rest ? bs::oxor(lo[2 * rest], xa[b]) : xa[b];
+        lo[2 * s + 1] = rest ? bs::oxor(lo[2 * rest + 1], xb[b]) : xb[b];
+        hi[2 * s] = rest ? bs::oxor(hi[2 * rest], xa[4 + b]) : xa[4 + b];
+        hi[2 * s + 1] = rest ? bs::oxor(hi[2 * rest + 1], xb[4 + b]) : xb[4 + b];
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int w = 0; w < 2; w++) {
+            const cmask m = mk + (i * 8 + w * 4) * 2;
+            uint32_t l[4], h[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                l[q] = m[q * 2];
+                h[q] = m[q * 2 + 1];
+            }
+            uint32_t(&ca)[4] = *reinterpret_cast<uint32_t(*)[4]>(&aa[i][w * 4]);
+            uint32_t(&cb)[4] = *reinterpret_cast<uint32_t(*)[4]>(&ab[i][w * 4]);
+            pick4(ca, cb, l, h, lo, hi);
+        }
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int p = 0; p < 8; p++) asm volatile("" : "+v"(aa[i][p]), "+v"(ab[i][p]));
+}
+
+__device__ __forceinline__ void load(uint8_t *const (&pc)[4], uint32_t off, uint32_t (&xa)[8], uint32_t (&xb)[8]) {
+    const uint4 v0 = ld16(pc[0] + off), v1 = ld16(pc[1] + off), v2 = ld16(pc[2] + off), v3 = ld16(pc[3] + off);
+    xa[0] = v0.x; xa[1] = v0.y; xa[2] = v0.z; xa[3] = v0.w;
+    xa[4] = v1.x; xa[5] = v1.y; xa[6] = v1.z; xa[7] = v1.w;
+    xb[0] = v2.x; xb[1] = v2.y; xb[2] = v2.z; xb[3] = v2.w;
+    xb[4] = v3.x; xb[5] = v3.y; xb[6] = v3.z; xb[7] = v3.w;
+}
+
+// one unit: columns pc[0..3]; the next source's loads are issued before the
+// current one's XOR work
+template <int R>
+__device__ __forceinline__ void unit(uint8_t *const (&pc)[4], uint32_t stride, int k, cmask mk, bool live,
+                                     uint64_t od) {
+    uint32_t aa[R][8], ab[R][8];
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int p = 0; p < 8; p++) aa[i][p] = ab[i][p] = 0;
+    uint32_t xa[8], xb[8];
+    load(pc, 0, xa, xb);
+    for (int j = 0; j < k; j++) {
+        uint32_t na[8], nb[8];
+        load(pc, (uint32_t)min(j + 1, k - 1) * stride, na, nb);
+        bs::tr8(xa);
+        bs::tr8(xb);
+        source<R>(xa, xb, aa, ab, mk + (size_t)j * (R * 16));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            xa[q] = na[q];
+            xb[q] = nb[q];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        bs::tr8(aa[i]);
+        bs::tr8(ab[i]);
+        if (live) {
+            const size_t o = od + (size_t)(k + i) * stride;
+            st16(pc[0] + o, make_uint4(aa[i][0], aa[i][1], aa[i][2], aa[i][3]));
+            st16(pc[1] + o, make_uint4(aa[i][4], aa[i][5], aa[i][6], aa[i][7]));
+            st16(pc[2] + o, make_uint4(ab[i][0], ab[i][1], ab[i][2], ab[i][3]));
+            st16(pc[3] + o, make_uint4(ab[i][4], ab[i][5], ab[i][6], ab[i][7]));
+        }
+    }
+}
+
+// columns u + c * h (c < 4) of a window with ncol columns, h = ceil(ncol / 4);
+// a column past the end repeats column u (same inputs and outputs)
+__device__ __forceinline__ void unit_cols(uint8_t *base, uint32_t u, uint32_t h, uint32_t ncol, uint8_t *(&pc)[4]) {
+    pc[0] = base + u * 16u;
+#pragma unroll
+    for (int c = 1; c < 4; c++) pc[c] = u + c * h < ncol ? pc[0] + c * h * 16u : pc[0];
+}
+
+}  // namespace rbs4
+
 // Unit spaces as gf_encode_bs_kernel (flat over uniform windows, group mode
 // otherwise); the masks are the code's, R = its r.
 #ifndef FECGPU_RBS_MINW
 #define FECGPU_RBS_MINW 4  // runtime bit-sliced encode: waves per SIMD asked of the register allocator
 #endif
 template <int R, bool FLAT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FECGPU_RBS_MINW, 8)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kRbsCols == 4 ? 1 : FECGPU_RBS_MINW, 8)))
 void gf_encode_rbs_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
     const rbs::cmask mk = (rbs::cmask)a.enc_bs;
     const int k = a.k;
+    constexpr uint32_t C = kRbsCols;  // columns per unit
+    // one unit of window base (units h, columns ncol)
+    auto run = [&](uint8_t *base, uint32_t u, uint32_t h, uint32_t ncol, uint32_t stride, bool live, uint64_t od) {
+        if constexpr (C == 4) {
+            uint8_t *pc[4];
+            rbs4::unit_cols(base, u, h, ncol, pc);
+            rbs4::unit<R>(pc, stride, k, mk, live, od);
+        } else {
+            uint8_t *pa, *pb;
+            bs::unit_cols(base, u, h, ncol, pa, pb);
+            rbs::unit<R, FECGPU_RBS_U>(pa, pb, stride, k, mk, live, od);
+        }
+    };
     if constexpr (FLAT) {
-        const uint32_t ncol = a.ncol, h = (ncol + 1) >> 1;
+        const uint32_t ncol = a.ncol, h = (ncol + C - 1) / C;
         const uint64_t total = a.nwin * h;
         for (XcdRange xr = xcd_range((total + kBlock - 1) / kBlock, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
             uint64_t s = xr.cur * kBlock + threadIdx.x;
             const bool live = s < total;
             if (!live) s = total - 1;
             const uint64_t w = s / h;
-            const uint32_t u = (uint32_t)(s - w * h);
-            uint8_t *pa, *pb;
-            bs::unit_cols(a.win + w * a.wpitch, u, h, ncol, pa, pb);
-            rbs::unit<R, FECGPU_RBS_U>(pa, pb, a.stride, k, mk, live, a.out_delta + w * a.out_wdelta);
+            run(a.win + w * a.wpitch, (uint32_t)(s - w * h), h, ncol, a.stride, live, a.out_delta + w * a.out_wdelta);
         }
     } else {
         __shared__ GroupLds g;
@@ -1073,7 +1233,7 @@ void gf_encode_rbs_kernel(BatchArgs a) {
             group_geometry(a, g, w0, nb);
             __syncthreads();
             if (threadIdx.x < 64)
-                block_prefix(g.pfx, (int)threadIdx.x < nb ? (g.ncol[threadIdx.x] + 1u) >> 1 : 0u, threadIdx.x);
+                block_prefix(g.pfx, (int)threadIdx.x < nb ? (g.ncol[threadIdx.x] + C - 1) / C : 0u, threadIdx.x);
             __syncthreads();
             const uint32_t total = g.pfx[nb];
             int wl = 0;
@@ -1081,11 +1241,8 @@ void gf_encode_rbs_kernel(BatchArgs a) {
                 const bool live = s0 + threadIdx.x < total;
                 const uint32_t s = live ? s0 + threadIdx.x : total - 1;
                 while (s >= g.pfx[wl + 1]) wl++;
-                uint8_t *pa, *pb;
-                bs::unit_cols(reinterpret_cast<uint8_t *>(g.base[wl]), s - g.pfx[wl], g.pfx[wl + 1] - g.pfx[wl],
-                              g.ncol[wl], pa, pb);
-                rbs::unit<R, FECGPU_RBS_U>(pa, pb, g.stride[wl], k, mk, live,
-                                           a.out_delta + (w0 + wl) * a.out_wdelta);
+                run(reinterpret_cast<uint8_t *>(g.base[wl]), s - g.pfx[wl], g.pfx[wl + 1] - g.pfx[wl], g.ncol[wl],
+                    g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
             }
             __syncthreads();
         }
@@ -2258,7 +2415,7 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
         return hipErrorInvalidValue;
     }
     if (p.rbitslice) {
-        const uint64_t want = (a.nwin * ((a.ncol + 1) / 2) + kBlock - 1) / kBlock;
+        const uint64_t want = (a.nwin * ((a.ncol + kRbsCols - 1) / kRbsCols) + kBlock - 1) / kBlock;
         switch (a.r) {
 #define FECGPU_RBS_CASE(R_)                                                                        \
             case R_:                                                                               \
