@@ -186,6 +186,10 @@ void sw_build_plan(const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep
     std::vector<uint64_t> eq;  // one system's equations (reused)
     size_t jp = 0;             // first received repair that can hold the next system's sources
     P.unk.reserve(lost.size());
+    P.comps.reserve(lost.size());
+    P.eqr.reserve(4 * lost.size());
+    P.eqc.reserve(4 * lost.size());
+    P.eqh.reserve(4 * lost.size());
     for (size_t x = 0; x < lost.size(); x++) {
         while (ip < pr.size() && hdr[pr[ip]].fss <= lost[x]) {
             max_end = std::max(max_end, hdr[pr[ip]].fss + hdr[pr[ip]].nss);
