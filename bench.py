@@ -14,6 +14,9 @@ Workloads (BASELINE.json configs):
                         exactly r sources erased per window
   --config 4          : GF(2^8) k=32 r=8, mixed MTU 1200/9000 LENPREFIX,
                         131,072 windows per GPU (1M over 8), i.i.d. 10% erasures
+  --config 7          : sliding-window RLC (RFC 8681): 524,288 x 1200 B sources per
+                        GPU, a repair after every 8 over the last 32, 2% i.i.d. loss
+                        of sources and repairs (a widening row, not a BASELINE config)
 Multi-GPU: one process per GPU, windows sharded by rank with no data-path
 collective (weak scaling); RCCL only carries the barrier, the max-over-ranks
 time reduction and the 8-byte digest all-gather.  `--gpus N` launched without
@@ -156,6 +159,44 @@ def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
                       f"{dt:.1f} s on {threads} host threads"}
 
 
+def cpu_baseline_sw(cfg, seconds: float) -> dict:
+    """Config 7: the C oracle (oracle/fec_oracle.c orc_sw_encode / orc_sw_decode,
+    scalar, one thread; kind "port") on bounded slices of the stream: 8,192
+    sources with their repairs, same schedule and loss rate.  The oracle decodes
+    every lost source of a slice in one Gauss-Jordan, so slices stay small."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(_ROOT, "oracle"))
+    import oracle as O  # test/baseline infrastructure only
+
+    O.lib()
+    n, L, stride, k, W = 8192, cfg.L, cfg.stride, cfg.k, cfg.window
+    nrep = n // k
+    end = (np.arange(nrep, dtype=np.int64) + 1) * k
+    hdr = np.zeros(nrep, O.SW_REPAIR_DTYPE)
+    hdr["fss"] = np.maximum(0, end - W)
+    hdr["nss"] = end - hdr["fss"]
+    hdr["key"], hdr["dt"] = np.arange(nrep) & 0xFFFF, 15
+    rng = np.random.default_rng(workloads.SEED)
+    tot, src_b, reps = 0.0, 0, 0
+    while tot < seconds and reps < 1000:
+        src = np.zeros((n, stride), np.uint8)
+        src[:, :L] = rng.integers(0, 256, (n, L), dtype=np.uint8)
+        sp = (rng.random(n) >= cfg.loss).astype(np.uint8)
+        rp = (rng.random(nrep) >= cfg.loss).astype(np.uint8)
+        t0 = time.perf_counter()
+        rep = O.sw_encode(src, hdr, L)
+        src[sp == 0] = 0
+        O.sw_decode(src, sp, rep, rp, hdr, L)
+        tot += time.perf_counter() - t0
+        src_b += n * L
+        reps += 1
+    return {"value": round(src_b / tot / 1e9, 5), "unit": "GB/s", "cores": 1, "kind": "port",
+            "codec": "oracle/fec_oracle.c orc_sw_encode + orc_sw_decode (scalar C; one Gauss-Jordan "
+                     "over all lost sources of a slice)",
+            "sample": f"{reps} slices of {n} sources x {L} B (W {W}, step {k}, loss {cfg.loss}), "
+                      f"{tot:.1f} s on 1 host thread"}
+
+
 def launch_ranks(args) -> int:
     """`bench.py --gpus N` without a launcher: run N ranks (one per GPU) through a
     torch.distributed.run child and return its exit code.  Called before anything
@@ -202,7 +243,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     cfg = workloads.CONFIGS[args.config]
-    if args.matrix != "cauchy" and cfg.scheme != "xor":
+    if args.matrix != "cauchy" and cfg.scheme not in ("xor", "sw"):
         cfg = dataclasses.replace(cfg, matrix=args.matrix, name=f"{cfg.name}-{args.matrix}")
     nwin = args.nwin or cfg.nwin_per_gpu
     w0, nwin = shard.weak_shard(rank, world, nwin)  # this rank's global window range
@@ -219,7 +260,13 @@ def main():
         ctx.set_tuning("host_direct", args.host_direct)
     if args.host_chunk_mb:
         ctx.set_tuning("host_chunk_mb", args.host_chunk_mb)
-    if cfg.host:  # config 5: host buffers, PCIe-inclusive (never the headline value)
+    if cfg.scheme == "sw":  # config 7: one sliding-window stream per rank
+        batch = workloads.SwBatch.allocate(cfg, nwin, dev)
+        log(f"rank {rank}: {cfg.name}, {batch.nsrc} sources, {batch.nrep} repairs, "
+            f"{(batch.src.numel() + batch.rep.numel()) / 2**30:.2f} GiB")
+        batch.synthesize(ctx, w0)
+        batch.make_erasures(ctx, w0)
+    elif cfg.host:  # config 5: host buffers, PCIe-inclusive (never the headline value)
         batch = workloads.HostBatch.allocate(cfg, nwin, dev)
         log(f"rank {rank}: {cfg.name}, windows [{w0}, {w0 + nwin}), "
             f"{batch.buf.nbytes / 2**30:.2f} GiB pinned host")
@@ -295,14 +342,17 @@ def main():
 
     if rank == 0:
         dom = "decode" if dec_ms > enc_ms else "encode"
-        dom_ms = max(enc_ms, dec_ms)
+        if cfg.scheme == "sw":  # the decode call is host-plan bound; its kernels are minor
+            dom = "encode"
+        dom_ms = enc_ms if dom == "encode" else dec_ms
         achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
         traffic, traffic_src = (pmc_traffic(args.config, dom) if nwin == cfg.nwin_per_gpu and cfg.matrix == "cauchy"
                                 else (None, None))
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
             log("cpu baseline")
-            cpu = cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads)
+            cpu = (cpu_baseline_sw(cfg, args.cpu_seconds) if cfg.scheme == "sw" else
+                   cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads))
         peak, bound = (PCIE_PEAK_GBS, "pcie") if cfg.host else (HBM_PEAK_GBS, "hbm")
         line = {
             "metric": ("GB/s source-packet bytes FEC encode+decode, host buffers, PCIe-inclusive"
@@ -324,15 +374,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (on-device splitmix64 packets, seeded erasures)",
-            "config": {
+            "data": ("synthetic (seeded torch bytes on the device, seeded host loss flags)" if cfg.scheme == "sw"
+                     else "synthetic (on-device splitmix64 packets, seeded erasures)"),
+            "config": ({
+                "workload": cfg.name, "scheme": "sliding-window RLC (RFC 8681)",
+                "sources_per_gpu": nwin * cfg.k, "repairs_per_gpu": nwin, "window": cfg.window,
+                "step": cfg.k, "packet_bytes": cfg.L, "erasures": cfg.erasure_desc,
+                "parallelism": f"stream per rank x{world}",
+                "decode": "host plan + device kernels per call (arrival flags are host data)",
+            } if cfg.scheme == "sw" else {
                 "workload": cfg.name,
                 "scheme": cfg.scheme, "k": cfg.k, "r": cfg.r,
                 **({"matrix": cfg.matrix} if cfg.scheme != "xor" else {}),
                 "windows_per_gpu": nwin, "packet_bytes": cfg.L if cfg.workload == 0 else "1200|9000 mixed",
                 "erasures": cfg.erasure_desc,
                 "parallelism": f"window-shard x{world}",
-            },
+            }),
             "kernels_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
             "kernel_timing": ("host wall clock per synchronous call" if cfg.host else
                               f"HIP events on the launch stream around encode/decode, "

@@ -31,6 +31,8 @@ class Config:
     matrix: str = "cauchy"  # GF parity rows: cauchy | vandermonde | rlc (bench.py --matrix)
     rlc_key: int = 0
     rlc_dt: int = 15
+    window: int = 0        # scheme "sw": a repair after every k sources over the last `window`
+    loss: float = 0.0      # scheme "sw": i.i.d. loss of sources and repairs
 
     @property
     def code(self) -> Code:
@@ -59,6 +61,10 @@ CONFIGS = {
               ERASURE_EXACT, "one source per XOR group (e=r=2)", host=True),
     6: Config("cfg5gf-stream-gf256-k8r2-1200B-pinned-host", "gf256", 8, 2, WORKLOAD_FIXED, 1200,
               65536, ERASURE_EXACT, "exactly r=2 sources per window", host=True),
+    # sliding-window RLC (RFC 8681, fecgpu_sw_*): 65,536 repairs per GPU, one every
+    # k = 8 sources over the last 32, over 524,288 sources x 1200 B (one stream per rank)
+    7: Config("cfg7-sw-rlc-W32-step8-1200B-512k", "sw", 8, 1, WORKLOAD_FIXED, 1200, 65536, ERASURE_IID,
+              "i.i.d. p=0.02 over sources and repairs", matrix="rlc", window=32, loss=0.02),
 }
 
 
@@ -284,3 +290,96 @@ class HostBatch:
         v[:, :c.k] = saved
         return {"ok": mism == 0 and bool(ok.all()), "windows": self.nwin,
                 "mismatched_ok_windows": mism, "unrecoverable": int((~ok).sum())}
+
+
+@dataclass
+class SwBatch:
+    """Config 7: one sliding-window RLC stream per rank (RFC 8681 with m = 8):
+    nsrc = nwin * k sources of L bytes resident in HBM, nwin repairs, a repair
+    after every k sources over the last `window` (repair_key = its index, DT 15).
+    One step = fecgpu_sw_encode of every repair, then fecgpu_sw_decode at the
+    config's loss rate (the receiver's arrival flags are host data, so the decode
+    call plans on the host and waits for its kernels)."""
+    cfg: Config
+    nsrc: int
+    nrep: int
+    src: torch.Tensor        # [nsrc, stride] u8
+    rep: torch.Tensor        # [nrep, stride] u8
+    hdr: "np.ndarray"        # SW_REPAIR_DTYPE [nrep]
+    d_hdr: torch.Tensor      # the headers on the device
+    sp: "np.ndarray"         # source arrived flags
+    rp: "np.ndarray"         # repair arrived flags
+    st: "np.ndarray"         # per-source status of the last decode
+
+    @staticmethod
+    def allocate(cfg: Config, nwin: int, dev) -> "SwBatch":
+        import numpy as np
+        from . import SW_REPAIR_DTYPE
+        nsrc, stride = nwin * cfg.k, cfg.stride
+        hdr = np.zeros(nwin, SW_REPAIR_DTYPE)
+        end = (np.arange(nwin, dtype=np.int64) + 1) * cfg.k
+        fss = np.maximum(0, end - cfg.window)
+        hdr["fss"], hdr["nss"], hdr["key"], hdr["dt"] = fss, end - fss, np.arange(nwin) & 0xFFFF, 15
+        return SwBatch(cfg, nsrc, nwin, torch.zeros((nsrc, stride), dtype=torch.uint8, device=dev),
+                       torch.zeros((nwin, stride), dtype=torch.uint8, device=dev), hdr,
+                       torch.from_numpy(hdr.view(np.uint8).copy()).to(dev),
+                       np.ones(nsrc, np.uint8), np.ones(nwin, np.uint8), np.zeros(nsrc, np.uint8))
+
+    def synthesize(self, ctx: Context, w0: int) -> None:
+        g = torch.Generator(device=self.src.device).manual_seed(SEED ^ w0)
+        self.src[:, :self.cfg.L] = torch.randint(0, 256, (self.nsrc, self.cfg.L), dtype=torch.uint8,
+                                                 device=self.src.device, generator=g)
+
+    def make_erasures(self, ctx: Context, w0: int) -> None:
+        import numpy as np
+        rng = np.random.default_rng(SEED + w0)
+        self.sp[:] = rng.random(self.nsrc) >= self.cfg.loss
+        self.rp[:] = rng.random(self.nrep) >= self.cfg.loss
+
+    def encode(self, ctx: Context) -> None:
+        c = self.cfg
+        ctx.sw_encode(self.src, self.rep, self.d_hdr, nsrc=self.nsrc, nrep=self.nrep, sym_len=c.L,
+                      stride=c.stride, max_window=c.window)
+
+    def decode(self, ctx: Context) -> int:
+        c = self.cfg
+        return ctx.sw_decode(self.src, self.sp, self.rep, self.rp, self.hdr, self.st, nsrc=self.nsrc,
+                             nrep=self.nrep, sym_len=c.L, stride=c.stride)
+
+    def source_bytes(self) -> int:
+        return self.nsrc * self.cfg.L
+
+    def algorithmic_bytes(self) -> dict:
+        """encode: every source read once and every repair written, (nsrc + nrep) * L
+        (a source sits in window / k windows; the re-reads are the kernel's, not the
+        algorithm's).  decode: per recovered source one equation, i.e. its repair's
+        window read (window + 1 rows: the sources and the repair) and the source
+        written, (window + 2) * L each."""
+        c = self.cfg
+        lost = int((self.sp == 0).sum())
+        return {"encode": (self.nsrc + self.nrep) * c.L, "decode": lost * (c.window + 2) * c.L}
+
+    def digest(self, ctx: Context, w0: int) -> int:
+        """Checksum of the repairs (sum of their 8-byte words mod 2^64)."""
+        self.encode(ctx)
+        torch.cuda.synchronize()
+        return int(self.rep[:, :self.cfg.stride // 8 * 8].contiguous().view(torch.int64).sum().item()) & (2**64 - 1)
+
+    def verify(self, ctx: Context, w0: int) -> dict:
+        """Poison the lost sources, decode once, compare every source reported
+        recovered with the copy taken before; then restore the stream."""
+        import numpy as np
+        c = self.cfg
+        self.encode(ctx)
+        saved = self.src.clone()
+        lost = torch.from_numpy(self.sp == 0).to(self.src.device)
+        self.src[lost] = 0xAB
+        n = self.decode(ctx)
+        torch.cuda.synchronize()
+        ok = torch.from_numpy(self.st == STATUS_OK).to(self.src.device)
+        mism = int((ok & ~(self.src[:, :c.L] == saved[:, :c.L]).all(1)).sum().item())
+        nlost = int(lost.sum().item())
+        unrec = int((self.st != STATUS_OK).sum())
+        self.src.copy_(saved)
+        return {"ok": mism == 0 and n + unrec == nlost, "sources": self.nsrc, "lost": nlost, "recovered": n,
+                "unrecovered": unrec, "mismatched_recovered": mism}

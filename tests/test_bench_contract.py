@@ -37,6 +37,15 @@ def test_cpu_baseline_leg(bench, cfgid):
     assert out["value"] > 0 and cfg.name in out["sample"]
 
 
+def test_cpu_baseline_leg_sliding_window(bench):
+    """Config 7 (sliding-window RLC): the scalar C oracle on bounded slices."""
+    from fecgpu import workloads
+    cfg = workloads.CONFIGS[7]
+    out = bench.cpu_baseline_sw(cfg, 0.05)
+    assert out["unit"] == "GB/s" and out["cores"] == 1 and out["kind"] == "port"
+    assert out["value"] > 0 and "8192 sources" in out["sample"]
+
+
 @pytest.mark.parametrize("cfgid,kernel", [(2, "encode"), (2, "decode"), (3, "encode"), (3, "decode"),
                                           (4, "encode"), (4, "decode")])
 def test_committed_pmc_traffic(bench, cfgid, kernel):

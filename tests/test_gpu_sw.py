@@ -273,3 +273,25 @@ def test_sw_full_size_roundtrip(ctx):
                          hdr_array(hp), L)
     assert np.array_equal(st[:c], ost)
     assert np.array_equal(od[ost == 0], sub[ost == 0])
+
+
+def test_bench_config7_batch(ctx):
+    """bench.py --config 7's SwBatch: its repairs equal the oracle's over the
+    stream's first sources, and its verify step (poison, decode, compare)
+    recovers every determined lost source byte for byte."""
+    from fecgpu import workloads
+    cfg = workloads.CONFIGS[7]
+    b = workloads.SwBatch.allocate(cfg, 2048, torch.device("cuda"))
+    b.synthesize(ctx, 0)
+    b.make_erasures(ctx, 0)
+    b.encode(ctx)
+    torch.cuda.synchronize()
+    n = 512
+    src = b.src[:n].cpu().numpy()
+    hdr = b.hdr[: n // cfg.k]
+    o = O.sw_encode(src, hdr, cfg.L)
+    assert np.array_equal(b.rep[: n // cfg.k, :cfg.L].cpu().numpy(), o[:, :cfg.L])
+    v = b.verify(ctx, 0)
+    assert v["ok"] and v["lost"] > 0 and v["recovered"] > 0.9 * v["lost"], v
+    alg = b.algorithmic_bytes()
+    assert alg["encode"] == (b.nsrc + b.nrep) * cfg.L
