@@ -1930,7 +1930,10 @@ __global__ __launch_bounds__(kBlock) void digest_kernel(DigestArgs a) {
 // combine kernel: input rows loaded per batch.  One output (repairs,
 // syndromes): 16 (sliding-window encode k 8 W 32: 0.370 vs 0.387 ms at 8,
 // 0.466 at 4; profiles/r02_sw_ab.txt); solves (8 outputs, register-bound): 8.
-#define FECGPU_COMB_U (R == 1 ? 16 : 8)
+#ifndef FECGPU_COMB_U_GRP
+#define FECGPU_COMB_U_GRP 8  // grouped encode jobs (R = 2, 4)
+#endif
+#define FECGPU_COMB_U (R == 1 ? 16 : R == 8 ? 8 : FECGPU_COMB_U_GRP)
 #endif
 
 #ifndef FECGPU_COMB_SKIP
