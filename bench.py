@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--grid-mult", type=int, default=0, help="tuning: persistent grid multiplier")
     ap.add_argument("--bitslice", type=int, choices=[0, 1], default=None,
                     help="tuning: GF encode by the bit-sliced kernels (1, default) or the table multiply (0)")
+    ap.add_argument("--bs-passes", type=int, default=0,
+                    help="tuning: bit-sliced encode on per-window lengths, 256-unit passes per window group")
     ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
     ap.add_argument("--bpc", type=int, default=0, help="tuning: persistent workgroups per CU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -252,6 +254,8 @@ def main():
         ctx.set_tuning("grid_mult", args.grid_mult)
     if args.bitslice is not None:
         ctx.set_tuning("bitslice", args.bitslice)
+    if args.bs_passes:
+        ctx.set_tuning("bs_passes", args.bs_passes)
     if args.wpb:
         ctx.set_tuning("wpb", args.wpb)
     if args.bpc:

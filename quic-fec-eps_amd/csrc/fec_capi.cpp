@@ -422,22 +422,31 @@ ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out)
         // q, q - 4) for which bit p of P[i][j] * 2^q is set; stored lo | hi << 8,
         // or as two dwords lo, hi (fec_kernels.hip rbs::)
         static constexpr GfTables g = make_gf_tables();
-        std::vector<uint32_t> m((size_t)k * r * 8 * kRbsPlaneDw, 0);
+        std::vector<uint32_t> m((size_t)k * r * 2 * kRbsDw4, 0);
         for (int j = 0; j < k; j++)
             for (int i = 0; i < r; i++) {
                 const uint8_t c = P[(size_t)i * k + j];
+                uint32_t *row = &m[((size_t)j * r + i) * 2 * kRbsDw4];  // this repair's 8 planes
                 for (int p = 0; p < 8; p++) {
                     uint32_t lo = 0, hi = 0;
                     for (int q = 0; q < 8; q++) {
                         const uint8_t col = c ? g.exp[g.log[c] + q] : 0;
                         if ((col >> p) & 1) (q < 4 ? lo : hi) |= 1u << (q & 3);
                     }
-                    uint32_t *d = &m[(((size_t)j * r + i) * 8 + p) * kRbsPlaneDw];
-                    if (kRbsPlaneDw == 2) {  // four-column units index register pairs: 2 x index
-                        d[0] = lo * (kRbsCols / 2);
-                        d[kRbsPlaneDw - 1] = hi * (kRbsCols / 2);
+                    if (kRbsCols == 4) {  // four-column units index register pairs: 2 x index
+                        if (kRbsDw4 == 8) {
+                            row[2 * p] = lo * 2;
+                            row[2 * p + 1] = hi * 2;
+                        } else if (kRbsDw4 == 4) {
+                            row[p] = lo * 2 | (hi * 2) << 16;
+                        } else {  // bytes lo, hi of plane p in dword p / 2
+                            row[p / 2] |= (lo * 2 | (hi * 2) << 8) << (16 * (p & 1));
+                        }
+                    } else if (kRbsDw4 == 8) {
+                        row[2 * p] = lo;
+                        row[2 * p + 1] = hi;
                     } else {
-                        d[0] = lo | hi << 8;
+                        row[p] = lo | hi << 8;
                     }
                 }
             }
@@ -790,7 +799,9 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         p.flat = false;
 #endif
         p.lds_bytes = 0;
-        const uint32_t units = ncol ? (ncol + 1) / 2 : (uint32_t)((stride >> 4) + 1) / 2;
+        // units of kRbsCols columns (the group sizing above counted pairs)
+        const uint32_t c16 = ncol ? ncol : stride >> 4;
+        const uint32_t units = (c16 + kRbsCols - 1) / kRbsCols;
         const uint32_t want = (uint32_t)ctx->bs_passes * kBlock;
         p.wpb = units ? std::max(1, std::min<int>(kMaxWpb, (int)((want + units - 1) / units))) : kMaxWpb;
     }

@@ -32,7 +32,7 @@ struct BatchArgs {
     const uint4 *enc_ab;       // encode tables [k][r] (TA lo/hi, TB lo/hi)
     const uint32_t *enc_c;     // encode tables [k][r] (TC)
     const uint8_t *coef;       // GF decode: parity rows P[r][k] of a non-Cauchy matrix (null: Cauchy)
-    const uint32_t *enc_bs;    // runtime bit-sliced encode: plane indices [k][r][8][kRbsPlaneDw]
+    const uint32_t *enc_bs;    // runtime bit-sliced encode: plane indices [k][r][2][kRbsDw4]
     uint64_t nwin;
     uint64_t gmask[kMaxR];     // XOR: members of group g (bit j)
     uint64_t step_win;         // flat mode: (grid threads) / ncol
@@ -86,7 +86,17 @@ struct LaunchPlan {
 #define FECGPU_RBS_COLS 4
 #endif
 constexpr int kRbsCols = FECGPU_RBS_COLS;
-constexpr int kRbsPlaneDw = FECGPU_RBS_WIDE || FECGPU_RBS_COLS == 4 ? 2 : 1;  // mask dwords per output plane
+#ifndef FECGPU_RBS4_PACK
+// four-column units, index table format: 0 = two dwords per plane (lo x 2,
+// hi x 2); 1 = one dword per plane (lo x 2 | hi x 2 << 16, one s_lshr per
+// plane); 2 = one dword per two planes (a byte per index, 1.5 s_lshr per
+// plane).  Smaller tables stay in the scalar cache (k48 r8: 24 KB at 0)
+#define FECGPU_RBS4_PACK 2
+#endif
+// dwords of the index table per 4 output planes
+constexpr int kRbsDw4 = FECGPU_RBS_COLS == 4 ? (FECGPU_RBS4_PACK == 2 ? 2 : FECGPU_RBS4_PACK == 1 ? 4 : 8)
+                                             : (FECGPU_RBS_WIDE ? 8 : 4);
+constexpr int kRbsPlaneDw = kRbsDw4 >= 4 ? kRbsDw4 / 4 : 1;  // mask dwords per output plane (0.5: see kRbsDw4)
 
 // GF encode of (k, r, matrix) has a compiled bit-sliced kernel.
 bool bitslice_supported(int k, int r, int matrix);

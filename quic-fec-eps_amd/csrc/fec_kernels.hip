@@ -1052,13 +1052,20 @@ namespace rbs4 {
 using rbs::cmask;
 
 #define R4_IN(A, N, R0) "{v" #R0 "}"(A[N])
+#if FECGPU_RBS4_PACK  // l[q] = lo x 2 | hi x 2 << 16: M0[7:0] takes the low byte
+#define R4_HI(Q) "s_lshr_b32 %[t], %[l" #Q "], 16\n\ts_set_gpr_idx_idx %[t]\n\t"
+#define R4_ON "s_lshr_b32 %[t], %[l0], 16\n\ts_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
+#else
+#define R4_HI(Q) "s_set_gpr_idx_idx %[h" #Q "]\n\t"
+#define R4_ON "s_set_gpr_idx_on %[h0], gpr_idx(SRC0)\n\t"
+#endif
 #define R4_PAIR(Q0, Q1, TA, TB)                                                 \
-    "s_set_gpr_idx_idx %[h" #Q0 "]\n\t"                                        \
+    R4_HI(Q0)                                                                   \
     "v_mov_b64 v[" #TA ":" #TB "], v[64:65]\n\t"                               \
     "s_set_gpr_idx_idx %[l" #Q0 "]\n\t"                                        \
     "v_bitop3_b32 %[a" #Q0 "], v32, %[a" #Q0 "], v" #TA " bitop3:0x96\n\t"      \
     "v_bitop3_b32 %[b" #Q0 "], v33, %[b" #Q0 "], v" #TB " bitop3:0x96\n\t"      \
-    "s_set_gpr_idx_idx %[h" #Q1 "]\n\t"                                        \
+    R4_HI(Q1)                                                                   \
     "v_mov_b64 v[" #TA ":" #TB "], v[64:65]\n\t"                               \
     "s_set_gpr_idx_idx %[l" #Q1 "]\n\t"                                        \
     "v_bitop3_b32 %[a" #Q1 "], v32, %[a" #Q1 "], v" #TA " bitop3:0x96\n\t"      \
@@ -1067,11 +1074,30 @@ using rbs::cmask;
 // planes q = 0..3 of one repair half: (a[q], b[q]) ^= lo[l[q]] ^ hi[h[q]]
 __device__ __forceinline__ void pick4(uint32_t (&a)[4], uint32_t (&b)[4], const uint32_t (&l)[4],
                                       const uint32_t (&h)[4], const uint32_t (&lo)[32], const uint32_t (&hi)[32]) {
-    asm("s_set_gpr_idx_on %[h0], gpr_idx(SRC0)\n\t"
+    uint32_t t;  // packed indices: the index shifted down
+#if FECGPU_RBS4_PACK == 2  // l[0] = planes 0, 1 and l[1] = planes 2, 3, a byte per index
+#define R4_B(D, QA, QB, TA, TB)                                                 \
+    "s_lshr_b32 %[t], %[" D "], 8\n\ts_set_gpr_idx_idx %[t]\n\t"               \
+    "v_mov_b64 v[" #TA ":" #TB "], v[64:65]\n\t"                               \
+    "s_set_gpr_idx_idx %[" D "]\n\t"                                           \
+    "v_bitop3_b32 %[a" #QA "], v32, %[a" #QA "], v" #TA " bitop3:0x96\n\t"      \
+    "v_bitop3_b32 %[b" #QA "], v33, %[b" #QA "], v" #TB " bitop3:0x96\n\t"      \
+    "s_lshr_b32 %[t], %[" D "], 24\n\ts_set_gpr_idx_idx %[t]\n\t"              \
+    "v_mov_b64 v[" #TA ":" #TB "], v[64:65]\n\t"                               \
+    "s_lshr_b32 %[t], %[" D "], 16\n\ts_set_gpr_idx_idx %[t]\n\t"              \
+    "v_bitop3_b32 %[a" #QB "], v32, %[a" #QB "], v" #TA " bitop3:0x96\n\t"      \
+    "v_bitop3_b32 %[b" #QB "], v33, %[b" #QB "], v" #TB " bitop3:0x96\n\t"
+    asm("s_set_gpr_idx_on %[l0], gpr_idx(SRC0)\n\t"  // any index: the first set below replaces it
+        R4_B("l0", 0, 1, 96, 97) R4_B("l1", 2, 3, 98, 99)
+        "s_set_gpr_idx_off"
+#undef R4_B
+#else
+    asm(R4_ON
         R4_PAIR(0, 1, 96, 97) R4_PAIR(2, 3, 98, 99)
         "s_set_gpr_idx_off"
+#endif
         : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]),
-          [b0] "+v"(b[0]), [b1] "+v"(b[1]), [b2] "+v"(b[2]), [b3] "+v"(b[3])
+          [b0] "+v"(b[0]), [b1] "+v"(b[1]), [b2] "+v"(b[2]), [b3] "+v"(b[3]), [t] "=&s"(t)
         : [l0] "s"(l[0]), [l1] "s"(l[1]), [l2] "s"(l[2]), [l3] "s"(l[3]),
           [h0] "s"(h[0]), [h1] "s"(h[1]), [h2] "s"(h[2]), [h3] "s"(h[3]),
           R4_IN(lo, 0, 32), R4_IN(lo, 1, 33), R4_IN(lo, 2, 34), R4_IN(lo, 3, 35),
@@ -1094,9 +1120,11 @@ __device__ __forceinline__ void pick4(uint32_t (&a)[4], uint32_t (&b)[4], const 
 }
 #undef R4_IN
 #undef R4_PAIR
+#undef R4_HI
+#undef R4_ON
 
 // acc ^= one source (planes xa of columns 0-1, xb of columns 2-3) times its
-// mask row mk ([R][8][2] dwords: lo, hi indices x 2)
+// mask row mk ([R][2][kRbsDw4] dwords: lo, hi indices x 2, or packed)
 template <int R>
 __device__ __forceinline__ void source(const uint32_t (&xa)[8], const uint32_t (&xb)[8], uint32_t (&aa)[R][8],
                                        uint32_t (&ab)[R][8], cmask mk) {
@@ -1117,12 +1145,17 @@ __device__ __forceinline__ void source(const uint32_t (&xa)[8], const uint32_t (
     for (int i = 0; i < R; i++)
 #pragma unroll
         for (int w = 0; w < 2; w++) {
-            const cmask m = mk + (i * 8 + w * 4) * 2;
+            const cmask m = mk + (i * 2 + w) * kRbsDw4;
             uint32_t l[4], h[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                l[q] = m[q * 2];
-                h[q] = m[q * 2 + 1];
+                if (kRbsDw4 == 2) {  // two dwords for the 4 planes (l[2], l[3], h unused)
+                    l[q] = q < 2 ? m[q] : 0u;
+                    h[q] = l[q];
+                } else {
+                    l[q] = m[q * kRbsPlaneDw];
+                    h[q] = m[q * kRbsPlaneDw + kRbsPlaneDw - 1];  // = l[q] when packed (unused)
+                }
             }
             uint32_t(&ca)[4] = *reinterpret_cast<uint32_t(*)[4]>(&aa[i][w * 4]);
             uint32_t(&cb)[4] = *reinterpret_cast<uint32_t(*)[4]>(&ab[i][w * 4]);
@@ -1159,7 +1192,7 @@ __device__ __forceinline__ void unit(uint8_t *const (&pc)[4], uint32_t stride, i
         load(pc, (uint32_t)min(j + 1, k - 1) * stride, na, nb);
         bs::tr8(xa);
         bs::tr8(xb);
-        source<R>(xa, xb, aa, ab, mk + (size_t)j * (R * 16));
+        source<R>(xa, xb, aa, ab, mk + (size_t)j * (R * 2 * kRbsDw4));
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < 8; q++) {

@@ -11,6 +11,6 @@ run() {  # name lib args...
 for rep in 1 2; do
   run base quic-fec-eps_amd/lib/libfecgpu.so --config 4 --matrix rlc
   run table quic-fec-eps_amd/lib/libfecgpu.so --config 4 --matrix rlc --bitslice 0
-  for v in cols2; do run $v quic-fec-eps_amd/lib/libfecgpu_$v.so --config 4 --matrix rlc; done
+  for v in pack0; do run $v quic-fec-eps_amd/lib/libfecgpu_$v.so --config 4 --matrix rlc; done
 done
 run cauchy quic-fec-eps_amd/lib/libfecgpu.so --config 4
