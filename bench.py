@@ -350,7 +350,8 @@ def main():
             dom = "encode"
         dom_ms = enc_ms if dom == "encode" else dec_ms
         achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
-        traffic, traffic_src = (pmc_traffic(args.config, dom) if nwin == cfg.nwin_per_gpu and cfg.matrix == "cauchy"
+        traffic, traffic_src = (pmc_traffic(args.config, dom)
+                                if nwin == cfg.nwin_per_gpu and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
                                 else (None, None))
         cpu = None
         if args.cpu_seconds > 0 and world == 1:

@@ -57,6 +57,8 @@ for s in "$@"; do
         pmc3w) pmc pmc3w 3 WRITE_SIZE ;;
         pmc4r) pmc pmc4r 4 FETCH_SIZE ;;
         pmc4w) pmc pmc4w 4 WRITE_SIZE ;;
+        pmc7r) pmc pmc7r 7 FETCH_SIZE ;;
+        pmc7w) pmc pmc7w 7 WRITE_SIZE ;;
         sqa*) c=${s#sqa}; pmc sqa$c $c SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
         sqb*) c=${s#sqb}; pmc sqb$c $c SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE ;;
         micro) step micro 600 python scripts/microbench.py ;;

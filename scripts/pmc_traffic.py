@@ -16,12 +16,22 @@ import json
 import statistics
 
 
-def per_kernel(path, counter):
+def kind(name, config):
+    """encode / decode / None for a kernel name (config 7, sliding window: the
+    encode is the grouped combine pass, comb_kernel<4>)."""
+    if "fecgpu" not in name:
+        return None
+    if config == 7:
+        return "encode" if "comb_kernel<4>" in name else None
+    return "encode" if "encode" in name else "decode" if "decode" in name else None
+
+
+def per_kernel(path, counter, config):
     out = collections.defaultdict(list)
     for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
-        n = r["Kernel_Name"]
-        if r["Counter_Name"] == counter and "fecgpu" in n and ("encode" in n or "decode" in n):
-            out["encode" if "encode" in n else "decode"].append(float(r["Counter_Value"]))
+        kd = kind(r["Kernel_Name"], config)
+        if r["Counter_Name"] == counter and kd:
+            out[kd].append(float(r["Counter_Value"]))
     return {k: statistics.median(v) for k, v in out.items()}
 
 
@@ -32,8 +42,8 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    f = per_kernel(a.fetch, "FETCH_SIZE")
-    w = per_kernel(a.write, "WRITE_SIZE")
+    f = per_kernel(a.fetch, "FETCH_SIZE", a.config)
+    w = per_kernel(a.write, "WRITE_SIZE", a.config)
     res = {"config": a.config, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
            "read = 2 x FETCH_SIZE x 1024 (gfx950 correction), write = WRITE_SIZE x 1024",
            "kernels": {}}
