@@ -137,7 +137,7 @@ void    fecgpu_host_free(void *p);
  * rows, r = 8, k in {16, 24, 32} — uses it, and of any other code with r >= 5
  * the runtime-mask bit-sliced kernel; 0: the table multiply for every code);
  * "sw_group" (sliding-window encode: consecutive repairs per combine job, each
- * source loaded once per group; 1, 2 or 4, default 4);
+ * source loaded once per group; 1, 2, 4 or 8, default 4);
  * "bs_passes" (bit-sliced encode on per-window lengths: 256-unit passes per
  * window group at the longest window, default 8); "conn_streams" (streams per
  * device shared round robin by the encoders / decoders created afterwards,

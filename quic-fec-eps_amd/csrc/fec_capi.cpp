@@ -158,7 +158,7 @@ struct fecgpu_ctx {
     size_t pinned_cache_cap = (size_t)1 << 30;
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
-    int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4)
+    int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
     // FECGPU_CHECK builds: bytes taken off the end of every checked range, so a
     // test can see the checker fire on a correct kernel ("check_shrink")
     int check_shrink = 0;
@@ -301,7 +301,7 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         return 0;
     }
     if (!std::strcmp(key, "sw_group")) {
-        if (value != 1 && value != 2 && value != 4) return FECGPU_ERR_INVALID_ARG;
+        if (value != 1 && value != 2 && value != 4 && value != 8) return FECGPU_ERR_INVALID_ARG;
         ctx->sw_group = (int)value;  // calls and objects created from now on
         return 0;
     }

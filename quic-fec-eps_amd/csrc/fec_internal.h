@@ -192,6 +192,7 @@ struct CombArgs {
     // encode's per-repair tail), at most extra_max; the grid covers the maximum
     const uint32_t *extra;
     uint64_t extra_max;
+    int skip;                  // grouped encode jobs: skip zero coefficients (wave-uniform test)
     uint32_t ncol, stride;
     int wpb, nin_max, nout_max;
     uint32_t job_lds;

@@ -2018,9 +2018,9 @@ __device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, in
                 // active lane needs.  With >= 64 columns per job a wave spans at
                 // most two jobs, its first and last active lanes'; otherwise no skip.
                 uint32_t nzm = 0xffu;
-                // only grouped encode jobs (R = 2, 4) have zero runs; single
-                // repairs, syndromes and solves are dense (+5 % time with the test)
-                if (R > 1 && R < 8 && skip) {
+                // only grouped encode launches (CombArgs::skip) have zero runs;
+                // single repairs, syndromes and solves are dense (+5 % time with the test)
+                if (R > 1 && skip) {
                     const uint32_t z = rg.nz[q];
                     const int last = 63 - __builtin_clzll(__builtin_amdgcn_read_exec());
                     nzm = __builtin_amdgcn_readfirstlane(z) | __builtin_amdgcn_readlane(z, last);
@@ -2133,7 +2133,7 @@ __global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
             const int nw = __builtin_amdgcn_readfirstlane(ne);
             const CombRegion<R> rg(regions + (size_t)jl * a.job_lds, a.nin_max);
             comb_dispatch<R>(nw, reinterpret_cast<const uint8_t *>(s_in[jl]) + col * 16u, a.stride,
-                             (int)s_nin[jl], ne, col, rg, a.ncol >= 64);
+                             (int)s_nin[jl], ne, col, rg, a.skip && a.ncol >= 64);
         }
         __syncthreads();
     }

@@ -48,7 +48,7 @@ bool header_ok(const fecgpu_sw_repair &h, uint64_t nsrc) {
 ssize_t run_comb(const CombJob *jobs, uint64_t njobs, const uint8_t *coef, const uint64_t *outs,
                  const uint8_t *in_base, uint8_t *out_base, const uint8_t *xor_base, uint32_t S,
                  uint32_t stride, int R, int nin_max, hipStream_t s, const uint32_t *extra = nullptr,
-                 uint64_t extra_max = 0) {
+                 uint64_t extra_max = 0, bool skip = false) {
     CombArgs a{};
     a.jobs = jobs;
     a.coef = coef;
@@ -59,12 +59,15 @@ ssize_t run_comb(const CombJob *jobs, uint64_t njobs, const uint8_t *coef, const
     a.njobs = njobs;
     a.extra = extra;
     a.extra_max = extra_max;
+    a.skip = skip;
     a.ncol = (S + 15u) >> 4;
     a.stride = stride;
     a.nin_max = std::max(1, nin_max);
     a.nout_max = R;
     a.job_lds = comb_job_lds(a.nin_max, R);
-    a.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(a.ncol, a.job_lds, kCombBudget)));
+    // groups of 8 have 8-output tables over a wider span: a larger share of the CU's LDS
+    const uint32_t budget = skip && R == 8 ? kCombBudget * 2 : kCombBudget;
+    a.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(a.ncol, a.job_lds, budget)));
     SW_TRY(launch_comb(a, R, s), "sliding-window combine launch");
     return 0;
 }
@@ -76,7 +79,10 @@ namespace fecgpu {
 // Repairs per group and the union span a group may cover: W + 3 steps for
 // 4 repairs at W / step = 4, so 2 * max_window keeps the overlapping stream
 // shapes grouped and the job tables small (comb_job_lds).
-int sw_span_max(int max_window) { return std::min<int>(kSwCoefPitch, 2 * std::max(1, max_window)); }
+int sw_span_max(int max_window, int group) {
+    // groups of 8: W + 7 steps at W / step = 4, within 3 * max_window
+    return std::min<int>(kSwCoefPitch, (group > 4 ? 3 : 2) * std::max(1, max_window));
+}
 
 // Host replica of sw_enc_group's fit test: every group's clipped windows span
 // at most span_max sources (then the per-repair tail is not launched).
@@ -107,7 +113,7 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
     ca.stride = stride;
     ca.max_window = max_window;
     ca.group = nrep > 1 && group > 1 ? group : 1;
-    ca.span_max = sw_span_max(max_window);
+    ca.span_max = sw_span_max(max_window, ca.group);
     ca.jobs = static_cast<CombJob *>(pj);
     ca.coef = static_cast<uint8_t *>(pc);
     ca.outs = static_cast<uint64_t *>(po);
@@ -123,7 +129,7 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
     SW_TRY(hipMemsetAsync(ca.tail, 0, sizeof(uint32_t), s), "sliding-window tail reset");
     SW_TRY(launch_sw_enc_coef(ca, s), "sliding-window coefficient launch");
     return run_comb(ca.jobs, ngroups, ca.coef, ca.outs, src, rep, nullptr, S, stride, ca.group,
-                    std::max(ca.span_max, max_window), s, tail ? ca.tail : nullptr, nrep);
+                    std::max(ca.span_max, max_window), s, tail ? ca.tail : nullptr, nrep, true);
 }
 
 }  // namespace fecgpu

@@ -114,7 +114,7 @@ def test_sw_encode_device_headers_are_clipped(ctx):
 
 
 @pytest.mark.parametrize("L", [300, 1200])   # < 64 / >= 64 columns: zero-skip off / on
-@pytest.mark.parametrize("group", [1, 2, 4])
+@pytest.mark.parametrize("group", [1, 2, 4, 8])
 @pytest.mark.parametrize("host", [False, True], ids=["dev_hdr", "host_hdr"])
 def test_sw_encode_grouped_jobs(group, host, L):
     """Grouped encode jobs (ctx "sw_group"): consecutive repairs share one combine
