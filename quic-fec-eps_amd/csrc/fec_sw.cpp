@@ -147,60 +147,98 @@ ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_
     return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s, group, hdr_host);
 }
 
-// Host arrays of a decode's linked systems (see fecgpu_sw_decode).
+// A decode's linked systems (see fecgpu_sw_decode).  The arrays the GPU reads
+// (comps | unk | eqr | eqc | eqh) are written straight into the ctx's pinned
+// staging block at offsets sized for the worst case (sw_plan_layout), so the
+// plan goes up with one copy per array and no host-side repacking; the device
+// block uses the same offsets.  lost / eq are per-thread scratch
+// (sw_plan_scratch) that keeps its capacity from call to call.
 struct SwPlan {
-    std::vector<SwComp> comps;
-    std::vector<uint64_t> unk, eqr;
-    std::vector<uint32_t> eqc;
-    std::vector<fecgpu_sw_repair> eqh;
+    SwComp *comps = nullptr;
+    uint64_t *unk = nullptr, *eqr = nullptr;
+    uint32_t *eqc = nullptr;
+    fecgpu_sw_repair *eqh = nullptr;
+    uint8_t *ustat = nullptr;  // statuses of the unknowns, copied back
+    uint64_t ncomp = 0, nunk = 0, neq = 0;
+    std::vector<uint64_t> lost, eq;  // lost sources ascending; one system's equations
     uint64_t amat = 0, nsolve = 0, tcoef = 0;
     int max_nss = 1, max_p = 1;
 };
 
-// Lost sources, ascending, split into linked systems: consecutive lost sources
+SwPlan &sw_plan_scratch() {
+    thread_local SwPlan P;
+    std::vector<uint64_t> lost = std::move(P.lost), eq = std::move(P.eq);
+    lost.clear();
+    eq.clear();
+    P = SwPlan{};
+    P.lost = std::move(lost);
+    P.eq = std::move(eq);
+    return P;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Offsets of the plan arrays for nlost lost sources and nrep repairs: at most
+// nlost systems and unknowns, and at most nrep equations (a received repair
+// holding lost sources of two systems would link them, so each repair is an
+// equation of one system at most).
+struct SwLayout {
+    size_t o_unk, o_eqr, o_eqc, o_eqh, meta, o_ust, host;
+};
+SwLayout sw_plan_layout(uint64_t nlost, uint64_t nrep) {
+    SwLayout L;
+    L.o_unk = align256(nlost * sizeof(SwComp));
+    L.o_eqr = L.o_unk + align256(nlost * 8);
+    L.o_eqc = L.o_eqr + align256(nrep * 8);
+    L.o_eqh = L.o_eqc + align256(nrep * 4);
+    L.meta = L.o_eqh + align256(nrep * sizeof(fecgpu_sw_repair));
+    L.o_ust = L.meta;  // host only: the unknowns' statuses
+    L.host = L.o_ust + nlost;
+    return L;
+}
+
+// Per-source statuses (0 present, 1 lost) and the lost sources, ascending, in
+// one pass over the arrival flags, 8 at a time: bit 7 of byte b of
+// ((v & 0x7f..) + 0x7f..) | v is set iff flag b is nonzero (no carries cross
+// bytes), so the status word is its complement shifted down.
+uint64_t sw_scan_lost(const uint8_t *src_present, uint64_t nsrc, uint8_t *src_status,
+                      std::vector<uint64_t> &lost) {
+    constexpr uint64_t k7f = 0x7f7f7f7f7f7f7f7full, k01 = 0x0101010101010101ull;
+    uint64_t i = 0;
+    for (; i + 8 <= nsrc; i += 8) {
+        uint64_t v;
+        std::memcpy(&v, src_present + i, 8);
+        const uint64_t st = ~((((v & k7f) + k7f) | v) >> 7) & k01;
+        std::memcpy(src_status + i, &st, 8);
+        for (uint64_t m = st; m; m &= m - 1) lost.push_back(i + ((uint64_t)__builtin_ctzll(m) >> 3));
+    }
+    for (; i < nsrc; i++) {
+        src_status[i] = src_present[i] ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
+        if (!src_present[i]) lost.push_back(i);
+    }
+    return lost.size();
+}
+
+// P.lost (ascending) split into linked systems: consecutive lost sources
 // a < b are linked iff a received repair's window holds both, i.e. some
 // received repair with fss <= a ends past b (windows are intervals, so this
 // links every pair a repair holds).  Each system's equations are the received
 // repairs whose windows hold one of its lost sources (the first kSwMaxEq).
 // Systems of more than kSwMaxUnknowns lost sources, or with no equation, are
-// left out (their sources stay lost).
-void sw_build_plan(const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep_present,
-                   const fecgpu_sw_repair *hdr, uint64_t nrep, SwPlan &P) {
-    // lost sources: 8 flags at a time, skipping words with no zero byte
-    std::vector<uint64_t> lost;
-    uint64_t i = 0;
-    for (; i + 8 <= nsrc; i += 8) {
-        uint64_t v;
-        std::memcpy(&v, src_present + i, 8);
-        if (!((v - 0x0101010101010101ull) & ~v & 0x8080808080808080ull)) continue;
-        for (int b = 0; b < 8; b++)
-            if (!src_present[i + b]) lost.push_back(i + b);
-    }
-    for (; i < nsrc; i++)
-        if (!src_present[i]) lost.push_back(i);
-    std::vector<uint64_t> pr;  // received repairs, fss ascending (headers are sorted)
-    pr.reserve(nrep);
-    uint64_t wmax = 1;  // longest received window: a repair holding source i has fss > i - wmax
-    for (uint64_t t = 0; t < nrep; t++)
-        if (rep_present[t]) {
-            pr.push_back(t);
-            wmax = std::max<uint64_t>(wmax, hdr[t].nss);
-        }
-    size_t ip = 0;
+// left out (their sources stay lost).  wmax: an upper bound of the received
+// windows' nss (a repair holding source i has fss > i - wmax).  Headers are in
+// fss order, so the repairs are walked directly with their arrival flags.
+void sw_build_plan(const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep,
+                   uint64_t wmax, SwPlan &P) {
+    const std::vector<uint64_t> &lost = P.lost;
+    std::vector<uint64_t> &eq = P.eq;
+    uint64_t ip = 0;  // repairs with fss <= the current lost source are folded into max_end
     uint64_t max_end = 0;
     size_t start = 0;
-    std::vector<uint64_t> eq;  // one system's equations (reused)
-    size_t jp = 0;             // first received repair that can hold the next system's sources
-    P.unk.reserve(lost.size());
-    P.comps.reserve(lost.size());
-    P.eqr.reserve(4 * lost.size());
-    P.eqc.reserve(4 * lost.size());
-    P.eqh.reserve(4 * lost.size());
+    uint64_t jp = 0;  // first repair that can hold the next system's sources
     for (size_t x = 0; x < lost.size(); x++) {
-        while (ip < pr.size() && hdr[pr[ip]].fss <= lost[x]) {
-            max_end = std::max(max_end, hdr[pr[ip]].fss + hdr[pr[ip]].nss);
-            ip++;
-        }
+        for (; ip < nrep && hdr[ip].fss <= lost[x]; ip++)
+            if (rep_present[ip]) max_end = std::max(max_end, hdr[ip].fss + hdr[ip].nss);
         if (x + 1 < lost.size() && max_end > lost[x + 1]) continue;
         // system = lost[start .. x]
         const uint64_t *U = lost.data() + start;
@@ -210,17 +248,18 @@ void sw_build_plan(const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep
         // systems come in ascending order, so the first candidate repair only
         // moves forward (a sweep, not a search per system)
         const uint64_t lo = U[0] >= wmax ? U[0] - wmax + 1 : 0;
-        while (jp < pr.size() && hdr[pr[jp]].fss < lo) jp++;
+        while (jp < nrep && hdr[jp].fss < lo) jp++;
         eq.clear();
-        for (size_t it = jp; it < pr.size() && hdr[pr[it]].fss <= U[e - 1] && eq.size() < (size_t)kSwMaxEq; ++it) {
-            const fecgpu_sw_repair &h = hdr[pr[it]];
+        for (uint64_t it = jp; it < nrep && hdr[it].fss <= U[e - 1] && eq.size() < (size_t)kSwMaxEq; ++it) {
+            if (!rep_present[it]) continue;
+            const fecgpu_sw_repair &h = hdr[it];
             const uint64_t *u = e == 1 ? U : std::lower_bound(U, U + e, h.fss);
-            if (u != U + e && *u >= h.fss && *u < h.fss + h.nss) eq.push_back(pr[it]);
+            if (u != U + e && *u >= h.fss && *u < h.fss + h.nss) eq.push_back(it);
         }
         if (eq.empty()) continue;
         SwComp c{};
-        c.u_off = P.unk.size();
-        c.q_off = P.eqr.size();
+        c.u_off = P.nunk;
+        c.q_off = P.neq;
         c.a_off = P.amat;
         c.j_off = P.nsolve;
         c.t_off = P.tcoef;  // relative; the syndrome coefficients go first
@@ -231,55 +270,47 @@ void sw_build_plan(const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep
         P.nsolve += (e + kSwSolveOut - 1) / kSwSolveOut;
         P.tcoef += (uint64_t)((e + kSwSolveOut - 1) / kSwSolveOut * kSwSolveOut) * c.p;
         P.max_p = std::max(P.max_p, (int)c.p);
-        const uint32_t ci = (uint32_t)P.comps.size();
-        for (size_t j = 0; j < e; j++) P.unk.push_back(U[j]);
+        const uint32_t ci = (uint32_t)P.ncomp;
+        for (size_t j = 0; j < e; j++) P.unk[P.nunk++] = U[j];
         for (uint64_t t : eq) {
-            P.eqr.push_back(t);
-            P.eqc.push_back(ci);
-            P.eqh.push_back(hdr[t]);
+            P.eqr[P.neq] = t;
+            P.eqc[P.neq] = ci;
+            P.eqh[P.neq++] = hdr[t];
             P.max_nss = std::max(P.max_nss, (int)hdr[t].nss);
         }
-        P.comps.push_back(c);
+        P.comps[P.ncomp++] = c;
     }
 }
 
-size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
-
-// Device part of a decode: src / rep device pointers, plan P on the host.
-ssize_t sw_decode_dev(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *rep, SwPlan &P, uint32_t S,
-                      uint32_t stride, const uint8_t **ustat, hipStream_t s) {
-    const uint64_t neq = P.eqr.size(), nunk = P.unk.size(), ncomp = P.comps.size();
+// Device part of a decode: src / rep device pointers, plan P in the pinned
+// staging block at layout L.
+ssize_t sw_decode_dev(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *rep, SwPlan &P, const SwLayout &L,
+                      uint32_t S, uint32_t stride, hipStream_t s) {
+    const uint64_t neq = P.neq, nunk = P.nunk, ncomp = P.ncomp;
     const uint64_t coef_syn = neq * kSwCoefPitch;
-    for (SwComp &c : P.comps) {
-        c.t_off += coef_syn;
-        c.o_off += neq;
+    for (uint64_t c = 0; c < ncomp; c++) {
+        P.comps[c].t_off += coef_syn;
+        P.comps[c].o_off += neq;
     }
-    // one metadata block: comps | unk | eqr | eqc | eqh, then amat, ustat, syndrome rows
-    const size_t o_unk = align256(ncomp * sizeof(SwComp));
-    const size_t o_eqr = o_unk + align256(nunk * 8);
-    const size_t o_eqc = o_eqr + align256(neq * 8);
-    const size_t o_eqh = o_eqc + align256(neq * 4);
-    const size_t o_amat = o_eqh + align256(neq * sizeof(fecgpu_sw_repair));
+    // device block: the plan arrays at L's offsets, then amat, ustat, syndrome rows
+    const size_t o_unk = L.o_unk, o_eqr = L.o_eqr, o_eqc = L.o_eqc, o_eqh = L.o_eqh;
+    const size_t o_amat = L.meta;
     const size_t o_ust = o_amat + align256(P.amat);
     const size_t o_syn = o_ust + align256(nunk);
     const size_t total = o_syn + neq * (size_t)stride;
-    // the plan goes up from (and the statuses come back to) the ctx's pinned
-    // staging block: a pageable copy of ~2 MB was a third of the call
-    void *ph = nullptr;
-    RC_TRY(ctx_sw_host(ctx, o_amat + nunk, &ph));
-    uint8_t *meta = static_cast<uint8_t *>(ph);
-    std::memcpy(meta, P.comps.data(), ncomp * sizeof(SwComp));
-    std::memcpy(meta + o_unk, P.unk.data(), nunk * 8);
-    std::memcpy(meta + o_eqr, P.eqr.data(), neq * 8);
-    std::memcpy(meta + o_eqc, P.eqc.data(), neq * 4);
-    std::memcpy(meta + o_eqh, P.eqh.data(), neq * sizeof(fecgpu_sw_repair));
+    const uint8_t *meta = reinterpret_cast<const uint8_t *>(P.comps);
     void *pm = nullptr, *pj = nullptr, *pc = nullptr, *po = nullptr;
     RC_TRY(ctx_sw_scratch(ctx, 6, total, &pm));
     RC_TRY(ctx_sw_scratch(ctx, 0, (neq + P.nsolve) * sizeof(CombJob), &pj));
     RC_TRY(ctx_sw_scratch(ctx, 1, coef_syn + P.tcoef, &pc));
     RC_TRY(ctx_sw_scratch(ctx, 2, (neq + nunk) * sizeof(uint64_t), &po));
     uint8_t *m = static_cast<uint8_t *>(pm);
-    SW_TRY(hipMemcpyAsync(m, meta, o_amat, hipMemcpyHostToDevice, s), "H2D sw plan");
+    // the used part of each array (from pinned memory: a pageable copy of
+    // ~2 MB was a third of the call)
+    const size_t part[5][2] = {{0, ncomp * sizeof(SwComp)}, {o_unk, nunk * 8}, {o_eqr, neq * 8},
+                               {o_eqc, neq * 4}, {o_eqh, neq * sizeof(fecgpu_sw_repair)}};
+    for (const auto &pt : part)
+        SW_TRY(hipMemcpyAsync(m + pt[0], meta + pt[0], pt[1], hipMemcpyHostToDevice, s), "H2D sw plan");
     CombJob *jobs = static_cast<CombJob *>(pj);
     uint8_t *coef = static_cast<uint8_t *>(pc);
     uint64_t *outs = static_cast<uint64_t *>(po);
@@ -314,9 +345,8 @@ ssize_t sw_decode_dev(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *rep, SwPlan 
     RC_TRY(run_comb(jobs, neq, coef, outs, src, synd, rep, S, stride, 1, P.max_nss, s));
     RC_TRY(run_comb(jobs + neq, P.nsolve, coef, outs, synd, src, nullptr, S, stride, kSwSolveOut,
                     P.max_p, s));
-    SW_TRY(hipMemcpyAsync(meta + o_amat, m + o_ust, nunk, hipMemcpyDeviceToHost, s), "D2H sw status");
-    *ustat = meta + o_amat;  // valid once the stream has completed
-    return 0;
+    SW_TRY(hipMemcpyAsync(P.ustat, m + o_ust, nunk, hipMemcpyDeviceToHost, s), "D2H sw status");
+    return 0;  // P.ustat is valid once the stream has completed
 }
 
 }  // namespace
@@ -367,19 +397,28 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
     if (!ctx || !src || !src_present || !src_status || nsrc == 0) return FECGPU_ERR_INVALID_ARG;
     if (nrep && (!rep || !rep_present || !hdr)) return FECGPU_ERR_INVALID_ARG;
     RC_TRY(check_geometry(sym_len, stride, src, nrep ? rep : src));
+    uint64_t wmax = 1, prev_fss = 0;
     for (uint64_t t = 0; t < nrep; t++) {
         if (!header_ok(hdr[t], nsrc)) return FECGPU_ERR_INVALID_ARG;
-        if (t && hdr[t].fss < hdr[t - 1].fss) return FECGPU_ERR_INVALID_ARG;  // fss nondecreasing
+        if (hdr[t].fss < prev_fss) return FECGPU_ERR_INVALID_ARG;  // fss nondecreasing
+        prev_fss = hdr[t].fss;
+        wmax = std::max<uint64_t>(wmax, hdr[t].nss);
     }
-    uint64_t nlost = 0;
-    for (uint64_t i = 0; i < nsrc; i++) {
-        src_status[i] = src_present[i] ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
-        nlost += !src_present[i];
-    }
+    SwPlan &P = sw_plan_scratch();
+    const uint64_t nlost = sw_scan_lost(src_present, nsrc, src_status, P.lost);
     if (nlost == 0 || nrep == 0) return 0;
-    SwPlan P;
-    sw_build_plan(src_present, nsrc, rep_present, hdr, nrep, P);
-    if (P.comps.empty()) return 0;
+    const SwLayout L = sw_plan_layout(nlost, nrep);
+    void *ph = nullptr;
+    RC_TRY(ctx_sw_host(ctx, L.host, &ph));
+    uint8_t *meta = static_cast<uint8_t *>(ph);
+    P.comps = reinterpret_cast<SwComp *>(meta);
+    P.unk = reinterpret_cast<uint64_t *>(meta + L.o_unk);
+    P.eqr = reinterpret_cast<uint64_t *>(meta + L.o_eqr);
+    P.eqc = reinterpret_cast<uint32_t *>(meta + L.o_eqc);
+    P.eqh = reinterpret_cast<fecgpu_sw_repair *>(meta + L.o_eqh);
+    P.ustat = meta + L.o_ust;
+    sw_build_plan(rep_present, hdr, nrep, wmax, P);
+    if (P.ncomp == 0) return 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     RC_TRY(ctx_sw_begin(ctx, s));
     uint8_t *dsrc = src;
@@ -393,15 +432,14 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
         dsrc = static_cast<uint8_t *>(ds);
         drep = static_cast<uint8_t *>(dr);
     }
-    const uint8_t *ustat = nullptr;
-    RC_TRY(sw_decode_dev(ctx, dsrc, drep, P, sym_len, stride, &ustat, s));
+    RC_TRY(sw_decode_dev(ctx, dsrc, drep, P, L, sym_len, stride, s));
     if (flags & FECGPU_F_HOST_PTRS)
         SW_TRY(hipMemcpyAsync(src, dsrc, nsrc * stride, hipMemcpyDeviceToHost, s), "D2H sw sources");
     RC_TRY(ctx_sw_end(ctx, s));
     SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
     ssize_t rec = 0;
-    for (size_t u = 0; u < P.unk.size(); u++)
-        if (ustat[u] == 0) {
+    for (uint64_t u = 0; u < P.nunk; u++)
+        if (P.ustat[u] == 0) {
             src_status[P.unk[u]] = FECGPU_STATUS_OK;
             rec++;
         }
