@@ -7,7 +7,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/fecgpu.h"
@@ -148,11 +154,10 @@ ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_
 }
 
 // A decode's linked systems (see fecgpu_sw_decode).  The arrays the GPU reads
-// (comps | unk | eqr | eqc | eqh) are written straight into the ctx's pinned
-// staging block at offsets sized for the worst case (sw_plan_layout), so the
-// plan goes up with one copy per array and no host-side repacking; the device
-// block uses the same offsets.  lost / eq are per-thread scratch
-// (sw_plan_scratch) that keeps its capacity from call to call.
+// (comps | unk | eqr | eqc | eqh) are written into the ctx's pinned staging
+// block at offsets sized for the worst case (sw_plan_layout), so the plan goes
+// up with one copy per array and no host-side repacking; the device block uses
+// the same offsets.  The same struct is a sweep's output cursor (SwPart).
 struct SwPlan {
     SwComp *comps = nullptr;
     uint64_t *unk = nullptr, *eqr = nullptr;
@@ -160,19 +165,17 @@ struct SwPlan {
     fecgpu_sw_repair *eqh = nullptr;
     uint8_t *ustat = nullptr;  // statuses of the unknowns, copied back
     uint64_t ncomp = 0, nunk = 0, neq = 0;
-    std::vector<uint64_t> lost, eq;  // lost sources ascending; one system's equations
     uint64_t amat = 0, nsolve = 0, tcoef = 0;
     int max_nss = 1, max_p = 1;
+    std::vector<uint64_t> lost;  // lost sources ascending (per-thread scratch, see sw_plan_scratch)
 };
 
 SwPlan &sw_plan_scratch() {
     thread_local SwPlan P;
-    std::vector<uint64_t> lost = std::move(P.lost), eq = std::move(P.eq);
+    std::vector<uint64_t> lost = std::move(P.lost);
     lost.clear();
-    eq.clear();
     P = SwPlan{};
     P.lost = std::move(lost);
-    P.eq = std::move(eq);
     return P;
 }
 
@@ -197,29 +200,47 @@ SwLayout sw_plan_layout(uint64_t nlost, uint64_t nrep) {
     return L;
 }
 
-// Per-source statuses (0 present, 1 lost) and the lost sources, ascending, in
-// one pass over the arrival flags, 8 at a time: bit 7 of byte b of
-// ((v & 0x7f..) + 0x7f..) | v is set iff flag b is nonzero (no carries cross
-// bytes), so the status word is its complement shifted down.
-uint64_t sw_scan_lost(const uint8_t *src_present, uint64_t nsrc, uint8_t *src_status,
-                      std::vector<uint64_t> &lost) {
+// Statuses (0 present, 1 lost) of sources [lo, hi) and their lost indices,
+// ascending, in one pass over the arrival flags, 8 at a time (lo a multiple of
+// 8): bit 7 of byte b of ((v & 0x7f..) + 0x7f..) | v is set iff flag b is
+// nonzero (no carries cross bytes), so the status word is its complement
+// shifted down.
+void sw_scan_lost(const uint8_t *src_present, uint64_t lo, uint64_t hi, uint8_t *src_status,
+                  std::vector<uint64_t> &lost) {
     constexpr uint64_t k7f = 0x7f7f7f7f7f7f7f7full, k01 = 0x0101010101010101ull;
-    uint64_t i = 0;
-    for (; i + 8 <= nsrc; i += 8) {
+    uint64_t i = lo;
+    for (; i + 8 <= hi; i += 8) {
         uint64_t v;
         std::memcpy(&v, src_present + i, 8);
         const uint64_t st = ~((((v & k7f) + k7f) | v) >> 7) & k01;
         std::memcpy(src_status + i, &st, 8);
         for (uint64_t m = st; m; m &= m - 1) lost.push_back(i + ((uint64_t)__builtin_ctzll(m) >> 3));
     }
-    for (; i < nsrc; i++) {
+    for (; i < hi; i++) {
         src_status[i] = src_present[i] ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
         if (!src_present[i]) lost.push_back(i);
     }
-    return lost.size();
 }
 
-// P.lost (ascending) split into linked systems: consecutive lost sources
+// First repair whose fss >= lo (headers are in fss order).
+uint64_t sw_first_repair(const fecgpu_sw_repair *hdr, uint64_t nrep, uint64_t lo) {
+    return (uint64_t)(std::partition_point(hdr, hdr + nrep, [lo](const fecgpu_sw_repair &h) { return h.fss < lo; }) -
+                      hdr);
+}
+
+// lost[x] begins a linked system iff no received repair with fss <= lost[x-1]
+// ends past lost[x] (only repairs with fss > lost[x-1] - wmax can).
+bool sw_system_start(const uint64_t *lost, size_t x, const uint8_t *rep_present,
+                     const fecgpu_sw_repair *hdr, uint64_t nrep, uint64_t wmax) {
+    if (x == 0) return true;
+    const uint64_t p = lost[x - 1];
+    for (uint64_t t = sw_first_repair(hdr, nrep, p >= wmax ? p - wmax + 1 : 0); t < nrep && hdr[t].fss <= p; t++)
+        if (rep_present[t] && hdr[t].fss + hdr[t].nss > lost[x]) return false;
+    return true;
+}
+
+// The sweep over lost[0 .. nl), which begins a system and ends where the next
+// one begins (or at the end of the lost sources): consecutive lost sources
 // a < b are linked iff a received repair's window holds both, i.e. some
 // received repair with fss <= a ends past b (windows are intervals, so this
 // links every pair a repair holds).  Each system's equations are the received
@@ -228,20 +249,22 @@ uint64_t sw_scan_lost(const uint8_t *src_present, uint64_t nsrc, uint8_t *src_st
 // left out (their sources stay lost).  wmax: an upper bound of the received
 // windows' nss (a repair holding source i has fss > i - wmax).  Headers are in
 // fss order, so the repairs are walked directly with their arrival flags.
-void sw_build_plan(const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep,
-                   uint64_t wmax, SwPlan &P) {
-    const std::vector<uint64_t> &lost = P.lost;
-    std::vector<uint64_t> &eq = P.eq;
-    uint64_t ip = 0;  // repairs with fss <= the current lost source are folded into max_end
+// Offsets in O's systems are relative to O's own arrays.
+void sw_sweep(const uint64_t *lost, size_t nl, const uint8_t *rep_present, const fecgpu_sw_repair *hdr,
+              uint64_t nrep, uint64_t wmax, SwPlan &O) {
+    if (nl == 0) return;
+    uint64_t eq[kSwMaxEq];
+    const uint64_t first = sw_first_repair(hdr, nrep, lost[0] >= wmax ? lost[0] - wmax + 1 : 0);
+    uint64_t ip = first;  // repairs with fss <= the current lost source are folded into max_end
+    uint64_t jp = first;  // first repair that can hold the next system's sources
     uint64_t max_end = 0;
     size_t start = 0;
-    uint64_t jp = 0;  // first repair that can hold the next system's sources
-    for (size_t x = 0; x < lost.size(); x++) {
+    for (size_t x = 0; x < nl; x++) {
         for (; ip < nrep && hdr[ip].fss <= lost[x]; ip++)
             if (rep_present[ip]) max_end = std::max(max_end, hdr[ip].fss + hdr[ip].nss);
-        if (x + 1 < lost.size() && max_end > lost[x + 1]) continue;
+        if (x + 1 < nl && max_end > lost[x + 1]) continue;
         // system = lost[start .. x]
-        const uint64_t *U = lost.data() + start;
+        const uint64_t *U = lost + start;
         const size_t e = x + 1 - start;
         start = x + 1;
         if (e > (size_t)kSwMaxUnknowns) continue;
@@ -249,37 +272,240 @@ void sw_build_plan(const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint
         // moves forward (a sweep, not a search per system)
         const uint64_t lo = U[0] >= wmax ? U[0] - wmax + 1 : 0;
         while (jp < nrep && hdr[jp].fss < lo) jp++;
-        eq.clear();
-        for (uint64_t it = jp; it < nrep && hdr[it].fss <= U[e - 1] && eq.size() < (size_t)kSwMaxEq; ++it) {
+        int neq = 0;
+        for (uint64_t it = jp; it < nrep && hdr[it].fss <= U[e - 1] && neq < kSwMaxEq; ++it) {
             if (!rep_present[it]) continue;
             const fecgpu_sw_repair &h = hdr[it];
             const uint64_t *u = e == 1 ? U : std::lower_bound(U, U + e, h.fss);
-            if (u != U + e && *u >= h.fss && *u < h.fss + h.nss) eq.push_back(it);
+            if (u != U + e && *u >= h.fss && *u < h.fss + h.nss) eq[neq++] = it;
         }
-        if (eq.empty()) continue;
+        if (neq == 0) continue;
         SwComp c{};
-        c.u_off = P.nunk;
-        c.q_off = P.neq;
-        c.a_off = P.amat;
-        c.j_off = P.nsolve;
-        c.t_off = P.tcoef;  // relative; the syndrome coefficients go first
+        c.u_off = O.nunk;
+        c.q_off = O.neq;
+        c.a_off = O.amat;
+        c.j_off = O.nsolve;
+        c.t_off = O.tcoef;  // relative; the syndrome coefficients go first
         c.o_off = c.u_off;  // relative; the syndrome outputs go first
         c.e = (uint32_t)e;
-        c.p = (uint32_t)eq.size();
-        P.amat += (uint64_t)c.e * c.p;
-        P.nsolve += (e + kSwSolveOut - 1) / kSwSolveOut;
-        P.tcoef += (uint64_t)((e + kSwSolveOut - 1) / kSwSolveOut * kSwSolveOut) * c.p;
-        P.max_p = std::max(P.max_p, (int)c.p);
-        const uint32_t ci = (uint32_t)P.ncomp;
-        for (size_t j = 0; j < e; j++) P.unk[P.nunk++] = U[j];
-        for (uint64_t t : eq) {
-            P.eqr[P.neq] = t;
-            P.eqc[P.neq] = ci;
-            P.eqh[P.neq++] = hdr[t];
-            P.max_nss = std::max(P.max_nss, (int)hdr[t].nss);
+        c.p = (uint32_t)neq;
+        O.amat += (uint64_t)c.e * c.p;
+        O.nsolve += (e + kSwSolveOut - 1) / kSwSolveOut;
+        O.tcoef += (uint64_t)((e + kSwSolveOut - 1) / kSwSolveOut * kSwSolveOut) * c.p;
+        O.max_p = std::max(O.max_p, (int)c.p);
+        const uint32_t ci = (uint32_t)O.ncomp;
+        for (size_t j = 0; j < e; j++) O.unk[O.nunk++] = U[j];
+        for (int q = 0; q < neq; q++) {
+            const uint64_t t = eq[q];
+            O.eqr[O.neq] = t;
+            O.eqc[O.neq] = ci;
+            O.eqh[O.neq++] = hdr[t];
+            O.max_nss = std::max(O.max_nss, (int)hdr[t].nss);
         }
-        P.comps[P.ncomp++] = c;
+        O.comps[O.ncomp++] = c;
     }
+}
+
+// Process-wide helper threads for large plans (FECGPU_PLAN_THREADS, default 4
+// including the caller; 1 = always serial).  Workers spin briefly between
+// runs (a stream of decodes comes every few hundred microseconds), then
+// sleep.  One plan holds the pool at a time (acquire); a caller that finds it
+// held plans alone.  The pool is never torn down (its threads are detached).
+class PlanPool {
+  public:
+    static PlanPool &get() {
+        static PlanPool *pool = new PlanPool();
+        return *pool;
+    }
+    int size() const { return n_; }
+    std::unique_lock<std::mutex> acquire() { return std::unique_lock<std::mutex>(run_mu_, std::try_to_lock); }
+    // fn(i) for every i in [0, size()), i = 0 on the caller; the caller holds acquire()'s lock
+    void run(const std::function<void(int)> &fn) {
+        fn_ = &fn;
+        pending_.store(n_ - 1, std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        fn(0);
+        while (pending_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+    }
+
+  private:
+    PlanPool() {
+        int n = 4;
+        if (const char *e = std::getenv("FECGPU_PLAN_THREADS")) n = std::atoi(e);
+        n = std::max(1, std::min(n, std::max(1, (int)std::thread::hardware_concurrency())));
+        n_ = std::min(n, kMaxThreads);
+        for (int i = 1; i < n_; i++) std::thread([this, i] { work(i); }).detach();
+    }
+    void work(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            for (int spin = 0; gen_.load(std::memory_order_acquire) == seen; spin++) {
+                if (spin < (1 << 16)) {
+                    __builtin_ia32_pause();
+                    continue;
+                }
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+                break;
+            }
+            seen = gen_.load(std::memory_order_acquire);
+            (*fn_)(i);
+            pending_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+
+  public:
+    static constexpr int kMaxThreads = 16;
+
+  private:
+    int n_ = 1;
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> pending_{0};
+    const std::function<void(int)> *fn_ = nullptr;
+};
+
+// One helper's share of a parallel plan: its source chunk's lost list, then
+// its systems in its own arrays (capacity kept from call to call).
+struct SwPart {
+    std::vector<uint64_t> lost;
+    std::vector<SwComp> comps;
+    std::vector<uint64_t> unk, eqr;
+    std::vector<uint32_t> eqc;
+    std::vector<fecgpu_sw_repair> eqh;
+    SwPlan out;
+    size_t lo = 0, hi = 0;  // range of the global lost list whose systems this part plans
+};
+
+constexpr uint64_t kSwParallelSources = 1u << 16;  // below this the plan runs on the caller alone
+
+// Statuses, lost list, staging and systems of one decode.  Returns the number
+// of lost sources (P.lost), or a negative error; P's arrays point into the
+// staging block host(bytes, &p) returns (the ctx's pinned block) at layout L
+// (not requested when nothing is lost).  threads: 0 = the pool's size.
+template <class HostBlock>
+ssize_t sw_plan(HostBlock &&host, const uint8_t *src_present, uint64_t nsrc, uint8_t *src_status,
+                const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep, uint64_t wmax,
+                SwPlan &P, SwLayout &L, int threads = 0) {
+    auto bind = [&](void *ph) {
+        uint8_t *meta = static_cast<uint8_t *>(ph);
+        P.comps = reinterpret_cast<SwComp *>(meta);
+        P.unk = reinterpret_cast<uint64_t *>(meta + L.o_unk);
+        P.eqr = reinterpret_cast<uint64_t *>(meta + L.o_eqr);
+        P.eqc = reinterpret_cast<uint32_t *>(meta + L.o_eqc);
+        P.eqh = reinterpret_cast<fecgpu_sw_repair *>(meta + L.o_eqh);
+        P.ustat = meta + L.o_ust;
+    };
+    PlanPool &pool = PlanPool::get();
+    const int n = threads > 0 ? std::min(threads, pool.size()) : pool.size();
+    std::unique_lock<std::mutex> held;
+    if (n > 1 && nsrc >= kSwParallelSources) held = pool.acquire();
+    const bool par = held.owns_lock();
+    static SwPart parts[PlanPool::kMaxThreads];  // used while the pool is held only
+    if (par) {
+        pool.run([&](int i) {
+            if (i >= n) return;  // a smaller share than the pool
+            const uint64_t lo = (nsrc * (uint64_t)i / n) & ~7ull;
+            const uint64_t hi = i + 1 == n ? nsrc : (nsrc * (uint64_t)(i + 1) / n) & ~7ull;
+            parts[i].lost.clear();
+            sw_scan_lost(src_present, lo, hi, src_status, parts[i].lost);
+        });
+        for (int i = 0; i < n; i++) P.lost.insert(P.lost.end(), parts[i].lost.begin(), parts[i].lost.end());
+    } else {
+        sw_scan_lost(src_present, 0, nsrc, src_status, P.lost);
+    }
+    const uint64_t nlost = P.lost.size();
+    if (nlost == 0 || nrep == 0) return (ssize_t)nlost;
+    L = sw_plan_layout(nlost, nrep);
+    void *ph = nullptr;
+    RC_TRY(host(L.host, &ph));
+    bind(ph);
+    const uint64_t *lost = P.lost.data();
+    if (!par || nlost < 1024) {
+        sw_sweep(lost, nlost, rep_present, hdr, nrep, wmax, P);
+        return (ssize_t)nlost;
+    }
+    pool.run([&](int i) {
+        if (i >= n) return;  // a smaller share than the pool
+        // this part's systems: from the first system start at or after its
+        // nominal share of the lost list to the next part's
+        auto start_at = [&](int j) {
+            if (j >= n) return (size_t)nlost;
+            size_t x = (size_t)(nlost * (uint64_t)j / n);
+            while (x < nlost && !sw_system_start(lost, x, rep_present, hdr, nrep, wmax)) x++;
+            return x;
+        };
+        SwPart &q = parts[i];
+        q.lo = start_at(i);
+        q.hi = std::max(q.lo, start_at(i + 1));
+        const size_t nl = q.hi - q.lo;
+        uint64_t ne = 0;  // bound on equations: repairs with fss in [lost[lo] - wmax + 1, lost[hi - 1]]
+        if (nl) {
+            const uint64_t a = lost[q.lo], b = lost[q.hi - 1];
+            ne = sw_first_repair(hdr, nrep, b + 1) - sw_first_repair(hdr, nrep, a >= wmax ? a - wmax + 1 : 0);
+        }
+        if (q.comps.size() < nl) q.comps.resize(nl);
+        if (q.unk.size() < nl) q.unk.resize(nl);
+        if (q.eqr.size() < ne) {
+            q.eqr.resize(ne);
+            q.eqc.resize(ne);
+            q.eqh.resize(ne);
+        }
+        q.out = SwPlan{};
+        q.out.comps = q.comps.data();
+        q.out.unk = q.unk.data();
+        q.out.eqr = q.eqr.data();
+        q.out.eqc = q.eqc.data();
+        q.out.eqh = q.eqh.data();
+        sw_sweep(lost + q.lo, nl, rep_present, hdr, nrep, wmax, q.out);
+    });
+    // concatenate the parts in order, rebasing their offsets
+    struct Base { uint64_t comp, unk, eq, amat, nsolve, tcoef; };
+    Base base[PlanPool::kMaxThreads];
+    Base acc{0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < n; i++) {
+        const SwPlan &o = parts[i].out;
+        base[i] = acc;
+        acc.comp += o.ncomp;
+        acc.unk += o.nunk;
+        acc.eq += o.neq;
+        acc.amat += o.amat;
+        acc.nsolve += o.nsolve;
+        acc.tcoef += o.tcoef;
+        P.max_nss = std::max(P.max_nss, o.max_nss);
+        P.max_p = std::max(P.max_p, o.max_p);
+    }
+    P.ncomp = acc.comp;
+    P.nunk = acc.unk;
+    P.neq = acc.eq;
+    P.amat = acc.amat;
+    P.nsolve = acc.nsolve;
+    P.tcoef = acc.tcoef;
+    pool.run([&](int i) {
+        if (i >= n) return;  // a smaller share than the pool
+        const SwPlan &o = parts[i].out;
+        const Base &b = base[i];
+        for (uint64_t j = 0; j < o.ncomp; j++) {
+            SwComp c = o.comps[j];
+            c.u_off += b.unk;
+            c.o_off += b.unk;
+            c.q_off += b.eq;
+            c.a_off += b.amat;
+            c.j_off += b.nsolve;
+            c.t_off += b.tcoef;
+            P.comps[b.comp + j] = c;
+        }
+        std::memcpy(P.unk + b.unk, o.unk, o.nunk * 8);
+        std::memcpy(P.eqr + b.eq, o.eqr, o.neq * 8);
+        std::memcpy(P.eqh + b.eq, o.eqh, o.neq * sizeof(fecgpu_sw_repair));
+        for (uint64_t j = 0; j < o.neq; j++) P.eqc[b.eq + j] = o.eqc[j] + (uint32_t)b.comp;
+    });
+    return (ssize_t)nlost;
 }
 
 // Device part of a decode: src / rep device pointers, plan P in the pinned
@@ -405,19 +631,10 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
         wmax = std::max<uint64_t>(wmax, hdr[t].nss);
     }
     SwPlan &P = sw_plan_scratch();
-    const uint64_t nlost = sw_scan_lost(src_present, nsrc, src_status, P.lost);
-    if (nlost == 0 || nrep == 0) return 0;
-    const SwLayout L = sw_plan_layout(nlost, nrep);
-    void *ph = nullptr;
-    RC_TRY(ctx_sw_host(ctx, L.host, &ph));
-    uint8_t *meta = static_cast<uint8_t *>(ph);
-    P.comps = reinterpret_cast<SwComp *>(meta);
-    P.unk = reinterpret_cast<uint64_t *>(meta + L.o_unk);
-    P.eqr = reinterpret_cast<uint64_t *>(meta + L.o_eqr);
-    P.eqc = reinterpret_cast<uint32_t *>(meta + L.o_eqc);
-    P.eqh = reinterpret_cast<fecgpu_sw_repair *>(meta + L.o_eqh);
-    P.ustat = meta + L.o_ust;
-    sw_build_plan(rep_present, hdr, nrep, wmax, P);
+    SwLayout L{};
+    const ssize_t nlost = sw_plan([ctx](size_t bytes, void **p) { return ctx_sw_host(ctx, bytes, p); }, src_present,
+                                  nsrc, src_status, rep_present, hdr, nrep, wmax, P, L);
+    if (nlost <= 0 || nrep == 0) return nlost < 0 ? nlost : 0;
     if (P.ncomp == 0) return 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     RC_TRY(ctx_sw_begin(ctx, s));

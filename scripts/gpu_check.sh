@@ -48,6 +48,14 @@ for s in "$@"; do
         prof2) step prof2 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof2 -o run -- \
                    python bench.py ;;  # the driver's default command, as is
         prof5) prof prof5 5 ;;
+        prof7) prof prof7 7 ;;
+        swplan) step swplan 120 ./scripts/sw_plan_probe ;;  # host-only: the decode plan's phases
+        abplan)  # cfg7: decode host plan on the caller alone vs the helper pool, interleaved twice
+            for rep in 1 2; do
+                FECGPU_PLAN_THREADS=1 step abplan_t1_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
+                step abplan_t4_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
+                FECGPU_PLAN_THREADS=8 step abplan_t8_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
+            done ;;
         prof3) prof prof3 3 ;;
         prof4) prof prof4 4 ;;
         prof4rlc) prof prof4rlc 4 --matrix rlc ;;
