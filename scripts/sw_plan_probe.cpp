@@ -4,7 +4,7 @@
 // plan (status/lost scan + sweep) on the caller alone and on the helper pool,
 // whose output must equal the serial plan's array for array.  Compiles the
 // library's own fec_sw.cpp into the probe (its helpers are file-local); no
-// GPU call.  Median of 50 runs.
+// GPU call.  Median of 50 runs (argv: [threads [runs]]).
 #include "../quic-fec-eps_amd/csrc/fec_sw.cpp"
 
 #include <chrono>
@@ -36,6 +36,7 @@ int main(int argc, char **argv) {
         hdr[t] = fecgpu_sw_repair{fss, (uint16_t)(end - fss), (uint16_t)(t & 0xffff), 15, {0, 0, 0}};
     }
     const int threads = argc > 1 ? std::atoi(argv[1]) : 0;
+    const int reps = argc > 2 ? std::max(1, std::atoi(argv[2])) : 50;
     std::vector<uint8_t> pin;
     auto host = [&](size_t bytes, void **p) -> ssize_t {
         if (pin.size() < bytes) pin.resize(bytes);
@@ -56,7 +57,7 @@ int main(int argc, char **argv) {
         std::vector<double> th, t1s, tps;
         Copy ref{}, got{};
         uint64_t nlost = 0, ncomp = 0, neq = 0;
-        for (int rep = 0; rep < 50; rep++) {
+        for (int rep = 0; rep < reps; rep++) {
             const auto t0 = clk::now();
             uint64_t wmax = 1, prev = 0;
             for (uint64_t t = 0; t < nrep; t++) {
