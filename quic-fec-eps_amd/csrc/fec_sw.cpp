@@ -34,7 +34,10 @@ namespace {
         if (r_ < 0) return r_;     \
     } while (0)
 
-constexpr uint32_t kCombBudget = 40u << 10;  // LDS of one combine workgroup's job tables
+#ifndef FECGPU_COMB_BUDGET_KB
+#define FECGPU_COMB_BUDGET_KB 40
+#endif
+constexpr uint32_t kCombBudget = FECGPU_COMB_BUDGET_KB << 10;  // LDS of one combine workgroup's job tables
 constexpr int kSwSolveOut = 8;               // recovered sources per solve job
 
 ssize_t check_geometry(uint32_t sym_len, uint32_t stride, const void *a, const void *b) {
