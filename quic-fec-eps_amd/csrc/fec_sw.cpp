@@ -34,10 +34,20 @@ namespace {
         if (r_ < 0) return r_;     \
     } while (0)
 
+// LDS of one combine workgroup's job tables.  Jobs of >= 64 columns (a wave's
+// worth) get the smaller budget: fewer jobs per workgroup (3 at S = 1200 B,
+// W 32 step 8 groups of 4: one pass at 0.88 lane use) and more workgroups per
+// CU.  cfg7 encode 0.249 -> 0.229 ms against 40 KB (7 jobs, 2 passes), 64 KB
+// 0.282 ms, 96 KB 0.513 ms (profiles/r02_comb_budget_ab.txt).  Narrow jobs
+// keep the larger budget, which packs more of them per pass.
 #ifndef FECGPU_COMB_BUDGET_KB
 #define FECGPU_COMB_BUDGET_KB 40
 #endif
-constexpr uint32_t kCombBudget = FECGPU_COMB_BUDGET_KB << 10;  // LDS of one combine workgroup's job tables
+#ifndef FECGPU_COMB_BUDGET_WIDE_KB
+#define FECGPU_COMB_BUDGET_WIDE_KB 20
+#endif
+constexpr uint32_t kCombBudget = FECGPU_COMB_BUDGET_KB << 10;
+constexpr uint32_t kCombBudgetWide = FECGPU_COMB_BUDGET_WIDE_KB << 10;
 constexpr int kSwSolveOut = 8;               // recovered sources per solve job
 
 ssize_t check_geometry(uint32_t sym_len, uint32_t stride, const void *a, const void *b) {
@@ -75,7 +85,8 @@ ssize_t run_comb(const CombJob *jobs, uint64_t njobs, const uint8_t *coef, const
     a.nout_max = R;
     a.job_lds = comb_job_lds(a.nin_max, R);
     // groups of 8 have 8-output tables over a wider span: a larger share of the CU's LDS
-    const uint32_t budget = skip && R == 8 ? kCombBudget * 2 : kCombBudget;
+    const uint32_t base = a.ncol >= 64 ? kCombBudgetWide : kCombBudget;
+    const uint32_t budget = skip && R == 8 ? base * 2 : base;
     a.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(a.ncol, a.job_lds, budget)));
     SW_TRY(launch_comb(a, R, s), "sliding-window combine launch");
     return 0;
