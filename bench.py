@@ -67,6 +67,8 @@ def parse():
                     help="tuning: bit-sliced encode on per-window lengths, 256-unit passes per window group")
     ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
     ap.add_argument("--bpc", type=int, default=0, help="tuning: persistent workgroups per CU")
+    ap.add_argument("--sw-group", type=int, default=0, choices=[0, 1, 2, 4, 8],
+                    help="tuning (config 7): sliding-window repairs per combine job (0 = library default)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1: nccl (= RCCL, one rank per GPU) or gloo (rehearsal: ranks may "
                          "share a GPU; the reductions run on the host)")
@@ -260,6 +262,8 @@ def main():
         ctx.set_tuning("wpb", args.wpb)
     if args.bpc:
         ctx.set_tuning("blocks_per_cu", args.bpc)
+    if args.sw_group:
+        ctx.set_tuning("sw_group", args.sw_group)
     if args.host_direct >= 0:
         ctx.set_tuning("host_direct", args.host_direct)
     if args.host_chunk_mb:

@@ -49,7 +49,13 @@ for s in "$@"; do
                    python bench.py ;;  # the driver's default command, as is
         prof5) prof prof5 5 ;;
         prof7) prof prof7 7 ;;
-        swplan) step swplan 120 ./scripts/sw_plan_probe ;;  # host-only: the decode plan's phases
+        swplan) step swplan 120 ./scripts/sw_plan_probe ;;
+        abgroup)  # cfg7: sliding-window repairs per combine job, interleaved twice
+            for rep in 1 2; do
+                for gsz in 2 4 8; do
+                    step abgroup_g${gsz}_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify --sw-group $gsz
+                done
+            done ;;  # host-only: the decode plan's phases
         abplan)  # cfg7: decode host plan on the caller alone vs the helper pool, interleaved twice
             for rep in 1 2; do
                 FECGPU_PLAN_THREADS=1 step abplan_t1_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
