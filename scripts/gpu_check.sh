@@ -50,6 +50,15 @@ for s in "$@"; do
         prof5) prof prof5 5 ;;
         prof7) prof prof7 7 ;;
         swplan) step swplan 120 ./scripts/sw_plan_probe ;;
+        abvar7)  # cfg7: default build vs every lib/libfecgpu_*.so variant (no check build), interleaved 3 times
+            for rep in 1 2 3; do
+                step abvar7_base_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
+                for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
+                    n=$(basename $v .so); n=${n#libfecgpu_}
+                    [ "$n" = check ] && continue
+                    FECGPU_LIB=$v step abvar7_${n}_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
+                done
+            done ;;
         abgroup)  # cfg7: sliding-window repairs per combine job, interleaved twice
             for rep in 1 2; do
                 for gsz in 2 4 8; do
