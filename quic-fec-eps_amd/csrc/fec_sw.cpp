@@ -398,15 +398,14 @@ struct SwPart {
 
 constexpr uint64_t kSwParallelSources = 1u << 16;  // below this the plan runs on the caller alone
 
-// Header checks (FECGPU_ERR_INVALID_ARG before anything is written), statuses,
-// lost list, staging and systems of one decode.  Returns the number
+// Statuses, lost list, staging and systems of one decode.  Returns the number
 // of lost sources (P.lost), or a negative error; P's arrays point into the
 // staging block host(bytes, &p) returns (the ctx's pinned block) at layout L
 // (not requested when nothing is lost).  threads: 0 = the pool's size.
 template <class HostBlock>
 ssize_t sw_plan(HostBlock &&host, const uint8_t *src_present, uint64_t nsrc, uint8_t *src_status,
-                const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep, SwPlan &P,
-                SwLayout &L, int threads = 0) {
+                const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep, uint64_t wmax,
+                SwPlan &P, SwLayout &L, int threads = 0) {
     auto bind = [&](void *ph) {
         uint8_t *meta = static_cast<uint8_t *>(ph);
         P.comps = reinterpret_cast<SwComp *>(meta);
@@ -422,30 +421,6 @@ ssize_t sw_plan(HostBlock &&host, const uint8_t *src_present, uint64_t nsrc, uin
     if (n > 1 && nsrc >= kSwParallelSources) held = pool.acquire();
     const bool par = held.owns_lock();
     static SwPart parts[PlanPool::kMaxThreads];  // used while the pool is held only
-    // headers: each valid, fss nondecreasing; wmax = the longest window
-    auto check = [&](uint64_t lo, uint64_t hi, uint64_t &wm) {
-        for (uint64_t t = lo; t < hi; t++) {
-            if (!header_ok(hdr[t], nsrc) || (t && hdr[t].fss < hdr[t - 1].fss)) return false;
-            wm = std::max<uint64_t>(wm, hdr[t].nss);
-        }
-        return true;
-    };
-    uint64_t wmax = 1;
-    if (par) {
-        uint64_t wm[PlanPool::kMaxThreads];
-        bool ok[PlanPool::kMaxThreads];
-        pool.run([&](int i) {
-            if (i >= n) return;  // a smaller share than the pool
-            wm[i] = 1;
-            ok[i] = check(nrep * (uint64_t)i / n, nrep * (uint64_t)(i + 1) / n, wm[i]);
-        });
-        for (int i = 0; i < n; i++) {
-            if (!ok[i]) return FECGPU_ERR_INVALID_ARG;
-            wmax = std::max(wmax, wm[i]);
-        }
-    } else if (!check(0, nrep, wmax)) {
-        return FECGPU_ERR_INVALID_ARG;
-    }
     if (par) {
         pool.run([&](int i) {
             if (i >= n) return;  // a smaller share than the pool
@@ -662,10 +637,17 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
     if (!ctx || !src || !src_present || !src_status || nsrc == 0) return FECGPU_ERR_INVALID_ARG;
     if (nrep && (!rep || !rep_present || !hdr)) return FECGPU_ERR_INVALID_ARG;
     RC_TRY(check_geometry(sym_len, stride, src, nrep ? rep : src));
+    uint64_t wmax = 1, prev_fss = 0;
+    for (uint64_t t = 0; t < nrep; t++) {
+        if (!header_ok(hdr[t], nsrc)) return FECGPU_ERR_INVALID_ARG;
+        if (hdr[t].fss < prev_fss) return FECGPU_ERR_INVALID_ARG;  // fss nondecreasing
+        prev_fss = hdr[t].fss;
+        wmax = std::max<uint64_t>(wmax, hdr[t].nss);
+    }
     SwPlan &P = sw_plan_scratch();
     SwLayout L{};
     const ssize_t nlost = sw_plan([ctx](size_t bytes, void **p) { return ctx_sw_host(ctx, bytes, p); }, src_present,
-                                  nsrc, src_status, rep_present, hdr, nrep, P, L);
+                                  nsrc, src_status, rep_present, hdr, nrep, wmax, P, L);
     if (nlost <= 0 || nrep == 0) return nlost < 0 ? nlost : 0;
     if (P.ncomp == 0) return 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);

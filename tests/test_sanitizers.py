@@ -53,5 +53,4 @@ def test_sw_plan_pool_equals_serial_under_tsan(tmp_path):
     r = subprocess.run([str(exe), "4", "3"], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert r.stdout.count('"equal": true') == 3, r.stdout
-    assert '"invalid_headers_refused": true' in r.stdout, r.stdout
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
