@@ -2054,8 +2054,16 @@ __device__ __forceinline__ void comb_dispatch(int nw, const uint8_t *in, uint32_
     }
 }
 
+#ifndef FECGPU_COMB_MINW
+#define FECGPU_COMB_MINW 0  // >0: the grouped encode's combine (R = 4) asks for this many waves per SIMD
+#endif
+#if FECGPU_COMB_MINW > 0
+#define COMB_WAVES __attribute__((amdgpu_waves_per_eu(R == 4 ? FECGPU_COMB_MINW : 1, 8)))
+#else
+#define COMB_WAVES
+#endif
 template <int R>
-__global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
+__global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
     extern __shared__ uint4 dyn[];
     __shared__ uint32_t s_pfx[kMaxWpb + 1];
     __shared__ uint64_t s_in[kMaxWpb];
