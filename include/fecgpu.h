@@ -47,9 +47,12 @@
 extern "C" {
 #endif
 
-#define FECGPU_ABI_VERSION 3  /* 2: REPAIR frames carry nsrc; decoder limits / recovered queue;
+#define FECGPU_ABI_VERSION 4  /* 2: REPAIR frames carry nsrc; decoder limits / recovered queue;
                                  3: fecgpu_code.rlc_key / rlc_dt, FECGPU_MATRIX_RLC, sliding-window
-                                    RLC (fecgpu_sw_*, SW frames, fecgpu_frame.key / dt) */
+                                    RLC (fecgpu_sw_*, SW frames, fecgpu_frame.key / dt);
+                                 4: the nsrc-carrying REPAIR frame has its own type 0xfec4 (ABI 1's
+                                    0xfec1 layout had no nsrc and is rejected, never misparsed);
+                                    sliding-window decode without a system-size cap */
 
 /* errors (mirror quiche's QUICHE_ERR_DONE = -1, QUICHE_ERR_BUFFER_TOO_SHORT = -2 style) */
 enum fecgpu_error {
@@ -289,7 +292,7 @@ ssize_t fecgpu_decoder_tick(fecgpu_decoder *dec, uint64_t now_us);
  * nsrc = real sources of the window (fecgpu_encoder_window_sources), 1..k.
  * Frame types sit in QUIC's extension space.  Host-only, no device calls. */
 #define FECGPU_FRAME_SOURCE_ID 0xfec0u
-#define FECGPU_FRAME_REPAIR 0xfec1u
+#define FECGPU_FRAME_REPAIR 0xfec4u /* 0xfec1 = the ABI-1 REPAIR without nsrc: not accepted */
 /* sliding-window code (RFC 8681 FEC payload IDs):
  *   SW_SOURCE: type | esi                                  (next to a source payload)
  *   SW_REPAIR: type | fss | nss | repair_key | dt | length | symbol bytes */
@@ -446,7 +449,8 @@ ssize_t fecgpu_sw_decoder_new(fecgpu_ctx *ctx, const fecgpu_sw_params *p, fecgpu
 void    fecgpu_sw_decoder_free(fecgpu_sw_decoder *dec);
 ssize_t fecgpu_sw_decoder_add_source(fecgpu_sw_decoder *dec, uint64_t esi, const uint8_t *pkt,
                                      size_t len);
-/* hdr->fss absolute; sym: E bytes */
+/* hdr->fss absolute; sym: E bytes.  INVALID_ARG (nothing changed) for a window
+ * longer than the session's `window`; DONE if it starts behind the kept span. */
 ssize_t fecgpu_sw_decoder_add_repair(fecgpu_sw_decoder *dec, const fecgpu_sw_repair *hdr,
                                      const uint8_t *sym, size_t len);
 /* Decode now; returns the number of sources recovered (also queued for

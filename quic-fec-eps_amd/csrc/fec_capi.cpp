@@ -162,6 +162,9 @@ struct fecgpu_ctx {
     // FECGPU_CHECK builds: bytes taken off the end of every checked range, so a
     // test can see the checker fire on a correct kernel ("check_shrink")
     int check_shrink = 0;
+    // fault injection for tests ("fault_launches"): the next N launches of the
+    // sliding-window encoder objects fail with FECGPU_ERR_DEVICE, launching nothing
+    int fault_launches = 0;
     // sliding-window calls: device scratch slots and the last call's end event, per device
     std::map<int, std::vector<std::pair<void *, size_t>>> sw_scratch;
     std::map<int, hipEvent_t> sw_event;
@@ -276,6 +279,12 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         if (!FECGPU_CHECK) return FECGPU_ERR_UNSUPPORTED;  // release build: nothing is checked
         if (value < 0 || value > (1 << 20)) return FECGPU_ERR_INVALID_ARG;
         ctx->check_shrink = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "fault_launches")) {
+        if (value < 0 || value > (1 << 20)) return FECGPU_ERR_INVALID_ARG;
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ctx->fault_launches = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "bs_passes")) {
@@ -1021,6 +1030,14 @@ int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget) {
 }
 
 int ctx_sw_group(const fecgpu_ctx *ctx) { return ctx->sw_group; }
+
+bool ctx_fault_take(fecgpu_ctx *ctx) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->fault_launches <= 0) return false;
+    ctx->fault_launches--;
+    g_last_error = "injected launch fault (tuning \"fault_launches\")";
+    return true;
+}
 
 ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p) {
     int dev = 0;

@@ -285,6 +285,9 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
                        const fecgpu_sw_repair *hdr_host = nullptr);
 // the ctx's "sw_group" tuning (repairs per sliding-window encode job)
 int ctx_sw_group(const fecgpu_ctx *ctx);
+// tests: true (and the thread's error text set) while the ctx's "fault_launches"
+// count lasts, consuming one
+bool ctx_fault_take(fecgpu_ctx *ctx);
 int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget);
 ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p);
 // the ctx's pinned host staging block for sliding-window decodes (grown on

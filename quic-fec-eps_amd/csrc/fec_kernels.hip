@@ -937,6 +937,11 @@ typedef const uint32_t *cmask;
     "v_bitop3_b32 %[a" #Q "], %[u], %[a" #Q "], %[" #T "] bitop3:0x96\n\t" \
     "s_set_gpr_idx_on %[d" #Q "], gpr_idx(SRC0)\n\t"
 #endif
+// M0 is a reserved register: clang warns that declaring it clobbered is not a
+// promise it will be preserved, but the declaration still puts an implicit def
+// of M0 on the asm, so no M0 def/use pair of the compiler's is scheduled across it
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void pick4(uint32_t &a0, uint32_t &a1, uint32_t &a2, uint32_t &a3,
                                       const uint32_t (&d)[4], const uint32_t (&e)[4], const uint32_t (&lo)[16],
                                       const uint32_t (&hi)[16]) {
@@ -959,8 +964,10 @@ __device__ __forceinline__ void pick4(uint32_t &a0, uint32_t &a1, uint32_t &a2, 
           RBS_IN(hi, 0, 48), RBS_IN(hi, 1, 49), RBS_IN(hi, 2, 50), RBS_IN(hi, 3, 51),
           RBS_IN(hi, 4, 52), RBS_IN(hi, 5, 53), RBS_IN(hi, 6, 54), RBS_IN(hi, 7, 55),
           RBS_IN(hi, 8, 56), RBS_IN(hi, 9, 57), RBS_IN(hi, 10, 58), RBS_IN(hi, 11, 59),
-          RBS_IN(hi, 12, 60), RBS_IN(hi, 13, 61), RBS_IN(hi, 14, 62), RBS_IN(hi, 15, 63));
+          RBS_IN(hi, 12, 60), RBS_IN(hi, 13, 61), RBS_IN(hi, 14, 62), RBS_IN(hi, 15, 63)
+        : "m0", "scc");  // index mode writes M0; s_lshr (packed indices) writes SCC
 }
+#pragma clang diagnostic pop
 #undef RBS_IN
 #undef RBS_PLANE
 #undef RBS_HI
@@ -1072,6 +1079,9 @@ using rbs::cmask;
     "v_bitop3_b32 %[b" #Q1 "], v33, %[b" #Q1 "], v" #TB " bitop3:0x96\n\t"
 
 // planes q = 0..3 of one repair half: (a[q], b[q]) ^= lo[l[q]] ^ hi[h[q]]
+// (M0 declared clobbered as in rbs::pick4)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void pick4(uint32_t (&a)[4], uint32_t (&b)[4], const uint32_t (&l)[4],
                                       const uint32_t (&h)[4], const uint32_t (&lo)[32], const uint32_t (&hi)[32]) {
     uint32_t t;  // packed indices: the index shifted down
@@ -1116,8 +1126,9 @@ __device__ __forceinline__ void pick4(uint32_t (&a)[4], uint32_t (&b)[4], const 
           R4_IN(hi, 20, 84), R4_IN(hi, 21, 85), R4_IN(hi, 22, 86), R4_IN(hi, 23, 87),
           R4_IN(hi, 24, 88), R4_IN(hi, 25, 89), R4_IN(hi, 26, 90), R4_IN(hi, 27, 91),
           R4_IN(hi, 28, 92), R4_IN(hi, 29, 93), R4_IN(hi, 30, 94), R4_IN(hi, 31, 95)
-        : "v96", "v97", "v98", "v99");
+        : "v96", "v97", "v98", "v99", "m0", "scc");  // index mode writes M0, s_lshr SCC
 }
+#pragma clang diagnostic pop
 #undef R4_IN
 #undef R4_PAIR
 #undef R4_HI

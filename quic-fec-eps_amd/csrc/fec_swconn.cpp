@@ -110,7 +110,10 @@ struct fecgpu_sw_decoder {
 
 namespace {
 
-// Launches the scheduled repairs in a free slot (ERR_LIMIT: none free).
+// Launches up to `batch` scheduled repairs (the oldest) in a free slot
+// (ERR_LIMIT: none free).  On a failed launch nothing is consumed: the repairs
+// stay scheduled, the slot stays free (its kernels, if any ran, are waited for
+// first, so a retry never overlaps them).
 ssize_t enc_launch(fecgpu_sw_encoder *e) {
     if (e->sched.empty()) return 0;
     int k = -1;
@@ -118,21 +121,30 @@ ssize_t enc_launch(fecgpu_sw_encoder *e) {
         if (!e->slot[i].used) { k = i; break; }
     if (k < 0) return FECGPU_ERR_LIMIT;
     auto &S = e->slot[k];
-    S.n = e->sched.size();
-    S.popped = 0;
-    S.abs = e->sched;
-    for (size_t t = 0; t < S.n; t++) {
+    const size_t n = std::min<size_t>(e->sched.size(), e->p.batch);  // the slot's rows
+    for (size_t t = 0; t < n; t++) {
         S.hdr[t] = e->sched[t];
         S.hdr[t].fss -= e->base;
     }
-    const ssize_t rc = sw_encode_core(e->src, e->cap, S.rep, S.hdr, S.n, e->p.window, e->p.symbol_size, e->stride,
+    ssize_t rc = ctx_fault_take(e->ctx)
+                     ? (ssize_t)FECGPU_ERR_DEVICE
+                     : sw_encode_core(e->src, e->cap, S.rep, S.hdr, n, e->p.window, e->p.symbol_size, e->stride,
                                       S.jobs, S.coef, S.outs, e->s, e->group, S.hdr);
-    if (rc < 0) return rc;
-    SWC_TRY(hipEventRecord(S.ev, e->s), "hipEventRecord");
+    if (rc >= 0) {
+        const hipError_t er = hipEventRecord(S.ev, e->s);
+        if (er != hipSuccess) rc = set_dev_error(er, "hipEventRecord");
+    }
+    if (rc < 0) {
+        (void)hipStreamSynchronize(e->s);
+        return rc;
+    }
+    S.n = n;
+    S.popped = 0;
+    S.abs.assign(e->sched.begin(), e->sched.begin() + n);
     S.used = true;
     e->order.push_back(k);
-    e->sched.clear();
-    return (ssize_t)S.n;
+    e->sched.erase(e->sched.begin(), e->sched.begin() + n);
+    return (ssize_t)n;
 }
 
 // Room for the next source: move the rows still needed to the front.
@@ -251,6 +263,13 @@ ssize_t fecgpu_sw_encoder_add_source(fecgpu_sw_encoder *e, const uint8_t *pkt, s
     if (e->p.framing == FECGPU_FRAMING_LENPREFIX ? len + 2 > e->p.symbol_size : len != e->p.symbol_size)
         return FECGPU_ERR_BUFFER_TOO_SHORT;
     const bool schedules = (e->next + 1) % e->p.step == 0;
+    if (schedules && e->sched.size() >= e->p.batch) {
+        // a full batch left behind by a failed launch: it goes first (or the
+        // call fails with nothing consumed), so a slot never takes more than batch
+        if (!enc_slot_free(e)) return FECGPU_ERR_LIMIT;
+        const ssize_t rc = enc_launch(e);
+        if (rc < 0) return rc;
+    }
     if (schedules && e->sched.size() + 1 >= e->p.batch && !enc_slot_free(e)) return FECGPU_ERR_LIMIT;
     if (e->next == e->base + e->cap) {
         const ssize_t rc = enc_compact(e);
@@ -267,17 +286,17 @@ ssize_t fecgpu_sw_encoder_add_source(fecgpu_sw_encoder *e, const uint8_t *pkt, s
         h.key = (uint16_t)(e->key++ & 0xFFFF);
         h.dt = e->p.dt;
         e->sched.push_back(h);
-        if (e->sched.size() >= e->p.batch) {
-            const ssize_t rc = enc_launch(e);
-            if (rc < 0) return rc;
-        }
+        // the source is stored and its repair scheduled: a failed launch leaves
+        // the batch scheduled, and the next call that schedules (or a flush)
+        // launches it first or fails with nothing consumed
+        if (e->sched.size() >= e->p.batch) (void)enc_launch(e);
     }
     return 0;
 }
 
 ssize_t fecgpu_sw_encoder_flush(fecgpu_sw_encoder *e) {
     if (!e) return FECGPU_ERR_INVALID_ARG;
-    if (enc_slot_free(e)) {  // else the scheduled repairs wait for a slot (read repairs first)
+    while (!e->sched.empty() && enc_slot_free(e)) {  // else the rest waits for a slot (read repairs first)
         const ssize_t rc = enc_launch(e);
         if (rc < 0) return rc;
     }
@@ -362,10 +381,13 @@ ssize_t fecgpu_sw_decoder_add_repair(fecgpu_sw_decoder *d, const fecgpu_sw_repai
                                      size_t len) {
     if (!d || !h || !sym || h->nss == 0 || h->nss > FECGPU_SW_MAX_WINDOW || h->dt > 15 || h->fss >= (1ull << 62))
         return FECGPU_ERR_INVALID_ARG;
+    // a window longer than the session's W is malformed: rejected before it can
+    // move the span (advancing first would give up every buffered source)
+    if (h->nss > d->p.window) return FECGPU_ERR_INVALID_ARG;
     if (len != d->p.symbol_size) return FECGPU_ERR_BUFFER_TOO_SHORT;
     if (h->fss < d->base) return FECGPU_ERR_DONE;  // its window reaches behind the kept span
+    // nss <= W <= cap / 2, so after the advance the whole window is inside the span
     if (h->fss + h->nss > d->base + d->cap) dec_advance(d, h->fss + h->nss - 1);
-    if (h->fss < d->base) return FECGPU_ERR_DONE;
     if (d->nrep == d->rcap) {
         dec_drop_old(d);
         if (d->nrep == d->rcap) {  // still full: the oldest repair goes

@@ -69,7 +69,7 @@ FRAME_SW_SOURCE, FRAME_SW_REPAIR = 0xFEC2, 0xFEC3
 SW_MAX_WINDOW, SW_MAX_UNKNOWNS, SW_MAX_EQUATIONS = 255, 64, 96
 # fecgpu_sw_repair as a numpy dtype (16 bytes, the C layout)
 SW_REPAIR_DTYPE = [("fss", "<u8"), ("nss", "<u2"), ("key", "<u2"), ("dt", "u1"), ("reserved", "u1", (3,))]
-FRAME_SOURCE_ID, FRAME_REPAIR = 0xFEC0, 0xFEC1
+FRAME_SOURCE_ID, FRAME_REPAIR = 0xFEC0, 0xFEC4
 
 
 class FecError(RuntimeError):

@@ -48,6 +48,16 @@ def test_repair_nsrc_round_trip(nsrc):
     assert b[4:6] == bytes([0x40, 77]) and b[6:11] == bytes([32, 8, nsrc, 2, 3])
 
 
+def test_abi1_repair_type_rejected():
+    """the nsrc-carrying REPAIR layout has its own type (0xfec4); a
+    frame of ABI 1's type 0xfec1 (no nsrc field) is rejected, never misparsed."""
+    good = fecgpu.frame_repair(5, 16, 4, 1, b"xyz")
+    assert good[:4] == bytes([0x80, 0x00, 0xFE, 0xC4])  # 4-byte varint type
+    with pytest.raises(fecgpu.FecError) as e:
+        fecgpu.frame_parse(bytes([0x80, 0x00, 0xFE, 0xC1]) + good[4:])
+    assert e.value.code == fecgpu.ERR_INVALID_ARG
+
+
 @pytest.mark.parametrize("nsrc", [0, 33])
 def test_repair_nsrc_out_of_range(nsrc):
     with pytest.raises(fecgpu.FecError) as e:

@@ -104,6 +104,54 @@ def test_sw_encoder_limit_until_repairs_are_read(ctx):
     enc.close()
 
 
+def test_sw_encoder_survives_failed_launches(ctx):
+    """a failed launch must not let the scheduled list grow
+    past `batch` (it would overrun the slot's rows).  Launches fail by fault
+    injection; the source that scheduled the failed batch is kept, the next
+    scheduling call retries the batch first and fails with nothing consumed, and
+    once launches work again every repair equals the oracle's."""
+    E, W, step, batch, n = 64, 8, 2, 4, 120
+    rng = np.random.default_rng(3)
+    pk = packets(rng, n, E, "fixed")
+    enc = fecgpu.SwEncoder(ctx, fecgpu.sw_params(E, W, step, batch=batch))
+    reps, i, failed = [], 0, 0
+    ctx.set_tuning("fault_launches", 5)
+    while i < n:
+        try:
+            assert enc.add_source(pk[i]) == i
+            i += 1
+        except fecgpu.FecError as e:  # the retried batch failed: nothing consumed
+            assert e.code == fecgpu.ERR_DEVICE
+            failed += 1
+        while (r := enc.next_repair()) is not None:
+            reps.append(r)
+    enc.flush()
+    while (r := enc.next_repair()) is not None:
+        reps.append(r)
+    assert failed == 4  # the first failure is the consuming call's own launch (not reported)
+    assert len(reps) == n // step
+    hdr = [h for h, _ in reps]
+    assert [h[2] for h in hdr] == list(range(n // step))
+    ref = O.sw_encode(frame(pk, E, "fixed"), hdr_array(hdr), E)
+    for t, (_, sym) in enumerate(reps):
+        assert sym == ref[t, :E].tobytes(), t
+    enc.close()
+
+
+def test_sw_decoder_rejects_overlong_window_before_advancing(ctx):
+    """a SW_REPAIR whose nss exceeds the session's window is
+    INVALID_ARG and leaves the buffered sources alone."""
+    E, W = 32, 8
+    dec = fecgpu.SwDecoder(ctx, fecgpu.sw_params(E, W, 2, framing="fixed", span=64))
+    for esi in range(10):
+        assert dec.add_source(esi, bytes([esi]) * E) == 0
+    with pytest.raises(fecgpu.FecError) as ei:
+        dec.add_repair((10_000, W + 1, 0, 15), b"z" * E)
+    assert ei.value.code == fecgpu.ERR_INVALID_ARG
+    assert all(dec.recovered(esi) == bytes([esi]) * E for esi in range(10))
+    dec.close()
+
+
 @pytest.mark.parametrize("E,W,step,framing,dt,batch,n", CASES[:3])
 @pytest.mark.parametrize("loss", [0.05, 0.15])
 def test_sw_frames_only_receiver_matches_oracle(ctx, E, W, step, framing, dt, batch, n, loss):
