@@ -128,6 +128,13 @@ int64_t orc_sw_decode(uint8_t *src, const uint8_t *src_present, uint64_t nsrc, c
                       const uint8_t *rep_present, const orc_sw_repair *hdr, uint64_t nrep,
                       uint32_t S, uint32_t stride, uint8_t *status);
 
+/* Same statuses and recovered bytes as orc_sw_decode, by banded elimination
+ * with no size limit (fec_sw_banded.c; the algorithm of the GPU's long-system
+ * path).  Returns #recovered. */
+int64_t orc_sw_decode_banded(uint8_t *src, const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep,
+                             const uint8_t *rep_present, const orc_sw_repair *hdr, uint64_t nrep,
+                             uint32_t S, uint32_t stride, uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

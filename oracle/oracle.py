@@ -58,6 +58,7 @@ def lib():
             "orc_rlc_coefs": (i32, [u32, i32, i32, vp]),
             "orc_sw_encode": (None, [vp, u64, u32, u32, vp, u64, vp]),
             "orc_sw_decode": (ctypes.c_int64, [vp, vp, u64, vp, vp, vp, u64, u32, u32, vp]),
+            "orc_sw_decode_banded": (ctypes.c_int64, [vp, vp, u64, vp, vp, vp, u64, u32, u32, vp]),
             "orc_sm64": (u64, [u64]),
             "orc_pkt_len": (u32, [i32, u64, u64, i32, i32, u32]),
             "orc_sym_len": (u32, [i32, u64, u64, i32, u32]),
@@ -150,6 +151,17 @@ def sw_decode(src: np.ndarray, src_present: np.ndarray, rep: np.ndarray, rep_pre
     st = np.zeros(nsrc, np.uint8)
     n = lib().orc_sw_decode(_p(src), _p(src_present), nsrc, _p(rep), _p(rep_present), _p(hdr),
                             len(hdr), S, stride, _p(st))
+    return st, int(n)
+
+
+def sw_decode_banded(src: np.ndarray, src_present: np.ndarray, rep: np.ndarray, rep_present: np.ndarray,
+                     hdr: np.ndarray, S: int):
+    """Same contract and results as sw_decode, by banded elimination (no size
+    limit; oracle/fec_sw_banded.c).  In place on src; -> (status, #recovered)."""
+    nsrc, stride = src.shape
+    st = np.zeros(nsrc, np.uint8)
+    n = lib().orc_sw_decode_banded(_p(src), _p(src_present), nsrc, _p(rep), _p(rep_present), _p(hdr),
+                                   len(hdr), S, stride, _p(st))
     return st, int(n)
 
 
