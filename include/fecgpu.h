@@ -140,7 +140,11 @@ void    fecgpu_host_free(void *p);
  * rows, r = 8, k in {16, 24, 32} — uses it, and of any other code with r >= 5
  * the runtime-mask bit-sliced kernel; 0: the table multiply for every code);
  * "sw_group" (sliding-window encode: consecutive repairs per combine job, each
- * source loaded once per group; 1, 2, 4 or 8, default 4);
+ * source loaded once per group; 1, 2, 4 or 8, default 4); "sw_long_min"
+ * (sliding-window decode: linked systems of at least this many lost sources
+ * take the banded long-system path, default 65 — systems of <= 64 lost
+ * sources and <= 96 repairs are solved by one wave each); "sw_log_entries"
+ * (the long-system operation log, default 8 x (sources + repairs));
  * "bs_passes" (bit-sliced encode on per-window lengths: 256-unit passes per
  * window group at the longest window, default 8); "conn_streams" (streams per
  * device shared round robin by the encoders / decoders created afterwards,
@@ -361,8 +365,6 @@ ssize_t fecgpu_digest_batch(fecgpu_ctx *ctx, const fecgpu_code *code, const uint
  * (repair_key, nss, dt) from the RFC 8682 TinyMT32 PRNG: the REPAIR frame of
  * RFC 8681 carries exactly these fields (repair_key, DT, NSS, FSS_ESI). */
 #define FECGPU_SW_MAX_WINDOW 255 /* nss limit (sources per encoding window) */
-#define FECGPU_SW_MAX_UNKNOWNS 64 /* decode: lost sources one linked system may hold */
-#define FECGPU_SW_MAX_EQUATIONS 96 /* decode: received repairs one linked system uses */
 
 typedef struct fecgpu_sw_repair {
     uint64_t fss;        /* first source of the encoding window (index into the batch) */
@@ -388,19 +390,31 @@ ssize_t fecgpu_sw_encode(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uin
  * src_present[i] / rep_present[t] nonzero = received, hdr[t] the repairs'
  * headers (fss nondecreasing), src_status[i] out: 0 = present or recovered,
  * 1 = still lost.  src / rep are device pointers (FECGPU_F_HOST_PTRS: host).
- * Lost sources are split into linked systems (two lost sources are linked
- * when a received repair's window holds both); each system is solved by
- * Gauss-Jordan with pivot search over its received repairs on the GPU, and
- * every lost source its repairs determine is recovered — also when the
- * system as a whole is rank deficient.  A system of more than
- * FECGPU_SW_MAX_UNKNOWNS lost sources stays lost (status 1); one with more
- * than FECGPU_SW_MAX_EQUATIONS received repairs uses the first ones (in
- * header order).  Synchronous on
- * `stream`; returns the number of sources recovered, or a negative error. */
+ * Every lost source that the received repairs determine is recovered — the
+ * result of one Gauss-Jordan elimination over all lost sources and all
+ * received repairs, also where that system is rank deficient — with no limit
+ * on how many lost sources the repairs link together.  The whole decode is
+ * planned and run on the GPU (the bookkeeping is copied up, the statuses
+ * down).  Synchronous on `stream`; returns the number of sources recovered,
+ * or a negative error (INVALID_ARG for a bad or unordered header; nothing is
+ * written then).  Nsrc and nrep < 2^32 - 256. */
 ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_present, uint64_t nsrc,
                          const uint8_t *rep, const uint8_t *rep_present,
                          const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t sym_len,
                          uint32_t stride, uint8_t *src_status, uint32_t flags, void *stream);
+/* The same decode with the receiver's bookkeeping on the device: src,
+ * src_present, rep, rep_present, hdr and src_status are all device pointers
+ * (FECGPU_F_HOST_PTRS is invalid).  Asynchronous on `stream` and returns 0,
+ * the statuses valid once the stream reaches the end of the call; with
+ * FECGPU_F_SYNC it waits and returns the number recovered, or INVALID_ARG if
+ * a header is bad or out of order (the kernels check them; then nothing is
+ * recovered and the statuses are the arrival flags).  A long linked system
+ * whose operation log does not fit the ctx's reservation is retried larger
+ * with FECGPU_F_SYNC, else it stays lost (tuning "sw_log_entries"). */
+ssize_t fecgpu_sw_decode_device(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_present, uint64_t nsrc,
+                                const uint8_t *rep, const uint8_t *rep_present,
+                                const struct fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t sym_len,
+                                uint32_t stride, uint8_t *src_status, uint32_t flags, void *stream);
 
 /* ---- sliding-window per-connection objects ----------------------------
  * The Connection's per-packet API for the sliding-window code (RFC 8681

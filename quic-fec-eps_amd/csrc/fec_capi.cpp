@@ -159,6 +159,9 @@ struct fecgpu_ctx {
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
     int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
+    int sw_long_min = kSwSmallE + 1;  // sliding-window decode: unknowns that force the long-system path
+    uint64_t sw_log_entries = 0;      // long-system operation log: fixed size (tuning), 0 = automatic
+    uint64_t sw_log_seen = 0;         // the largest log an overflow asked for on this ctx
     // FECGPU_CHECK builds: bytes taken off the end of every checked range, so a
     // test can see the checker fire on a correct kernel ("check_shrink")
     int check_shrink = 0;
@@ -312,6 +315,16 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
     if (!std::strcmp(key, "sw_group")) {
         if (value != 1 && value != 2 && value != 4 && value != 8) return FECGPU_ERR_INVALID_ARG;
         ctx->sw_group = (int)value;  // calls and objects created from now on
+        return 0;
+    }
+    if (!std::strcmp(key, "sw_long_min")) {
+        if (value < 1 || value > (1 << 30)) return FECGPU_ERR_INVALID_ARG;
+        ctx->sw_long_min = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "sw_log_entries")) {
+        if (value < 0 || value > (1ll << 34)) return FECGPU_ERR_INVALID_ARG;
+        ctx->sw_log_entries = (uint64_t)value;
         return 0;
     }
     if (!std::strcmp(key, "bitslice")) {
@@ -1030,6 +1043,20 @@ int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget) {
 }
 
 int ctx_sw_group(const fecgpu_ctx *ctx) { return ctx->sw_group; }
+
+int ctx_sw_long_min(const fecgpu_ctx *ctx) { return ctx->sw_long_min; }
+
+uint64_t ctx_sw_log_entries(const fecgpu_ctx *ctx, uint64_t nsrc, uint64_t nrep) {
+    if (ctx->sw_log_entries) return ctx->sw_log_entries;
+    // a long system needs 2 (p + e + sum of its equations' unknowns) entries;
+    // 8 per source and repair covers systems averaging ~3 unknowns per window
+    return std::max<uint64_t>({(uint64_t)1 << 16, 8 * (nsrc + nrep), ctx->sw_log_seen});
+}
+
+void ctx_sw_log_grow(fecgpu_ctx *ctx, uint64_t entries) {
+    if (!ctx->sw_log_entries) ctx->sw_log_seen = std::max(ctx->sw_log_seen, entries);
+    else ctx->sw_log_entries = std::max(ctx->sw_log_entries, entries);
+}
 
 bool ctx_fault_take(fecgpu_ctx *ctx) {
     std::lock_guard<std::mutex> lk(ctx->mu);

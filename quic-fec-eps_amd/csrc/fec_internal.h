@@ -176,8 +176,6 @@ struct CombJob {
 };
 constexpr uint64_t kNoXor = ~0ull;
 constexpr int kSwMaxWindow = FECGPU_SW_MAX_WINDOW;
-constexpr int kSwMaxUnknowns = FECGPU_SW_MAX_UNKNOWNS;
-constexpr int kSwMaxEq = FECGPU_SW_MAX_EQUATIONS;
 constexpr uint32_t kSwCoefPitch = 256;  // coefficient bytes per repair job
 
 struct CombArgs {
@@ -197,9 +195,14 @@ struct CombArgs {
     int wpb, nin_max, nout_max;
     uint32_t job_lds;
     uint32_t nx;
+    // device-sized launch (decode): the job count is *extra alone, the widest
+    // job *nin_dev (<= nin_max); each workgroup fits as many jobs as its
+    // `budget` bytes of LDS hold at that width
+    const uint32_t *nin_dev;
+    uint32_t budget;
 };
 // LDS bytes per job of comb_kernel<R> at nin_max inputs
-inline uint32_t comb_job_lds(int nin_max, int R) {
+__host__ __device__ inline uint32_t comb_job_lds(int nin_max, int R) {
     const uint32_t rt = R == 1 ? 1u : (uint32_t)(R + 3) & ~3u;
     return ((uint32_t)nin_max * (16u * R + 4u * rt + 1u) + 8u * R + 8u + 15u) & ~15u;
 }
@@ -231,41 +234,76 @@ inline uint64_t sw_enc_jobs(uint64_t nrep, int group) {
     return group > 1 ? (nrep + group - 1) / group + nrep + 1 : nrep;
 }
 
-// one linked system of a decode: lost sources unk[u_off ..+ e) (ascending),
-// received repairs eqh[q_off ..+ p) (their syndromes: scratch rows q_off..),
-// A [p][e] at amat + a_off, solve jobs jobs[j_off ..+ ceil(e / 8)] with
-// coefficients at coef + t_off ([round_up(e, 8)][p]) and outputs outs[o_off + d]
-struct SwComp {
-    uint64_t u_off, q_off, a_off, j_off, t_off, o_off;
-    uint32_t e, p;
+// ---- sliding-window decode, planned on the device (fec_swdec.hip) ----
+// The lost sources are split into linked systems (two consecutive lost
+// sources are linked when a received repair's window holds both).  A system
+// of at most kSwSmallE unknowns and kSwSmallP equations is solved by one wave
+// (Gauss-Jordan on [A | I]: solve jobs over its syndromes); a longer one by
+// banded elimination (one wave plans it into an operation log, then waves
+// replay the log over 256-byte column chunks of the data).
+constexpr int kSwSmallE = 64;   // unknowns of a small system
+constexpr int kSwSmallP = 96;   // equations (received repairs) of a small system
+constexpr int kSwRows = 256;    // long systems: rows alive at once (equations covering one source)
+constexpr int kSwChunk = 4096;  // sources per planning chunk
+
+struct SwDecCtr {  // per call, zeroed before the first kernel
+    uint32_t nlost, wmax, maxp, err;   // err: bit 0 bad header; bit 1 log / pivot-area capacity
+                                       // exceeded (retry larger); bit 2 more than kSwRows rows alive
+    uint32_t nsyn, nsol, nouts, nlong; // syndrome jobs, solve jobs, solve outputs, long systems
+    uint32_t npiv, recovered, pad0, pad1;
+    unsigned long long ncoef, nlog;    // solve coefficient bytes, long-system log entries
 };
-struct SwSynArgs {  // thread per equation: syndrome coefficients and jobs, and A
-    const fecgpu_sw_repair *eqh;  // headers of the equations (compact copies)
-    const uint64_t *eqr;          // their repair indices
-    const uint32_t *eqc;          // their systems
-    const SwComp *comps;
-    const uint64_t *unk;
-    uint64_t neq;
-    uint32_t stride;
-    CombJob *jobs;
-    uint8_t *coef;
-    uint64_t *outs;
-    uint8_t *amat;
+// one long system: lost[x0 .. x0 + e), candidate repairs [t_lo, t_hi); its
+// forward / backward logs and first pivot row (set by the planner)
+struct SwLong {
+    uint32_t x0, e, t_lo, t_hi;
+    unsigned long long fwd, bwd;
+    uint32_t nfwd, nbwd, piv0, ok;
 };
-hipError_t launch_sw_syn(const SwSynArgs &a, hipStream_t s);
-struct SwPlanArgs {  // wave per system: Gauss-Jordan, solve jobs, per-unknown status
-    const SwComp *comps;
-    uint64_t ncomp;
-    const uint8_t *amat;
-    const uint64_t *unk;
-    uint32_t stride;
-    CombJob *jobs;
-    CombJob *syn_jobs;  // the syndrome jobs (equation g at syn_jobs[g]): emptied when no solve reads them
-    uint8_t *coef;
-    uint64_t *outs;
-    uint8_t *ustat;
+// a long system's operation: kind | slot a << 8 | slot b << 16, aux, a GF
+// multiply table (CoefTab), aux2
+struct SwOp {
+    uint32_t op, aux;
+    uint32_t tab[5];
+    uint32_t aux2;
 };
-hipError_t launch_sw_plan(const SwPlanArgs &a, hipStream_t s);
+enum : uint32_t { kOpLoad = 1, kOpElim = 2, kOpStore = 3, kOpXBegin = 4, kOpXTerm = 5, kOpXEnd = 6, kOpXFree = 7 };
+
+struct SwDecArgs {
+    const uint8_t *src_present, *rep_present;  // device
+    const fecgpu_sw_repair *hdr;               // device
+    uint8_t *stat;                             // [nsrc] out: 0 present / recovered, 1 lost
+    uint64_t nsrc, nrep;
+    uint32_t stride, S, nchunk;
+    int long_min;                              // systems with e >= long_min take the long path
+    uint32_t *reach;                           // [nsrc] max window end of the received repairs starting there
+    uint32_t *chunk;                           // [2 * nchunk] lost count / max reach per chunk, then scanned
+    uint32_t *lost, *reachL;                   // [nsrc] lost sources; prefix max of reach at each
+    SwDecCtr *ctr;
+    CombJob *syn_jobs;                         // [nrep]
+    uint64_t *syn_outs;                        // [nrep]
+    uint8_t *coef;                             // [nrep][kSwCoefPitch]: repair t's syndrome coefficients
+    CombJob *sol_jobs;                         // [sol_cap]
+    uint64_t *sol_outs;                        // [outs_cap]
+    uint8_t *sol_coef;                         // [coef_cap]
+    uint64_t sol_cap, outs_cap, coef_cap;
+    SwLong *longs;                             // [long_cap]
+    uint64_t long_cap;
+    SwOp *log;                                 // [log_cap]
+    uint64_t log_cap;
+    uint32_t *synrow;                          // [nrep] long systems: syndrome row of repair t (~0: none)
+    uint8_t *pivcoef;                          // [piv_cap][256] long systems: pivot rows' coefficients
+    uint32_t *colpiv;                          // [nsrc] long systems: pivot row of column x (~0 free)
+    uint32_t *pivhi;                           // [piv_cap] last unknown of each pivot row
+    uint32_t *pivt;                            // [piv_cap] its repair index
+    uint8_t *pivdata;                          // [piv_cap][stride] long systems: pivot rows' data
+    uint64_t piv_cap;
+    uint8_t *src;                              // the sources (replay writes recovered ones)
+    const uint8_t *synd;                       // syndrome rows (g * stride)
+};
+hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s);    // statuses, lost list, systems
+hipError_t launch_sw_dec_long(const SwDecArgs &a, hipStream_t s);    // long systems: logs, syndrome jobs
+hipError_t launch_sw_dec_replay(const SwDecArgs &a, hipStream_t s);  // long systems: data
 
 // fec_capi.cpp services for fec_sw.cpp: the thread's FECGPU_ERR_DEVICE text,
 // the group-size choice of the block kernels, device scratch slots of the ctx
@@ -285,6 +323,13 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
                        const fecgpu_sw_repair *hdr_host = nullptr);
 // the ctx's "sw_group" tuning (repairs per sliding-window encode job)
 int ctx_sw_group(const fecgpu_ctx *ctx);
+// "sw_long_min": systems of at least this many unknowns take the long-system
+// path even when the small one would fit (default kSwSmallE + 1)
+int ctx_sw_long_min(const fecgpu_ctx *ctx);
+// entries of the long-system operation log a decode of nsrc / nrep reserves
+// ("sw_log_entries" tuning, else grown past any overflow seen on this ctx)
+uint64_t ctx_sw_log_entries(const fecgpu_ctx *ctx, uint64_t nsrc, uint64_t nrep);
+void ctx_sw_log_grow(fecgpu_ctx *ctx, uint64_t entries);
 // tests: true (and the thread's error text set) while the ctx's "fault_launches"
 // count lasts, consuming one
 bool ctx_fault_take(fecgpu_ctx *ctx);

@@ -2073,6 +2073,25 @@ __device__ __forceinline__ void comb_dispatch(int nw, const uint8_t *in, uint32_
 #else
 #define COMB_WAVES
 #endif
+// Device twin of the host's choose_wpb (fec_capi.cpp): jobs per workgroup that
+// fit `budget` bytes at job_lds each, picked for lane use over ncol columns.
+__device__ __forceinline__ int choose_wpb_dev(uint32_t ncol, uint32_t job_lds, uint32_t budget) {
+    int maxw = kMaxWpb;
+    if (job_lds) maxw = max(1, min(maxw, (int)(budget / job_lds)));
+    if (ncol == 0) return maxw;
+    int best = 1;
+    float best_u = -1.f;
+    for (int w = 1; w <= maxw; w++) {
+        const uint32_t slots = (uint32_t)w * ncol, passes = (slots + kBlock - 1) / kBlock;
+        const float u = (float)slots / (float)(passes * kBlock) - (passes < 2 ? 0.05f : 0.f);
+        if (u > best_u + 1e-6f) {
+            best_u = u;
+            best = w;
+        }
+    }
+    return best;
+}
+
 template <int R>
 __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
     extern __shared__ uint4 dyn[];
@@ -2095,14 +2114,21 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
     __syncthreads();
 #endif
     const uint64_t njobs = a.njobs + (a.extra ? (uint64_t)*a.extra : 0ull);
-    for (XcdRange xr = xcd_range((njobs + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
-        const uint64_t j0 = xr.cur * a.wpb;
-        const int nb = (int)min((uint64_t)a.wpb, njobs - j0);
+    int nin_max = a.nin_max, wpb = a.wpb;
+    uint32_t job_lds = a.job_lds;
+    if (a.nin_dev) {  // device-sized: the widest job is known on the device only
+        nin_max = max(1, min((int)*a.nin_dev, a.nin_max));
+        job_lds = comb_job_lds(nin_max, R);
+        wpb = choose_wpb_dev(a.ncol, job_lds, a.budget);
+    }
+    for (XcdRange xr = xcd_range((njobs + wpb - 1) / wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+        const uint64_t j0 = xr.cur * wpb;
+        const int nb = (int)min((uint64_t)wpb, njobs - j0);
         // plan: wave w builds the tables of jobs w, w + 4, ...
         for (int jl = wave; jl < nb; jl += kBlock / 64) {
             const CombJob J = a.jobs[j0 + jl];
-            const int nin = min((int)J.nin, a.nin_max), nout = min((int)J.nout, R);
-            const CombRegion<R> rg(regions + (size_t)jl * a.job_lds, a.nin_max);
+            const int nin = min((int)J.nin, nin_max), nout = min((int)J.nout, R);
+            const CombRegion<R> rg(regions + (size_t)jl * job_lds, nin_max);
             const uint8_t *cf = a.coef + J.coef_off;
             for (int i = lane; i < nout * nin; i += 64) {
                 const int u = i / nin, q = i - u * nin;
@@ -2150,7 +2176,7 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
             const uint32_t col = s - s_pfx[i];
             const int ne = s_ne[jl];
             const int nw = __builtin_amdgcn_readfirstlane(ne);
-            const CombRegion<R> rg(regions + (size_t)jl * a.job_lds, a.nin_max);
+            const CombRegion<R> rg(regions + (size_t)jl * job_lds, nin_max);
             comb_dispatch<R>(nw, reinterpret_cast<const uint8_t *>(s_in[jl]) + col * 16u, a.stride,
                              (int)s_nin[jl], ne, col, rg, a.skip && a.ncol >= 64);
         }
@@ -2230,138 +2256,6 @@ __device__ __forceinline__ void sw_enc_single(const SwEncCoefArgs &a, uint64_t t
     J.nout = 1;
     a.jobs[jt] = J;
     a.outs[t] = t * a.stride;
-}
-
-// Decode, lane per equation g (a received repair of system c): coefficients
-// of its window with the system's lost sources zeroed (the syndrome job:
-// s_g = rep + sum of the received sources' terms, into scratch row g), and the
-// lost sources' coefficients into row g - q_off of the system's A [p][e].
-__global__ __launch_bounds__(kBlock) void sw_syn_kernel(SwSynArgs a) {
-    const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (g >= a.neq) return;
-    const fecgpu_sw_repair h = a.eqh[g];
-    const SwComp c = a.comps[a.eqc[g]];
-    const uint64_t *U = a.unk + c.u_off;
-    uint8_t *cc = a.coef + g * kSwCoefPitch;
-    uint8_t *arow = a.amat + c.a_off + (g - c.q_off) * c.e;
-    const int nss = min((int)h.nss, kSwMaxWindow);
-    (void)rlc_coefs(h.key, nss, min((uint32_t)h.dt, 15u), cc);
-    for (uint32_t u = 0; u < c.e; u++) arow[u] = 0;
-    uint32_t u = 0;
-    for (int j = 0; j < nss; j++) {
-        const uint64_t i = h.fss + j;
-        while (u < c.e && U[u] < i) u++;
-        if (u < c.e && U[u] == i) {
-            arow[u] = cc[j];
-            cc[j] = 0;
-        }
-    }
-    CombJob J;
-    J.in_off = h.fss * a.stride;
-    J.coef_off = g * kSwCoefPitch;
-    J.out_list = g;
-    J.xor_off = a.eqr[g] * a.stride;
-    J.nin = (uint32_t)nss;
-    J.nout = 1;
-    a.jobs[g] = J;
-    a.outs[g] = g * a.stride;
-}
-
-// Decode, wave per linked system: Gauss-Jordan with pivot search on [A | I]
-// (p <= 96 rows, e <= 64 unknowns; row pitch 160 in LDS).  Column c with no
-// pivot is free; unknown c is determined iff its pivot row is zero on every
-// free column, and then x_c = sum_t M[P_c][e + t] * s_t.  Writes the solve
-// jobs (8 determined unknowns each, inputs = the system's syndrome rows), their
-// coefficient rows and output rows, and every unknown's status, and empties
-// the syndrome jobs of equations no solve reads (only pivot rows can appear
-// in M[P_c][e + t]: a non-pivot row never enters a pivot row), so about one
-// syndrome per lost source is computed instead of one per received repair.
-constexpr int kSwPitch = kSwMaxUnknowns + kSwMaxEq;
-__global__ __launch_bounds__(kBlock) void sw_plan_kernel(SwPlanArgs a) {
-    extern __shared__ uint4 dyn[];
-    __shared__ uint8_t s_exp[512];
-    __shared__ uint8_t s_log[256];
-    __shared__ int8_t s_piv[kBlock / 64][kSwMaxUnknowns];  // pivot row of column c, -1 free
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
-    for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
-    __syncthreads();
-    const uint64_t ci = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
-    if (ci >= a.ncomp) return;  // no block-wide barrier below
-    const SwComp c = a.comps[ci];
-    const int e = (int)c.e, p = (int)c.p, W = e + p;
-    uint8_t *M = reinterpret_cast<uint8_t *>(dyn) + (size_t)wave * kSwMaxEq * kSwPitch;
-    int8_t *piv = s_piv[wave];
-    const uint8_t *A = a.amat + c.a_off;
-    for (int q = 0; q < p; q++)
-        for (int j = lane; j < W; j += 64) M[q * kSwPitch + j] = j < e ? A[q * e + j] : (uint8_t)(j - e == q);
-    WAVE_SYNC();
-    uint64_t used0 = 0, used1 = 0;  // wave-uniform: rows 0..63, 64..95 already pivots
-    for (int col = 0; col < e; col++) {
-        const bool c0 = lane < p && !((used0 >> lane) & 1) && M[lane * kSwPitch + col] != 0;
-        const bool c1 = lane + 64 < p && !((used1 >> lane) & 1) && M[(lane + 64) * kSwPitch + col] != 0;
-        const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
-        int pr = -1;
-        if (b0) pr = (int)__ffsll((unsigned long long)b0) - 1;
-        else if (b1) pr = 64 + (int)__ffsll((unsigned long long)b1) - 1;
-        if (lane == 0) piv[col] = (int8_t)pr;
-        if (pr < 0) continue;  // free column (uniform)
-        if (pr < 64) used0 |= 1ull << pr;
-        else used1 |= 1ull << (pr - 64);
-        uint8_t *P = M + pr * kSwPitch;
-        const uint32_t iv = gf_inv_lds(s_exp, s_log, P[col]);
-        WAVE_SYNC();
-        for (int j = lane; j < W; j += 64) P[j] = (uint8_t)gf_mul_lds(s_exp, s_log, P[j], iv);
-        WAVE_SYNC();
-        for (int q = lane; q < p; q += 64) {
-            if (q == pr) continue;
-            uint8_t *row = M + q * kSwPitch;
-            const uint32_t f = row[col];
-            if (!f) continue;
-            for (int j = 0; j < W; j++) row[j] ^= (uint8_t)gf_mul_lds(s_exp, s_log, f, P[j]);
-        }
-        WAVE_SYNC();
-    }
-    WAVE_SYNC();
-    // determined unknowns (lane c), compacted in column order
-    bool det = false;
-    int prc = -1;
-    if (lane < e) {
-        prc = piv[lane];
-        det = prc >= 0;
-        for (int j = 0; j < e && det; j++)
-            if (piv[j] < 0 && M[prc * kSwPitch + j]) det = false;
-    }
-    const uint64_t dm = __ballot(det);
-    const int ndet = __popcll(dm);
-    if (lane < e) {
-        a.ustat[c.u_off + lane] = det ? 0 : 1;
-        if (det) {
-            const int d = __popcll(dm & ((1ull << lane) - 1));
-            uint8_t *cf = a.coef + c.t_off + (uint64_t)d * p;
-            for (int t = 0; t < p; t++) cf[t] = M[prc * kSwPitch + e + t];
-            a.outs[c.o_off + d] = a.unk[c.u_off + lane] * a.stride;
-        }
-    }
-    // syndromes no solve reads (non-pivot rows, undetermined unknowns' rows)
-    // are not computed: the plan runs before the syndrome pass
-    for (int q = lane; q < p; q += 64) {
-        bool need = false;
-        for (int col = 0; col < e && !need; col++)
-            need = ((dm >> col) & 1) && M[piv[col] * kSwPitch + e + q] != 0;
-        if (!need) a.syn_jobs[c.q_off + q].nout = 0;
-    }
-    const int njob = (e + 7) / 8;
-    if (lane < njob) {
-        CombJob J;
-        J.in_off = c.q_off * a.stride;
-        J.coef_off = c.t_off + (uint64_t)lane * 8 * p;
-        J.out_list = c.o_off + (uint64_t)lane * 8;
-        J.xor_off = kNoXor;
-        J.nin = (uint32_t)p;
-        J.nout = (uint32_t)max(0, min(8, ndet - 8 * lane));
-        a.jobs[c.j_off + lane] = J;
-    }
 }
 
 // ========================================================== launchers ===
@@ -2534,10 +2428,24 @@ hipError_t launch_erasure(const EraseArgs &a, hipStream_t s) {
 hipError_t launch_comb(CombArgs a, int R, hipStream_t s) {
     const uint64_t nmax = a.njobs + (a.extra ? a.extra_max : 0);
     if (nmax == 0) return hipSuccess;
-    const uint64_t groups = (nmax + a.wpb - 1) / a.wpb;
-    a.nx = groups >= 8 ? 8 : 1;
-    const uint64_t grid = (groups + a.nx - 1) / a.nx * a.nx;  // one group per workgroup
-    const uint32_t lds = a.job_lds * (uint32_t)a.wpb;
+    uint64_t grid;
+    uint32_t lds;
+    if (a.nin_dev) {
+        // device-sized: persistent, 2 x the workgroups resident at the budget
+        // (the job count and widths are device data; surplus workgroups exit)
+        lds = a.budget;
+        const void *fn = R == 1 ? (const void *)comb_kernel<1> : R == 2 ? (const void *)comb_kernel<2>
+                       : R == 4 ? (const void *)comb_kernel<4> : (const void *)comb_kernel<8>;
+        const uint64_t groups_max = nmax;  // at least one job per group
+        grid = std::min<uint64_t>(groups_max, (uint64_t)resident_blocks(fn, lds) * 2);
+        a.nx = grid >= 8 ? 8 : 1;
+        grid = std::max<uint64_t>(a.nx, grid / a.nx * a.nx);
+    } else {
+        const uint64_t groups = (nmax + a.wpb - 1) / a.wpb;
+        a.nx = groups >= 8 ? 8 : 1;
+        grid = (groups + a.nx - 1) / a.nx * a.nx;  // one group per workgroup
+        lds = a.job_lds * (uint32_t)a.wpb;
+    }
     switch (R) {
         case 1: hipLaunchKernelGGL(comb_kernel<1>, dim3((unsigned)grid), dim3(kBlock), lds, s, a); break;
         case 2: hipLaunchKernelGGL(comb_kernel<2>, dim3((unsigned)grid), dim3(kBlock), lds, s, a); break;
@@ -2551,20 +2459,6 @@ hipError_t launch_comb(CombArgs a, int R, hipStream_t s) {
 hipError_t launch_sw_enc_coef(const SwEncCoefArgs &a, hipStream_t s) {
     if (a.nrep == 0) return hipSuccess;
     hipLaunchKernelGGL(sw_enc_coef_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_sw_syn(const SwSynArgs &a, hipStream_t s) {
-    if (a.neq == 0) return hipSuccess;
-    hipLaunchKernelGGL(sw_syn_kernel, dim3((unsigned)((a.neq + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_sw_plan(const SwPlanArgs &a, hipStream_t s) {
-    if (a.ncomp == 0) return hipSuccess;
-    constexpr int per = kBlock / 64;
-    const uint32_t lds = (uint32_t)per * kSwMaxEq * kSwPitch;
-    hipLaunchKernelGGL(sw_plan_kernel, dim3((unsigned)((a.ncomp + per - 1) / per)), dim3(kBlock), lds, s, a);
     return hipGetLastError();
 }
 

@@ -1,19 +1,16 @@
 // fec_sw.cpp — sliding-window random linear code entry points (include/fecgpu.h
-// fecgpu_sw_encode / fecgpu_sw_decode; RFC 8681 with m = 8; SURVEY.md Appendix
-// B q6).  Host side: argument checks, staging, the decode's split of the lost
-// sources into linked systems, and the launches of fec_kernels.hip's
-// sliding-window kernels.  No CPU fallback: every symbol byte is computed on
-// the GPU.
+// fecgpu_sw_encode / fecgpu_sw_decode / fecgpu_sw_decode_device; RFC 8681 with
+// m = 8).  Host side: argument checks, staging and the
+// launches.  The decode is planned on the device (fec_swdec.hip): the host
+// copies the receiver's bookkeeping up (or takes it on the device) and reads
+// statuses and counters back.  No CPU fallback: every symbol byte is computed
+// on the GPU.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
-#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
-#include <mutex>
-#include <thread>
 #include <vector>
 
 #include "../../include/fecgpu.h"
@@ -49,6 +46,8 @@ namespace {
 constexpr uint32_t kCombBudget = FECGPU_COMB_BUDGET_KB << 10;
 constexpr uint32_t kCombBudgetWide = FECGPU_COMB_BUDGET_WIDE_KB << 10;
 constexpr int kSwSolveOut = 8;               // recovered sources per solve job
+// sources and repairs per call: the device plan numbers them in 32 bits
+constexpr uint64_t kSwMaxSources = (1ull << 32) - 256;
 
 ssize_t check_geometry(uint32_t sym_len, uint32_t stride, const void *a, const void *b) {
     if (stride == 0 || (stride & 15) || sym_len == 0 || sym_len > stride) return FECGPU_ERR_INVALID_ARG;
@@ -167,426 +166,167 @@ ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_
     return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s, group, hdr_host);
 }
 
-// A decode's linked systems (see fecgpu_sw_decode).  The arrays the GPU reads
-// (comps | unk | eqr | eqc | eqh) are written into the ctx's pinned staging
-// block at offsets sized for the worst case (sw_plan_layout), so the plan goes
-// up with one copy per array and no host-side repacking; the device block uses
-// the same offsets.  The same struct is a sweep's output cursor (SwPart).
-struct SwPlan {
-    SwComp *comps = nullptr;
-    uint64_t *unk = nullptr, *eqr = nullptr;
-    uint32_t *eqc = nullptr;
-    fecgpu_sw_repair *eqh = nullptr;
-    uint8_t *ustat = nullptr;  // statuses of the unknowns, copied back
-    uint64_t ncomp = 0, nunk = 0, neq = 0;
-    uint64_t amat = 0, nsolve = 0, tcoef = 0;
-    int max_nss = 1, max_p = 1;
-    std::vector<uint64_t> lost;  // lost sources ascending (per-thread scratch, see sw_plan_scratch)
-};
-
-SwPlan &sw_plan_scratch() {
-    thread_local SwPlan P;
-    std::vector<uint64_t> lost = std::move(P.lost);
-    lost.clear();
-    P = SwPlan{};
-    P.lost = std::move(lost);
-    return P;
-}
-
+// ---- decode (device plan: fec_swdec.hip) ----------------------------------
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Offsets of the plan arrays for nlost lost sources and nrep repairs: at most
-// nlost systems and unknowns, and at most nrep equations (a received repair
-// holding lost sources of two systems would link them, so each repair is an
-// equation of one system at most).
-struct SwLayout {
-    size_t o_unk, o_eqr, o_eqc, o_eqh, meta, o_ust, host;
+// Device scratch of one decode, carved out of ctx slot 6 (plan arrays, jobs,
+// long-system tables), slot 7 (syndrome rows), slot 8 (long systems' pivot
+// rows), slot 9 (their operation log) and slot 10 (device copies of host
+// bookkeeping).
+struct DecBlock {
+    size_t o_reach, o_chunk, o_lost, o_reachL, o_ctr, o_synj, o_syno, o_coef, o_solj, o_solo, o_solc, o_long,
+        o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, total;
+    uint64_t sol_cap, coef_cap, long_cap, piv_cap;
 };
-SwLayout sw_plan_layout(uint64_t nlost, uint64_t nrep) {
-    SwLayout L;
-    L.o_unk = align256(nlost * sizeof(SwComp));
-    L.o_eqr = L.o_unk + align256(nlost * 8);
-    L.o_eqc = L.o_eqr + align256(nrep * 8);
-    L.o_eqh = L.o_eqc + align256(nrep * 4);
-    L.meta = L.o_eqh + align256(nrep * sizeof(fecgpu_sw_repair));
-    L.o_ust = L.meta;  // host only: the unknowns' statuses
-    L.host = L.o_ust + nlost;
+DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
+    DecBlock L{};
+    const uint64_t nchunk = (nsrc + kSwChunk - 1) / kSwChunk;
+    L.sol_cap = std::max<uint64_t>(1, std::min(nsrc, nrep));
+    L.coef_cap = L.sol_cap * kSwSmallP;
+    L.long_cap = nsrc / (uint64_t)std::max(1, std::min(kSwSmallE + 1, long_min)) + 1;
+    L.piv_cap = std::max<uint64_t>(1, nrep);
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o += align256(bytes);
+        return at;
+    };
+    L.o_reach = take((nsrc + 1) * 4);
+    L.o_chunk = take(2 * nchunk * 4);
+    L.o_lost = take(nsrc * 4);
+    L.o_reachL = take(nsrc * 4);
+    L.o_ctr = take(sizeof(SwDecCtr));
+    L.o_synj = take(nrep * sizeof(CombJob));
+    L.o_syno = take(nrep * 8);
+    L.o_coef = take(nrep * (size_t)kSwCoefPitch);
+    L.o_solj = take(L.sol_cap * sizeof(CombJob));
+    L.o_solo = take(L.sol_cap * 8);
+    L.o_solc = take(L.coef_cap);
+    L.o_long = take(L.long_cap * sizeof(SwLong));
+    L.o_synrow = take(nrep * 4);
+    L.o_pivc = take(L.piv_cap * 256);
+    L.o_colpiv = take(nsrc * 4);
+    L.o_pivhi = take(L.piv_cap * 4);
+    L.o_pivt = take(L.piv_cap * 4);
+    L.total = o;
     return L;
 }
 
-// Statuses (0 present, 1 lost) of sources [lo, hi) and their lost indices,
-// ascending, in one pass over the arrival flags, 8 at a time (lo a multiple of
-// 8): bit 7 of byte b of ((v & 0x7f..) + 0x7f..) | v is set iff flag b is
-// nonzero (no carries cross bytes), so the status word is its complement
-// shifted down.
-void sw_scan_lost(const uint8_t *src_present, uint64_t lo, uint64_t hi, uint8_t *src_status,
-                  std::vector<uint64_t> &lost) {
-    constexpr uint64_t k7f = 0x7f7f7f7f7f7f7f7full, k01 = 0x0101010101010101ull;
-    uint64_t i = lo;
-    for (; i + 8 <= hi; i += 8) {
-        uint64_t v;
-        std::memcpy(&v, src_present + i, 8);
-        const uint64_t st = ~((((v & k7f) + k7f) | v) >> 7) & k01;
-        std::memcpy(src_status + i, &st, 8);
-        for (uint64_t m = st; m; m &= m - 1) lost.push_back(i + ((uint64_t)__builtin_ctzll(m) >> 3));
-    }
-    for (; i < hi; i++) {
-        src_status[i] = src_present[i] ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
-        if (!src_present[i]) lost.push_back(i);
-    }
+// One decode on the device.  src / rep / present / rep_present / hdr / stat
+// are device pointers; ctr_out (pinned, nullable) receives the counters once
+// the stream reaches the end of the call.
+ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, uint64_t nsrc, const uint8_t *rep,
+                       const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t S,
+                       uint32_t stride, uint8_t *stat, hipStream_t s, SwDecCtr *ctr_out, uint64_t log_entries) {
+    const int long_min = ctx_sw_long_min(ctx);
+    const DecBlock L = dec_block(nsrc, nrep, long_min);
+    void *pb = nullptr, *psyn = nullptr, *ppiv = nullptr, *plog = nullptr;
+    RC_TRY(ctx_sw_scratch(ctx, 6, L.total, &pb));
+    RC_TRY(ctx_sw_scratch(ctx, 7, std::max<uint64_t>(1, nrep) * stride, &psyn));
+    RC_TRY(ctx_sw_scratch(ctx, 8, L.piv_cap * stride, &ppiv));
+    RC_TRY(ctx_sw_scratch(ctx, 9, log_entries * sizeof(SwOp), &plog));
+    uint8_t *b = static_cast<uint8_t *>(pb);
+    SwDecArgs a{};
+    a.src_present = present;
+    a.rep_present = rep_present;
+    a.hdr = hdr;
+    a.stat = stat;
+    a.nsrc = nsrc;
+    a.nrep = nrep;
+    a.stride = stride;
+    a.S = S;
+    a.nchunk = (uint32_t)((nsrc + kSwChunk - 1) / kSwChunk);
+    a.long_min = long_min;
+    a.reach = reinterpret_cast<uint32_t *>(b + L.o_reach);
+    a.chunk = reinterpret_cast<uint32_t *>(b + L.o_chunk);
+    a.lost = reinterpret_cast<uint32_t *>(b + L.o_lost);
+    a.reachL = reinterpret_cast<uint32_t *>(b + L.o_reachL);
+    a.ctr = reinterpret_cast<SwDecCtr *>(b + L.o_ctr);
+    a.syn_jobs = reinterpret_cast<CombJob *>(b + L.o_synj);
+    a.syn_outs = reinterpret_cast<uint64_t *>(b + L.o_syno);
+    a.coef = b + L.o_coef;
+    a.sol_jobs = reinterpret_cast<CombJob *>(b + L.o_solj);
+    a.sol_outs = reinterpret_cast<uint64_t *>(b + L.o_solo);
+    a.sol_coef = b + L.o_solc;
+    a.sol_cap = a.outs_cap = L.sol_cap;
+    a.coef_cap = L.coef_cap;
+    a.longs = reinterpret_cast<SwLong *>(b + L.o_long);
+    a.long_cap = L.long_cap;
+    a.log = static_cast<SwOp *>(plog);
+    a.log_cap = log_entries;
+    a.synrow = reinterpret_cast<uint32_t *>(b + L.o_synrow);
+    a.pivcoef = b + L.o_pivc;
+    a.colpiv = reinterpret_cast<uint32_t *>(b + L.o_colpiv);
+    a.pivhi = reinterpret_cast<uint32_t *>(b + L.o_pivhi);
+    a.pivt = reinterpret_cast<uint32_t *>(b + L.o_pivt);
+    a.pivdata = static_cast<uint8_t *>(ppiv);
+    a.piv_cap = L.piv_cap;
+    a.src = src;
+    a.synd = static_cast<const uint8_t *>(psyn);
+
+    SW_TRY(hipMemsetAsync(a.ctr, 0, sizeof(SwDecCtr), s), "sliding-window decode counters");
+    SW_TRY(hipMemsetAsync(a.reach, 0, (nsrc + 1) * 4, s), "sliding-window decode reach");
+    SW_TRY(launch_sw_dec_plan(a, s), "sliding-window decode plan launch");
+    SW_TRY(launch_sw_dec_long(a, s), "sliding-window long-system plan launch");
+    const uint32_t ncol = (S + 15u) >> 4;
+    // syndromes (one output each, at most the widest window of inputs), then the
+    // small systems' solves (<= 8 outputs over <= kSwSmallP syndromes)
+    CombArgs sa{};
+    sa.jobs = a.syn_jobs;
+    sa.coef = a.coef;
+    sa.outs = a.syn_outs;
+    sa.in_base = src;
+    sa.out_base = static_cast<uint8_t *>(psyn);
+    sa.xor_base = rep;
+    sa.extra = &a.ctr->nsyn;
+    sa.extra_max = nrep;
+    sa.ncol = ncol;
+    sa.stride = stride;
+    sa.nin_max = kSwMaxWindow;
+    sa.nout_max = 1;
+    sa.nin_dev = &a.ctr->wmax;
+    sa.budget = ncol >= 64 ? kCombBudgetWide : kCombBudget;
+    SW_TRY(launch_comb(sa, 1, s), "sliding-window syndrome launch");
+    CombArgs va = sa;
+    va.jobs = a.sol_jobs;
+    va.coef = a.sol_coef;
+    va.outs = a.sol_outs;
+    va.in_base = static_cast<const uint8_t *>(psyn);
+    va.out_base = src;
+    va.xor_base = nullptr;
+    va.extra = &a.ctr->nsol;
+    va.extra_max = L.sol_cap;
+    va.nin_max = kSwSmallP;
+    va.nout_max = kSwSolveOut;
+    va.nin_dev = &a.ctr->maxp;
+    SW_TRY(launch_comb(va, kSwSolveOut, s), "sliding-window solve launch");
+    SW_TRY(launch_sw_dec_replay(a, s), "sliding-window long-system replay launch");
+    if (ctr_out) SW_TRY(hipMemcpyAsync(ctr_out, a.ctr, sizeof(SwDecCtr), hipMemcpyDeviceToHost, s), "D2H sw counters");
+    return 0;
 }
 
-// First repair whose fss >= lo (headers are in fss order).
-uint64_t sw_first_repair(const fecgpu_sw_repair *hdr, uint64_t nrep, uint64_t lo) {
-    return (uint64_t)(std::partition_point(hdr, hdr + nrep, [lo](const fecgpu_sw_repair &h) { return h.fss < lo; }) -
-                      hdr);
-}
-
-// lost[x] begins a linked system iff no received repair with fss <= lost[x-1]
-// ends past lost[x] (only repairs with fss > lost[x-1] - wmax can).
-bool sw_system_start(const uint64_t *lost, size_t x, const uint8_t *rep_present,
-                     const fecgpu_sw_repair *hdr, uint64_t nrep, uint64_t wmax) {
-    if (x == 0) return true;
-    const uint64_t p = lost[x - 1];
-    for (uint64_t t = sw_first_repair(hdr, nrep, p >= wmax ? p - wmax + 1 : 0); t < nrep && hdr[t].fss <= p; t++)
-        if (rep_present[t] && hdr[t].fss + hdr[t].nss > lost[x]) return false;
-    return true;
-}
-
-// The sweep over lost[0 .. nl), which begins a system and ends where the next
-// one begins (or at the end of the lost sources): consecutive lost sources
-// a < b are linked iff a received repair's window holds both, i.e. some
-// received repair with fss <= a ends past b (windows are intervals, so this
-// links every pair a repair holds).  Each system's equations are the received
-// repairs whose windows hold one of its lost sources (the first kSwMaxEq).
-// Systems of more than kSwMaxUnknowns lost sources, or with no equation, are
-// left out (their sources stay lost).  wmax: an upper bound of the received
-// windows' nss (a repair holding source i has fss > i - wmax).  Headers are in
-// fss order, so the repairs are walked directly with their arrival flags.
-// Offsets in O's systems are relative to O's own arrays.
-void sw_sweep(const uint64_t *lost, size_t nl, const uint8_t *rep_present, const fecgpu_sw_repair *hdr,
-              uint64_t nrep, uint64_t wmax, SwPlan &O) {
-    if (nl == 0) return;
-    uint64_t eq[kSwMaxEq];
-    const uint64_t first = sw_first_repair(hdr, nrep, lost[0] >= wmax ? lost[0] - wmax + 1 : 0);
-    uint64_t ip = first;  // repairs with fss <= the current lost source are folded into max_end
-    uint64_t jp = first;  // first repair that can hold the next system's sources
-    uint64_t max_end = 0;
-    size_t start = 0;
-    for (size_t x = 0; x < nl; x++) {
-        for (; ip < nrep && hdr[ip].fss <= lost[x]; ip++)
-            if (rep_present[ip]) max_end = std::max(max_end, hdr[ip].fss + hdr[ip].nss);
-        if (x + 1 < nl && max_end > lost[x + 1]) continue;
-        // system = lost[start .. x]
-        const uint64_t *U = lost + start;
-        const size_t e = x + 1 - start;
-        start = x + 1;
-        if (e > (size_t)kSwMaxUnknowns) continue;
-        // systems come in ascending order, so the first candidate repair only
-        // moves forward (a sweep, not a search per system)
-        const uint64_t lo = U[0] >= wmax ? U[0] - wmax + 1 : 0;
-        while (jp < nrep && hdr[jp].fss < lo) jp++;
-        int neq = 0;
-        for (uint64_t it = jp; it < nrep && hdr[it].fss <= U[e - 1] && neq < kSwMaxEq; ++it) {
-            if (!rep_present[it]) continue;
-            const fecgpu_sw_repair &h = hdr[it];
-            const uint64_t *u = e == 1 ? U : std::lower_bound(U, U + e, h.fss);
-            if (u != U + e && *u >= h.fss && *u < h.fss + h.nss) eq[neq++] = it;
-        }
-        if (neq == 0) continue;
-        SwComp c{};
-        c.u_off = O.nunk;
-        c.q_off = O.neq;
-        c.a_off = O.amat;
-        c.j_off = O.nsolve;
-        c.t_off = O.tcoef;  // relative; the syndrome coefficients go first
-        c.o_off = c.u_off;  // relative; the syndrome outputs go first
-        c.e = (uint32_t)e;
-        c.p = (uint32_t)neq;
-        O.amat += (uint64_t)c.e * c.p;
-        O.nsolve += (e + kSwSolveOut - 1) / kSwSolveOut;
-        O.tcoef += (uint64_t)((e + kSwSolveOut - 1) / kSwSolveOut * kSwSolveOut) * c.p;
-        O.max_p = std::max(O.max_p, (int)c.p);
-        const uint32_t ci = (uint32_t)O.ncomp;
-        for (size_t j = 0; j < e; j++) O.unk[O.nunk++] = U[j];
-        for (int q = 0; q < neq; q++) {
-            const uint64_t t = eq[q];
-            O.eqr[O.neq] = t;
-            O.eqc[O.neq] = ci;
-            O.eqh[O.neq++] = hdr[t];
-            O.max_nss = std::max(O.max_nss, (int)hdr[t].nss);
-        }
-        O.comps[O.ncomp++] = c;
-    }
-}
-
-// Process-wide helper threads for large plans (FECGPU_PLAN_THREADS, default 4
-// including the caller; 1 = always serial).  Workers spin briefly between
-// runs (a stream of decodes comes every few hundred microseconds), then
-// sleep.  One plan holds the pool at a time (acquire); a caller that finds it
-// held plans alone.  The pool is never torn down (its threads are detached).
-class PlanPool {
-  public:
-    static PlanPool &get() {
-        static PlanPool *pool = new PlanPool();
-        return *pool;
-    }
-    int size() const { return n_; }
-    std::unique_lock<std::mutex> acquire() { return std::unique_lock<std::mutex>(run_mu_, std::try_to_lock); }
-    // fn(i) for every i in [0, size()), i = 0 on the caller; the caller holds acquire()'s lock
-    void run(const std::function<void(int)> &fn) {
-        fn_ = &fn;
-        pending_.store(n_ - 1, std::memory_order_relaxed);
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            gen_.fetch_add(1, std::memory_order_release);
-        }
-        cv_.notify_all();
-        fn(0);
-        while (pending_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
-    }
-
-  private:
-    PlanPool() {
-        int n = 4;
-        if (const char *e = std::getenv("FECGPU_PLAN_THREADS")) n = std::atoi(e);
-        n = std::max(1, std::min(n, std::max(1, (int)std::thread::hardware_concurrency())));
-        n_ = std::min(n, kMaxThreads);
-        for (int i = 1; i < n_; i++) std::thread([this, i] { work(i); }).detach();
-    }
-    void work(int i) {
-        uint64_t seen = 0;
-        for (;;) {
-            for (int spin = 0; gen_.load(std::memory_order_acquire) == seen; spin++) {
-                if (spin < (1 << 16)) {
-                    __builtin_ia32_pause();
-                    continue;
-                }
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
-                break;
-            }
-            seen = gen_.load(std::memory_order_acquire);
-            (*fn_)(i);
-            pending_.fetch_sub(1, std::memory_order_acq_rel);
-        }
-    }
-
-  public:
-    static constexpr int kMaxThreads = 16;
-
-  private:
-    int n_ = 1;
-    std::mutex run_mu_, mu_;
-    std::condition_variable cv_;
-    std::atomic<uint64_t> gen_{0};
-    std::atomic<int> pending_{0};
-    const std::function<void(int)> *fn_ = nullptr;
-};
-
-// One helper's share of a parallel plan: its source chunk's lost list, then
-// its systems in its own arrays (capacity kept from call to call).
-struct SwPart {
-    std::vector<uint64_t> lost;
-    std::vector<SwComp> comps;
-    std::vector<uint64_t> unk, eqr;
-    std::vector<uint32_t> eqc;
-    std::vector<fecgpu_sw_repair> eqh;
-    SwPlan out;
-    size_t lo = 0, hi = 0;  // range of the global lost list whose systems this part plans
-};
-
-constexpr uint64_t kSwParallelSources = 1u << 16;  // below this the plan runs on the caller alone
-
-// Statuses, lost list, staging and systems of one decode.  Returns the number
-// of lost sources (P.lost), or a negative error; P's arrays point into the
-// staging block host(bytes, &p) returns (the ctx's pinned block) at layout L
-// (not requested when nothing is lost).  threads: 0 = the pool's size.
-template <class HostBlock>
-ssize_t sw_plan(HostBlock &&host, const uint8_t *src_present, uint64_t nsrc, uint8_t *src_status,
-                const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep, uint64_t wmax,
-                SwPlan &P, SwLayout &L, int threads = 0) {
-    auto bind = [&](void *ph) {
-        uint8_t *meta = static_cast<uint8_t *>(ph);
-        P.comps = reinterpret_cast<SwComp *>(meta);
-        P.unk = reinterpret_cast<uint64_t *>(meta + L.o_unk);
-        P.eqr = reinterpret_cast<uint64_t *>(meta + L.o_eqr);
-        P.eqc = reinterpret_cast<uint32_t *>(meta + L.o_eqc);
-        P.eqh = reinterpret_cast<fecgpu_sw_repair *>(meta + L.o_eqh);
-        P.ustat = meta + L.o_ust;
-    };
-    PlanPool &pool = PlanPool::get();
-    const int n = threads > 0 ? std::min(threads, pool.size()) : pool.size();
-    std::unique_lock<std::mutex> held;
-    if (n > 1 && nsrc >= kSwParallelSources) held = pool.acquire();
-    const bool par = held.owns_lock();
-    static SwPart parts[PlanPool::kMaxThreads];  // used while the pool is held only
-    if (par) {
-        pool.run([&](int i) {
-            if (i >= n) return;  // a smaller share than the pool
-            const uint64_t lo = (nsrc * (uint64_t)i / n) & ~7ull;
-            const uint64_t hi = i + 1 == n ? nsrc : (nsrc * (uint64_t)(i + 1) / n) & ~7ull;
-            parts[i].lost.clear();
-            sw_scan_lost(src_present, lo, hi, src_status, parts[i].lost);
-        });
-        for (int i = 0; i < n; i++) P.lost.insert(P.lost.end(), parts[i].lost.begin(), parts[i].lost.end());
-    } else {
-        sw_scan_lost(src_present, 0, nsrc, src_status, P.lost);
-    }
-    const uint64_t nlost = P.lost.size();
-    if (nlost == 0 || nrep == 0) return (ssize_t)nlost;
-    L = sw_plan_layout(nlost, nrep);
+// Synchronous decode with the counters read back: retries once with a larger
+// operation log if a long system overflowed it (a decode is idempotent: it
+// reads only received symbols and rewrites the lost ones).
+ssize_t sw_decode_sync(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, uint64_t nsrc, const uint8_t *rep,
+                       const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t S,
+                       uint32_t stride, uint8_t *stat, hipStream_t s, const std::function<ssize_t()> &after) {
     void *ph = nullptr;
-    RC_TRY(host(L.host, &ph));
-    bind(ph);
-    const uint64_t *lost = P.lost.data();
-    if (!par || nlost < 1024) {
-        sw_sweep(lost, nlost, rep_present, hdr, nrep, wmax, P);
-        return (ssize_t)nlost;
+    RC_TRY(ctx_sw_host(ctx, sizeof(SwDecCtr), &ph));
+    SwDecCtr *ctr = static_cast<SwDecCtr *>(ph);
+    uint64_t log_entries = ctx_sw_log_entries(ctx, nsrc, nrep);
+    for (int attempt = 0;; attempt++) {
+        RC_TRY(sw_decode_core(ctx, src, present, nsrc, rep, rep_present, hdr, nrep, S, stride, stat, s, ctr,
+                              log_entries));
+        RC_TRY(after());
+        SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (ctr->err & 1u) return FECGPU_ERR_INVALID_ARG;
+        if (!(ctr->err & 2u)) break;
+        if (attempt == 2) return set_dev_error(hipErrorOutOfMemory, "sliding-window decode: operation log capacity");
+        log_entries = std::max<uint64_t>(log_entries * 4, (uint64_t)ctr->nlog + 1);
+        ctx_sw_log_grow(ctx, log_entries);
     }
-    pool.run([&](int i) {
-        if (i >= n) return;  // a smaller share than the pool
-        // this part's systems: from the first system start at or after its
-        // nominal share of the lost list to the next part's
-        auto start_at = [&](int j) {
-            if (j >= n) return (size_t)nlost;
-            size_t x = (size_t)(nlost * (uint64_t)j / n);
-            while (x < nlost && !sw_system_start(lost, x, rep_present, hdr, nrep, wmax)) x++;
-            return x;
-        };
-        SwPart &q = parts[i];
-        q.lo = start_at(i);
-        q.hi = std::max(q.lo, start_at(i + 1));
-        const size_t nl = q.hi - q.lo;
-        uint64_t ne = 0;  // bound on equations: repairs with fss in [lost[lo] - wmax + 1, lost[hi - 1]]
-        if (nl) {
-            const uint64_t a = lost[q.lo], b = lost[q.hi - 1];
-            ne = sw_first_repair(hdr, nrep, b + 1) - sw_first_repair(hdr, nrep, a >= wmax ? a - wmax + 1 : 0);
-        }
-        if (q.comps.size() < nl) q.comps.resize(nl);
-        if (q.unk.size() < nl) q.unk.resize(nl);
-        if (q.eqr.size() < ne) {
-            q.eqr.resize(ne);
-            q.eqc.resize(ne);
-            q.eqh.resize(ne);
-        }
-        q.out = SwPlan{};
-        q.out.comps = q.comps.data();
-        q.out.unk = q.unk.data();
-        q.out.eqr = q.eqr.data();
-        q.out.eqc = q.eqc.data();
-        q.out.eqh = q.eqh.data();
-        sw_sweep(lost + q.lo, nl, rep_present, hdr, nrep, wmax, q.out);
-    });
-    // concatenate the parts in order, rebasing their offsets
-    struct Base { uint64_t comp, unk, eq, amat, nsolve, tcoef; };
-    Base base[PlanPool::kMaxThreads];
-    Base acc{0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < n; i++) {
-        const SwPlan &o = parts[i].out;
-        base[i] = acc;
-        acc.comp += o.ncomp;
-        acc.unk += o.nunk;
-        acc.eq += o.neq;
-        acc.amat += o.amat;
-        acc.nsolve += o.nsolve;
-        acc.tcoef += o.tcoef;
-        P.max_nss = std::max(P.max_nss, o.max_nss);
-        P.max_p = std::max(P.max_p, o.max_p);
-    }
-    P.ncomp = acc.comp;
-    P.nunk = acc.unk;
-    P.neq = acc.eq;
-    P.amat = acc.amat;
-    P.nsolve = acc.nsolve;
-    P.tcoef = acc.tcoef;
-    pool.run([&](int i) {
-        if (i >= n) return;  // a smaller share than the pool
-        const SwPlan &o = parts[i].out;
-        const Base &b = base[i];
-        for (uint64_t j = 0; j < o.ncomp; j++) {
-            SwComp c = o.comps[j];
-            c.u_off += b.unk;
-            c.o_off += b.unk;
-            c.q_off += b.eq;
-            c.a_off += b.amat;
-            c.j_off += b.nsolve;
-            c.t_off += b.tcoef;
-            P.comps[b.comp + j] = c;
-        }
-        std::memcpy(P.unk + b.unk, o.unk, o.nunk * 8);
-        std::memcpy(P.eqr + b.eq, o.eqr, o.neq * 8);
-        std::memcpy(P.eqh + b.eq, o.eqh, o.neq * sizeof(fecgpu_sw_repair));
-        for (uint64_t j = 0; j < o.neq; j++) P.eqc[b.eq + j] = o.eqc[j] + (uint32_t)b.comp;
-    });
-    return (ssize_t)nlost;
-}
-
-// Device part of a decode: src / rep device pointers, plan P in the pinned
-// staging block at layout L.
-ssize_t sw_decode_dev(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *rep, SwPlan &P, const SwLayout &L,
-                      uint32_t S, uint32_t stride, hipStream_t s) {
-    const uint64_t neq = P.neq, nunk = P.nunk, ncomp = P.ncomp;
-    const uint64_t coef_syn = neq * kSwCoefPitch;
-    for (uint64_t c = 0; c < ncomp; c++) {
-        P.comps[c].t_off += coef_syn;
-        P.comps[c].o_off += neq;
-    }
-    // device block: the plan arrays at L's offsets, then amat, ustat, syndrome rows
-    const size_t o_unk = L.o_unk, o_eqr = L.o_eqr, o_eqc = L.o_eqc, o_eqh = L.o_eqh;
-    const size_t o_amat = L.meta;
-    const size_t o_ust = o_amat + align256(P.amat);
-    const size_t o_syn = o_ust + align256(nunk);
-    const size_t total = o_syn + neq * (size_t)stride;
-    const uint8_t *meta = reinterpret_cast<const uint8_t *>(P.comps);
-    void *pm = nullptr, *pj = nullptr, *pc = nullptr, *po = nullptr;
-    RC_TRY(ctx_sw_scratch(ctx, 6, total, &pm));
-    RC_TRY(ctx_sw_scratch(ctx, 0, (neq + P.nsolve) * sizeof(CombJob), &pj));
-    RC_TRY(ctx_sw_scratch(ctx, 1, coef_syn + P.tcoef, &pc));
-    RC_TRY(ctx_sw_scratch(ctx, 2, (neq + nunk) * sizeof(uint64_t), &po));
-    uint8_t *m = static_cast<uint8_t *>(pm);
-    // the used part of each array (from pinned memory: a pageable copy of
-    // ~2 MB was a third of the call)
-    const size_t part[5][2] = {{0, ncomp * sizeof(SwComp)}, {o_unk, nunk * 8}, {o_eqr, neq * 8},
-                               {o_eqc, neq * 4}, {o_eqh, neq * sizeof(fecgpu_sw_repair)}};
-    for (const auto &pt : part)
-        SW_TRY(hipMemcpyAsync(m + pt[0], meta + pt[0], pt[1], hipMemcpyHostToDevice, s), "H2D sw plan");
-    CombJob *jobs = static_cast<CombJob *>(pj);
-    uint8_t *coef = static_cast<uint8_t *>(pc);
-    uint64_t *outs = static_cast<uint64_t *>(po);
-    uint8_t *synd = m + o_syn;
-
-    SwSynArgs ya{};
-    ya.eqh = reinterpret_cast<const fecgpu_sw_repair *>(m + o_eqh);
-    ya.eqr = reinterpret_cast<const uint64_t *>(m + o_eqr);
-    ya.eqc = reinterpret_cast<const uint32_t *>(m + o_eqc);
-    ya.comps = reinterpret_cast<const SwComp *>(m);
-    ya.unk = reinterpret_cast<const uint64_t *>(m + o_unk);
-    ya.neq = neq;
-    ya.stride = stride;
-    ya.jobs = jobs;
-    ya.coef = coef;
-    ya.outs = outs;
-    ya.amat = m + o_amat;
-    SW_TRY(launch_sw_syn(ya, s), "sliding-window syndrome coefficient launch");
-
-    SwPlanArgs pa{};
-    pa.comps = ya.comps;
-    pa.ncomp = ncomp;
-    pa.amat = m + o_amat;
-    pa.unk = ya.unk;
-    pa.stride = stride;
-    pa.jobs = jobs + neq;
-    pa.syn_jobs = jobs;
-    pa.coef = coef;
-    pa.outs = outs;
-    pa.ustat = m + o_ust;
-    SW_TRY(launch_sw_plan(pa, s), "sliding-window plan launch");
-    RC_TRY(run_comb(jobs, neq, coef, outs, src, synd, rep, S, stride, 1, P.max_nss, s));
-    RC_TRY(run_comb(jobs + neq, P.nsolve, coef, outs, synd, src, nullptr, S, stride, kSwSolveOut,
-                    P.max_p, s));
-    SW_TRY(hipMemcpyAsync(P.ustat, m + o_ust, nunk, hipMemcpyDeviceToHost, s), "D2H sw status");
-    return 0;  // P.ustat is valid once the stream has completed
+    return (ssize_t)ctr->recovered;
 }
 
 }  // namespace
@@ -636,22 +376,28 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
                          uint32_t stride, uint8_t *src_status, uint32_t flags, void *stream) {
     if (!ctx || !src || !src_present || !src_status || nsrc == 0) return FECGPU_ERR_INVALID_ARG;
     if (nrep && (!rep || !rep_present || !hdr)) return FECGPU_ERR_INVALID_ARG;
+    if (nsrc >= kSwMaxSources || nrep >= kSwMaxSources) return FECGPU_ERR_UNSUPPORTED;
     RC_TRY(check_geometry(sym_len, stride, src, nrep ? rep : src));
-    uint64_t wmax = 1, prev_fss = 0;
+    uint64_t prev_fss = 0;
     for (uint64_t t = 0; t < nrep; t++) {
         if (!header_ok(hdr[t], nsrc)) return FECGPU_ERR_INVALID_ARG;
         if (hdr[t].fss < prev_fss) return FECGPU_ERR_INVALID_ARG;  // fss nondecreasing
         prev_fss = hdr[t].fss;
-        wmax = std::max<uint64_t>(wmax, hdr[t].nss);
     }
-    SwPlan &P = sw_plan_scratch();
-    SwLayout L{};
-    const ssize_t nlost = sw_plan([ctx](size_t bytes, void **p) { return ctx_sw_host(ctx, bytes, p); }, src_present,
-                                  nsrc, src_status, rep_present, hdr, nrep, wmax, P, L);
-    if (nlost <= 0 || nrep == 0) return nlost < 0 ? nlost : 0;
-    if (P.ncomp == 0) return 0;
+    if (nrep == 0) {  // nothing to decode with: statuses only
+        for (uint64_t i = 0; i < nsrc; i++) src_status[i] = src_present[i] ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
+        return 0;
+    }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     RC_TRY(ctx_sw_begin(ctx, s));
+    // the bookkeeping (flags, headers, statuses) goes up and comes back down
+    void *pm = nullptr;
+    const size_t o_rp = align256(nsrc), o_hdr = o_rp + align256(nrep), o_st = o_hdr + align256(nrep * sizeof(fecgpu_sw_repair));
+    RC_TRY(ctx_sw_scratch(ctx, 10, o_st + nsrc, &pm));
+    uint8_t *m = static_cast<uint8_t *>(pm);
+    SW_TRY(hipMemcpyAsync(m, src_present, nsrc, hipMemcpyHostToDevice, s), "H2D sw source flags");
+    SW_TRY(hipMemcpyAsync(m + o_rp, rep_present, nrep, hipMemcpyHostToDevice, s), "H2D sw repair flags");
+    SW_TRY(hipMemcpyAsync(m + o_hdr, hdr, nrep * sizeof(fecgpu_sw_repair), hipMemcpyHostToDevice, s), "H2D sw headers");
     uint8_t *dsrc = src;
     const uint8_t *drep = rep;
     if (flags & FECGPU_F_HOST_PTRS) {
@@ -663,18 +409,39 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
         dsrc = static_cast<uint8_t *>(ds);
         drep = static_cast<uint8_t *>(dr);
     }
-    RC_TRY(sw_decode_dev(ctx, dsrc, drep, P, L, sym_len, stride, s));
-    if (flags & FECGPU_F_HOST_PTRS)
-        SW_TRY(hipMemcpyAsync(src, dsrc, nsrc * stride, hipMemcpyDeviceToHost, s), "D2H sw sources");
+    const ssize_t rc = sw_decode_sync(
+        ctx, dsrc, m, nsrc, drep, m + o_rp, reinterpret_cast<const fecgpu_sw_repair *>(m + o_hdr), nrep, sym_len,
+        stride, m + o_st, s, [&]() -> ssize_t {
+            SW_TRY(hipMemcpyAsync(src_status, m + o_st, nsrc, hipMemcpyDeviceToHost, s), "D2H sw statuses");
+            if (flags & FECGPU_F_HOST_PTRS)
+                SW_TRY(hipMemcpyAsync(src, dsrc, nsrc * stride, hipMemcpyDeviceToHost, s), "D2H sw sources");
+            return 0;
+        });
     RC_TRY(ctx_sw_end(ctx, s));
-    SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
-    ssize_t rec = 0;
-    for (uint64_t u = 0; u < P.nunk; u++)
-        if (P.ustat[u] == 0) {
-            src_status[P.unk[u]] = FECGPU_STATUS_OK;
-            rec++;
-        }
-    return rec;
+    return rc;
+}
+
+ssize_t fecgpu_sw_decode_device(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_present, uint64_t nsrc,
+                                const uint8_t *rep, const uint8_t *rep_present, const fecgpu_sw_repair *hdr,
+                                uint64_t nrep, uint32_t sym_len, uint32_t stride, uint8_t *src_status,
+                                uint32_t flags, void *stream) {
+    if (!ctx || !src || !src_present || !src_status || nsrc == 0) return FECGPU_ERR_INVALID_ARG;
+    if (nrep && (!rep || !rep_present || !hdr)) return FECGPU_ERR_INVALID_ARG;
+    if (flags & FECGPU_F_HOST_PTRS) return FECGPU_ERR_INVALID_ARG;
+    if (nsrc >= kSwMaxSources || nrep >= kSwMaxSources) return FECGPU_ERR_UNSUPPORTED;
+    RC_TRY(check_geometry(sym_len, stride, src, nrep ? rep : src));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    RC_TRY(ctx_sw_begin(ctx, s));
+    ssize_t rc = 0;
+    if (flags & FECGPU_F_SYNC) {
+        rc = sw_decode_sync(ctx, src, src_present, nsrc, rep, rep_present, hdr, nrep, sym_len, stride, src_status, s,
+                            [] { return (ssize_t)0; });
+    } else {
+        rc = sw_decode_core(ctx, src, src_present, nsrc, rep, rep_present, hdr, nrep, sym_len, stride, src_status, s,
+                            nullptr, ctx_sw_log_entries(ctx, nsrc, nrep));
+    }
+    RC_TRY(ctx_sw_end(ctx, s));
+    return rc;
 }
 
 }  // extern "C"

@@ -1,0 +1,976 @@
+// fec_swdec.hip — sliding-window RLC decode (RFC 8681, m = 8) planned on the
+// device: include/fecgpu.h fecgpu_sw_decode / fecgpu_sw_decode_device
+// (DESIGN.md §4b).  No CPU work besides argument
+// checks: the receiver's arrival flags and repair headers go to the GPU and
+// every step below runs there.
+//
+//  1. plan (sw_dec_{hdr,count,scan,lost}_kernel): per-call scans over the
+//     arrival flags — statuses, the lost list in stream order, and for each
+//     lost source the farthest window end of the received repairs that start
+//     at or before it (a system ends where that reach stops short of the next
+//     lost source).  The reach array is then reused as rank[i] = lost sources
+//     before i, which gives any window's unknown range in two loads.
+//  2. systems (sw_dec_sys_kernel): a wave per system start.  A system of at
+//     most 64 unknowns and 96 equations is solved by that wave: coefficients
+//     from the RFC 8682 PRNG, Gauss-Jordan with pivot search on [A | I] in LDS,
+//     solve jobs x_u = sum_t T[u][t] s_t for the determined unknowns (also
+//     when the system is rank deficient), syndrome jobs only for the rows a
+//     solve reads.  A longer system is queued for step 3.
+//  3. long systems (sw_dec_long_kernel): a wave per system plans a banded
+//     elimination (oracle/fec_sw_banded.c is its CPU statement) into an
+//     operation log — forward elimination with the pivot whose range ends
+//     first (rows never widen, so at most the repairs covering one source are
+//     alive at once), a null-space sweep from the last column down that marks
+//     the determined unknowns exactly, and back substitution with the free
+//     unknowns at 0.  sw_dec_replay_kernel replays the log over the data, a
+//     wave per (system, 256-byte column chunk), rows in LDS.
+//  4. data (fec_kernels.hip comb_kernel, sized on the device): syndromes
+//     s_t = repair_t + sum of the received sources' terms, then the small
+//     systems' solves; then the replay.
+#include "fec_internal.h"
+
+namespace fecgpu {
+
+namespace {
+
+__constant__ GfTables c_gfs = make_gf_tables();
+
+#define SWD_WAVE_SYNC()                                         \
+    do {                                                        \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); \
+        __builtin_amdgcn_wave_barrier();                        \
+    } while (0)
+
+struct GfLds {
+    uint8_t exp[512];
+    uint8_t log[256];
+};
+__device__ __forceinline__ void gf_load(GfLds &g) {
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) g.exp[i] = c_gfs.exp[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) g.log[i] = c_gfs.log[i];
+}
+__device__ __forceinline__ uint32_t gmul(const GfLds &g, uint32_t a, uint32_t b) {
+    return (a && b) ? g.exp[g.log[a] + g.log[b]] : 0u;
+}
+__device__ __forceinline__ uint32_t ginv(const GfLds &g, uint32_t a) { return g.exp[255 - g.log[a]]; }
+
+// four packed bytes times the coefficient of table t (a_lo, a_hi, b_lo, b_hi, c)
+__device__ __forceinline__ uint32_t tmul(uint32_t x, const uint32_t (&t)[5]) {
+    return __builtin_amdgcn_perm(t[1], t[0], x & 0x07070707u) ^
+           __builtin_amdgcn_perm(t[3], t[2], (x >> 3) & 0x07070707u) ^
+           __builtin_amdgcn_perm(t[4], t[4], (x >> 6) & 0x03030303u);
+}
+__device__ __forceinline__ void set_tab(uint32_t (&t)[5], uint32_t c) {
+    const CoefTab ct = make_coef_tab(c);
+    t[0] = ct.a_lo;
+    t[1] = ct.a_hi;
+    t[2] = ct.b_lo;
+    t[3] = ct.b_hi;
+    t[4] = ct.c;
+}
+
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return (1ull << lane) - 1ull; }
+
+template <class T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = min(v, (uint32_t)__shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = min(v, (uint64_t)__shfl_xor((unsigned long long)v, o));
+    return v;
+}
+
+// First header t in [lo, hi) with fss >= key (headers in fss order), by the
+// whole wave: 64-ary steps, so three rounds of loads for 2^16 headers.
+__device__ uint64_t wave_lower_bound(const fecgpu_sw_repair *h, uint64_t lo, uint64_t hi, uint64_t key, int lane) {
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t pos = min(lo + (uint64_t)(lane + 1) * step, hi) - 1;  // last of segment `lane`
+        const uint64_t b = __ballot(h[pos].fss >= key);
+        if (!b) return hi;
+        const int f = __ffsll((unsigned long long)b) - 1;
+        const uint64_t nlo = lo + (uint64_t)f * step;
+        hi = min(lo + (uint64_t)(f + 1) * step, hi);
+        lo = nlo;
+    }
+    const uint64_t pos = lo + (uint64_t)lane;
+    const uint64_t b = __ballot(pos < hi && h[pos].fss >= key);
+    return b ? lo + (uint64_t)(__ffsll((unsigned long long)b) - 1) : hi;
+}
+
+// ================================================================ plan ===
+// Headers: validity (device headers are checked here; host headers were
+// checked by the caller too), the widest received window, and per source the
+// farthest end of the received repairs starting there.
+__global__ __launch_bounds__(kBlock) void sw_dec_hdr_kernel(SwDecArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool bad = false;
+    uint32_t w = 0;
+    if (t < a.nrep) {
+        const fecgpu_sw_repair h = a.hdr[t];
+        bad = h.nss < 1 || h.nss > kSwMaxWindow || h.dt > 15 || h.fss > a.nsrc || a.nsrc - h.fss < h.nss;
+        if (t > 0 && a.hdr[t - 1].fss > h.fss) bad = true;
+        if (!bad && a.rep_present[t]) {
+            w = h.nss;
+            atomicMax(&a.reach[h.fss], (uint32_t)(h.fss + h.nss));
+        }
+    }
+    w = wave_max(w);
+    const uint64_t anybad = __ballot(bad);
+    if ((threadIdx.x & 63) == 0) {
+        if (w) atomicMax(&a.ctr->wmax, w);
+        if (anybad) atomicOr(&a.ctr->err, 1u);
+    }
+}
+
+// Block per chunk of 4096 sources (16 per thread): statuses (1 = lost), lost
+// count and max reach of the chunk.
+__global__ __launch_bounds__(kBlock) void sw_dec_count_kernel(SwDecArgs a) {
+    __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t i0 = (uint64_t)blockIdx.x * kSwChunk + threadIdx.x * 16u;
+    uint32_t cnt = 0, mx = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint64_t i = i0 + j;
+        if (i < a.nsrc) {
+            const bool lost = a.src_present[i] == 0;
+            cnt += lost;
+            a.stat[i] = lost ? FECGPU_STATUS_UNRECOVERABLE : FECGPU_STATUS_OK;
+            mx = max(mx, a.reach[i]);
+        }
+    }
+    cnt = wave_sum(cnt);
+    mx = wave_max(mx);
+    if (lane == 0) {
+        s_c[wave] = cnt;
+        s_m[wave] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t c = 0, m = 0;
+        for (int w = 0; w < kBlock / 64; w++) {
+            c += s_c[w];
+            m = max(m, s_m[w]);
+        }
+        a.chunk[2 * blockIdx.x] = c;
+        a.chunk[2 * blockIdx.x + 1] = m;
+    }
+}
+
+// One block: exclusive sum of the chunks' lost counts and exclusive max of
+// their reaches; the total lost count.
+__global__ __launch_bounds__(1024) void sw_dec_scan_kernel(SwDecArgs a) {
+    __shared__ uint32_t s_sum[16], s_max[16];
+    __shared__ uint32_t s_cc, s_cm;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_cc = s_cm = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < a.nchunk; b0 += 1024) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint32_t c = b < a.nchunk ? a.chunk[2 * b] : 0u, m = b < a.nchunk ? a.chunk[2 * b + 1] : 0u;
+        uint32_t ic = c, im = m;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(ic, o), ym = __shfl_up(im, o);
+            if (lane >= o) {
+                ic += y;
+                im = max(im, ym);
+            }
+        }
+        uint32_t em = __shfl_up(im, 1);  // exclusive max within the wave
+        if (lane == 0) em = 0;
+        if (lane == 63) {
+            s_sum[wave] = ic;
+            s_max[wave] = im;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = s_cc, am = s_cm;
+            for (int w = 0; w < 16; w++) {
+                const uint32_t ts = s_sum[w], tm = s_max[w];
+                s_sum[w] = acc;
+                s_max[w] = am;
+                acc += ts;
+                am = max(am, tm);
+            }
+            s_cc = acc;
+            s_cm = am;
+        }
+        __syncthreads();
+        if (b < a.nchunk) {
+            a.chunk[2 * b] = s_sum[wave] + ic - c;
+            a.chunk[2 * b + 1] = max(s_max[wave], em);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.ctr->nlost = s_cc;
+}
+
+// Block per chunk: the lost sources in order with the reach at each, and
+// rank[i] = lost sources before i (written over the reach array).
+__global__ __launch_bounds__(kBlock) void sw_dec_lost_kernel(SwDecArgs a) {
+    __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint64_t i0 = (uint64_t)b * kSwChunk + threadIdx.x * 16u;
+    uint32_t r[16], mask = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint64_t i = i0 + j;
+        r[j] = 0;
+        if (i < a.nsrc) {
+            r[j] = a.reach[i];
+            mask |= (a.src_present[i] == 0 ? 1u : 0u) << j;
+        }
+    }
+    uint32_t tm = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) tm = max(tm, r[j]);
+    const uint32_t cnt = __popc(mask);
+    uint32_t ic = cnt, im = tm;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(ic, o), ym = __shfl_up(im, o);
+        if (lane >= o) {
+            ic += y;
+            im = max(im, ym);
+        }
+    }
+    uint32_t em = __shfl_up(im, 1);
+    if (lane == 0) em = 0;
+    if (lane == 63) {
+        s_c[wave] = ic;
+        s_m[wave] = im;
+    }
+    __syncthreads();
+    uint32_t wc = 0, wm = 0;
+    for (int w = 0; w < wave; w++) {
+        wc += s_c[w];
+        wm = max(wm, s_m[w]);
+    }
+    uint32_t off = a.chunk[2 * b] + wc + ic - cnt;
+    uint32_t run = max(max(a.chunk[2 * b + 1], wm), em);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint64_t i = i0 + j;
+        if (i >= a.nsrc) break;
+        run = max(run, r[j]);
+        a.reach[i] = off;  // rank[i]
+        if ((mask >> j) & 1u) {
+            a.lost[off] = (uint32_t)i;
+            a.reachL[off] = run;
+            off++;
+        }
+    }
+    if (i0 <= a.nsrc && a.nsrc <= i0 + 16 && a.nsrc > 0) a.reach[a.nsrc] = off;  // rank[nsrc] = nlost
+}
+
+// ============================================================= systems ===
+constexpr int kSwPitch = kSwSmallE + kSwSmallP;  // LDS row of [A | I] (e <= 64, p <= 96)
+
+// the repair's window holds a lost source of the system lost[x .. x + e)
+__device__ __forceinline__ bool holds(const SwDecArgs &a, const fecgpu_sw_repair &h, uint32_t x, uint32_t e) {
+    const uint32_t r0 = a.reach[h.fss], r1 = a.reach[h.fss + h.nss];
+    return r1 > r0 && r0 < x + e && r1 > x;
+}
+
+// One wave solves the small system lost[x .. x + e) with its p equations
+// (repair indices eq[]): the round-2 sw_plan_kernel, now fed on the device.
+__device__ void small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e, int p, const uint32_t *U,
+                            const uint32_t *eq, uint8_t *M, int8_t *piv, int lane) {
+    const int W = e + p;
+    uint32_t g0 = 0;
+    if (lane == 0) g0 = atomicAdd(&a.ctr->nsyn, (uint32_t)p);
+    g0 = __shfl(g0, 0);
+    for (int q = 0; q < p; q++)
+        for (int j = lane; j < W; j += 64) M[q * kSwPitch + j] = (uint8_t)(j >= e && j - e == q);
+    SWD_WAVE_SYNC();
+    // lane per equation: its coefficients (RFC 8681 §3.6); the lost sources'
+    // go into A, the received sources' into its syndrome job
+    for (int q = lane; q < p; q += 64) {
+        const uint32_t t = eq[q];
+        const fecgpu_sw_repair h = a.hdr[t];
+        uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
+        Tinymt32 st;
+        tinymt32_init(st, h.key);
+        const uint32_t dt = h.dt;
+        int u = 0;
+        uint32_t word = 0;
+        for (int j = 0; j < (int)h.nss; j++) {
+            uint32_t c = 0;
+            if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
+                do {
+                    c = tinymt32_u32(st) & 0xFFu;
+                } while (c == 0);
+            }
+            const uint64_t i = h.fss + (uint64_t)j;
+            while (u < e && U[u] < i) u++;
+            if (u < e && U[u] == i) {
+                M[q * kSwPitch + u] = (uint8_t)c;
+                c = 0;
+            }
+            word |= c << (8 * (j & 3));
+            if ((j & 3) == 3) {
+                cc[j >> 2] = word;
+                word = 0;
+            }
+        }
+        if (h.nss & 3) cc[h.nss >> 2] = word;
+        CombJob J;
+        J.in_off = h.fss * a.stride;
+        J.coef_off = (uint64_t)t * kSwCoefPitch;
+        J.out_list = g0 + q;
+        J.xor_off = (uint64_t)t * a.stride;
+        J.nin = h.nss;
+        J.nout = 1;
+        a.syn_jobs[g0 + q] = J;
+        a.syn_outs[g0 + q] = (uint64_t)(g0 + q) * a.stride;
+    }
+    SWD_WAVE_SYNC();
+    uint64_t used0 = 0, used1 = 0;  // wave-uniform: rows 0..63, 64..95 already pivots
+    for (int col = 0; col < e; col++) {
+        const bool c0 = lane < p && !((used0 >> lane) & 1) && M[lane * kSwPitch + col] != 0;
+        const bool c1 = lane + 64 < p && !((used1 >> lane) & 1) && M[(lane + 64) * kSwPitch + col] != 0;
+        const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
+        int pr = -1;
+        if (b0) pr = (int)__ffsll((unsigned long long)b0) - 1;
+        else if (b1) pr = 64 + (int)__ffsll((unsigned long long)b1) - 1;
+        if (lane == 0) piv[col] = (int8_t)pr;
+        if (pr < 0) continue;  // free column (uniform)
+        if (pr < 64) used0 |= 1ull << pr;
+        else used1 |= 1ull << (pr - 64);
+        uint8_t *P = M + pr * kSwPitch;
+        const uint32_t iv = ginv(g, P[col]);
+        SWD_WAVE_SYNC();
+        for (int j = lane; j < W; j += 64) P[j] = (uint8_t)gmul(g, P[j], iv);
+        SWD_WAVE_SYNC();
+        for (int q = lane; q < p; q += 64) {
+            if (q == pr) continue;
+            uint8_t *row = M + q * kSwPitch;
+            const uint32_t f = row[col];
+            if (!f) continue;
+            for (int j = 0; j < W; j++) row[j] ^= (uint8_t)gmul(g, f, P[j]);
+        }
+        SWD_WAVE_SYNC();
+    }
+    SWD_WAVE_SYNC();
+    bool det = false;
+    int prc = -1;
+    if (lane < e) {
+        prc = piv[lane];
+        det = prc >= 0;
+        for (int j = 0; j < e && det; j++)
+            if (piv[j] < 0 && M[prc * kSwPitch + j]) det = false;
+    }
+    const uint64_t dm = __ballot(det);
+    const int ndet = __popcll(dm);
+    // syndromes no solve reads (non-pivot rows, undetermined unknowns' rows)
+    // are not computed: only pivot rows can appear in a solve row
+    for (int q = lane; q < p; q += 64) {
+        bool need = false;
+        for (int col = 0; col < e && !need; col++) need = ((dm >> col) & 1) && M[piv[col] * kSwPitch + e + q] != 0;
+        if (!need) a.syn_jobs[g0 + q].nout = 0;
+    }
+    if (ndet == 0) return;
+    const int nj = (ndet + 7) / 8;
+    uint32_t j0 = 0, o0 = 0;
+    unsigned long long c0 = 0;
+    if (lane == 0) {
+        j0 = atomicAdd(&a.ctr->nsol, (uint32_t)nj);
+        o0 = atomicAdd(&a.ctr->nouts, (uint32_t)ndet);
+        c0 = atomicAdd(&a.ctr->ncoef, (unsigned long long)ndet * p);
+        atomicAdd(&a.ctr->recovered, (uint32_t)ndet);
+        atomicMax(&a.ctr->maxp, (uint32_t)p);
+    }
+    j0 = __shfl(j0, 0);
+    o0 = __shfl(o0, 0);
+    c0 = __shfl(c0, 0);
+    if (det) {
+        const int d = __popcll(dm & lanes_below(lane));
+        uint8_t *cf = a.sol_coef + c0 + (uint64_t)d * p;
+        for (int t = 0; t < p; t++) cf[t] = M[prc * kSwPitch + e + t];
+        a.sol_outs[o0 + d] = (uint64_t)U[lane] * a.stride;
+        a.stat[U[lane]] = FECGPU_STATUS_OK;
+    }
+    if (lane < nj) {
+        CombJob J;
+        J.in_off = (uint64_t)g0 * a.stride;
+        J.coef_off = c0 + (uint64_t)lane * 8 * p;
+        J.out_list = o0 + (uint64_t)lane * 8;
+        J.xor_off = kNoXor;
+        J.nin = (uint32_t)p;
+        J.nout = (uint32_t)min(8, ndet - 8 * lane);
+        a.sol_jobs[j0 + lane] = J;
+    }
+}
+
+// A wave per lost source; the waves at a system start find its extent and
+// equations and solve it (small) or queue it (long).
+__global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
+    __shared__ GfLds g;
+    __shared__ uint8_t s_M[kBlock / 64][kSwSmallP * kSwPitch];
+    __shared__ uint32_t s_U[kBlock / 64][kSwSmallE];
+    __shared__ uint32_t s_eq[kBlock / 64][kSwSmallP];
+    __shared__ int8_t s_piv[kBlock / 64][kSwSmallE];
+    gf_load(g);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (a.ctr->err & 1u) return;
+    const uint32_t nlost = a.ctr->nlost, wmax = max(1u, a.ctr->wmax);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t x = (uint64_t)blockIdx.x * (kBlock / 64) + wave; x < nlost; x += nwaves) {
+        const uint32_t lx = a.lost[x];
+        if (x > 0 && a.reachL[x - 1] > lx) continue;  // not a system start (uniform)
+        // extent: up to the next start
+        uint32_t e = 1;
+        for (;;) {
+            const uint64_t y = x + e + lane;
+            const bool stop = y >= nlost || a.reachL[y - 1] <= a.lost[y];
+            const uint64_t b = __ballot(stop);
+            if (b) {
+                e += __ffsll((unsigned long long)b) - 1;
+                break;
+            }
+            e += 64;
+        }
+        const uint32_t last = a.lost[x + e - 1];
+        const uint64_t t_lo = wave_lower_bound(a.hdr, 0, a.nrep, lx >= wmax ? lx - wmax + 1 : 0, lane);
+        const uint64_t t_hi = wave_lower_bound(a.hdr, t_lo, a.nrep, (uint64_t)last + 1, lane);
+        bool small = (int)e <= kSwSmallE && (int)e < a.long_min;
+        uint32_t p = 0;
+        if (small) {
+            if (lane < (int)e) s_U[wave][lane] = a.lost[x + lane];
+            for (uint64_t t0 = t_lo; t0 < t_hi; t0 += 64) {
+                const uint64_t t = t0 + lane;
+                bool hd = false;
+                if (t < t_hi && a.rep_present[t]) hd = holds(a, a.hdr[t], (uint32_t)x, e);
+                const uint64_t b = __ballot(hd);
+                const uint32_t n = __popcll(b);
+                if (p + n > (uint32_t)kSwSmallP) {
+                    small = false;
+                    break;
+                }
+                if (hd) s_eq[wave][p + __popcll(b & lanes_below(lane))] = (uint32_t)t;
+                p += n;
+            }
+        }
+        if (!small) {
+            if (lane == 0) {
+                const uint32_t k = atomicAdd(&a.ctr->nlong, 1u);
+                if (k < a.long_cap) {
+                    SwLong L{};
+                    L.x0 = (uint32_t)x;
+                    L.e = e;
+                    L.t_lo = (uint32_t)t_lo;
+                    L.t_hi = (uint32_t)t_hi;
+                    a.longs[k] = L;
+                } else {
+                    atomicOr(&a.ctr->err, 2u);
+                }
+            }
+            continue;
+        }
+        if (p == 0) continue;  // no received repair holds it: stays lost
+        SWD_WAVE_SYNC();
+        small_solve(a, g, (uint32_t)x, (int)e, (int)p, s_U[wave], s_eq[wave], s_M[wave], s_piv[wave], lane);
+    }
+}
+
+// ========================================================= long systems ===
+constexpr int kStg = 64;  // generated rows waiting for admission
+
+struct LongLds {
+    GfLds g;
+    uint8_t rowc[kSwRows][256];  // forward: row coefficients (unknown u at [u & 255]); backward: VT
+    uint8_t stg[kStg][256];      // generated rows
+    uint32_t stg_t[kStg], stg_lo[kStg], stg_hi[kStg];
+    uint32_t act[kSwRows];       // alive rows (slots), in admission order
+    uint32_t row_hi[kSwRows], row_t[kSwRows];
+    uint8_t freel[kSwRows];      // free slots (stack)
+    uint8_t fq[kSwRows];         // elimination factor per alive position
+    uint8_t prow[256];           // backward: the pivot row
+};
+
+__device__ __forceinline__ void emit(SwOp *op, uint32_t kind, uint32_t sa, uint32_t sb, uint32_t aux, uint32_t aux2,
+                                     const uint32_t (&tab)[5]) {
+    SwOp o;
+    o.op = kind | (sa << 8) | (sb << 16);
+    o.aux = aux;
+#pragma unroll
+    for (int i = 0; i < 5; i++) o.tab[i] = tab[i];
+    o.aux2 = aux2;
+    *op = o;
+}
+
+// Generate the next batch of rows (up to 64 equations from repair *next on)
+// into the staging area; returns the number staged (0: no more repairs).
+__device__ int long_refill(const SwDecArgs &a, LongLds &L, const SwLong &S, uint64_t &next, int lane) {
+    int n = 0;
+    while (n == 0 && next < S.t_hi) {
+        const uint64_t t = next + lane;
+        bool hd = false;
+        fecgpu_sw_repair h{};
+        if (t < S.t_hi && a.rep_present[t]) {
+            h = a.hdr[t];
+            hd = holds(a, h, S.x0, S.e);
+        }
+        const uint64_t b = __ballot(hd);
+        n = __popcll(b);
+        if (hd) {
+            const int k = __popcll(b & lanes_below(lane));
+            const uint32_t lo = a.reach[h.fss] - S.x0, hi = a.reach[h.fss + h.nss] - 1 - S.x0;
+            L.stg_t[k] = (uint32_t)t;
+            L.stg_lo[k] = lo;
+            L.stg_hi[k] = hi;
+            uint8_t *row = L.stg[k];
+            for (uint32_t u = lo; u <= hi; u++) row[u & 255] = 0;
+            uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
+            Tinymt32 st;
+            tinymt32_init(st, h.key);
+            const uint32_t dt = h.dt;
+            uint32_t word = 0;
+            for (int j = 0; j < (int)h.nss; j++) {
+                uint32_t c = 0;
+                if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
+                    do {
+                        c = tinymt32_u32(st) & 0xFFu;
+                    } while (c == 0);
+                }
+                const uint64_t i = h.fss + (uint64_t)j;
+                if (!a.src_present[i]) {
+                    row[(a.reach[i] - S.x0) & 255] = (uint8_t)c;
+                    c = 0;
+                }
+                word |= c << (8 * (j & 3));
+                if ((j & 3) == 3) {
+                    cc[j >> 2] = word;
+                    word = 0;
+                }
+            }
+            if (h.nss & 3) cc[h.nss >> 2] = word;
+        }
+        next += 64;
+    }
+    SWD_WAVE_SYNC();
+    return n;
+}
+
+// A wave per long system: forward elimination, null-space sweep, logs.
+__global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
+    extern __shared__ uint4 dyn_long[];
+    LongLds &L = *reinterpret_cast<LongLds *>(dyn_long);
+    gf_load(L.g);
+    __syncthreads();
+    const int lane = threadIdx.x;
+    if (a.ctr->err & 1u) return;
+    const uint32_t nlong = min(a.ctr->nlong, (uint32_t)a.long_cap);
+    uint32_t notab[5] = {0, 0, 0, 0, 0};
+    for (uint32_t k = blockIdx.x; k < nlong; k += gridDim.x) {
+        SwLong S = a.longs[k];
+        const uint32_t e = S.e, x0 = S.x0;
+        // pass 0: equations and their total width, for the log's reservation
+        uint32_t p = 0;
+        unsigned long long wsum = 0;
+        for (uint64_t t0 = S.t_lo; t0 < S.t_hi; t0 += 64) {
+            const uint64_t t = t0 + lane;
+            bool hd = false;
+            uint32_t w = 0;
+            if (t < S.t_hi && a.rep_present[t]) {
+                const fecgpu_sw_repair h = a.hdr[t];
+                hd = holds(a, h, x0, e);
+                if (hd) w = a.reach[h.fss + h.nss] - a.reach[h.fss];
+            }
+            p += __popcll(__ballot(hd));
+            wsum += wave_sum((unsigned long long)w);
+        }
+        S.ok = 0;
+        S.nfwd = S.nbwd = 0;
+        if (p == 0) {
+            if (lane == 0) a.longs[k] = S;
+            continue;
+        }
+        const unsigned long long need = 2ull * p + 2ull * wsum + 2ull * e;
+        const uint32_t npmax = min(p, e);
+        unsigned long long base = 0;
+        uint32_t piv0 = 0;
+        if (lane == 0) {
+            base = atomicAdd(&a.ctr->nlog, need);
+            piv0 = atomicAdd(&a.ctr->npiv, npmax);
+        }
+        base = __shfl(base, 0);
+        piv0 = __shfl(piv0, 0);
+        if (base + need > a.log_cap || (uint64_t)piv0 + npmax > a.piv_cap) {
+            if (lane == 0) {
+                atomicOr(&a.ctr->err, 2u);
+                a.longs[k] = S;
+            }
+            continue;
+        }
+        SwOp *fwd = a.log + base;
+        SwOp *bwd = fwd + p + wsum + p;
+        // ---- forward elimination ----
+        for (int i = lane; i < kSwRows; i += 64) L.freel[i] = (uint8_t)(kSwRows - 1 - i);
+        int nfree = kSwRows, nact = 0, sh = 0, sn = 0;
+        uint32_t nf = 0, npiv = 0, B = 1;
+        uint64_t next = S.t_lo;
+        bool fail = false;
+        SWD_WAVE_SYNC();
+        for (uint32_t c = 0; c < e && !fail; c++) {
+            // admit the rows whose range starts here
+            for (;;) {
+                if (sh == sn) {
+                    if (next >= S.t_hi) break;
+                    sn = long_refill(a, L, S, next, lane);
+                    sh = 0;
+                    if (sn == 0) break;
+                }
+                if (L.stg_lo[sh] > c) break;  // rows arrive in order of lo, and every lo <= c is admitted by now
+                if (nfree == 0) {
+                    fail = true;
+                    break;
+                }
+                const uint32_t slot = L.freel[--nfree];
+                reinterpret_cast<uint32_t *>(L.rowc[slot])[lane] = reinterpret_cast<const uint32_t *>(L.stg[sh])[lane];
+                if (lane == 0) {
+                    L.row_hi[slot] = L.stg_hi[sh];
+                    L.row_t[slot] = L.stg_t[sh];
+                    L.act[nact] = slot;
+                    a.synrow[L.stg_t[sh]] = ~0u;
+                    emit(fwd + nf, kOpLoad, slot, 0, L.stg_t[sh], 0, notab);
+                }
+                nact++;
+                nf++;
+                sh++;
+                SWD_WAVE_SYNC();
+            }
+            if (fail) break;
+            // pivot: the alive row with a nonzero at c whose range ends first
+            const uint32_t cs = c & 255;
+            uint64_t best = ~0ull;
+            for (int i = lane; i < nact; i += 64) {
+                const uint32_t s = L.act[i];
+                if (L.rowc[s][cs]) best = min(best, ((uint64_t)L.row_hi[s] << 9) | (uint64_t)i);
+            }
+            best = wave_min64(best);
+            if (best == ~0ull) {
+                if (lane == 0) a.colpiv[x0 + c] = ~0u;
+            } else {
+                const int ppos = (int)(best & 511);
+                const uint32_t P = L.act[ppos];
+                const uint32_t hiP = L.row_hi[P];
+                const uint32_t ip = ginv(L.g, L.rowc[P][cs]);
+                // factors and ELIM entries
+                uint32_t ne = 0;
+                for (int i0 = 0; i0 < nact; i0 += 64) {
+                    const int i = i0 + lane;
+                    uint32_t f = 0;
+                    if (i < nact && i != ppos) f = gmul(L.g, L.rowc[L.act[i]][cs], ip);
+                    if (i < nact) L.fq[i] = (uint8_t)f;
+                    const uint64_t b = __ballot(f != 0);
+                    if (f) {
+                        uint32_t tab[5];
+                        set_tab(tab, f);
+                        emit(fwd + nf + ne + __popcll(b & lanes_below(lane)), kOpElim, L.act[i], P, 0, 0, tab);
+                    }
+                    ne += __popcll(b);
+                }
+                nf += ne;
+                SWD_WAVE_SYNC();
+                // row updates over [c, hiP]: lanes over (alive position, column) pairs
+                const uint32_t wP = hiP - c + 1;
+                const uint32_t total = (uint32_t)nact * wP;
+                for (uint32_t w0 = 0; w0 < total; w0 += 64) {
+                    const uint32_t wi = w0 + lane;
+                    if (wi < total) {
+                        const uint32_t i = wi / wP, j = c + wi % wP;
+                        const uint32_t f = L.fq[i];
+                        if (f) {
+                            uint8_t *r = &L.rowc[L.act[i]][j & 255];
+                            *r ^= (uint8_t)gmul(L.g, f, L.rowc[P][j & 255]);
+                        }
+                    }
+                }
+                SWD_WAVE_SYNC();
+                // the pivot row: coefficients to the pivot area, STORE
+                const uint32_t pv = piv0 + npiv;
+                reinterpret_cast<uint32_t *>(a.pivcoef + (uint64_t)pv * 256)[lane] =
+                    reinterpret_cast<const uint32_t *>(L.rowc[P])[lane];
+                if (lane == 0) {
+                    a.pivhi[pv] = hiP;
+                    a.pivt[pv] = L.row_t[P];
+                    a.colpiv[x0 + c] = pv;
+                    emit(fwd + nf, kOpStore, P, 0, pv, 0, notab);
+                }
+                nf++;
+                npiv++;
+                B = max(B, wP);
+            }
+            // retire the pivot and the rows whose range ends at c (now zero)
+            const uint32_t P = best == ~0ull ? ~0u : L.act[best & 511];
+            int keep = 0;
+            for (int i0 = 0; i0 < nact; i0 += 64) {
+                const int i = i0 + lane;
+                const uint32_t s = i < nact ? L.act[i] : 0u;
+                const bool live = i < nact && s != P && L.row_hi[s] > c;
+                const bool dead = i < nact && !live;
+                const uint64_t bl = __ballot(live), bd = __ballot(dead);
+                SWD_WAVE_SYNC();
+                if (live) L.act[keep + __popcll(bl & lanes_below(lane))] = s;
+                if (dead) L.freel[nfree + __popcll(bd & lanes_below(lane))] = (uint8_t)s;
+                keep += __popcll(bl);
+                nfree += __popcll(bd);
+                SWD_WAVE_SYNC();
+            }
+            nact = keep;
+        }
+        if (fail) {  // more rows alive than kSwRows: the system stays lost
+            if (lane == 0) {
+                atomicOr(&a.ctr->err, 4u);
+                a.longs[k] = S;
+            }
+            continue;
+        }
+        // syndrome jobs for the pivot rows (the only rows whose data is used)
+        uint32_t g0 = 0;
+        if (lane == 0) g0 = atomicAdd(&a.ctr->nsyn, npiv);
+        g0 = __shfl(g0, 0);
+        for (uint32_t q = lane; q < npiv; q += 64) {
+            const uint32_t t = a.pivt[piv0 + q];
+            const fecgpu_sw_repair h = a.hdr[t];
+            CombJob J;
+            J.in_off = h.fss * a.stride;
+            J.coef_off = (uint64_t)t * kSwCoefPitch;
+            J.out_list = g0 + q;
+            J.xor_off = (uint64_t)t * a.stride;
+            J.nin = h.nss;
+            J.nout = 1;
+            a.syn_jobs[g0 + q] = J;
+            a.syn_outs[g0 + q] = (uint64_t)(g0 + q) * a.stride;
+            a.synrow[t] = g0 + q;
+        }
+        // ---- null-space sweep and back substitution log ----
+        // VT[coordinate & 255][vector] bytes (LDS rowc), nv vectors
+        uint8_t(*VT)[256] = L.rowc;
+        uint32_t nv = 0, nb = 0, ndet = 0;
+        for (int c = (int)e - 1; c >= 0; c--) {
+            const uint32_t cs = (uint32_t)c & 255;
+            const uint32_t pv = a.colpiv[x0 + c];
+            if (pv == ~0u) {
+                if (nv == (uint32_t)kSwRows) {
+                    // reduce to a basis of the projection on [c + 1, c + B)
+                    uint32_t rank = 0;
+                    for (uint32_t jj = 1; jj < B && rank < nv; jj++) {
+                        const uint32_t s = (uint32_t)(c + jj) & 255;
+                        uint32_t first = ~0u;
+                        for (uint32_t v = rank + lane; v < nv; v += 64)
+                            if (VT[s][v]) first = min(first, v);
+                        first = wave_min(first);
+                        if (first == ~0u) continue;
+                        if (first != rank)
+                            for (int cc2 = lane; cc2 < 256; cc2 += 64) {
+                                const uint8_t t0 = VT[cc2][first];
+                                VT[cc2][first] = VT[cc2][rank];
+                                VT[cc2][rank] = t0;
+                            }
+                        SWD_WAVE_SYNC();
+                        const uint32_t iv = ginv(L.g, VT[s][rank]);
+                        // eliminate coordinate s from the vectors after `rank`
+                        const uint32_t nvv = nv - rank - 1;
+                        for (uint32_t w0 = 0; w0 < nvv * B; w0 += 64) {
+                            const uint32_t wi = w0 + lane;
+                            if (wi < nvv * B) {
+                                const uint32_t v = rank + 1 + wi / B, s2 = (uint32_t)(c + wi % B) & 255;
+                                const uint32_t f = gmul(L.g, VT[s][v], iv);
+                                if (f && s2 != s) VT[s2][v] ^= (uint8_t)gmul(L.g, f, VT[s2][rank]);
+                            }
+                        }
+                        SWD_WAVE_SYNC();
+                        for (uint32_t v = rank + 1 + lane; v < nv; v += 64) VT[s][v] = 0;
+                        SWD_WAVE_SYNC();
+                        rank++;
+                    }
+                    nv = rank;
+                }
+                // coordinate c of every vector is 0; the new vector is e_c
+                reinterpret_cast<uint32_t *>(VT[cs])[lane] = 0;
+                SWD_WAVE_SYNC();
+                for (int cc2 = lane; cc2 < 256; cc2 += 64) VT[cc2][nv] = (uint8_t)(cc2 == (int)cs);
+                nv++;
+                if (lane == 0) emit(bwd + nb, kOpXFree, cs, 0, 0, 0, notab);
+                nb++;
+                SWD_WAVE_SYNC();
+                continue;
+            }
+            reinterpret_cast<uint32_t *>(L.prow)[lane] = reinterpret_cast<const uint32_t *>(a.pivcoef + (uint64_t)pv * 256)[lane];
+            const uint32_t hi = a.pivhi[pv];
+            SWD_WAVE_SYNC();
+            const uint32_t ip = ginv(L.g, L.prow[cs]);
+            uint32_t det = 1;
+            if (nv) {
+                uint32_t acc = 0;
+                for (uint32_t j = (uint32_t)c + 1; j <= hi; j++) {
+                    const uint32_t cj = L.prow[j & 255];
+                    if (!cj) continue;
+                    uint32_t tab[5];
+                    set_tab(tab, cj);
+                    acc ^= tmul(reinterpret_cast<const uint32_t *>(VT[j & 255])[lane], tab);
+                }
+                uint32_t tip[5];
+                set_tab(tip, ip);
+                acc = tmul(acc, tip);
+                // bytes of vectors >= nv are not vectors
+                const uint32_t v0 = 4u * lane;
+                const uint32_t keepm = v0 + 4 <= nv ? 0xFFFFFFFFu : v0 >= nv ? 0u : (0xFFFFFFFFu >> (8 * (v0 + 4 - nv)));
+                acc &= keepm;
+                reinterpret_cast<uint32_t *>(VT[cs])[lane] = acc;
+                det = __ballot(acc != 0) ? 0u : 1u;
+            }
+            // back substitution entries: x_c = ip * y_P + sum (ip * a_Pj) x_j
+            {
+                uint32_t tip[5];
+                set_tab(tip, ip);
+                if (lane == 0) emit(bwd + nb, kOpXBegin, cs, 0, pv, 0, tip);
+                nb++;
+                const uint32_t w = hi - (uint32_t)c;
+                for (uint32_t j0 = 0; j0 < w; j0 += 64) {
+                    const uint32_t j = (uint32_t)c + 1 + j0 + lane;
+                    const uint32_t cj = j0 + lane < w ? L.prow[j & 255] : 0u;
+                    const uint64_t b = __ballot(cj != 0);
+                    if (cj) {
+                        uint32_t tab[5];
+                        set_tab(tab, gmul(L.g, cj, ip));
+                        emit(bwd + nb + __popcll(b & lanes_below(lane)), kOpXTerm, j & 255, 0, 0, 0, tab);
+                    }
+                    nb += __popcll(b);
+                }
+                const uint32_t src_i = a.lost[x0 + c];
+                if (lane == 0) emit(bwd + nb, kOpXEnd, 0, cs, det ? src_i : ~0u, 0, notab);
+                nb++;
+            }
+            if (det) {
+                if (lane == 0) a.stat[a.lost[x0 + c]] = FECGPU_STATUS_OK;
+                ndet++;
+            }
+            SWD_WAVE_SYNC();
+        }
+        if (lane == 0) {
+            S.ok = 1;
+            S.fwd = base;
+            S.nfwd = nf;
+            S.bwd = base + p + wsum + p;
+            S.nbwd = nb;
+            S.piv0 = piv0;
+            a.longs[k] = S;
+            if (ndet) atomicAdd(&a.ctr->recovered, ndet);
+        }
+    }
+}
+
+// A wave per (long system, 64-dword column chunk): replay the log.
+__global__ __launch_bounds__(64) void sw_dec_replay_kernel(SwDecArgs a) {
+    __shared__ uint32_t slots[kSwRows][64];
+    const int lane = threadIdx.x;
+    if (a.ctr->err & 1u) return;
+    const uint32_t nlong = min(a.ctr->nlong, (uint32_t)a.long_cap);
+    const uint32_t ndw = ((a.S + 15u) >> 4) * 4u;  // whole 16-B columns, as the combine passes
+    const uint32_t nch = (ndw + 63) / 64;
+    const uint64_t units = (uint64_t)nlong * nch;
+    for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+        const uint32_t s = (uint32_t)(u / nch), ch = (uint32_t)(u % nch);
+        const SwLong S = a.longs[s];
+        if (!S.ok) continue;
+        const uint32_t dw = ch * 64 + lane;
+        const bool live = dw < ndw;
+        const uint64_t boff = (uint64_t)dw * 4;
+        const SwOp *op = a.log + S.fwd;
+        for (uint32_t i = 0; i < S.nfwd; i++) {
+            const SwOp o = op[i];
+            const uint32_t kind = o.op & 0xFFu, sa = (o.op >> 8) & 0xFFu, sb = (o.op >> 16) & 0xFFu;
+            if (kind == kOpElim) {
+                const uint32_t t[5] = {o.tab[0], o.tab[1], o.tab[2], o.tab[3], o.tab[4]};
+                slots[sa][lane] ^= tmul(slots[sb][lane], t);
+            } else if (kind == kOpLoad) {
+                const uint32_t g = a.synrow[o.aux];
+                uint32_t v = 0;
+                if (g != ~0u && live) v = *reinterpret_cast<const uint32_t *>(a.synd + (uint64_t)g * a.stride + boff);
+                slots[sa][lane] = v;
+            } else if (kind == kOpStore) {
+                if (live) *reinterpret_cast<uint32_t *>(a.pivdata + (uint64_t)o.aux * a.stride + boff) = slots[sa][lane];
+            }
+        }
+        op = a.log + S.bwd;
+        uint32_t x = 0;
+        for (uint32_t i = 0; i < S.nbwd; i++) {
+            const SwOp o = op[i];
+            const uint32_t kind = o.op & 0xFFu, sa = (o.op >> 8) & 0xFFu, sb = (o.op >> 16) & 0xFFu;
+            const uint32_t t[5] = {o.tab[0], o.tab[1], o.tab[2], o.tab[3], o.tab[4]};
+            if (kind == kOpXTerm) {
+                x ^= tmul(slots[sa][lane], t);
+            } else if (kind == kOpXBegin) {
+                x = live ? tmul(*reinterpret_cast<const uint32_t *>(a.pivdata + (uint64_t)o.aux * a.stride + boff), t)
+                         : 0u;
+            } else if (kind == kOpXEnd) {
+                slots[sb][lane] = x;
+                if (o.aux != ~0u && live) *reinterpret_cast<uint32_t *>(a.src + (uint64_t)o.aux * a.stride + boff) = x;
+            } else if (kind == kOpXFree) {
+                slots[sa][lane] = 0;
+            }
+        }
+    }
+}
+
+int cu_count() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
+    return cus;
+}
+
+}  // namespace
+
+hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
+    if (a.nrep) hipLaunchKernelGGL(sw_dec_hdr_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(sw_dec_count_kernel, dim3(a.nchunk), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(sw_dec_scan_kernel, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(sw_dec_lost_kernel, dim3(a.nchunk), dim3(kBlock), 0, s, a);
+    if (a.nrep) {
+        // a wave per lost source at most; persistent beyond two blocks per CU
+        const uint64_t want = (a.nsrc + kBlock / 64 - 1) / (kBlock / 64);
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 2));
+        hipLaunchKernelGGL(sw_dec_sys_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_sw_dec_long(const SwDecArgs &a, hipStream_t s) {
+    if (a.nrep == 0) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(sw_dec_long_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(LongLds));
+    if (e != hipSuccess) return e;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(a.long_cap, (uint64_t)cu_count()));
+    hipLaunchKernelGGL(sw_dec_long_kernel, dim3(grid), dim3(64), sizeof(LongLds), s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sw_dec_replay(const SwDecArgs &a, hipStream_t s) {
+    if (a.nrep == 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(a.long_cap * 64, (uint64_t)cu_count() * 4));
+    hipLaunchKernelGGL(sw_dec_replay_kernel, dim3(grid), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace fecgpu

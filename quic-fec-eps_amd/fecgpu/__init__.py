@@ -57,7 +57,7 @@ EXPORTS = (
     "fecgpu_decoder_tick",
     "fecgpu_frame_source_id_len", "fecgpu_frame_write_source_id", "fecgpu_frame_repair_len",
     "fecgpu_frame_write_repair", "fecgpu_frame_write_repair_header", "fecgpu_frame_parse",
-    "fecgpu_sw_encode", "fecgpu_sw_decode",
+    "fecgpu_sw_encode", "fecgpu_sw_decode", "fecgpu_sw_decode_device",
     "fecgpu_frame_write_sw_source", "fecgpu_frame_write_sw_repair",
     "fecgpu_sw_encoder_new", "fecgpu_sw_encoder_free", "fecgpu_sw_encoder_add_source",
     "fecgpu_sw_encoder_flush", "fecgpu_sw_encoder_next_repair",
@@ -66,7 +66,7 @@ EXPORTS = (
     "fecgpu_sw_decoder_next_recovered",
 )
 FRAME_SW_SOURCE, FRAME_SW_REPAIR = 0xFEC2, 0xFEC3
-SW_MAX_WINDOW, SW_MAX_UNKNOWNS, SW_MAX_EQUATIONS = 255, 64, 96
+SW_MAX_WINDOW = 255
 # fecgpu_sw_repair as a numpy dtype (16 bytes, the C layout)
 SW_REPAIR_DTYPE = [("fss", "<u8"), ("nss", "<u2"), ("key", "<u2"), ("dt", "u1"), ("reserved", "u1", (3,))]
 FRAME_SOURCE_ID, FRAME_REPAIR = 0xFEC0, 0xFEC4
@@ -207,6 +207,7 @@ def _lib():
             "fecgpu_frame_parse": (sz, [vp, ctypes.c_size_t, ctypes.POINTER(fecgpu_frame)]),
             "fecgpu_sw_encode": (sz, [vp, vp, u64, vp, vp, u64, u32, u32, u32, u32, vp]),
             "fecgpu_sw_decode": (sz, [vp, vp, vp, u64, vp, vp, vp, u64, u32, u32, vp, u32, vp]),
+            "fecgpu_sw_decode_device": (sz, [vp, vp, vp, u64, vp, vp, vp, u64, u32, u32, vp, u32, vp]),
             "fecgpu_frame_write_sw_source": (sz, [vp, ctypes.c_size_t, u64]),
             "fecgpu_frame_write_sw_repair": (sz, [vp, ctypes.c_size_t, ctypes.POINTER(fecgpu_sw_repair), vp,
                                                   ctypes.c_size_t]),
@@ -376,6 +377,15 @@ class Context:
             self._h, _ptr(src), _ptr(src_present), nsrc, _ptr(rep), _ptr(rep_present), _ptr(hdr),
             nrep, sym_len, stride, _ptr(src_status), flags,
             _stream(stream) if not flags & F_HOST_PTRS else None), "fecgpu_sw_decode")
+
+    def sw_decode_device(self, src, src_present, rep, rep_present, hdr, src_status, *, nsrc: int,
+                         nrep: int, sym_len: int, stride: int, flags: int = 0, stream=None) -> int:
+        """fecgpu_sw_decode_device: the same decode with the bookkeeping (flags, headers,
+        statuses) in device memory too.  Asynchronous (returns 0) unless flags has F_SYNC,
+        which returns the number recovered."""
+        return _check(_lib().fecgpu_sw_decode_device(
+            self._h, _ptr(src), _ptr(src_present), nsrc, _ptr(rep), _ptr(rep_present), _ptr(hdr),
+            nrep, sym_len, stride, _ptr(src_status), flags, _stream(stream)), "fecgpu_sw_decode_device")
 
     def synth_batch(self, code: Code, workload: int, seed: int, w0: int, win, sym_len, *,
                     L: int, stride: int, nwin: int, stream=None) -> int:

@@ -49,7 +49,6 @@ for s in "$@"; do
                    python bench.py ;;  # the driver's default command, as is
         prof5) prof prof5 5 ;;
         prof7) prof prof7 7 ;;
-        swplan) step swplan 120 ./scripts/sw_plan_probe ;;
         abvar7)  # cfg7: default build vs every lib/libfecgpu_*.so variant (no check build), interleaved 3 times
             for rep in 1 2 3; do
                 step abvar7_base_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
