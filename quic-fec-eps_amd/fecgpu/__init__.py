@@ -320,6 +320,10 @@ class Context:
         else:
             rc = _lib().fecgpu_ctx_new(None, 0, ctypes.byref(self._h))
         _check(rc, "fecgpu_ctx_new")
+        # per-connection objects made from this ctx: the C ABI requires them freed
+        # before the ctx, so close() frees whatever is still open first
+        import weakref
+        self._children = weakref.WeakSet()
 
     @property
     def handle(self):
@@ -330,6 +334,8 @@ class Context:
 
     def close(self):
         if self._h:
+            for child in list(self._children):
+                child.close()
             _lib().fecgpu_ctx_free(self._h)
             self._h = ctypes.c_void_p()
 
@@ -435,6 +441,7 @@ class Encoder:
 
     def __init__(self, ctx: Context, code: Code, max_len: int, batch: int = 64):
         self._ctx = ctx  # keep the ctx alive
+        ctx._children.add(self)
         self.code = code
         self._h = ctypes.c_void_p()
         _check(_lib().fecgpu_encoder_new(ctx.handle, ctypes.byref(code.c), max_len, batch,
@@ -492,6 +499,7 @@ class Decoder:
 
     def __init__(self, ctx: Context, code: Code, max_len: int, batch: int = 64):
         self._ctx = ctx
+        ctx._children.add(self)
         self.code = code
         self._h = ctypes.c_void_p()
         _check(_lib().fecgpu_decoder_new(ctx.handle, ctypes.byref(code.c), max_len, batch,
@@ -569,6 +577,7 @@ class SwEncoder:
 
     def __init__(self, ctx: Context, params: fecgpu_sw_params):
         self._ctx = ctx
+        ctx._children.add(self)
         self.params = params
         self._h = ctypes.c_void_p()
         _check(_lib().fecgpu_sw_encoder_new(ctx.handle, ctypes.byref(params), ctypes.byref(self._h)),
@@ -611,6 +620,7 @@ class SwDecoder:
 
     def __init__(self, ctx: Context, params: fecgpu_sw_params):
         self._ctx = ctx
+        ctx._children.add(self)
         self.params = params
         self._h = ctypes.c_void_p()
         _check(_lib().fecgpu_sw_decoder_new(ctx.handle, ctypes.byref(params), ctypes.byref(self._h)),

@@ -297,9 +297,12 @@ class SwBatch:
     """Config 7: one sliding-window RLC stream per rank (RFC 8681 with m = 8):
     nsrc = nwin * k sources of L bytes resident in HBM, nwin repairs, a repair
     after every k sources over the last `window` (repair_key = its index, DT 15).
-    One step = fecgpu_sw_encode of every repair, then fecgpu_sw_decode at the
-    config's loss rate (the receiver's arrival flags are host data, so the decode
-    call plans on the host and waits for its kernels)."""
+    One step = fecgpu_sw_encode of every repair, then the decode at the config's
+    loss rate.  The receiver's bookkeeping (arrival flags, headers, statuses) is
+    kept on the device and the decode is planned there too
+    (fecgpu_sw_decode_device, asynchronous like the encode); `host_meta` uses
+    fecgpu_sw_decode instead (flags and headers copied up, statuses down, one
+    synchronous call)."""
     cfg: Config
     nsrc: int
     nrep: int
@@ -310,6 +313,10 @@ class SwBatch:
     sp: "np.ndarray"         # source arrived flags
     rp: "np.ndarray"         # repair arrived flags
     st: "np.ndarray"         # per-source status of the last decode
+    d_sp: torch.Tensor = None  # the flags and statuses on the device
+    d_rp: torch.Tensor = None
+    d_st: torch.Tensor = None
+    host_meta: bool = False
 
     @staticmethod
     def allocate(cfg: Config, nwin: int, dev) -> "SwBatch":
@@ -335,16 +342,30 @@ class SwBatch:
         rng = np.random.default_rng(SEED + w0)
         self.sp[:] = rng.random(self.nsrc) >= self.cfg.loss
         self.rp[:] = rng.random(self.nrep) >= self.cfg.loss
+        dev = self.src.device
+        self.d_sp = torch.from_numpy(self.sp).to(dev)
+        self.d_rp = torch.from_numpy(self.rp).to(dev)
+        self.d_st = torch.zeros(self.nsrc, dtype=torch.uint8, device=dev)
 
     def encode(self, ctx: Context) -> None:
         c = self.cfg
         ctx.sw_encode(self.src, self.rep, self.d_hdr, nsrc=self.nsrc, nrep=self.nrep, sym_len=c.L,
                       stride=c.stride, max_window=c.window)
 
-    def decode(self, ctx: Context) -> int:
+    def decode(self, ctx: Context, sync: bool = False) -> int:
+        """Asynchronous (returns 0) unless `sync` or host_meta: then the number recovered,
+        with self.st holding the statuses."""
+        from . import F_SYNC
         c = self.cfg
-        return ctx.sw_decode(self.src, self.sp, self.rep, self.rp, self.hdr, self.st, nsrc=self.nsrc,
-                             nrep=self.nrep, sym_len=c.L, stride=c.stride)
+        if self.host_meta:
+            return ctx.sw_decode(self.src, self.sp, self.rep, self.rp, self.hdr, self.st, nsrc=self.nsrc,
+                                 nrep=self.nrep, sym_len=c.L, stride=c.stride)
+        n = ctx.sw_decode_device(self.src, self.d_sp, self.rep, self.d_rp, self.d_hdr, self.d_st,
+                                 nsrc=self.nsrc, nrep=self.nrep, sym_len=c.L, stride=c.stride,
+                                 flags=F_SYNC if sync else 0)
+        if sync:
+            self.st[:] = self.d_st.cpu().numpy()
+        return n
 
     def source_bytes(self) -> int:
         return self.nsrc * self.cfg.L
@@ -374,7 +395,7 @@ class SwBatch:
         saved = self.src.clone()
         lost = torch.from_numpy(self.sp == 0).to(self.src.device)
         self.src[lost] = 0xAB
-        n = self.decode(ctx)
+        n = self.decode(ctx, sync=True)
         torch.cuda.synchronize()
         ok = torch.from_numpy(self.st == STATUS_OK).to(self.src.device)
         mism = int((ok & ~(self.src[:, :c.L] == saved[:, :c.L]).all(1)).sum().item())

@@ -113,7 +113,7 @@ def test_sw_encoder_survives_failed_launches(ctx):
     E, W, step, batch, n = 64, 8, 2, 4, 120
     rng = np.random.default_rng(3)
     pk = packets(rng, n, E, "fixed")
-    enc = fecgpu.SwEncoder(ctx, fecgpu.sw_params(E, W, step, batch=batch))
+    enc = fecgpu.SwEncoder(ctx, fecgpu.sw_params(E, W, step, framing="fixed", batch=batch))
     reps, i, failed = [], 0, 0
     ctx.set_tuning("fault_launches", 5)
     while i < n:
@@ -133,9 +133,9 @@ def test_sw_encoder_survives_failed_launches(ctx):
     hdr = [h for h, _ in reps]
     assert [h[2] for h in hdr] == list(range(n // step))
     ref = O.sw_encode(frame(pk, E, "fixed"), hdr_array(hdr), E)
+    enc.close()
     for t, (_, sym) in enumerate(reps):
         assert sym == ref[t, :E].tobytes(), t
-    enc.close()
 
 
 def test_sw_decoder_rejects_overlong_window_before_advancing(ctx):
