@@ -249,9 +249,8 @@ constexpr int kSwChunk = 4096;  // sources per planning chunk
 struct SwDecCtr {  // per call, zeroed before the first kernel
     uint32_t nlost, wmax, maxp, err;   // err: bit 0 bad header; bit 1 log / pivot-area capacity
                                        // exceeded (retry larger); bit 2 more than kSwRows rows alive
-    uint32_t nsyn, nsol, nouts, nlong; // syndrome jobs, solve jobs, solve outputs, long systems
-    uint32_t npiv, recovered, pad0, pad1;
-    unsigned long long ncoef, nlog;    // solve coefficient bytes, long-system log entries
+    uint32_t neq, nlong, npiv, recovered;  // equations (= syndrome job slots), long systems, pivot rows
+    unsigned long long nlog;           // long-system log entries
 };
 // one long system: lost[x0 .. x0 + e), candidate repairs [t_lo, t_hi); its
 // forward / backward logs and first pivot row (set by the planner)
@@ -276,17 +275,22 @@ struct SwDecArgs {
     uint64_t nsrc, nrep;
     uint32_t stride, S, nchunk;
     int long_min;                              // systems with e >= long_min take the long path
-    uint32_t *reach;                           // [nsrc] max window end of the received repairs starting there
-    uint32_t *chunk;                           // [2 * nchunk] lost count / max reach per chunk, then scanned
+    uint32_t *reach;                           // [nsrc + 1] max window end of the received repairs
+                                               // starting there, then rank[i] = lost sources before i
+    uint32_t *rcnt;                            // [nsrc + 1] repairs starting there, then repfirst[i] =
+                                               // repairs starting before i
+    uint32_t *chunk;                           // [3 * nchunk] lost count / max reach / repairs per chunk,
+                                               // then their exclusive scans
+    uint32_t *echunk;                          // [nrep / 4096 + 1] equations per repair chunk, then scanned
+    uint32_t *eqidx;                           // [nrep] equation number of repair t (equations only)
     uint32_t *lost, *reachL;                   // [nsrc] lost sources; prefix max of reach at each
     SwDecCtr *ctr;
-    CombJob *syn_jobs;                         // [nrep]
+    CombJob *syn_jobs;                         // [nrep] syndrome job of equation g
     uint64_t *syn_outs;                        // [nrep]
     uint8_t *coef;                             // [nrep][kSwCoefPitch]: repair t's syndrome coefficients
-    CombJob *sol_jobs;                         // [sol_cap]
-    uint64_t *sol_outs;                        // [outs_cap]
-    uint8_t *sol_coef;                         // [coef_cap]
-    uint64_t sol_cap, outs_cap, coef_cap;
+    CombJob *sol_jobs;                         // [nsrc] solve jobs of a small system in its unknowns' slots
+    uint64_t *sol_outs;                        // [nsrc] their outputs (unknown x + d)
+    uint8_t *sol_coef;                         // [nrep * kSwSmallE] coefficients (64 B per equation)
     SwLong *longs;                             // [long_cap]
     uint64_t long_cap;
     SwOp *log;                                 // [log_cap]

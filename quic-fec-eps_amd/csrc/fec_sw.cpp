@@ -174,15 +174,13 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // rows), slot 9 (their operation log) and slot 10 (device copies of host
 // bookkeeping).
 struct DecBlock {
-    size_t o_reach, o_chunk, o_lost, o_reachL, o_ctr, o_synj, o_syno, o_coef, o_solj, o_solo, o_solc, o_long,
-        o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, total;
-    uint64_t sol_cap, coef_cap, long_cap, piv_cap;
+    size_t o_reach, o_rcnt, o_chunk, o_echunk, o_eqidx, o_lost, o_reachL, o_ctr, o_synj, o_syno, o_coef, o_solj,
+        o_solo, o_solc, o_long, o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, total;
+    uint64_t long_cap, piv_cap;
 };
 DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
     DecBlock L{};
-    const uint64_t nchunk = (nsrc + kSwChunk - 1) / kSwChunk;
-    L.sol_cap = std::max<uint64_t>(1, std::min(nsrc, nrep));
-    L.coef_cap = L.sol_cap * kSwSmallP;
+    const uint64_t nchunk = (nsrc + kSwChunk - 1) / kSwChunk, nrc = (nrep + kSwChunk - 1) / kSwChunk;
     L.long_cap = nsrc / (uint64_t)std::max(1, std::min(kSwSmallE + 1, long_min)) + 1;
     L.piv_cap = std::max<uint64_t>(1, nrep);
     size_t o = 0;
@@ -192,16 +190,19 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
         return at;
     };
     L.o_reach = take((nsrc + 1) * 4);
-    L.o_chunk = take(2 * nchunk * 4);
+    L.o_rcnt = take((nsrc + 1) * 4);
+    L.o_chunk = take(3 * nchunk * 4);
+    L.o_echunk = take((nrc + 1) * 4);
+    L.o_eqidx = take(nrep * 4);
     L.o_lost = take(nsrc * 4);
     L.o_reachL = take(nsrc * 4);
     L.o_ctr = take(sizeof(SwDecCtr));
     L.o_synj = take(nrep * sizeof(CombJob));
     L.o_syno = take(nrep * 8);
     L.o_coef = take(nrep * (size_t)kSwCoefPitch);
-    L.o_solj = take(L.sol_cap * sizeof(CombJob));
-    L.o_solo = take(L.sol_cap * 8);
-    L.o_solc = take(L.coef_cap);
+    L.o_solj = take(nsrc * sizeof(CombJob));
+    L.o_solo = take(nsrc * 8);
+    L.o_solc = take(nrep * (size_t)kSwSmallE);
     L.o_long = take(L.long_cap * sizeof(SwLong));
     L.o_synrow = take(nrep * 4);
     L.o_pivc = take(L.piv_cap * 256);
@@ -238,7 +239,10 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.nchunk = (uint32_t)((nsrc + kSwChunk - 1) / kSwChunk);
     a.long_min = long_min;
     a.reach = reinterpret_cast<uint32_t *>(b + L.o_reach);
+    a.rcnt = reinterpret_cast<uint32_t *>(b + L.o_rcnt);
     a.chunk = reinterpret_cast<uint32_t *>(b + L.o_chunk);
+    a.echunk = reinterpret_cast<uint32_t *>(b + L.o_echunk);
+    a.eqidx = reinterpret_cast<uint32_t *>(b + L.o_eqidx);
     a.lost = reinterpret_cast<uint32_t *>(b + L.o_lost);
     a.reachL = reinterpret_cast<uint32_t *>(b + L.o_reachL);
     a.ctr = reinterpret_cast<SwDecCtr *>(b + L.o_ctr);
@@ -248,8 +252,6 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.sol_jobs = reinterpret_cast<CombJob *>(b + L.o_solj);
     a.sol_outs = reinterpret_cast<uint64_t *>(b + L.o_solo);
     a.sol_coef = b + L.o_solc;
-    a.sol_cap = a.outs_cap = L.sol_cap;
-    a.coef_cap = L.coef_cap;
     a.longs = reinterpret_cast<SwLong *>(b + L.o_long);
     a.long_cap = L.long_cap;
     a.log = static_cast<SwOp *>(plog);
@@ -265,7 +267,8 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.synd = static_cast<const uint8_t *>(psyn);
 
     SW_TRY(hipMemsetAsync(a.ctr, 0, sizeof(SwDecCtr), s), "sliding-window decode counters");
-    SW_TRY(hipMemsetAsync(a.reach, 0, (nsrc + 1) * 4, s), "sliding-window decode reach");
+    // reach and rcnt are adjacent: one memset
+    SW_TRY(hipMemsetAsync(a.reach, 0, L.o_chunk - L.o_reach, s), "sliding-window decode reach");
     SW_TRY(launch_sw_dec_plan(a, s), "sliding-window decode plan launch");
     SW_TRY(launch_sw_dec_long(a, s), "sliding-window long-system plan launch");
     const uint32_t ncol = (S + 15u) >> 4;
@@ -278,7 +281,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     sa.in_base = src;
     sa.out_base = static_cast<uint8_t *>(psyn);
     sa.xor_base = rep;
-    sa.extra = &a.ctr->nsyn;
+    sa.extra = &a.ctr->neq;
     sa.extra_max = nrep;
     sa.ncol = ncol;
     sa.stride = stride;
@@ -294,8 +297,8 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     va.in_base = static_cast<const uint8_t *>(psyn);
     va.out_base = src;
     va.xor_base = nullptr;
-    va.extra = &a.ctr->nsol;
-    va.extra_max = L.sol_cap;
+    va.extra = &a.ctr->nlost;  // a slot per unknown, filled by its small system
+    va.extra_max = nsrc;
     va.nin_max = kSwSmallP;
     va.nout_max = kSwSolveOut;
     va.nin_dev = &a.ctr->maxp;

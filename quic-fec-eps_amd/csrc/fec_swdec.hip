@@ -113,8 +113,9 @@ __device__ uint64_t wave_lower_bound(const fecgpu_sw_repair *h, uint64_t lo, uin
 
 // ================================================================ plan ===
 // Headers: validity (device headers are checked here; host headers were
-// checked by the caller too), the widest received window, and per source the
-// farthest end of the received repairs starting there.
+// checked by the caller too), the widest received window, per source the
+// farthest end of the received repairs starting there and the number of
+// repairs starting there.
 __global__ __launch_bounds__(kBlock) void sw_dec_hdr_kernel(SwDecArgs a) {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool bad = false;
@@ -123,9 +124,12 @@ __global__ __launch_bounds__(kBlock) void sw_dec_hdr_kernel(SwDecArgs a) {
         const fecgpu_sw_repair h = a.hdr[t];
         bad = h.nss < 1 || h.nss > kSwMaxWindow || h.dt > 15 || h.fss > a.nsrc || a.nsrc - h.fss < h.nss;
         if (t > 0 && a.hdr[t - 1].fss > h.fss) bad = true;
-        if (!bad && a.rep_present[t]) {
-            w = h.nss;
-            atomicMax(&a.reach[h.fss], (uint32_t)(h.fss + h.nss));
+        if (!bad) {
+            atomicAdd(&a.rcnt[h.fss], 1u);
+            if (a.rep_present[t]) {
+                w = h.nss;
+                atomicMax(&a.reach[h.fss], (uint32_t)(h.fss + h.nss));
+            }
         }
     }
     w = wave_max(w);
@@ -136,13 +140,13 @@ __global__ __launch_bounds__(kBlock) void sw_dec_hdr_kernel(SwDecArgs a) {
     }
 }
 
-// Block per chunk of 4096 sources (16 per thread): statuses (1 = lost), lost
-// count and max reach of the chunk.
+// Block per chunk of 4096 sources (16 per thread): statuses (1 = lost), and
+// the chunk's lost count, max reach and repair count.
 __global__ __launch_bounds__(kBlock) void sw_dec_count_kernel(SwDecArgs a) {
-    __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64];
+    __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64], s_r[kBlock / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t i0 = (uint64_t)blockIdx.x * kSwChunk + threadIdx.x * 16u;
-    uint32_t cnt = 0, mx = 0;
+    uint32_t cnt = 0, mx = 0, rc = 0;
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         const uint64_t i = i0 + j;
@@ -151,103 +155,118 @@ __global__ __launch_bounds__(kBlock) void sw_dec_count_kernel(SwDecArgs a) {
             cnt += lost;
             a.stat[i] = lost ? FECGPU_STATUS_UNRECOVERABLE : FECGPU_STATUS_OK;
             mx = max(mx, a.reach[i]);
+            rc += a.rcnt[i];
         }
     }
     cnt = wave_sum(cnt);
+    rc = wave_sum(rc);
     mx = wave_max(mx);
     if (lane == 0) {
         s_c[wave] = cnt;
         s_m[wave] = mx;
+        s_r[wave] = rc;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t c = 0, m = 0;
+        uint32_t c = 0, m = 0, r = 0;
         for (int w = 0; w < kBlock / 64; w++) {
             c += s_c[w];
             m = max(m, s_m[w]);
+            r += s_r[w];
         }
-        a.chunk[2 * blockIdx.x] = c;
-        a.chunk[2 * blockIdx.x + 1] = m;
+        a.chunk[3 * blockIdx.x] = c;
+        a.chunk[3 * blockIdx.x + 1] = m;
+        a.chunk[3 * blockIdx.x + 2] = r;
     }
 }
 
-// One block: exclusive sum of the chunks' lost counts and exclusive max of
-// their reaches; the total lost count.
-__global__ __launch_bounds__(1024) void sw_dec_scan_kernel(SwDecArgs a) {
-    __shared__ uint32_t s_sum[16], s_max[16];
-    __shared__ uint32_t s_cc, s_cm;
+// One block: exclusive scans of `cols` interleaved per-chunk columns of arr
+// (column 1 by max when max1, the others by sum); the totals of column 0 go to
+// *total0.
+__global__ __launch_bounds__(1024) void sw_dec_scan_kernel(uint32_t *arr, uint32_t n, int cols, int max1,
+                                                           uint32_t *total0) {
+    __shared__ uint32_t s_w[3][16];
+    __shared__ uint32_t s_carry[3];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_cc = s_cm = 0;
+    if (threadIdx.x < 3) s_carry[threadIdx.x] = 0;
     __syncthreads();
-    for (uint32_t b0 = 0; b0 < a.nchunk; b0 += 1024) {
+    for (uint32_t b0 = 0; b0 < n; b0 += 1024) {
         const uint32_t b = b0 + threadIdx.x;
-        const uint32_t c = b < a.nchunk ? a.chunk[2 * b] : 0u, m = b < a.nchunk ? a.chunk[2 * b + 1] : 0u;
-        uint32_t ic = c, im = m;
+        uint32_t v[3], inc[3], exc[3];
+        for (int k = 0; k < cols; k++) {
+            v[k] = b < n ? arr[(uint64_t)cols * b + k] : 0u;
+            const bool mx = max1 && k == 1;
+            uint32_t x = v[k];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(ic, o), ym = __shfl_up(im, o);
-            if (lane >= o) {
-                ic += y;
-                im = max(im, ym);
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (lane >= o) x = mx ? max(x, y) : x + y;
             }
-        }
-        uint32_t em = __shfl_up(im, 1);  // exclusive max within the wave
-        if (lane == 0) em = 0;
-        if (lane == 63) {
-            s_sum[wave] = ic;
-            s_max[wave] = im;
+            inc[k] = x;
+            uint32_t e = __shfl_up(x, 1);
+            exc[k] = lane == 0 ? 0u : e;
+            if (lane == 63) s_w[k][wave] = x;
         }
         __syncthreads();
         if (threadIdx.x == 0) {
-            uint32_t acc = s_cc, am = s_cm;
-            for (int w = 0; w < 16; w++) {
-                const uint32_t ts = s_sum[w], tm = s_max[w];
-                s_sum[w] = acc;
-                s_max[w] = am;
-                acc += ts;
-                am = max(am, tm);
+            for (int k = 0; k < cols; k++) {
+                const bool mx = max1 && k == 1;
+                uint32_t acc = s_carry[k];
+                for (int w = 0; w < 16; w++) {
+                    const uint32_t t = s_w[k][w];
+                    s_w[k][w] = acc;
+                    acc = mx ? max(acc, t) : acc + t;
+                }
+                s_carry[k] = acc;
             }
-            s_cc = acc;
-            s_cm = am;
         }
         __syncthreads();
-        if (b < a.nchunk) {
-            a.chunk[2 * b] = s_sum[wave] + ic - c;
-            a.chunk[2 * b + 1] = max(s_max[wave], em);
-        }
+        if (b < n)
+            for (int k = 0; k < cols; k++) {
+                const bool mx = max1 && k == 1;
+                arr[(uint64_t)cols * b + k] = mx ? max(s_w[k][wave], exc[k]) : s_w[k][wave] + exc[k];
+            }
+        (void)inc;
         __syncthreads();
     }
-    if (threadIdx.x == 0) a.ctr->nlost = s_cc;
+    if (threadIdx.x == 0 && total0) *total0 = s_carry[0];
 }
 
-// Block per chunk: the lost sources in order with the reach at each, and
-// rank[i] = lost sources before i (written over the reach array).
+// Block per chunk of sources: the lost sources in order with the reach at
+// each (an empty solve job for each, which its system may fill), rank[i] =
+// lost sources before i (over reach) and repfirst[i] = repairs starting
+// before i (over rcnt).
 __global__ __launch_bounds__(kBlock) void sw_dec_lost_kernel(SwDecArgs a) {
-    __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64];
+    __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64], s_r[kBlock / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t i0 = (uint64_t)b * kSwChunk + threadIdx.x * 16u;
-    uint32_t r[16], mask = 0;
+    uint32_t r[16], rn[16], mask = 0;
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         const uint64_t i = i0 + j;
-        r[j] = 0;
+        r[j] = rn[j] = 0;
         if (i < a.nsrc) {
             r[j] = a.reach[i];
+            rn[j] = a.rcnt[i];
             mask |= (a.src_present[i] == 0 ? 1u : 0u) << j;
         }
     }
-    uint32_t tm = 0;
+    uint32_t tm = 0, tr = 0;
 #pragma unroll
-    for (int j = 0; j < 16; j++) tm = max(tm, r[j]);
+    for (int j = 0; j < 16; j++) {
+        tm = max(tm, r[j]);
+        tr += rn[j];
+    }
     const uint32_t cnt = __popc(mask);
-    uint32_t ic = cnt, im = tm;
+    uint32_t ic = cnt, im = tm, ir = tr;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(ic, o), ym = __shfl_up(im, o);
+        const uint32_t y = __shfl_up(ic, o), ym = __shfl_up(im, o), yr = __shfl_up(ir, o);
         if (lane >= o) {
             ic += y;
             im = max(im, ym);
+            ir += yr;
         }
     }
     uint32_t em = __shfl_up(im, 1);
@@ -255,47 +274,122 @@ __global__ __launch_bounds__(kBlock) void sw_dec_lost_kernel(SwDecArgs a) {
     if (lane == 63) {
         s_c[wave] = ic;
         s_m[wave] = im;
+        s_r[wave] = ir;
     }
     __syncthreads();
-    uint32_t wc = 0, wm = 0;
+    uint32_t wc = 0, wm = 0, wr = 0;
     for (int w = 0; w < wave; w++) {
         wc += s_c[w];
         wm = max(wm, s_m[w]);
+        wr += s_r[w];
     }
-    uint32_t off = a.chunk[2 * b] + wc + ic - cnt;
-    uint32_t run = max(max(a.chunk[2 * b + 1], wm), em);
+    uint32_t off = a.chunk[3 * b] + wc + ic - cnt;
+    uint32_t run = max(max(a.chunk[3 * b + 1], wm), em);
+    uint32_t rep = a.chunk[3 * b + 2] + wr + ir - tr;
+    CombJob E{};
+    E.xor_off = kNoXor;
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         const uint64_t i = i0 + j;
         if (i >= a.nsrc) break;
         run = max(run, r[j]);
-        a.reach[i] = off;  // rank[i]
+        a.reach[i] = off;   // rank[i]
+        a.rcnt[i] = rep;    // repfirst[i]
+        rep += rn[j];
         if ((mask >> j) & 1u) {
             a.lost[off] = (uint32_t)i;
             a.reachL[off] = run;
+            a.sol_jobs[off] = E;
             off++;
         }
     }
-    if (i0 <= a.nsrc && a.nsrc <= i0 + 16 && a.nsrc > 0) a.reach[a.nsrc] = off;  // rank[nsrc] = nlost
+    if (i0 <= a.nsrc && a.nsrc <= i0 + 16) {  // the thread holding the end: rank / repfirst of nsrc
+        a.reach[a.nsrc] = off;
+        a.rcnt[a.nsrc] = rep;
+    }
 }
 
-// ============================================================= systems ===
-constexpr int kSwPitch = kSwSmallE + kSwSmallP;  // LDS row of [A | I] (e <= 64, p <= 96)
-
-// the repair's window holds a lost source of the system lost[x .. x + e)
+// the repair's window holds a lost source (rank = lost sources before i)
+__device__ __forceinline__ bool holds_any(const SwDecArgs &a, const fecgpu_sw_repair &h) {
+    return a.reach[h.fss + h.nss] > a.reach[h.fss];
+}
+// ... of the system lost[x .. x + e)
 __device__ __forceinline__ bool holds(const SwDecArgs &a, const fecgpu_sw_repair &h, uint32_t x, uint32_t e) {
     const uint32_t r0 = a.reach[h.fss], r1 = a.reach[h.fss + h.nss];
     return r1 > r0 && r0 < x + e && r1 > x;
 }
 
+// Block per chunk of 4096 repairs: equations (received repairs that hold a
+// lost source) counted.  A system's equations are consecutive among all
+// equations in repair order (a repair between two of them would link the
+// systems), so numbering the equations gives every system a contiguous range
+// of syndrome jobs and rows with no allocation.
+__global__ __launch_bounds__(kBlock) void sw_dec_eqcount_kernel(SwDecArgs a) {
+    __shared__ uint32_t s_c[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kSwChunk + threadIdx.x * 16u;
+    uint32_t cnt = 0;
+    if (!(a.ctr->err & 1u))
+        for (int j = 0; j < 16; j++) {
+            const uint64_t t = t0 + j;
+            if (t < a.nrep && a.rep_present[t] && holds_any(a, a.hdr[t])) cnt++;
+        }
+    cnt = wave_sum(cnt);
+    if (lane == 0) s_c[wave] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t c = 0;
+        for (int w = 0; w < kBlock / 64; w++) c += s_c[w];
+        a.echunk[blockIdx.x] = c;
+    }
+}
+
+// Block per chunk of repairs: eqidx[t] (equations only) and an empty
+// syndrome job in each equation's slot, which its system fills.
+__global__ __launch_bounds__(kBlock) void sw_dec_eqwrite_kernel(SwDecArgs a) {
+    __shared__ uint32_t s_c[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kSwChunk + threadIdx.x * 16u;
+    if (a.ctr->err & 1u) return;
+    uint32_t mask = 0;
+    for (int j = 0; j < 16; j++) {
+        const uint64_t t = t0 + j;
+        if (t < a.nrep && a.rep_present[t] && holds_any(a, a.hdr[t])) mask |= 1u << j;
+    }
+    const uint32_t cnt = __popc(mask);
+    uint32_t ic = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(ic, o);
+        if (lane >= o) ic += y;
+    }
+    if (lane == 63) s_c[wave] = ic;
+    __syncthreads();
+    uint32_t wc = 0;
+    for (int w = 0; w < wave; w++) wc += s_c[w];
+    uint32_t g = a.echunk[blockIdx.x] + wc + ic - cnt;
+    CombJob E{};
+    E.xor_off = kNoXor;
+    for (int j = 0; j < 16; j++) {
+        const uint64_t t = t0 + j;
+        if (t >= a.nrep) break;
+        if ((mask >> j) & 1u) {
+            a.eqidx[t] = g;
+            a.syn_jobs[g] = E;
+            g++;
+        }
+    }
+}
+
+// ============================================================= systems ===
+constexpr int kSwPitch = kSwSmallE + kSwSmallP;  // LDS row of [A | I] (e <= 64, p <= 96)
+
 // One wave solves the small system lost[x .. x + e) with its p equations
-// (repair indices eq[]): the round-2 sw_plan_kernel, now fed on the device.
-__device__ void small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e, int p, const uint32_t *U,
-                            const uint32_t *eq, uint8_t *M, int8_t *piv, int lane) {
+// (repair indices eq[], equation numbers g0 ..): the round-2 sw_plan_kernel,
+// fed on the device.  Returns the unknowns it determined.
+__device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e, int p, uint32_t g0,
+                           const uint32_t *U, const uint32_t *eq, uint8_t *M, int8_t *piv, int lane) {
     const int W = e + p;
-    uint32_t g0 = 0;
-    if (lane == 0) g0 = atomicAdd(&a.ctr->nsyn, (uint32_t)p);
-    g0 = __shfl(g0, 0);
     for (int q = 0; q < p; q++)
         for (int j = lane; j < W; j += 64) M[q * kSwPitch + j] = (uint8_t)(j >= e && j - e == q);
     SWD_WAVE_SYNC();
@@ -385,37 +479,29 @@ __device__ void small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int 
         for (int col = 0; col < e && !need; col++) need = ((dm >> col) & 1) && M[piv[col] * kSwPitch + e + q] != 0;
         if (!need) a.syn_jobs[g0 + q].nout = 0;
     }
-    if (ndet == 0) return;
-    const int nj = (ndet + 7) / 8;
-    uint32_t j0 = 0, o0 = 0;
-    unsigned long long c0 = 0;
-    if (lane == 0) {
-        j0 = atomicAdd(&a.ctr->nsol, (uint32_t)nj);
-        o0 = atomicAdd(&a.ctr->nouts, (uint32_t)ndet);
-        c0 = atomicAdd(&a.ctr->ncoef, (unsigned long long)ndet * p);
-        atomicAdd(&a.ctr->recovered, (uint32_t)ndet);
-        atomicMax(&a.ctr->maxp, (uint32_t)p);
-    }
-    j0 = __shfl(j0, 0);
-    o0 = __shfl(o0, 0);
-    c0 = __shfl(c0, 0);
+    if (ndet == 0) return 0;
+    // solve jobs in the system's unknown slots x .. (ndet <= e), outputs at
+    // x + d, coefficients at 64 bytes per equation from g0 (ndet * p <= 64 * p)
+    const uint64_t c0 = (uint64_t)g0 * kSwSmallE;
     if (det) {
         const int d = __popcll(dm & lanes_below(lane));
         uint8_t *cf = a.sol_coef + c0 + (uint64_t)d * p;
         for (int t = 0; t < p; t++) cf[t] = M[prc * kSwPitch + e + t];
-        a.sol_outs[o0 + d] = (uint64_t)U[lane] * a.stride;
+        a.sol_outs[x + d] = (uint64_t)U[lane] * a.stride;
         a.stat[U[lane]] = FECGPU_STATUS_OK;
     }
+    const int nj = (ndet + 7) / 8;
     if (lane < nj) {
         CombJob J;
         J.in_off = (uint64_t)g0 * a.stride;
         J.coef_off = c0 + (uint64_t)lane * 8 * p;
-        J.out_list = o0 + (uint64_t)lane * 8;
+        J.out_list = x + (uint64_t)lane * 8;
         J.xor_off = kNoXor;
         J.nin = (uint32_t)p;
         J.nout = (uint32_t)min(8, ndet - 8 * lane);
-        a.sol_jobs[j0 + lane] = J;
+        a.sol_jobs[x + lane] = J;
     }
+    return ndet;
 }
 
 // A wave per lost source; the waves at a system start find its extent and
@@ -432,6 +518,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     if (a.ctr->err & 1u) return;
     const uint32_t nlost = a.ctr->nlost, wmax = max(1u, a.ctr->wmax);
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
+    uint32_t rec = 0, maxp = 0;  // this wave's recovered count, widest solve
     for (uint64_t x = (uint64_t)blockIdx.x * (kBlock / 64) + wave; x < nlost; x += nwaves) {
         const uint32_t lx = a.lost[x];
         if (x > 0 && a.reachL[x - 1] > lx) continue;  // not a system start (uniform)
@@ -448,10 +535,10 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
             e += 64;
         }
         const uint32_t last = a.lost[x + e - 1];
-        const uint64_t t_lo = wave_lower_bound(a.hdr, 0, a.nrep, lx >= wmax ? lx - wmax + 1 : 0, lane);
-        const uint64_t t_hi = wave_lower_bound(a.hdr, t_lo, a.nrep, (uint64_t)last + 1, lane);
+        // candidate repairs: fss in [lx - wmax + 1, last]
+        const uint64_t t_lo = a.rcnt[lx >= wmax ? lx - wmax + 1 : 0], t_hi = a.rcnt[(uint64_t)last + 1];
         bool small = (int)e <= kSwSmallE && (int)e < a.long_min;
-        uint32_t p = 0;
+        uint32_t p = 0, t_first = 0;
         if (small) {
             if (lane < (int)e) s_U[wave][lane] = a.lost[x + lane];
             for (uint64_t t0 = t_lo; t0 < t_hi; t0 += 64) {
@@ -465,6 +552,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
                     break;
                 }
                 if (hd) s_eq[wave][p + __popcll(b & lanes_below(lane))] = (uint32_t)t;
+                if (p == 0 && b) t_first = (uint32_t)(t0 + __ffsll((unsigned long long)b) - 1);
                 p += n;
             }
         }
@@ -486,7 +574,15 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
         }
         if (p == 0) continue;  // no received repair holds it: stays lost
         SWD_WAVE_SYNC();
-        small_solve(a, g, (uint32_t)x, (int)e, (int)p, s_U[wave], s_eq[wave], s_M[wave], s_piv[wave], lane);
+        const uint32_t g0 = a.eqidx[t_first];
+        const int nd = small_solve(a, g, (uint32_t)x, (int)e, (int)p, g0, s_U[wave], s_eq[wave], s_M[wave],
+                                   s_piv[wave], lane);
+        rec += (uint32_t)nd;
+        if (nd) maxp = max(maxp, p);
+    }
+    if (lane == 0) {
+        if (rec) atomicAdd(&a.ctr->recovered, rec);
+        if (maxp) atomicMax(&a.ctr->maxp, maxp);
     }
 }
 
@@ -744,23 +840,22 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
             }
             continue;
         }
-        // syndrome jobs for the pivot rows (the only rows whose data is used)
-        uint32_t g0 = 0;
-        if (lane == 0) g0 = atomicAdd(&a.ctr->nsyn, npiv);
-        g0 = __shfl(g0, 0);
+        // syndrome jobs for the pivot rows (the only rows whose data is used), in
+        // their equations' slots; the other equations' slots stay empty
         for (uint32_t q = lane; q < npiv; q += 64) {
             const uint32_t t = a.pivt[piv0 + q];
+            const uint32_t gq = a.eqidx[t];
             const fecgpu_sw_repair h = a.hdr[t];
             CombJob J;
             J.in_off = h.fss * a.stride;
             J.coef_off = (uint64_t)t * kSwCoefPitch;
-            J.out_list = g0 + q;
+            J.out_list = gq;
             J.xor_off = (uint64_t)t * a.stride;
             J.nin = h.nss;
             J.nout = 1;
-            a.syn_jobs[g0 + q] = J;
-            a.syn_outs[g0 + q] = (uint64_t)(g0 + q) * a.stride;
-            a.synrow[t] = g0 + q;
+            a.syn_jobs[gq] = J;
+            a.syn_outs[gq] = (uint64_t)gq * a.stride;
+            a.synrow[t] = gq;
         }
         // ---- null-space sweep and back substitution log ----
         // VT[coordinate & 255][vector] bytes (LDS rowc), nv vectors
@@ -945,9 +1040,13 @@ int cu_count() {
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
     if (a.nrep) hipLaunchKernelGGL(sw_dec_hdr_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(sw_dec_count_kernel, dim3(a.nchunk), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(sw_dec_scan_kernel, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(sw_dec_scan_kernel, dim3(1), dim3(1024), 0, s, a.chunk, a.nchunk, 3, 1, &a.ctr->nlost);
     hipLaunchKernelGGL(sw_dec_lost_kernel, dim3(a.nchunk), dim3(kBlock), 0, s, a);
     if (a.nrep) {
+        const uint32_t nrc = (uint32_t)((a.nrep + kSwChunk - 1) / kSwChunk);
+        hipLaunchKernelGGL(sw_dec_eqcount_kernel, dim3(nrc), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(sw_dec_scan_kernel, dim3(1), dim3(1024), 0, s, a.echunk, nrc, 1, 0, &a.ctr->neq);
+        hipLaunchKernelGGL(sw_dec_eqwrite_kernel, dim3(nrc), dim3(kBlock), 0, s, a);
         // a wave per lost source at most; persistent beyond two blocks per CU
         const uint64_t want = (a.nsrc + kBlock / 64 - 1) / (kBlock / 64);
         const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 2));
