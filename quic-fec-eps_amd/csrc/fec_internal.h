@@ -249,7 +249,8 @@ constexpr int kSwChunk = 4096;  // sources per planning chunk
 struct SwDecCtr {  // per call, zeroed before the first kernel
     uint32_t nlost, wmax, maxp, err;   // err: bit 0 bad header; bit 1 log / pivot-area capacity
                                        // exceeded (retry larger); bit 2 more than kSwRows rows alive
-    uint32_t neq, nlong, npiv, recovered;  // equations (= syndrome job slots), long systems, pivot rows
+    uint32_t nmid, nlong, npiv, recovered;  // queued mid / long systems, pivot rows, recovered
+    uint32_t maxin, pad0, pad1, pad2;       // widest small-system solve (syndrome rows)
     unsigned long long nlog;           // long-system log entries
 };
 // one long system: lost[x0 .. x0 + e), candidate repairs [t_lo, t_hi); its
@@ -281,17 +282,16 @@ struct SwDecArgs {
                                                // repairs starting before i
     uint32_t *chunk;                           // [3 * nchunk] lost count / max reach / repairs per chunk,
                                                // then their exclusive scans
-    uint32_t *echunk;                          // [nrep / 4096 + 1] equations per repair chunk, then scanned
-    uint32_t *eqidx;                           // [nrep] equation number of repair t (equations only)
     uint32_t *lost, *reachL;                   // [nsrc] lost sources; prefix max of reach at each
     SwDecCtr *ctr;
-    CombJob *syn_jobs;                         // [nrep] syndrome job of equation g
+    CombJob *syn_jobs;                         // [nrep] syndrome job of repair t (empty unless needed)
     uint64_t *syn_outs;                        // [nrep]
     uint8_t *coef;                             // [nrep][kSwCoefPitch]: repair t's syndrome coefficients
     CombJob *sol_jobs;                         // [nsrc] solve jobs of a small system in its unknowns' slots
     uint64_t *sol_outs;                        // [nsrc] their outputs (unknown x + d)
-    uint8_t *sol_coef;                         // [nrep * kSwSmallE] coefficients (64 B per equation)
+    uint8_t *sol_coef;                         // [nrep * kSwSmallE] coefficients (64 B per repair)
     SwLong *longs;                             // [long_cap]
+    SwLong *mids;                              // [long_cap] small systems too wide for the tiny pass
     uint64_t long_cap;
     SwOp *log;                                 // [log_cap]
     uint64_t log_cap;

@@ -46,6 +46,11 @@ namespace {
 constexpr uint32_t kCombBudget = FECGPU_COMB_BUDGET_KB << 10;
 constexpr uint32_t kCombBudgetWide = FECGPU_COMB_BUDGET_WIDE_KB << 10;
 constexpr int kSwSolveOut = 8;               // recovered sources per solve job
+constexpr int kSwSolveIn = 128;              // syndrome rows a small system's solve reads (fec_swdec.hip)
+// LDS of a solve workgroup: its jobs' 8-output tables over the widest range of
+// syndrome rows (device-sized); more room than the encode's budget keeps
+// several jobs per workgroup
+constexpr uint32_t kSolveBudget = 64u << 10;
 // sources and repairs per call: the device plan numbers them in 32 bits
 constexpr uint64_t kSwMaxSources = (1ull << 32) - 256;
 
@@ -174,14 +179,15 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // rows), slot 9 (their operation log) and slot 10 (device copies of host
 // bookkeeping).
 struct DecBlock {
-    size_t o_reach, o_rcnt, o_chunk, o_echunk, o_eqidx, o_lost, o_reachL, o_ctr, o_synj, o_syno, o_coef, o_solj,
-        o_solo, o_solc, o_long, o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, total;
+    size_t o_reach, o_rcnt, o_chunk, o_lost, o_reachL, o_ctr, o_synj, o_syno, o_coef, o_solj, o_solo, o_solc,
+        o_long, o_mid, o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, total;
     uint64_t long_cap, piv_cap;
 };
 DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
     DecBlock L{};
-    const uint64_t nchunk = (nsrc + kSwChunk - 1) / kSwChunk, nrc = (nrep + kSwChunk - 1) / kSwChunk;
-    L.long_cap = nsrc / (uint64_t)std::max(1, std::min(kSwSmallE + 1, long_min)) + 1;
+    const uint64_t nchunk = (nsrc + kSwChunk - 1) / kSwChunk;
+    (void)long_min;
+    L.long_cap = nsrc + 1;  // queued systems (mid or long): at most one per lost source
     L.piv_cap = std::max<uint64_t>(1, nrep);
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -192,8 +198,6 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
     L.o_reach = take((nsrc + 1) * 4);
     L.o_rcnt = take((nsrc + 1) * 4);
     L.o_chunk = take(3 * nchunk * 4);
-    L.o_echunk = take((nrc + 1) * 4);
-    L.o_eqidx = take(nrep * 4);
     L.o_lost = take(nsrc * 4);
     L.o_reachL = take(nsrc * 4);
     L.o_ctr = take(sizeof(SwDecCtr));
@@ -204,6 +208,7 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
     L.o_solo = take(nsrc * 8);
     L.o_solc = take(nrep * (size_t)kSwSmallE);
     L.o_long = take(L.long_cap * sizeof(SwLong));
+    L.o_mid = take(L.long_cap * sizeof(SwLong));
     L.o_synrow = take(nrep * 4);
     L.o_pivc = take(L.piv_cap * 256);
     L.o_colpiv = take(nsrc * 4);
@@ -241,8 +246,6 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.reach = reinterpret_cast<uint32_t *>(b + L.o_reach);
     a.rcnt = reinterpret_cast<uint32_t *>(b + L.o_rcnt);
     a.chunk = reinterpret_cast<uint32_t *>(b + L.o_chunk);
-    a.echunk = reinterpret_cast<uint32_t *>(b + L.o_echunk);
-    a.eqidx = reinterpret_cast<uint32_t *>(b + L.o_eqidx);
     a.lost = reinterpret_cast<uint32_t *>(b + L.o_lost);
     a.reachL = reinterpret_cast<uint32_t *>(b + L.o_reachL);
     a.ctr = reinterpret_cast<SwDecCtr *>(b + L.o_ctr);
@@ -253,6 +256,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.sol_outs = reinterpret_cast<uint64_t *>(b + L.o_solo);
     a.sol_coef = b + L.o_solc;
     a.longs = reinterpret_cast<SwLong *>(b + L.o_long);
+    a.mids = reinterpret_cast<SwLong *>(b + L.o_mid);
     a.long_cap = L.long_cap;
     a.log = static_cast<SwOp *>(plog);
     a.log_cap = log_entries;
@@ -281,8 +285,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     sa.in_base = src;
     sa.out_base = static_cast<uint8_t *>(psyn);
     sa.xor_base = rep;
-    sa.extra = &a.ctr->neq;
-    sa.extra_max = nrep;
+    sa.njobs = nrep;  // a slot per repair; the needed ones filled by their systems
     sa.ncol = ncol;
     sa.stride = stride;
     sa.nin_max = kSwMaxWindow;
@@ -299,9 +302,11 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     va.xor_base = nullptr;
     va.extra = &a.ctr->nlost;  // a slot per unknown, filled by its small system
     va.extra_max = nsrc;
-    va.nin_max = kSwSmallP;
+    va.njobs = 0;
+    va.nin_max = kSwSolveIn;
     va.nout_max = kSwSolveOut;
-    va.nin_dev = &a.ctr->maxp;
+    va.nin_dev = &a.ctr->maxin;
+    va.budget = kSolveBudget;
     SW_TRY(launch_comb(va, kSwSolveOut, s), "sliding-window solve launch");
     SW_TRY(launch_sw_dec_replay(a, s), "sliding-window long-system replay launch");
     if (ctr_out) SW_TRY(hipMemcpyAsync(ctr_out, a.ctr, sizeof(SwDecCtr), hipMemcpyDeviceToHost, s), "D2H sw counters");

@@ -124,6 +124,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_hdr_kernel(SwDecArgs a) {
         const fecgpu_sw_repair h = a.hdr[t];
         bad = h.nss < 1 || h.nss > kSwMaxWindow || h.dt > 15 || h.fss > a.nsrc || a.nsrc - h.fss < h.nss;
         if (t > 0 && a.hdr[t - 1].fss > h.fss) bad = true;
+        CombJob E{};
+        E.xor_off = kNoXor;
+        a.syn_jobs[t] = E;  // filled if repair t becomes a needed syndrome
         if (!bad) {
             atomicAdd(&a.rcnt[h.fss], 1u);
             if (a.rep_present[t]) {
@@ -235,30 +238,21 @@ __global__ __launch_bounds__(1024) void sw_dec_scan_kernel(uint32_t *arr, uint32
 // Block per chunk of sources: the lost sources in order with the reach at
 // each (an empty solve job for each, which its system may fill), rank[i] =
 // lost sources before i (over reach) and repfirst[i] = repairs starting
-// before i (over rcnt).
+// before i (over rcnt).  Two passes over the thread's 16 sources (the second
+// re-reads them from cache; no other thread touches them) keep registers low;
+// the per-source outputs go out as 16-byte stores.
 __global__ __launch_bounds__(kBlock) void sw_dec_lost_kernel(SwDecArgs a) {
     __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64], s_r[kBlock / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t b = blockIdx.x;
     const uint64_t i0 = (uint64_t)b * kSwChunk + threadIdx.x * 16u;
-    uint32_t r[16], rn[16], mask = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const uint64_t i = i0 + j;
-        r[j] = rn[j] = 0;
-        if (i < a.nsrc) {
-            r[j] = a.reach[i];
-            rn[j] = a.rcnt[i];
-            mask |= (a.src_present[i] == 0 ? 1u : 0u) << j;
-        }
+    const uint32_t n = (uint32_t)min<uint64_t>(16, a.nsrc > i0 ? a.nsrc - i0 : 0);
+    uint32_t cnt = 0, tm = 0, tr = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        cnt += a.src_present[i0 + j] == 0;
+        tm = max(tm, a.reach[i0 + j]);
+        tr += a.rcnt[i0 + j];
     }
-    uint32_t tm = 0, tr = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        tm = max(tm, r[j]);
-        tr += rn[j];
-    }
-    const uint32_t cnt = __popc(mask);
     uint32_t ic = cnt, im = tm, ir = tr;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -288,19 +282,30 @@ __global__ __launch_bounds__(kBlock) void sw_dec_lost_kernel(SwDecArgs a) {
     uint32_t rep = a.chunk[3 * b + 2] + wr + ir - tr;
     CombJob E{};
     E.xor_off = kNoXor;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const uint64_t i = i0 + j;
-        if (i >= a.nsrc) break;
-        run = max(run, r[j]);
-        a.reach[i] = off;   // rank[i]
-        a.rcnt[i] = rep;    // repfirst[i]
-        rep += rn[j];
-        if ((mask >> j) & 1u) {
-            a.lost[off] = (uint32_t)i;
-            a.reachL[off] = run;
-            a.sol_jobs[off] = E;
-            off++;
+    for (uint32_t j0 = 0; j0 < n; j0 += 4) {
+        uint32_t rk[4], rf[4];
+        for (uint32_t j = j0; j < j0 + 4; j++) {
+            rk[j - j0] = off;
+            rf[j - j0] = rep;
+            if (j >= n) continue;
+            const uint64_t i = i0 + j;
+            run = max(run, a.reach[i]);
+            rep += a.rcnt[i];
+            if (a.src_present[i] == 0) {
+                a.lost[off] = (uint32_t)i;
+                a.reachL[off] = run;
+                a.sol_jobs[off] = E;
+                off++;
+            }
+        }
+        if (j0 + 4 <= n) {
+            *reinterpret_cast<uint4 *>(a.reach + i0 + j0) = make_uint4(rk[0], rk[1], rk[2], rk[3]);  // rank
+            *reinterpret_cast<uint4 *>(a.rcnt + i0 + j0) = make_uint4(rf[0], rf[1], rf[2], rf[3]);   // repfirst
+        } else {
+            for (uint32_t j = j0; j < n; j++) {
+                a.reach[i0 + j] = rk[j - j0];
+                a.rcnt[i0 + j] = rf[j - j0];
+            }
         }
     }
     if (i0 <= a.nsrc && a.nsrc <= i0 + 16) {  // the thread holding the end: rank / repfirst of nsrc
@@ -319,79 +324,39 @@ __device__ __forceinline__ bool holds(const SwDecArgs &a, const fecgpu_sw_repair
     return r1 > r0 && r0 < x + e && r1 > x;
 }
 
-// Block per chunk of 4096 repairs: equations (received repairs that hold a
-// lost source) counted.  A system's equations are consecutive among all
-// equations in repair order (a repair between two of them would link the
-// systems), so numbering the equations gives every system a contiguous range
-// of syndrome jobs and rows with no allocation.
-__global__ __launch_bounds__(kBlock) void sw_dec_eqcount_kernel(SwDecArgs a) {
-    __shared__ uint32_t s_c[kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t t0 = (uint64_t)blockIdx.x * kSwChunk + threadIdx.x * 16u;
-    uint32_t cnt = 0;
-    if (!(a.ctr->err & 1u))
-        for (int j = 0; j < 16; j++) {
-            const uint64_t t = t0 + j;
-            if (t < a.nrep && a.rep_present[t] && holds_any(a, a.hdr[t])) cnt++;
-        }
-    cnt = wave_sum(cnt);
-    if (lane == 0) s_c[wave] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t c = 0;
-        for (int w = 0; w < kBlock / 64; w++) c += s_c[w];
-        a.echunk[blockIdx.x] = c;
-    }
-}
-
-// Block per chunk of repairs: eqidx[t] (equations only) and an empty
-// syndrome job in each equation's slot, which its system fills.
-__global__ __launch_bounds__(kBlock) void sw_dec_eqwrite_kernel(SwDecArgs a) {
-    __shared__ uint32_t s_c[kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t t0 = (uint64_t)blockIdx.x * kSwChunk + threadIdx.x * 16u;
-    if (a.ctr->err & 1u) return;
-    uint32_t mask = 0;
-    for (int j = 0; j < 16; j++) {
-        const uint64_t t = t0 + j;
-        if (t < a.nrep && a.rep_present[t] && holds_any(a, a.hdr[t])) mask |= 1u << j;
-    }
-    const uint32_t cnt = __popc(mask);
-    uint32_t ic = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(ic, o);
-        if (lane >= o) ic += y;
-    }
-    if (lane == 63) s_c[wave] = ic;
-    __syncthreads();
-    uint32_t wc = 0;
-    for (int w = 0; w < wave; w++) wc += s_c[w];
-    uint32_t g = a.echunk[blockIdx.x] + wc + ic - cnt;
-    CombJob E{};
-    E.xor_off = kNoXor;
-    for (int j = 0; j < 16; j++) {
-        const uint64_t t = t0 + j;
-        if (t >= a.nrep) break;
-        if ((mask >> j) & 1u) {
-            a.eqidx[t] = g;
-            a.syn_jobs[g] = E;
-            g++;
-        }
-    }
-}
-
 // ============================================================= systems ===
-constexpr int kSwPitch = kSwSmallE + kSwSmallP;  // LDS row of [A | I] (e <= 64, p <= 96)
+// Small systems are solved by one wave each with [A | I] in LDS: "tiny" ones
+// (e <= 16, p <= 48: 3 KB of LDS per wave, so occupancy is set by registers)
+// in the pass over the lost sources, larger ones queued to a pass with room for
+// e <= 64, p <= 96.  Syndrome job / row of equation t: slot t (the hdr kernel
+// empties every slot); a system's solve reads its syndrome rows t_first ..
+// t_last (the repairs in between that are not its equations get coefficient
+// 0: the ranges of two systems never interleave, since a repair between two
+// equations of one system that held a lost source of another would link them).
+constexpr int kSwTinyE = 16, kSwTinyP = 48;
+constexpr int kSwSolveIn = 128;  // widest syndrome range a small system's solve reads
+
+template <int ME, int MP>
+struct SysLds {
+    static constexpr int kPitch = ME + MP;
+    uint8_t M[MP * kPitch];
+    uint32_t U[ME];
+    uint32_t eq[MP];
+    int8_t piv[ME];
+};
 
 // One wave solves the small system lost[x .. x + e) with its p equations
-// (repair indices eq[], equation numbers g0 ..): the round-2 sw_plan_kernel,
-// fed on the device.  Returns the unknowns it determined.
-__device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e, int p, uint32_t g0,
-                           const uint32_t *U, const uint32_t *eq, uint8_t *M, int8_t *piv, int lane) {
+// (repair indices eq[], ascending): the round-2 sw_plan_kernel, fed on the
+// device.  Returns the unknowns it determined; *nin the solve's input rows.
+template <int ME, int MP>
+__device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e, int p, SysLds<ME, MP> &S,
+                           int lane, uint32_t *nin_out) {
+    constexpr int kPitch = SysLds<ME, MP>::kPitch;
+    uint8_t *M = S.M;
+    const uint32_t *U = S.U, *eq = S.eq;
     const int W = e + p;
     for (int q = 0; q < p; q++)
-        for (int j = lane; j < W; j += 64) M[q * kSwPitch + j] = (uint8_t)(j >= e && j - e == q);
+        for (int j = lane; j < W; j += 64) M[q * kPitch + j] = (uint8_t)(j >= e && j - e == q);
     SWD_WAVE_SYNC();
     // lane per equation: its coefficients (RFC 8681 §3.6); the lost sources'
     // go into A, the received sources' into its syndrome job
@@ -414,7 +379,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
             const uint64_t i = h.fss + (uint64_t)j;
             while (u < e && U[u] < i) u++;
             if (u < e && U[u] == i) {
-                M[q * kSwPitch + u] = (uint8_t)c;
+                M[q * kPitch + u] = (uint8_t)c;
                 c = 0;
             }
             word |= c << (8 * (j & 3));
@@ -427,34 +392,34 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         CombJob J;
         J.in_off = h.fss * a.stride;
         J.coef_off = (uint64_t)t * kSwCoefPitch;
-        J.out_list = g0 + q;
+        J.out_list = t;
         J.xor_off = (uint64_t)t * a.stride;
         J.nin = h.nss;
         J.nout = 1;
-        a.syn_jobs[g0 + q] = J;
-        a.syn_outs[g0 + q] = (uint64_t)(g0 + q) * a.stride;
+        a.syn_jobs[t] = J;
+        a.syn_outs[t] = (uint64_t)t * a.stride;
     }
     SWD_WAVE_SYNC();
-    uint64_t used0 = 0, used1 = 0;  // wave-uniform: rows 0..63, 64..95 already pivots
+    uint64_t used0 = 0, used1 = 0;  // wave-uniform: rows 0..63, 64..127 already pivots
     for (int col = 0; col < e; col++) {
-        const bool c0 = lane < p && !((used0 >> lane) & 1) && M[lane * kSwPitch + col] != 0;
-        const bool c1 = lane + 64 < p && !((used1 >> lane) & 1) && M[(lane + 64) * kSwPitch + col] != 0;
+        const bool c0 = lane < p && !((used0 >> lane) & 1) && M[lane * kPitch + col] != 0;
+        const bool c1 = MP > 64 && lane + 64 < p && !((used1 >> lane) & 1) && M[(lane + 64) * kPitch + col] != 0;
         const uint64_t b0 = __ballot(c0), b1 = __ballot(c1);
         int pr = -1;
         if (b0) pr = (int)__ffsll((unsigned long long)b0) - 1;
         else if (b1) pr = 64 + (int)__ffsll((unsigned long long)b1) - 1;
-        if (lane == 0) piv[col] = (int8_t)pr;
+        if (lane == 0) S.piv[col] = (int8_t)pr;
         if (pr < 0) continue;  // free column (uniform)
         if (pr < 64) used0 |= 1ull << pr;
         else used1 |= 1ull << (pr - 64);
-        uint8_t *P = M + pr * kSwPitch;
+        uint8_t *P = M + pr * kPitch;
         const uint32_t iv = ginv(g, P[col]);
         SWD_WAVE_SYNC();
         for (int j = lane; j < W; j += 64) P[j] = (uint8_t)gmul(g, P[j], iv);
         SWD_WAVE_SYNC();
         for (int q = lane; q < p; q += 64) {
             if (q == pr) continue;
-            uint8_t *row = M + q * kSwPitch;
+            uint8_t *row = M + q * kPitch;
             const uint32_t f = row[col];
             if (!f) continue;
             for (int j = 0; j < W; j++) row[j] ^= (uint8_t)gmul(g, f, P[j]);
@@ -465,10 +430,10 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     bool det = false;
     int prc = -1;
     if (lane < e) {
-        prc = piv[lane];
+        prc = S.piv[lane];
         det = prc >= 0;
         for (int j = 0; j < e && det; j++)
-            if (piv[j] < 0 && M[prc * kSwPitch + j]) det = false;
+            if (S.piv[j] < 0 && M[prc * kPitch + j]) det = false;
     }
     const uint64_t dm = __ballot(det);
     const int ndet = __popcll(dm);
@@ -476,49 +441,104 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     // are not computed: only pivot rows can appear in a solve row
     for (int q = lane; q < p; q += 64) {
         bool need = false;
-        for (int col = 0; col < e && !need; col++) need = ((dm >> col) & 1) && M[piv[col] * kSwPitch + e + q] != 0;
-        if (!need) a.syn_jobs[g0 + q].nout = 0;
+        for (int col = 0; col < e && !need; col++) need = ((dm >> col) & 1) && M[S.piv[col] * kPitch + e + q] != 0;
+        if (!need) a.syn_jobs[eq[q]].nout = 0;
     }
     if (ndet == 0) return 0;
     // solve jobs in the system's unknown slots x .. (ndet <= e), outputs at
-    // x + d, coefficients at 64 bytes per equation from g0 (ndet * p <= 64 * p)
-    const uint64_t c0 = (uint64_t)g0 * kSwSmallE;
+    // x + d; inputs the syndrome rows t_first .. t_last, coefficients at 64
+    // bytes per repair from t_first (ndet <= 64, so ndet * nin fits)
+    const uint32_t t_first = eq[0], nin = eq[p - 1] - t_first + 1;
+    const uint64_t c0 = (uint64_t)t_first * kSwSmallE;
     if (det) {
         const int d = __popcll(dm & lanes_below(lane));
-        uint8_t *cf = a.sol_coef + c0 + (uint64_t)d * p;
-        for (int t = 0; t < p; t++) cf[t] = M[prc * kSwPitch + e + t];
+        uint8_t *cf = a.sol_coef + c0 + (uint64_t)d * nin;
+        int q = 0;
+        for (uint32_t r = 0; r < nin; r++) {
+            uint8_t v = 0;
+            if (q < p && eq[q] == t_first + r) v = M[prc * kPitch + e + q++];
+            cf[r] = v;
+        }
         a.sol_outs[x + d] = (uint64_t)U[lane] * a.stride;
         a.stat[U[lane]] = FECGPU_STATUS_OK;
     }
     const int nj = (ndet + 7) / 8;
     if (lane < nj) {
         CombJob J;
-        J.in_off = (uint64_t)g0 * a.stride;
-        J.coef_off = c0 + (uint64_t)lane * 8 * p;
+        J.in_off = (uint64_t)t_first * a.stride;
+        J.coef_off = c0 + (uint64_t)lane * 8 * nin;
         J.out_list = x + (uint64_t)lane * 8;
         J.xor_off = kNoXor;
-        J.nin = (uint32_t)p;
+        J.nin = nin;
         J.nout = (uint32_t)min(8, ndet - 8 * lane);
         a.sol_jobs[x + lane] = J;
     }
+    *nin_out = nin;
     return ndet;
 }
 
+// The system lost[x .. x + e) with candidate repairs [t_lo, t_hi): solved here
+// when its equations fit ME / MP (and the range of syndrome rows kSwSolveIn),
+// else queued for the next pass (mid, then long).
+template <int ME, int MP, bool MID>
+__device__ void sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, uint32_t x, uint32_t e,
+                        uint64_t t_lo, uint64_t t_hi, int lane, uint32_t &rec, uint32_t &maxin) {
+    bool fits = (int)e <= ME && (int)e < a.long_min;
+    uint32_t p = 0;
+    if (fits) {
+        if (lane < (int)e) S.U[lane] = a.lost[x + lane];
+        for (uint64_t t0 = t_lo; t0 < t_hi; t0 += 64) {
+            const uint64_t t = t0 + lane;
+            bool hd = false;
+            if (t < t_hi && a.rep_present[t]) hd = holds(a, a.hdr[t], x, e);
+            const uint64_t b = __ballot(hd);
+            const uint32_t n = __popcll(b);
+            if (p + n > (uint32_t)MP) {
+                fits = false;
+                break;
+            }
+            if (hd) S.eq[p + __popcll(b & lanes_below(lane))] = (uint32_t)t;
+            p += n;
+        }
+        SWD_WAVE_SYNC();
+        if (fits && p && S.eq[p - 1] - S.eq[0] + 1 > (uint32_t)kSwSolveIn) fits = false;
+    }
+    if (!fits) {
+        if (lane == 0) {
+            const bool to_mid = !MID && (int)e <= kSwSmallE && (int)e < a.long_min;
+            const uint32_t k = atomicAdd(to_mid ? &a.ctr->nmid : &a.ctr->nlong, 1u);
+            if (k < a.long_cap) {
+                SwLong L{};
+                L.x0 = x;
+                L.e = e;
+                L.t_lo = (uint32_t)t_lo;
+                L.t_hi = (uint32_t)t_hi;
+                (to_mid ? a.mids : a.longs)[k] = L;
+            } else {
+                atomicOr(&a.ctr->err, 2u);
+            }
+        }
+        return;
+    }
+    if (p == 0) return;  // no received repair holds it: stays lost
+    uint32_t nin = 0;
+    const int nd = small_solve<ME, MP>(a, g, x, (int)e, (int)p, S, lane, &nin);
+    rec += (uint32_t)nd;
+    if (nd) maxin = max(maxin, nin);
+}
+
 // A wave per lost source; the waves at a system start find its extent and
-// equations and solve it (small) or queue it (long).
+// solve it (tiny) or queue it (mid, long).
 __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     __shared__ GfLds g;
-    __shared__ uint8_t s_M[kBlock / 64][kSwSmallP * kSwPitch];
-    __shared__ uint32_t s_U[kBlock / 64][kSwSmallE];
-    __shared__ uint32_t s_eq[kBlock / 64][kSwSmallP];
-    __shared__ int8_t s_piv[kBlock / 64][kSwSmallE];
+    __shared__ SysLds<kSwTinyE, kSwTinyP> s_sys[kBlock / 64];
     gf_load(g);
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (a.ctr->err & 1u) return;
     const uint32_t nlost = a.ctr->nlost, wmax = max(1u, a.ctr->wmax);
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
-    uint32_t rec = 0, maxp = 0;  // this wave's recovered count, widest solve
+    uint32_t rec = 0, maxin = 0;  // this wave's recovered count, widest solve
     for (uint64_t x = (uint64_t)blockIdx.x * (kBlock / 64) + wave; x < nlost; x += nwaves) {
         const uint32_t lx = a.lost[x];
         if (x > 0 && a.reachL[x - 1] > lx) continue;  // not a system start (uniform)
@@ -537,52 +557,32 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
         const uint32_t last = a.lost[x + e - 1];
         // candidate repairs: fss in [lx - wmax + 1, last]
         const uint64_t t_lo = a.rcnt[lx >= wmax ? lx - wmax + 1 : 0], t_hi = a.rcnt[(uint64_t)last + 1];
-        bool small = (int)e <= kSwSmallE && (int)e < a.long_min;
-        uint32_t p = 0, t_first = 0;
-        if (small) {
-            if (lane < (int)e) s_U[wave][lane] = a.lost[x + lane];
-            for (uint64_t t0 = t_lo; t0 < t_hi; t0 += 64) {
-                const uint64_t t = t0 + lane;
-                bool hd = false;
-                if (t < t_hi && a.rep_present[t]) hd = holds(a, a.hdr[t], (uint32_t)x, e);
-                const uint64_t b = __ballot(hd);
-                const uint32_t n = __popcll(b);
-                if (p + n > (uint32_t)kSwSmallP) {
-                    small = false;
-                    break;
-                }
-                if (hd) s_eq[wave][p + __popcll(b & lanes_below(lane))] = (uint32_t)t;
-                if (p == 0 && b) t_first = (uint32_t)(t0 + __ffsll((unsigned long long)b) - 1);
-                p += n;
-            }
-        }
-        if (!small) {
-            if (lane == 0) {
-                const uint32_t k = atomicAdd(&a.ctr->nlong, 1u);
-                if (k < a.long_cap) {
-                    SwLong L{};
-                    L.x0 = (uint32_t)x;
-                    L.e = e;
-                    L.t_lo = (uint32_t)t_lo;
-                    L.t_hi = (uint32_t)t_hi;
-                    a.longs[k] = L;
-                } else {
-                    atomicOr(&a.ctr->err, 2u);
-                }
-            }
-            continue;
-        }
-        if (p == 0) continue;  // no received repair holds it: stays lost
-        SWD_WAVE_SYNC();
-        const uint32_t g0 = a.eqidx[t_first];
-        const int nd = small_solve(a, g, (uint32_t)x, (int)e, (int)p, g0, s_U[wave], s_eq[wave], s_M[wave],
-                                   s_piv[wave], lane);
-        rec += (uint32_t)nd;
-        if (nd) maxp = max(maxp, p);
+        sys_one<kSwTinyE, kSwTinyP, false>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin);
     }
     if (lane == 0) {
         if (rec) atomicAdd(&a.ctr->recovered, rec);
-        if (maxp) atomicMax(&a.ctr->maxp, maxp);
+        if (maxin) atomicMax(&a.ctr->maxin, maxin);
+    }
+}
+
+// The queued systems too wide for the tiny pass: a wave each, up to 64
+// unknowns and 96 equations; wider ones go on to the long-system pass.
+__global__ __launch_bounds__(kBlock) void sw_dec_mid_kernel(SwDecArgs a) {
+    __shared__ GfLds g;
+    __shared__ SysLds<kSwSmallE, kSwSmallP> s_sys[kBlock / 64];
+    gf_load(g);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (a.ctr->err & 1u) return;
+    const uint32_t nmid = min(a.ctr->nmid, (uint32_t)a.long_cap);
+    uint32_t rec = 0, maxin = 0;
+    for (uint32_t k = blockIdx.x * (kBlock / 64) + wave; k < nmid; k += gridDim.x * (kBlock / 64)) {
+        const SwLong L = a.mids[k];
+        sys_one<kSwSmallE, kSwSmallP, true>(a, g, s_sys[wave], L.x0, L.e, L.t_lo, L.t_hi, lane, rec, maxin);
+    }
+    if (lane == 0) {
+        if (rec) atomicAdd(&a.ctr->recovered, rec);
+        if (maxin) atomicMax(&a.ctr->maxin, maxin);
     }
 }
 
@@ -841,10 +841,10 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
             continue;
         }
         // syndrome jobs for the pivot rows (the only rows whose data is used), in
-        // their equations' slots; the other equations' slots stay empty
+        // their repairs' slots; the other slots stay empty
         for (uint32_t q = lane; q < npiv; q += 64) {
             const uint32_t t = a.pivt[piv0 + q];
-            const uint32_t gq = a.eqidx[t];
+            const uint32_t gq = t;
             const fecgpu_sw_repair h = a.hdr[t];
             CombJob J;
             J.in_off = h.fss * a.stride;
@@ -1043,14 +1043,12 @@ hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(sw_dec_scan_kernel, dim3(1), dim3(1024), 0, s, a.chunk, a.nchunk, 3, 1, &a.ctr->nlost);
     hipLaunchKernelGGL(sw_dec_lost_kernel, dim3(a.nchunk), dim3(kBlock), 0, s, a);
     if (a.nrep) {
-        const uint32_t nrc = (uint32_t)((a.nrep + kSwChunk - 1) / kSwChunk);
-        hipLaunchKernelGGL(sw_dec_eqcount_kernel, dim3(nrc), dim3(kBlock), 0, s, a);
-        hipLaunchKernelGGL(sw_dec_scan_kernel, dim3(1), dim3(1024), 0, s, a.echunk, nrc, 1, 0, &a.ctr->neq);
-        hipLaunchKernelGGL(sw_dec_eqwrite_kernel, dim3(nrc), dim3(kBlock), 0, s, a);
-        // a wave per lost source at most; persistent beyond two blocks per CU
+        // a wave per lost source at most; persistent beyond what fits the chip
         const uint64_t want = (a.nsrc + kBlock / 64 - 1) / (kBlock / 64);
-        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 2));
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 6));
         hipLaunchKernelGGL(sw_dec_sys_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL(sw_dec_mid_kernel, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(a.long_cap, (uint64_t)cu_count() * 2))),
+                           dim3(kBlock), 0, s, a);
     }
     return hipGetLastError();
 }
