@@ -135,11 +135,18 @@ __global__ __launch_bounds__(kBlock) void sw_dec_hdr_kernel(SwDecArgs a) {
             }
         }
     }
+    __shared__ uint32_t s_w[kBlock / 64];
     w = wave_max(w);
     const uint64_t anybad = __ballot(bad);
     if ((threadIdx.x & 63) == 0) {
-        if (w) atomicMax(&a.ctr->wmax, w);
+        s_w[threadIdx.x >> 6] = w;
         if (anybad) atomicOr(&a.ctr->err, 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t m = 0;
+        for (int i = 0; i < kBlock / 64; i++) m = max(m, s_w[i]);
+        if (m) atomicMax(&a.ctr->wmax, m);  // one atomic per block
     }
 }
 
@@ -527,6 +534,27 @@ __device__ void sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, u
     if (nd) maxin = max(maxin, nin);
 }
 
+// The block's recovered count and widest solve into the call's counters: one
+// atomic each per block (same-address atomics from every wave serialised at
+// the L2 and cost more than the systems themselves).
+__device__ __forceinline__ void block_counts(const SwDecArgs &a, uint32_t rec, uint32_t maxin, int lane, int wave) {
+    __shared__ uint32_t s_rec[kBlock / 64], s_in[kBlock / 64];
+    if (lane == 0) {
+        s_rec[wave] = rec;
+        s_in[wave] = maxin;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t r = 0, m = 0;
+        for (int w = 0; w < kBlock / 64; w++) {
+            r += s_rec[w];
+            m = max(m, s_in[w]);
+        }
+        if (r) atomicAdd(&a.ctr->recovered, r);
+        if (m) atomicMax(&a.ctr->maxin, m);
+    }
+}
+
 // A wave per lost source; the waves at a system start find its extent and
 // solve it (tiny) or queue it (mid, long).
 __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
@@ -559,10 +587,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
         const uint64_t t_lo = a.rcnt[lx >= wmax ? lx - wmax + 1 : 0], t_hi = a.rcnt[(uint64_t)last + 1];
         sys_one<kSwTinyE, kSwTinyP, false>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin);
     }
-    if (lane == 0) {
-        if (rec) atomicAdd(&a.ctr->recovered, rec);
-        if (maxin) atomicMax(&a.ctr->maxin, maxin);
-    }
+    block_counts(a, rec, maxin, lane, wave);
 }
 
 // The queued systems too wide for the tiny pass: a wave each, up to 64
@@ -580,10 +605,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_mid_kernel(SwDecArgs a) {
         const SwLong L = a.mids[k];
         sys_one<kSwSmallE, kSwSmallP, true>(a, g, s_sys[wave], L.x0, L.e, L.t_lo, L.t_hi, lane, rec, maxin);
     }
-    if (lane == 0) {
-        if (rec) atomicAdd(&a.ctr->recovered, rec);
-        if (maxin) atomicMax(&a.ctr->maxin, maxin);
-    }
+    block_counts(a, rec, maxin, lane, wave);
 }
 
 // ========================================================= long systems ===

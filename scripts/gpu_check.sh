@@ -47,6 +47,8 @@ for s in "$@"; do
                    --dist-backend gloo ;;  # N>1 rehearsal: 2 ranks share the box's GPU
         prof2) step prof2 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof2 -o run -- \
                    python bench.py ;;  # the driver's default command, as is
+        swtests) step swtests 300 python -u -m pytest tests/test_gpu_swconn.py tests/test_gpu_sw.py -q -x \
+                     --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         prof5) prof prof5 5 ;;
         prof7) prof prof7 7 ;;
         abvar7)  # cfg7: default build vs every lib/libfecgpu_*.so variant (no check build), interleaved 3 times
