@@ -195,12 +195,12 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
         o += align256(bytes);
         return at;
     };
+    L.o_ctr = take(sizeof(SwDecCtr));  // ctr, reach and rcnt adjacent: one memset clears them
     L.o_reach = take((nsrc + 1) * 4);
     L.o_rcnt = take((nsrc + 1) * 4);
     L.o_chunk = take(3 * nchunk * 4);
     L.o_lost = take(nsrc * 4);
     L.o_reachL = take(nsrc * 4);
-    L.o_ctr = take(sizeof(SwDecCtr));
     L.o_synj = take(nrep * sizeof(CombJob));
     L.o_syno = take(nrep * 8);
     L.o_coef = take(nrep * (size_t)kSwCoefPitch);
@@ -270,9 +270,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.src = src;
     a.synd = static_cast<const uint8_t *>(psyn);
 
-    SW_TRY(hipMemsetAsync(a.ctr, 0, sizeof(SwDecCtr), s), "sliding-window decode counters");
-    // reach and rcnt are adjacent: one memset
-    SW_TRY(hipMemsetAsync(a.reach, 0, L.o_chunk - L.o_reach, s), "sliding-window decode reach");
+    SW_TRY(hipMemsetAsync(a.ctr, 0, L.o_chunk - L.o_ctr, s), "sliding-window decode counters");
     SW_TRY(launch_sw_dec_plan(a, s), "sliding-window decode plan launch");
     SW_TRY(launch_sw_dec_long(a, s), "sliding-window long-system plan launch");
     const uint32_t ncol = (S + 15u) >> 4;

@@ -361,9 +361,9 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     constexpr int kPitch = SysLds<ME, MP>::kPitch;
     uint8_t *M = S.M;
     const uint32_t *U = S.U, *eq = S.eq;
-    const int W = e + p;
+    const int W = e + p, W4 = (W + 3) / 4;  // row bytes, dwords
     for (int q = 0; q < p; q++)
-        for (int j = lane; j < W; j += 64) M[q * kPitch + j] = (uint8_t)(j >= e && j - e == q);
+        for (int j = lane; j < 4 * W4; j += 64) M[q * kPitch + j] = (uint8_t)(j >= e && j - e == q);
     SWD_WAVE_SYNC();
     // lane per equation: its coefficients (RFC 8681 §3.6); the lost sources'
     // go into A, the received sources' into its syndrome job
@@ -419,17 +419,25 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         if (pr < 0) continue;  // free column (uniform)
         if (pr < 64) used0 |= 1ull << pr;
         else used1 |= 1ull << (pr - 64);
+        // rows as dwords: a multiply is one split-table product per 4 bytes
         uint8_t *P = M + pr * kPitch;
+        uint32_t *Pw = reinterpret_cast<uint32_t *>(P);
         const uint32_t iv = ginv(g, P[col]);
         SWD_WAVE_SYNC();
-        for (int j = lane; j < W; j += 64) P[j] = (uint8_t)gmul(g, P[j], iv);
+        {
+            uint32_t tab[5];
+            set_tab(tab, iv);
+            for (int j = lane; j < W4; j += 64) Pw[j] = tmul(Pw[j], tab);
+        }
         SWD_WAVE_SYNC();
         for (int q = lane; q < p; q += 64) {
             if (q == pr) continue;
-            uint8_t *row = M + q * kPitch;
-            const uint32_t f = row[col];
+            uint32_t *row = reinterpret_cast<uint32_t *>(M + q * kPitch);
+            const uint32_t f = M[q * kPitch + col];
             if (!f) continue;
-            for (int j = 0; j < W; j++) row[j] ^= (uint8_t)gmul(g, f, P[j]);
+            uint32_t tab[5];
+            set_tab(tab, f);
+            for (int j = 0; j < W4; j++) row[j] ^= tmul(Pw[j], tab);
         }
         SWD_WAVE_SYNC();
     }
