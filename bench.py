@@ -17,6 +17,10 @@ Workloads (BASELINE.json configs):
   --config 7          : sliding-window RLC (RFC 8681): 524,288 x 1200 B sources per
                         GPU, a repair after every 8 over the last 32, 2% i.i.d. loss
                         of sources and repairs (a widening row, not a BASELINE config)
+The default run (one GPU, config 2) also times configs 3, 4 and 7 in the same
+process and reports them under "configs" in the same JSON line (each with its
+own ms_per_step, roofline, cpu_baseline and verify); the headline fields are
+config 2's.
 Multi-GPU: one process per GPU, windows sharded by rank with no data-path
 collective (weak scaling); RCCL only carries the barrier, the max-over-ranks
 time reduction and the 8-byte digest all-gather.  `--gpus N` launched without
@@ -79,6 +83,9 @@ def parse():
     ap.add_argument("--host-direct", type=int, default=-1,
                     help="tuning (config 5/6): kernels write outputs to mapped host memory, bit 0 encode, bit 1 decode")
     ap.add_argument("--host-chunk-mb", type=int, default=0, help="tuning (config 5/6): pipeline chunk size")
+    ap.add_argument("--extra-configs", type=int, choices=[0, 1], default=1,
+                    help="one-GPU default run (config 2): also time configs 3, 4 and 7 in this process and "
+                         "report them under \"configs\" (0 = config 2 only)")
     return ap.parse_args()
 
 
@@ -223,34 +230,13 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd).returncode
 
 
-def main():
-    args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a mislabelled run")
-        sys.exit(2)
-    log(f"rank {rank}/{world} (local {local}) starting, backend "
-        f"{args.dist_backend if world > 1 else 'none'}")
-    if world > 1:
-        if args.dist_backend == "nccl":  # RCCL: one rank per GPU
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:  # rehearsal of the N>1 path with ranks sharing the box's GPUs
-            torch.cuda.set_device(local % torch.cuda.device_count())
-            dist.init_process_group("gloo")
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+# extra configs timed by the default one-GPU run: config ->
+# (steps, warmup); cfg3 warms up longer (its first ~10 calls run slow while the
+# clocks and TLBs settle)
+EXTRA_CONFIGS = {3: (10, 10), 4: (5, 2), 7: (50, 10)}
 
-    cfg = workloads.CONFIGS[args.config]
-    if args.matrix != "cauchy" and cfg.scheme not in ("xor", "sw"):
-        cfg = dataclasses.replace(cfg, matrix=args.matrix, name=f"{cfg.name}-{args.matrix}")
-    nwin = args.nwin or cfg.nwin_per_gpu
-    w0, nwin = shard.weak_shard(rank, world, nwin)  # this rank's global window range
+
+def make_ctx(args):
     ctx = fecgpu.Context()
     if args.grid_mult:
         ctx.set_tuning("grid_mult", args.grid_mult)
@@ -268,6 +254,18 @@ def main():
         ctx.set_tuning("host_direct", args.host_direct)
     if args.host_chunk_mb:
         ctx.set_tuning("host_chunk_mb", args.host_chunk_mb)
+    return ctx
+
+
+def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, warmup: int, nwin_arg: int):
+    """Time `steps` steps of one config (after `warmup`), verify, digest; rank 0
+    returns the JSON line's dict (others None).  Raises nothing on a failed
+    verify: the line carries it."""
+    cfg = workloads.CONFIGS[cfgid]
+    if args.matrix != "cauchy" and cfg.scheme not in ("xor", "sw"):
+        cfg = dataclasses.replace(cfg, matrix=args.matrix, name=f"{cfg.name}-{args.matrix}")
+    nwin = nwin_arg or cfg.nwin_per_gpu
+    w0, nwin = shard.weak_shard(rank, world, nwin)  # this rank's global window range
     if cfg.scheme == "sw":  # config 7: one sliding-window stream per rank
         batch = workloads.SwBatch.allocate(cfg, nwin, dev)
         log(f"rank {rank}: {cfg.name}, {batch.nsrc} sources, {batch.nrep} repairs, "
@@ -288,14 +286,14 @@ def main():
     src_bytes = batch.source_bytes()      # per rank, per step
     alg = batch.algorithmic_bytes()       # {'encode': B, 'decode': B} per launch
 
-    log("warmup")
-    for _ in range(args.warmup):
+    log(f"{cfg.name}: warmup {warmup}")
+    for _ in range(warmup):
         batch.encode(ctx)
         batch.decode(ctx)
     torch.cuda.synchronize()
 
     every = args.event_every
-    ev_steps = [i for i in range(args.steps) if every > 0 and i % every == 0]
+    ev_steps = [i for i in range(steps) if every > 0 and i % every == 0]
     ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
               torch.cuda.Event(enable_timing=True)) for i in ev_steps}
     host_t = [0.0, 0.0]
@@ -303,7 +301,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         if cfg.host:  # synchronous calls on the library's own streams
             ta = time.perf_counter()
             batch.encode(ctx)
@@ -327,104 +325,152 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if cfg.host:
-        enc_ms, dec_ms = host_t[0] * 1e3 / args.steps, host_t[1] * 1e3 / args.steps
+        enc_ms, dec_ms = host_t[0] * 1e3 / steps, host_t[1] * 1e3 / steps
     elif not ev:
         enc_ms = dec_ms = float("nan")
     else:
         enc_ms = sum(a.elapsed_time(b) for a, b, _ in ev.values()) / len(ev)
         dec_ms = sum(b.elapsed_time(c) for _, b, c in ev.values()) / len(ev)
 
-    log(f"timed {args.steps} steps: {elapsed:.4f} s (encode {enc_ms:.3f} ms, decode {dec_ms:.3f} ms)")
+    log(f"{cfg.name}: timed {steps} steps: {elapsed:.4f} s (encode {enc_ms:.3f} ms, decode {dec_ms:.3f} ms)")
     elapsed, tot = shard.reduce_run(elapsed, src_bytes, dev if args.dist_backend == "nccl" else None)
-    total_src = float(tot) * args.steps
+    total_src = float(tot) * steps
     value = total_src / elapsed / 1e9
 
     verify = None if args.no_verify else batch.verify(ctx, w0)
-    log(f"verify: {verify}")
+    log(f"{cfg.name}: verify: {verify}")
     # run digest of every rank's encoded windows, gathered over RCCL (8 B per
     # rank over xGMI: the path's only collective, outside the timed region)
     digest = None
     if verify is not None and not cfg.host:
         digest = shard.gather_digest(batch.digest(ctx, w0),
                                      dev if args.dist_backend == "nccl" else None)
-
-    if rank == 0:
-        dom = "decode" if dec_ms > enc_ms else "encode"
-        dom_ms = enc_ms if dom == "encode" else dec_ms
-        achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
-        traffic, traffic_src = (pmc_traffic(args.config, dom)
-                                if nwin == cfg.nwin_per_gpu and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
-                                else (None, None))
-        cpu = None
-        if args.cpu_seconds > 0 and world == 1:
-            log("cpu baseline")
-            cpu = (cpu_baseline_sw(cfg, args.cpu_seconds) if cfg.scheme == "sw" else
-                   cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads))
-        peak, bound = (PCIE_PEAK_GBS, "pcie") if cfg.host else (HBM_PEAK_GBS, "hbm")
-        line = {
-            "metric": ("GB/s source-packet bytes FEC encode+decode, host buffers, PCIe-inclusive"
-                       if cfg.host else
-                       "GB/s source-packet bytes FEC encode+decode, device-resident, per MI355X"),
-            "value": round(value, 3),
+    del batch
+    torch.cuda.empty_cache()
+    if rank != 0:
+        return None
+    dom = "decode" if dec_ms > enc_ms else "encode"
+    dom_ms = enc_ms if dom == "encode" else dec_ms
+    achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+    traffic, traffic_src = (pmc_traffic(cfgid, dom)
+                            if nwin == cfg.nwin_per_gpu and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
+                            else (None, None))
+    cpu = None
+    if args.cpu_seconds > 0 and world == 1:
+        log(f"{cfg.name}: cpu baseline")
+        cpu = (cpu_baseline_sw(cfg, args.cpu_seconds) if cfg.scheme == "sw" else
+               cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads))
+    peak, bound = (PCIE_PEAK_GBS, "pcie") if cfg.host else (HBM_PEAK_GBS, "hbm")
+    return {
+        "metric": ("GB/s source-packet bytes FEC encode+decode, host buffers, PCIe-inclusive"
+                   if cfg.host else
+                   "GB/s source-packet bytes FEC encode+decode, device-resident, per MI355X"),
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "ranks": world,
+        "gpus_used": min(world, torch.cuda.device_count()),
+        "rehearsal": (None if world <= torch.cuda.device_count() else
+                      f"{world} ranks share {torch.cuda.device_count()} GPU(s) ({args.dist_backend}): "
+                      f"exercises the N>1 path, not a multi-GPU measurement"),
+        "value_per_gpu": round(value / world, 3),
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": ("synthetic (seeded torch bytes on the device, seeded host loss flags)" if cfg.scheme == "sw"
+                 else "synthetic (on-device splitmix64 packets, seeded erasures)"),
+        "config": ({
+            "workload": cfg.name, "scheme": "sliding-window RLC (RFC 8681)",
+            "sources_per_gpu": nwin * cfg.k, "repairs_per_gpu": nwin, "window": cfg.window,
+            "step": cfg.k, "packet_bytes": cfg.L, "erasures": cfg.erasure_desc,
+            "parallelism": f"stream per rank x{world}",
+            "decode": "planned on the device (fecgpu_sw_decode_device: arrival flags, headers and "
+                      "statuses in HBM; no host work per call)",
+        } if cfg.scheme == "sw" else {
+            "workload": cfg.name,
+            "scheme": cfg.scheme, "k": cfg.k, "r": cfg.r,
+            **({"matrix": cfg.matrix} if cfg.scheme != "xor" else {}),
+            "windows_per_gpu": nwin, "packet_bytes": cfg.L if cfg.workload == 0 else "1200|9000 mixed",
+            "erasures": cfg.erasure_desc,
+            "parallelism": f"window-shard x{world}",
+        }),
+        "kernels_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
+        "kernel_timing": ("host wall clock per synchronous call" if cfg.host else
+                          f"HIP events on the launch stream around encode/decode, "
+                          f"every {args.event_every}th timed step ({len(ev)} samples)"),
+        "roofline": {
+            "bound": bound,
+            "kernel": dom,
+            "achieved": round(achieved, 1),
+            "peak": peak,
             "unit": "GB/s",
-            "n_gpus": world,
-            "ranks": world,
-            "gpus_used": min(world, torch.cuda.device_count()),
-            "rehearsal": (None if world <= torch.cuda.device_count() else
-                          f"{world} ranks share {torch.cuda.device_count()} GPU(s) ({args.dist_backend}): "
-                          f"exercises the N>1 path, not a multi-GPU measurement"),
-            "value_per_gpu": round(value / world, 3),
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": ("synthetic (seeded torch bytes on the device, seeded host loss flags)" if cfg.scheme == "sw"
-                     else "synthetic (on-device splitmix64 packets, seeded erasures)"),
-            "config": ({
-                "workload": cfg.name, "scheme": "sliding-window RLC (RFC 8681)",
-                "sources_per_gpu": nwin * cfg.k, "repairs_per_gpu": nwin, "window": cfg.window,
-                "step": cfg.k, "packet_bytes": cfg.L, "erasures": cfg.erasure_desc,
-                "parallelism": f"stream per rank x{world}",
-                "decode": "planned on the device (fecgpu_sw_decode_device: arrival flags, headers and "
-                          "statuses in HBM; no host work per call)",
-            } if cfg.scheme == "sw" else {
-                "workload": cfg.name,
-                "scheme": cfg.scheme, "k": cfg.k, "r": cfg.r,
-                **({"matrix": cfg.matrix} if cfg.scheme != "xor" else {}),
-                "windows_per_gpu": nwin, "packet_bytes": cfg.L if cfg.workload == 0 else "1200|9000 mixed",
-                "erasures": cfg.erasure_desc,
-                "parallelism": f"window-shard x{world}",
-            }),
-            "kernels_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
-            "kernel_timing": ("host wall clock per synchronous call" if cfg.host else
-                              f"HIP events on the launch stream around encode/decode, "
-                              f"every {args.event_every}th timed step ({len(ev)} samples)"),
-            "roofline": {
-                "bound": bound,
-                "kernel": dom,
-                "achieved": round(achieved, 1),
-                "peak": peak,
-                "unit": "GB/s",
-                "frac": round(achieved / peak, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "alg_bytes_per_launch": alg[dom],
-            },
-            "roofline_other": {
-                k2: round(alg[k2] / (ms * 1e-3) / 1e9, 1)
-                for k2, ms in (("encode", enc_ms), ("decode", dec_ms))
-            },
-            "cpu_baseline": cpu,
-            "verify": verify,
-            "digest": None if digest is None else f"{digest:016x}",
-        }
+            "frac": round(achieved / peak, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "alg_bytes_per_launch": alg[dom],
+        },
+        "roofline_other": {
+            k2: round(alg[k2] / (ms * 1e-3) / 1e9, 1)
+            for k2, ms in (("encode", enc_ms), ("decode", dec_ms))
+        },
+        "cpu_baseline": cpu,
+        "verify": verify,
+        "digest": None if digest is None else f"{digest:016x}",
+    }
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a mislabelled run")
+        sys.exit(2)
+    log(f"rank {rank}/{world} (local {local}) starting, backend "
+        f"{args.dist_backend if world > 1 else 'none'}")
+    if world > 1:
+        if args.dist_backend == "nccl":  # RCCL: one rank per GPU
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:  # rehearsal of the N>1 path with ranks sharing the box's GPUs
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ctx = make_ctx(args)
+    line = run_config(args.config, args, rank, world, dev, ctx, args.steps, args.warmup, args.nwin)
+    ok = line is None or line["verify"] is None or line["verify"].get("ok", False)
+    # the default one-GPU run also times the other single-GPU configs in this
+    # process (each on its own batch, freed after), under "configs"; the
+    # headline line above is config 2's as before
+    if world == 1 and args.extra_configs and args.config == 2 and not args.nwin:
+        extras = {}
+        for cid, (st, wu) in EXTRA_CONFIGS.items():
+            try:
+                sub = run_config(cid, args, rank, world, dev, ctx, st, wu, 0)
+            except Exception as exc:  # keep the headline line; report the failure
+                log(f"config {cid} failed: {exc!r}")
+                extras[f"cfg{cid}"] = {"error": repr(exc)}
+                ok = False
+                continue
+            ok = ok and (sub["verify"] is None or sub["verify"].get("ok", False))
+            extras[f"cfg{cid}"] = {k: sub[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup",
+                                                       "config", "kernels_ms", "roofline", "roofline_other",
+                                                       "cpu_baseline", "verify", "digest")}
+        line["configs"] = extras
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if verify is not None and not verify.get("ok", False):
+    if not ok:
         sys.exit(3)
 
 
