@@ -361,3 +361,328 @@ void orc_decode_batch_simd(int scheme, int k, int r, const uint32_t *S, uint32_t
                            int nthreads) {
     run_sbatch(1, scheme, k, r, S, stride, nwin, present, status, wins, nthreads);
 }
+
+/* ------------------------------------------ sliding-window RLC (cfg7) --- */
+/* The CPU baseline of the sliding-window code (RFC 8681, m = 8): encode is a
+ * dot product per repair over its window; decode splits the lost sources into
+ * linked systems, gives each thread a run of whole systems and solves them by
+ * the banded elimination of fec_sw_banded.c (forward elimination with the
+ * earliest-ending pivot, null-space sweep, back substitution), with every data
+ * row operation vectorised.  Outputs equal orc_sw_encode / orc_sw_decode
+ * (tests/test_oracle_simd.py). */
+
+/* y ^= c * x over n bytes */
+__attribute__((target("avx2,gfni"))) static void axpy_gfni(uint8_t *y, uint8_t c, const uint8_t *x, uint32_t n,
+                                                           const coef_t *t) {
+    uint32_t p = 0;
+    const __m256i m = _mm256_set1_epi64x((long long)t->gfni);
+    for (; p + 32 <= n; p += 32) {
+        const __m256i d = _mm256_loadu_si256((const __m256i *)(x + p));
+        _mm256_storeu_si256((__m256i *)(y + p), _mm256_xor_si256(_mm256_loadu_si256((const __m256i *)(y + p)),
+                                                                 _mm256_gf2p8affine_epi64_epi8(d, m, 0)));
+    }
+    for (; p < n; p++) y[p] ^= gmul(c, x[p]);
+}
+__attribute__((target("avx2"))) static void axpy_avx2(uint8_t *y, uint8_t c, const uint8_t *x, uint32_t n,
+                                                      const coef_t *t) {
+    const __m256i mask = _mm256_set1_epi8(0x0f);
+    const __m256i tl = _mm256_loadu_si256((const __m256i *)t->lo), th = _mm256_loadu_si256((const __m256i *)t->hi);
+    uint32_t p = 0;
+    for (; p + 32 <= n; p += 32) {
+        const __m256i d = _mm256_loadu_si256((const __m256i *)(x + p));
+        const __m256i pr = _mm256_xor_si256(_mm256_shuffle_epi8(tl, _mm256_and_si256(d, mask)),
+                                            _mm256_shuffle_epi8(th, _mm256_and_si256(_mm256_srli_epi64(d, 4), mask)));
+        _mm256_storeu_si256((__m256i *)(y + p), _mm256_xor_si256(_mm256_loadu_si256((const __m256i *)(y + p)), pr));
+    }
+    for (; p < n; p++) y[p] ^= gmul(c, x[p]);
+}
+static void axpy(int level, uint8_t *y, uint8_t c, const uint8_t *x, uint32_t n) {
+    if (!c) return;
+    if (level == 0) {
+        for (uint32_t p = 0; p < n; p++) y[p] ^= gmul(c, x[p]);
+        return;
+    }
+    coef_t t;
+    coef_make(c, &t);
+    if (level >= 2) axpy_gfni(y, c, x, n, &t);
+    else axpy_avx2(y, c, x, n, &t);
+}
+
+typedef struct {
+    const uint8_t *src;
+    uint32_t S, stride;
+    const orc_sw_repair *hdr;
+    uint64_t lo, hi;
+    uint8_t *rep;
+    int level;
+} swenc_t;
+
+static void *run_swenc(void *p) {
+    const swenc_t *j = (const swenc_t *)p;
+    uint8_t cc[256];
+    coef_t tab[256];
+    const uint8_t *in[256];
+    for (uint64_t t = j->lo; t < j->hi; t++) {
+        const orc_sw_repair *h = &j->hdr[t];
+        orc_rlc_coefs(h->key, h->nss, h->dt, cc);
+        for (int q = 0; q < h->nss; q++) {
+            coef_make(cc[q], &tab[q]);
+            in[q] = j->src + (h->fss + (uint64_t)q) * j->stride;
+        }
+        uint8_t *out = j->rep + t * j->stride;
+        dot(j->level, h->nss, in, 1, &out, tab, j->S);
+    }
+    return NULL;
+}
+
+void orc_sw_encode_simd(const uint8_t *src, uint64_t nsrc, uint32_t S, uint32_t stride, const orc_sw_repair *hdr,
+                        uint64_t nrep, uint8_t *rep, int nthreads) {
+    (void)nsrc;
+    tables_init();
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    swenc_t jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        swenc_t x = {src, S, stride, hdr, nrep * (uint64_t)t / (uint64_t)nthreads,
+                     nrep * (uint64_t)(t + 1) / (uint64_t)nthreads, rep, orc_simd_level()};
+        jobs[t] = x;
+        if (nthreads == 1) run_swenc(&jobs[t]);
+        else pthread_create(&th[t], NULL, run_swenc, &jobs[t]);
+    }
+    if (nthreads > 1)
+        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+typedef struct {
+    int64_t lo, hi;  /* unknown range (system-local indices) */
+    uint8_t *a;      /* coefficients of unknowns lo..hi */
+    uint8_t *s;      /* right-hand side */
+} srow_t;
+
+typedef struct {
+    uint8_t *src;
+    const uint8_t *src_present, *rep, *rep_present;
+    const orc_sw_repair *hdr;
+    uint64_t nrep;
+    uint32_t S, stride;
+    uint8_t *status;
+    const int64_t *lost, *rank;  /* lost sources; rank[i] = lost sources before i */
+    int64_t xa, xb;              /* this part's lost range (whole systems) */
+    uint64_t ta, tb;             /* candidate repairs (fss in the part's span) */
+    int level;
+    int64_t rec;
+} swdec_t;
+
+static uint8_t scoef(const srow_t *r, int64_t c) { return (c < r->lo || c > r->hi) ? 0 : r->a[c - r->lo]; }
+
+static void *run_swdec(void *pp) {
+    swdec_t *J = (swdec_t *)pp;
+    const int64_t x0 = J->xa, e = J->xb - J->xa;
+    const uint32_t S = J->S;
+    if (e <= 0) return NULL;
+    srow_t *R = calloc(J->tb - J->ta + 1, sizeof(srow_t));
+    int64_t p = 0;
+    uint8_t cc[256];
+    for (uint64_t t = J->ta; t < J->tb; t++) {
+        if (!J->rep_present[t]) continue;
+        const orc_sw_repair *h = &J->hdr[t];
+        const int64_t r0 = J->rank[h->fss], r1 = J->rank[h->fss + h->nss];
+        if (r1 <= r0 || r0 >= J->xb || r1 <= J->xa) continue;  /* holds none of this part's unknowns */
+        srow_t *r = &R[p++];
+        r->lo = r0 - x0;
+        r->hi = r1 - 1 - x0;
+        r->a = calloc((size_t)(r->hi - r->lo + 1), 1);
+        r->s = malloc(S);
+        memcpy(r->s, J->rep + t * J->stride, S);
+        orc_rlc_coefs(h->key, h->nss, h->dt, cc);
+        /* syndrome: the received sources' terms, one vectorised dot */
+        const uint8_t *in[257];
+        coef_t tab[257];
+        int nin = 0;
+        in[nin] = r->s;
+        coef_make(1, &tab[nin++]);
+        for (int j = 0; j < h->nss; j++) {
+            const uint64_t i = h->fss + (uint64_t)j;
+            if (!J->src_present[i]) {
+                r->a[J->rank[i] - x0 - r->lo] = cc[j];
+            } else if (cc[j]) {
+                in[nin] = J->src + i * J->stride;
+                coef_make(cc[j], &tab[nin++]);
+            }
+        }
+        uint8_t *out = r->s;  /* in place: the dot reads each 32-B block before writing it */
+        dot(J->level, nin, in, 1, &out, tab, S);
+    }
+    /* forward elimination (rows in order of lo: repairs are in fss order) */
+    int64_t *piv = malloc(sizeof(int64_t) * e), *act = malloc(sizeof(int64_t) * (p ? p : 1));
+    int64_t nact = 0, next = 0, B = 1;
+    for (int64_t c = 0; c < e; c++) {
+        while (next < p && R[next].lo == c) act[nact++] = next++;
+        int64_t P = -1;
+        for (int64_t x = 0; x < nact; x++)
+            if (scoef(&R[act[x]], c) && (P < 0 || R[act[x]].hi < R[P].hi)) P = act[x];
+        piv[c] = P;
+        if (P >= 0) {
+            const srow_t *rp = &R[P];
+            const uint8_t ip = ginv(scoef(rp, c));
+            for (int64_t x = 0; x < nact; x++) {
+                srow_t *r = &R[act[x]];
+                if (act[x] == P || !scoef(r, c)) continue;
+                const uint8_t f = gmul(scoef(r, c), ip);
+                for (int64_t jj = c; jj <= rp->hi; jj++) r->a[jj - r->lo] ^= gmul(f, scoef(rp, jj));
+                axpy(J->level, r->s, f, rp->s, S);
+            }
+            if (rp->hi - c + 1 > B) B = rp->hi - c + 1;
+        }
+        int64_t w = 0;
+        for (int64_t x = 0; x < nact; x++)
+            if (act[x] != P && R[act[x]].hi > c) act[w++] = act[x];
+        nact = w;
+    }
+    /* null-space sweep (vectors over coordinates c .. c + 255, slot j % 256) */
+    uint8_t *det = calloc(e, 1);
+    int64_t cap = 64, nv = 0;
+    uint8_t *V = malloc((size_t)cap * 256);
+    for (int64_t c = e - 1; c >= 0; c--) {
+        const int sc = (int)(c & 255);
+        const int64_t P = piv[c];
+        if (P < 0) {
+            for (int64_t v = 0; v < nv; v++) V[v * 256 + sc] = 0;
+            if (nv == cap) { cap *= 2; V = realloc(V, (size_t)cap * 256); }
+            memset(V + nv * 256, 0, 256);
+            V[nv * 256 + sc] = 1;
+            nv++;
+        } else {
+            const srow_t *rp = &R[P];
+            const uint8_t ip = ginv(scoef(rp, c));
+            int zero = 1;
+            for (int64_t v = 0; v < nv; v++) {
+                uint8_t acc = 0;
+                for (int64_t j = c + 1; j <= rp->hi; j++) acc ^= gmul(scoef(rp, j), V[v * 256 + (j & 255)]);
+                acc = gmul(acc, ip);
+                V[v * 256 + sc] = acc;
+                zero &= acc == 0;
+            }
+            det[c] = (uint8_t)zero;
+        }
+        if (nv > 2 * B + 8) {  /* basis of the projection on [c, c + B) */
+            int64_t rank = 0;
+            for (int64_t jj = 0; jj < B && rank < nv; jj++) {
+                const int s = (int)((c + jj) & 255);
+                int64_t pv = -1;
+                for (int64_t v = rank; v < nv; v++)
+                    if (V[v * 256 + s]) { pv = v; break; }
+                if (pv < 0) continue;
+                if (pv != rank)
+                    for (int b = 0; b < 256; b++) {
+                        uint8_t tt = V[pv * 256 + b]; V[pv * 256 + b] = V[rank * 256 + b]; V[rank * 256 + b] = tt;
+                    }
+                const uint8_t iv = ginv(V[rank * 256 + s]);
+                for (int64_t v = rank + 1; v < nv; v++) {
+                    const uint8_t f = gmul(V[v * 256 + s], iv);
+                    if (!f) continue;
+                    for (int64_t j2 = 0; j2 < B; j2++) {
+                        const int s2 = (int)((c + j2) & 255);
+                        V[v * 256 + s2] ^= gmul(f, V[rank * 256 + s2]);
+                    }
+                }
+                rank++;
+            }
+            nv = rank;
+        }
+    }
+    /* back substitution (free unknowns 0): one vectorised dot per pivot */
+    uint8_t *X = calloc(256, S ? S : 1);
+    const uint8_t *in[257];
+    coef_t tab[257];
+    for (int64_t c = e - 1; c >= 0; c--) {
+        uint8_t *x = X + (size_t)(c & 255) * S;
+        const int64_t P = piv[c];
+        if (P < 0) {
+            memset(x, 0, S);
+            continue;
+        }
+        const srow_t *rp = &R[P];
+        const uint8_t ip = ginv(scoef(rp, c));
+        int nin = 0;
+        in[nin] = rp->s;
+        coef_make(ip, &tab[nin++]);
+        for (int64_t j = c + 1; j <= rp->hi; j++) {
+            const uint8_t a = scoef(rp, j);
+            if (!a) continue;
+            in[nin] = X + (size_t)(j & 255) * S;
+            coef_make(gmul(a, ip), &tab[nin++]);
+        }
+        dot(J->level, nin, in, 1, &x, tab, S);
+        if (det[c]) {
+            memcpy(J->src + (uint64_t)J->lost[x0 + c] * J->stride, x, S);
+            J->status[J->lost[x0 + c]] = ORC_OK;
+            J->rec++;
+        }
+    }
+    for (int64_t q = 0; q < p; q++) { free(R[q].a); free(R[q].s); }
+    free(R); free(piv); free(act); free(det); free(V); free(X);
+    return NULL;
+}
+
+/* Headers must be in fss order (the API's order); returns #recovered. */
+int64_t orc_sw_decode_simd(uint8_t *src, const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep,
+                           const uint8_t *rep_present, const orc_sw_repair *hdr, uint64_t nrep, uint32_t S,
+                           uint32_t stride, uint8_t *status, int nthreads) {
+    tables_init();
+    int64_t *rank = malloc(sizeof(int64_t) * (nsrc + 1)), *lost = malloc(sizeof(int64_t) * (nsrc ? nsrc : 1));
+    int64_t e = 0;
+    for (uint64_t i = 0; i < nsrc; i++) {
+        rank[i] = e;
+        status[i] = src_present[i] ? ORC_OK : ORC_UNRECOVERABLE;
+        if (!src_present[i]) lost[e++] = (int64_t)i;
+    }
+    rank[nsrc] = e;
+    /* system starts: lost[x] starts a system iff no received repair starting at
+     * or before lost[x - 1] reaches past lost[x] (reach = prefix max of ends) */
+    uint64_t wmax = 1;
+    for (uint64_t t = 0; t < nrep; t++)
+        if (hdr[t].nss > wmax) wmax = hdr[t].nss;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    int64_t cut[257];
+    cut[0] = 0;
+    {
+        uint64_t t = 0, reach = 0;
+        int part = 1;
+        for (int64_t x = 1; x < e && part < nthreads; x++) {
+            for (; t < nrep && hdr[t].fss <= (uint64_t)lost[x - 1]; t++)
+                if (rep_present[t] && hdr[t].fss + hdr[t].nss > reach) reach = hdr[t].fss + hdr[t].nss;
+            if (reach <= (uint64_t)lost[x] && x >= e * part / nthreads) cut[part++] = x;
+        }
+        for (; part <= nthreads; part++) cut[part] = e;
+    }
+    pthread_t th[256];
+    swdec_t jobs[256];
+    int64_t rec = 0;
+    for (int t = 0; t < nthreads; t++) {
+        swdec_t x = {src, src_present, rep, rep_present, hdr, nrep, S, stride, status, lost, rank,
+                     cut[t], cut[t + 1], 0, 0, orc_simd_level(), 0};
+        if (x.xb > x.xa) {
+            const uint64_t a = (uint64_t)lost[x.xa], b = (uint64_t)lost[x.xb - 1];
+            uint64_t lo = 0, hi = nrep;  /* first repair with fss >= a - wmax + 1 */
+            const uint64_t key = a >= wmax ? a - wmax + 1 : 0;
+            while (lo < hi) { const uint64_t m = (lo + hi) / 2; if (hdr[m].fss < key) lo = m + 1; else hi = m; }
+            x.ta = lo;
+            hi = nrep;
+            while (lo < hi) { const uint64_t m = (lo + hi) / 2; if (hdr[m].fss <= b) lo = m + 1; else hi = m; }
+            x.tb = lo;
+        }
+        jobs[t] = x;
+        if (nthreads == 1) run_swdec(&jobs[t]);
+        else pthread_create(&th[t], NULL, run_swdec, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++) {
+        if (nthreads > 1) pthread_join(th[t], NULL);
+        rec += jobs[t].rec;
+    }
+    free(rank);
+    free(lost);
+    return rec;
+}

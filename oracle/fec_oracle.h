@@ -135,6 +135,16 @@ int64_t orc_sw_decode_banded(uint8_t *src, const uint8_t *src_present, uint64_t 
                              const uint8_t *rep_present, const orc_sw_repair *hdr, uint64_t nrep,
                              uint32_t S, uint32_t stride, uint8_t *status);
 
+/* CPU baseline of the sliding-window code (fec_cpu_simd.c): the same outputs as
+ * orc_sw_encode / orc_sw_decode, vectorised at orc_simd_level() and spread over
+ * nthreads (encode: repairs; decode: runs of whole linked systems).  Decode
+ * needs the headers in fss order. */
+void    orc_sw_encode_simd(const uint8_t *src, uint64_t nsrc, uint32_t S, uint32_t stride,
+                           const orc_sw_repair *hdr, uint64_t nrep, uint8_t *rep, int nthreads);
+int64_t orc_sw_decode_simd(uint8_t *src, const uint8_t *src_present, uint64_t nsrc, const uint8_t *rep,
+                           const uint8_t *rep_present, const orc_sw_repair *hdr, uint64_t nrep,
+                           uint32_t S, uint32_t stride, uint8_t *status, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -76,6 +76,8 @@ def lib():
             "orc_simd_set_level": (None, [i32]),
             "orc_encode_batch_simd": (None, [i32, i32, i32, vp, u32, u64, vp, i32]),
             "orc_decode_batch_simd": (None, [i32, i32, i32, vp, u32, u64, vp, vp, vp, i32]),
+            "orc_sw_encode_simd": (None, [vp, u64, u32, u32, vp, u64, vp, i32]),
+            "orc_sw_decode_simd": (ctypes.c_int64, [vp, vp, u64, vp, vp, vp, u64, u32, u32, vp, i32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -162,6 +164,26 @@ def sw_decode_banded(src: np.ndarray, src_present: np.ndarray, rep: np.ndarray, 
     st = np.zeros(nsrc, np.uint8)
     n = lib().orc_sw_decode_banded(_p(src), _p(src_present), nsrc, _p(rep), _p(rep_present), _p(hdr),
                                    len(hdr), S, stride, _p(st))
+    return st, int(n)
+
+
+def sw_encode_simd(src: np.ndarray, hdr: np.ndarray, S: int, nthreads: int = 1) -> np.ndarray:
+    """sw_encode on the CPU baseline codec (fec_cpu_simd.c; same outputs)."""
+    nsrc, stride = src.shape
+    rep = np.zeros((len(hdr), stride), np.uint8)
+    src = np.ascontiguousarray(src)
+    lib().orc_sw_encode_simd(_p(src), nsrc, S, stride, _p(hdr), len(hdr), _p(rep), nthreads)
+    return rep
+
+
+def sw_decode_simd(src: np.ndarray, src_present: np.ndarray, rep: np.ndarray, rep_present: np.ndarray,
+                   hdr: np.ndarray, S: int, nthreads: int = 1):
+    """sw_decode on the CPU baseline codec (headers in fss order).  In place;
+    -> (status, #recovered)."""
+    nsrc, stride = src.shape
+    st = np.zeros(nsrc, np.uint8)
+    n = lib().orc_sw_decode_simd(_p(src), _p(src_present), nsrc, _p(rep), _p(rep_present), _p(hdr),
+                                 len(hdr), S, stride, _p(st), nthreads)
     return st, int(n)
 
 

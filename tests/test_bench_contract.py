@@ -38,12 +38,13 @@ def test_cpu_baseline_leg(bench, cfgid):
 
 
 def test_cpu_baseline_leg_sliding_window(bench):
-    """Config 7 (sliding-window RLC): the scalar C oracle on bounded slices."""
+    """Config 7 (sliding-window RLC): the vectorised, threaded CPU codec on the
+    config's stream shape (here a shortened stream)."""
     from fecgpu import workloads
     cfg = workloads.CONFIGS[7]
-    out = bench.cpu_baseline_sw(cfg, 0.05)
-    assert out["unit"] == "GB/s" and out["cores"] == 1 and out["kind"] == "port"
-    assert out["value"] > 0 and "8192 sources" in out["sample"]
+    out = bench.cpu_baseline_sw(cfg, 0.05, 2, nsrc=16384)
+    assert out["unit"] == "GB/s" and out["cores"] == 2 and out["kind"] == "port"
+    assert out["value"] > 0 and "16384 sources" in out["sample"] and "simd" in out["codec"]
 
 
 @pytest.mark.parametrize("cfgid,kernel", [(2, "encode"), (2, "decode"), (3, "encode"), (3, "decode"),

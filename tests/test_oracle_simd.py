@@ -46,3 +46,44 @@ def test_simd_levels_match_scalar_oracle(O, scheme, k, r, wl, L, era):
         for w in range(nwin):
             assert np.array_equal(dec[w, :k, :S[w]], ref_dec[w, :k, :S[w]]), (level, w)
     O.simd_set_level(-1)
+
+
+def _sw_case(O, seed, nsrc, k, W, dt, L, loss):
+    import np_oracle as N
+    rng = np.random.default_rng(seed)
+    stride = O.round_up(L, 16)
+    src = np.zeros((nsrc, stride), np.uint8)
+    src[:, :L] = rng.integers(0, 256, (nsrc, L), dtype=np.uint8)
+    h = N.sw_schedule(nsrc, k, W, key0=seed, dt=dt)
+    hdr = np.zeros(len(h), O.SW_REPAIR_DTYPE)
+    for t, (fss, nss, key, d) in enumerate(h):
+        hdr[t]["fss"], hdr[t]["nss"], hdr[t]["key"], hdr[t]["dt"] = fss, nss, key, d
+    sp = (rng.random(nsrc) >= loss).astype(np.uint8)
+    rp = (rng.random(len(h)) >= loss).astype(np.uint8)
+    return src, hdr, sp, rp
+
+
+@pytest.mark.parametrize("nsrc,k,W,dt,L,loss", [(3000, 8, 32, 15, 1200, 0.02), (3000, 8, 32, 15, 100, 0.10),
+                                                (2000, 4, 64, 15, 33, 0.15), (1500, 1, 255, 15, 40, 0.05),
+                                                (1200, 3, 20, 3, 17, 0.2)])
+def test_sw_simd_codec_matches_oracle(O, nsrc, k, W, dt, L, loss):
+    """The sliding-window CPU baseline (fec_cpu_simd.c orc_sw_*_simd: vectorised,
+    threads over repairs / runs of whole linked systems) equals the scalar oracle
+    (orc_sw_encode, and the banded decode equal to the dense one) at every SIMD
+    level and thread count, long linked systems included."""
+    src, hdr, sp, rp = _sw_case(O, nsrc + W, nsrc, k, W, dt, L, loss)
+    ref = O.sw_encode(src, hdr, L)
+    od = src.copy()
+    od[sp == 0] = 0xAB
+    ost, on = O.sw_decode_banded(od, sp, ref, rp, hdr, L)
+    for level in range(O.simd_detect() + 1):
+        O.simd_set_level(level)
+        for nth in (1, 5):
+            rep = O.sw_encode_simd(src, hdr, L, nth)
+            assert np.array_equal(rep[:, :L], ref[:, :L]), (level, nth)
+            d = src.copy()
+            d[sp == 0] = 0xAB
+            st, n = O.sw_decode_simd(d, sp, rep, rp, hdr, L, nth)
+            assert np.array_equal(st, ost) and n == on, (level, nth)
+            assert np.array_equal(d[:, :L], od[:, :L]), (level, nth)
+    O.simd_set_level(-1)
