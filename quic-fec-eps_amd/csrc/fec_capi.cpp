@@ -159,6 +159,7 @@ struct fecgpu_ctx {
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
     int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
+    int sw_stream = 1;  // sliding-window encode: 0 combine jobs, 1 / 2 streaming (dwords per lane)
     int sw_long_min = kSwSmallE + 1;  // sliding-window decode: unknowns that force the long-system path
     uint64_t sw_log_entries = 0;      // long-system operation log: fixed size (tuning), 0 = automatic
     uint64_t sw_log_seen = 0;         // the largest log an overflow asked for on this ctx
@@ -315,6 +316,11 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
     if (!std::strcmp(key, "sw_group")) {
         if (value != 1 && value != 2 && value != 4 && value != 8) return FECGPU_ERR_INVALID_ARG;
         ctx->sw_group = (int)value;  // calls and objects created from now on
+        return 0;
+    }
+    if (!std::strcmp(key, "sw_stream")) {
+        if (value < 0 || value > 2) return FECGPU_ERR_INVALID_ARG;
+        ctx->sw_stream = (int)value;  // calls and objects created from now on
         return 0;
     }
     if (!std::strcmp(key, "sw_long_min")) {
@@ -1043,6 +1049,8 @@ int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget) {
 }
 
 int ctx_sw_group(const fecgpu_ctx *ctx) { return ctx->sw_group; }
+
+int ctx_sw_stream(const fecgpu_ctx *ctx) { return ctx->sw_stream; }
 
 int ctx_sw_long_min(const fecgpu_ctx *ctx) { return ctx->sw_long_min; }
 

@@ -234,6 +234,41 @@ inline uint64_t sw_enc_jobs(uint64_t nrep, int group) {
     return group > 1 ? (nrep + group - 1) / group + nrep + 1 : nrep;
 }
 
+// Streaming encode (fec_swenc.hip): a workgroup takes a run of segments of
+// up to kSwSeg consecutive repairs and streams each segment's source range
+// once, every source multiplied into the accumulators of the repairs whose
+// windows hold it.  Accumulator slot m of pass p carries the repairs
+// p + m P, p + (m + A) P, ... of the segment in turn, which needs each window
+// to start at or after the end of the one A P repairs before it (P = 1 and
+// A = ceil(W / step) for a regular schedule; the workgroup picks the smallest
+// P, then A <= kSwSlots, that its segment's headers allow).
+constexpr int kSwSeg = 64;
+constexpr int kSwSlots = 8;
+constexpr int kSwStreamU = 8;  // sources per batch (a regular schedule's step divides it: whole batches)
+struct SwStreamArgs {
+    const uint8_t *src;
+    uint8_t *rep;
+    const fecgpu_sw_repair *hdr;
+    uint64_t nsrc, nrep;
+    uint32_t stride;
+    uint32_t ncu;       // column units (C dwords each) of a symbol
+    uint32_t cpass;     // column units per column pass (= block size)
+    int max_window;     // table rows per repair
+    int segcap;         // repairs per segment (<= kSwSeg)
+    uint64_t nseg;      // segments; workgroup b takes [b nseg / grid, (b + 1) nseg / grid)
+    uint32_t lds;       // dynamic LDS bytes
+};
+// C: dwords per lane (1 or 2); LDS budget per workgroup in bytes
+hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t s);
+// LDS per streaming-encode repair: kSwStreamU zero tables and max_window
+// tables (20 B each), coefficient bytes
+inline uint32_t sw_stream_rep_lds(int max_window) {
+    return (uint32_t)(max_window + kSwStreamU) * 20u + (uint32_t)max_window;
+}
+inline uint32_t sw_stream_lds(int segcap, int max_window) {
+    return ((uint32_t)segcap * sw_stream_rep_lds(max_window) + kSwStreamU * 20u + 64u + 15u) & ~15u;
+}
+
 // ---- sliding-window decode, planned on the device (fec_swdec.hip) ----
 // The lost sources are split into linked systems (two consecutive lost
 // sources are linked when a received repair's window holds both).  A system
@@ -324,9 +359,12 @@ ssize_t set_dev_error(hipError_t e, const char *what);
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *jobs,
                        void *coef, void *outs, hipStream_t s, int group = 1,
-                       const fecgpu_sw_repair *hdr_host = nullptr);
+                       const fecgpu_sw_repair *hdr_host = nullptr, int stream = 0);
 // the ctx's "sw_group" tuning (repairs per sliding-window encode job)
 int ctx_sw_group(const fecgpu_ctx *ctx);
+// the ctx's "sw_stream" tuning: 0 combine jobs, 1 / 2 the streaming encode
+// with 1 / 2 dwords per lane
+int ctx_sw_stream(const fecgpu_ctx *ctx);
 // "sw_long_min": systems of at least this many unknowns take the long-system
 // path even when the small one would fit (default kSwSmallE + 1)
 int ctx_sw_long_min(const fecgpu_ctx *ctx);

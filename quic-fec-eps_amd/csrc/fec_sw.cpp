@@ -51,6 +51,13 @@ constexpr int kSwSolveIn = 128;              // syndrome rows a small system's s
 // syndrome rows (device-sized); more room than the encode's budget keeps
 // several jobs per workgroup
 constexpr uint32_t kSolveBudget = 64u << 10;
+// LDS for one streaming-encode workgroup's multiply tables (segment of up to
+// kSwSeg repairs x max_window coefficients x 21 B): 43 KB for 64 repairs at W 32
+#ifndef FECGPU_STREAM_BUDGET_KB
+#define FECGPU_STREAM_BUDGET_KB 44
+#endif
+constexpr uint32_t kStreamBudget = FECGPU_STREAM_BUDGET_KB << 10;
+constexpr uint64_t kSwStreamSources = 1ull << 32;  // the streaming encode's source positions are 32-bit
 // sources and repairs per call: the device plan numbers them in 32 bits
 constexpr uint64_t kSwMaxSources = (1ull << 32) - 256;
 
@@ -129,7 +136,21 @@ bool sw_groups_fit(const fecgpu_sw_repair *h, uint64_t nrep, uint64_t nsrc, int 
 
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *pj, void *pc,
-                       void *po, hipStream_t s, int group, const fecgpu_sw_repair *hdr_host) {
+                       void *po, hipStream_t s, int group, const fecgpu_sw_repair *hdr_host, int stream) {
+    if (stream > 0 && nsrc < kSwStreamSources) {
+        SwStreamArgs sa{};
+        sa.src = src;
+        sa.rep = rep;
+        sa.hdr = hdr;
+        sa.nsrc = nsrc;
+        sa.nrep = nrep;
+        sa.stride = stride;
+        sa.max_window = max_window;
+        const int C = stream >= 2 ? 2 : 1;
+        sa.ncu = ((S + 15u) >> 4) * 4u / (uint32_t)C;
+        SW_TRY(launch_sw_stream(sa, C, kStreamBudget, s), "sliding-window streaming encode launch");
+        return 0;
+    }
     SwEncCoefArgs ca{};
     ca.hdr = hdr;
     ca.nrep = nrep;
@@ -164,7 +185,10 @@ ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_
                       const fecgpu_sw_repair *hdr, uint64_t nrep, int max_window, uint32_t S,
                       uint32_t stride, hipStream_t s, const fecgpu_sw_repair *hdr_host = nullptr) {
     void *pj = nullptr, *pc = nullptr, *po = nullptr;
-    const int group = ctx_sw_group(ctx);
+    const int group = ctx_sw_group(ctx), stream = ctx_sw_stream(ctx);
+    if (stream > 0 && nsrc < kSwStreamSources)
+        return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, nullptr, nullptr, nullptr, s,
+                              group, hdr_host, stream);
     RC_TRY(ctx_sw_scratch(ctx, 0, sw_enc_jobs(nrep, group) * sizeof(CombJob), &pj));
     RC_TRY(ctx_sw_scratch(ctx, 1, nrep * kSwCoefPitch, &pc));
     RC_TRY(ctx_sw_scratch(ctx, 2, nrep * sizeof(uint64_t), &po));

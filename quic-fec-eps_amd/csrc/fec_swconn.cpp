@@ -77,7 +77,8 @@ struct fecgpu_sw_encoder {
     uint64_t cap = 0, base = 0, next = 0;
     std::vector<fecgpu_sw_repair> sched;  // scheduled, not launched (absolute fss)
     uint32_t key = 0;
-    int group = 1;  // repairs per combine job (ctx "sw_group")
+    int group = 1;   // repairs per combine job (ctx "sw_group")
+    int stream = 0;  // streaming encode (ctx "sw_stream")
     struct Slot {
         fecgpu_sw_repair *hdr = nullptr;  // pinned, fss relative to the base at launch
         uint8_t *rep = nullptr;           // pinned rows
@@ -129,7 +130,7 @@ ssize_t enc_launch(fecgpu_sw_encoder *e) {
     ssize_t rc = ctx_fault_take(e->ctx)
                      ? (ssize_t)FECGPU_ERR_DEVICE
                      : sw_encode_core(e->src, e->cap, S.rep, S.hdr, n, e->p.window, e->p.symbol_size, e->stride,
-                                      S.jobs, S.coef, S.outs, e->s, e->group, S.hdr);
+                                      S.jobs, S.coef, S.outs, e->s, e->group, S.hdr, e->stream);
     if (rc >= 0) {
         const hipError_t er = hipEventRecord(S.ev, e->s);
         if (er != hipSuccess) rc = set_dev_error(er, "hipEventRecord");
@@ -216,6 +217,7 @@ ssize_t fecgpu_sw_encoder_new(fecgpu_ctx *ctx, const fecgpu_sw_params *p, fecgpu
     e->ctx = ctx;
     e->p = *p;
     e->group = ctx_sw_group(ctx);
+    e->stream = ctx_sw_stream(ctx);
     e->stride = (p->symbol_size + 15u) & ~15u;
     e->cap = 4ull * (p->window + (uint64_t)p->batch * p->step);
     rc = [&]() -> ssize_t {

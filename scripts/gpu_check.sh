@@ -49,6 +49,14 @@ for s in "$@"; do
                    python bench.py ;;  # the driver's default command, as is
         swtests) step swtests 300 python -u -m pytest tests/test_gpu_swconn.py tests/test_gpu_sw.py -q -x \
                      --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+        streamtests) step streamtests 300 python -u -m pytest tests/test_gpu_swstream.py -q -x \
+                     --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+        abstream7)  # cfg7: sliding-window encode modes, interleaved twice
+            for rep in 1 2; do
+                for m in 0 1 2; do
+                    step abstream7_m${m}_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify --sw-stream $m
+                done
+            done ;;
         prof5) prof prof5 5 ;;
         prof7) prof prof7 7 ;;
         abvar7)  # cfg7: default build vs every lib/libfecgpu_*.so variant (no check build), interleaved 3 times
@@ -83,6 +91,10 @@ for s in "$@"; do
         pmc4w) pmc pmc4w 4 WRITE_SIZE ;;
         pmc7r) pmc pmc7r 7 FETCH_SIZE ;;
         pmc7w) pmc pmc7w 7 WRITE_SIZE ;;
+        pmc7sq) pmc pmc7sq 7 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+                    SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_WAIT_INST_LDS ;;
+        pmc7sq2) pmc pmc7sq2 7 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT \
+                    SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_SMEM ;;
         sqa*) c=${s#sqa}; pmc sqa$c $c SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
         sqb*) c=${s#sqb}; pmc sqb$c $c SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE ;;
         micro) step micro 600 python scripts/microbench.py ;;

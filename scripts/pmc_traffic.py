@@ -18,11 +18,11 @@ import statistics
 
 def kind(name, config):
     """encode / decode / None for a kernel name (config 7, sliding window: the
-    encode is the grouped combine pass, comb_kernel<4>)."""
+    encode is sw_stream_kernel, or comb_kernel<4> with sw_stream 0)."""
     if "fecgpu" not in name:
         return None
-    if config == 7:
-        return "encode" if "comb_kernel<4>" in name else None
+    if config == 7:  # the streaming encode, or the combine-job one (sw_stream 0)
+        return "encode" if ("sw_stream_kernel" in name or "comb_kernel<4>" in name) else None
     return "encode" if "encode" in name else "decode" if "decode" in name else None
 
 

@@ -125,6 +125,7 @@ def test_sw_encode_grouped_jobs(group, host, L):
     with every group fitting: equal to the oracle."""
     c = fecgpu.Context()
     try:
+        c.set_tuning("sw_stream", 0)   # the combine-job encode
         c.set_tuning("sw_group", group)
         nsrc, W = 700, 32
         stride = O.round_up(L, 16)
