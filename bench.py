@@ -76,6 +76,10 @@ def parse():
                          "-1 the library default")
     ap.add_argument("--sw-group", type=int, default=0, choices=[0, 1, 2, 4, 8],
                     help="tuning (config 7): sliding-window repairs per combine job (0 = library default)")
+    ap.add_argument("--sw-loss", type=float, default=-1.0,
+                    help="config 7: i.i.d. loss rate of sources and repairs (-1 = the config's 2 %%)")
+    ap.add_argument("--sw-window", type=int, default=0,
+                    help="config 7: repair window in sources (0 = the config's 32)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1: nccl (= RCCL, one rank per GPU) or gloo (rehearsal: ranks may "
                          "share a GPU; the reductions run on the host)")
@@ -285,6 +289,11 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
     cfg = workloads.CONFIGS[cfgid]
     if args.matrix != "cauchy" and cfg.scheme not in ("xor", "sw"):
         cfg = dataclasses.replace(cfg, matrix=args.matrix, name=f"{cfg.name}-{args.matrix}")
+    if cfg.scheme == "sw" and (args.sw_loss >= 0 or args.sw_window > 0):
+        loss = args.sw_loss if args.sw_loss >= 0 else cfg.loss
+        win = args.sw_window or cfg.window
+        cfg = dataclasses.replace(cfg, loss=loss, window=win, name=f"{cfg.name}-W{win}-loss{loss:g}",
+                                  erasure_desc=f"i.i.d. p={loss:g} over sources and repairs")
     nwin = nwin_arg or cfg.nwin_per_gpu
     w0, nwin = shard.weak_shard(rank, world, nwin)  # this rank's global window range
     if cfg.scheme == "sw":  # config 7: one sliding-window stream per rank
@@ -374,7 +383,8 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
     dom_ms = enc_ms if dom == "encode" else dec_ms
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
     traffic, traffic_src = (pmc_traffic(cfgid, dom)
-                            if nwin == cfg.nwin_per_gpu and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
+                            if nwin == cfg.nwin_per_gpu and cfg.name == workloads.CONFIGS[cfgid].name
+                            and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
                             else (None, None))
     cpu = None
     if args.cpu_seconds > 0 and world == 1:

@@ -232,19 +232,26 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
         sws_window(pl, v[m], nn, f[m], e[m]);
     }
     const uint32_t hi = rfl(pl.phi[p]);
+    uint32_t s = rfl(pl.plo[p]);
+    if (s >= hi) return;  // an empty pass (hi >= 1 below)
     const uint8_t *base = a.src + rfl64(pl.lo) * stride;
+    // rows s0 .. s0 + U - 1, clamped to hi - 1 (valid rows only).  Every batch
+    // issues its loads unconditionally: with a load under a branch the
+    // compiler's wait counts merge to the stricter path, and the batch waited
+    // for the rows it had just prefetched (s_waitcnt vmcnt(7..0) in its body).
     auto load = [&](uint32_t s0, uint32_t (&x)[U][C]) __attribute__((always_inline)) {
+        s0 = rfl(min(s0, hi - 1));
 #if FECGPU_SWS_BUF
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t *>(base + (uint64_t)s0 * stride), 0, (int)(U * stride), kRsrcWord3);
+        const uint32_t last = rfl(hi - 1 - s0);  // scalar: rows past it reload row hi - 1
 #pragma unroll
-        for (int i = 0; i < U; i++) ldc_buf<C>(r, loff, (min(s0 + (uint32_t)i, hi - 1) - s0) * (uint32_t)stride, x[i]);
+        for (int i = 0; i < U; i++) ldc_buf<C>(r, loff, min((uint32_t)i, last) * (uint32_t)stride, x[i]);
 #else
 #pragma unroll
         for (int i = 0; i < U; i++) ldc<C>(base + (uint64_t)min(s0 + (uint32_t)i, hi - 1) * stride + loff, x[i]);
 #endif
     };
-    uint32_t s = rfl(pl.plo[p]);
     // one batch: multiply the rows in X, while the next batch's rows load into Y
     auto batch = [&](uint32_t (&X)[U][C], uint32_t (&Y)[U][C]) __attribute__((always_inline)) -> bool {
         if (s >= hi) return false;
@@ -253,7 +260,7 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
         for (int m = 1; m < A; m++) ev = min(ev, e[m]);
         const uint32_t L = min((uint32_t)U, min(ev, hi) - s);  // >= 1
         const uint32_t sn = s + L;
-        if (sn < hi) load(sn, Y);
+        load(sn, Y);  // past the end: a harmless reload of row hi - 1
         // slot m's entry for source s + i: tb[m] + i (its repair's zero run
         // before the window; repair 0's zero run while the window is ahead)
         const uint4 *tab[A];
@@ -314,14 +321,14 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
         for (int m = 1; m < A; m++) fmin = min(fmin, f[m]);
         if (fmin > sn) {  // no window open at sn: skip to the next one's start
             s = fmin;
-            if (s < hi) load(s, Y);
+            load(s, Y);
         } else {
             s = sn;
         }
         return true;
     };
     uint32_t XA[U][C], XB[U][C];
-    if (s < hi) load(s, XA);
+    load(s, XA);
 #if FECGPU_SWS_PINGPONG
     // two batches per trip, the row buffers trading roles (no copies); one
     // exit on a flag (a loop with two exits loses the bookkeeping's

@@ -57,6 +57,16 @@ for s in "$@"; do
                     step abstream7_m${m}_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify --sw-stream $m
                 done
             done ;;
+        absb7)  # cfg7 streaming encode: LDS budget variants (lib/libfecgpu_sb*.so) and C = 2, interleaved twice
+            for rep in 1 2; do
+                step absb7_base_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
+                step absb7_c2_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify --sw-stream 2
+                for v in quic-fec-eps_amd/lib/libfecgpu_sb*.so; do
+                    [ -e "$v" ] || continue
+                    n=$(basename $v .so); n=${n#libfecgpu_}
+                    FECGPU_LIB=$v step absb7_${n}_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
+                done
+            done ;;
         prof5) prof prof5 5 ;;
         prof7) prof prof7 7 ;;
         abvar7)  # cfg7: default build vs every lib/libfecgpu_*.so variant (no check build), interleaved 3 times

@@ -399,10 +399,13 @@ def test_sw_decode_host_pointers_and_args(ctx):
                       flags=fecgpu.F_HOST_PTRS)
 
 
-def test_sw_full_size_roundtrip(ctx):
+@pytest.mark.parametrize("loss", [0.02, 0.10])
+def test_sw_full_size_roundtrip(ctx, loss):
     """131,072 sources of 1200 B (157 MB), a repair after every 8 over the last 32, 2 %
-    i.i.d. loss of sources and repairs: every source the decoder reports recovered
-    equals the original, and every status equals the oracle's over the whole stream."""
+    (config 7's rate) or 10 % i.i.d. loss of sources and repairs: every source the
+    decoder reports recovered equals the original, and every status equals the
+    oracle's global decode over the whole stream (at 10 % the repairs, 1 per 8
+    sources, no longer cover the losses: long linked systems, mostly rank deficient)."""
     nsrc, L, stride, k, W = 131072, 1200, 1200, 8, 32
     g = torch.Generator(device="cuda").manual_seed(7)
     d_src = torch.randint(0, 256, (nsrc, stride), dtype=torch.uint8, device="cuda", generator=g)
@@ -413,8 +416,8 @@ def test_sw_full_size_roundtrip(ctx):
     ctx.sw_encode(d_src, d_rep, d_hdr, nsrc=nsrc, nrep=len(h), sym_len=L, stride=stride, max_window=W)
     orig = d_src.clone()
     rng = np.random.default_rng(1)
-    sp = (rng.random(nsrc) >= 0.02).astype(np.uint8)
-    rp = (rng.random(len(h)) >= 0.02).astype(np.uint8)
+    sp = (rng.random(nsrc) >= loss).astype(np.uint8)
+    rp = (rng.random(len(h)) >= loss).astype(np.uint8)
     lost = torch.from_numpy(sp == 0).cuda()
     d_src[lost] = 0xCD
     st = np.zeros(nsrc, np.uint8)
@@ -422,7 +425,7 @@ def test_sw_full_size_roundtrip(ctx):
     torch.cuda.synchronize()
     ok = torch.from_numpy(st == 0).cuda()
     assert torch.equal(d_src[ok], orig[ok])
-    assert n == int(((sp == 0) & (st == 0)).sum()) and n > 0.9 * (sp == 0).sum()
+    assert n == int(((sp == 0) & (st == 0)).sum()) and n > (0.9 if loss < 0.05 else 0.0) * (sp == 0).sum()
     # the whole stream against the banded oracle (equal to the dense one, test_sw_oracle.py)
     full = orig.cpu().numpy()
     od = full.copy()
