@@ -363,6 +363,23 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
         dec_ms = sum(b.elapsed_time(c) for _, b, c in ev.values()) / len(ev)
 
     log(f"{cfg.name}: timed {steps} steps: {elapsed:.4f} s (encode {enc_ms:.3f} ms, decode {dec_ms:.3f} ms)")
+    decode_only = None
+    if cfg.scheme == "sw" and steps > 0:
+        # the receiver alone (no encode launch to hide its plan under): `steps`
+        # back-to-back decode calls, wall clock and HIP events on the launch stream
+        torch.cuda.synchronize()
+        d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ta = time.perf_counter()
+        d0.record()
+        for _ in range(steps):
+            batch.decode(ctx)
+        d1.record()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - ta) * 1e3 / steps
+        decode_only = {"steps": steps, "ms_per_call": round(d0.elapsed_time(d1) / steps, 4),
+                       "wall_ms_per_call": round(wall, 4),
+                       "what": "fecgpu_sw_decode_device calls back to back, no encode in between"}
+        log(f"{cfg.name}: decode only {decode_only['ms_per_call']:.4f} ms per call")
     elapsed, tot = shard.reduce_run(elapsed, src_bytes, dev if args.dist_backend == "nccl" else None)
     total_src = float(tot) * steps
     value = total_src / elapsed / 1e9
@@ -449,6 +466,7 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
             for k2, ms in (("encode", enc_ms), ("decode", dec_ms))
         },
         "cpu_baseline": cpu,
+        **({"decode_only": decode_only} if decode_only else {}),
         "verify": verify,
         "digest": None if digest is None else f"{digest:016x}",
     }
@@ -495,7 +513,8 @@ def main():
             ok = ok and (sub["verify"] is None or sub["verify"].get("ok", False))
             extras[f"cfg{cid}"] = {k: sub[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup",
                                                        "config", "kernels_ms", "roofline", "roofline_other",
-                                                       "cpu_baseline", "verify", "digest")}
+                                                       "cpu_baseline", "verify", "digest", "decode_only")
+                                 if k in sub}
         line["configs"] = extras
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -438,7 +438,8 @@ typedef struct fecgpu_sw_params {
     uint8_t  reserved[3];
     uint32_t batch;       /* repairs per encode launch / per automatic decoder flush, >= 1 */
     uint32_t span;        /* receiver: sources kept behind the newest (0 = 16 x window +
-                             2 x batch x step); repairs whose window starts before it are dropped
+                             5 x batch x step: the sender's 4 launch slots plus the filling
+                             batch); repairs whose window starts before it are dropped
                              (add_repair returns FECGPU_ERR_DONE) */
 } fecgpu_sw_params;
 

@@ -175,6 +175,11 @@ struct CombJob {
     uint32_t nin, nout;
 };
 constexpr uint64_t kNoXor = ~0ull;
+// CombJob::nout flag: the xor row is multiplied by the coefficient byte after
+// the job's [nout][nin] block (output u: coef[nout * nin + u]) instead of
+// added as is (a sliding-window decode's one-unknown system: syndrome and
+// solve in one job, fec_swdec.hip small_solve)
+constexpr uint32_t kCombXorScaled = 1u << 31;
 constexpr int kSwMaxWindow = FECGPU_SW_MAX_WINDOW;
 constexpr uint32_t kSwCoefPitch = 256;  // coefficient bytes per repair job
 
@@ -204,7 +209,8 @@ struct CombArgs {
 // LDS bytes per job of comb_kernel<R> at nin_max inputs
 __host__ __device__ inline uint32_t comb_job_lds(int nin_max, int R) {
     const uint32_t rt = R == 1 ? 1u : (uint32_t)(R + 3) & ~3u;
-    return ((uint32_t)nin_max * (16u * R + 4u * rt + 1u) + 8u * R + 8u + 15u) & ~15u;
+    // nin_max input rows' tables plus one row for the xor row's multiplier
+    return ((uint32_t)(nin_max + 1) * (16u * R + 4u * rt + 1u) + 8u * R + 8u + 15u) & ~15u;
 }
 hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
 

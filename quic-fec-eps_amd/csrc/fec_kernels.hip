@@ -1994,14 +1994,19 @@ __global__ __launch_bounds__(kBlock) void digest_kernel(DigestArgs a) {
 template <int R>
 struct CombRegion {
     static constexpr int RT = R == 1 ? 1 : ((R + 3) & ~3);
-    uint4 *ab;
-    uint32_t *tc;
+    uint4 *ab;       // [nin_max + 1][R]: row nin_max = the xor row's multiplier (1 unless scaled)
+    uint32_t *tc;    // [nin_max + 1][RT]
+    uint4 *xab;
+    uint32_t *xtc;
     uint64_t *optr;  // [R] + xor pointer at optr[R]
     uint8_t *nz;
     __device__ __forceinline__ CombRegion(uint8_t *region, int nin_max) {
+        const size_t n = (size_t)nin_max + 1;
         ab = reinterpret_cast<uint4 *>(region);
-        tc = reinterpret_cast<uint32_t *>(region + (size_t)nin_max * R * 16);
-        optr = reinterpret_cast<uint64_t *>(region + (size_t)nin_max * (16 * R + 4 * RT));
+        tc = reinterpret_cast<uint32_t *>(region + n * R * 16);
+        xab = ab + (size_t)nin_max * R;
+        xtc = tc + (size_t)nin_max * RT;
+        optr = reinterpret_cast<uint64_t *>(region + n * (16 * R + 4 * RT));
         nz = reinterpret_cast<uint8_t *>(optr + R + 1);
     }
 };
@@ -2050,7 +2055,80 @@ __device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, in
         }
     }
     const uint64_t xp = rg.optr[R];
-    if (xp) acc[0] = xor4(acc[0], ld16(reinterpret_cast<const uint8_t *>(xp) + col * 16u));
+    if (xp) gmac(acc[0], split(ld16(reinterpret_cast<const uint8_t *>(xp) + col * 16u)), rg.xab[0], rg.xtc[0]);
+#pragma unroll
+    for (int m = 0; m < NE; m++)
+        if (m < ne) st16(reinterpret_cast<uint8_t *>(rg.optr[m]) + col * 16u, acc[m]);
+}
+
+#ifndef FECGPU_COMB_PF
+#define FECGPU_COMB_PF 1  // one-output combine jobs: next rows loaded while this batch multiplies
+#endif
+// comb_slot with the rows of batch i + 1 in flight while batch i multiplies
+// (two 8-row buffers) and the xor row loaded with the first batch.  A
+// workgroup streams its jobs' slots pass after pass, so without the prefetch
+// every batch is a dependent round trip to HBM (the syndrome pass of a
+// sliding-window decode: 3 per slot).  The trip count is the wave's largest
+// nin (its lanes may belong to two jobs), so the loop and every load are
+// wave-uniform: no load sits under a lane-dependent branch, where the
+// compiler's wait counts would merge to the stricter path.  Rows past a
+// lane's nin reload its last row and are not multiplied.
+template <int R, int NE>
+__device__ __forceinline__ void comb_slot_pf(const uint8_t *in, uint32_t stride, int nin, int ne, uint32_t col,
+                                             const CombRegion<R> &rg, bool skip) {
+    constexpr int U = 8, RT = CombRegion<R>::RT;
+    uint4 acc[NE];
+#pragma unroll
+    for (int m = 0; m < NE; m++) acc[m] = zero4();
+    int nw = nin;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) nw = max(nw, __shfl_xor(nw, o));
+    nw = __builtin_amdgcn_readfirstlane(nw);
+    const uint64_t xp = rg.optr[R];
+    // without an xor row: a load of row 0 (a valid address), discarded
+    const uint4 xv = ld16(xp ? reinterpret_cast<const uint8_t *>(xp) + col * 16u : in);
+    auto load = [&](uint4 (&v)[U], int q0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < U; t++) v[t] = ld16(in + (uint32_t)min(q0 + t, nin - 1) * stride);
+    };
+    auto mac = [&](const uint4 (&v)[U], int q0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < U; t++) {
+            const int q = q0 + t;
+            if (q < nin) {
+                uint32_t nzm = 0xffu;
+#if FECGPU_COMB_SKIP
+                if (R > 1 && skip) {
+                    const uint32_t z = rg.nz[q];
+                    const int last = 63 - __builtin_clzll(__builtin_amdgcn_read_exec());
+                    nzm = __builtin_amdgcn_readfirstlane(z) | __builtin_amdgcn_readlane(z, last);
+                }
+#endif
+                if (!nzm) continue;
+                const Split sp = split(v[t]);
+#pragma unroll
+                for (int m = 0; m < NE; m++)
+                    if ((nzm >> m) & 1u) gmac(acc[m], sp, rg.ab[q * R + m], rg.tc[q * RT + m]);
+            }
+        }
+    };
+    uint4 va[U], vb[U];
+    load(va, 0);
+    for (int q0 = 0;; q0 += 2 * U) {
+        if (q0 + U >= nw) {  // uniform
+            mac(va, q0);
+            break;
+        }
+        load(vb, q0 + U);
+        mac(va, q0);
+        if (q0 + 2 * U >= nw) {
+            mac(vb, q0 + U);
+            break;
+        }
+        load(va, q0 + 2 * U);
+        mac(vb, q0 + U);
+    }
+    if (xp) gmac(acc[0], split(xv), rg.xab[0], rg.xtc[0]);  // the xor row times its multiplier
 #pragma unroll
     for (int m = 0; m < NE; m++)
         if (m < ne) st16(reinterpret_cast<uint8_t *>(rg.optr[m]) + col * 16u, acc[m]);
@@ -2060,8 +2138,16 @@ template <int R, int NE = R>
 __device__ __forceinline__ void comb_dispatch(int nw, const uint8_t *in, uint32_t stride, int nin, int ne,
                                               uint32_t col, const CombRegion<R> &rg, bool skip) {
     if constexpr (NE >= 1) {
-        if (nw == NE) comb_slot<R, NE>(in, stride, nin, ne, col, rg, skip);
-        else comb_dispatch<R, NE - 1>(nw, in, stride, nin, ne, col, rg, skip);
+        if constexpr (FECGPU_COMB_PF && R == 1) {
+            if (nw == NE) {
+                comb_slot_pf<R, NE>(in, stride, nin, ne, col, rg, skip);
+                return;
+            }
+        } else if (nw == NE) {
+            comb_slot<R, NE>(in, stride, nin, ne, col, rg, skip);
+            return;
+        }
+        comb_dispatch<R, NE - 1>(nw, in, stride, nin, ne, col, rg, skip);
     }
 }
 
@@ -2127,7 +2213,7 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
         // plan: wave w builds the tables of jobs w, w + 4, ...
         for (int jl = wave; jl < nb; jl += kBlock / 64) {
             const CombJob J = a.jobs[j0 + jl];
-            const int nin = min((int)J.nin, nin_max), nout = min((int)J.nout, R);
+            const int nin = min((int)J.nin, nin_max), nout = min((int)(J.nout & ~kCombXorScaled), R);
             const CombRegion<R> rg(regions + (size_t)jl * job_lds, nin_max);
             const uint8_t *cf = a.coef + J.coef_off;
             for (int i = lane; i < nout * nin; i += 64) {
@@ -2141,7 +2227,12 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
                 for (int u = 0; u < nout; u++) m |= (cf[u * nin + q] != 0 ? 1u : 0u) << u;
                 rg.nz[q] = (uint8_t)m;
             }
-            if (lane < nout) rg.optr[lane] = reinterpret_cast<uint64_t>(a.out_base) + a.outs[J.out_list + lane];
+            if (lane < nout) {
+                rg.optr[lane] = reinterpret_cast<uint64_t>(a.out_base) + a.outs[J.out_list + lane];
+                const CoefTab ct = make_coef_tab((J.nout & kCombXorScaled) ? cf[nout * nin + lane] : 1u);
+                rg.xab[lane] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+                rg.xtc[lane] = ct.c;
+            }
             if (lane == 0) {
                 rg.optr[R] = J.xor_off == kNoXor ? 0ull : reinterpret_cast<uint64_t>(a.xor_base) + J.xor_off;
                 s_in[jl] = reinterpret_cast<uint64_t>(a.in_base) + J.in_off;

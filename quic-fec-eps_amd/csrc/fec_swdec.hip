@@ -341,6 +341,9 @@ __device__ __forceinline__ bool holds(const SwDecArgs &a, const fecgpu_sw_repair
 // 0: the ranges of two systems never interleave, since a repair between two
 // equations of one system that held a lost source of another would link them).
 constexpr int kSwTinyE = 16, kSwTinyP = 48;
+#ifndef FECGPU_SWD_FUSE1
+#define FECGPU_SWD_FUSE1 1  // one-unknown systems: syndrome and solve as one combine job
+#endif
 constexpr int kSwSolveIn = 128;  // widest syndrome range a small system's solve reads
 
 template <int ME, int MP>
@@ -460,6 +463,32 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         if (!need) a.syn_jobs[eq[q]].nout = 0;
     }
     if (ndet == 0) return 0;
+#if FECGPU_SWD_FUSE1
+    // One unknown (most systems at low loss): x = s_t / c for the pivot
+    // equation t, s_t = repair_t + sum of its received sources' terms.  Its
+    // syndrome job computes x directly: coefficients times 1/c, the repair row
+    // times 1/c (kCombXorScaled), output the lost source's row.  No syndrome
+    // row, no solve job.  Nothing else reads that row with a nonzero
+    // coefficient: a received repair holding it is an equation of this system.
+    if (e == 1) {
+        const int pr = S.piv[0];
+        const uint32_t t = eq[pr];
+        const uint32_t iv = M[pr * kPitch + e + pr];  // T[pr][pr] = 1 / c
+        const uint32_t nss = a.hdr[t].nss;
+        uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
+        uint32_t tab[5];
+        set_tab(tab, iv);
+        for (uint32_t j = lane; j < (nss + 3) / 4; j += 64) cc[j] = tmul(cc[j], tab);
+        SWD_WAVE_SYNC();
+        if (lane == 0) {
+            a.coef[(uint64_t)t * kSwCoefPitch + nss] = (uint8_t)iv;  // nss < kSwCoefPitch
+            a.syn_jobs[t].nout = 1u | kCombXorScaled;
+            a.syn_outs[t] = (uint64_t)(a.src + (uint64_t)U[0] * a.stride) - (uint64_t)a.synd;
+            a.stat[U[0]] = FECGPU_STATUS_OK;
+        }
+        return 1;
+    }
+#endif
     // solve jobs in the system's unknown slots x .. (ndet <= e), outputs at
     // x + d; inputs the syndrome rows t_first .. t_last, coefficients at 64
     // bytes per repair from t_first (ndet <= 64, so ndet * nin fits)
