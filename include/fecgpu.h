@@ -85,7 +85,8 @@ enum fecgpu_status { FECGPU_STATUS_OK = 0, FECGPU_STATUS_UNRECOVERABLE = 1 };
 #define FECGPU_F_HOST_PTRS 1u
 #define FECGPU_F_SYNC 2u
 
-#define FECGPU_MAX_K 64
+#define FECGPU_MAX_K 64       /* k + r of the per-connection objects, XOR and the workload helpers */
+#define FECGPU_MAX_WIDE_N 256 /* k + r of GF(2^8) codes through fecgpu_encode_batch / fecgpu_decode_batch */
 #define FECGPU_MAX_R 8
 #define FECGPU_MAX_SYMBOL (1u << 24) /* symbol length / pitch limit (QUIC packets are < 64 KiB) */
 
@@ -94,7 +95,8 @@ typedef struct fecgpu_code {
     uint32_t matrix;  /* enum fecgpu_matrix (GF256 only) */
     uint32_t framing; /* enum fecgpu_framing */
     uint16_t k;       /* source symbols per window, 1..64 */
-    uint16_t r;       /* repair symbols per window, 1..8, k + r <= 64, XOR: r <= k */
+    uint16_t r;       /* repair symbols per window, 1..8; k + r <= 64, or (GF(2^8), batch entry
+                         points only) <= 256; XOR: r <= k */
     uint32_t poly;    /* field polynomial, 0x11D (0 = default) */
     uint16_t rlc_key; /* MATRIX_RLC: repair_key of parity row 0 (row i: rlc_key + i mod 2^16) */
     uint8_t rlc_dt;   /* MATRIX_RLC: RFC 8681 density threshold DT, 0..15 (15 = dense:
@@ -170,7 +172,10 @@ ssize_t fecgpu_encode_split(fecgpu_ctx *ctx, const fecgpu_code *code, const uint
                             uint8_t *repair, const uint32_t *sym_len, uint32_t sym_len_all,
                             uint32_t stride, uint64_t nwin, uint32_t flags, void *stream);
 
-/* Recovery: present[w] bit i = symbol i received.
+/* Recovery: present[w] bit i = symbol i received; codes
+ * with k + r > 64 take ceil((k + r) / 64) words per window (bit i of window w
+ * in word present[w * words + i / 64], bit i % 64), device pointers and a
+ * uniform stride only, and their missing rows are read (times zero).
  * Missing sources are recovered in place; status[w] = FECGPU_STATUS_*.
  * Symbols whose bit is clear are never read.  XOR recovers every group with
  * exactly one missing source and its repair, even when others are lost.

@@ -174,6 +174,8 @@ struct fecgpu_ctx {
     std::map<int, hipEvent_t> sw_event;
     void *sw_host = nullptr;  // pinned staging of sliding-window decodes (ctx_sw_host)
     size_t sw_host_bytes = 0;
+    // codes with k + r > 64: parity rows on each device, by (device, k, r, matrix, key, dt)
+    std::map<std::tuple<int, int, int, int, int, int>, uint8_t *> wide_rows;
 };
 
 extern "C" {
@@ -202,7 +204,8 @@ ssize_t fecgpu_code_check(const fecgpu_code *code) {
     if (code->framing != FECGPU_FRAMING_FIXED && code->framing != FECGPU_FRAMING_LENPREFIX)
         return FECGPU_ERR_INVALID_ARG;
     if (code->k < 1 || code->r < 1) return FECGPU_ERR_INVALID_ARG;
-    if (code->k + code->r > FECGPU_MAX_K) return FECGPU_ERR_UNSUPPORTED;
+    if (code->k + code->r > (code->scheme == FECGPU_SCHEME_GF256 ? FECGPU_MAX_WIDE_N : FECGPU_MAX_K))
+        return FECGPU_ERR_UNSUPPORTED;
     if (code->r > FECGPU_MAX_R) return FECGPU_ERR_UNSUPPORTED;
     if (code->scheme == FECGPU_SCHEME_XOR && code->r > code->k) return FECGPU_ERR_INVALID_ARG;
     if (code->scheme == FECGPU_SCHEME_GF256 && code->matrix != FECGPU_MATRIX_CAUCHY &&
@@ -213,6 +216,19 @@ ssize_t fecgpu_code_check(const fecgpu_code *code) {
     if (code->poly != 0 && code->poly != 0x11D) return FECGPU_ERR_UNSUPPORTED;
     return 0;
 }
+
+}  // extern "C"
+
+namespace fecgpu {
+// Everything but the batch entry points takes codes of one 64-bit mask
+ssize_t code_check_narrow(const fecgpu_code *code) {
+    const ssize_t rc = fecgpu_code_check(code);
+    if (rc) return rc;
+    return code->k + code->r > FECGPU_MAX_K ? FECGPU_ERR_UNSUPPORTED : 0;
+}
+}  // namespace fecgpu
+
+extern "C" {
 
 ssize_t fecgpu_code_parity_rows(const fecgpu_code *code, uint8_t *out, size_t cap) {
     ssize_t rc = fecgpu_code_check(code);
@@ -369,6 +385,10 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
             if (b.first) (void)hipFree(b.first);
     }
     if (ctx->sw_host) (void)hipHostFree(ctx->sw_host);
+    for (auto &kv : ctx->wide_rows) {
+        (void)hipSetDevice(std::get<0>(kv.first));
+        (void)hipFree(kv.second);
+    }
     for (auto &kv : ctx->sw_event) {
         (void)hipSetDevice(kv.first);
         (void)hipEventDestroy(kv.second);
@@ -609,6 +629,52 @@ ssize_t run_host_multi(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, ui
     return (ssize_t)nwin;
 }
 
+// GF codes with k + r > 64 (fec_wide.hip): device pointers, uniform stride.
+// The parity rows go up once per code and device; the jobs, output lists and
+// decode matrices live in a ctx scratch slot shared with the sliding-window
+// calls (ordered by ctx_sw_begin / ctx_sw_end).
+ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win, const uint64_t *win_off,
+                 const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride, uint64_t nwin,
+                 const uint64_t *present, uint8_t *status, uint32_t flags, hipStream_t s) {
+    if (win_off || (flags & FECGPU_F_HOST_PTRS)) return FECGPU_ERR_UNSUPPORTED;
+    const int k = code->k, r = code->r, n = k + r;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    uint8_t *P = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        const auto key = std::make_tuple(dev, k, r, (int)code->matrix, (int)code->rlc_key, (int)code->rlc_dt);
+        auto it = ctx->wide_rows.find(key);
+        if (it == ctx->wide_rows.end()) {
+            std::vector<uint8_t> rows;
+            host_parity_rows(code, rows);
+            void *d = nullptr;
+            HIP_TRY(hipMalloc(&d, rows.size()), "hipMalloc wide parity rows");
+            HIP_TRY(hipMemcpy(d, rows.data(), rows.size(), hipMemcpyHostToDevice), "H2D wide parity rows");
+            it = ctx->wide_rows.emplace(key, static_cast<uint8_t *>(d)).first;
+        }
+        P = it->second;
+    }
+    const auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t o_out = up(nwin * sizeof(CombJob)), o_coef = o_out + up(nwin * kMaxR * sizeof(uint64_t));
+    const size_t total = o_coef + (decode ? nwin * kMaxR * (size_t)n : 0);
+    ssize_t rc = ctx_sw_begin(ctx, s);
+    if (rc) return rc;
+    void *scratch = nullptr;
+    rc = ctx_sw_scratch(ctx, 11, total, &scratch);
+    if (rc) return rc;
+    uint8_t *b = static_cast<uint8_t *>(scratch);
+    // per-window lengths: every window's columns up to the stride
+    const uint32_t ncol = sym_len ? stride / 16u : (sym_len_all + 15u) / 16u;
+    HIP_TRY(launch_wide(win, present, status, P, nwin, stride, ncol, k, r, decode, reinterpret_cast<CombJob *>(b),
+                        reinterpret_cast<uint64_t *>(b + o_out), b + o_coef, s),
+            "wide batch launch");
+    rc = ctx_sw_end(ctx, s);
+    if (rc) return rc;
+    if (flags & FECGPU_F_SYNC) HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+    return (ssize_t)nwin;
+}
+
 ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t *win,
                   const uint64_t *win_off, const uint32_t *sym_len, uint32_t sym_len_all,
                   uint32_t stride, uint64_t nwin, const uint64_t *present, uint8_t *status,
@@ -619,6 +685,9 @@ ssize_t run_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t
     if (decode && (!present || !status)) return FECGPU_ERR_INVALID_ARG;
     if (nwin == 0) return 0;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (code->k + code->r > FECGPU_MAX_K)
+        return run_wide(ctx, code, decode, win, win_off, sym_len, sym_len_all, stride, nwin, present, status, flags,
+                        s);
 
     // host pointers, uniform layout: chunked copy/compute pipeline on every device
     if ((flags & FECGPU_F_HOST_PTRS) && !win_off)
@@ -993,7 +1062,7 @@ namespace fecgpu {
 ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
                      hipStream_t s, bool remote, int dev) {
     if (!ctx || !a.win) return FECGPU_ERR_INVALID_ARG;
-    ssize_t rc = fecgpu_code_check(code);
+    ssize_t rc = code_check_narrow(code);
     if (rc) return rc;
     if (a.nwin == 0) return 0;
     // the object's own device: its stream, pinned windows and tables live there
@@ -1153,6 +1222,7 @@ ssize_t fecgpu_encode_split(fecgpu_ctx *ctx, const fecgpu_code *code, const uint
                             uint32_t stride, uint64_t nwin, uint32_t flags, void *stream) {
     if (!ctx || !repair) return FECGPU_ERR_INVALID_ARG;
     ssize_t rc = validate_batch(code, src, sym_len, sym_len_all, stride, nullptr);
+    if (!rc) rc = code_check_narrow(code);
     if (rc) return rc;
     if ((reinterpret_cast<uintptr_t>(repair) & 15) != 0) return FECGPU_ERR_INVALID_ARG;
     if (flags & FECGPU_F_HOST_PTRS) return FECGPU_ERR_UNSUPPORTED;  // device pointers only
@@ -1189,7 +1259,7 @@ ssize_t fecgpu_synth_batch(fecgpu_ctx *ctx, const fecgpu_code *code, int workloa
                            uint64_t w0, uint8_t *win, uint32_t *sym_len, uint32_t L,
                            uint32_t stride, uint64_t nwin, void *stream) {
     if (!ctx || !win) return FECGPU_ERR_INVALID_ARG;
-    ssize_t rc = fecgpu_code_check(code);
+    ssize_t rc = code_check_narrow(code);
     if (rc) return rc;
     if (workload != 0 && workload != 1) return FECGPU_ERR_INVALID_ARG;
     if (stride == 0 || (stride & 15)) return FECGPU_ERR_INVALID_ARG;
@@ -1205,7 +1275,7 @@ ssize_t fecgpu_synth_batch(fecgpu_ctx *ctx, const fecgpu_code *code, int workloa
 ssize_t fecgpu_erasure_batch(fecgpu_ctx *ctx, const fecgpu_code *code, int erasure, uint64_t seed,
                              uint64_t w0, uint64_t *present, uint64_t nwin, void *stream) {
     if (!ctx || !present) return FECGPU_ERR_INVALID_ARG;
-    ssize_t rc = fecgpu_code_check(code);
+    ssize_t rc = code_check_narrow(code);
     if (rc) return rc;
     if (erasure < 0 || erasure > 2) return FECGPU_ERR_INVALID_ARG;
     EraseArgs a{present, seed, w0, nwin, code->k, code->r, (int)code->scheme, erasure};
@@ -1218,7 +1288,7 @@ ssize_t fecgpu_digest_batch(fecgpu_ctx *ctx, const fecgpu_code *code, const uint
                             const uint32_t *sym_len, uint32_t sym_len_all, uint32_t stride,
                             uint64_t w0, uint64_t nwin, uint64_t *digest, void *stream) {
     if (!ctx || !win || !digest) return FECGPU_ERR_INVALID_ARG;
-    ssize_t rc = fecgpu_code_check(code);
+    ssize_t rc = code_check_narrow(code);
     if (rc) return rc;
     if (stride == 0 || (stride & 15)) return FECGPU_ERR_INVALID_ARG;
     if (!sym_len && (sym_len_all == 0 || sym_len_all > stride)) return FECGPU_ERR_INVALID_ARG;

@@ -244,7 +244,7 @@ extern "C" {
 ssize_t fecgpu_encoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t max_len,
                            uint32_t batch, fecgpu_encoder **out) {
     if (!ctx || !out || max_len == 0 || batch == 0) return FECGPU_ERR_INVALID_ARG;
-    ssize_t rc = fecgpu_code_check(code);
+    ssize_t rc = fecgpu::code_check_narrow(code);
     if (rc) return rc;
     if (is_lenprefix(*code) && max_len > 65535) return FECGPU_ERR_INVALID_ARG;
     auto *e = new fecgpu_encoder();
@@ -588,7 +588,7 @@ extern "C" {
 ssize_t fecgpu_decoder_new(fecgpu_ctx *ctx, const fecgpu_code *code, uint32_t max_len,
                            uint32_t batch, fecgpu_decoder **out) {
     if (!ctx || !out || max_len == 0 || batch == 0) return FECGPU_ERR_INVALID_ARG;
-    ssize_t rc = fecgpu_code_check(code);
+    ssize_t rc = fecgpu::code_check_narrow(code);
     if (rc) return rc;
     if (is_lenprefix(*code) && max_len > 65535) return FECGPU_ERR_INVALID_ARG;
     auto *d = new fecgpu_decoder();

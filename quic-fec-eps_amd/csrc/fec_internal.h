@@ -213,6 +213,11 @@ __host__ __device__ inline uint32_t comb_job_lds(int nin_max, int R) {
     return ((uint32_t)(nin_max + 1) * (16u * R + 4u * rt + 1u) + 8u * R + 8u + 15u) & ~15u;
 }
 hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
+// GF block codes with k + r > 64 (fec_wide.hip): a plan / job kernel, then the
+// combine kernel over a job per window
+hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
+                       uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
+                       uint64_t *outs, uint8_t *coef, hipStream_t s);
 
 // encode: job t = repair t (coefficients at coef + t * kSwCoefPitch, output rep row t).
 // group > 1: the repairs t0 = g * group .. t0 + group - 1 share job g when
@@ -382,6 +387,7 @@ void ctx_sw_log_grow(fecgpu_ctx *ctx, uint64_t entries);
 // count lasts, consuming one
 bool ctx_fault_take(fecgpu_ctx *ctx);
 int choose_wpb_for(uint32_t ncol, uint32_t lds_per_unit, uint32_t lds_budget);
+ssize_t code_check_narrow(const fecgpu_code *code);  // fecgpu_code_check and k + r <= 64
 ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p);
 // the ctx's pinned host staging block for sliding-window decodes (grown on
 // demand; a decode synchronizes before returning, so the next may reuse it)

@@ -1,0 +1,223 @@
+// fec_wide.hip — GF(2^8) block codes wider than one 64-bit mask: k + r up to
+// 256 (the Cauchy construction's limit), r <= 8,
+// through fecgpu_encode_batch / fecgpu_decode_batch (include/fecgpu.h: present
+// masks of ceil((k + r) / 64) words per window).
+//
+// The windows run through the sliding-window path's combine kernel
+// (fec_kernels.hip comb_kernel<8>): a job per window, its input rows one
+// contiguous range of the window, up to 8 outputs, a coefficient block
+// [nout][nin].
+//  * encode: inputs the k sources, outputs the r repairs, coefficients the
+//    code's parity rows P[r][k] (one block shared by every job);
+//  * decode: a wave per window plans it (wide_dec_plan_kernel): the missing
+//    sources m_u (e <= r), the system A[t][u] = P[sel_t][m_u] of every present
+//    repair reduced by Gauss-Jordan with pivot search (so an RLC window is
+//    recovered whenever its present repairs have rank e), and the decode
+//    matrix D[u][q] over all k + r rows of the window: received sources
+//    sum_c T[P_u][P_c] P[sel_c][q], the pivot repairs T[P_u][P_c], zero for
+//    missing sources and unused repairs (their rows are read and multiplied
+//    by zero).  The job writes x_u to the missing rows in place.
+#include "fec_internal.h"
+
+namespace fecgpu {
+
+namespace {
+
+__constant__ GfTables c_gfw = make_gf_tables();
+
+#define WIDE_WAVE_SYNC()                                        \
+    do {                                                        \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); \
+        __builtin_amdgcn_wave_barrier();                        \
+    } while (0)
+
+struct WideArgs {
+    uint8_t *win;
+    const uint64_t *present;  // [nwin][nw]
+    uint8_t *status;
+    const uint8_t *P;         // parity rows [r][k] on the device
+    uint64_t nwin, wpitch;
+    uint32_t stride;
+    int k, r, nw;
+    CombJob *jobs;   // [nwin]
+    uint64_t *outs;  // [nwin][8] (encode: [nwin][r])
+    uint8_t *coef;   // decode: [nwin][8][k + r]
+};
+
+__global__ __launch_bounds__(kBlock) void wide_enc_jobs_kernel(WideArgs a) {
+    const uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (w >= a.nwin) return;
+    CombJob J;
+    J.in_off = w * a.wpitch;
+    J.coef_off = 0;
+    J.out_list = w * (uint64_t)a.r;
+    J.xor_off = kNoXor;
+    J.nin = (uint32_t)a.k;
+    J.nout = (uint32_t)a.r;
+    a.jobs[w] = J;
+    for (int i = 0; i < a.r; i++) a.outs[w * a.r + i] = w * a.wpitch + (uint64_t)(a.k + i) * a.stride;
+}
+
+__device__ __forceinline__ uint32_t wmul(const uint8_t *ex, const uint8_t *lg, uint32_t x, uint32_t y) {
+    return (x && y) ? ex[lg[x] + lg[y]] : 0u;
+}
+
+// A wave per window: plan, job, status.
+__global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
+    __shared__ uint8_t s_exp[512], s_log[256];
+    __shared__ uint8_t s_m[kBlock / 64][kMaxR];  // missing sources, ascending
+    for (int i = threadIdx.x; i < 512; i += kBlock) s_exp[i] = c_gfw.exp[i];
+    for (int i = threadIdx.x; i < 256; i += kBlock) s_log[i] = c_gfw.log[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+    if (w >= a.nwin) return;  // whole waves: no barrier below
+    const int k = a.k, r = a.r, n = k + r;
+    const uint64_t *pw = a.present + w * (uint64_t)a.nw;
+    CombJob J{};
+    J.xor_off = kNoXor;
+    // missing sources (the first kMaxR kept) and their count
+    int e = 0;
+    for (int c0 = 0; c0 < k; c0 += 64) {
+        const int i = c0 + lane;
+        const bool miss = i < k && !((pw[i >> 6] >> (i & 63)) & 1ull);
+        const uint64_t b = __ballot(miss);
+        const int pos = e + __popcll(b & ((1ull << lane) - 1ull));
+        if (miss && pos < kMaxR) s_m[wave][pos] = (uint8_t)i;
+        e += __popcll(b);
+    }
+    const bool rp = lane < r && ((pw[(k + lane) >> 6] >> ((k + lane) & 63)) & 1ull);
+    const uint32_t rep = (uint32_t)__ballot(rp);  // present repairs (bit i: repair i)
+    const int np = __popcll(rep);
+    WIDE_WAVE_SYNC();
+    if (e == 0 || e > r || np < e) {
+        if (lane == 0) {
+            a.status[w] = e == 0 ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
+            a.jobs[w] = J;
+        }
+        return;
+    }
+    // [A | I], lane = t * 8 + u: row t = the t-th present repair, column u
+    const int t = lane >> 3, u = lane & 7;
+    int sel_t = 0;
+    {
+        uint32_t rr = rep;
+        for (int i = 0; i < t && rr; i++) rr &= rr - 1;
+        sel_t = rr ? __ffs(rr) - 1 : 0;
+    }
+    const bool row = t < np;
+    const int m_u = u < e ? (int)s_m[wave][u] : 0;
+    uint32_t xl = (row && u < e) ? a.P[(size_t)sel_t * k + m_u] : 0u;
+    uint32_t xr = (row && t == u) ? 1u : 0u;
+    uint32_t used = 0;  // rows already pivots (wave-uniform)
+    int my_piv = 0;     // lane c < e: pivot row of column c
+    for (int c = 0; c < e; c++) {
+        const uint64_t cand = __ballot(row && u == c && !((used >> t) & 1u) && xl != 0);
+        if (!cand) {  // rank < e: the window stays lost
+            if (lane == 0) {
+                a.status[w] = FECGPU_STATUS_UNRECOVERABLE;
+                a.jobs[w] = J;
+            }
+            return;
+        }
+        const int pr = (int)(__ffsll((unsigned long long)cand) - 1) >> 3;
+        used |= 1u << pr;
+        if (lane == c) my_piv = pr;
+        const uint32_t pv = __shfl(xl, pr * 8 + c, 64);
+        const uint32_t ip = s_exp[255 - s_log[pv]];
+        if (t == pr) {
+            xl = wmul(s_exp, s_log, xl, ip);
+            xr = wmul(s_exp, s_log, xr, ip);
+        }
+        const uint32_t f = __shfl(xl, t * 8 + c, 64);
+        const uint32_t rl = __shfl(xl, pr * 8 + u, 64);
+        const uint32_t rq = __shfl(xr, pr * 8 + u, 64);
+        if (t != pr && row) {
+            xl ^= wmul(s_exp, s_log, f, rl);
+            xr ^= wmul(s_exp, s_log, f, rq);
+        }
+    }
+    // D[u][q] over the window's n rows, entry idx = u * n + q; T[P_u][P_c] =
+    // xr of lane P_u * 8 + P_c, the repair of pivot row P_c = sel of row P_c
+    uint8_t *D = a.coef + w * (uint64_t)(kMaxR * n);
+    for (int base = 0; base < e * n; base += 64) {
+        const int idx = base + lane;
+        const int du = min(idx / n, e - 1), q = idx - du * n;
+        const int pu = __shfl(my_piv, du, 64);
+        uint32_t d = 0;
+        bool miss = false;
+        if (q < k) miss = !((pw[q >> 6] >> (q & 63)) & 1ull);
+        for (int c = 0; c < e; c++) {
+            const int pc = __shfl(my_piv, c, 64);
+            const uint32_t tv = __shfl(xr, (pu * 8 + pc) & 63, 64);
+            uint32_t rr = rep;
+            for (int i = 0; i < pc && rr; i++) rr &= rr - 1;
+            const int sc = __ffs(rr) - 1;  // repair of pivot row pc
+            if (q < k) {
+                if (!miss) d ^= wmul(s_exp, s_log, tv, a.P[(size_t)sc * k + q]);
+            } else if (q - k == sc) {
+                d = tv;
+            }
+        }
+        if (idx < e * n) D[idx] = (uint8_t)d;
+    }
+    if (lane < e) a.outs[w * kMaxR + lane] = w * a.wpitch + (uint64_t)s_m[wave][lane] * a.stride;
+    if (lane == 0) {
+        J.in_off = w * a.wpitch;
+        J.coef_off = w * (uint64_t)(kMaxR * n);
+        J.out_list = w * kMaxR;
+        J.nin = (uint32_t)n;
+        J.nout = (uint32_t)e;
+        a.jobs[w] = J;
+        a.status[w] = FECGPU_STATUS_OK;
+    }
+}
+
+}  // namespace
+
+// Wide batch (k + r > 64): device pointers, uniform stride; scratch from the
+// caller (jobs, outs, coef, P already on the device).  The caller orders the
+// call against others that share the scratch.
+hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
+                       uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
+                       uint64_t *outs, uint8_t *coef, hipStream_t s) {
+    WideArgs a{};
+    a.win = win;
+    a.present = present;
+    a.status = status;
+    a.P = P_dev;
+    a.nwin = nwin;
+    a.stride = stride;
+    a.wpitch = (uint64_t)(k + r) * stride;
+    a.k = k;
+    a.r = r;
+    a.nw = (k + r + 63) / 64;
+    a.jobs = jobs;
+    a.outs = outs;
+    a.coef = coef;
+    if (decode)
+        hipLaunchKernelGGL(wide_dec_plan_kernel, dim3((unsigned)((nwin + kBlock / 64 - 1) / (kBlock / 64))),
+                           dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(wide_enc_jobs_kernel, dim3((unsigned)((nwin + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    CombArgs c{};
+    c.jobs = jobs;
+    c.coef = decode ? coef : P_dev;
+    c.outs = outs;
+    c.in_base = win;
+    c.out_base = win;
+    c.xor_base = nullptr;
+    c.njobs = nwin;
+    c.ncol = ncol;
+    c.stride = stride;
+    c.nin_max = decode ? k + r : k;
+    c.nout_max = kMaxR;
+    c.job_lds = comb_job_lds(c.nin_max, kMaxR);
+    c.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c.job_lds, 64u << 10)));
+    return launch_comb(c, kMaxR, s);
+}
+
+}  // namespace fecgpu

@@ -67,6 +67,21 @@ for s in "$@"; do
                     FECGPU_LIB=$v step absb7_${n}_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
                 done
             done ;;
+        abdec)  # GF decode variants: e = r = 8 sweep rows, cfg3, cfg4 (lib/libfecgpu_*.so), interleaved twice
+            libs=quic-fec-eps_amd/lib/libfecgpu.so
+            for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
+                [ "$(basename $v)" = libfecgpu_check.so ] || libs=$libs,$v
+            done
+            step abdec_c3 300 python scripts/ab.py --config 3 --libs $libs
+            step abdec_c4 300 python scripts/ab.py --config 4 --libs $libs
+            for rep in 1 2; do
+                step abdec_sweep_base_$rep 300 python scripts/code_sweep.py r8
+                for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
+                    n=$(basename $v .so); n=${n#libfecgpu_}
+                    [ "$n" = check ] && continue
+                    FECGPU_LIB=$v step abdec_sweep_${n}_$rep 300 python scripts/code_sweep.py r8
+                done
+            done ;;
         prof5) prof prof5 5 ;;
         prof7) prof prof7 7 ;;
         abvar7)  # cfg7: default build vs every lib/libfecgpu_*.so variant (no check build), interleaved 3 times

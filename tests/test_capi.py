@@ -63,7 +63,10 @@ def test_header_compiles_as_c():
     (1, 16, 4, 0, 0, 0, 0),
     (1, 32, 8, 1, 0, 0x11D, 0),
     (1, 56, 8, 0, 0, 0, 0),
-    (1, 57, 8, 0, 0, 0, fecgpu.ERR_UNSUPPORTED),   # k + r > 64
+    (1, 57, 8, 0, 0, 0, 0),                        # k + r > 64: GF batch entry points (fec_wide.hip)
+    (1, 248, 8, 0, 0, 0, 0),                       # k + r = 256: the Cauchy limit
+    (1, 249, 8, 0, 0, 0, fecgpu.ERR_UNSUPPORTED),  # k + r > 256
+    (0, 60, 8, 0, 0, 0, fecgpu.ERR_UNSUPPORTED),   # XOR: k + r <= 64
     (1, 8, 9, 0, 0, 0, fecgpu.ERR_UNSUPPORTED),    # r > 8
     (0, 2, 3, 0, 0, 0, fecgpu.ERR_INVALID_ARG),    # XOR r > k
     (1, 0, 1, 0, 0, 0, fecgpu.ERR_INVALID_ARG),
