@@ -41,6 +41,9 @@
 #endif
 #define FECGPU_GF_U (R <= 4 ? 2 : FECGPU_GF_U_HI)
 #endif
+#ifndef FECGPU_PLAN_TP
+#define FECGPU_PLAN_TP 1  // GF decode plans: table entries written along the output index first
+#endif
 #ifndef FECGPU_GFD_U
 // GF decode: input rows loaded per batch.  8 at every r: decode's input rows
 // come through an LDS index (received sources, chosen repairs), so a deeper
@@ -1469,7 +1472,13 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, uint64_t pres, int lane,
     // D[u][q] for idx = u*k + q; every __shfl with the whole wave active
     for (int base = 0; base < e * k; base += 64) {
         const int idx = base + lane;
+#if FECGPU_PLAN_TP
+        // idx = dq * e + du: consecutive lanes write consecutive table entries
+        // (lanes along dq put 4 lanes of every 8 on the same LDS banks)
+        const int dq = idx / e, du = idx - dq * e;
+#else
         const int du = idx / k, dq = idx - du * k;
+#endif
         const int Au = __shfl(A, du & 63, 64);
         const int Kq = __shfl(K, dq & 63, 64);
         const int z = __shfl(zq, dq & 63, 64);
@@ -1561,7 +1570,13 @@ __device__ void plan_gf_gj(const BatchArgs &a, uint64_t w, int lane, uint8_t *re
     const int kr = k - e;
     for (int base = 0; base < e * k; base += 64) {
         const int idx = base + lane;
+#if FECGPU_PLAN_TP
+        // idx = dq * e + du: consecutive lanes write consecutive table entries
+        // (lanes along dq put 4 lanes of every 8 on the same LDS banks)
+        const int dq = idx / e, du = idx - dq * e;
+#else
         const int du = idx / k, dq = idx - du * k;
+#endif
         const bool live = idx < e * k;
         const bool is_src = dq < kr;
         const uint32_t j = (live && is_src) ? insym[dq] : 0u;
@@ -1661,7 +1676,13 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
     // D[u][q] for idx = u*k + q; Ainv'[u][c] = T[P_u][P_c] = xr of lane P_u*8 + P_c
     for (int base = 0; base < e * k; base += 64) {
         const int idx = base + lane;
+#if FECGPU_PLAN_TP
+        // idx = dq * e + du: consecutive lanes write consecutive table entries
+        // (lanes along dq put 4 lanes of every 8 on the same LDS banks)
+        const int dq = idx / e, du = idx - dq * e;
+#else
         const int du = idx / k, dq = idx - du * k;
+#endif
         const bool live = idx < e * k;
         const bool is_src = dq < kr;
         const uint32_t j = (live && is_src) ? insym[dq] : 0u;
@@ -1691,10 +1712,12 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
 
 // GF decode of one slot for NE outputs (wave-uniform): acc[u] = sum_q D[u][q]
 // * in_q over the k inputs, U rows loaded per batch; output u is stored when
-// u < ne (this lane's window).
-template <int R, int NE>
+// u < ne (this lane's window).  OFF: the first output (the outputs OFF ..
+// OFF + NE - 1 of the window's plan; a multiple of 4).
+template <int R, int NE, int OFF = 0>
 __device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t out_delta,
                                          const DecRegion<R> &rg) {
+    static_assert(OFF % 4 == 0 && OFF + NE <= R, "output range");
     constexpr int U = FECGPU_GFD_U, R4 = DecRegion<R>::R4;
     static_assert(U == 2 || U == 4 || U == 8, "row offsets are padded to 8 rows");
     uint4 acc[NE];
@@ -1725,14 +1748,14 @@ __device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t 
                 uint32_t c0[R4], c1[R4];
 #pragma unroll
                 for (int j = 0; j < (NE + 3) / 4; j++) {
-                    const uint4 x = *reinterpret_cast<const uint4 *>(rg.tc + q * R4 + 4 * j);
-                    const uint4 y = *reinterpret_cast<const uint4 *>(rg.tc + (q + 1) * R4 + 4 * j);
+                    const uint4 x = *reinterpret_cast<const uint4 *>(rg.tc + q * R4 + OFF + 4 * j);
+                    const uint4 y = *reinterpret_cast<const uint4 *>(rg.tc + (q + 1) * R4 + OFF + 4 * j);
                     c0[4 * j] = x.x; c0[4 * j + 1] = x.y; c0[4 * j + 2] = x.z; c0[4 * j + 3] = x.w;
                     c1[4 * j] = y.x; c1[4 * j + 1] = y.y; c1[4 * j + 2] = y.z; c1[4 * j + 3] = y.w;
                 }
 #pragma unroll
                 for (int m = 0; m < NE; m++)
-                    gmac2(acc[m], s0, s1, rg.ab[q * R + m], c0[m], rg.ab[(q + 1) * R + m], c1[m]);
+                    gmac2(acc[m], s0, s1, rg.ab[q * R + OFF + m], c0[m], rg.ab[(q + 1) * R + OFF + m], c1[m]);
                 t0 = t + 2;
             }
         }
@@ -1745,23 +1768,39 @@ __device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t 
                 uint32_t c[R4];
 #pragma unroll
                 for (int j = 0; j < (NE + 3) / 4; j++) {
-                    const uint4 x = *reinterpret_cast<const uint4 *>(rg.tc + q * R4 + 4 * j);
+                    const uint4 x = *reinterpret_cast<const uint4 *>(rg.tc + q * R4 + OFF + 4 * j);
                     c[4 * j] = x.x; c[4 * j + 1] = x.y; c[4 * j + 2] = x.z; c[4 * j + 3] = x.w;
                 }
 #pragma unroll
-                for (int m = 0; m < NE; m++) gmac(acc[m], sp, rg.ab[q * R + m], c[m]);
+                for (int m = 0; m < NE; m++) gmac(acc[m], sp, rg.ab[q * R + OFF + m], c[m]);
             }
         }
     }
 #pragma unroll
     for (int m = 0; m < NE; m++)
-        if (m < ne) st16(base + out_delta + rg.ooff[m], acc[m]);
+        if (OFF + m < ne) st16(base + out_delta + rg.ooff[OFF + m], acc[m]);
 }
+
+#ifndef FECGPU_GFD_SPLIT
+// GF decode of more than 4 outputs per wave: two passes over the inputs (outputs
+// 0-3, then the rest; the second reads the rows from L2), so the kernel keeps
+// the 4-output register footprint (R = 8: 155 -> 122 VGPRs, 3 -> 4 waves/SIMD).
+// Off: in-process A/B (profiles/r03_gf_decode_ab.txt) the second pass costs
+// more than the extra wave gains (cfg4 decode 4.68 vs 4.56 ms, e = 8 rows -7 %)
+#define FECGPU_GFD_SPLIT 0
+#endif
 
 template <int R, int NE = R>
 __device__ __forceinline__ void dec_dispatch(int nw, uint8_t *base, int k, int ne, uint64_t out_delta,
                                              const DecRegion<R> &rg) {
     if constexpr (NE >= 1) {
+        if constexpr (FECGPU_GFD_SPLIT && NE > 4) {
+            if (nw == NE) {
+                dec_slot<R, 4, 0>(base, k, ne, out_delta, rg);
+                dec_slot<R, NE - 4, 4>(base, k, ne, out_delta, rg);
+                return;
+            }
+        }
         if (nw == NE) dec_slot<R, NE>(base, k, ne, out_delta, rg);
         else dec_dispatch<R, NE - 1>(nw, base, k, ne, out_delta, rg);
     }
