@@ -341,6 +341,9 @@ __device__ __forceinline__ bool holds(const SwDecArgs &a, const fecgpu_sw_repair
 // 0: the ranges of two systems never interleave, since a repair between two
 // equations of one system that held a lost source of another would link them).
 constexpr int kSwTinyE = 16, kSwTinyP = 48;
+#ifndef FECGPU_SWD_COEF
+#define FECGPU_SWD_COEF 1  // coefficients of the repairs holding lost sources drawn by a thread each, up front
+#endif
 #ifndef FECGPU_SWD_FUSE1
 #define FECGPU_SWD_FUSE1 1  // one-unknown systems: syndrome and solve as one combine job
 #endif
@@ -373,6 +376,18 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     for (int q = lane; q < p; q += 64) {
         const uint32_t t = eq[q];
         const fecgpu_sw_repair h = a.hdr[t];
+#if FECGPU_SWD_COEF
+        // the row was drawn by sw_dec_coef_kernel: move the unknowns' entries
+        // into A (the unknowns are ascending; the window holds a run of them)
+        uint8_t *cb = a.coef + (uint64_t)t * kSwCoefPitch;
+        for (int u = 0; u < e; u++) {
+            const uint64_t i = U[u];
+            if (i < h.fss) continue;
+            if (i >= h.fss + h.nss) break;
+            M[q * kPitch + u] = cb[i - h.fss];
+            cb[i - h.fss] = 0;
+        }
+#else
         uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
         Tinymt32 st;
         tinymt32_init(st, h.key);
@@ -399,6 +414,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
             }
         }
         if (h.nss & 3) cc[h.nss >> 2] = word;
+#endif
         CombJob J;
         J.in_off = h.fss * a.stride;
         J.coef_off = (uint64_t)t * kSwCoefPitch;
@@ -590,6 +606,38 @@ __device__ __forceinline__ void block_counts(const SwDecArgs &a, uint32_t rec, u
         if (r) atomicAdd(&a.ctr->recovered, r);
         if (m) atomicMax(&a.ctr->maxin, m);
     }
+}
+
+// Thread per repair: the RFC 8681 coefficients of every received repair whose
+// window holds a lost source, into its syndrome coefficient row.  The system
+// passes then read them (small_solve moves the unknowns' entries into A and
+// zeroes them); drawn here, every lane of a wave draws one, instead of a
+// wave per system drawing its few equations' on as many lanes.  The
+// long-system pass draws its own rows again (and overwrites these).
+__global__ __launch_bounds__(kBlock) void sw_dec_coef_kernel(SwDecArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= a.nrep || (a.ctr->err & 1u) || !a.rep_present[t]) return;
+    const fecgpu_sw_repair h = a.hdr[t];
+    if (!holds_any(a, h)) return;
+    uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + t * kSwCoefPitch);
+    Tinymt32 st;
+    tinymt32_init(st, h.key);
+    const uint32_t dt = h.dt;
+    uint32_t word = 0;
+    for (int j = 0; j < (int)h.nss; j++) {
+        uint32_t c = 0;
+        if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
+            do {
+                c = tinymt32_u32(st) & 0xFFu;
+            } while (c == 0);
+        }
+        word |= c << (8 * (j & 3));
+        if ((j & 3) == 3) {
+            cc[j >> 2] = word;
+            word = 0;
+        }
+    }
+    if (h.nss & 3) cc[h.nss >> 2] = word;
 }
 
 // A wave per lost source; the waves at a system start find its extent and
@@ -1102,6 +1150,9 @@ hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(sw_dec_scan_kernel, dim3(1), dim3(1024), 0, s, a.chunk, a.nchunk, 3, 1, &a.ctr->nlost);
     hipLaunchKernelGGL(sw_dec_lost_kernel, dim3(a.nchunk), dim3(kBlock), 0, s, a);
     if (a.nrep) {
+#if FECGPU_SWD_COEF
+        hipLaunchKernelGGL(sw_dec_coef_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+#endif
         // a wave per lost source at most; persistent beyond what fits the chip
         const uint64_t want = (a.nsrc + kBlock / 64 - 1) / (kBlock / 64);
         const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 6));
