@@ -2190,6 +2190,9 @@ __device__ __forceinline__ void comb_dispatch(int nw, const uint8_t *in, uint32_
     }
 }
 
+#ifndef FECGPU_COMB_HDR
+#define FECGPU_COMB_HDR 1  // combine plans: a wave's job headers in one round of loads
+#endif
 #ifndef FECGPU_COMB_MINW
 #define FECGPU_COMB_MINW 0  // >0: the grouped encode's combine (R = 4) asks for this many waves per SIMD
 #endif
@@ -2249,9 +2252,32 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
     for (XcdRange xr = xcd_range((njobs + wpb - 1) / wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
         const uint64_t j0 = xr.cur * wpb;
         const int nb = (int)min((uint64_t)wpb, njobs - j0);
-        // plan: wave w builds the tables of jobs w, w + 4, ...
-        for (int jl = wave; jl < nb; jl += kBlock / 64) {
+        // plan: wave w builds the tables of jobs w, w + 4, ...  Their headers
+        // come in one round of loads, a lane each (the decode passes walk a
+        // slot per repair or unknown, most of them empty: one dependent load
+        // per job was most of those passes' time)
+        constexpr int NW = kBlock / 64;
+#if FECGPU_COMB_HDR
+        CombJob Jl{};
+        Jl.xor_off = kNoXor;
+        if (wave + NW * lane < nb) Jl = a.jobs[j0 + wave + NW * lane];
+#endif
+        for (int ji = 0, jl = wave; jl < nb; ji++, jl += NW) {
+#if FECGPU_COMB_HDR
+            const auto rl64 = [&](uint64_t v) __attribute__((always_inline)) {
+                return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, ji) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), ji) << 32);
+            };
+            CombJob J;
+            J.in_off = rl64(Jl.in_off);
+            J.coef_off = rl64(Jl.coef_off);
+            J.out_list = rl64(Jl.out_list);
+            J.xor_off = rl64(Jl.xor_off);
+            J.nin = (uint32_t)__builtin_amdgcn_readlane((int)Jl.nin, ji);
+            J.nout = (uint32_t)__builtin_amdgcn_readlane((int)Jl.nout, ji);
+#else
             const CombJob J = a.jobs[j0 + jl];
+#endif
             const int nin = min((int)J.nin, nin_max), nout = min((int)(J.nout & ~kCombXorScaled), R);
             const CombRegion<R> rg(regions + (size_t)jl * job_lds, nin_max);
             const uint8_t *cf = a.coef + J.coef_off;

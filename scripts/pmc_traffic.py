@@ -21,18 +21,28 @@ def kind(name, config):
     encode is sw_stream_kernel, or comb_kernel<4> with sw_stream 0)."""
     if "fecgpu" not in name:
         return None
-    if config == 7:  # the streaming encode, or the combine-job one (sw_stream 0)
-        return "encode" if ("sw_stream_kernel" in name or "comb_kernel<4>" in name) else None
+    if config == 7:  # the streaming encode (or the combine-job one, sw_stream 0); the decode's chain
+        if "sw_stream_kernel" in name or "comb_kernel<4>" in name:
+            return "encode"
+        return "decode" if ("sw_dec_" in name or "comb_kernel<1>" in name or "comb_kernel<8>" in name) else None
     return "encode" if "encode" in name else "decode" if "decode" in name else None
 
 
 def per_kernel(path, counter, config):
     out = collections.defaultdict(list)
+    calls = 0  # config 7: decode calls (one header kernel each); the chain's bytes are summed per call
     for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
+        if r["Counter_Name"] != counter:
+            continue
+        if config == 7 and "sw_dec_hdr_kernel" in r["Kernel_Name"]:
+            calls += 1
         kd = kind(r["Kernel_Name"], config)
-        if r["Counter_Name"] == counter and kd:
+        if kd:
             out[kd].append(float(r["Counter_Value"]))
-    return {k: statistics.median(v) for k, v in out.items()}
+    res = {k: statistics.median(v) for k, v in out.items()}
+    if config == 7 and calls and "decode" in out:
+        res["decode"] = sum(out["decode"]) / calls
+    return res
 
 
 def main():
