@@ -680,6 +680,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
 __global__ __launch_bounds__(kBlock) void sw_dec_mid_kernel(SwDecArgs a) {
     __shared__ GfLds g;
     __shared__ SysLds<kSwSmallE, kSwSmallP> s_sys[kBlock / 64];
+    // nothing queued for this block (the common case): out before the tables
+    // (a whole block leaves together: the counters are the previous kernels')
+    if ((a.ctr->err & 1u) || (uint64_t)blockIdx.x * (kBlock / 64) >= min(a.ctr->nmid, (uint32_t)a.long_cap)) return;
     gf_load(g);
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -776,6 +779,7 @@ __device__ int long_refill(const SwDecArgs &a, LongLds &L, const SwLong &S, uint
 __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
     extern __shared__ uint4 dyn_long[];
     LongLds &L = *reinterpret_cast<LongLds *>(dyn_long);
+    if ((a.ctr->err & 1u) || blockIdx.x >= min(a.ctr->nlong, (uint32_t)a.long_cap)) return;  // nothing for this block
     gf_load(L.g);
     __syncthreads();
     const int lane = threadIdx.x;

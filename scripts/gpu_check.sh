@@ -40,6 +40,7 @@ for s in "$@"; do
         bench3) step bench3 600 python bench.py --config 3 --steps 10 --warmup 2 --cpu-seconds 10 ;;
         bench4) step bench4 600 python bench.py --config 4 --steps 5 --warmup 1 --cpu-seconds 10 ;;
         bench7) step bench7 600 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 10 ;;
+        bench7l10) step bench7l10 600 python bench.py --config 7 --steps 20 --warmup 5 --cpu-seconds 0 --sw-loss 0.1 ;;
         bench5) step bench5 600 python bench.py --config 5 --steps 10 --warmup 2 --cpu-seconds 0 ;;
         bench6) step bench6 600 python bench.py --config 6 --steps 10 --warmup 2 --cpu-seconds 0 ;;
         dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
