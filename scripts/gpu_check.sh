@@ -94,6 +94,15 @@ for s in "$@"; do
                     FECGPU_LIB=$v step abvar7_${n}_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
                 done
             done ;;
+        abvar7l10)  # cfg7 at 10 % loss: default build vs every variant, interleaved twice
+            for rep in 1 2; do
+                step abvar7l10_base_$rep 300 python bench.py --config 7 --steps 20 --warmup 5 --cpu-seconds 0 --no-verify --sw-loss 0.1
+                for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
+                    n=$(basename $v .so); n=${n#libfecgpu_}
+                    [ "$n" = check ] && continue
+                    FECGPU_LIB=$v step abvar7l10_${n}_$rep 300 python bench.py --config 7 --steps 20 --warmup 5 --cpu-seconds 0 --no-verify --sw-loss 0.1
+                done
+            done ;;
         abgroup)  # cfg7: sliding-window repairs per combine job, interleaved twice
             for rep in 1 2; do
                 for gsz in 2 4 8; do
