@@ -50,7 +50,10 @@ constexpr int kSwSolveIn = 128;              // syndrome rows a small system's s
 // LDS of a solve workgroup: its jobs' 8-output tables over the widest range of
 // syndrome rows (device-sized); more room than the encode's budget keeps
 // several jobs per workgroup
-constexpr uint32_t kSolveBudget = 64u << 10;
+#ifndef FECGPU_SOLVE_BUDGET_KB
+#define FECGPU_SOLVE_BUDGET_KB 64  // A/B (r03): 32 KB faster (0.235 vs 0.241 ms per cfg7 decode call), not yet verified as default
+#endif
+constexpr uint32_t kSolveBudget = FECGPU_SOLVE_BUDGET_KB << 10;
 // LDS for one streaming-encode workgroup's multiply tables (segment of up to
 // kSwSeg repairs x max_window coefficients x 21 B): 43 KB for 64 repairs at W 32
 #ifndef FECGPU_STREAM_BUDGET_KB
