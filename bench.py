@@ -484,13 +484,22 @@ def main():
         sys.exit(2)
     log(f"rank {rank}/{world} (local {local}) starting, backend "
         f"{args.dist_backend if world > 1 else 'none'}")
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
     if world > 1:
         if args.dist_backend == "nccl":  # RCCL: one rank per GPU
+            if ndev == 0:
+                log(f"rank {rank}: no GPU visible; RCCL needs one per rank")
+                sys.exit(2)
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:  # rehearsal of the N>1 path with ranks sharing the box's GPUs
-            torch.cuda.set_device(local % torch.cuda.device_count())
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo")  # host-only: every rank joins before any can leave
+            if ndev == 0:
+                log(f"rank {rank}: no GPU visible; nothing to time")
+                dist.barrier()
+                dist.destroy_process_group()
+                sys.exit(2)
+            torch.cuda.set_device(local % ndev)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())

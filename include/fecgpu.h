@@ -47,12 +47,13 @@
 extern "C" {
 #endif
 
-#define FECGPU_ABI_VERSION 4  /* 2: REPAIR frames carry nsrc; decoder limits / recovered queue;
+#define FECGPU_ABI_VERSION 5  /* 2: REPAIR frames carry nsrc; decoder limits / recovered queue;
                                  3: fecgpu_code.rlc_key / rlc_dt, FECGPU_MATRIX_RLC, sliding-window
                                     RLC (fecgpu_sw_*, SW frames, fecgpu_frame.key / dt);
                                  4: the nsrc-carrying REPAIR frame has its own type 0xfec4 (ABI 1's
                                     0xfec1 layout had no nsrc and is rejected, never misparsed);
-                                    sliding-window decode without a system-size cap */
+                                    sliding-window decode without a system-size cap;
+                                 5: fecgpu_sw_decode_errors (asynchronous decodes' error flags) */
 
 /* errors (mirror quiche's QUICHE_ERR_DONE = -1, QUICHE_ERR_BUFFER_TOO_SHORT = -2 style) */
 enum fecgpu_error {
@@ -415,11 +416,25 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
  * a header is bad or out of order (the kernels check them; then nothing is
  * recovered and the statuses are the arrival flags).  A long linked system
  * whose operation log does not fit the ctx's reservation is retried larger
- * with FECGPU_F_SYNC, else it stays lost (tuning "sw_log_entries"). */
+ * with FECGPU_F_SYNC; without it, that system stays lost and the call raises
+ * FECGPU_SW_ERR_CAPACITY for fecgpu_sw_decode_errors (a bad header raises
+ * FECGPU_SW_ERR_HEADER), so an asynchronous caller can tell an overflow from
+ * a source the repairs do not determine (tuning "sw_log_entries"). */
 ssize_t fecgpu_sw_decode_device(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_present, uint64_t nsrc,
                                 const uint8_t *rep, const uint8_t *rep_present,
                                 const struct fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t sym_len,
                                 uint32_t stride, uint8_t *src_status, uint32_t flags, void *stream);
+
+/* Error flags raised by asynchronous fecgpu_sw_decode_device calls on the
+ * current device since the last query, OR-ed together: waits until every
+ * sliding-window call issued on the ctx so far has finished, stores the flags
+ * in *flags and clears them.  After FECGPU_SW_ERR_CAPACITY the ctx's later
+ * calls reserve a log large enough for what overflowed (a synchronous decode
+ * of the same inputs recovers what was left lost).  Returns 0 or a negative
+ * error. */
+#define FECGPU_SW_ERR_HEADER   1u /* a header was bad or out of order: that call recovered nothing */
+#define FECGPU_SW_ERR_CAPACITY 2u /* a long system's operation log did not fit: its sources stayed lost */
+ssize_t fecgpu_sw_decode_errors(fecgpu_ctx *ctx, uint32_t *flags);
 
 /* ---- sliding-window per-connection objects ----------------------------
  * The Connection's per-packet API for the sliding-window code (RFC 8681

@@ -172,6 +172,7 @@ struct fecgpu_ctx {
     // sliding-window calls: device scratch slots and the last call's end event, per device
     std::map<int, std::vector<std::pair<void *, size_t>>> sw_scratch;
     std::map<int, hipEvent_t> sw_event;
+    std::map<int, SwSticky *> sw_sticky;  // asynchronous decodes' error flags, per device
     void *sw_host = nullptr;  // pinned staging of sliding-window decodes (ctx_sw_host)
     size_t sw_host_bytes = 0;
     // codes with k + r > 64: parity rows on each device, by (device, k, r, matrix, key, dt)
@@ -385,6 +386,10 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
             if (b.first) (void)hipFree(b.first);
     }
     if (ctx->sw_host) (void)hipHostFree(ctx->sw_host);
+    for (auto &kv : ctx->sw_sticky) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second);
+    }
     for (auto &kv : ctx->wide_rows) {
         (void)hipSetDevice(std::get<0>(kv.first));
         (void)hipFree(kv.second);
@@ -1170,6 +1175,32 @@ ssize_t ctx_sw_host(fecgpu_ctx *ctx, size_t bytes, void **p) {
         ctx->sw_host_bytes = want;
     }
     *p = ctx->sw_host;
+    return 0;
+}
+
+ssize_t ctx_sw_sticky(fecgpu_ctx *ctx, SwSticky **p) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    SwSticky *&w = ctx->sw_sticky[dev];
+    if (!w) {
+        void *m = nullptr;
+        HIP_TRY(hipMalloc(&m, sizeof(SwSticky)), "hipMalloc sw error flags");
+        const hipError_t e = hipMemset(m, 0, sizeof(SwSticky));
+        if (e != hipSuccess) {
+            (void)hipFree(m);
+            return dev_err(e, "hipMemset sw error flags");
+        }
+        w = static_cast<SwSticky *>(m);
+    }
+    *p = w;
+    return 0;
+}
+
+ssize_t ctx_sw_wait(fecgpu_ctx *ctx) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    auto it = ctx->sw_event.find(dev);
+    if (it != ctx->sw_event.end()) HIP_TRY(hipEventSynchronize(it->second), "hipEventSynchronize");
     return 0;
 }
 

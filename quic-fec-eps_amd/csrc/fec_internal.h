@@ -289,12 +289,16 @@ inline uint32_t sw_stream_lds(int segcap, int max_window) {
 // replay the log over 256-byte column chunks of the data).
 constexpr int kSwSmallE = 64;   // unknowns of a small system
 constexpr int kSwSmallP = 96;   // equations (received repairs) of a small system
-constexpr int kSwRows = 256;    // long systems: rows alive at once (equations covering one source)
+constexpr int kSwRows = 256;    // long systems: row slots (more rows alive at one column are reduced
+                                // to a basis first: they span at most 255 columns, fec_swdec.hip)
 constexpr int kSwChunk = 4096;  // sources per planning chunk
 
+// SwDecCtr::err / SwSticky::err bits
+constexpr uint32_t kSwErrHeader = 1u;    // a bad or unordered header: the call recovers nothing
+constexpr uint32_t kSwErrCapacity = 2u;  // a long system's operation log (or the queue) did not fit:
+                                         // that system stays lost (a larger log fixes it)
 struct SwDecCtr {  // per call, zeroed before the first kernel
-    uint32_t nlost, wmax, maxp, err;   // err: bit 0 bad header; bit 1 log / pivot-area capacity
-                                       // exceeded (retry larger); bit 2 more than kSwRows rows alive
+    uint32_t nlost, wmax, maxp, err;   // err: kSwErr* bits
     uint32_t nmid, nlong, npiv, recovered;  // queued mid / long systems, pivot rows, recovered
     uint32_t maxin, pad0, pad1, pad2;       // widest small-system solve (syndrome rows)
     unsigned long long nlog;           // long-system log entries
@@ -313,7 +317,14 @@ struct SwOp {
     uint32_t tab[5];
     uint32_t aux2;
 };
-enum : uint32_t { kOpLoad = 1, kOpElim = 2, kOpStore = 3, kOpXBegin = 4, kOpXTerm = 5, kOpXEnd = 6, kOpXFree = 7 };
+enum : uint32_t { kOpLoad = 1, kOpElim = 2, kOpStore = 3, kOpXBegin = 4, kOpXTerm = 5, kOpXEnd = 6, kOpXFree = 7,
+                  kOpJump = 8 /* the log continues at aux | aux2 << 32 */ };
+// Error flags of asynchronous decodes, OR-ed across calls on one device until
+// read (fecgpu_sw_decode_errors); need = the largest log an overflow asked for
+struct SwSticky {
+    uint32_t err, pad;
+    unsigned long long need;
+};
 
 struct SwDecArgs {
     const uint8_t *src_present, *rep_present;  // device
@@ -350,6 +361,7 @@ struct SwDecArgs {
     uint64_t piv_cap;
     uint8_t *src;                              // the sources (replay writes recovered ones)
     const uint8_t *synd;                       // syndrome rows (g * stride)
+    SwSticky *sticky;                          // nullable: asynchronous calls also raise errors here
 };
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s);    // statuses, lost list, systems
 hipError_t launch_sw_dec_long(const SwDecArgs &a, hipStream_t s);    // long systems: logs, syndrome jobs
@@ -392,6 +404,10 @@ ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p);
 // the ctx's pinned host staging block for sliding-window decodes (grown on
 // demand; a decode synchronizes before returning, so the next may reuse it)
 ssize_t ctx_sw_host(fecgpu_ctx *ctx, size_t bytes, void **p);
+// the current device's sticky error word of asynchronous decodes (allocated zeroed)
+ssize_t ctx_sw_sticky(fecgpu_ctx *ctx, SwSticky **p);
+// waits until the current device's sliding-window calls issued so far have finished
+ssize_t ctx_sw_wait(fecgpu_ctx *ctx);
 ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);
 ssize_t ctx_sw_end(fecgpu_ctx *ctx, hipStream_t s);
 

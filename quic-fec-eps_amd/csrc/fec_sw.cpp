@@ -51,7 +51,7 @@ constexpr int kSwSolveIn = 128;              // syndrome rows a small system's s
 // syndrome rows (device-sized); more room than the encode's budget keeps
 // several jobs per workgroup
 #ifndef FECGPU_SOLVE_BUDGET_KB
-#define FECGPU_SOLVE_BUDGET_KB 64  // A/B (r03): 32 KB faster (0.235 vs 0.241 ms per cfg7 decode call), not yet verified as default
+#define FECGPU_SOLVE_BUDGET_KB 32  // A/B (r03): 32 KB 0.235 vs 64 KB 0.241 ms per cfg7 decode call (1.62 vs 1.71 at 10 % loss)
 #endif
 constexpr uint32_t kSolveBudget = FECGPU_SOLVE_BUDGET_KB << 10;
 // LDS for one streaming-encode workgroup's multiply tables (segment of up to
@@ -63,6 +63,7 @@ constexpr uint32_t kStreamBudget = FECGPU_STREAM_BUDGET_KB << 10;
 constexpr uint64_t kSwStreamSources = 1ull << 32;  // the streaming encode's source positions are 32-bit
 // sources and repairs per call: the device plan numbers them in 32 bits
 constexpr uint64_t kSwMaxSources = (1ull << 32) - 256;
+constexpr int kSwMaxRetries = 4;  // larger-log rounds of a synchronous decode
 
 ssize_t check_geometry(uint32_t sym_len, uint32_t stride, const void *a, const void *b) {
     if (stride == 0 || (stride & 15) || sym_len == 0 || sym_len > stride) return FECGPU_ERR_INVALID_ARG;
@@ -247,10 +248,12 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
 
 // One decode on the device.  src / rep / present / rep_present / hdr / stat
 // are device pointers; ctr_out (pinned, nullable) receives the counters once
-// the stream reaches the end of the call.
+// the stream reaches the end of the call; sticky (nullable, asynchronous
+// calls) collects its errors for fecgpu_sw_decode_errors.
 ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, uint64_t nsrc, const uint8_t *rep,
                        const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t S,
-                       uint32_t stride, uint8_t *stat, hipStream_t s, SwDecCtr *ctr_out, uint64_t log_entries) {
+                       uint32_t stride, uint8_t *stat, hipStream_t s, SwDecCtr *ctr_out, uint64_t log_entries,
+                       SwSticky *sticky = nullptr) {
     const int long_min = ctx_sw_long_min(ctx);
     const DecBlock L = dec_block(nsrc, nrep, long_min);
     void *pb = nullptr, *psyn = nullptr, *ppiv = nullptr, *plog = nullptr;
@@ -296,6 +299,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.piv_cap = L.piv_cap;
     a.src = src;
     a.synd = static_cast<const uint8_t *>(psyn);
+    a.sticky = sticky;
 
     SW_TRY(hipMemsetAsync(a.ctr, 0, L.o_chunk - L.o_ctr, s), "sliding-window decode counters");
     SW_TRY(launch_sw_dec_plan(a, s), "sliding-window decode plan launch");
@@ -338,9 +342,12 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     return 0;
 }
 
-// Synchronous decode with the counters read back: retries once with a larger
-// operation log if a long system overflowed it (a decode is idempotent: it
-// reads only received symbols and rewrites the lost ones).
+// Synchronous decode with the counters read back.  A long system whose
+// operation log overflowed the reservation is decoded again with a log sized
+// past what the overflow asked for (a decode is idempotent: it reads only
+// received symbols and rewrites the lost ones); kSwMaxRetries such rounds,
+// each at least 4x larger, then FECGPU_ERR_DEVICE.  No other condition leaves
+// a determined source lost.
 ssize_t sw_decode_sync(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, uint64_t nsrc, const uint8_t *rep,
                        const uint8_t *rep_present, const fecgpu_sw_repair *hdr, uint64_t nrep, uint32_t S,
                        uint32_t stride, uint8_t *stat, hipStream_t s, const std::function<ssize_t()> &after) {
@@ -353,9 +360,12 @@ ssize_t sw_decode_sync(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
                               log_entries));
         RC_TRY(after());
         SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
-        if (ctr->err & 1u) return FECGPU_ERR_INVALID_ARG;
-        if (!(ctr->err & 2u)) break;
-        if (attempt == 2) return set_dev_error(hipErrorOutOfMemory, "sliding-window decode: operation log capacity");
+        if (ctr->err & kSwErrHeader) return FECGPU_ERR_INVALID_ARG;
+        if (ctr->err & ~(kSwErrHeader | kSwErrCapacity))
+            return set_dev_error(hipErrorUnknown, "sliding-window decode: unexpected device error flag");
+        if (!(ctr->err & kSwErrCapacity)) break;
+        if (attempt == kSwMaxRetries)
+            return set_dev_error(hipErrorOutOfMemory, "sliding-window decode: operation log capacity");
         log_entries = std::max<uint64_t>(log_entries * 4, (uint64_t)ctr->nlog + 1);
         ctx_sw_log_grow(ctx, log_entries);
     }
@@ -470,11 +480,28 @@ ssize_t fecgpu_sw_decode_device(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *sr
         rc = sw_decode_sync(ctx, src, src_present, nsrc, rep, rep_present, hdr, nrep, sym_len, stride, src_status, s,
                             [] { return (ssize_t)0; });
     } else {
+        SwSticky *sticky = nullptr;
+        RC_TRY(ctx_sw_sticky(ctx, &sticky));
         rc = sw_decode_core(ctx, src, src_present, nsrc, rep, rep_present, hdr, nrep, sym_len, stride, src_status, s,
-                            nullptr, ctx_sw_log_entries(ctx, nsrc, nrep));
+                            nullptr, ctx_sw_log_entries(ctx, nsrc, nrep), sticky);
     }
     RC_TRY(ctx_sw_end(ctx, s));
     return rc;
+}
+
+ssize_t fecgpu_sw_decode_errors(fecgpu_ctx *ctx, uint32_t *flags) {
+    if (!ctx || !flags) return FECGPU_ERR_INVALID_ARG;
+    *flags = 0;
+    SwSticky *d = nullptr;
+    RC_TRY(ctx_sw_sticky(ctx, &d));
+    RC_TRY(ctx_sw_wait(ctx));  // every sliding-window call issued so far on this device
+    SwSticky h{};
+    SW_TRY(hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost), "D2H sw error flags");
+    SW_TRY(hipMemset(d, 0, sizeof(h)), "sw error flags reset");
+    // the next asynchronous calls reserve what the overflow asked for, twice over
+    if (h.err & kSwErrCapacity) ctx_sw_log_grow(ctx, std::max<uint64_t>(2 * h.need, 1u << 16));
+    *flags = h.err;
+    return 0;
 }
 
 }  // extern "C"

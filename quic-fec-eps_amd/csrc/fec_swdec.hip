@@ -71,6 +71,16 @@ __device__ __forceinline__ void set_tab(uint32_t (&t)[5], uint32_t c) {
 
 __device__ __forceinline__ uint64_t lanes_below(int lane) { return (1ull << lane) - 1ull; }
 
+// An error of this call (kSwErr* bits), also raised in the ctx's sticky word for
+// asynchronous calls (need: the log size an overflow asked for)
+__device__ __forceinline__ void dec_err(const SwDecArgs &a, uint32_t bits, unsigned long long need = 0) {
+    atomicOr(&a.ctr->err, bits);
+    if (a.sticky) {
+        atomicOr(&a.sticky->err, bits);
+        if (need) atomicMax(&a.sticky->need, need);
+    }
+}
+
 template <class T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
@@ -140,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_hdr_kernel(SwDecArgs a) {
     const uint64_t anybad = __ballot(bad);
     if ((threadIdx.x & 63) == 0) {
         s_w[threadIdx.x >> 6] = w;
-        if (anybad) atomicOr(&a.ctr->err, 1u);
+        if (anybad) dec_err(a, kSwErrHeader);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -575,7 +585,7 @@ __device__ void sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, u
                 L.t_hi = (uint32_t)t_hi;
                 (to_mid ? a.mids : a.longs)[k] = L;
             } else {
-                atomicOr(&a.ctr->err, 2u);
+                dec_err(a, kSwErrCapacity);
             }
         }
         return;
@@ -708,6 +718,7 @@ struct LongLds {
     uint32_t row_hi[kSwRows], row_t[kSwRows];
     uint8_t freel[kSwRows];      // free slots (stack)
     uint8_t fq[kSwRows];         // elimination factor per alive position
+    uint8_t lead[kSwRows];       // compaction: alive position holds a leading row
     uint8_t prow[256];           // backward: the pivot row
 };
 
@@ -775,6 +786,113 @@ __device__ int long_refill(const SwDecArgs &a, LongLds &L, const SwLong &S, uint
     return n;
 }
 
+// Forward log writer of one long system (wave-uniform): entries go to
+// a.log[pos ..); a chunk that runs out is linked to a new one, taken from the
+// call's log counter, by a kOpJump entry (the replay follows it).
+constexpr uint64_t kLogChunk = 4096;
+struct LogW {
+    uint64_t pos, end;  // next entry; chunk end (its last entry kept for a jump)
+    uint32_t count;     // entries written, jumps included (the replay's trip count)
+};
+
+// Room for n more entries at w.pos; false when the log is full (the caller
+// gives the system up with kSwErrCapacity).
+__device__ bool log_room(const SwDecArgs &a, LogW &w, uint32_t n, int lane) {
+    if (w.pos + n < w.end) return true;
+    const unsigned long long size = max<unsigned long long>((unsigned long long)n + 1, kLogChunk);
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&a.ctr->nlog, size);
+    base = __shfl(base, 0);
+    if (base + size > a.log_cap) {
+        if (lane == 0) dec_err(a, kSwErrCapacity, base + size);
+        return false;
+    }
+    if (lane == 0) {
+        const uint32_t notab[5] = {0, 0, 0, 0, 0};
+        emit(a.log + w.pos, kOpJump, 0, 0, (uint32_t)base, (uint32_t)(base >> 32), notab);
+    }
+    w.pos = base;
+    w.end = base + size;
+    w.count++;
+    return true;
+}
+
+// All kSwRows slots are taken at column c and another row is due.  The alive
+// rows are zero before c and end by c + 254 (a window holds at most 255
+// sources), so at most 255 of them are independent.  Reduce them to echelon
+// form over columns c .. c + 254 — per column, the row with a nonzero there
+// that ends first leads, as in the forward pass, so no row widens — and free
+// the rows left zero: they were combinations of the others, so dropping them
+// changes neither the row space nor any unknown the system determines.  The
+// eliminations are logged like the forward ones (the replay applies them to the
+// rows' data).  Frees at least one slot; false if the log is full.
+__device__ bool long_compact(const SwDecArgs &a, LongLds &L, uint32_t c, int &nact, int &nfree, LogW &fw,
+                             int lane) {
+    for (int i = lane; i < nact; i += 64) L.lead[i] = 0;
+    SWD_WAVE_SYNC();
+    int nlead = 0;
+    for (uint32_t jj = 0; jj < (uint32_t)kSwRows - 1 && nlead < nact; jj++) {
+        const uint32_t j = (c + jj) & 255;
+        uint64_t best = ~0ull;
+        for (int i = lane; i < nact; i += 64) {
+            const uint32_t s = L.act[i];
+            if (!L.lead[i] && L.rowc[s][j]) best = min(best, ((uint64_t)L.row_hi[s] << 9) | (uint64_t)i);
+        }
+        best = wave_min64(best);
+        if (best == ~0ull) continue;  // no unled row has column j (uniform)
+        const int ppos = (int)(best & 511);
+        const uint32_t P = L.act[ppos], hiP = L.row_hi[P];
+        const uint32_t ip = ginv(L.g, L.rowc[P][j]);
+        for (int i0 = 0; i0 < nact; i0 += 64) {
+            if (!log_room(a, fw, 64, lane)) return false;
+            const int i = i0 + lane;
+            uint32_t f = 0;
+            if (i < nact && i != ppos && !L.lead[i]) f = gmul(L.g, L.rowc[L.act[i]][j], ip);
+            if (i < nact) L.fq[i] = (uint8_t)f;
+            const uint64_t b = __ballot(f != 0);
+            if (f) {
+                uint32_t tab[5];
+                set_tab(tab, f);
+                emit(a.log + fw.pos + __popcll(b & lanes_below(lane)), kOpElim, L.act[i], P, 0, 0, tab);
+            }
+            fw.pos += __popcll(b);
+            fw.count += __popcll(b);
+        }
+        SWD_WAVE_SYNC();
+        if (lane == 0) L.lead[ppos] = 1;
+        // the unled rows are zero on [c, c + jj) (eliminated or empty there): update [c + jj, hiP]
+        const uint32_t wP = hiP - (c + jj) + 1;
+        const uint32_t total = (uint32_t)nact * wP;
+        for (uint32_t w0 = 0; w0 < total; w0 += 64) {
+            const uint32_t wi = w0 + lane;
+            if (wi < total) {
+                const uint32_t i = wi / wP, col = (c + jj + wi % wP) & 255;
+                const uint32_t f = L.fq[i];
+                if (f) L.rowc[L.act[i]][col] ^= (uint8_t)gmul(L.g, f, L.rowc[P][col]);
+            }
+        }
+        SWD_WAVE_SYNC();
+        nlead++;
+    }
+    // keep the leading rows (in admission order), free the rest
+    int keep = 0;
+    for (int i0 = 0; i0 < nact; i0 += 64) {
+        const int i = i0 + lane;
+        const uint32_t s = i < nact ? L.act[i] : 0u;
+        const bool live = i < nact && L.lead[i];
+        const bool dead = i < nact && !live;
+        const uint64_t bl = __ballot(live), bd = __ballot(dead);
+        SWD_WAVE_SYNC();
+        if (live) L.act[keep + __popcll(bl & lanes_below(lane))] = s;
+        if (dead) L.freel[nfree + __popcll(bd & lanes_below(lane))] = (uint8_t)s;
+        keep += __popcll(bl);
+        nfree += __popcll(bd);
+        SWD_WAVE_SYNC();
+    }
+    nact = keep;
+    return true;
+}
+
 // A wave per long system: forward elimination, null-space sweep, logs.
 __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
     extern __shared__ uint4 dyn_long[];
@@ -810,7 +928,10 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
             if (lane == 0) a.longs[k] = S;
             continue;
         }
-        const unsigned long long need = 2ull * p + 2ull * wsum + 2ull * e;
+        // forward: loads p, stores <= p, eliminations <= wsum (more after a
+        // compaction: chained chunks), one entry kept for a jump; backward:
+        // per column a free mark, or begin + end + the pivot row's terms (<= wsum)
+        const unsigned long long nfw0 = 2ull * p + wsum + 1, need = nfw0 + wsum + 2ull * e;
         const uint32_t npmax = min(p, e);
         unsigned long long base = 0;
         uint32_t piv0 = 0;
@@ -822,17 +943,17 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
         piv0 = __shfl(piv0, 0);
         if (base + need > a.log_cap || (uint64_t)piv0 + npmax > a.piv_cap) {
             if (lane == 0) {
-                atomicOr(&a.ctr->err, 2u);
+                dec_err(a, kSwErrCapacity, base + need);
                 a.longs[k] = S;
             }
             continue;
         }
-        SwOp *fwd = a.log + base;
-        SwOp *bwd = fwd + p + wsum + p;
+        LogW fw{base, base + nfw0, 0};
+        SwOp *bwd = a.log + base + nfw0;
         // ---- forward elimination ----
         for (int i = lane; i < kSwRows; i += 64) L.freel[i] = (uint8_t)(kSwRows - 1 - i);
         int nfree = kSwRows, nact = 0, sh = 0, sn = 0;
-        uint32_t nf = 0, npiv = 0, B = 1;
+        uint32_t npiv = 0, B = 1;
         uint64_t next = S.t_lo;
         bool fail = false;
         SWD_WAVE_SYNC();
@@ -846,7 +967,11 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                     if (sn == 0) break;
                 }
                 if (L.stg_lo[sh] > c) break;  // rows arrive in order of lo, and every lo <= c is admitted by now
-                if (nfree == 0) {
+                if (nfree == 0 && !long_compact(a, L, c, nact, nfree, fw, lane)) {
+                    fail = true;  // log full
+                    break;
+                }
+                if (!log_room(a, fw, 1, lane)) {
                     fail = true;
                     break;
                 }
@@ -857,10 +982,11 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                     L.row_t[slot] = L.stg_t[sh];
                     L.act[nact] = slot;
                     a.synrow[L.stg_t[sh]] = ~0u;
-                    emit(fwd + nf, kOpLoad, slot, 0, L.stg_t[sh], 0, notab);
+                    emit(a.log + fw.pos, kOpLoad, slot, 0, L.stg_t[sh], 0, notab);
                 }
                 nact++;
-                nf++;
+                fw.pos++;
+                fw.count++;
                 sh++;
                 SWD_WAVE_SYNC();
             }
@@ -881,8 +1007,11 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                 const uint32_t hiP = L.row_hi[P];
                 const uint32_t ip = ginv(L.g, L.rowc[P][cs]);
                 // factors and ELIM entries
-                uint32_t ne = 0;
-                for (int i0 = 0; i0 < nact; i0 += 64) {
+                for (int i0 = 0; i0 < nact && !fail; i0 += 64) {
+                    if (!log_room(a, fw, 64, lane)) {
+                        fail = true;
+                        break;
+                    }
                     const int i = i0 + lane;
                     uint32_t f = 0;
                     if (i < nact && i != ppos) f = gmul(L.g, L.rowc[L.act[i]][cs], ip);
@@ -891,11 +1020,15 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                     if (f) {
                         uint32_t tab[5];
                         set_tab(tab, f);
-                        emit(fwd + nf + ne + __popcll(b & lanes_below(lane)), kOpElim, L.act[i], P, 0, 0, tab);
+                        emit(a.log + fw.pos + __popcll(b & lanes_below(lane)), kOpElim, L.act[i], P, 0, 0, tab);
                     }
-                    ne += __popcll(b);
+                    fw.pos += __popcll(b);
+                    fw.count += __popcll(b);
                 }
-                nf += ne;
+                if (fail || !log_room(a, fw, 1, lane)) {
+                    fail = true;
+                    break;
+                }
                 SWD_WAVE_SYNC();
                 // row updates over [c, hiP]: lanes over (alive position, column) pairs
                 const uint32_t wP = hiP - c + 1;
@@ -920,9 +1053,10 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                     a.pivhi[pv] = hiP;
                     a.pivt[pv] = L.row_t[P];
                     a.colpiv[x0 + c] = pv;
-                    emit(fwd + nf, kOpStore, P, 0, pv, 0, notab);
+                    emit(a.log + fw.pos, kOpStore, P, 0, pv, 0, notab);
                 }
-                nf++;
+                fw.pos++;
+                fw.count++;
                 npiv++;
                 B = max(B, wP);
             }
@@ -944,11 +1078,8 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
             }
             nact = keep;
         }
-        if (fail) {  // more rows alive than kSwRows: the system stays lost
-            if (lane == 0) {
-                atomicOr(&a.ctr->err, 4u);
-                a.longs[k] = S;
-            }
+        if (fail) {  // the log is full (kSwErrCapacity raised): the system stays lost
+            if (lane == 0) a.longs[k] = S;
             continue;
         }
         // syndrome jobs for the pivot rows (the only rows whose data is used), in
@@ -1076,8 +1207,8 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
         if (lane == 0) {
             S.ok = 1;
             S.fwd = base;
-            S.nfwd = nf;
-            S.bwd = base + p + wsum + p;
+            S.nfwd = fw.count;
+            S.bwd = base + nfw0;
             S.nbwd = nb;
             S.piv0 = piv0;
             a.longs[k] = S;
@@ -1102,11 +1233,13 @@ __global__ __launch_bounds__(64) void sw_dec_replay_kernel(SwDecArgs a) {
         const uint32_t dw = ch * 64 + lane;
         const bool live = dw < ndw;
         const uint64_t boff = (uint64_t)dw * 4;
-        const SwOp *op = a.log + S.fwd;
+        uint64_t at = S.fwd;
         for (uint32_t i = 0; i < S.nfwd; i++) {
-            const SwOp o = op[i];
+            const SwOp o = a.log[at++];
             const uint32_t kind = o.op & 0xFFu, sa = (o.op >> 8) & 0xFFu, sb = (o.op >> 16) & 0xFFu;
-            if (kind == kOpElim) {
+            if (kind == kOpJump) {
+                at = (uint64_t)o.aux | ((uint64_t)o.aux2 << 32);
+            } else if (kind == kOpElim) {
                 const uint32_t t[5] = {o.tab[0], o.tab[1], o.tab[2], o.tab[3], o.tab[4]};
                 slots[sa][lane] ^= tmul(slots[sb][lane], t);
             } else if (kind == kOpLoad) {
@@ -1118,7 +1251,7 @@ __global__ __launch_bounds__(64) void sw_dec_replay_kernel(SwDecArgs a) {
                 if (live) *reinterpret_cast<uint32_t *>(a.pivdata + (uint64_t)o.aux * a.stride + boff) = slots[sa][lane];
             }
         }
-        op = a.log + S.bwd;
+        const SwOp *op = a.log + S.bwd;
         uint32_t x = 0;
         for (uint32_t i = 0; i < S.nbwd; i++) {
             const SwOp o = op[i];

@@ -32,6 +32,7 @@ _MATRIX_IDS = {"cauchy": MATRIX_CAUCHY, "vandermonde": MATRIX_VANDERMONDE, "rlc"
 FRAMING_FIXED, FRAMING_LENPREFIX = 0, 1
 STATUS_OK, STATUS_UNRECOVERABLE = 0, 1
 F_HOST_PTRS, F_SYNC = 1, 2
+SW_ERR_HEADER, SW_ERR_CAPACITY = 1, 2  # fecgpu_sw_decode_errors flags
 MAX_K, MAX_R = 64, 8
 WORKLOAD_FIXED, WORKLOAD_MIXED = 0, 1
 ERASURE_NONE, ERASURE_EXACT, ERASURE_IID = 0, 1, 2
@@ -57,7 +58,7 @@ EXPORTS = (
     "fecgpu_decoder_tick",
     "fecgpu_frame_source_id_len", "fecgpu_frame_write_source_id", "fecgpu_frame_repair_len",
     "fecgpu_frame_write_repair", "fecgpu_frame_write_repair_header", "fecgpu_frame_parse",
-    "fecgpu_sw_encode", "fecgpu_sw_decode", "fecgpu_sw_decode_device",
+    "fecgpu_sw_encode", "fecgpu_sw_decode", "fecgpu_sw_decode_device", "fecgpu_sw_decode_errors",
     "fecgpu_frame_write_sw_source", "fecgpu_frame_write_sw_repair",
     "fecgpu_sw_encoder_new", "fecgpu_sw_encoder_free", "fecgpu_sw_encoder_add_source",
     "fecgpu_sw_encoder_flush", "fecgpu_sw_encoder_next_repair",
@@ -208,6 +209,7 @@ def _lib():
             "fecgpu_sw_encode": (sz, [vp, vp, u64, vp, vp, u64, u32, u32, u32, u32, vp]),
             "fecgpu_sw_decode": (sz, [vp, vp, vp, u64, vp, vp, vp, u64, u32, u32, vp, u32, vp]),
             "fecgpu_sw_decode_device": (sz, [vp, vp, vp, u64, vp, vp, vp, u64, u32, u32, vp, u32, vp]),
+            "fecgpu_sw_decode_errors": (sz, [vp, ctypes.POINTER(ctypes.c_uint32)]),
             "fecgpu_frame_write_sw_source": (sz, [vp, ctypes.c_size_t, u64]),
             "fecgpu_frame_write_sw_repair": (sz, [vp, ctypes.c_size_t, ctypes.POINTER(fecgpu_sw_repair), vp,
                                                   ctypes.c_size_t]),
@@ -392,6 +394,14 @@ class Context:
         return _check(_lib().fecgpu_sw_decode_device(
             self._h, _ptr(src), _ptr(src_present), nsrc, _ptr(rep), _ptr(rep_present), _ptr(hdr),
             nrep, sym_len, stride, _ptr(src_status), flags, _stream(stream)), "fecgpu_sw_decode_device")
+
+    def sw_decode_errors(self) -> int:
+        """fecgpu_sw_decode_errors: the SW_ERR_* flags raised by asynchronous
+        sw_decode_device calls on the current device since the last query (waits for
+        them; clears the flags)."""
+        f = ctypes.c_uint32(0)
+        _check(_lib().fecgpu_sw_decode_errors(self._h, ctypes.byref(f)), "fecgpu_sw_decode_errors")
+        return int(f.value)
 
     def synth_batch(self, code: Code, workload: int, seed: int, w0: int, win, sym_len, *,
                     L: int, stride: int, nwin: int, stream=None) -> int:

@@ -80,6 +80,9 @@ def test_gpus_flag_launches_n_ranks(bench):
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert "launching 2 ranks" in r.stderr
     assert "rank 0/2" in r.stderr and "rank 1/2" in r.stderr, r.stderr[-3000:]
+    # no GPU here: both ranks join the gloo group, then leave cleanly (exit 2, which the launcher reports as a failure), never
+    # one rank torn down by the launcher before the other has started
+    assert r.stderr.count("no GPU visible") == 2 and r.returncode != 0, r.stderr[-3000:]
 
 
 def test_gpus_flag_refuses_without_enough_gpus(bench):

@@ -115,7 +115,7 @@ def test_null_and_invalid_args_before_device():
     assert L.fecgpu_ctx_new(None, 0, None) == fecgpu.ERR_INVALID_ARG
     assert L.fecgpu_strerror(fecgpu.ERR_UNRECOVERABLE) == b"unrecoverable"
     assert L.fecgpu_strerror(fecgpu.ERR_LIMIT) == b"limit reached"
-    assert L.fecgpu_abi_version() == 4
+    assert L.fecgpu_abi_version() == 5
 
 
 def test_no_cpu_fallback_without_gpu():

@@ -379,6 +379,123 @@ def test_sw_decode_log_overflow_retries():
         c.close()
 
 
+def two_per_step(nsrc, W, key0, dt=15):
+    """Two repairs after every source over the last W (distinct keys): about
+    2 W received repairs cover each source."""
+    h = []
+    for t, (fss, nss, _, _) in enumerate(N.sw_schedule(nsrc, 1, W)):
+        h += [(fss, nss, (key0 + 2 * t) & 0xFFFF, dt), (fss, nss, (key0 + 2 * t + 1) & 0xFFFF, dt)]
+    return hdr_array(h)
+
+
+@pytest.mark.parametrize("loss", [0.02, 0.10, 0.30])
+def test_sw_decode_two_repairs_per_step_W255(ctx, loss):
+    """More repairs alive at one column than the long-system pass has row slots
+    (256): 2 repairs per step at W = 255, step 1, so ~500 received repairs cover
+    every lost source.  The pass reduces its alive rows to a basis when the
+    slots run out (fec_swdec.hip long_compact); statuses, count and every byte
+    equal the banded oracle's global decode."""
+    nsrc, L, W = 2500, 24, 255
+    stride = O.round_up(L, 16)
+    src = stream(nsrc, L, stride, 255 + int(loss * 100))
+    hdr = two_per_step(nsrc, W, key0=int(loss * 1000))
+    rep = O.sw_encode(src, hdr, L)
+    rng = np.random.default_rng(int(loss * 1000) + 1)
+    sp = (rng.random(nsrc) >= loss).astype(np.uint8)
+    rp = (rng.random(len(hdr)) >= loss).astype(np.uint8)
+    assert max_system(sp, rp, hdr) > 100
+    assert check_vs_oracle(ctx, src, sp, rep, rp, hdr, L) == (sp == 0).sum()
+
+
+@pytest.mark.parametrize("nsame,dt,lost", [(320, 15, 150), (700, 15, 250), (400, 2, 120), (300, 15, 255)])
+def test_sw_decode_many_repairs_one_fss(ctx, nsame, dt, lost):
+    """More than 300 received repairs sharing one fss (all over the same 255
+    sources, `lost` of them lost) inside a regular W 32 step 4 stream: every
+    one is alive at the system's first column.  DT 2 makes sparse rows (the
+    shared window partly undetermined).  Equal to the banded oracle."""
+    nsrc, L, W0 = 1200, 40, 255
+    stride = O.round_up(L, 16)
+    src = stream(nsrc, L, stride, nsame + dt)
+    base = N.sw_schedule(nsrc, 4, 32, key0=7)
+    fss0 = 400
+    same = [(fss0, W0, (1000 + u) & 0xFFFF, dt) for u in range(nsame)]
+    h = sorted(base + same, key=lambda x: x[0])   # fss nondecreasing (stable: base first)
+    hdr = hdr_array(h)
+    rep = O.sw_encode(src, hdr, L)
+    rng = np.random.default_rng(nsame + lost)
+    sp = (rng.random(nsrc) >= 0.03).astype(np.uint8)
+    sp[fss0 + rng.choice(W0, lost, replace=False)] = 0
+    rp = np.ones(len(hdr), np.uint8)
+    rp[rng.choice(len(hdr), len(hdr) // 50, replace=False)] = 0
+    check_vs_oracle(ctx, src, sp, rep, rp, hdr, L)
+
+
+def test_sw_decode_compaction_with_small_log():
+    """The compaction's eliminations overflow a long system's first log chunk:
+    chained chunks (kOpJump) and, with a tiny reservation ("sw_log_entries" =
+    4096), the synchronous retries; equal to the oracle."""
+    c = fecgpu.Context()
+    try:
+        nsrc, L, W = 1500, 16, 255
+        stride = O.round_up(L, 16)
+        src = stream(nsrc, L, stride, 77)
+        hdr = two_per_step(nsrc, W, key0=77)
+        rep = O.sw_encode(src, hdr, L)
+        rng = np.random.default_rng(77)
+        sp = (rng.random(nsrc) >= 0.2).astype(np.uint8)
+        rp = (rng.random(len(hdr)) >= 0.2).astype(np.uint8)
+        for entries in (0, 4096):
+            if entries:
+                c.set_tuning("sw_log_entries", entries)
+            check_vs_oracle(c, src, sp, rep, rp, hdr, L)
+    finally:
+        c.close()
+
+
+def test_sw_decode_async_error_flags():
+    """Asynchronous decodes raise their errors where the caller can read them
+    (fecgpu_sw_decode_errors): with "sw_log_entries" = 16
+    the long systems overflow and SW_ERR_CAPACITY is set (the flags clear on
+    read); a reversed header list raises SW_ERR_HEADER; a clean call raises
+    nothing."""
+    c = fecgpu.Context()
+    try:
+        nsrc, L, k, W = 2000, 32, 2, 64
+        stride = O.round_up(L, 16)
+        src = stream(nsrc, L, stride, 8)
+        hdr = hdr_array(N.sw_schedule(nsrc, k, W, key0=8, dt=15))
+        rep = O.sw_encode(src, hdr, L)
+        rng = np.random.default_rng(8)
+        sp = (rng.random(nsrc) >= 0.2).astype(np.uint8)
+        rp = np.ones(len(hdr), np.uint8)
+        od, ost, on = oracle_decode(src, sp, rep, rp, hdr, L)
+
+        def run(h):
+            d = src.copy()
+            d[sp == 0] = 0xAB
+            d_src = torch.from_numpy(d).cuda()
+            d_st = torch.zeros(nsrc, dtype=torch.uint8, device="cuda")
+            assert c.sw_decode_device(d_src, torch.from_numpy(sp).cuda(), torch.from_numpy(rep).cuda(),
+                                      torch.from_numpy(rp).cuda(), torch.from_numpy(h.view(np.uint8).copy()).cuda(),
+                                      d_st, nsrc=nsrc, nrep=len(h), sym_len=L, stride=stride) == 0
+            return d_src, d_st
+
+        assert c.sw_decode_errors() == 0
+        c.set_tuning("sw_log_entries", 16)
+        run(hdr)
+        assert c.sw_decode_errors() == fecgpu.SW_ERR_CAPACITY
+        assert c.sw_decode_errors() == 0
+        c.set_tuning("sw_log_entries", 0)   # automatic: grown past the overflow
+        d_src, d_st = run(hdr)
+        assert c.sw_decode_errors() == 0
+        assert np.array_equal(d_st.cpu().numpy(), ost)
+        assert np.array_equal(d_src.cpu().numpy()[:, :L], od[:, :L])
+        run(hdr[::-1].copy())
+        assert c.sw_decode_errors() == fecgpu.SW_ERR_HEADER
+    finally:
+        c.close()
+
+
 def test_sw_decode_host_pointers_and_args(ctx):
     nsrc, L, stride = 200, 40, 48
     src = stream(nsrc, L, stride, 29)
