@@ -253,10 +253,15 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd).returncode
 
 
-# extra configs timed by the default one-GPU run: config ->
-# (steps, warmup); cfg3 warms up longer (its first ~10 calls run slow while the
-# clocks and TLBs settle)
-EXTRA_CONFIGS = {3: (10, 10), 4: (5, 2), 7: (50, 10)}
+# extra configs timed by the default run:
+# config -> (steps, warmup); cfg3 warms up longer (its first ~10 calls run slow
+# while the clocks and TLBs settle).  One GPU: configs 3, 4, 5
+# (host buffers, PCIe-inclusive: bound "pcie", never the headline) and 7.  N
+# ranks: the device-resident configs, each rank on its own window shard (cfg4:
+# 131,072 windows per rank, the 1M windows of BASELINE config 4 at N = 8) with
+# the digest gathered over RCCL.
+EXTRA_CONFIGS = {3: (10, 10), 4: (5, 2), 5: (10, 2), 7: (50, 10)}
+EXTRA_CONFIGS_MULTI = (3, 4, 7)
 
 
 def make_ctx(args):
@@ -317,6 +322,13 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
     alg = batch.algorithmic_bytes()       # {'encode': B, 'decode': B} per launch
 
     log(f"{cfg.name}: warmup {warmup}")
+    if cfg.scheme == "sw":
+        # one synchronous decode first: it sizes the long-system log for this
+        # stream (the asynchronous timed calls never retry), and any error it
+        # cannot fix is raised here
+        batch.encode(ctx)
+        batch.decode(ctx, sync=True)
+        ctx.sw_decode_errors()  # start the timed calls with clear flags
     for _ in range(warmup):
         batch.encode(ctx)
         batch.decode(ctx)
@@ -380,11 +392,18 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
                        "wall_ms_per_call": round(wall, 4),
                        "what": "fecgpu_sw_decode_device calls back to back, no encode in between"}
         log(f"{cfg.name}: decode only {decode_only['ms_per_call']:.4f} ms per call")
+    # error flags of every asynchronous decode timed above (a long system left
+    # undecoded by a full operation log would have done less work): any flag
+    # fails the line
+    async_errors = ctx.sw_decode_errors() if cfg.scheme == "sw" else None
     elapsed, tot = shard.reduce_run(elapsed, src_bytes, dev if args.dist_backend == "nccl" else None)
     total_src = float(tot) * steps
     value = total_src / elapsed / 1e9
 
     verify = None if args.no_verify else batch.verify(ctx, w0)
+    if async_errors:
+        log(f"{cfg.name}: asynchronous decodes raised error flags {async_errors:#x}")
+        verify = dict(verify or {}, ok=False, async_error_flags=async_errors)
     log(f"{cfg.name}: verify: {verify}")
     # run digest of every rank's encoded windows, gathered over RCCL (8 B per
     # rank over xGMI: the path's only collective, outside the timed region)
@@ -404,7 +423,7 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
                             and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
                             else (None, None))
     cpu = None
-    if args.cpu_seconds > 0 and world == 1:
+    if args.cpu_seconds > 0 and world == 1 and not cfg.host:  # cfg5's codec and shape are cfg2's
         log(f"{cfg.name}: cpu baseline")
         cpu = (cpu_baseline_sw(cfg, args.cpu_seconds, args.cpu_threads) if cfg.scheme == "sw" else
                cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads))
@@ -467,6 +486,7 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
         },
         "cpu_baseline": cpu,
         **({"decode_only": decode_only} if decode_only else {}),
+        **({"async_error_flags": async_errors} if async_errors is not None else {}),
         "verify": verify,
         "digest": None if digest is None else f"{digest:016x}",
     }
@@ -509,9 +529,11 @@ def main():
     # the default one-GPU run also times the other single-GPU configs in this
     # process (each on its own batch, freed after), under "configs"; the
     # headline line above is config 2's as before
-    if world == 1 and args.extra_configs and args.config == 2 and not args.nwin:
+    if args.extra_configs and args.config == 2 and not args.nwin:
         extras = {}
         for cid, (st, wu) in EXTRA_CONFIGS.items():
+            if world > 1 and cid not in EXTRA_CONFIGS_MULTI:
+                continue
             try:
                 sub = run_config(cid, args, rank, world, dev, ctx, st, wu, 0)
             except Exception as exc:  # keep the headline line; report the failure
@@ -519,12 +541,16 @@ def main():
                 extras[f"cfg{cid}"] = {"error": repr(exc)}
                 ok = False
                 continue
+            if sub is None:  # ranks other than 0
+                continue
             ok = ok and (sub["verify"] is None or sub["verify"].get("ok", False))
-            extras[f"cfg{cid}"] = {k: sub[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup",
+            extras[f"cfg{cid}"] = {k: sub[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup",
                                                        "config", "kernels_ms", "roofline", "roofline_other",
-                                                       "cpu_baseline", "verify", "digest", "decode_only")
+                                                       "cpu_baseline", "verify", "digest", "decode_only",
+                                                       "async_error_flags", "value_per_gpu")
                                  if k in sub}
-        line["configs"] = extras
+        if line is not None:
+            line["configs"] = extras
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
