@@ -173,6 +173,12 @@ struct fecgpu_ctx {
     std::map<int, std::vector<std::pair<void *, size_t>>> sw_scratch;
     std::map<int, hipEvent_t> sw_event;
     std::map<int, SwSticky *> sw_sticky;  // asynchronous decodes' error flags, per device
+    struct LbState {
+        void *mem = nullptr;
+        uint64_t nchunk = 0;
+        uint32_t epoch = 0;
+    };
+    std::map<int, LbState> sw_lb;  // fused decode plan's look-back state, per device
     void *sw_host = nullptr;  // pinned staging of sliding-window decodes (ctx_sw_host)
     size_t sw_host_bytes = 0;
     // codes with k + r > 64: parity rows on each device, by (device, k, r, matrix, key, dt)
@@ -389,6 +395,10 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
     for (auto &kv : ctx->sw_sticky) {
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second);
+    }
+    for (auto &kv : ctx->sw_lb) {
+        (void)hipSetDevice(kv.first);
+        if (kv.second.mem) (void)hipFree(kv.second.mem);
     }
     for (auto &kv : ctx->wide_rows) {
         (void)hipSetDevice(std::get<0>(kv.first));
@@ -1193,6 +1203,34 @@ ssize_t ctx_sw_sticky(fecgpu_ctx *ctx, SwSticky **p) {
         w = static_cast<SwSticky *>(m);
     }
     *p = w;
+    return 0;
+}
+
+ssize_t ctx_sw_lookback(fecgpu_ctx *ctx, uint64_t nchunk, SwLookback *lb, uint32_t *epoch) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    auto &st = ctx->sw_lb[dev];
+    // layout: ticket (256 B), flags [cap], aggregates [cap], inclusive [cap]
+    auto bytes = [](uint64_t cap) { return 256 + cap * 4 + cap * 32; };
+    if (st.nchunk < nchunk || st.epoch >= (1u << 29)) {
+        const uint64_t cap = (std::max<uint64_t>(nchunk, std::max<uint64_t>(256, st.nchunk + st.nchunk / 2)) + 3) & ~3ull;
+        if (st.mem) {
+            HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+            HIP_TRY(hipFree(st.mem), "hipFree");
+            st.mem = nullptr;
+            st.nchunk = 0;
+        }
+        HIP_TRY(hipMalloc(&st.mem, bytes(cap)), "hipMalloc sw look-back");
+        HIP_TRY(hipMemset(st.mem, 0, bytes(cap)), "hipMemset sw look-back");
+        st.nchunk = cap;
+        st.epoch = 0;
+    }
+    uint8_t *m = static_cast<uint8_t *>(st.mem);
+    lb->ticket = reinterpret_cast<uint32_t *>(m);
+    lb->flag = reinterpret_cast<uint32_t *>(m + 256);
+    lb->agg = reinterpret_cast<uint4 *>(m + 256 + st.nchunk * 4);
+    lb->inc = lb->agg + st.nchunk;
+    *epoch = ++st.epoch;
     return 0;
 }
 

@@ -291,12 +291,18 @@ constexpr int kSwSmallE = 64;   // unknowns of a small system
 constexpr int kSwSmallP = 96;   // equations (received repairs) of a small system
 constexpr int kSwRows = 256;    // long systems: row slots (more rows alive at one column are reduced
                                 // to a basis first: they span at most 255 columns, fec_swdec.hip)
-constexpr int kSwChunk = 4096;  // sources per planning chunk
+constexpr int kSwChunk = 4096;  // sources per planning chunk (FECGPU_SWD_FUSED 0)
+constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
+#ifndef FECGPU_SWD_FUSED
+#define FECGPU_SWD_FUSED 1  // the decode plan as one look-back launch (sw_dec_plan_kernel) instead of
+                            // a memset and five passes
+#endif
 
 // SwDecCtr::err / SwSticky::err bits
 constexpr uint32_t kSwErrHeader = 1u;    // a bad or unordered header: the call recovers nothing
 constexpr uint32_t kSwErrCapacity = 2u;  // a long system's operation log (or the queue) did not fit:
                                          // that system stays lost (a larger log fixes it)
+constexpr uint32_t kSwErrInternal = 4u;  // the fused plan's look-back gave up (never expected)
 struct SwDecCtr {  // per call, zeroed before the first kernel
     uint32_t nlost, wmax, maxp, err;   // err: kSwErr* bits
     uint32_t nmid, nlong, npiv, recovered;  // queued mid / long systems, pivot rows, recovered
@@ -362,6 +368,13 @@ struct SwDecArgs {
     uint8_t *src;                              // the sources (replay writes recovered ones)
     const uint8_t *synd;                       // syndrome rows (g * stride)
     SwSticky *sticky;                          // nullable: asynchronous calls also raise errors here
+    // fused plan (FECGPU_SWD_FUSED): look-back state of the chunks, kept across
+    // calls (ctx_sw_lookback): flags (epoch << 2 | state), aggregates, inclusive
+    // prefixes, and the ticket counter that orders the chunks
+    uint32_t *lb_flag;
+    uint4 *lb_agg, *lb_inc;
+    uint32_t *lb_ticket;  // [0] next chunk, [1] blocks done
+    uint32_t epoch;
 };
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s);    // statuses, lost list, systems
 hipError_t launch_sw_dec_long(const SwDecArgs &a, hipStream_t s);    // long systems: logs, syndrome jobs
@@ -406,6 +419,17 @@ ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p);
 ssize_t ctx_sw_host(fecgpu_ctx *ctx, size_t bytes, void **p);
 // the current device's sticky error word of asynchronous decodes (allocated zeroed)
 ssize_t ctx_sw_sticky(fecgpu_ctx *ctx, SwSticky **p);
+// Look-back state of the fused decode plan on the current device for nchunk
+// chunks (zeroed when first allocated or grown): *epoch is this call's epoch
+// (never 0; flags of earlier calls never match it).  ticket[0] hands out the
+// chunks, ticket[1] counts finished blocks; the last block resets both, so
+// every launch starts at 0.  Calls on one ctx are ordered (ctx_sw_begin), so
+// one state per device serves them all.
+struct SwLookback {
+    uint32_t *flag, *ticket;
+    uint4 *agg, *inc;
+};
+ssize_t ctx_sw_lookback(fecgpu_ctx *ctx, uint64_t nchunk, SwLookback *lb, uint32_t *epoch);
 // waits until the current device's sliding-window calls issued so far have finished
 ssize_t ctx_sw_wait(fecgpu_ctx *ctx);
 ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);

@@ -301,7 +301,18 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.synd = static_cast<const uint8_t *>(psyn);
     a.sticky = sticky;
 
+#if FECGPU_SWD_FUSED
+    {  // the plan kernel writes the counters itself: nothing to clear
+        SwLookback lb{};
+        RC_TRY(ctx_sw_lookback(ctx, (nsrc + kSwPlanChunk - 1) / kSwPlanChunk, &lb, &a.epoch));
+        a.lb_flag = lb.flag;
+        a.lb_agg = lb.agg;
+        a.lb_inc = lb.inc;
+        a.lb_ticket = lb.ticket;
+    }
+#else
     SW_TRY(hipMemsetAsync(a.ctr, 0, L.o_chunk - L.o_ctr, s), "sliding-window decode counters");
+#endif
     SW_TRY(launch_sw_dec_plan(a, s), "sliding-window decode plan launch");
     SW_TRY(launch_sw_dec_long(a, s), "sliding-window long-system plan launch");
     const uint32_t ncol = (S + 15u) >> 4;

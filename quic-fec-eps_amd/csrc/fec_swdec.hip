@@ -624,11 +624,7 @@ __device__ __forceinline__ void block_counts(const SwDecArgs &a, uint32_t rec, u
 // zeroes them); drawn here, every lane of a wave draws one, instead of a
 // wave per system drawing its few equations' on as many lanes.  The
 // long-system pass draws its own rows again (and overwrites these).
-__global__ __launch_bounds__(kBlock) void sw_dec_coef_kernel(SwDecArgs a) {
-    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= a.nrep || (a.ctr->err & 1u) || !a.rep_present[t]) return;
-    const fecgpu_sw_repair h = a.hdr[t];
-    if (!holds_any(a, h)) return;
+__device__ __forceinline__ void draw_row(const SwDecArgs &a, uint64_t t, const fecgpu_sw_repair &h) {
     uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + t * kSwCoefPitch);
     Tinymt32 st;
     tinymt32_init(st, h.key);
@@ -648,6 +644,322 @@ __global__ __launch_bounds__(kBlock) void sw_dec_coef_kernel(SwDecArgs a) {
         }
     }
     if (h.nss & 3) cc[h.nss >> 2] = word;
+}
+
+__global__ __launch_bounds__(kBlock) void sw_dec_coef_kernel(SwDecArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= a.nrep || (a.ctr->err & 1u) || !a.rep_present[t]) return;
+    const fecgpu_sw_repair h = a.hdr[t];
+    if (!holds_any(a, h)) return;
+    draw_row(a, t, h);
+}
+
+// ======================================================= fused plan ===
+// One launch for the whole plan (FECGPU_SWD_FUSED): a block per chunk of
+// kPlanChunk sources, in ticket order, chained by a decoupled look-back over
+// (lost sources, farthest reach, repairs, widest window | error bits) so no
+// pass waits for a separate scan.  Per chunk: its repairs' header range (the
+// headers are in fss order; every block also checks its share of headers, so a
+// bad or unordered list raises kSwErrHeader and the later kernels stand down),
+// reach / repair counts in LDS, statuses, the lost list with its prefix-max
+// reach, rank / repfirst, empty job slots, and the RFC 8681 coefficient rows of
+// the chunk's received repairs that hold a lost source (a 255-source halo of
+// arrival flags past the chunk answers that locally).  The last chunk writes
+// the call's counters, so nothing is cleared before the launch.
+constexpr int kPlanChunk = kSwPlanChunk;
+constexpr int kPlanPer = kPlanChunk / kBlock;  // sources per thread
+constexpr int kPlanHalo = 256;                 // >= kSwMaxWindow
+static_assert(kPlanPer == 8, "the per-thread source loads are 8 bytes");
+constexpr uint32_t kLbAgg = 1u, kLbInc = 2u;
+
+struct LbRec {  // lost sources, max reach, repairs, widest window | error bits << 16
+    uint32_t lost, reach, rep, wme;
+};
+__device__ __forceinline__ LbRec lb_join(const LbRec &x, const LbRec &y) {  // x before y
+    LbRec r;
+    r.lost = x.lost + y.lost;
+    r.reach = max(x.reach, y.reach);
+    r.rep = x.rep + y.rep;
+    r.wme = max(x.wme & 0xFFFFu, y.wme & 0xFFFFu) | ((x.wme | y.wme) & 0xFFFF0000u);
+    return r;
+}
+__device__ __forceinline__ uint32_t lb_flag_load(const uint32_t *f) {
+    return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_publish(const SwDecArgs &a, uint32_t c, const LbRec &r, uint32_t state) {
+    uint4 *dst = (state == kLbInc ? a.lb_inc : a.lb_agg) + c;
+    __hip_atomic_store(&dst->x, r.lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&dst->y, r.reach, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&dst->z, r.rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&dst->w, r.wme, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.lb_flag[c], (a.epoch << 2) | state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ LbRec lb_read(const uint4 *src) {
+    LbRec r;
+    r.lost = __hip_atomic_load(&src->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r.reach = __hip_atomic_load(&src->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r.rep = __hip_atomic_load(&src->z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r.wme = __hip_atomic_load(&src->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return r;
+}
+
+__global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
+    __shared__ uint32_t s_reach[kPlanChunk], s_rcnt[kPlanChunk];
+    __shared__ uint32_t s_bits[(kPlanChunk + kPlanHalo) / 32];      // lost flags, chunk + halo
+    __shared__ uint32_t s_wpfx[(kPlanChunk + kPlanHalo) / 32 + 1];  // lost before each word
+    __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64], s_r[kBlock / 64], s_w[kBlock / 64];
+    __shared__ uint32_t s_chunk, s_bad;
+    __shared__ uint64_t s_t0, s_t1;
+    __shared__ LbRec s_excl;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t nch = (uint32_t)((a.nsrc + kPlanChunk - 1) / kPlanChunk);
+    if (tid == 0) {
+        // chunks in dispatch order, so the look-back never waits on a block not
+        // yet running (the counter starts every launch at 0; modulo: a counter
+        // left behind by an aborted launch still hands out each chunk once)
+        s_chunk = atomicAdd(&a.lb_ticket[0], 1u) % nch;
+        s_bad = 0;
+    }
+    for (int i = tid; i < kPlanChunk; i += kBlock) {
+        s_reach[i] = 0;
+        s_rcnt[i] = 0;
+    }
+    __syncthreads();
+    const uint32_t c = s_chunk;
+    const uint64_t i0 = (uint64_t)c * kPlanChunk, i1 = min(i0 + kPlanChunk, a.nsrc);
+    // the chunk's repairs: fss in [i0, i1) (wave 0 / wave 1 search in parallel)
+    if (wave < 2) {
+        const uint64_t key = wave == 0 ? i0 : i1;
+        const uint64_t t = (wave == 1 && i1 == a.nsrc) ? a.nrep : wave_lower_bound(a.hdr, 0, a.nrep, key, lane);
+        if (lane == 0) (wave == 0 ? s_t0 : s_t1) = t;
+    }
+    // this block's share of the header checks, and of emptying the syndrome job
+    // slots (every slot, whatever the headers hold: the syndrome pass walks them all)
+    bool bad = false;
+    {
+        const uint64_t h0 = (uint64_t)c * a.nrep / nch, h1 = (uint64_t)(c + 1) * a.nrep / nch;
+        CombJob E{};
+        E.xor_off = kNoXor;
+        for (uint64_t t = h0 + tid; t < h1; t += kBlock) {
+            a.syn_jobs[t] = E;
+            const fecgpu_sw_repair h = a.hdr[t];
+            bad |= h.nss < 1 || h.nss > kSwMaxWindow || h.dt > 15 || h.fss > a.nsrc || a.nsrc - h.fss < h.nss;
+            if (t > 0 && a.hdr[t - 1].fss > h.fss) bad = true;
+        }
+    }
+    if (__ballot(bad) && lane == 0) s_bad = 1;
+    __syncthreads();
+    const uint64_t t0 = s_t0, t1 = max(s_t0, s_t1);
+    // reach / repair counts of the chunk's sources
+    uint32_t wm = 0;
+    for (uint64_t t = t0 + tid; t < t1; t += kBlock) {
+        const fecgpu_sw_repair h = a.hdr[t];
+        if (h.fss >= i0 && h.fss < i1 && h.nss >= 1 && h.nss <= kSwMaxWindow) {
+            atomicAdd(&s_rcnt[h.fss - i0], 1u);
+            if (a.rep_present[t]) {
+                wm = max(wm, (uint32_t)h.nss);
+                atomicMax(&s_reach[h.fss - i0], (uint32_t)(h.fss + h.nss));
+            }
+        }
+    }
+    // arrival flags: 8 sources per thread, and the halo past the chunk
+    const uint32_t n = (uint32_t)(i1 - i0), my0 = (uint32_t)tid * kPlanPer;
+    uint32_t lostm = 0;  // bit j: source i0 + my0 + j lost
+    // 8-byte flag loads / status stores where both arrays allow (caller pointers)
+    const bool vec = ((reinterpret_cast<uintptr_t>(a.src_present) | reinterpret_cast<uintptr_t>(a.stat)) & 7u) == 0;
+    if (vec && my0 + kPlanPer <= n) {
+        const uint2 pv = *reinterpret_cast<const uint2 *>(a.src_present + i0 + my0);
+        uint2 st;
+        for (int j = 0; j < 8; j++) {
+            const uint32_t byte = ((j < 4 ? pv.x : pv.y) >> (8 * (j & 3))) & 0xFFu;
+            lostm |= (byte == 0 ? 1u : 0u) << j;
+        }
+        st.x = ((lostm & 1u) ? 1u : 0u) | ((lostm & 2u) ? 1u << 8 : 0u) | ((lostm & 4u) ? 1u << 16 : 0u) |
+               ((lostm & 8u) ? 1u << 24 : 0u);
+        st.y = ((lostm & 16u) ? 1u : 0u) | ((lostm & 32u) ? 1u << 8 : 0u) | ((lostm & 64u) ? 1u << 16 : 0u) |
+               ((lostm & 128u) ? 1u << 24 : 0u);
+        *reinterpret_cast<uint2 *>(a.stat + i0 + my0) = st;  // FECGPU_STATUS_UNRECOVERABLE = 1 when lost
+    } else {
+        for (uint32_t j = 0; my0 + j < n && j < kPlanPer; j++) {
+            const bool lost = a.src_present[i0 + my0 + j] == 0;
+            lostm |= (lost ? 1u : 0u) << j;
+            a.stat[i0 + my0 + j] = lost ? FECGPU_STATUS_UNRECOVERABLE : FECGPU_STATUS_OK;
+        }
+    }
+    {  // the chunk's bits: 4 threads per word
+        const uint32_t sh = (uint32_t)(tid & 3) * 8u;
+        uint32_t wv = lostm << sh;
+        wv |= __shfl_xor(wv, 1);
+        wv |= __shfl_xor(wv, 2);
+        if ((tid & 3) == 0) s_bits[tid >> 2] = wv;
+    }
+    if (tid < kPlanHalo / 32) {  // halo words
+        uint32_t wv = 0;
+        for (int j = 0; j < 32; j++) {
+            const uint64_t i = i1 + (uint64_t)tid * 32 + j;
+            if (i < a.nsrc && a.src_present[i] == 0) wv |= 1u << j;
+        }
+        // a short last chunk: its halo follows its last source directly
+        if (n == (uint32_t)kPlanChunk) s_bits[kPlanChunk / 32 + tid] = wv;
+    }
+    if (n < (uint32_t)kPlanChunk) {  // last chunk (nothing past nsrc): clear the tail words
+        for (uint32_t w = tid; w < (kPlanChunk + kPlanHalo) / 32; w += kBlock)
+            if (w * 32 >= ((n + 31) & ~31u)) s_bits[w] = 0;
+    }
+    __syncthreads();
+    // per thread: its 8 sources' lost count, max reach, repair count
+    uint32_t cnt = __popc(lostm), tm = 0, tr = 0;
+    for (int j = 0; j < kPlanPer; j++)
+        if (my0 + j < n) {
+            tm = max(tm, s_reach[my0 + j]);
+            tr += s_rcnt[my0 + j];
+        }
+    uint32_t ic = cnt, im = tm, ir = tr;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(ic, o), ym = __shfl_up(im, o), yr = __shfl_up(ir, o);
+        if (lane >= o) {
+            ic += y;
+            im = max(im, ym);
+            ir += yr;
+        }
+    }
+    uint32_t em = __shfl_up(im, 1);
+    if (lane == 0) em = 0;
+    wm = wave_max(wm);
+    if (lane == 63) {
+        s_c[wave] = ic;
+        s_m[wave] = im;
+        s_r[wave] = ir;
+    }
+    if (lane == 0) s_w[wave] = wm;
+    // lost before each word of the chunk + halo (the coefficient pass's window test)
+    if (wave == 0) {
+        constexpr int NW = (kPlanChunk + kPlanHalo) / 32;
+        uint32_t carry = 0;
+        for (int w0 = 0; w0 < NW; w0 += 64) {
+            const uint32_t v = w0 + lane < NW ? __popc(s_bits[w0 + lane]) : 0u;
+            uint32_t x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            if (w0 + lane < NW) s_wpfx[w0 + lane] = carry + x - v;
+            carry += __shfl(x, 63);
+        }
+        if (lane == 0) s_wpfx[NW] = carry;
+    }
+    __syncthreads();
+    uint32_t wc = 0, wmx = 0, wr = 0;
+    for (int w = 0; w < wave; w++) {
+        wc += s_c[w];
+        wmx = max(wmx, s_m[w]);
+        wr += s_r[w];
+    }
+    if (tid == 0) {
+        LbRec agg{0, 0, 0, 0};
+        for (int w = 0; w < kBlock / 64; w++) {
+            agg.lost += s_c[w];
+            agg.reach = max(agg.reach, s_m[w]);
+            agg.rep += s_r[w];
+            agg.wme = max(agg.wme, s_w[w]);
+        }
+        if (s_bad) agg.wme |= kSwErrHeader << 16;
+        LbRec ex{0, 0, 0, 0};
+        if (c == 0) {
+            lb_publish(a, c, agg, kLbInc);
+        } else {
+            lb_publish(a, c, agg, kLbAgg);
+            uint32_t spins = 0;
+            for (int64_t q = (int64_t)c - 1; q >= 0;) {
+                const uint32_t f = lb_flag_load(&a.lb_flag[q]);
+                if ((f >> 2) != a.epoch || (f & 3u) == 0) {
+                    // bounded: a predecessor that never publishes (which the
+                    // dispatch order rules out) ends as an error, not a hang
+                    if (++spins == (1u << 24)) {
+                        ex.wme |= kSwErrInternal << 16;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                const bool inc = (f & 3u) == kLbInc;
+                ex = lb_join(lb_read(inc ? a.lb_inc + q : a.lb_agg + q), ex);
+                if (inc) break;
+                q--;
+            }
+            lb_publish(a, c, lb_join(ex, agg), kLbInc);
+        }
+        s_excl = ex;
+        if (c == nch - 1) {  // the call's counters (nothing was cleared before the launch)
+            const LbRec tot = lb_join(ex, agg);
+            SwDecCtr z{};
+            z.nlost = tot.lost;
+            z.wmax = tot.wme & 0xFFFFu;
+            z.err = tot.wme >> 16;
+            *a.ctr = z;
+            if (z.err && a.sticky) atomicOr(&a.sticky->err, z.err);
+        }
+    }
+    __syncthreads();
+    const LbRec ex = s_excl;
+    // lost list, rank / repfirst (as sw_dec_lost_kernel)
+    uint32_t off = ex.lost + wc + ic - cnt;
+    uint32_t run = max(max(ex.reach, wmx), em);
+    uint32_t repc = ex.rep + wr + ir - tr;
+    CombJob E{};
+    E.xor_off = kNoXor;
+    uint32_t rk[kPlanPer], rf[kPlanPer];
+#pragma unroll
+    for (int j = 0; j < kPlanPer; j++) {
+        rk[j] = off;
+        rf[j] = repc;
+        if (my0 + j < n) {
+            const uint64_t i = i0 + my0 + j;
+            run = max(run, s_reach[my0 + j]);
+            repc += s_rcnt[my0 + j];
+            if ((lostm >> j) & 1u) {
+                a.lost[off] = (uint32_t)i;
+                a.reachL[off] = run;
+                a.sol_jobs[off] = E;
+                off++;
+            }
+        }
+    }
+    if (my0 + kPlanPer <= n) {
+        uint4 *rkp = reinterpret_cast<uint4 *>(a.reach + i0 + my0), *rfp = reinterpret_cast<uint4 *>(a.rcnt + i0 + my0);
+        rkp[0] = make_uint4(rk[0], rk[1], rk[2], rk[3]);
+        rkp[1] = make_uint4(rk[4], rk[5], rk[6], rk[7]);
+        rfp[0] = make_uint4(rf[0], rf[1], rf[2], rf[3]);
+        rfp[1] = make_uint4(rf[4], rf[5], rf[6], rf[7]);
+    } else {
+        for (uint32_t j = 0; my0 + j < n && j < kPlanPer; j++) {
+            a.reach[i0 + my0 + j] = rk[j];
+            a.rcnt[i0 + my0 + j] = rf[j];
+        }
+    }
+    if (my0 <= n && n <= my0 + kPlanPer && i1 == a.nsrc) {  // the thread holding the end
+        a.reach[a.nsrc] = off;
+        a.rcnt[a.nsrc] = repc;
+    }
+    // coefficient rows of the chunk's received repairs whose window holds a lost source
+    for (uint64_t t = t0 + tid; t < t1; t += kBlock) {
+        if (!a.rep_present[t]) continue;
+        const fecgpu_sw_repair h = a.hdr[t];
+        if (h.fss < i0 || h.fss >= i1 || h.nss < 1 || h.nss > kSwMaxWindow || a.nsrc - h.fss < h.nss) continue;
+        const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
+        const auto before = [&](uint32_t j) {
+            return s_wpfx[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u));
+        };
+        if (before(hi) > before(lo)) draw_row(a, t, h);
+    }
+    // the last block out resets the tickets for the next launch
+    __syncthreads();
+    if (tid == 0 && atomicAdd(&a.lb_ticket[1], 1u) == nch - 1) {
+        atomicExch(&a.lb_ticket[0], 0u);
+        atomicExch(&a.lb_ticket[1], 0u);
+    }
 }
 
 // A wave per lost source; the waves at a system start find its extent and
@@ -1282,6 +1594,11 @@ int cu_count() {
 }  // namespace
 
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
+#if FECGPU_SWD_FUSED
+    hipLaunchKernelGGL(sw_dec_plan_kernel, dim3((unsigned)((a.nsrc + kPlanChunk - 1) / kPlanChunk)), dim3(kBlock), 0, s,
+                       a);
+    if (a.nrep) {
+#else
     if (a.nrep) hipLaunchKernelGGL(sw_dec_hdr_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(sw_dec_count_kernel, dim3(a.nchunk), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(sw_dec_scan_kernel, dim3(1), dim3(1024), 0, s, a.chunk, a.nchunk, 3, 1, &a.ctr->nlost);
@@ -1289,6 +1606,7 @@ hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
     if (a.nrep) {
 #if FECGPU_SWD_COEF
         hipLaunchKernelGGL(sw_dec_coef_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+#endif
 #endif
         // a wave per lost source at most; persistent beyond what fits the chip
         const uint64_t want = (a.nsrc + kBlock / 64 - 1) / (kBlock / 64);
