@@ -347,9 +347,11 @@ struct SwDecArgs {
                                                // then their exclusive scans
     uint32_t *lost, *reachL;                   // [nsrc] lost sources; prefix max of reach at each
     SwDecCtr *ctr;
-    CombJob *syn_jobs;                         // [nrep] syndrome job of repair t (empty unless needed)
-    uint64_t *syn_outs;                        // [nrep]
-    uint8_t *coef;                             // [nrep][kSwCoefPitch]: repair t's syndrome coefficients
+    CombJob *syn_jobs;                         // [nrep] syndrome job of repair t (empty unless needed),
+                                               // then [nsrc] (fused plan) the one-unknown systems'
+                                               // jobs by lost index
+    uint64_t *syn_outs;                        // [nrep + nsrc]
+    uint8_t *coef;                             // [nrep + nsrc][kSwCoefPitch]: syndrome coefficients
     CombJob *sol_jobs;                         // [nsrc] solve jobs of a small system in its unknowns' slots
     uint64_t *sol_outs;                        // [nsrc] their outputs (unknown x + d)
     uint8_t *sol_coef;                         // [nrep * kSwSmallE] coefficients (64 B per repair)
@@ -375,6 +377,8 @@ struct SwDecArgs {
     uint4 *lb_agg, *lb_inc;
     uint32_t *lb_ticket;  // [0] next chunk, [1] blocks done
     uint32_t epoch;
+    uint8_t *lkind;       // [nsrc] per lost index, from the fused plan: 0 member of a larger
+                          // system, 1 recovered alone, 2 a larger system's first, 3 alone, lost
 };
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s);    // statuses, lost list, systems
 hipError_t launch_sw_dec_long(const SwDecArgs &a, hipStream_t s);    // long systems: logs, syndrome jobs

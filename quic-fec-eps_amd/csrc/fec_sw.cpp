@@ -208,7 +208,7 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // bookkeeping).
 struct DecBlock {
     size_t o_reach, o_rcnt, o_chunk, o_lost, o_reachL, o_ctr, o_synj, o_syno, o_coef, o_solj, o_solo, o_solc,
-        o_long, o_mid, o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, total;
+        o_long, o_mid, o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, o_lkind, total;
     uint64_t long_cap, piv_cap;
 };
 DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
@@ -229,9 +229,12 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
     L.o_chunk = take(3 * nchunk * 4);
     L.o_lost = take(nsrc * 4);
     L.o_reachL = take(nsrc * 4);
-    L.o_synj = take(nrep * sizeof(CombJob));
-    L.o_syno = take(nrep * 8);
-    L.o_coef = take(nrep * (size_t)kSwCoefPitch);
+    // syndrome slots: one per repair, and (fused plan) one per lost source for
+    // the one-unknown systems the plan solves
+    const uint64_t nsyn = nrep + (FECGPU_SWD_FUSED ? nsrc : 0);
+    L.o_synj = take(nsyn * sizeof(CombJob));
+    L.o_syno = take(nsyn * 8);
+    L.o_coef = take(nsyn * (size_t)kSwCoefPitch);
     L.o_solj = take(nsrc * sizeof(CombJob));
     L.o_solo = take(nsrc * 8);
     L.o_solc = take(nrep * (size_t)kSwSmallE);
@@ -242,6 +245,7 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
     L.o_colpiv = take(nsrc * 4);
     L.o_pivhi = take(L.piv_cap * 4);
     L.o_pivt = take(L.piv_cap * 4);
+    L.o_lkind = take(FECGPU_SWD_FUSED ? nsrc : 0);
     L.total = o;
     return L;
 }
@@ -295,6 +299,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.colpiv = reinterpret_cast<uint32_t *>(b + L.o_colpiv);
     a.pivhi = reinterpret_cast<uint32_t *>(b + L.o_pivhi);
     a.pivt = reinterpret_cast<uint32_t *>(b + L.o_pivt);
+    a.lkind = b + L.o_lkind;
     a.pivdata = static_cast<uint8_t *>(ppiv);
     a.piv_cap = L.piv_cap;
     a.src = src;
@@ -326,6 +331,10 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     sa.out_base = static_cast<uint8_t *>(psyn);
     sa.xor_base = rep;
     sa.njobs = nrep;  // a slot per repair; the needed ones filled by their systems
+#if FECGPU_SWD_FUSED
+    sa.extra = &a.ctr->nlost;  // then a slot per lost source: the plan's one-unknown systems
+    sa.extra_max = nsrc;
+#endif
     sa.ncol = ncol;
     sa.stride = stride;
     sa.nin_max = kSwMaxWindow;

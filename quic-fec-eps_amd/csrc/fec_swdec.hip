@@ -672,8 +672,10 @@ constexpr int kPlanHalo = 256;                 // >= kSwMaxWindow
 static_assert(kPlanPer == 8, "the per-thread source loads are 8 bytes");
 constexpr uint32_t kLbAgg = 1u, kLbInc = 2u;
 
-struct LbRec {  // lost sources, max reach, repairs, widest window | error bits << 16
-    uint32_t lost, reach, rep, wme;
+// lost sources, max reach, repairs, widest window | error bits << 16, and the
+// reach at the last lost source (prefix max of reach up to it: its reachL)
+struct LbRec {
+    uint32_t lost, reach, rep, wme, L;
 };
 __device__ __forceinline__ LbRec lb_join(const LbRec &x, const LbRec &y) {  // x before y
     LbRec r;
@@ -681,36 +683,67 @@ __device__ __forceinline__ LbRec lb_join(const LbRec &x, const LbRec &y) {  // x
     r.reach = max(x.reach, y.reach);
     r.rep = x.rep + y.rep;
     r.wme = max(x.wme & 0xFFFFu, y.wme & 0xFFFFu) | ((x.wme | y.wme) & 0xFFFF0000u);
+    r.L = y.lost ? max(x.reach, y.L) : x.L;
     return r;
 }
 __device__ __forceinline__ uint32_t lb_flag_load(const uint32_t *f) {
     return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
 }
+// records are two uint4 per chunk (lb_agg / lb_inc [2 * chunk])
 __device__ __forceinline__ void lb_publish(const SwDecArgs &a, uint32_t c, const LbRec &r, uint32_t state) {
-    uint4 *dst = (state == kLbInc ? a.lb_inc : a.lb_agg) + c;
-    __hip_atomic_store(&dst->x, r.lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&dst->y, r.reach, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&dst->z, r.rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&dst->w, r.wme, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t *dst = reinterpret_cast<uint32_t *>((state == kLbInc ? a.lb_inc : a.lb_agg) + 2 * (size_t)c);
+    const uint32_t v[5] = {r.lost, r.reach, r.rep, r.wme, r.L};
+#pragma unroll
+    for (int i = 0; i < 5; i++) __hip_atomic_store(dst + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&a.lb_flag[c], (a.epoch << 2) | state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ LbRec lb_read(const uint4 *src) {
-    LbRec r;
-    r.lost = __hip_atomic_load(&src->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    r.reach = __hip_atomic_load(&src->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    r.rep = __hip_atomic_load(&src->z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    r.wme = __hip_atomic_load(&src->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return r;
+__device__ __forceinline__ LbRec lb_read(const uint4 *src2) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(src2);
+    uint32_t v[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) v[i] = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return LbRec{v[0], v[1], v[2], v[3], v[4]};
+}
+
+// One-unknown systems (most of them at low loss) are finished here too: the
+// lost source x at position i is alone in its system iff the reach of the
+// sources up to the previous lost source stops at or before i and its own
+// reach stops at or before the next lost source (the halo shows whether there
+// is one within 255 sources).  Its pivot is the first received repair t
+// holding it with a nonzero coefficient there (the small solver's choice), and
+// x = s_t / c: a combine job in syndrome slot nrep + (x's lost index) over t's
+// window with the coefficients times 1/c and t's row times 1/c (as
+// FECGPU_SWD_FUSE1).  lkind[x] tells the system pass what is left: 0 a member
+// of a larger system, 1 recovered here, 2 a larger system's first unknown,
+// 3 alone but undetermined.
+__device__ __forceinline__ uint8_t coef_at(const fecgpu_sw_repair &h, uint32_t j) {  // RFC 8681 coefficient j
+    Tinymt32 st;
+    tinymt32_init(st, h.key);
+    const uint32_t dt = h.dt;
+    uint32_t c = 0;
+    for (uint32_t q = 0; q <= j; q++) {
+        c = 0;
+        if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
+            do {
+                c = tinymt32_u32(st) & 0xFFu;
+            } while (c == 0);
+        }
+    }
+    return (uint8_t)c;
 }
 
 __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     __shared__ uint32_t s_reach[kPlanChunk], s_rcnt[kPlanChunk];
+    __shared__ uint32_t s_lpos[kPlanChunk], s_rl[kPlanChunk];  // per local lost source: position, reachL
+    __shared__ uint32_t s_rf[kPlanChunk + 1];                  // repfirst of the chunk's sources (and of i1)
+    __shared__ uint32_t s_rcb[kPlanHalo], s_rfb[kPlanHalo];    // repairs starting in [i0 - 256, i0), repfirst there
     __shared__ uint32_t s_bits[(kPlanChunk + kPlanHalo) / 32];      // lost flags, chunk + halo
     __shared__ uint32_t s_wpfx[(kPlanChunk + kPlanHalo) / 32 + 1];  // lost before each word
     __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64], s_r[kBlock / 64], s_w[kBlock / 64];
-    __shared__ uint32_t s_chunk, s_bad;
-    __shared__ uint64_t s_t0, s_t1;
-    __shared__ LbRec s_excl;
+    __shared__ uint32_t s_lh[kBlock / 64], s_lv[kBlock / 64];
+    __shared__ uint32_t s_chunk, s_bad, s_wmb;
+    __shared__ uint64_t s_t0, s_t1, s_tb;
+    __shared__ LbRec s_excl, s_agg;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t nch = (uint32_t)((a.nsrc + kPlanChunk - 1) / kPlanChunk);
     if (tid == 0) {
@@ -719,19 +752,23 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         // left behind by an aborted launch still hands out each chunk once)
         s_chunk = atomicAdd(&a.lb_ticket[0], 1u) % nch;
         s_bad = 0;
+        s_wmb = 0;
     }
     for (int i = tid; i < kPlanChunk; i += kBlock) {
         s_reach[i] = 0;
         s_rcnt[i] = 0;
     }
+    s_rcb[tid] = 0;
     __syncthreads();
     const uint32_t c = s_chunk;
     const uint64_t i0 = (uint64_t)c * kPlanChunk, i1 = min(i0 + kPlanChunk, a.nsrc);
-    // the chunk's repairs: fss in [i0, i1) (wave 0 / wave 1 search in parallel)
-    if (wave < 2) {
-        const uint64_t key = wave == 0 ? i0 : i1;
+    const uint64_t ib = i0 >= (uint64_t)kPlanHalo ? i0 - kPlanHalo : 0;  // back region [ib, i0)
+    // the chunk's repairs (fss in [i0, i1)) and those of the back region: three
+    // searches, a wave each
+    if (wave < 3) {
+        const uint64_t key = wave == 0 ? i0 : wave == 1 ? i1 : ib;
         const uint64_t t = (wave == 1 && i1 == a.nsrc) ? a.nrep : wave_lower_bound(a.hdr, 0, a.nrep, key, lane);
-        if (lane == 0) (wave == 0 ? s_t0 : s_t1) = t;
+        if (lane == 0) (wave == 0 ? s_t0 : wave == 1 ? s_t1 : s_tb) = t;
     }
     // this block's share of the header checks, and of emptying the syndrome job
     // slots (every slot, whatever the headers hold: the syndrome pass walks them all)
@@ -749,19 +786,27 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     }
     if (__ballot(bad) && lane == 0) s_bad = 1;
     __syncthreads();
-    const uint64_t t0 = s_t0, t1 = max(s_t0, s_t1);
-    // reach / repair counts of the chunk's sources
-    uint32_t wm = 0;
-    for (uint64_t t = t0 + tid; t < t1; t += kBlock) {
+    const uint64_t t0 = s_t0, t1 = max(s_t0, s_t1), tb = min(s_tb, t0);
+    // reach / repair counts of the chunk's sources and the back region's
+    // repair counts; the widest received window among them (pivot searches)
+    uint32_t wm = 0, wmb = 0;
+    for (uint64_t t = tb + tid; t < t1; t += kBlock) {
         const fecgpu_sw_repair h = a.hdr[t];
-        if (h.fss >= i0 && h.fss < i1 && h.nss >= 1 && h.nss <= kSwMaxWindow) {
+        const bool rp = a.rep_present[t] != 0;
+        if (h.nss < 1 || h.nss > kSwMaxWindow) continue;
+        if (h.fss >= i0 && h.fss < i1) {
             atomicAdd(&s_rcnt[h.fss - i0], 1u);
-            if (a.rep_present[t]) {
+            if (rp) {
                 wm = max(wm, (uint32_t)h.nss);
                 atomicMax(&s_reach[h.fss - i0], (uint32_t)(h.fss + h.nss));
             }
+        } else if (h.fss >= ib && h.fss < i0) {
+            atomicAdd(&s_rcb[h.fss - (i0 - kPlanHalo)], 1u);
         }
+        if (rp) wmb = max(wmb, (uint32_t)h.nss);
     }
+    wmb = wave_max(wmb);
+    if (lane == 0 && wmb) atomicMax(&s_wmb, wmb);
     // arrival flags: 8 sources per thread, and the halo past the chunk
     const uint32_t n = (uint32_t)(i1 - i0), my0 = (uint32_t)tid * kPlanPer;
     uint32_t lostm = 0;  // bit j: source i0 + my0 + j lost
@@ -849,6 +894,19 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             carry += __shfl(x, 63);
         }
         if (lane == 0) s_wpfx[NW] = carry;
+    } else if (wave == 1) {  // repfirst over the back region: tb + repairs starting before each source
+        uint32_t carry = (uint32_t)tb;
+        for (int q0 = 0; q0 < kPlanHalo; q0 += 64) {
+            const uint32_t v = s_rcb[q0 + lane];
+            uint32_t x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            s_rfb[q0 + lane] = carry + x - v;
+            carry += __shfl(x, 63);
+        }
     }
     __syncthreads();
     uint32_t wc = 0, wmx = 0, wr = 0;
@@ -857,16 +915,36 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         wmx = max(wmx, s_m[w]);
         wr += s_r[w];
     }
+    {  // the chunk-local reachL of the last lost source (the look-back's L)
+        uint32_t run = max(wmx, em), myl = 0;
+        bool has = false;
+        for (int j = 0; j < kPlanPer; j++)
+            if (my0 + j < n) {
+                run = max(run, s_reach[my0 + j]);
+                if ((lostm >> j) & 1u) {
+                    myl = run;
+                    has = true;
+                }
+            }
+        const uint64_t hb = __ballot(has);  // uniform: the last lane holding a lost source
+        const uint32_t lv = hb ? (uint32_t)__builtin_amdgcn_readlane((int)myl, 63 - __builtin_clzll(hb)) : 0u;
+        if (lane == 0) {
+            s_lh[wave] = hb != 0;
+            s_lv[wave] = lv;
+        }
+    }
+    __syncthreads();
     if (tid == 0) {
-        LbRec agg{0, 0, 0, 0};
+        LbRec agg{0, 0, 0, 0, 0};
         for (int w = 0; w < kBlock / 64; w++) {
             agg.lost += s_c[w];
             agg.reach = max(agg.reach, s_m[w]);
             agg.rep += s_r[w];
             agg.wme = max(agg.wme, s_w[w]);
+            if (s_lh[w]) agg.L = s_lv[w];
         }
         if (s_bad) agg.wme |= kSwErrHeader << 16;
-        LbRec ex{0, 0, 0, 0};
+        LbRec ex{0, 0, 0, 0, 0};
         if (c == 0) {
             lb_publish(a, c, agg, kLbInc);
         } else {
@@ -885,13 +963,14 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                     continue;
                 }
                 const bool inc = (f & 3u) == kLbInc;
-                ex = lb_join(lb_read(inc ? a.lb_inc + q : a.lb_agg + q), ex);
+                ex = lb_join(lb_read((inc ? a.lb_inc : a.lb_agg) + 2 * (size_t)q), ex);
                 if (inc) break;
                 q--;
             }
             lb_publish(a, c, lb_join(ex, agg), kLbInc);
         }
         s_excl = ex;
+        s_agg = agg;
         if (c == nch - 1) {  // the call's counters (nothing was cleared before the launch)
             const LbRec tot = lb_join(ex, agg);
             SwDecCtr z{};
@@ -904,7 +983,8 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     }
     __syncthreads();
     const LbRec ex = s_excl;
-    // lost list, rank / repfirst (as sw_dec_lost_kernel)
+    // lost list, rank / repfirst (as sw_dec_lost_kernel); positions and reachL
+    // of the chunk's lost sources in LDS for the one-unknown systems below
     uint32_t off = ex.lost + wc + ic - cnt;
     uint32_t run = max(max(ex.reach, wmx), em);
     uint32_t repc = ex.rep + wr + ir - tr;
@@ -917,12 +997,15 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         rf[j] = repc;
         if (my0 + j < n) {
             const uint64_t i = i0 + my0 + j;
+            s_rf[my0 + j] = repc;
             run = max(run, s_reach[my0 + j]);
             repc += s_rcnt[my0 + j];
             if ((lostm >> j) & 1u) {
                 a.lost[off] = (uint32_t)i;
                 a.reachL[off] = run;
                 a.sol_jobs[off] = E;
+                s_lpos[off - ex.lost] = my0 + j;
+                s_rl[off - ex.lost] = run;
                 off++;
             }
         }
@@ -939,20 +1022,106 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             a.rcnt[i0 + my0 + j] = rf[j];
         }
     }
+    if (my0 <= n && n <= my0 + kPlanPer) s_rf[n] = repc;  // repfirst at i1
     if (my0 <= n && n <= my0 + kPlanPer && i1 == a.nsrc) {  // the thread holding the end
         a.reach[a.nsrc] = off;
         a.rcnt[a.nsrc] = repc;
     }
+    const auto before = [&](uint32_t j) {  // lost sources in [i0, i0 + j), j <= chunk + halo
+        return s_wpfx[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u));
+    };
     // coefficient rows of the chunk's received repairs whose window holds a lost source
     for (uint64_t t = t0 + tid; t < t1; t += kBlock) {
         if (!a.rep_present[t]) continue;
         const fecgpu_sw_repair h = a.hdr[t];
         if (h.fss < i0 || h.fss >= i1 || h.nss < 1 || h.nss > kSwMaxWindow || a.nsrc - h.fss < h.nss) continue;
         const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
-        const auto before = [&](uint32_t j) {
-            return s_wpfx[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u));
-        };
         if (before(hi) > before(lo)) draw_row(a, t, h);
+    }
+    __syncthreads();
+    // the chunk's lost sources: one-unknown systems solved, the rest classified
+    const uint32_t nl = s_agg.lost, wmb_all = s_wmb;
+    for (uint32_t k = tid; k < nl; k += kBlock) {
+        const uint32_t u = ex.lost + k, pos = s_lpos[k], rl = s_rl[k];
+        const uint64_t i = i0 + pos;
+        const uint32_t prl = k > 0 ? s_rl[k - 1] : (ex.lost ? ex.L : 0u);
+        const bool start = u == 0 || prl <= i;
+        // the next lost source: in the chunk, else in the halo (a window reaches
+        // at most 255 sources past i, so none there means none in reach)
+        uint64_t nxt = ~0ull;
+        if (k + 1 < nl) {
+            nxt = i0 + s_lpos[k + 1];
+        } else {
+            for (uint32_t w = (pos + 1) >> 5; w < (kPlanChunk + kPlanHalo) / 32 && nxt == ~0ull; w++) {
+                uint32_t bits = s_bits[w];
+                if (w == (pos + 1) >> 5) bits &= ~((1u << ((pos + 1) & 31)) - 1u);
+                if (bits) nxt = i0 + w * 32 + __ffs(bits) - 1;
+            }
+        }
+        // (tuning "sw_long_min" 1 sends every system, these too, down the long path)
+        const bool single = start && (nxt == ~0ull || rl <= nxt) && a.long_min > 1;
+        uint8_t kind = start ? 2 : 0;
+        CombJob J = E;  // syndrome slot nrep + u: empty unless x is solved here
+        if (single) {
+            kind = 3;
+            // candidates: received repairs with fss in [i - wmb + 1, i] (repair order)
+            const uint64_t lo = i + 1 > (uint64_t)wmb_all ? max(i + 1 - wmb_all, ib) : ib;
+            const auto rfirst = [&](uint64_t p) -> uint64_t {
+                return p < i0 ? s_rfb[p - (i0 - kPlanHalo)] : s_rf[p - i0];
+            };
+            const uint64_t ta = rfirst(lo), te = rfirst(i + 1);
+            for (uint64_t t = ta; t < te; t++) {
+                if (!a.rep_present[t]) continue;
+                const fecgpu_sw_repair h = a.hdr[t];
+                if (h.fss > i || h.fss + h.nss <= i) continue;
+                const uint32_t j = (uint32_t)(i - h.fss);
+                const uint8_t cj = h.dt == 15 ? 1 : coef_at(h, j);  // DT 15: never zero
+                if (!cj) continue;
+                // the job: t's coefficients times 1/c (0 at x), t's row times 1/c
+                const uint64_t slot = a.nrep + u;
+                uint8_t *row = a.coef + slot * kSwCoefPitch;
+                Tinymt32 st;
+                tinymt32_init(st, h.key);
+                const uint32_t dt = h.dt;
+                uint32_t word = 0, cx = 0;
+                uint32_t tab[5];
+                for (int q = 0; q < (int)h.nss; q++) {
+                    uint32_t cq = 0;
+                    if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
+                        do {
+                            cq = tinymt32_u32(st) & 0xFFu;
+                        } while (cq == 0);
+                    }
+                    if ((uint32_t)q == j) {
+                        cx = cq;
+                        cq = 0;
+                    }
+                    word |= cq << (8 * (q & 3));
+                    if ((q & 3) == 3) {
+                        reinterpret_cast<uint32_t *>(row)[q >> 2] = word;
+                        word = 0;
+                    }
+                }
+                if (h.nss & 3) reinterpret_cast<uint32_t *>(row)[h.nss >> 2] = word;
+                const uint32_t iv = c_gfs.exp[255 - c_gfs.log[cx]];
+                set_tab(tab, iv);
+                for (uint32_t q = 0; q < ((uint32_t)h.nss + 3) / 4; q++)
+                    reinterpret_cast<uint32_t *>(row)[q] = tmul(reinterpret_cast<uint32_t *>(row)[q], tab);
+                row[h.nss] = (uint8_t)iv;  // the xor row's multiplier (nss < kSwCoefPitch)
+                J.in_off = h.fss * a.stride;
+                J.coef_off = slot * kSwCoefPitch;
+                J.out_list = slot;
+                J.xor_off = t * a.stride;
+                J.nin = h.nss;
+                J.nout = 1u | kCombXorScaled;
+                a.syn_outs[slot] = (uint64_t)(a.src + i * a.stride) - (uint64_t)a.synd;
+                a.stat[i] = FECGPU_STATUS_OK;
+                kind = 1;
+                break;
+            }
+        }
+        a.syn_jobs[a.nrep + u] = J;
+        a.lkind[u] = kind;
     }
     // the last block out resets the tickets for the next launch
     __syncthreads();
@@ -975,8 +1144,16 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     uint32_t rec = 0, maxin = 0;  // this wave's recovered count, widest solve
     for (uint64_t x = (uint64_t)blockIdx.x * (kBlock / 64) + wave; x < nlost; x += nwaves) {
+#if FECGPU_SWD_FUSED
+        // the plan classified every lost source and solved the one-unknown systems
+        const uint32_t kind = a.lkind[x];
+        rec += kind == 1u;
+        if (kind != 2u) continue;  // uniform
+        const uint32_t lx = a.lost[x];
+#else
         const uint32_t lx = a.lost[x];
         if (x > 0 && a.reachL[x - 1] > lx) continue;  // not a system start (uniform)
+#endif
         // extent: up to the next start
         uint32_t e = 1;
         for (;;) {
