@@ -90,6 +90,11 @@ def parse():
     ap.add_argument("--host-direct", type=int, default=-1,
                     help="tuning (config 5/6): kernels write outputs to mapped host memory, bit 0 encode, bit 1 decode")
     ap.add_argument("--host-chunk-mb", type=int, default=0, help="tuning (config 5/6): pipeline chunk size")
+    ap.add_argument("--k", type=int, default=0,
+                    help="GF codes wider than one mask (k + r > 64, fec_wide.hip): sources per window; with "
+                         "--r, config 3's workload (1200-B packets, exactly r sources erased) on that code, "
+                         "~5 GB of source bytes per GPU")
+    ap.add_argument("--r", type=int, default=0, help="repairs per window for --k")
     ap.add_argument("--extra-configs", type=int, choices=[0, 1], default=1,
                     help="one-GPU default run (config 2): also time configs 3, 4 and 7 in this process and "
                          "report them under \"configs\" (0 = config 2 only)")
@@ -299,9 +304,19 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
         win = args.sw_window or cfg.window
         cfg = dataclasses.replace(cfg, loss=loss, window=win, name=f"{cfg.name}-W{win}-loss{loss:g}",
                                   erasure_desc=f"i.i.d. p={loss:g} over sources and repairs")
+    wide = args.k > 0 and cfg.scheme == "gf256" and cfg.workload == 0 and not cfg.host
+    if wide:  # a code wider than one mask on config 3's workload
+        cfg = dataclasses.replace(cfg, k=args.k, r=args.r, name=f"cfg3wide-gf256-k{args.k}r{args.r}-1200B",
+                                  nwin_per_gpu=max(1, 5_033_164_800 // (args.k * cfg.L)),
+                                  erasure_desc=f"exactly r={args.r} sources per window")
     nwin = nwin_arg or cfg.nwin_per_gpu
     w0, nwin = shard.weak_shard(rank, world, nwin)  # this rank's global window range
-    if cfg.scheme == "sw":  # config 7: one sliding-window stream per rank
+    if wide:
+        batch = workloads.WideBatch.allocate(cfg, nwin, dev)
+        log(f"rank {rank}: {cfg.name}, windows [{w0}, {w0 + nwin}), {batch.win.numel() / 2**30:.2f} GiB")
+        batch.synthesize(ctx, w0)
+        batch.make_erasures(ctx, w0)
+    elif cfg.scheme == "sw":  # config 7: one sliding-window stream per rank
         batch = workloads.SwBatch.allocate(cfg, nwin, dev)
         log(f"rank {rank}: {cfg.name}, {batch.nsrc} sources, {batch.nrep} repairs, "
             f"{(batch.src.numel() + batch.rep.numel()) / 2**30:.2f} GiB")
@@ -419,13 +434,14 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
     dom_ms = enc_ms if dom == "encode" else dec_ms
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
     traffic, traffic_src = (pmc_traffic(cfgid, dom)
-                            if nwin == cfg.nwin_per_gpu and cfg.name == workloads.CONFIGS[cfgid].name
+                            if nwin == cfg.nwin_per_gpu and cfg.name == workloads.CONFIGS[cfgid].name and not wide
                             and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
                             else (None, None))
     cpu = None
     if args.cpu_seconds > 0 and world == 1 and not cfg.host:  # cfg5's codec and shape are cfg2's
         log(f"{cfg.name}: cpu baseline")
         cpu = (cpu_baseline_sw(cfg, args.cpu_seconds, args.cpu_threads) if cfg.scheme == "sw" else
+               None if wide else  # the CPU codec's block code is k + r <= 64
                cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads))
     peak, bound = (PCIE_PEAK_GBS, "pcie") if cfg.host else (HBM_PEAK_GBS, "hbm")
     return {
@@ -494,6 +510,11 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
 
 def main():
     args = parse()
+    if args.k:
+        if args.k + args.r <= 64 or args.r < 1 or args.r > 8 or args.k + args.r > 256:
+            log("--k/--r: a GF code with 64 < k + r <= 256 and 1 <= r <= 8")
+            sys.exit(2)
+        args.config = 3  # the wide code runs on config 3's workload
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -529,7 +550,7 @@ def main():
     # the default one-GPU run also times the other single-GPU configs in this
     # process (each on its own batch, freed after), under "configs"; the
     # headline line above is config 2's as before
-    if args.extra_configs and args.config == 2 and not args.nwin:
+    if args.extra_configs and args.config == 2 and not args.nwin and not args.k:
         extras = {}
         for cid, (st, wu) in EXTRA_CONFIGS.items():
             if world > 1 and cid not in EXTRA_CONFIGS_MULTI:

@@ -404,3 +404,91 @@ class SwBatch:
         self.src.copy_(saved)
         return {"ok": mism == 0 and n + unrec == nlost, "sources": self.nsrc, "lost": nlost, "recovered": n,
                 "unrecovered": unrec, "mismatched_recovered": mism}
+
+
+@dataclass
+class WideBatch:
+    """GF(2^8) block codes with k + r > 64 (fec_wide.hip; bench.py --k/--r):
+    nwin windows of k + r symbols of L bytes in HBM, sources seeded random bytes
+    (torch generator on the device), exactly r sources erased per window (the
+    decode's worst case: e = r), present masks of ceil((k + r) / 64) words."""
+    cfg: Config
+    nwin: int
+    win: torch.Tensor        # [nwin, k + r, stride] u8
+    present: torch.Tensor    # [nwin, words] int64 (u64)
+    status: torch.Tensor     # [nwin] u8
+    erased: torch.Tensor     # [nwin, k + r] bool
+
+    @staticmethod
+    def allocate(cfg: Config, nwin: int, dev) -> "WideBatch":
+        n = cfg.k + cfg.r
+        words = (n + 63) // 64
+        return WideBatch(cfg, nwin, torch.zeros((nwin, n, cfg.stride), dtype=torch.uint8, device=dev),
+                         torch.zeros((nwin, words), dtype=torch.int64, device=dev),
+                         torch.zeros(nwin, dtype=torch.uint8, device=dev),
+                         torch.zeros((nwin, n), dtype=torch.bool, device=dev))
+
+    def synthesize(self, ctx: Context, w0: int) -> None:
+        c = self.cfg
+        g = torch.Generator(device=self.win.device).manual_seed(SEED ^ w0)
+        self.win[:, :c.k, :c.L] = torch.randint(0, 256, (self.nwin, c.k, c.L), dtype=torch.uint8,
+                                                device=self.win.device, generator=g)
+
+    def make_erasures(self, ctx: Context, w0: int) -> None:
+        c = self.cfg
+        g = torch.Generator(device=self.win.device).manual_seed(SEED + 1 + w0)
+        key = torch.rand((self.nwin, c.k), device=self.win.device, generator=g)
+        miss = key.argsort(dim=1)[:, :c.r]  # r distinct sources per window
+        self.erased.zero_()
+        self.erased.scatter_(1, miss, True)
+        n = c.k + c.r
+        pres = ~self.erased
+        words = self.present.shape[1]
+        self.present.zero_()
+        sh = torch.arange(64, device=self.win.device, dtype=torch.int64)
+        for wd in range(words):
+            bits = pres[:, wd * 64:min(n, wd * 64 + 64)].to(torch.int64)
+            self.present[:, wd] = (bits << sh[:bits.shape[1]]).sum(1)
+
+    def encode(self, ctx: Context) -> None:
+        c = self.cfg
+        ctx.encode_batch(c.code, self.win, nwin=self.nwin, stride=c.stride, sym_len_all=c.L)
+
+    def decode(self, ctx: Context) -> None:
+        c = self.cfg
+        ctx.decode_batch(c.code, self.win, self.present, self.status, nwin=self.nwin, stride=c.stride,
+                         sym_len_all=c.L)
+
+    def source_bytes(self) -> int:
+        return self.nwin * self.cfg.k * self.cfg.L
+
+    def algorithmic_bytes(self) -> dict:
+        """encode (k + r) * L per window; decode: k rows read (k - r received
+        sources and the r repairs) and r written, (k + r) * L."""
+        c = self.cfg
+        return {"encode": self.nwin * (c.k + c.r) * c.L, "decode": self.nwin * (c.k + c.r) * c.L}
+
+    def digest(self, ctx: Context, w0: int) -> int:
+        """Checksum of the encoded windows (sum of their 8-byte words mod 2^64)."""
+        self.encode(ctx)
+        torch.cuda.synchronize()
+        return int(self.win.view(torch.int64).sum().item()) & (2**64 - 1)
+
+    def verify(self, ctx: Context, w0: int, chunk: int = 2048) -> dict:
+        c = self.cfg
+        self.encode(ctx)
+        saved = self.win[:, :c.k].clone()
+        self.win[self.erased] = 0xAB
+        self.decode(ctx)
+        torch.cuda.synchronize()
+        ok = self.status == STATUS_OK
+        mism = 0
+        for s0 in range(0, self.nwin, chunk):
+            eq = (self.win[s0:s0 + chunk, :c.k, :c.L] == saved[s0:s0 + chunk, :, :c.L]).flatten(1).all(1)
+            mism += int((ok[s0:s0 + chunk] & ~eq).sum().item())
+        unrec = int((~ok).sum().item())
+        self.win[:, :c.k] = saved
+        del saved
+        # every window has exactly r erasures: an MDS code recovers all of them
+        return {"ok": mism == 0 and (unrec == 0 or not c.mds), "windows": self.nwin,
+                "mismatched_ok_windows": mism, "unrecoverable": unrec}

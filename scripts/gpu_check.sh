@@ -41,6 +41,12 @@ for s in "$@"; do
         bench4) step bench4 600 python bench.py --config 4 --steps 5 --warmup 1 --cpu-seconds 10 ;;
         bench7) step bench7 600 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 10 ;;
         bench7l10) step bench7l10 600 python bench.py --config 7 --steps 20 --warmup 5 --cpu-seconds 0 --sw-loss 0.1 ;;
+        benchw120) step benchw120 600 python bench.py --k 120 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 ;;
+        benchw248) step benchw248 600 python bench.py --k 248 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 ;;
+        profw120) step profw120 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profw120 -o run -- \
+                      python bench.py --k 120 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 ;;
+        profw248) step profw248 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profw248 -o run -- \
+                      python bench.py --k 248 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 ;;
         bench5) step bench5 600 python bench.py --config 5 --steps 10 --warmup 2 --cpu-seconds 0 ;;
         bench6) step bench6 600 python bench.py --config 6 --steps 10 --warmup 2 --cpu-seconds 0 ;;
         dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
