@@ -204,13 +204,28 @@ struct CombArgs {
     // job *nin_dev (<= nin_max); each workgroup fits as many jobs as its
     // `budget` bytes of LDS hold at that width
     const uint32_t *nin_dev;
+    int extra_shift;  // the device count counts 2^extra_shift units per job
     uint32_t budget;
+    // every job has the same coefficient block (a block code's parity rows:
+    // wide encode): [nout_max][nin_max] at coef, its tables built once per
+    // workgroup and shared by the workgroup's jobs (job regions hold only their
+    // output pointers), so more jobs fit a workgroup
+    int shared_coef;
 };
 // LDS bytes per job of comb_kernel<R> at nin_max inputs
 __host__ __device__ inline uint32_t comb_job_lds(int nin_max, int R) {
     const uint32_t rt = R == 1 ? 1u : (uint32_t)(R + 3) & ~3u;
     // nin_max input rows' tables plus one row for the xor row's multiplier
     return ((uint32_t)(nin_max + 1) * (16u * R + 4u * rt + 1u) + 8u * R + 8u + 15u) & ~15u;
+}
+// shared_coef launches: the shared tables, then a small region per job
+__host__ __device__ inline uint32_t comb_shared_lds(int nin_max, int R) {
+    const uint32_t rt = R == 1 ? 1u : (uint32_t)(R + 3) & ~3u;
+    return ((uint32_t)nin_max * (16u * R + 4u * rt + 1u) + 15u) & ~15u;
+}
+__host__ __device__ inline uint32_t comb_job_small_lds(int R) {
+    const uint32_t rt = R == 1 ? 1u : (uint32_t)(R + 3) & ~3u;
+    return (16u * R + 4u * rt + 8u * (R + 1) + 15u) & ~15u;
 }
 hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
 // GF block codes with k + r > 64 (fec_wide.hip): a plan / job kernel, then the
@@ -293,6 +308,10 @@ constexpr int kSwRows = 256;    // long systems: row slots (more rows alive at o
                                 // to a basis first: they span at most 255 columns, fec_swdec.hip)
 constexpr int kSwChunk = 4096;  // sources per planning chunk (FECGPU_SWD_FUSED 0)
 constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
+#ifndef FECGPU_SWD_SOLVE_LIST
+#define FECGPU_SWD_SOLVE_LIST 1  // fused plan: solve jobs in a compact list (one atomic per system)
+                                 // instead of slots per unknown (the solve pass walks every slot)
+#endif
 #ifndef FECGPU_SWD_FUSED
 #define FECGPU_SWD_FUSED 1  // the decode plan as one look-back launch (sw_dec_plan_kernel) instead of
                             // a memset and five passes
@@ -306,7 +325,11 @@ constexpr uint32_t kSwErrInternal = 4u;  // the fused plan's look-back gave up (
 struct SwDecCtr {  // per call, zeroed before the first kernel
     uint32_t nlost, wmax, maxp, err;   // err: kSwErr* bits
     uint32_t nmid, nlong, npiv, recovered;  // queued mid / long systems, pivot rows, recovered
-    uint32_t maxin, pad0, pad1, pad2;       // widest small-system solve (syndrome rows)
+    uint32_t maxin;                    // widest small-system solve (syndrome rows)
+    // fused plan: solve outputs handed out, 8 per solve job (a system takes
+    // ceil(determined / 8) jobs at once: job j writes outputs 8j ..), so the
+    // solve pass walks only real jobs (nsolout >> 3 of them)
+    uint32_t nsolout, pad0, pad1, pad2, pad3;
     unsigned long long nlog;           // long-system log entries
 };
 // one long system: lost[x0 .. x0 + e), candidate repairs [t_lo, t_hi); its

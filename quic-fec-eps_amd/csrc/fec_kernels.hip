@@ -2048,6 +2048,16 @@ struct CombRegion {
         optr = reinterpret_cast<uint64_t *>(region + n * (16 * R + 4 * RT));
         nz = reinterpret_cast<uint8_t *>(optr + R + 1);
     }
+    // CombArgs::shared_coef: tables and nonzero masks shared (comb_shared_lds),
+    // the xor row's tables and the output pointers per job (comb_job_small_lds)
+    __device__ __forceinline__ CombRegion(uint8_t *tabs, uint8_t *job, int nin_max) {
+        ab = reinterpret_cast<uint4 *>(tabs);
+        tc = reinterpret_cast<uint32_t *>(tabs + (size_t)nin_max * R * 16);
+        nz = tabs + (size_t)nin_max * (16 * R + 4 * RT);
+        xab = reinterpret_cast<uint4 *>(job);
+        xtc = reinterpret_cast<uint32_t *>(job + R * 16);
+        optr = reinterpret_cast<uint64_t *>(job + R * 16 + RT * 4);
+    }
 };
 
 // One slot (job, 16-B column) for NE outputs (wave-uniform): acc[u] = sum_q
@@ -2241,7 +2251,7 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
     }
     __syncthreads();
 #endif
-    const uint64_t njobs = a.njobs + (a.extra ? (uint64_t)*a.extra : 0ull);
+    const uint64_t njobs = a.njobs + (a.extra ? (uint64_t)(*a.extra >> a.extra_shift) : 0ull);
     int nin_max = a.nin_max, wpb = a.wpb;
     uint32_t job_lds = a.job_lds;
     if (a.nin_dev) {  // device-sized: the widest job is known on the device only
@@ -2249,6 +2259,30 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
         job_lds = comb_job_lds(nin_max, R);
         wpb = choose_wpb_dev(a.ncol, job_lds, a.budget);
     }
+    // shared coefficient block: its tables once per workgroup, before any group
+    const bool shared = a.shared_coef != 0;
+    const uint32_t tab_lds = shared ? comb_shared_lds(nin_max, R) : 0u;
+    if (shared) {
+        job_lds = comb_job_small_lds(R);
+        const int nout = min(a.nout_max, R);
+        const CombRegion<R> rg(regions, regions + tab_lds, nin_max);
+        for (int i = tid; i < nout * nin_max; i += kBlock) {
+            const int u = i / nin_max, q = i - u * nin_max;
+            const CoefTab ct = make_coef_tab(a.coef[i]);
+            rg.ab[q * R + u] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+            rg.tc[q * RT + u] = ct.c;
+        }
+        for (int q = tid; q < nin_max; q += kBlock) {
+            uint32_t m = 0;
+            for (int u = 0; u < nout; u++) m |= (a.coef[u * nin_max + q] != 0 ? 1u : 0u) << u;
+            rg.nz[q] = (uint8_t)m;
+        }
+        __syncthreads();
+    }
+    const auto region = [&](int jl) __attribute__((always_inline)) {
+        return shared ? CombRegion<R>(regions, regions + tab_lds + (size_t)jl * job_lds, nin_max)
+                      : CombRegion<R>(regions + (size_t)jl * job_lds, nin_max);
+    };
     for (XcdRange xr = xcd_range((njobs + wpb - 1) / wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
         const uint64_t j0 = xr.cur * wpb;
         const int nb = (int)min((uint64_t)wpb, njobs - j0);
@@ -2279,18 +2313,20 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
             const CombJob J = a.jobs[j0 + jl];
 #endif
             const int nin = min((int)J.nin, nin_max), nout = min((int)(J.nout & ~kCombXorScaled), R);
-            const CombRegion<R> rg(regions + (size_t)jl * job_lds, nin_max);
+            const CombRegion<R> rg = region(jl);
             const uint8_t *cf = a.coef + J.coef_off;
-            for (int i = lane; i < nout * nin; i += 64) {
-                const int u = i / nin, q = i - u * nin;
-                const CoefTab ct = make_coef_tab(cf[i]);
-                rg.ab[q * R + u] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
-                rg.tc[q * RT + u] = ct.c;
-            }
-            for (int q = lane; q < nin; q += 64) {
-                uint32_t m = 0;
-                for (int u = 0; u < nout; u++) m |= (cf[u * nin + q] != 0 ? 1u : 0u) << u;
-                rg.nz[q] = (uint8_t)m;
+            if (!shared) {
+                for (int i = lane; i < nout * nin; i += 64) {
+                    const int u = i / nin, q = i - u * nin;
+                    const CoefTab ct = make_coef_tab(cf[i]);
+                    rg.ab[q * R + u] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+                    rg.tc[q * RT + u] = ct.c;
+                }
+                for (int q = lane; q < nin; q += 64) {
+                    uint32_t m = 0;
+                    for (int u = 0; u < nout; u++) m |= (cf[u * nin + q] != 0 ? 1u : 0u) << u;
+                    rg.nz[q] = (uint8_t)m;
+                }
             }
             if (lane < nout) {
                 rg.optr[lane] = reinterpret_cast<uint64_t>(a.out_base) + a.outs[J.out_list + lane];
@@ -2332,7 +2368,7 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
             const uint32_t col = s - s_pfx[i];
             const int ne = s_ne[jl];
             const int nw = __builtin_amdgcn_readfirstlane(ne);
-            const CombRegion<R> rg(regions + (size_t)jl * job_lds, nin_max);
+            const CombRegion<R> rg = region(jl);
             comb_dispatch<R>(nw, reinterpret_cast<const uint8_t *>(s_in[jl]) + col * 16u, a.stride,
                              (int)s_nin[jl], ne, col, rg, a.skip && a.ncol >= 64);
         }
@@ -2600,7 +2636,8 @@ hipError_t launch_comb(CombArgs a, int R, hipStream_t s) {
         const uint64_t groups = (nmax + a.wpb - 1) / a.wpb;
         a.nx = groups >= 8 ? 8 : 1;
         grid = (groups + a.nx - 1) / a.nx * a.nx;  // one group per workgroup
-        lds = a.job_lds * (uint32_t)a.wpb;
+        lds = a.shared_coef ? comb_shared_lds(a.nin_max, R) + comb_job_small_lds(R) * (uint32_t)a.wpb
+                            : a.job_lds * (uint32_t)a.wpb;
     }
     switch (R) {
         case 1: hipLaunchKernelGGL(comb_kernel<1>, dim3((unsigned)grid), dim3(kBlock), lds, s, a); break;

@@ -235,8 +235,10 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
     L.o_synj = take(nsyn * sizeof(CombJob));
     L.o_syno = take(nsyn * 8);
     L.o_coef = take(nsyn * (size_t)kSwCoefPitch);
-    L.o_solj = take(nsrc * sizeof(CombJob));
-    L.o_solo = take(nsrc * 8);
+    // solve jobs / outputs: a slot per unknown, or (fused plan) a compact list
+    // with outputs padded to 8 per system (multi-unknown systems: <= 4.5 per unknown)
+    L.o_solj = take((nsrc + 8) * sizeof(CombJob));
+    L.o_solo = take((FECGPU_SWD_FUSED && FECGPU_SWD_SOLVE_LIST ? 5 * nsrc + 8 : nsrc) * 8);
     L.o_solc = take(nrep * (size_t)kSwSmallE);
     L.o_long = take(L.long_cap * sizeof(SwLong));
     L.o_mid = take(L.long_cap * sizeof(SwLong));
@@ -349,8 +351,14 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     va.in_base = static_cast<const uint8_t *>(psyn);
     va.out_base = src;
     va.xor_base = nullptr;
+#if FECGPU_SWD_FUSED && FECGPU_SWD_SOLVE_LIST
+    va.extra = &a.ctr->nsolout;  // the compact list: a job per 8 outputs
+    va.extra_shift = 3;
+    va.extra_max = nsrc + 8;
+#else
     va.extra = &a.ctr->nlost;  // a slot per unknown, filled by its small system
     va.extra_max = nsrc;
+#endif
     va.njobs = 0;
     va.nin_max = kSwSolveIn;
     va.nout_max = kSwSolveOut;

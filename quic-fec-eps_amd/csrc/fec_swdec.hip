@@ -515,11 +515,21 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         return 1;
     }
 #endif
-    // solve jobs in the system's unknown slots x .. (ndet <= e), outputs at
-    // x + d; inputs the syndrome rows t_first .. t_last, coefficients at 64
-    // bytes per repair from t_first (ndet <= 64, so ndet * nin fits)
+    // solve jobs (ndet <= e): inputs the syndrome rows t_first .. t_last,
+    // coefficients at 64 bytes per repair from t_first (ndet <= 64, so
+    // ndet * nin fits).  Fused plan: outputs and jobs from one counter, 8
+    // outputs per job, so the solve pass walks only real jobs; else in the
+    // system's unknown slots x .. (outputs at x + d).
     const uint32_t t_first = eq[0], nin = eq[p - 1] - t_first + 1;
     const uint64_t c0 = (uint64_t)t_first * kSwSmallE;
+#if FECGPU_SWD_FUSED && FECGPU_SWD_SOLVE_LIST
+    uint32_t ob = 0;
+    if (lane == 0) ob = atomicAdd(&a.ctr->nsolout, (uint32_t)(ndet + 7) & ~7u);
+    ob = __shfl(ob, 0);
+    const uint64_t o0 = ob, j0 = ob >> 3;
+#else
+    const uint64_t o0 = x, j0 = x;
+#endif
     if (det) {
         const int d = __popcll(dm & lanes_below(lane));
         uint8_t *cf = a.sol_coef + c0 + (uint64_t)d * nin;
@@ -529,7 +539,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
             if (q < p && eq[q] == t_first + r) v = M[prc * kPitch + e + q++];
             cf[r] = v;
         }
-        a.sol_outs[x + d] = (uint64_t)U[lane] * a.stride;
+        a.sol_outs[o0 + d] = (uint64_t)U[lane] * a.stride;
         a.stat[U[lane]] = FECGPU_STATUS_OK;
     }
     const int nj = (ndet + 7) / 8;
@@ -537,11 +547,11 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         CombJob J;
         J.in_off = (uint64_t)t_first * a.stride;
         J.coef_off = c0 + (uint64_t)lane * 8 * nin;
-        J.out_list = x + (uint64_t)lane * 8;
+        J.out_list = o0 + (uint64_t)lane * 8;
         J.xor_off = kNoXor;
         J.nin = nin;
         J.nout = (uint32_t)min(8, ndet - 8 * lane);
-        a.sol_jobs[x + lane] = J;
+        a.sol_jobs[j0 + lane] = J;
     }
     *nin_out = nin;
     return ndet;
@@ -1003,7 +1013,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             if ((lostm >> j) & 1u) {
                 a.lost[off] = (uint32_t)i;
                 a.reachL[off] = run;
-                a.sol_jobs[off] = E;
+#if !FECGPU_SWD_SOLVE_LIST
+                a.sol_jobs[off] = E;  // solve jobs in the unknowns' slots: empty unless filled
+#endif
                 s_lpos[off - ex.lost] = my0 + j;
                 s_rl[off - ex.lost] = run;
                 off++;
@@ -1325,7 +1337,10 @@ __device__ bool long_compact(const SwDecArgs &a, LongLds &L, uint32_t c, int &na
         uint64_t best = ~0ull;
         for (int i = lane; i < nact; i += 64) {
             const uint32_t s = L.act[i];
-            if (!L.lead[i] && L.rowc[s][j]) best = min(best, ((uint64_t)L.row_hi[s] << 9) | (uint64_t)i);
+            // a row's ring bytes past its hi were never written (staging writes
+            // [lo, hi] only): look at column c + jj only inside the row's range
+            if (!L.lead[i] && c + jj <= L.row_hi[s] && L.rowc[s][j])
+                best = min(best, ((uint64_t)L.row_hi[s] << 9) | (uint64_t)i);
         }
         best = wave_min64(best);
         if (best == ~0ull) continue;  // no unled row has column j (uniform)
@@ -1336,7 +1351,8 @@ __device__ bool long_compact(const SwDecArgs &a, LongLds &L, uint32_t c, int &na
             if (!log_room(a, fw, 64, lane)) return false;
             const int i = i0 + lane;
             uint32_t f = 0;
-            if (i < nact && i != ppos && !L.lead[i]) f = gmul(L.g, L.rowc[L.act[i]][j], ip);
+            if (i < nact && i != ppos && !L.lead[i] && c + jj <= L.row_hi[L.act[i]])
+                f = gmul(L.g, L.rowc[L.act[i]][j], ip);
             if (i < nact) L.fq[i] = (uint8_t)f;
             const uint64_t b = __ballot(f != 0);
             if (f) {
@@ -1671,7 +1687,7 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                 set_tab(tip, ip);
                 if (lane == 0) emit(bwd + nb, kOpXBegin, cs, 0, pv, 0, tip);
                 nb++;
-                const uint32_t w = hi - (uint32_t)c;
+                const uint32_t w = hi >= (uint32_t)c ? hi - (uint32_t)c : 0u;  // a pivot row ends at or after its column
                 for (uint32_t j0 = 0; j0 < w; j0 += 64) {
                     const uint32_t j = (uint32_t)c + 1 + j0 + lane;
                     const uint32_t cj = j0 + lane < w ? L.prow[j & 255] : 0u;

@@ -25,6 +25,10 @@ namespace {
 
 __constant__ GfTables c_gfw = make_gf_tables();
 
+#ifndef FECGPU_WIDE_SHARED
+#define FECGPU_WIDE_SHARED 1  // wide encode: parity-row tables shared by a workgroup's jobs
+#endif
+
 #define WIDE_WAVE_SYNC()                                        \
     do {                                                        \
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); \
@@ -214,9 +218,23 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
     c.ncol = ncol;
     c.stride = stride;
     c.nin_max = decode ? k + r : k;
-    c.nout_max = kMaxR;
+    c.nout_max = decode ? kMaxR : r;
     c.job_lds = comb_job_lds(c.nin_max, kMaxR);
-    c.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c.job_lds, 64u << 10)));
+    constexpr uint32_t kBudget = 64u << 10;
+#if FECGPU_WIDE_SHARED
+    if (!decode) {
+        // every encode job multiplies by the same parity rows: one table block per
+        // workgroup, so the jobs per workgroup follow lane use alone (1200-B rows
+        // are 75 of a workgroup's 256 lanes)
+        c.shared_coef = 1;
+        // at most nwin / 1024 jobs each, so the grid keeps >= 4 workgroups per CU
+        const uint32_t cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxWpb, nwin / 1024));
+        const uint32_t room = std::min<uint32_t>(kBudget - comb_shared_lds(k, kMaxR), cap * comb_job_small_lds(kMaxR));
+        c.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, comb_job_small_lds(kMaxR), room)));
+        return launch_comb(c, kMaxR, s);
+    }
+#endif
+    c.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c.job_lds, kBudget)));
     return launch_comb(c, kMaxR, s);
 }
 

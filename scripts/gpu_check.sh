@@ -18,6 +18,11 @@ step() {  # name timeout cmd...
         echo "stopping after $name (rc=$rc)"
         exit $rc
     fi
+    # a test killed by pytest-timeout may leave its kernel on the card: no more GPU work
+    if grep -q "+++ Timeout +++" "gpurun_out/$name.log"; then
+        echo "stopping after $name (a test timed out)"
+        exit 124
+    fi
     return 0
 }
 prof() {  # name config extra-args...
@@ -56,6 +61,9 @@ for s in "$@"; do
                    python bench.py ;;  # the driver's default command, as is
         swtests) step swtests 300 python -u -m pytest tests/test_gpu_swconn.py tests/test_gpu_sw.py -q -x \
                      --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+        swnew) step swnew 240 python -u -m pytest tests/test_gpu_sw.py -q -x -k \
+                   "two_repairs or many_repairs or compaction or async_error or log_overflow or long_path" \
+                   --timeout 60 --timeout-method thread -p no:cacheprovider ;;
         streamtests) step streamtests 300 python -u -m pytest tests/test_gpu_swstream.py -q -x \
                      --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         abstream7)  # cfg7: sliding-window encode modes, interleaved twice
