@@ -268,6 +268,13 @@ inline uint64_t sw_enc_jobs(uint64_t nrep, int group) {
 // to start at or after the end of the one A P repairs before it (P = 1 and
 // A = ceil(W / step) for a regular schedule; the workgroup picks the smallest
 // P, then A <= kSwSlots, that its segment's headers allow).
+#ifndef FECGPU_SWS_SGPR
+// streaming encode: multiply tables in global memory (a table pass first), read
+// by scalar loads: 4-entry tables over the bit pairs of a byte, so each v_perm
+// takes one SGPR (gfx950 reads at most one SGPR per VALU op) and no LDS read
+// per product (fec_swenc.hip)
+#define FECGPU_SWS_SGPR 0  // A/B pending (round 4)
+#endif
 constexpr int kSwSeg = 64;
 constexpr int kSwSlots = 8;
 constexpr int kSwStreamU = 8;  // sources per batch (a regular schedule's step divides it: whole batches)
@@ -283,7 +290,15 @@ struct SwStreamArgs {
     int segcap;         // repairs per segment (<= kSwSeg)
     uint64_t nseg;      // segments; workgroup b takes [b nseg / grid, (b + 1) nseg / grid)
     uint32_t lds;       // dynamic LDS bytes
+    // nullable: device scratch of sw_stream_gtab_bytes(nrep, max_window) for the
+    // multiply tables in global memory, read by scalar loads (FECGPU_SWS_SGPR):
+    // 4-entry tables (one SGPR feeds a v_perm), no LDS tables
+    void *gtab;
 };
+// [kSwStreamU zero entries][per repair: kSwStreamU zeros, max_window entries][kSwStreamU zeros], 16 B each
+inline uint64_t sw_stream_gtab_bytes(uint64_t nrep, int max_window) {
+    return (2ull * kSwStreamU + nrep * (uint64_t)(max_window + kSwStreamU)) * 16ull;
+}
 // C: dwords per lane (1 or 2); LDS budget per workgroup in bytes
 hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t s);
 // LDS per streaming-encode repair: kSwStreamU zero tables and max_window
@@ -422,7 +437,7 @@ ssize_t set_dev_error(hipError_t e, const char *what);
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *jobs,
                        void *coef, void *outs, hipStream_t s, int group = 1,
-                       const fecgpu_sw_repair *hdr_host = nullptr, int stream = 0);
+                       const fecgpu_sw_repair *hdr_host = nullptr, int stream = 0, void *gtab = nullptr);
 // the ctx's "sw_group" tuning (repairs per sliding-window encode job)
 int ctx_sw_group(const fecgpu_ctx *ctx);
 // the ctx's "sw_stream" tuning: 0 combine jobs, 1 / 2 the streaming encode

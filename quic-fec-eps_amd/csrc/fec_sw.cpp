@@ -140,9 +140,11 @@ bool sw_groups_fit(const fecgpu_sw_repair *h, uint64_t nrep, uint64_t nsrc, int 
 
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *pj, void *pc,
-                       void *po, hipStream_t s, int group, const fecgpu_sw_repair *hdr_host, int stream) {
+                       void *po, hipStream_t s, int group, const fecgpu_sw_repair *hdr_host, int stream,
+                       void *gtab) {
     if (stream > 0 && nsrc < kSwStreamSources) {
         SwStreamArgs sa{};
+        sa.gtab = gtab;
         sa.src = src;
         sa.rep = rep;
         sa.hdr = hdr;
@@ -190,9 +192,13 @@ ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_
                       uint32_t stride, hipStream_t s, const fecgpu_sw_repair *hdr_host = nullptr) {
     void *pj = nullptr, *pc = nullptr, *po = nullptr;
     const int group = ctx_sw_group(ctx), stream = ctx_sw_stream(ctx);
-    if (stream > 0 && nsrc < kSwStreamSources)
+    if (stream > 0 && nsrc < kSwStreamSources) {
+        // the streaming encode's multiply tables in global memory (scalar loads)
+        void *gt = nullptr;
+        if (FECGPU_SWS_SGPR) RC_TRY(ctx_sw_scratch(ctx, 1, sw_stream_gtab_bytes(nrep, std::max(1, max_window)), &gt));
         return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, nullptr, nullptr, nullptr, s,
-                              group, hdr_host, stream);
+                              group, hdr_host, stream, gt);
+    }
     RC_TRY(ctx_sw_scratch(ctx, 0, sw_enc_jobs(nrep, group) * sizeof(CombJob), &pj));
     RC_TRY(ctx_sw_scratch(ctx, 1, nrep * kSwCoefPitch, &pc));
     RC_TRY(ctx_sw_scratch(ctx, 2, nrep * sizeof(uint64_t), &po));

@@ -41,6 +41,9 @@ constexpr int kSwsAmax = FECGPU_SWS_AMAX < kSwSlots ? FECGPU_SWS_AMAX : kSwSlots
 #define FECGPU_SWS_BUF 1  // source rows by buffer loads (scalar row offsets)
 #endif
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const u32x4 *k4p;  // uniform loads: s_load_dwordx4
+
 #define SWS_WAVE_SYNC()                                         \
     do {                                                        \
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); \
@@ -114,6 +117,7 @@ struct SwsPlan {
 };
 
 __device__ __forceinline__ void sws_plan(const SwStreamArgs &a, SwsPlan &pl, uint8_t *CB, uint64_t j0, int n, int lane) {
+    // CB null: the tables are in global memory (FECGPU_SWS_SGPR), no coefficients here
     const int W = a.max_window;
     uint64_t fss = 0, end = 0;
     bool ne = false;
@@ -133,7 +137,7 @@ __device__ __forceinline__ void sws_plan(const SwStreamArgs &a, SwsPlan &pl, uin
         const int v = __popcll(bne & below);
         pl.fe[v] = make_uint2((uint32_t)(fss - lo), (uint32_t)(end - lo));
         pl.out[v] = (uint16_t)lane;
-        (void)rlc_coefs(h.key, (int)(end - fss), min((uint32_t)h.dt, 15u), CB + (size_t)v * W);
+        if (CB) (void)rlc_coefs(h.key, (int)(end - fss), min((uint32_t)h.dt, 15u), CB + (size_t)v * W);
     }
     if (lane < n && !ne) pl.empty[__popcll(bem & below)] = (uint16_t)lane;
     SWS_WAVE_SYNC();
@@ -193,6 +197,70 @@ __device__ __forceinline__ void gmac_c(uint32_t (&acc)[C], const SplitC<C> &s, u
                  __builtin_amdgcn_perm(tc, tc, s.c[d]);
 }
 
+// 4-entry tables: c*x = Q0[x & 3] ^ Q1[(x >> 2) & 3] ^ Q2[(x >> 4) & 3] ^ Q3[x >> 6]
+// with Qk[b] = c * (b << 2k): Q0 = TA's low dword, Q3 = TC (make_coef_tab)
+template <int C>
+struct Split4 {
+    uint32_t i[4][C];
+};
+template <int C>
+__device__ __forceinline__ Split4<C> split4(const uint32_t (&x)[C]) {
+    Split4<C> s;
+#pragma unroll
+    for (int d = 0; d < C; d++) {
+        s.i[0][d] = x[d] & 0x03030303u;
+        s.i[1][d] = (x[d] >> 2) & 0x03030303u;
+        s.i[2][d] = (x[d] >> 4) & 0x03030303u;
+        s.i[3][d] = (x[d] >> 6) & 0x03030303u;
+    }
+    return s;
+}
+__device__ __forceinline__ u32x4 quad_tab(uint32_t c) {
+    uint32_t p[8];
+    p[0] = c & 0xFFu;
+    for (int b = 1; b < 8; b++) p[b] = gf_xtime(p[b - 1]);
+    u32x4 q;
+    q.x = (p[0] << 8) ^ (p[1] << 16) ^ ((p[0] ^ p[1]) << 24);
+    q.y = (p[2] << 8) ^ (p[3] << 16) ^ ((p[2] ^ p[3]) << 24);
+    q.z = (p[4] << 8) ^ (p[5] << 16) ^ ((p[4] ^ p[5]) << 24);
+    q.w = (p[6] << 8) ^ (p[7] << 16) ^ ((p[6] ^ p[7]) << 24);
+    return q;
+}
+
+// The global tables (FECGPU_SWS_SGPR): a thread per repair draws its clipped
+// window's coefficients and writes their 4-entry tables after a run of
+// kSwStreamU zero tables; entries past its window are zero; the array starts
+// and ends with kSwStreamU zero tables (sw_stream_gtab_bytes).
+__global__ __launch_bounds__(kBlock) void sws_tab_kernel(SwStreamArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    u32x4 *G = reinterpret_cast<u32x4 *>(a.gtab);
+    const int W = a.max_window, RW = W + kSwsU;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    if (t == 0)
+        for (int i = 0; i < kSwsU; i++) {
+            G[i] = z;
+            G[kSwsU + a.nrep * (uint64_t)RW + i] = z;
+        }
+    if (t >= a.nrep) return;
+    const fecgpu_sw_repair h = a.hdr[t];
+    const uint64_t fss = min(h.fss, a.nsrc);
+    const int nss = (int)min((uint64_t)min((int)h.nss, W), a.nsrc - fss);
+    u32x4 *row = G + kSwsU + t * (uint64_t)RW;
+    for (int i = 0; i < kSwsU; i++) row[i] = z;
+    Tinymt32 st;
+    tinymt32_init(st, h.key & 0xFFFFu);
+    const uint32_t dt = min((uint32_t)h.dt, 15u);
+    for (int q = 0; q < W; q++) {
+        uint32_t c = 0;
+        if (q < nss && (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt)) {
+            do {
+                c = tinymt32_u32(st) & 0xFFu;
+            } while (c == 0);
+        }
+        row[kSwsU + q] = c ? quad_tab(c) : z;
+    }
+}
+
 // Pass p of a segment over this lane's column (byte offset loff in a row):
 // A slots, repairs p, p + P, ... in slot order; every window is met in source
 // order, a slot's repair is stored when its last source is in.  Sources go in
@@ -213,10 +281,11 @@ __device__ __forceinline__ void sws_window(const SwsPlan &pl, uint32_t v, uint32
     }
 }
 
-template <int A, int C>
+template <int A, int C, bool G>
 __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &pl, const uint4 *AB,
                                          const uint32_t *TC, uint64_t j0, int p, int P, uint32_t loff,
                                          bool live) {
+    const k4p GT = (k4p)a.gtab;  // G: the global tables
     constexpr int U = kSwsU;
     static_assert(U % 2 == 0, "sources go in pairs");
     const uint32_t RW = (uint32_t)a.max_window + U, nn = rfl((uint32_t)pl.nn), stepv = (uint32_t)(A * P);
@@ -265,11 +334,17 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
         // before the window; repair 0's zero run while the window is ahead)
         const uint4 *tab[A];
         const uint32_t *tcb[A];
+        uint64_t gb[A];  // G: entry of source s of slot m's repair (0: the leading zero run)
 #pragma unroll
         for (int m = 0; m < A; m++) {
-            const uint32_t tb = f[m] < sn ? v[m] * RW + U + s - f[m] : 0u;
-            tab[m] = AB + tb;
-            tcb[m] = TC + tb;
+            if constexpr (G) {
+                const uint64_t t = j0 + (dense ? v[m] : rfl(pl.out[min(v[m], (uint32_t)kSwSeg - 1)]));
+                gb[m] = f[m] < sn ? (uint64_t)kSwsU + t * RW + U + s - f[m] : 0ull;
+            } else {
+                const uint32_t tb = f[m] < sn ? v[m] * RW + U + s - f[m] : 0u;
+                tab[m] = AB + tb;
+                tcb[m] = TC + tb;
+            }
         }
         // a batch cut short by a window end multiplies zero rows past it (their
         // table reads stay inside the LDS tables: kSwsU spare entries at the end)
@@ -279,6 +354,26 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
 #pragma unroll
                 for (int d = 0; d < C; d++) X[i][d] = (uint32_t)i < L ? X[i][d] : 0u;
         }
+        if constexpr (G) {
+            // per source and slot: one s_load_dwordx4 of 4 tables, 4 v_perm
+            // with an SGPR table each, two 3-input XORs
+#pragma unroll
+            for (int i = 0; i < U; i++) {
+                const Split4<C> q = split4<C>(X[i]);
+#pragma unroll
+                for (int m = 0; m < A; m++) {
+                    const u32x4 tq = GT[gb[m] + i];
+#pragma unroll
+                    for (int d = 0; d < C; d++) {
+                        uint32_t t = xor3s(acc[m][d], __builtin_amdgcn_perm(tq.x, tq.x, q.i[0][d]),
+                                           __builtin_amdgcn_perm(tq.y, tq.y, q.i[1][d]));
+                        acc[m][d] = xor3s(t, __builtin_amdgcn_perm(tq.z, tq.z, q.i[2][d]),
+                                          __builtin_amdgcn_perm(tq.w, tq.w, q.i[3][d]));
+                        asm volatile("" : "+v"(acc[m][d]));
+                    }
+                }
+            }
+        } else
         // sources in pairs: the six table lookups of two products fold into
         // the accumulator with three 3-input XORs
 #pragma unroll
@@ -348,7 +443,7 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
 #endif
 }
 
-template <int C>
+template <int C, bool G>
 __global__ __launch_bounds__(512) void sw_stream_kernel(SwStreamArgs a) {
     extern __shared__ uint4 sws_dyn[];
     __shared__ SwsPlan pl;
@@ -364,13 +459,13 @@ __global__ __launch_bounds__(512) void sw_stream_kernel(SwStreamArgs a) {
     for (uint64_t sg = sb; sg < se; sg++) {
         const uint64_t j0 = sg * (uint64_t)a.segcap;
         const int n = (int)min((uint64_t)a.segcap, a.nrep - j0);
-        if (wave == 0) sws_plan(a, pl, CB, j0, n, lane);
+        if (wave == 0) sws_plan(a, pl, G ? nullptr : CB, j0, n, lane);
         __syncthreads();
         const int nn = (int)rfl((uint32_t)pl.nn);
         // every entry a batch may read is a table: zero runs, coefficients,
         // zeros past a window (a cut-short batch reads up to kSwsU - 1 entries
         // on, and multiplies them by zero rows: the zero table gives 0)
-        for (int i = tid; i < nn * RW + kSwsU; i += blockDim.x) {
+        for (int i = tid; !G && i < nn * RW + kSwsU; i += blockDim.x) {
             const int v = i / RW, q = i - v * RW - kSwsU;
             CoefTab ct{0u, 0u, 0u, 0u, 0u};
             if (q >= 0 && v < nn && (uint32_t)q < pl.fe[v].y - pl.fe[v].x) ct = make_coef_tab(CB[v * W + q]);
@@ -390,17 +485,17 @@ __global__ __launch_bounds__(512) void sw_stream_kernel(SwStreamArgs a) {
             const uint32_t loff = min(cu, a.ncu - 1) * 4u * C;
             for (int p = 0; p < P; p++) {
                 switch (A) {
-                case 1: sws_pass<1, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 2: sws_pass<2, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 3: sws_pass<3, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                case 1: sws_pass<1, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                case 2: sws_pass<2, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                case 3: sws_pass<3, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
 #if FECGPU_SWS_AMAX > 4
-                case 4: sws_pass<4, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 5: sws_pass<5, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 6: sws_pass<6, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 7: sws_pass<7, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                default: sws_pass<8, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                case 4: sws_pass<4, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                case 5: sws_pass<5, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                case 6: sws_pass<6, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                case 7: sws_pass<7, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                default: sws_pass<8, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
 #else
-                default: sws_pass<4, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                default: sws_pass<4, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
 #endif
                 }
             }
@@ -442,15 +537,23 @@ uint64_t resident(const void *fn, int C, uint32_t block, uint32_t lds) {
 
 hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t s) {
     if (a.nrep == 0) return hipSuccess;
-    const void *fn = C == 2 ? reinterpret_cast<const void *>(sw_stream_kernel<2>)
-                            : reinterpret_cast<const void *>(sw_stream_kernel<1>);
+    const bool G = FECGPU_SWS_SGPR && a.gtab;
+    const void *fn = G ? (C == 2 ? reinterpret_cast<const void *>(sw_stream_kernel<2, true>)
+                                 : reinterpret_cast<const void *>(sw_stream_kernel<1, true>))
+                       : (C == 2 ? reinterpret_cast<const void *>(sw_stream_kernel<2, false>)
+                                 : reinterpret_cast<const void *>(sw_stream_kernel<1, false>));
     const int W = std::max(1, a.max_window);
     a.max_window = W;
     // column passes of at most 512 lanes, as even as 64-lane waves allow
     const uint32_t passes = (a.ncu + 511) / 512;
     a.cpass = ((a.ncu + passes - 1) / passes + 63) / 64 * 64;
-    a.segcap = (int)std::max<uint32_t>(1, std::min<uint32_t>(kSwSeg, budget / sw_stream_rep_lds(W)));
-    a.lds = sw_stream_lds(a.segcap, W);
+    a.segcap = G ? kSwSeg : (int)std::max<uint32_t>(1, std::min<uint32_t>(kSwSeg, budget / sw_stream_rep_lds(W)));
+    a.lds = G ? 0u : sw_stream_lds(a.segcap, W);
+    if (G) {
+        hipLaunchKernelGGL(sws_tab_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+        const hipError_t e0 = hipGetLastError();
+        if (e0 != hipSuccess) return e0;
+    }
     hipError_t e = hipSuccess;
     if (a.lds > 64u * 1024u) {
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds);
@@ -463,10 +566,16 @@ hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t 
     a.segcap = (int)std::max<uint64_t>(1, (a.nrep + R * rounds - 1) / (R * rounds));
     a.nseg = (a.nrep + a.segcap - 1) / a.segcap;
     const uint64_t grid = std::min<uint64_t>(a.nseg, R);
-    if (C == 2)
-        hipLaunchKernelGGL(sw_stream_kernel<2>, dim3((unsigned)grid), dim3(a.cpass), a.lds, s, a);
-    else
-        hipLaunchKernelGGL(sw_stream_kernel<1>, dim3((unsigned)grid), dim3(a.cpass), a.lds, s, a);
+    if (G) {
+        if (C == 2)
+            hipLaunchKernelGGL((sw_stream_kernel<2, true>), dim3((unsigned)grid), dim3(a.cpass), 0, s, a);
+        else
+            hipLaunchKernelGGL((sw_stream_kernel<1, true>), dim3((unsigned)grid), dim3(a.cpass), 0, s, a);
+    } else if (C == 2) {
+        hipLaunchKernelGGL((sw_stream_kernel<2, false>), dim3((unsigned)grid), dim3(a.cpass), a.lds, s, a);
+    } else {
+        hipLaunchKernelGGL((sw_stream_kernel<1, false>), dim3((unsigned)grid), dim3(a.cpass), a.lds, s, a);
+    }
     return hipGetLastError();
 }
 
