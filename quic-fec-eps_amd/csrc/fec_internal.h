@@ -327,6 +327,10 @@ constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
 #define FECGPU_SWD_SOLVE_LIST 1  // fused plan: solve jobs in a compact list (one atomic per system)
                                  // instead of slots per unknown (the solve pass walks every slot)
 #endif
+#ifndef FECGPU_SWD_ONEPASS
+#define FECGPU_SWD_ONEPASS 1  // fused plan: the system pass takes systems of up to 64 unknowns /
+                              // 96 equations itself (mid-size LDS per wave), no separate mid pass
+#endif
 #ifndef FECGPU_SWD_FUSED
 #define FECGPU_SWD_FUSED 1  // the decode plan as one look-back launch (sw_dec_plan_kernel) instead of
                             // a memset and five passes
@@ -344,7 +348,9 @@ struct SwDecCtr {  // per call, zeroed before the first kernel
     // fused plan: solve outputs handed out, 8 per solve job (a system takes
     // ceil(determined / 8) jobs at once: job j writes outputs 8j ..), so the
     // solve pass walks only real jobs (nsolout >> 3 of them)
-    uint32_t nsolout, pad0, pad1, pad2, pad3;
+    uint32_t nsolout;
+    uint32_t nstart;                   // fused plan: larger systems' first unknowns listed (starts)
+    uint32_t pad0, pad1, pad2;
     unsigned long long nlog;           // long-system log entries
 };
 // one long system: lost[x0 .. x0 + e), candidate repairs [t_lo, t_hi); its
@@ -417,6 +423,8 @@ struct SwDecArgs {
     uint32_t epoch;
     uint8_t *lkind;       // [nsrc] per lost index, from the fused plan: 0 member of a larger
                           // system, 1 recovered alone, 2 a larger system's first, 3 alone, lost
+    uint32_t *starts;     // [nsrc] fused plan: lost indices of the larger systems' first unknowns
+                          // (ctr->nstart of them, in no particular order)
 };
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s);    // statuses, lost list, systems
 hipError_t launch_sw_dec_long(const SwDecArgs &a, hipStream_t s);    // long systems: logs, syndrome jobs

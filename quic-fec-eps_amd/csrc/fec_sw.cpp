@@ -214,7 +214,7 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // bookkeeping).
 struct DecBlock {
     size_t o_reach, o_rcnt, o_chunk, o_lost, o_reachL, o_ctr, o_synj, o_syno, o_coef, o_solj, o_solo, o_solc,
-        o_long, o_mid, o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, o_lkind, total;
+        o_long, o_mid, o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, o_lkind, o_starts, total;
     uint64_t long_cap, piv_cap;
 };
 DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
@@ -254,6 +254,7 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
     L.o_pivhi = take(L.piv_cap * 4);
     L.o_pivt = take(L.piv_cap * 4);
     L.o_lkind = take(FECGPU_SWD_FUSED ? nsrc : 0);
+    L.o_starts = take(FECGPU_SWD_FUSED ? nsrc * 4 : 0);
     L.total = o;
     return L;
 }
@@ -308,6 +309,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.pivhi = reinterpret_cast<uint32_t *>(b + L.o_pivhi);
     a.pivt = reinterpret_cast<uint32_t *>(b + L.o_pivt);
     a.lkind = b + L.o_lkind;
+    a.starts = reinterpret_cast<uint32_t *>(b + L.o_starts);
     a.pivdata = static_cast<uint8_t *>(ppiv);
     a.piv_cap = L.piv_cap;
     a.src = src;

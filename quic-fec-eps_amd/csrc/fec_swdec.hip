@@ -752,6 +752,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64], s_r[kBlock / 64], s_w[kBlock / 64];
     __shared__ uint32_t s_lh[kBlock / 64], s_lv[kBlock / 64];
     __shared__ uint32_t s_chunk, s_bad, s_wmb;
+    __shared__ uint32_t s_nst, s_nsg, s_stbase;  // the chunk's larger-system starts, singles recovered
     __shared__ uint64_t s_t0, s_t1, s_tb;
     __shared__ LbRec s_excl, s_agg;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -763,6 +764,8 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         s_chunk = atomicAdd(&a.lb_ticket[0], 1u) % nch;
         s_bad = 0;
         s_wmb = 0;
+        s_nst = 0;
+        s_nsg = 0;
     }
     for (int i = tid; i < kPlanChunk; i += kBlock) {
         s_reach[i] = 0;
@@ -981,15 +984,6 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         }
         s_excl = ex;
         s_agg = agg;
-        if (c == nch - 1) {  // the call's counters (nothing was cleared before the launch)
-            const LbRec tot = lb_join(ex, agg);
-            SwDecCtr z{};
-            z.nlost = tot.lost;
-            z.wmax = tot.wme & 0xFFFFu;
-            z.err = tot.wme >> 16;
-            *a.ctr = z;
-            if (z.err && a.sticky) atomicOr(&a.sticky->err, z.err);
-        }
     }
     __syncthreads();
     const LbRec ex = s_excl;
@@ -1134,20 +1128,50 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         }
         a.syn_jobs[a.nrep + u] = J;
         a.lkind[u] = kind;
+        if (kind == 1) atomicAdd(&s_nsg, 1u);
+        if (kind == 2) s_rcnt[atomicAdd(&s_nst, 1u)] = u;  // s_rcnt is free after the lost list
     }
-    // the last block out resets the tickets for the next launch
+    // the chunk's larger-system starts onto the call's list (one atomic per block;
+    // ticket[2] / [3] count starts / singles and are cleared by the last block out)
     __syncthreads();
-    if (tid == 0 && atomicAdd(&a.lb_ticket[1], 1u) == nch - 1) {
-        atomicExch(&a.lb_ticket[0], 0u);
-        atomicExch(&a.lb_ticket[1], 0u);
+    if (tid == 0) {
+        s_stbase = s_nst ? atomicAdd(&a.lb_ticket[2], s_nst) : 0u;
+        if (s_nsg) atomicAdd(&a.lb_ticket[3], s_nsg);
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < s_nst; k += kBlock) a.starts[s_stbase + k] = s_rcnt[k];
+    // the last block out writes the call's counters (nothing was cleared before
+    // the launch) and resets the tickets for the next launch
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();
+        if (atomicAdd(&a.lb_ticket[1], 1u) == nch - 1) {
+            __threadfence();
+            const LbRec tot = lb_read(a.lb_inc + 2 * (size_t)(nch - 1));
+            SwDecCtr z{};
+            z.nlost = tot.lost;
+            z.wmax = tot.wme & 0xFFFFu;
+            z.err = tot.wme >> 16;
+            z.nstart = atomicExch(&a.lb_ticket[2], 0u);
+            z.recovered = atomicExch(&a.lb_ticket[3], 0u);
+            *a.ctr = z;
+            if (z.err && a.sticky) atomicOr(&a.sticky->err, z.err);
+            atomicExch(&a.lb_ticket[0], 0u);
+            atomicExch(&a.lb_ticket[1], 0u);
+        }
     }
 }
 
 // A wave per lost source; the waves at a system start find its extent and
 // solve it (tiny) or queue it (mid, long).
+#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS
+constexpr int kSysE = kSwSmallE, kSysP = kSwSmallP;  // the system pass's LDS per wave
+#else
+constexpr int kSysE = kSwTinyE, kSysP = kSwTinyP;
+#endif
 __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     __shared__ GfLds g;
-    __shared__ SysLds<kSwTinyE, kSwTinyP> s_sys[kBlock / 64];
+    __shared__ SysLds<kSysE, kSysP> s_sys[kBlock / 64];
     gf_load(g);
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1155,14 +1179,14 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     const uint32_t nlost = a.ctr->nlost, wmax = max(1u, a.ctr->wmax);
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     uint32_t rec = 0, maxin = 0;  // this wave's recovered count, widest solve
-    for (uint64_t x = (uint64_t)blockIdx.x * (kBlock / 64) + wave; x < nlost; x += nwaves) {
 #if FECGPU_SWD_FUSED
-        // the plan classified every lost source and solved the one-unknown systems
-        const uint32_t kind = a.lkind[x];
-        rec += kind == 1u;
-        if (kind != 2u) continue;  // uniform
+    // the plan solved the one-unknown systems and listed the larger ones' starts
+    const uint32_t nstart = a.ctr->nstart;
+    for (uint64_t k = (uint64_t)blockIdx.x * (kBlock / 64) + wave; k < nstart; k += nwaves) {
+        const uint64_t x = a.starts[k];
         const uint32_t lx = a.lost[x];
 #else
+    for (uint64_t x = (uint64_t)blockIdx.x * (kBlock / 64) + wave; x < nlost; x += nwaves) {
         const uint32_t lx = a.lost[x];
         if (x > 0 && a.reachL[x - 1] > lx) continue;  // not a system start (uniform)
 #endif
@@ -1181,7 +1205,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
         const uint32_t last = a.lost[x + e - 1];
         // candidate repairs: fss in [lx - wmax + 1, last]
         const uint64_t t_lo = a.rcnt[lx >= wmax ? lx - wmax + 1 : 0], t_hi = a.rcnt[(uint64_t)last + 1];
-        sys_one<kSwTinyE, kSwTinyP, false>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin);
+        // one pass (FECGPU_SWD_ONEPASS): up to the mid size here, longer ones to the long pass
+        sys_one<kSysE, kSysP, FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi,
+                                                                      lane, rec, maxin);
     }
     block_counts(a, rec, maxin, lane, wave);
 }
@@ -1803,10 +1829,16 @@ hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
 #endif
         // a wave per lost source at most; persistent beyond what fits the chip
         const uint64_t want = (a.nsrc + kBlock / 64 - 1) / (kBlock / 64);
+#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS
+        // mid-size LDS (64 KB per block): two blocks per CU
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 2));
+        hipLaunchKernelGGL(sw_dec_sys_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+#else
         const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 6));
         hipLaunchKernelGGL(sw_dec_sys_kernel, dim3(grid), dim3(kBlock), 0, s, a);
         hipLaunchKernelGGL(sw_dec_mid_kernel, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(a.long_cap, (uint64_t)cu_count() * 2))),
                            dim3(kBlock), 0, s, a);
+#endif
     }
     return hipGetLastError();
 }
