@@ -1210,8 +1210,9 @@ ssize_t ctx_sw_lookback(fecgpu_ctx *ctx, uint64_t nchunk, SwLookback *lb, uint32
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
     auto &st = ctx->sw_lb[dev];
-    // layout: ticket (256 B), flags [cap], aggregates [cap], inclusive [cap]
-    auto bytes = [](uint64_t cap) { return 256 + cap * 4 + cap * 32; };
+    // layout: tickets (256 B), flags [cap] u32, aggregates [cap] and inclusive
+    // prefixes [cap], 32 B (two uint4) per chunk each (fec_swdec.hip LbRec)
+    auto bytes = [](uint64_t cap) { return 256 + cap * 4 + cap * 2 * kLbRecBytes; };
     if (st.nchunk < nchunk || st.epoch >= (1u << 29)) {
         const uint64_t cap = (std::max<uint64_t>(nchunk, std::max<uint64_t>(256, st.nchunk + st.nchunk / 2)) + 3) & ~3ull;
         if (st.mem) {
@@ -1229,7 +1230,7 @@ ssize_t ctx_sw_lookback(fecgpu_ctx *ctx, uint64_t nchunk, SwLookback *lb, uint32
     lb->ticket = reinterpret_cast<uint32_t *>(m);
     lb->flag = reinterpret_cast<uint32_t *>(m + 256);
     lb->agg = reinterpret_cast<uint4 *>(m + 256 + st.nchunk * 4);
-    lb->inc = lb->agg + st.nchunk;
+    lb->inc = lb->agg + st.nchunk * (kLbRecBytes / sizeof(uint4));
     *epoch = ++st.epoch;
     return 0;
 }

@@ -419,7 +419,7 @@ struct SwDecArgs {
     // prefixes, and the ticket counter that orders the chunks
     uint32_t *lb_flag;
     uint4 *lb_agg, *lb_inc;
-    uint32_t *lb_ticket;  // [0] next chunk, [1] blocks done
+    uint32_t *lb_ticket;  // [0] next chunk, [1] blocks done, [2] starts listed, [3] singles, [4] error bits
     uint32_t epoch;
     uint8_t *lkind;       // [nsrc] per lost index, from the fused plan: 0 member of a larger
                           // system, 1 recovered alone, 2 a larger system's first, 3 alone, lost
@@ -477,8 +477,9 @@ ssize_t ctx_sw_sticky(fecgpu_ctx *ctx, SwSticky **p);
 // one state per device serves them all.
 struct SwLookback {
     uint32_t *flag, *ticket;
-    uint4 *agg, *inc;
+    uint4 *agg, *inc;  // kLbRecBytes per chunk each
 };
+constexpr uint64_t kLbRecBytes = 32;  // a chunk's look-back record: two uint4 (fec_swdec.hip LbRec)
 ssize_t ctx_sw_lookback(fecgpu_ctx *ctx, uint64_t nchunk, SwLookback *lb, uint32_t *epoch);
 // waits until the current device's sliding-window calls issued so far have finished
 ssize_t ctx_sw_wait(fecgpu_ctx *ctx);

@@ -699,7 +699,8 @@ __device__ __forceinline__ LbRec lb_join(const LbRec &x, const LbRec &y) {  // x
 __device__ __forceinline__ uint32_t lb_flag_load(const uint32_t *f) {
     return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
 }
-// records are two uint4 per chunk (lb_agg / lb_inc [2 * chunk])
+// records are two uint4 per chunk (lb_agg / lb_inc [2 * chunk]; kLbRecBytes)
+static_assert(kLbRecBytes == 2 * sizeof(uint4), "look-back record size");
 __device__ __forceinline__ void lb_publish(const SwDecArgs &a, uint32_t c, const LbRec &r, uint32_t state) {
     uint32_t *dst = reinterpret_cast<uint32_t *>((state == kLbInc ? a.lb_inc : a.lb_agg) + 2 * (size_t)c);
     const uint32_t v[5] = {r.lost, r.reach, r.rep, r.wme, r.L};
@@ -1139,7 +1140,12 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         if (s_nsg) atomicAdd(&a.lb_ticket[3], s_nsg);
     }
     __syncthreads();
-    for (uint32_t k = tid; k < s_nst; k += kBlock) a.starts[s_stbase + k] = s_rcnt[k];
+    // (a count left behind by an aborted launch: raise an error instead of writing past the list)
+    if ((uint64_t)s_stbase + s_nst > a.nsrc) {
+        if (tid == 0) atomicOr(&a.lb_ticket[4], kSwErrInternal);  // into the counters by the last block out
+    } else {
+        for (uint32_t k = tid; k < s_nst; k += kBlock) a.starts[s_stbase + k] = s_rcnt[k];
+    }
     // the last block out writes the call's counters (nothing was cleared before
     // the launch) and resets the tickets for the next launch
     __syncthreads();
@@ -1151,8 +1157,8 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             SwDecCtr z{};
             z.nlost = tot.lost;
             z.wmax = tot.wme & 0xFFFFu;
-            z.err = tot.wme >> 16;
-            z.nstart = atomicExch(&a.lb_ticket[2], 0u);
+            z.err = (tot.wme >> 16) | atomicExch(&a.lb_ticket[4], 0u);
+            z.nstart = min(atomicExch(&a.lb_ticket[2], 0u), (uint32_t)tot.lost);
             z.recovered = atomicExch(&a.lb_ticket[3], 0u);
             *a.ctr = z;
             if (z.err && a.sticky) atomicOr(&a.sticky->err, z.err);

@@ -62,7 +62,7 @@ for s in "$@"; do
         swtests) step swtests 300 python -u -m pytest tests/test_gpu_swconn.py tests/test_gpu_sw.py -q -x \
                      --timeout 120 --timeout-method thread -p no:cacheprovider ;;
         swnew) step swnew 240 python -u -m pytest tests/test_gpu_sw.py -q -x -k \
-                   "two_repairs or many_repairs or compaction or async_error or log_overflow or long_path" \
+                   "two_repairs or many_repairs or compaction or async_error or log_overflow or long_path or config7_scale or full_size" \
                    --timeout 60 --timeout-method thread -p no:cacheprovider ;;
         streamtests) step streamtests 300 python -u -m pytest tests/test_gpu_swstream.py -q -x \
                      --timeout 120 --timeout-method thread -p no:cacheprovider ;;

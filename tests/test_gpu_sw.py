@@ -516,14 +516,15 @@ def test_sw_decode_host_pointers_and_args(ctx):
                       flags=fecgpu.F_HOST_PTRS)
 
 
-@pytest.mark.parametrize("loss", [0.02, 0.10])
-def test_sw_full_size_roundtrip(ctx, loss):
-    """131,072 sources of 1200 B (157 MB), a repair after every 8 over the last 32, 2 %
+@pytest.mark.parametrize("loss,nsrc", [(0.02, 131072), (0.10, 131072), (0.02, 524288)])
+def test_sw_full_size_roundtrip(ctx, loss, nsrc):
+    """131,072 or 524,288 (config 7's stream: 256 chunks of the plan's look-back)
+    sources of 1200 B, a repair after every 8 over the last 32, 2 %
     (config 7's rate) or 10 % i.i.d. loss of sources and repairs: every source the
     decoder reports recovered equals the original, and every status equals the
     oracle's global decode over the whole stream (at 10 % the repairs, 1 per 8
     sources, no longer cover the losses: long linked systems, mostly rank deficient)."""
-    nsrc, L, stride, k, W = 131072, 1200, 1200, 8, 32
+    L, stride, k, W = 1200, 1200, 8, 32  # 524,288: config 7's stream (256 plan chunks)
     g = torch.Generator(device="cuda").manual_seed(7)
     d_src = torch.randint(0, 256, (nsrc, stride), dtype=torch.uint8, device="cuda", generator=g)
     h = N.sw_schedule(nsrc, k, W, key0=0)
@@ -550,6 +551,39 @@ def test_sw_full_size_roundtrip(ctx, loss):
     ost, on = O.sw_decode_banded(od, sp, d_rep.cpu().numpy(), rp, hdr, L)
     assert np.array_equal(st, ost) and n == on
     assert np.array_equal(od[ost == 0], full[ost == 0])
+
+
+def test_sw_decode_device_config7_scale(ctx):
+    """The bench's path at config 7's size: asynchronous fecgpu_sw_decode_device
+    (bookkeeping on the device) raises no error flag and leaves exactly the
+    statuses and bytes of the synchronous host-bookkeeping decode."""
+    nsrc, L, stride, k, W = 524288, 1200, 1200, 8, 32
+    g = torch.Generator(device="cuda").manual_seed(11)
+    d_src = torch.randint(0, 256, (nsrc, stride), dtype=torch.uint8, device="cuda", generator=g)
+    hdr = hdr_array(N.sw_schedule(nsrc, k, W, key0=3))
+    d_hdr = torch.from_numpy(hdr.view(np.uint8).copy()).cuda()
+    d_rep = torch.empty((len(hdr), stride), dtype=torch.uint8, device="cuda")
+    ctx.sw_encode(d_src, d_rep, d_hdr, nsrc=nsrc, nrep=len(hdr), sym_len=L, stride=stride, max_window=W)
+    rng = np.random.default_rng(2)
+    sp = (rng.random(nsrc) >= 0.02).astype(np.uint8)
+    rp = (rng.random(len(hdr)) >= 0.02).astype(np.uint8)
+    lost = torch.from_numpy(sp == 0).cuda()
+    orig = d_src.clone()
+    d_src[lost] = 0xCD
+    a_src = d_src.clone()
+    st = np.zeros(nsrc, np.uint8)
+    n = ctx.sw_decode(d_src, sp, d_rep, rp, hdr, st, nsrc=nsrc, nrep=len(hdr), sym_len=L, stride=stride)
+    assert ctx.sw_decode_errors() == 0
+    d_st = torch.full((nsrc,), 9, dtype=torch.uint8, device="cuda")
+    for _ in range(3):  # back to back, as the bench's timed loop
+        assert ctx.sw_decode_device(a_src, torch.from_numpy(sp).cuda(), d_rep, torch.from_numpy(rp).cuda(), d_hdr,
+                                    d_st, nsrc=nsrc, nrep=len(hdr), sym_len=L, stride=stride) == 0
+    assert ctx.sw_decode_errors() == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(d_st.cpu().numpy(), st)
+    assert torch.equal(a_src, d_src)
+    ok = torch.from_numpy(st == 0).cuda()
+    assert torch.equal(d_src[ok], orig[ok]) and n > 0.9 * (sp == 0).sum()
 
 
 def test_bench_config7_batch(ctx):
