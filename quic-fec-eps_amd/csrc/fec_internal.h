@@ -324,7 +324,7 @@ constexpr int kSwRows = 256;    // long systems: row slots (more rows alive at o
 constexpr int kSwChunk = 4096;  // sources per planning chunk (FECGPU_SWD_FUSED 0)
 constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
 #ifndef FECGPU_SWD_SOLVE_LIST
-#define FECGPU_SWD_SOLVE_LIST 1  // fused plan: solve jobs in a compact list (one atomic per system)
+#define FECGPU_SWD_SOLVE_LIST 0  // fused plan: solve jobs in a compact list (one atomic per system: 24 us slower on cfg7, r04)
                                  // instead of slots per unknown (the solve pass walks every slot)
 #endif
 #ifndef FECGPU_SWD_ONEPASS

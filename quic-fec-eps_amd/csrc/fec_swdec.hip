@@ -350,7 +350,7 @@ __device__ __forceinline__ bool holds(const SwDecArgs &a, const fecgpu_sw_repair
 // t_last (the repairs in between that are not its equations get coefficient
 // 0: the ranges of two systems never interleave, since a repair between two
 // equations of one system that held a lost source of another would link them).
-constexpr int kSwTinyE = 16, kSwTinyP = 48;
+[[maybe_unused]] constexpr int kSwTinyE = 16, kSwTinyP = 48;
 #ifndef FECGPU_SWD_COEF
 #define FECGPU_SWD_COEF 1  // coefficients of the repairs holding lost sources drawn by a thread each, up front
 #endif
@@ -958,33 +958,61 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             if (s_lh[w]) agg.L = s_lv[w];
         }
         if (s_bad) agg.wme |= kSwErrHeader << 16;
-        LbRec ex{0, 0, 0, 0, 0};
-        if (c == 0) {
-            lb_publish(a, c, agg, kLbInc);
-        } else {
-            lb_publish(a, c, agg, kLbAgg);
-            uint32_t spins = 0;
-            for (int64_t q = (int64_t)c - 1; q >= 0;) {
-                const uint32_t f = lb_flag_load(&a.lb_flag[q]);
-                if ((f >> 2) != a.epoch || (f & 3u) == 0) {
-                    // bounded: a predecessor that never publishes (which the
-                    // dispatch order rules out) ends as an error, not a hang
-                    if (++spins == (1u << 24)) {
-                        ex.wme |= kSwErrInternal << 16;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                const bool inc = (f & 3u) == kLbInc;
-                ex = lb_join(lb_read((inc ? a.lb_inc : a.lb_agg) + 2 * (size_t)q), ex);
-                if (inc) break;
-                q--;
-            }
-            lb_publish(a, c, lb_join(ex, agg), kLbInc);
-        }
-        s_excl = ex;
         s_agg = agg;
+        lb_publish(a, c, agg, c == 0 ? kLbInc : kLbAgg);
+    }
+    __syncthreads();
+    // decoupled look-back by wave 0, 64 predecessors per round: lane i polls
+    // chunk base - i; once every one of them has published, the records up to
+    // the nearest inclusive prefix are joined (lanes in chunk order) and the
+    // window moves back 64 chunks if there was none.  (One lane walking back
+    // serially cost a dependent load per predecessor: ~0.1 ms at 256 chunks.)
+    if (wave == 0) {
+        LbRec ex{0, 0, 0, 0, 0};
+        uint32_t spins = 0;
+        for (int64_t base = (int64_t)c - 1; base >= 0;) {
+            const int64_t q = base - lane;
+            const bool valid = q >= 0;
+            const uint32_t f = valid ? lb_flag_load(&a.lb_flag[q]) : 0u;
+            const bool ready = !valid || ((f >> 2) == a.epoch && (f & 3u) != 0);
+            if (__ballot(!ready)) {
+                // bounded: a predecessor that never publishes (which the
+                // dispatch order rules out) ends as an error, not a hang
+                if (++spins == (1u << 22)) {
+                    ex.wme |= kSwErrInternal << 16;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            const uint64_t incm = __ballot(valid && (f & 3u) == kLbInc);
+            const int n = incm ? __ffsll((unsigned long long)incm) : (int)min<int64_t>(64, base + 1);
+            LbRec r{0, 0, 0, 0, 0};
+            if (lane < n) r = lb_read((lane == n - 1 && incm ? a.lb_inc : a.lb_agg) + 2 * (size_t)q);
+            // ordered join: a higher lane holds an earlier chunk
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                LbRec o;
+                o.lost = __shfl_down(r.lost, d);
+                o.reach = __shfl_down(r.reach, d);
+                o.rep = __shfl_down(r.rep, d);
+                o.wme = __shfl_down(r.wme, d);
+                o.L = __shfl_down(r.L, d);
+                if (lane + d < 64 && (lane & (2 * d - 1)) == 0) r = lb_join(o, r);
+            }
+            r.lost = __shfl(r.lost, 0);
+            r.reach = __shfl(r.reach, 0);
+            r.rep = __shfl(r.rep, 0);
+            r.wme = __shfl(r.wme, 0);
+            r.L = __shfl(r.L, 0);
+            ex = lb_join(r, ex);
+            if (incm) break;
+            base -= 64;
+        }
+        if (lane == 0) {
+            if (c > 0) lb_publish(a, c, lb_join(ex, s_agg), kLbInc);
+            s_excl = ex;
+        }
     }
     __syncthreads();
     const LbRec ex = s_excl;
@@ -1078,20 +1106,24 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             };
             const uint64_t ta = rfirst(lo), te = rfirst(i + 1);
             for (uint64_t t = ta; t < te; t++) {
-                if (!a.rep_present[t]) continue;
+                const uint8_t rpt = a.rep_present[t];  // both loads in one round trip
                 const fecgpu_sw_repair h = a.hdr[t];
+                if (!rpt) continue;
                 if (h.fss > i || h.fss + h.nss <= i) continue;
                 const uint32_t j = (uint32_t)(i - h.fss);
-                const uint8_t cj = h.dt == 15 ? 1 : coef_at(h, j);  // DT 15: never zero
+                const uint8_t cj = coef_at(h, j);
                 if (!cj) continue;
-                // the job: t's coefficients times 1/c (0 at x), t's row times 1/c
+                // the job: t's coefficients times 1/c (0 at x), t's row times 1/c;
+                // the row drawn again and scaled 4 bytes at a time as it goes out
                 const uint64_t slot = a.nrep + u;
                 uint8_t *row = a.coef + slot * kSwCoefPitch;
+                const uint32_t iv = c_gfs.exp[255 - c_gfs.log[cj]];
+                uint32_t tab[5];
+                set_tab(tab, iv);
                 Tinymt32 st;
                 tinymt32_init(st, h.key);
                 const uint32_t dt = h.dt;
-                uint32_t word = 0, cx = 0;
-                uint32_t tab[5];
+                uint32_t word = 0;
                 for (int q = 0; q < (int)h.nss; q++) {
                     uint32_t cq = 0;
                     if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
@@ -1099,22 +1131,18 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                             cq = tinymt32_u32(st) & 0xFFu;
                         } while (cq == 0);
                     }
-                    if ((uint32_t)q == j) {
-                        cx = cq;
-                        cq = 0;
-                    }
+                    if ((uint32_t)q == j) cq = 0;
                     word |= cq << (8 * (q & 3));
                     if ((q & 3) == 3) {
-                        reinterpret_cast<uint32_t *>(row)[q >> 2] = word;
+                        reinterpret_cast<uint32_t *>(row)[q >> 2] = tmul(word, tab);
                         word = 0;
                     }
                 }
-                if (h.nss & 3) reinterpret_cast<uint32_t *>(row)[h.nss >> 2] = word;
-                const uint32_t iv = c_gfs.exp[255 - c_gfs.log[cx]];
-                set_tab(tab, iv);
-                for (uint32_t q = 0; q < ((uint32_t)h.nss + 3) / 4; q++)
-                    reinterpret_cast<uint32_t *>(row)[q] = tmul(reinterpret_cast<uint32_t *>(row)[q], tab);
-                row[h.nss] = (uint8_t)iv;  // the xor row's multiplier (nss < kSwCoefPitch)
+                // the last partial word, with the xor row's multiplier after the
+                // coefficients (nss < kSwCoefPitch)
+                uint32_t last = (h.nss & 3) ? tmul(word, tab) : 0u;
+                last |= iv << (8 * (h.nss & 3));
+                reinterpret_cast<uint32_t *>(row)[h.nss >> 2] = last;
                 J.in_off = h.fss * a.stride;
                 J.coef_off = slot * kSwCoefPitch;
                 J.out_list = slot;

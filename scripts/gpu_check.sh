@@ -28,12 +28,12 @@ step() {  # name timeout cmd...
 prof() {  # name config extra-args...
     local name=$1 cfg=$2; shift 2
     step "$name" 600 rocprofv3 --kernel-trace --stats -f csv -d "gpurun_out/$name" -o run -- \
-        python bench.py --config "$cfg" --steps 20 --warmup 10 --cpu-seconds 0 "$@"
+        python bench.py --config "$cfg" --steps 20 --warmup 10 --cpu-seconds 0 --extra-configs 0 "$@"
 }
 pmc() {  # name config counters...
     local name=$1 cfg=$2; shift 2
     step "$name" 600 rocprofv3 --kernel-trace --pmc "$@" -f csv -d "gpurun_out/$name" -o run -- \
-        python bench.py --config "$cfg" --steps 3 --warmup 1 --cpu-seconds 0 --no-verify
+        python bench.py --config "$cfg" --steps 3 --warmup 1 --cpu-seconds 0 --no-verify --extra-configs 0
 }
 [ $# -eq 0 ] && set -- smoke pytest bench2 prof2
 for s in "$@"; do
@@ -99,6 +99,12 @@ for s in "$@"; do
             done ;;
         prof5) prof prof5 5 ;;
         prof7) prof prof7 7 ;;
+        prof7v)  # cfg7 rocprofv3 of every lib/libfecgpu_*.so variant (no check build)
+            for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
+                n=$(basename $v .so); n=${n#libfecgpu_}
+                [ "$n" = check ] && continue
+                FECGPU_LIB=$v prof prof7_$n 7
+            done ;;
         abvar7)  # cfg7: default build vs every lib/libfecgpu_*.so variant (no check build), interleaved 3 times
             for rep in 1 2 3; do
                 step abvar7_base_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
