@@ -205,6 +205,10 @@ struct CombArgs {
     // `budget` bytes of LDS hold at that width
     const uint32_t *nin_dev;
     int extra_shift;  // the device count counts 2^extra_shift units per job
+    // device-sized launch: job groups dealt round-robin over every workgroup
+    // instead of XCD-contiguous regions (a dense run of real jobs among empty
+    // slots would otherwise land on one XCD)
+    int interleave;
     uint32_t budget;
     // every job has the same coefficient block (a block code's parity rows:
     // wide encode): [nout_max][nin_max] at coef, its tables built once per

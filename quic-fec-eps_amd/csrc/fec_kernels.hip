@@ -2630,7 +2630,7 @@ hipError_t launch_comb(CombArgs a, int R, hipStream_t s) {
                        : R == 4 ? (const void *)comb_kernel<4> : (const void *)comb_kernel<8>;
         const uint64_t groups_max = nmax;  // at least one job per group
         grid = std::min<uint64_t>(groups_max, (uint64_t)resident_blocks(fn, lds) * 2);
-        a.nx = grid >= 8 ? 8 : 1;
+        a.nx = grid >= 8 && !a.interleave ? 8 : 1;
         grid = std::max<uint64_t>(a.nx, grid / a.nx * a.nx);
     } else {
         const uint64_t groups = (nmax + a.wpb - 1) / a.wpb;

@@ -344,6 +344,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
 #if FECGPU_SWD_FUSED
     sa.extra = &a.ctr->nlost;  // then a slot per lost source: the plan's one-unknown systems
     sa.extra_max = nsrc;
+    sa.interleave = 1;  // those are dense at the end: deal the groups round-robin
 #endif
     sa.ncol = ncol;
     sa.stride = stride;

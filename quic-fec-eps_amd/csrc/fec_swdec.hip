@@ -743,7 +743,24 @@ __device__ __forceinline__ uint8_t coef_at(const fecgpu_sw_repair &h, uint32_t j
     return (uint8_t)c;
 }
 
+#ifndef FECGPU_SWD_TRACE
+#define FECGPU_SWD_TRACE 0  // measurement aid: the plan kernel prints its phases' times (3 blocks)
+#endif
+#if FECGPU_SWD_TRACE
+#define SWD_TRACE(n)                                   \
+    do {                                               \
+        if (threadIdx.x == 0) s_tr[n] = wall_clock64(); \
+    } while (0)
+#else
+#define SWD_TRACE(n) \
+    do {             \
+    } while (0)
+#endif
 __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
+#if FECGPU_SWD_TRACE
+    __shared__ unsigned long long s_tr[12];
+    if (threadIdx.x == 0) s_tr[0] = wall_clock64();
+#endif
     __shared__ uint32_t s_reach[kPlanChunk], s_rcnt[kPlanChunk];
     __shared__ uint32_t s_lpos[kPlanChunk], s_rl[kPlanChunk];  // per local lost source: position, reachL
     __shared__ uint32_t s_rf[kPlanChunk + 1];                  // repfirst of the chunk's sources (and of i1)
@@ -774,6 +791,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     }
     s_rcb[tid] = 0;
     __syncthreads();
+    SWD_TRACE(1);
     const uint32_t c = s_chunk;
     const uint64_t i0 = (uint64_t)c * kPlanChunk, i1 = min(i0 + kPlanChunk, a.nsrc);
     const uint64_t ib = i0 >= (uint64_t)kPlanHalo ? i0 - kPlanHalo : 0;  // back region [ib, i0)
@@ -800,6 +818,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     }
     if (__ballot(bad) && lane == 0) s_bad = 1;
     __syncthreads();
+    SWD_TRACE(2);
     const uint64_t t0 = s_t0, t1 = max(s_t0, s_t1), tb = min(s_tb, t0);
     // reach / repair counts of the chunk's sources and the back region's
     // repair counts; the widest received window among them (pivot searches)
@@ -852,20 +871,30 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         wv |= __shfl_xor(wv, 2);
         if ((tid & 3) == 0) s_bits[tid >> 2] = wv;
     }
-    if (tid < kPlanHalo / 32) {  // halo words
-        uint32_t wv = 0;
-        for (int j = 0; j < 32; j++) {
-            const uint64_t i = i1 + (uint64_t)tid * 32 + j;
-            if (i < a.nsrc && a.src_present[i] == 0) wv |= 1u << j;
+    if (wave == 0) {  // halo: 8 flags per lane of lanes 0-31, 4 lanes per word (full chunks only)
+        const bool hl = lane < kPlanHalo / 8 && n == (uint32_t)kPlanChunk;
+        uint32_t hw = 0;
+        if (hl) {
+            const uint64_t h0 = i1 + (uint64_t)lane * 8;
+            uint32_t m8 = 0;
+            if (vec && h0 + 8 <= a.nsrc) {  // one 8-byte load (the chunk is 8-aligned)
+                const uint2 pv = *reinterpret_cast<const uint2 *>(a.src_present + h0);
+                for (int j = 0; j < 8; j++) m8 |= ((((j < 4 ? pv.x : pv.y) >> (8 * (j & 3))) & 0xFFu) == 0 ? 1u : 0u) << j;
+            } else {
+                for (int j = 0; j < 8; j++) m8 |= (h0 + j < a.nsrc && a.src_present[h0 + j] == 0 ? 1u : 0u) << j;
+            }
+            hw = m8 << ((lane & 3) * 8);
         }
-        // a short last chunk: its halo follows its last source directly
-        if (n == (uint32_t)kPlanChunk) s_bits[kPlanChunk / 32 + tid] = wv;
+        hw |= __shfl_xor(hw, 1);  // the whole wave takes part in the shuffles
+        hw |= __shfl_xor(hw, 2);
+        if (hl && (lane & 3) == 0) s_bits[kPlanChunk / 32 + (lane >> 2)] = hw;
     }
     if (n < (uint32_t)kPlanChunk) {  // last chunk (nothing past nsrc): clear the tail words
         for (uint32_t w = tid; w < (kPlanChunk + kPlanHalo) / 32; w += kBlock)
             if (w * 32 >= ((n + 31) & ~31u)) s_bits[w] = 0;
     }
     __syncthreads();
+    SWD_TRACE(3);
     // per thread: its 8 sources' lost count, max reach, repair count
     uint32_t cnt = __popc(lostm), tm = 0, tr = 0;
     for (int j = 0; j < kPlanPer; j++)
@@ -923,6 +952,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         }
     }
     __syncthreads();
+    SWD_TRACE(4);
     uint32_t wc = 0, wmx = 0, wr = 0;
     for (int w = 0; w < wave; w++) {
         wc += s_c[w];
@@ -948,6 +978,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         }
     }
     __syncthreads();
+    SWD_TRACE(5);
     if (tid == 0) {
         LbRec agg{0, 0, 0, 0, 0};
         for (int w = 0; w < kBlock / 64; w++) {
@@ -962,6 +993,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         lb_publish(a, c, agg, c == 0 ? kLbInc : kLbAgg);
     }
     __syncthreads();
+    SWD_TRACE(6);
     // decoupled look-back by wave 0, 64 predecessors per round: lane i polls
     // chunk base - i; once every one of them has published, the records up to
     // the nearest inclusive prefix are joined (lanes in chunk order) and the
@@ -1015,6 +1047,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         }
     }
     __syncthreads();
+    SWD_TRACE(7);
     const LbRec ex = s_excl;
     // lost list, rank / repfirst (as sw_dec_lost_kernel); positions and reachL
     // of the chunk's lost sources in LDS for the one-unknown systems below
@@ -1074,6 +1107,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         if (before(hi) > before(lo)) draw_row(a, t, h);
     }
     __syncthreads();
+    SWD_TRACE(8);
     // the chunk's lost sources: one-unknown systems solved, the rest classified
     const uint32_t nl = s_agg.lost, wmb_all = s_wmb;
     for (uint32_t k = tid; k < nl; k += kBlock) {
@@ -1163,6 +1197,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     // the chunk's larger-system starts onto the call's list (one atomic per block;
     // ticket[2] / [3] count starts / singles and are cleared by the last block out)
     __syncthreads();
+    SWD_TRACE(9);
     if (tid == 0) {
         s_stbase = s_nst ? atomicAdd(&a.lb_ticket[2], s_nst) : 0u;
         if (s_nsg) atomicAdd(&a.lb_ticket[3], s_nsg);
@@ -1177,6 +1212,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     // the last block out writes the call's counters (nothing was cleared before
     // the launch) and resets the tickets for the next launch
     __syncthreads();
+    SWD_TRACE(10);
     if (tid == 0) {
         __threadfence();
         if (atomicAdd(&a.lb_ticket[1], 1u) == nch - 1) {
@@ -1194,6 +1230,15 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             atomicExch(&a.lb_ticket[1], 0u);
         }
     }
+#if FECGPU_SWD_TRACE
+    if (threadIdx.x == 0 && (s_chunk == 0 || s_chunk == nch / 2 || s_chunk == nch - 1)) {
+        const unsigned long long t11 = wall_clock64();
+        printf("swd plan chunk %u: %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu end %llu (start %llu)\n", s_chunk,
+               s_tr[1] - s_tr[0], s_tr[2] - s_tr[0], s_tr[3] - s_tr[0], s_tr[4] - s_tr[0], s_tr[5] - s_tr[0],
+               s_tr[6] - s_tr[0], s_tr[7] - s_tr[0], s_tr[8] - s_tr[0], s_tr[9] - s_tr[0], s_tr[10] - s_tr[0],
+               t11 - s_tr[0], s_tr[0]);
+    }
+#endif
 }
 
 // A wave per lost source; the waves at a system start find its extent and

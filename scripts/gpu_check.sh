@@ -93,16 +93,18 @@ for s in "$@"; do
                 step abdec_sweep_base_$rep 300 python scripts/code_sweep.py r8
                 for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
                     n=$(basename $v .so); n=${n#libfecgpu_}
-                    [ "$n" = check ] && continue
+                    case $n in check|trace) continue ;; esac
                     FECGPU_LIB=$v step abdec_sweep_${n}_$rep 300 python scripts/code_sweep.py r8
                 done
             done ;;
         prof5) prof prof5 5 ;;
         prof7) prof prof7 7 ;;
+        trace7) FECGPU_LIB=quic-fec-eps_amd/lib/libfecgpu_trace.so step trace7 300 python bench.py --config 7 \
+                    --steps 3 --warmup 1 --cpu-seconds 0 --no-verify --extra-configs 0 ;;
         prof7v)  # cfg7 rocprofv3 of every lib/libfecgpu_*.so variant (no check build)
             for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
                 n=$(basename $v .so); n=${n#libfecgpu_}
-                [ "$n" = check ] && continue
+                case $n in check|trace) continue ;; esac
                 FECGPU_LIB=$v prof prof7_$n 7
             done ;;
         abvar7)  # cfg7: default build vs every lib/libfecgpu_*.so variant (no check build), interleaved 3 times
@@ -110,7 +112,7 @@ for s in "$@"; do
                 step abvar7_base_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
                 for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
                     n=$(basename $v .so); n=${n#libfecgpu_}
-                    [ "$n" = check ] && continue
+                    case $n in check|trace) continue ;; esac
                     FECGPU_LIB=$v step abvar7_${n}_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
                 done
             done ;;
@@ -119,7 +121,7 @@ for s in "$@"; do
                 step abvar7l10_base_$rep 300 python bench.py --config 7 --steps 20 --warmup 5 --cpu-seconds 0 --no-verify --sw-loss 0.1
                 for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
                     n=$(basename $v .so); n=${n#libfecgpu_}
-                    [ "$n" = check ] && continue
+                    case $n in check|trace) continue ;; esac
                     FECGPU_LIB=$v step abvar7l10_${n}_$rep 300 python bench.py --config 7 --steps 20 --warmup 5 --cpu-seconds 0 --no-verify --sw-loss 0.1
                 done
             done ;;
