@@ -179,6 +179,7 @@ struct fecgpu_ctx {
         uint32_t epoch = 0;
     };
     std::map<int, LbState> sw_lb;  // fused decode plan's look-back state, per device
+    std::map<int, uint8_t *> rlc_tab;  // dense RFC 8681 coefficient table, per device (ctx_rlc_table)
     void *sw_host = nullptr;  // pinned staging of sliding-window decodes (ctx_sw_host)
     size_t sw_host_bytes = 0;
     // codes with k + r > 64: parity rows on each device, by (device, k, r, matrix, key, dt)
@@ -399,6 +400,10 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
     for (auto &kv : ctx->sw_lb) {
         (void)hipSetDevice(kv.first);
         if (kv.second.mem) (void)hipFree(kv.second.mem);
+    }
+    for (auto &kv : ctx->rlc_tab) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second);
     }
     for (auto &kv : ctx->wide_rows) {
         (void)hipSetDevice(std::get<0>(kv.first));
@@ -1232,6 +1237,25 @@ ssize_t ctx_sw_lookback(fecgpu_ctx *ctx, uint64_t nchunk, SwLookback *lb, uint32
     lb->agg = reinterpret_cast<uint4 *>(m + 256 + st.nchunk * 4);
     lb->inc = lb->agg + st.nchunk * (kLbRecBytes / sizeof(uint4));
     *epoch = ++st.epoch;
+    return 0;
+}
+
+ssize_t ctx_rlc_table(fecgpu_ctx *ctx, hipStream_t s, const uint8_t **tab) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    uint8_t *&t = ctx->rlc_tab[dev];
+    if (!t) {
+        void *m = nullptr;
+        HIP_TRY(hipMalloc(&m, kRlcTabBytes), "hipMalloc coefficient table");
+        hipError_t e = launch_rlc_table(static_cast<uint8_t *>(m), s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            (void)hipFree(m);
+            return dev_err(e, "coefficient table");
+        }
+        t = static_cast<uint8_t *>(m);
+    }
+    *tab = t;
     return 0;
 }
 

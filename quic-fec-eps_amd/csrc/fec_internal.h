@@ -256,6 +256,7 @@ struct SwEncCoefArgs {
     CombJob *jobs;
     uint8_t *coef;
     uint64_t *outs;
+    const uint8_t *rlc;  // nullable: the dense coefficient table (ctx_rlc_table)
 };
 hipError_t launch_sw_enc_coef(const SwEncCoefArgs &a, hipStream_t s);
 // job slots of an encode's scratch (group jobs, per-repair tail, and a
@@ -298,6 +299,7 @@ struct SwStreamArgs {
     // multiply tables in global memory, read by scalar loads (FECGPU_SWS_SGPR):
     // 4-entry tables (one SGPR feeds a v_perm), no LDS tables
     void *gtab;
+    const uint8_t *rlc;  // nullable: the dense coefficient table (ctx_rlc_table)
 };
 // [kSwStreamU zero entries][per repair: kSwStreamU zeros, max_window entries][kSwStreamU zeros], 16 B each
 inline uint64_t sw_stream_gtab_bytes(uint64_t nrep, int max_window) {
@@ -339,6 +341,17 @@ constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
 #define FECGPU_SWD_FUSED 1  // the decode plan as one look-back launch (sw_dec_plan_kernel) instead of
                             // a memset and five passes
 #endif
+
+#ifndef FECGPU_SW_RLCTAB
+#define FECGPU_SW_RLCTAB 1  // dense (dt 15) coefficient rows read from the ctx's table instead of
+                            // stepping TinyMT32 per coefficient (encode, decode plan, systems, long path)
+#endif
+// RFC 8681 coefficients at dt 15 depend on the repair key alone (a window takes
+// a prefix of the key's sequence): the table holds every key's 255, one
+// 256-byte row per key (byte 255 zero), 16 MiB per device (ctx_rlc_table)
+constexpr uint32_t kRlcRow = 256;
+constexpr uint64_t kRlcTabBytes = 65536ull * kRlcRow;
+hipError_t launch_rlc_table(uint8_t *tab, hipStream_t s);
 
 // SwDecCtr::err / SwSticky::err bits
 constexpr uint32_t kSwErrHeader = 1u;    // a bad or unordered header: the call recovers nothing
@@ -429,6 +442,7 @@ struct SwDecArgs {
                           // system, 1 recovered alone, 2 a larger system's first, 3 alone, lost
     uint32_t *starts;     // [nsrc] fused plan: lost indices of the larger systems' first unknowns
                           // (ctr->nstart of them, in no particular order)
+    const uint8_t *rlc;   // nullable: the dense coefficient table (kRlcRow bytes per repair key)
 };
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s);    // statuses, lost list, systems
 hipError_t launch_sw_dec_long(const SwDecArgs &a, hipStream_t s);    // long systems: logs, syndrome jobs
@@ -449,7 +463,8 @@ ssize_t set_dev_error(hipError_t e, const char *what);
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *jobs,
                        void *coef, void *outs, hipStream_t s, int group = 1,
-                       const fecgpu_sw_repair *hdr_host = nullptr, int stream = 0, void *gtab = nullptr);
+                       const fecgpu_sw_repair *hdr_host = nullptr, int stream = 0, void *gtab = nullptr,
+                       const uint8_t *rlc = nullptr);
 // the ctx's "sw_group" tuning (repairs per sliding-window encode job)
 int ctx_sw_group(const fecgpu_ctx *ctx);
 // the ctx's "sw_stream" tuning: 0 combine jobs, 1 / 2 the streaming encode
@@ -485,6 +500,9 @@ struct SwLookback {
 };
 constexpr uint64_t kLbRecBytes = 32;  // a chunk's look-back record: two uint4 (fec_swdec.hip LbRec)
 ssize_t ctx_sw_lookback(fecgpu_ctx *ctx, uint64_t nchunk, SwLookback *lb, uint32_t *epoch);
+// the current device's dense RFC 8681 coefficient table (kRlcTabBytes), drawn
+// on `s` the first time and waited for once, so any stream may read it after
+ssize_t ctx_rlc_table(fecgpu_ctx *ctx, hipStream_t s, const uint8_t **tab);
 // waits until the current device's sliding-window calls issued so far have finished
 ssize_t ctx_sw_wait(fecgpu_ctx *ctx);
 ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);

@@ -2411,7 +2411,7 @@ __device__ __forceinline__ void sw_enc_grouped(const SwEncCoefArgs &a, uint64_t 
     uint8_t *row = a.coef + t0 * kSwCoefPitch + (uint64_t)u * span;
     const int b = (int)(fss - lo);
     for (int q = 0; q < b; q++) row[q] = 0;
-    (void)rlc_coefs(h.key, nss, min((uint32_t)h.dt, 15u), row + b);
+    rlc_coefs_tab(a.rlc, h.key, nss, min((uint32_t)h.dt, 15u), row + b);
     for (int q = b + nss; q < (int)span; q++) row[q] = 0;
     a.outs[t] = t * a.stride;
     if (u == 0) {
@@ -2438,7 +2438,7 @@ __device__ __forceinline__ void sw_enc_single(const SwEncCoefArgs &a, uint64_t t
     const uint64_t fss = min(h.fss, a.nsrc);
     const int nss = (int)min((uint64_t)min((int)h.nss, a.max_window), a.nsrc - fss);
     uint8_t *cc = a.coef + t * kSwCoefPitch;
-    (void)rlc_coefs(h.key, nss, min((uint32_t)h.dt, 15u), cc);
+    rlc_coefs_tab(a.rlc, h.key, nss, min((uint32_t)h.dt, 15u), cc);
     CombJob J;
     J.in_off = fss * a.stride;
     J.coef_off = t * kSwCoefPitch;

@@ -158,6 +158,26 @@ FEC_HD bool rlc_coefs(uint32_t key, int n, uint32_t dt, uint8_t *cc) {
     return true;
 }
 
+// rlc_coefs read from the dense coefficient table (256 bytes per repair key:
+// every key's dt-15 sequence, fec_internal.h kRlcRow) when it holds the row, else
+// drawn; table words 8 at a time (independent loads, all in bounds: n <= 255)
+FEC_HD void rlc_coefs_tab(const uint8_t *tab, uint32_t key, int n, uint32_t dt, uint8_t *cc) {
+    if (!tab || dt != 15) {
+        (void)rlc_coefs(key, n, dt, cc);
+        return;
+    }
+    const uint32_t *row = reinterpret_cast<const uint32_t *>(tab + (size_t)(key & 0xFFFFu) * 256u);
+    for (int q0 = 0; q0 * 4 < n; q0 += 8) {
+        uint32_t w[8];
+        for (int k = 0; k < 8; k++) w[k] = row[q0 + k];
+        for (int k = 0; k < 8; k++)
+            for (int b = 0; b < 4; b++) {
+                const int j = (q0 + k) * 4 + b;
+                if (j < n) cc[j] = (uint8_t)(w[k] >> (8 * b));
+            }
+    }
+}
+
 // multiply by x (=2) in GF(2^8)/0x11D, one byte in the low 8 bits
 FEC_HD uint32_t gf_xtime(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x1Du : 0u)) & 0xFFu; }
 

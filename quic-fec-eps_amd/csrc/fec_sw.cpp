@@ -141,10 +141,11 @@ bool sw_groups_fit(const fecgpu_sw_repair *h, uint64_t nrep, uint64_t nsrc, int 
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *pj, void *pc,
                        void *po, hipStream_t s, int group, const fecgpu_sw_repair *hdr_host, int stream,
-                       void *gtab) {
+                       void *gtab, const uint8_t *rlc) {
     if (stream > 0 && nsrc < kSwStreamSources) {
         SwStreamArgs sa{};
         sa.gtab = gtab;
+        sa.rlc = rlc;
         sa.src = src;
         sa.rep = rep;
         sa.hdr = hdr;
@@ -168,6 +169,7 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
     ca.jobs = static_cast<CombJob *>(pj);
     ca.coef = static_cast<uint8_t *>(pc);
     ca.outs = static_cast<uint64_t *>(po);
+    ca.rlc = rlc;
     if (ca.group == 1) {
         SW_TRY(launch_sw_enc_coef(ca, s), "sliding-window coefficient launch");
         return run_comb(ca.jobs, nrep, ca.coef, ca.outs, src, rep, nullptr, S, stride, 1, max_window, s);
@@ -192,17 +194,20 @@ ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_
                       uint32_t stride, hipStream_t s, const fecgpu_sw_repair *hdr_host = nullptr) {
     void *pj = nullptr, *pc = nullptr, *po = nullptr;
     const int group = ctx_sw_group(ctx), stream = ctx_sw_stream(ctx);
+    const uint8_t *rlc = nullptr;
+    if (FECGPU_SW_RLCTAB) RC_TRY(ctx_rlc_table(ctx, s, &rlc));
     if (stream > 0 && nsrc < kSwStreamSources) {
         // the streaming encode's multiply tables in global memory (scalar loads)
         void *gt = nullptr;
         if (FECGPU_SWS_SGPR) RC_TRY(ctx_sw_scratch(ctx, 1, sw_stream_gtab_bytes(nrep, std::max(1, max_window)), &gt));
         return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, nullptr, nullptr, nullptr, s,
-                              group, hdr_host, stream, gt);
+                              group, hdr_host, stream, gt, rlc);
     }
     RC_TRY(ctx_sw_scratch(ctx, 0, sw_enc_jobs(nrep, group) * sizeof(CombJob), &pj));
     RC_TRY(ctx_sw_scratch(ctx, 1, nrep * kSwCoefPitch, &pc));
     RC_TRY(ctx_sw_scratch(ctx, 2, nrep * sizeof(uint64_t), &po));
-    return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s, group, hdr_host);
+    return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s, group, hdr_host, 0,
+                          nullptr, rlc);
 }
 
 // ---- decode (device plan: fec_swdec.hip) ----------------------------------
@@ -315,6 +320,9 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.src = src;
     a.synd = static_cast<const uint8_t *>(psyn);
     a.sticky = sticky;
+#if FECGPU_SW_RLCTAB
+    RC_TRY(ctx_rlc_table(ctx, s, &a.rlc));
+#endif
 
 #if FECGPU_SWD_FUSED
     {  // the plan kernel writes the counters itself: nothing to clear

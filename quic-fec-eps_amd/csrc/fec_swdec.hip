@@ -341,6 +341,129 @@ __device__ __forceinline__ bool holds(const SwDecArgs &a, const fecgpu_sw_repair
     return r1 > r0 && r0 < x + e && r1 > x;
 }
 
+// ================================================== coefficient table ===
+// RFC 8681 §3.6 at dt 15 draws every coefficient nonzero, so a repair's window
+// takes a prefix of one sequence per repair key: the 65536 sequences are drawn
+// once per device (ctx_rlc_table, 16 MiB) and the decode reads a row's words
+// instead of stepping TinyMT32 once or more per coefficient.  A thread's chain
+// of ~300 dependent generator steps (the key's 15 warm-up steps, the pivot's
+// coefficient, then its row again) set the plan kernel's critical path: two
+// thirds of it on cfg7 (FECGPU_SWD_TRACE, r04).  Other dt values draw as before.
+__global__ __launch_bounds__(kBlock) void rlc_table_kernel(uint8_t *tab) {
+    const uint32_t key = blockIdx.x * kBlock + threadIdx.x;
+    Tinymt32 st;
+    tinymt32_init(st, key);
+    uint4 *row = reinterpret_cast<uint4 *>(tab + (size_t)key * kRlcRow);
+    for (int q = 0; q < (int)(kRlcRow / 16); q++) {
+        uint32_t w[4];
+        for (int d = 0; d < 4; d++) {
+            w[d] = 0;
+            for (int b = 0; b < 4; b++) {
+                uint32_t c = 0;
+                if (q * 16 + d * 4 + b < kSwMaxWindow) {
+                    do {
+                        c = tinymt32_u32(st) & 0xFFu;
+                    } while (c == 0);
+                }
+                w[d] |= c << (8 * b);
+            }
+        }
+        row[q] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+static_assert(kRlcRow == 256 && kSwMaxWindow < (int)kRlcRow, "a table row holds a window's coefficients");
+
+__device__ __forceinline__ const uint4 *rlc_row(const SwDecArgs &a, const fecgpu_sw_repair &h) {
+#if FECGPU_SW_RLCTAB
+    return a.rlc && h.dt == 15 ? reinterpret_cast<const uint4 *>(a.rlc + (size_t)h.key * kRlcRow) : nullptr;
+#else
+    (void)a;
+    (void)h;
+    return nullptr;
+#endif
+}
+
+// f(q, w) for the words q < ceil(nss / 4) of the window's coefficients, 4 per
+// word (bytes past nss zero); from the table 64 coefficients per round trip
+template <class F>
+__device__ __forceinline__ void rlc_words(const SwDecArgs &a, const fecgpu_sw_repair &h, F f) {
+    const uint32_t nss = h.nss, nw = (nss + 3u) >> 2;
+    if (const uint4 *row = rlc_row(a, h)) {
+        for (uint32_t g = 0; g * 16 < nw; g++) {  // g <= 3: the row's 16 uint4 are in bounds
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = row[g * 4 + k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const uint32_t q = g * 16 + k * 4 + d;
+                    if (q < nw) {
+                        uint32_t w = w4[d];
+                        if (q == nw - 1 && (nss & 3u)) w &= (1u << (8 * (nss & 3u))) - 1u;
+                        f(q, w);
+                    }
+                }
+            }
+        }
+        return;
+    }
+    Tinymt32 st;
+    tinymt32_init(st, h.key);
+    const uint32_t dt = h.dt;
+    uint32_t word = 0;
+    for (uint32_t j = 0; j < nss; j++) {
+        uint32_t c = 0;
+        if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
+            do {
+                c = tinymt32_u32(st) & 0xFFu;
+            } while (c == 0);
+        }
+        word |= c << (8 * (j & 3));
+        if ((j & 3) == 3) {
+            f(j >> 2, word);
+            word = 0;
+        }
+    }
+    if (nss & 3u) f(nss >> 2, word);
+}
+
+// The window's coefficients one at a time (next(j) for j = 0, 1, ... in
+// order); from the table 16 per load, the next 16 loaded ahead
+struct RlcSeq {
+    const uint4 *row;
+    uint4 cur, nxt;
+    Tinymt32 st;
+    uint32_t dt;
+    __device__ __forceinline__ RlcSeq(const SwDecArgs &a, const fecgpu_sw_repair &h) : row(rlc_row(a, h)), dt(h.dt) {
+        if (row) {
+            cur = row[0];
+            nxt = row[1];
+        } else {
+            tinymt32_init(st, h.key);
+        }
+    }
+    __device__ __forceinline__ uint32_t next(uint32_t j) {
+        if (row) {
+            if (j && (j & 15u) == 0) {
+                cur = nxt;
+                nxt = row[min((j >> 4) + 1u, kRlcRow / 16 - 1)];
+            }
+            const uint32_t q = (j >> 2) & 3u;
+            const uint32_t w = q == 0 ? cur.x : q == 1 ? cur.y : q == 2 ? cur.z : cur.w;
+            return (w >> (8 * (j & 3))) & 0xFFu;
+        }
+        uint32_t c = 0;
+        if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
+            do {
+                c = tinymt32_u32(st) & 0xFFu;
+            } while (c == 0);
+        }
+        return c;
+    }
+};
+
 // ============================================================= systems ===
 // Small systems are solved by one wave each with [A | I] in LDS: "tiny" ones
 // (e <= 16, p <= 48: 3 KB of LDS per wave, so occupancy is set by registers)
@@ -399,18 +522,11 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         }
 #else
         uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
-        Tinymt32 st;
-        tinymt32_init(st, h.key);
-        const uint32_t dt = h.dt;
+        RlcSeq sq(a, h);
         int u = 0;
         uint32_t word = 0;
         for (int j = 0; j < (int)h.nss; j++) {
-            uint32_t c = 0;
-            if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
-                do {
-                    c = tinymt32_u32(st) & 0xFFu;
-                } while (c == 0);
-            }
+            uint32_t c = sq.next((uint32_t)j);
             const uint64_t i = h.fss + (uint64_t)j;
             while (u < e && U[u] < i) u++;
             if (u < e && U[u] == i) {
@@ -636,24 +752,7 @@ __device__ __forceinline__ void block_counts(const SwDecArgs &a, uint32_t rec, u
 // long-system pass draws its own rows again (and overwrites these).
 __device__ __forceinline__ void draw_row(const SwDecArgs &a, uint64_t t, const fecgpu_sw_repair &h) {
     uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + t * kSwCoefPitch);
-    Tinymt32 st;
-    tinymt32_init(st, h.key);
-    const uint32_t dt = h.dt;
-    uint32_t word = 0;
-    for (int j = 0; j < (int)h.nss; j++) {
-        uint32_t c = 0;
-        if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
-            do {
-                c = tinymt32_u32(st) & 0xFFu;
-            } while (c == 0);
-        }
-        word |= c << (8 * (j & 3));
-        if ((j & 3) == 3) {
-            cc[j >> 2] = word;
-            word = 0;
-        }
-    }
-    if (h.nss & 3) cc[h.nss >> 2] = word;
+    rlc_words(a, h, [&](uint32_t q, uint32_t w) { cc[q] = w; });
 }
 
 __global__ __launch_bounds__(kBlock) void sw_dec_coef_kernel(SwDecArgs a) {
@@ -727,7 +826,9 @@ __device__ __forceinline__ LbRec lb_read(const uint4 *src2) {
 // FECGPU_SWD_FUSE1).  lkind[x] tells the system pass what is left: 0 a member
 // of a larger system, 1 recovered here, 2 a larger system's first unknown,
 // 3 alone but undetermined.
-__device__ __forceinline__ uint8_t coef_at(const fecgpu_sw_repair &h, uint32_t j) {  // RFC 8681 coefficient j
+__device__ __forceinline__ uint8_t coef_at(const SwDecArgs &a, const fecgpu_sw_repair &h, uint32_t j) {
+    // RFC 8681 coefficient j
+    if (const uint4 *row = rlc_row(a, h)) return reinterpret_cast<const uint8_t *>(row)[j];
     Tinymt32 st;
     tinymt32_init(st, h.key);
     const uint32_t dt = h.dt;
@@ -1145,7 +1246,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                 if (!rpt) continue;
                 if (h.fss > i || h.fss + h.nss <= i) continue;
                 const uint32_t j = (uint32_t)(i - h.fss);
-                const uint8_t cj = coef_at(h, j);
+                const uint8_t cj = coef_at(a, h, j);
                 if (!cj) continue;
                 // the job: t's coefficients times 1/c (0 at x), t's row times 1/c;
                 // the row drawn again and scaled 4 bytes at a time as it goes out
@@ -1154,29 +1255,14 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                 const uint32_t iv = c_gfs.exp[255 - c_gfs.log[cj]];
                 uint32_t tab[5];
                 set_tab(tab, iv);
-                Tinymt32 st;
-                tinymt32_init(st, h.key);
-                const uint32_t dt = h.dt;
-                uint32_t word = 0;
-                for (int q = 0; q < (int)h.nss; q++) {
-                    uint32_t cq = 0;
-                    if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
-                        do {
-                            cq = tinymt32_u32(st) & 0xFFu;
-                        } while (cq == 0);
-                    }
-                    if ((uint32_t)q == j) cq = 0;
-                    word |= cq << (8 * (q & 3));
-                    if ((q & 3) == 3) {
-                        reinterpret_cast<uint32_t *>(row)[q >> 2] = tmul(word, tab);
-                        word = 0;
-                    }
-                }
-                // the last partial word, with the xor row's multiplier after the
-                // coefficients (nss < kSwCoefPitch)
-                uint32_t last = (h.nss & 3) ? tmul(word, tab) : 0u;
-                last |= iv << (8 * (h.nss & 3));
-                reinterpret_cast<uint32_t *>(row)[h.nss >> 2] = last;
+                // the xor row's multiplier follows the coefficients (nss < kSwCoefPitch):
+                // in the last partial word, or a word of its own
+                const uint32_t nq = h.nss >> 2, ivw = iv << (8 * (h.nss & 3));
+                rlc_words(a, h, [&](uint32_t q, uint32_t w) {
+                    if (q == (j >> 2)) w &= ~(0xFFu << (8 * (j & 3)));
+                    reinterpret_cast<uint32_t *>(row)[q] = tmul(w, tab) | (q == nq ? ivw : 0u);
+                });
+                if (!(h.nss & 3)) reinterpret_cast<uint32_t *>(row)[nq] = ivw;
                 J.in_off = h.fss * a.stride;
                 J.coef_off = slot * kSwCoefPitch;
                 J.out_list = slot;
@@ -1362,17 +1448,10 @@ __device__ int long_refill(const SwDecArgs &a, LongLds &L, const SwLong &S, uint
             uint8_t *row = L.stg[k];
             for (uint32_t u = lo; u <= hi; u++) row[u & 255] = 0;
             uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
-            Tinymt32 st;
-            tinymt32_init(st, h.key);
-            const uint32_t dt = h.dt;
+            RlcSeq sq(a, h);
             uint32_t word = 0;
             for (int j = 0; j < (int)h.nss; j++) {
-                uint32_t c = 0;
-                if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
-                    do {
-                        c = tinymt32_u32(st) & 0xFFu;
-                    } while (c == 0);
-                }
+                uint32_t c = sq.next((uint32_t)j);
                 const uint64_t i = h.fss + (uint64_t)j;
                 if (!a.src_present[i]) {
                     row[(a.reach[i] - S.x0) & 255] = (uint8_t)c;
@@ -1890,6 +1969,11 @@ int cu_count() {
 }
 
 }  // namespace
+
+hipError_t launch_rlc_table(uint8_t *tab, hipStream_t s) {
+    hipLaunchKernelGGL(rlc_table_kernel, dim3(65536 / kBlock), dim3(kBlock), 0, s, tab);
+    return hipGetLastError();
+}
 
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
 #if FECGPU_SWD_FUSED

@@ -137,7 +137,7 @@ __device__ __forceinline__ void sws_plan(const SwStreamArgs &a, SwsPlan &pl, uin
         const int v = __popcll(bne & below);
         pl.fe[v] = make_uint2((uint32_t)(fss - lo), (uint32_t)(end - lo));
         pl.out[v] = (uint16_t)lane;
-        if (CB) (void)rlc_coefs(h.key, (int)(end - fss), min((uint32_t)h.dt, 15u), CB + (size_t)v * W);
+        if (CB) rlc_coefs_tab(a.rlc, h.key, (int)(end - fss), min((uint32_t)h.dt, 15u), CB + (size_t)v * W);
     }
     if (lane < n && !ne) pl.empty[__popcll(bem & below)] = (uint16_t)lane;
     SWS_WAVE_SYNC();

@@ -81,6 +81,38 @@ def test_sw_encode_vs_oracle(ctx, nsrc, k, W, dt, L, mw):
     assert np.array_equal(g[:, :L], o[:, :L])
 
 
+@pytest.mark.parametrize("stream_enc", [1, 0], ids=["streaming", "combine"])
+def test_sw_coefficient_table_keys_and_mixed_dt(stream_enc):
+    """The dense (dt 15) coefficients come from the ctx's 16 MiB table of every
+    repair key's sequence, other dt values are drawn per coefficient: one stream
+    mixing both, keys spread over all 2^16 (0 and 65535 included), windows up to
+    255: encode and decode equal to the oracle."""
+    c = fecgpu.Context()
+    try:
+        c.set_tuning("sw_stream", stream_enc)
+        nsrc, L = 1500, 40
+        stride = O.round_up(L, 16)
+        src = stream(nsrc, L, stride, 77 + stream_enc)
+        h = []
+        for t, fss in enumerate(range(0, nsrc - 255, 3)):
+            nss = 255 if t % 5 == 0 else 1 + (t * 37) % 64
+            key = 65535 if t == 1 else (t * 2731) & 0xFFFF
+            h.append((fss, nss, key, 15 if t % 4 else (t // 4) % 15))
+        hdr = hdr_array(h)
+        o = O.sw_encode(src, hdr, L)
+        g = gpu_encode(c, src, hdr, L, 255)
+        assert np.array_equal(g[:, :L], o[:, :L])
+        rng = np.random.default_rng(5)
+        sp = (rng.random(nsrc) >= 0.05).astype(np.uint8)
+        rp = (rng.random(len(hdr)) >= 0.05).astype(np.uint8)
+        gd, gst, gn = gpu_decode(c, src, sp, o, rp, hdr, L)
+        od, ost, on = oracle_decode(src, sp, o, rp, hdr, L)
+        assert np.array_equal(gst, ost) and gn == on and gn > 0
+        assert np.array_equal(gd[:, :L], od[:, :L])
+    finally:
+        c.close()
+
+
 def test_sw_encode_host_pointers(ctx):
     nsrc, L, stride = 120, 50, 64
     src = stream(nsrc, L, stride, 3)
