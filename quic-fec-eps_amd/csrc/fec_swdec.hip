@@ -864,6 +864,10 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
 #endif
     __shared__ uint32_t s_reach[kPlanChunk], s_rcnt[kPlanChunk];
     __shared__ uint32_t s_lpos[kPlanChunk], s_rl[kPlanChunk];  // per local lost source: position, reachL
+    // per local lost source that may be alone: its pivot repair (~0: none), key | nss << 16 | j << 24,
+    // coefficient | dt << 8
+    __shared__ uint2 s_pv[kPlanChunk];
+    __shared__ uint16_t s_pcd[kPlanChunk];
     __shared__ uint32_t s_rf[kPlanChunk + 1];                  // repfirst of the chunk's sources (and of i1)
     __shared__ uint32_t s_rcb[kPlanHalo], s_rfb[kPlanHalo];    // repairs starting in [i0 - 256, i0), repfirst there
     __shared__ uint32_t s_bits[(kPlanChunk + kPlanHalo) / 32];      // lost flags, chunk + halo
@@ -1093,21 +1097,51 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         s_agg = agg;
         lb_publish(a, c, agg, c == 0 ? kLbInc : kLbAgg);
     }
+    // the chunk's lost sources in LDS (nothing here needs the look-back):
+    // positions, reachL within the chunk (the look-back's reach is joined in
+    // later), and repfirst of the chunk's sources counted from t0 (the
+    // repairs before i0: the same count as the look-back's, headers being in
+    // fss order; bad headers stop the call anyway)
+    {
+        uint32_t loff = wc + ic - cnt, lrun = max(wmx, em), lrep = (uint32_t)t0 + wr + ir - tr;
+#pragma unroll
+        for (int j = 0; j < kPlanPer; j++)
+            if (my0 + j < n) {
+                s_rf[my0 + j] = lrep;
+                lrun = max(lrun, s_reach[my0 + j]);
+                lrep += s_rcnt[my0 + j];
+                if ((lostm >> j) & 1u) {
+                    s_lpos[loff] = my0 + j;
+                    s_rl[loff] = lrun;
+                    loff++;
+                }
+            }
+        if (my0 <= n && n <= my0 + kPlanPer) s_rf[n] = lrep;  // repfirst at i1
+    }
     __syncthreads();
     SWD_TRACE(6);
-    // decoupled look-back by wave 0, 64 predecessors per round: lane i polls
-    // chunk base - i; once every one of them has published, the records up to
-    // the nearest inclusive prefix are joined (lanes in chunk order) and the
-    // window moves back 64 chunks if there was none.  (One lane walking back
-    // serially cost a dependent load per predecessor: ~0.1 ms at 256 chunks.)
+    const uint32_t nl = s_agg.lost, wmb_all = s_wmb;
     if (wave == 0) {
+        // decoupled look-back, 256 predecessors per round: lane l polls chunks
+        // base - 4l - k (k < 4); once all have published, the records back to
+        // the nearest inclusive prefix are joined (a lane's four in chunk
+        // order, then across lanes) and the window moves back 256 chunks if
+        // there was none.  Two round trips a round (flags, records): waiting
+        // on 256 predecessors 64 at a time took ~11 us at chunk 255 (r04 trace).
         LbRec ex{0, 0, 0, 0, 0};
         uint32_t spins = 0;
         for (int64_t base = (int64_t)c - 1; base >= 0;) {
-            const int64_t q = base - lane;
-            const bool valid = q >= 0;
-            const uint32_t f = valid ? lb_flag_load(&a.lb_flag[q]) : 0u;
-            const bool ready = !valid || ((f >> 2) == a.epoch && (f & 3u) != 0);
+            bool ready = true;
+            uint32_t incb = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int64_t q = base - 4 * lane - k;
+                if (q >= 0) {
+                    const uint32_t f = lb_flag_load(&a.lb_flag[q]);
+                    ready &= (f >> 2) == a.epoch && (f & 3u) != 0;
+                    if ((f & 3u) == kLbInc) incb |= 1u << k;
+                }
+            }
             if (__ballot(!ready)) {
                 // bounded: a predecessor that never publishes (which the
                 // dispatch order rules out) ends as an error, not a hang
@@ -1118,20 +1152,29 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
-            const uint64_t incm = __ballot(valid && (f & 3u) == kLbInc);
-            const int n = incm ? __ffsll((unsigned long long)incm) : (int)min<int64_t>(64, base + 1);
+            // nearest inclusive prefix: d = base - chunk (~0: none in this round)
+            const uint32_t dinc = wave_min(incb ? 4u * lane + (uint32_t)(__ffs(incb) - 1) : ~0u);
+            const int64_t nd = dinc != ~0u ? (int64_t)dinc + 1 : min<int64_t>(256, base + 1);
             LbRec r{0, 0, 0, 0, 0};
-            if (lane < n) r = lb_read((lane == n - 1 && incm ? a.lb_inc : a.lb_agg) + 2 * (size_t)q);
-            // ordered join: a higher lane holds an earlier chunk
+            LbRec v[4];
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
+            for (int k = 0; k < 4; k++) {
+                const int64_t d = 4 * lane + k;
+                v[k] = d < nd ? lb_read(((uint32_t)d == dinc ? a.lb_inc : a.lb_agg) + 2 * (size_t)(base - d))
+                              : LbRec{0, 0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int k = 3; k >= 0; k--) r = lb_join(r, v[k]);  // k = 3 is the lane's earliest
+            // ordered join: a higher lane holds earlier chunks
+#pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1) {
                 LbRec o;
-                o.lost = __shfl_down(r.lost, d);
-                o.reach = __shfl_down(r.reach, d);
-                o.rep = __shfl_down(r.rep, d);
-                o.wme = __shfl_down(r.wme, d);
-                o.L = __shfl_down(r.L, d);
-                if (lane + d < 64 && (lane & (2 * d - 1)) == 0) r = lb_join(o, r);
+                o.lost = __shfl_down(r.lost, dd);
+                o.reach = __shfl_down(r.reach, dd);
+                o.rep = __shfl_down(r.rep, dd);
+                o.wme = __shfl_down(r.wme, dd);
+                o.L = __shfl_down(r.L, dd);
+                if (lane + dd < 64 && (lane & (2 * dd - 1)) == 0) r = lb_join(o, r);
             }
             r.lost = __shfl(r.lost, 0);
             r.reach = __shfl(r.reach, 0);
@@ -1139,19 +1182,62 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             r.wme = __shfl(r.wme, 0);
             r.L = __shfl(r.L, 0);
             ex = lb_join(r, ex);
-            if (incm) break;
-            base -= 64;
+            if (dinc != ~0u) break;
+            base -= 256;
         }
         if (lane == 0) {
             if (c > 0) lb_publish(a, c, lb_join(ex, s_agg), kLbInc);
             s_excl = ex;
         }
+    } else {
+        // meanwhile (waves 1-3): the coefficient rows of the chunk's received
+        // repairs whose window holds a lost source, and the pivots of the lost
+        // sources that may be alone in their system
+        const auto before = [&](uint32_t j) {  // lost sources in [i0, i0 + j), j <= chunk + halo
+            return s_wpfx[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u));
+        };
+        for (uint64_t t = t0 + (tid - 64); t < t1; t += kBlock - 64) {
+            if (!a.rep_present[t]) continue;
+            const fecgpu_sw_repair h = a.hdr[t];
+            if (h.fss < i0 || h.fss >= i1 || h.nss < 1 || h.nss > kSwMaxWindow || a.nsrc - h.fss < h.nss) continue;
+            const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
+            if (before(hi) > before(lo)) draw_row(a, t, h);
+        }
+        for (uint32_t k = tid - 64; k < nl; k += kBlock - 64) {
+            uint32_t pt = ~0u, pw = 0, pc = 0;
+            const uint32_t pos = s_lpos[k];
+            const uint64_t i = i0 + pos;
+            if (a.long_min > 1 && (k + 1 >= nl || s_rl[k] <= i0 + s_lpos[k + 1])) {
+                // candidates: received repairs with fss in [i - wmb + 1, i] (repair
+                // order); the first whose coefficient at i is nonzero (the small
+                // solver's choice)
+                const uint64_t lo = i + 1 > (uint64_t)wmb_all ? max(i + 1 - wmb_all, ib) : ib;
+                const auto rfirst = [&](uint64_t p) -> uint64_t {
+                    return p < i0 ? s_rfb[p - (i0 - kPlanHalo)] : s_rf[p - i0];
+                };
+                const uint64_t ta = rfirst(lo), te = rfirst(i + 1);
+                for (uint64_t t = ta; t < te; t++) {
+                    const uint8_t rpt = a.rep_present[t];  // both loads in one round trip
+                    const fecgpu_sw_repair h = a.hdr[t];
+                    if (!rpt) continue;
+                    if (h.fss > i || h.fss + h.nss <= i) continue;
+                    const uint32_t j = (uint32_t)(i - h.fss);
+                    const uint8_t cj = coef_at(a, h, j);
+                    if (!cj) continue;
+                    pt = (uint32_t)t;
+                    pw = (uint32_t)h.key | (uint32_t)h.nss << 16 | j << 24;
+                    pc = cj | (uint32_t)h.dt << 8;
+                    break;
+                }
+            }
+            s_pv[k] = make_uint2(pt, pw);
+            s_pcd[k] = (uint16_t)pc;
+        }
     }
     __syncthreads();
     SWD_TRACE(7);
     const LbRec ex = s_excl;
-    // lost list, rank / repfirst (as sw_dec_lost_kernel); positions and reachL
-    // of the chunk's lost sources in LDS for the one-unknown systems below
+    // lost list, rank / repfirst (as sw_dec_lost_kernel)
     uint32_t off = ex.lost + wc + ic - cnt;
     uint32_t run = max(max(ex.reach, wmx), em);
     uint32_t repc = ex.rep + wr + ir - tr;
@@ -1164,7 +1250,6 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         rf[j] = repc;
         if (my0 + j < n) {
             const uint64_t i = i0 + my0 + j;
-            s_rf[my0 + j] = repc;
             run = max(run, s_reach[my0 + j]);
             repc += s_rcnt[my0 + j];
             if ((lostm >> j) & 1u) {
@@ -1173,8 +1258,6 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
 #if !FECGPU_SWD_SOLVE_LIST
                 a.sol_jobs[off] = E;  // solve jobs in the unknowns' slots: empty unless filled
 #endif
-                s_lpos[off - ex.lost] = my0 + j;
-                s_rl[off - ex.lost] = run;
                 off++;
             }
         }
@@ -1191,30 +1274,18 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             a.rcnt[i0 + my0 + j] = rf[j];
         }
     }
-    if (my0 <= n && n <= my0 + kPlanPer) s_rf[n] = repc;  // repfirst at i1
     if (my0 <= n && n <= my0 + kPlanPer && i1 == a.nsrc) {  // the thread holding the end
         a.reach[a.nsrc] = off;
         a.rcnt[a.nsrc] = repc;
     }
-    const auto before = [&](uint32_t j) {  // lost sources in [i0, i0 + j), j <= chunk + halo
-        return s_wpfx[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u));
-    };
-    // coefficient rows of the chunk's received repairs whose window holds a lost source
-    for (uint64_t t = t0 + tid; t < t1; t += kBlock) {
-        if (!a.rep_present[t]) continue;
-        const fecgpu_sw_repair h = a.hdr[t];
-        if (h.fss < i0 || h.fss >= i1 || h.nss < 1 || h.nss > kSwMaxWindow || a.nsrc - h.fss < h.nss) continue;
-        const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
-        if (before(hi) > before(lo)) draw_row(a, t, h);
-    }
+    // s_rcnt is read above and reused for the starts list below
     __syncthreads();
     SWD_TRACE(8);
     // the chunk's lost sources: one-unknown systems solved, the rest classified
-    const uint32_t nl = s_agg.lost, wmb_all = s_wmb;
     for (uint32_t k = tid; k < nl; k += kBlock) {
-        const uint32_t u = ex.lost + k, pos = s_lpos[k], rl = s_rl[k];
+        const uint32_t u = ex.lost + k, pos = s_lpos[k], rl = max(ex.reach, s_rl[k]);
         const uint64_t i = i0 + pos;
-        const uint32_t prl = k > 0 ? s_rl[k - 1] : (ex.lost ? ex.L : 0u);
+        const uint32_t prl = k > 0 ? max(ex.reach, s_rl[k - 1]) : (ex.lost ? ex.L : 0u);
         const bool start = u == 0 || prl <= i;
         // the next lost source: in the chunk, else in the halo (a window reaches
         // at most 255 sources past i, so none there means none in reach)
@@ -1234,25 +1305,20 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         CombJob J = E;  // syndrome slot nrep + u: empty unless x is solved here
         if (single) {
             kind = 3;
-            // candidates: received repairs with fss in [i - wmb + 1, i] (repair order)
-            const uint64_t lo = i + 1 > (uint64_t)wmb_all ? max(i + 1 - wmb_all, ib) : ib;
-            const auto rfirst = [&](uint64_t p) -> uint64_t {
-                return p < i0 ? s_rfb[p - (i0 - kPlanHalo)] : s_rf[p - i0];
-            };
-            const uint64_t ta = rfirst(lo), te = rfirst(i + 1);
-            for (uint64_t t = ta; t < te; t++) {
-                const uint8_t rpt = a.rep_present[t];  // both loads in one round trip
-                const fecgpu_sw_repair h = a.hdr[t];
-                if (!rpt) continue;
-                if (h.fss > i || h.fss + h.nss <= i) continue;
-                const uint32_t j = (uint32_t)(i - h.fss);
-                const uint8_t cj = coef_at(a, h, j);
-                if (!cj) continue;
+            const uint2 pv = s_pv[k];  // the pivot found during the look-back
+            if (pv.x != ~0u) {
+                const uint64_t t = pv.x;
+                const uint32_t cd = s_pcd[k], j = pv.y >> 24;
+                fecgpu_sw_repair h{};
+                h.fss = i - j;
+                h.nss = (uint16_t)((pv.y >> 16) & 0xFFu);
+                h.key = (uint16_t)(pv.y & 0xFFFFu);
+                h.dt = (uint8_t)(cd >> 8);
                 // the job: t's coefficients times 1/c (0 at x), t's row times 1/c;
-                // the row drawn again and scaled 4 bytes at a time as it goes out
+                // the row scaled 4 bytes at a time as it goes out
                 const uint64_t slot = a.nrep + u;
                 uint8_t *row = a.coef + slot * kSwCoefPitch;
-                const uint32_t iv = c_gfs.exp[255 - c_gfs.log[cj]];
+                const uint32_t iv = c_gfs.exp[255 - c_gfs.log[cd & 0xFFu]];
                 uint32_t tab[5];
                 set_tab(tab, iv);
                 // the xor row's multiplier follows the coefficients (nss < kSwCoefPitch):
@@ -1272,7 +1338,6 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                 a.syn_outs[slot] = (uint64_t)(a.src + i * a.stride) - (uint64_t)a.synd;
                 a.stat[i] = FECGPU_STATUS_OK;
                 kind = 1;
-                break;
             }
         }
         a.syn_jobs[a.nrep + u] = J;
