@@ -510,37 +510,41 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         const uint32_t t = eq[q];
         const fecgpu_sw_repair h = a.hdr[t];
 #if FECGPU_SWD_COEF
-        // the row was drawn by sw_dec_coef_kernel: move the unknowns' entries
-        // into A (the unknowns are ascending; the window holds a run of them)
-        uint8_t *cb = a.coef + (uint64_t)t * kSwCoefPitch;
-        for (int u = 0; u < e; u++) {
-            const uint64_t i = U[u];
-            if (i < h.fss) continue;
-            if (i >= h.fss + h.nss) break;
-            M[q * kPitch + u] = cb[i - h.fss];
-            cb[i - h.fss] = 0;
-        }
-#else
-        uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
-        RlcSeq sq(a, h);
-        int u = 0;
-        uint32_t word = 0;
-        for (int j = 0; j < (int)h.nss; j++) {
-            uint32_t c = sq.next((uint32_t)j);
-            const uint64_t i = h.fss + (uint64_t)j;
-            while (u < e && U[u] < i) u++;
-            if (u < e && U[u] == i) {
-                M[q * kPitch + u] = (uint8_t)c;
-                c = 0;
+        if (!rlc_row(a, h)) {
+            // the row was drawn by the plan (or sw_dec_coef_kernel): move the
+            // unknowns' entries into A (the unknowns are ascending; the window
+            // holds a run of them)
+            uint8_t *cb = a.coef + (uint64_t)t * kSwCoefPitch;
+            for (int u = 0; u < e; u++) {
+                const uint64_t i = U[u];
+                if (i < h.fss) continue;
+                if (i >= h.fss + h.nss) break;
+                M[q * kPitch + u] = cb[i - h.fss];
+                cb[i - h.fss] = 0;
             }
-            word |= c << (8 * (j & 3));
-            if ((j & 3) == 3) {
-                cc[j >> 2] = word;
-                word = 0;
-            }
-        }
-        if (h.nss & 3) cc[h.nss >> 2] = word;
+        } else
 #endif
+        {  // dense rows come from the coefficient table: read here, no row drawn before
+            uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
+            RlcSeq sq(a, h);
+            int u = 0;
+            uint32_t word = 0;
+            for (int j = 0; j < (int)h.nss; j++) {
+                uint32_t c = sq.next((uint32_t)j);
+                const uint64_t i = h.fss + (uint64_t)j;
+                while (u < e && U[u] < i) u++;
+                if (u < e && U[u] == i) {
+                    M[q * kPitch + u] = (uint8_t)c;
+                    c = 0;
+                }
+                word |= c << (8 * (j & 3));
+                if ((j & 3) == 3) {
+                    cc[j >> 2] = word;
+                    word = 0;
+                }
+            }
+            if (h.nss & 3) cc[h.nss >> 2] = word;
+        }
         CombJob J;
         J.in_off = h.fss * a.stride;
         J.coef_off = (uint64_t)t * kSwCoefPitch;
@@ -759,7 +763,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_coef_kernel(SwDecArgs a) {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (t >= a.nrep || (a.ctr->err & 1u) || !a.rep_present[t]) return;
     const fecgpu_sw_repair h = a.hdr[t];
-    if (!holds_any(a, h)) return;
+    if (rlc_row(a, h) || !holds_any(a, h)) return;  // dense rows: read from the table by the system pass
     draw_row(a, t, h);
 }
 
@@ -1191,8 +1195,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         }
     } else {
         // meanwhile (waves 1-3): the coefficient rows of the chunk's received
-        // repairs whose window holds a lost source, and the pivots of the lost
-        // sources that may be alone in their system
+        // repairs whose window holds a lost source (sparse ones: the system pass
+        // reads dense rows from the table), and the pivots of the lost sources
+        // that may be alone in their system
         const auto before = [&](uint32_t j) {  // lost sources in [i0, i0 + j), j <= chunk + halo
             return s_wpfx[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u));
         };
@@ -1201,7 +1206,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             const fecgpu_sw_repair h = a.hdr[t];
             if (h.fss < i0 || h.fss >= i1 || h.nss < 1 || h.nss > kSwMaxWindow || a.nsrc - h.fss < h.nss) continue;
             const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
-            if (before(hi) > before(lo)) draw_row(a, t, h);
+            if (!rlc_row(a, h) && before(hi) > before(lo)) draw_row(a, t, h);  // dense rows: from the table
         }
         for (uint32_t k = tid - 64; k < nl; k += kBlock - 64) {
             uint32_t pt = ~0u, pw = 0, pc = 0;
