@@ -1134,26 +1134,41 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         // on 256 predecessors 64 at a time took ~11 us at chunk 255 (r04 trace).
         LbRec ex{0, 0, 0, 0, 0};
         uint32_t spins = 0;
+        int64_t wait_q = (int64_t)c - 1;  // a chunk polled alone before the window is read
         for (int64_t base = (int64_t)c - 1; base >= 0;) {
+            // one flag by one lane until it has published: every waiting block
+            // polling its whole window (1 KB of flags from 255 blocks) made the
+            // flags' memory channel a hot spot that slowed every other access
+            while (wait_q >= 0) {
+                uint32_t f = 0;
+                if (lane == 0) f = lb_flag_load(&a.lb_flag[wait_q]);
+                f = __shfl(f, 0);
+                if ((f >> 2) == a.epoch && (f & 3u) != 0) break;
+                if (++spins == (1u << 22)) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            wait_q = -1;
             bool ready = true;
-            uint32_t incb = 0;
+            uint32_t incb = 0, nrd = ~0u;  // nrd: nearest unpublished d
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const int64_t q = base - 4 * lane - k;
                 if (q >= 0) {
                     const uint32_t f = lb_flag_load(&a.lb_flag[q]);
-                    ready &= (f >> 2) == a.epoch && (f & 3u) != 0;
+                    const bool pub = (f >> 2) == a.epoch && (f & 3u) != 0;
+                    ready &= pub;
+                    if (!pub) nrd = min(nrd, (uint32_t)(4 * lane + k));
                     if ((f & 3u) == kLbInc) incb |= 1u << k;
                 }
             }
             if (__ballot(!ready)) {
                 // bounded: a predecessor that never publishes (which the
                 // dispatch order rules out) ends as an error, not a hang
-                if (++spins == (1u << 22)) {
+                if (spins >= (1u << 22)) {
                     ex.wme |= kSwErrInternal << 16;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                wait_q = base - (int64_t)wave_min(nrd);  // poll the nearest unpublished one alone
                 continue;
             }
             // nearest inclusive prefix: d = base - chunk (~0: none in this round)
