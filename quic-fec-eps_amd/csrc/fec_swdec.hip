@@ -510,10 +510,12 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         const uint32_t t = eq[q];
         const fecgpu_sw_repair h = a.hdr[t];
 #if FECGPU_SWD_COEF
-        if (!rlc_row(a, h)) {
+        if (true) {
             // the row was drawn by the plan (or sw_dec_coef_kernel): move the
             // unknowns' entries into A (the unknowns are ascending; the window
-            // holds a run of them)
+            // holds a run of them).  (Reading dense rows from the table here
+            // instead, with the unknowns zeroed as the row goes out, cost the
+            // system pass 23 us on cfg7, r04: serial LDS lookups per coefficient.)
             uint8_t *cb = a.coef + (uint64_t)t * kSwCoefPitch;
             for (int u = 0; u < e; u++) {
                 const uint64_t i = U[u];
@@ -524,7 +526,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
             }
         } else
 #endif
-        {  // dense rows come from the coefficient table: read here, no row drawn before
+        {  // FECGPU_SWD_COEF 0: the row drawn here
             uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
             RlcSeq sq(a, h);
             int u = 0;
@@ -763,7 +765,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_coef_kernel(SwDecArgs a) {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (t >= a.nrep || (a.ctr->err & 1u) || !a.rep_present[t]) return;
     const fecgpu_sw_repair h = a.hdr[t];
-    if (rlc_row(a, h) || !holds_any(a, h)) return;  // dense rows: read from the table by the system pass
+    if (!holds_any(a, h)) return;
     draw_row(a, t, h);
 }
 
@@ -1210,9 +1212,8 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         }
     } else {
         // meanwhile (waves 1-3): the coefficient rows of the chunk's received
-        // repairs whose window holds a lost source (sparse ones: the system pass
-        // reads dense rows from the table), and the pivots of the lost sources
-        // that may be alone in their system
+        // repairs whose window holds a lost source, and the pivots of the lost
+        // sources that may be alone in their system
         const auto before = [&](uint32_t j) {  // lost sources in [i0, i0 + j), j <= chunk + halo
             return s_wpfx[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u));
         };
@@ -1221,7 +1222,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             const fecgpu_sw_repair h = a.hdr[t];
             if (h.fss < i0 || h.fss >= i1 || h.nss < 1 || h.nss > kSwMaxWindow || a.nsrc - h.fss < h.nss) continue;
             const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
-            if (!rlc_row(a, h) && before(hi) > before(lo)) draw_row(a, t, h);  // dense rows: from the table
+            if (before(hi) > before(lo)) draw_row(a, t, h);
         }
         for (uint32_t k = tid - 64; k < nl; k += kBlock - 64) {
             uint32_t pt = ~0u, pw = 0, pc = 0;
