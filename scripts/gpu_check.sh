@@ -150,6 +150,9 @@ for s in "$@"; do
         pmc7w) pmc pmc7w 7 WRITE_SIZE ;;
         pmc7sq) pmc pmc7sq 7 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
                     SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_WAIT_INST_LDS ;;
+        pmc7ic) step pmc7ic 120 rocprofv3 --kernel-trace --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_IFETCH SQ_WAVE_CYCLES \
+                    -f csv -d gpurun_out/pmc7ic -o run -- python bench.py --config 7 --steps 3 --warmup 1 --cpu-seconds 0 \
+                    --no-verify --extra-configs 0 ;;
         pmc7sq2) pmc pmc7sq2 7 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT \
                     SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_SMEM ;;
         sqa*) c=${s#sqa}; pmc sqa$c $c SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
