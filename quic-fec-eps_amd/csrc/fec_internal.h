@@ -209,6 +209,10 @@ struct CombArgs {
     // instead of XCD-contiguous regions (a dense run of real jobs among empty
     // slots would otherwise land on one XCD)
     int interleave;
+    // device-sized launch over mostly empty slots: each workgroup gathers the
+    // non-empty jobs of its share (runs of kCombRun slots dealt round-robin)
+    // into LDS and runs them in groups as large as `budget` holds
+    int sparse;
     uint32_t budget;
     // every job has the same coefficient block (a block code's parity rows:
     // wide encode): [nout_max][nin_max] at coef, its tables built once per
@@ -216,6 +220,8 @@ struct CombArgs {
     // output pointers), so more jobs fit a workgroup
     int shared_coef;
 };
+constexpr uint32_t kCombRun = 16;                                    // sparse launches: slots per run
+constexpr uint32_t kCombListLds = 256 * (uint32_t)sizeof(CombJob);   // sparse launches: one round's jobs
 // LDS bytes per job of comb_kernel<R> at nin_max inputs
 __host__ __device__ inline uint32_t comb_job_lds(int nin_max, int R) {
     const uint32_t rt = R == 1 ? 1u : (uint32_t)(R + 3) & ~3u;
@@ -332,6 +338,10 @@ constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
 #ifndef FECGPU_SWD_SOLVE_LIST
 #define FECGPU_SWD_SOLVE_LIST 0  // fused plan: solve jobs in a compact list (one atomic per system: 24 us slower on cfg7, r04)
                                  // instead of slots per unknown (the solve pass walks every slot)
+#endif
+#ifndef FECGPU_SWD_SPARSE
+#define FECGPU_SWD_SPARSE 1  // the syndrome and solve launches gather their non-empty job slots
+                             // (CombArgs::sparse) instead of walking every slot in groups
 #endif
 #ifndef FECGPU_SWD_ONEPASS
 #define FECGPU_SWD_ONEPASS 1  // fused plan: the system pass takes systems of up to 64 unknowns /

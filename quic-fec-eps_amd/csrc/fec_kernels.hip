@@ -2238,7 +2238,8 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
     __shared__ uint32_t s_nin[kMaxWpb];
     __shared__ uint8_t s_ne[kMaxWpb], s_perm[kMaxWpb];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint8_t *regions = reinterpret_cast<uint8_t *>(dyn);
+    // sparse launches: the gathered jobs' headers first (kCombListLds)
+    uint8_t *regions = reinterpret_cast<uint8_t *>(dyn) + (a.sparse ? kCombListLds : 0u);
     constexpr int RT = CombRegion<R>::RT;
 #if FECGPU_CHECK
     // the checked build bounds the block kernels' symbol accesses; the
@@ -2258,6 +2259,7 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
         nin_max = max(1, min((int)*a.nin_dev, a.nin_max));
         job_lds = comb_job_lds(nin_max, R);
         wpb = choose_wpb_dev(a.ncol, job_lds, a.budget);
+        if (a.sparse) wpb = max(1, min(kMaxWpb, (int)(a.budget / job_lds)));  // as many gathered jobs as fit
     }
     // shared coefficient block: its tables once per workgroup, before any group
     const bool shared = a.shared_coef != 0;
@@ -2283,18 +2285,18 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
         return shared ? CombRegion<R>(regions, regions + tab_lds + (size_t)jl * job_lds, nin_max)
                       : CombRegion<R>(regions + (size_t)jl * job_lds, nin_max);
     };
-    for (XcdRange xr = xcd_range((njobs + wpb - 1) / wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
-        const uint64_t j0 = xr.cur * wpb;
-        const int nb = (int)min((uint64_t)wpb, njobs - j0);
+    // one group of nb jobs (jobAt(jl): job jl of the group): tables, then its
+    // (job, column) slots over the workgroup
+    constexpr int NW = kBlock / 64;
+    const auto run_group = [&](int nb, auto &&jobAt) __attribute__((always_inline)) {
         // plan: wave w builds the tables of jobs w, w + 4, ...  Their headers
         // come in one round of loads, a lane each (the decode passes walk a
         // slot per repair or unknown, most of them empty: one dependent load
         // per job was most of those passes' time)
-        constexpr int NW = kBlock / 64;
 #if FECGPU_COMB_HDR
         CombJob Jl{};
         Jl.xor_off = kNoXor;
-        if (wave + NW * lane < nb) Jl = a.jobs[j0 + wave + NW * lane];
+        if (wave + NW * lane < nb) Jl = jobAt(wave + NW * lane);
 #endif
         for (int ji = 0, jl = wave; jl < nb; ji++, jl += NW) {
 #if FECGPU_COMB_HDR
@@ -2310,7 +2312,7 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
             J.nin = (uint32_t)__builtin_amdgcn_readlane((int)Jl.nin, ji);
             J.nout = (uint32_t)__builtin_amdgcn_readlane((int)Jl.nout, ji);
 #else
-            const CombJob J = a.jobs[j0 + jl];
+            const CombJob J = jobAt(jl);
 #endif
             const int nin = min((int)J.nin, nin_max), nout = min((int)(J.nout & ~kCombXorScaled), R);
             const CombRegion<R> rg = region(jl);
@@ -2373,6 +2375,63 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
                              (int)s_nin[jl], ne, col, rg, a.skip && a.ncol >= 64);
         }
         __syncthreads();
+    };
+    if (a.sparse) {
+        // mostly empty job slots (a decode's slot per repair / per unknown): the
+        // workgroup gathers the non-empty jobs of 256 slots at a time into LDS,
+        // then runs them in groups as large as its LDS holds.  Slots are dealt
+        // in runs of kCombRun consecutive ones, round-robin over the
+        // workgroups: every workgroup gets a like share of a dense region (the
+        // one-unknown systems' slots), and consecutive repairs (overlapping
+        // windows) stay together.
+        CombJob *s_list = reinterpret_cast<CombJob *>(dyn);
+        __shared__ uint32_t s_wc[NW + 1];
+        const int cap = max(1, min(kMaxWpb, wpb));
+        constexpr uint32_t kRuns = kBlock / kCombRun;  // runs per round
+        const uint64_t nrun = (njobs + kCombRun - 1) / kCombRun;
+        for (uint64_t r0 = blockIdx.x; r0 < nrun; r0 += (uint64_t)gridDim.x * kRuns) {
+            const uint64_t run = r0 + (uint64_t)gridDim.x * (tid / kCombRun);
+            const uint64_t slot = run * kCombRun + tid % kCombRun;
+            const CombJob J = a.jobs[min(slot, njobs - 1)];  // (njobs > 0 here)
+            const bool live = run < nrun && slot < njobs && (J.nout & ~kCombXorScaled) != 0;
+            const uint64_t b = __ballot(live);
+            if (lane == 0) s_wc[wave] = (uint32_t)__popcll(b);
+            __syncthreads();
+            uint32_t off = 0, k = 0;
+            for (int w = 0; w < NW; w++) {
+                off += w < wave ? s_wc[w] : 0u;
+                k += s_wc[w];
+            }
+            if (live) {
+                CombJob &L = s_list[off + __popcll(b & ((1ull << lane) - 1ull))];
+                L.in_off = J.in_off;
+                L.coef_off = J.coef_off;
+                L.out_list = J.out_list;
+                L.xor_off = J.xor_off;
+                L.nin = J.nin;
+                L.nout = J.nout;
+            }
+            __syncthreads();
+            for (uint32_t g0 = 0; g0 < k; g0 += (uint32_t)cap)
+                run_group((int)min<uint32_t>((uint32_t)cap, k - g0),
+                          [&](int jl) __attribute__((always_inline)) {
+                              const CombJob &L = s_list[g0 + jl];
+                              CombJob J;
+                              J.in_off = L.in_off;
+                              J.coef_off = L.coef_off;
+                              J.out_list = L.out_list;
+                              J.xor_off = L.xor_off;
+                              J.nin = L.nin;
+                              J.nout = L.nout;
+                              return J;
+                          });
+        }
+        return;
+    }
+    for (XcdRange xr = xcd_range((njobs + wpb - 1) / wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+        const uint64_t j0 = xr.cur * wpb;
+        const int nb = (int)min((uint64_t)wpb, njobs - j0);
+        run_group(nb, [&](int jl) __attribute__((always_inline)) { return a.jobs[j0 + jl]; });
     }
 }
 
@@ -2625,7 +2684,7 @@ hipError_t launch_comb(CombArgs a, int R, hipStream_t s) {
     if (a.nin_dev) {
         // device-sized: persistent, 2 x the workgroups resident at the budget
         // (the job count and widths are device data; surplus workgroups exit)
-        lds = a.budget;
+        lds = a.budget + (a.sparse ? kCombListLds : 0u);
         const void *fn = R == 1 ? (const void *)comb_kernel<1> : R == 2 ? (const void *)comb_kernel<2>
                        : R == 4 ? (const void *)comb_kernel<4> : (const void *)comb_kernel<8>;
         const uint64_t groups_max = nmax;  // at least one job per group

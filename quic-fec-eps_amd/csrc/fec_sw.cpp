@@ -354,6 +354,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     sa.extra_max = nsrc;
     sa.interleave = 1;  // those are dense at the end: deal the groups round-robin
 #endif
+    sa.sparse = FECGPU_SWD_SPARSE;
     sa.ncol = ncol;
     sa.stride = stride;
     sa.nin_max = kSwMaxWindow;
@@ -381,6 +382,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     va.nout_max = kSwSolveOut;
     va.nin_dev = &a.ctr->maxin;
     va.budget = kSolveBudget;
+    va.sparse = FECGPU_SWD_SPARSE;
     SW_TRY(launch_comb(va, kSwSolveOut, s), "sliding-window solve launch");
     SW_TRY(launch_sw_dec_replay(a, s), "sliding-window long-system replay launch");
     if (ctr_out) SW_TRY(hipMemcpyAsync(ctr_out, a.ctr, sizeof(SwDecCtr), hipMemcpyDeviceToHost, s), "D2H sw counters");
