@@ -159,7 +159,8 @@ struct fecgpu_ctx {
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
     int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
-    int sw_stream = 1;  // sliding-window encode: 0 combine jobs, 1 / 2 streaming (dwords per lane)
+    int sw_stream = FECGPU_SW_STREAM_DEFAULT;  // sliding-window encode: 0 combine jobs, 1..5 streaming
+                                               // (dwords per lane), kSwStreamAuto per symbol size
     int sw_long_min = kSwSmallE + 1;  // sliding-window decode: unknowns that force the long-system path
     uint64_t sw_log_entries = 0;      // long-system operation log: fixed size (tuning), 0 = automatic
     uint64_t sw_log_seen = 0;         // the largest log an overflow asked for on this ctx
@@ -343,7 +344,7 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         return 0;
     }
     if (!std::strcmp(key, "sw_stream")) {
-        if (value < 0 || value > 2) return FECGPU_ERR_INVALID_ARG;
+        if (value < 0 || value > kSwStreamAuto) return FECGPU_ERR_INVALID_ARG;
         ctx->sw_stream = (int)value;  // calls and objects created from now on
         return 0;
     }

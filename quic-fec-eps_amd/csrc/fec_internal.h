@@ -311,7 +311,7 @@ struct SwStreamArgs {
 inline uint64_t sw_stream_gtab_bytes(uint64_t nrep, int max_window) {
     return (2ull * kSwStreamU + nrep * (uint64_t)(max_window + kSwStreamU)) * 16ull;
 }
-// C: dwords per lane (1 or 2); LDS budget per workgroup in bytes
+// C: dwords per lane (1..5, dividing the row's dwords); LDS budget per workgroup in bytes
 hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t s);
 // LDS per streaming-encode repair: kSwStreamU zero tables and max_window
 // tables (20 B each), coefficient bytes
@@ -477,9 +477,14 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
                        const uint8_t *rlc = nullptr);
 // the ctx's "sw_group" tuning (repairs per sliding-window encode job)
 int ctx_sw_group(const fecgpu_ctx *ctx);
-// the ctx's "sw_stream" tuning: 0 combine jobs, 1 / 2 the streaming encode
-// with 1 / 2 dwords per lane
+// the ctx's "sw_stream" tuning: 0 combine jobs, 1..5 the streaming encode
+// with that many dwords per lane, kSwStreamAuto (default) chosen per symbol size
 int ctx_sw_stream(const fecgpu_ctx *ctx);
+constexpr int kSwStreamAuto = 6;
+#ifndef FECGPU_SW_STREAM_DEFAULT
+#define FECGPU_SW_STREAM_DEFAULT kSwStreamAuto  // the ctx's "sw_stream" default (A/B builds: 1)
+#endif
+int sw_stream_dwords(int stream, uint32_t S);
 // "sw_long_min": systems of at least this many unknowns take the long-system
 // path even when the small one would fit (default kSwSmallE + 1)
 int ctx_sw_long_min(const fecgpu_ctx *ctx);

@@ -138,6 +138,36 @@ bool sw_groups_fit(const fecgpu_sw_repair *h, uint64_t nrep, uint64_t nsrc, int 
     return true;
 }
 
+// Dwords per lane of the streaming encode for ctx "sw_stream" value `stream`
+// (1..5: that many, or the largest divisor of the row's dwords below it;
+// kSwStreamAuto: the cheapest by a per-row cost of waves x max(VALU, LDS)).
+// A lane's table reads (two LDS reads per product, the same on every lane)
+// are shared by its C dwords: at C = 1 the LDS, not the VALU, bounded the
+// kernel (profiles/r04, 62 % VALU busy).  The row's dwords D = 4 x 16-B
+// columns; C divides D so no lane runs past a row.
+int sw_stream_dwords(int stream, uint32_t S) {
+    const uint32_t D = ((S + 15u) >> 4) * 4u;
+    if (stream != kSwStreamAuto) {
+        int C = std::min(std::max(stream, 1), 5);
+        while (D % (uint32_t)C) C--;
+        return C;
+    }
+    int best = 1;
+    uint64_t best_cost = ~0ull;
+    for (int C = 1; C <= 5; C++) {
+        if (D % (uint32_t)C) continue;
+        const uint64_t units = D / (uint32_t)C, waves = (units + 63) / 64;
+        // per source row: VALU ~26 instructions per dword and slot group, LDS
+        // ~40 CU cycles of table reads per wave (cfg7 ISA, r04)
+        const uint64_t cost = waves * std::max<uint64_t>(26u * (uint32_t)C, 40u);
+        if (cost <= best_cost) {
+            best_cost = cost;
+            best = C;
+        }
+    }
+    return best;
+}
+
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *pj, void *pc,
                        void *po, hipStream_t s, int group, const fecgpu_sw_repair *hdr_host, int stream,
@@ -153,7 +183,7 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
         sa.nrep = nrep;
         sa.stride = stride;
         sa.max_window = max_window;
-        const int C = stream >= 2 ? 2 : 1;
+        const int C = sw_stream_dwords(stream, S);
         sa.ncu = ((S + 15u) >> 4) * 4u / (uint32_t)C;
         SW_TRY(launch_sw_stream(sa, C, kStreamBudget, s), "sliding-window streaming encode launch");
         return 0;

@@ -27,6 +27,10 @@ namespace fecgpu {
 namespace {
 
 constexpr int kSwsU = kSwStreamU;
+#ifndef FECGPU_SWS_WAVE_LDS_KB
+#define FECGPU_SWS_WAVE_LDS_KB 12  // multiply-table LDS per wave of a workgroup (capped by the budget)
+#endif
+constexpr uint32_t kSwsWaveLds = FECGPU_SWS_WAVE_LDS_KB << 10;
 #ifndef FECGPU_SWS_AMAX
 #define FECGPU_SWS_AMAX 4  // accumulator slots compiled (a segment needing more takes P > 1 passes)
 #endif
@@ -56,14 +60,27 @@ typedef __attribute__((address_space(1))) uint32_t *g32;
 typedef __attribute__((address_space(1))) const u32x2 *g64c;
 typedef __attribute__((address_space(1))) u32x2 *g64;
 
+// C dwords of a lane: one load / store for C = 1, 2, 4 (4: 16-B aligned, the
+// rows are), dword by dword for 3 and 5 (4-B aligned)
+typedef __attribute__((address_space(1))) const u32x4 *g128c;
+typedef __attribute__((address_space(1))) u32x4 *g128;
 template <int C>
 __device__ __forceinline__ void ldc(const uint8_t *p, uint32_t (&x)[C]) {
     if constexpr (C == 1) {
         x[0] = *(g32c)(p);
-    } else {
+    } else if constexpr (C == 2) {
         const u32x2 v = *(g64c)(p);
         x[0] = v.x;
         x[1] = v.y;
+    } else if constexpr (C == 4) {
+        const u32x4 v = *(g128c)(p);
+        x[0] = v.x;
+        x[1] = v.y;
+        x[2] = v.z;
+        x[3] = v.w;
+    } else {
+#pragma unroll
+        for (int d = 0; d < C; d++) x[d] = ((g32c)(p))[d];
     }
 }
 // Buffer loads: the resource (a batch's first row, scalar) plus a scalar row
@@ -74,19 +91,34 @@ template <int C>
 __device__ __forceinline__ void ldc_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t (&x)[C]) {
     if constexpr (C == 1) {
         x[0] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
-    } else {
+    } else if constexpr (C == 2) {
         const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
         x[0] = v.x;
         x[1] = v.y;
+    } else if constexpr (C == 4) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+        x[0] = v.x;
+        x[1] = v.y;
+        x[2] = v.z;
+        x[3] = v.w;
+    } else {
+#pragma unroll
+        for (int d = 0; d < C; d++) x[d] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff + 4 * d, (int)soff, 0);
     }
 }
 template <int C>
 __device__ __forceinline__ void stc(uint8_t *p, const uint32_t (&x)[C]) {
     if constexpr (C == 1) {
         *(g32)(p) = x[0];
-    } else {
+    } else if constexpr (C == 2) {
         const u32x2 v = {x[0], x[1]};
         *(g64)(p) = v;
+    } else if constexpr (C == 4) {
+        const u32x4 v = {x[0], x[1], x[2], x[3]};
+        *(g128)(p) = v;
+    } else {
+#pragma unroll
+        for (int d = 0; d < C; d++) ((g32)(p))[d] = x[d];
     }
 }
 
@@ -535,18 +567,32 @@ uint64_t resident(const void *fn, int C, uint32_t block, uint32_t lds) {
 }
 }  // namespace
 
+template <int C, bool G>
+const void *sws_fn() {
+    return reinterpret_cast<const void *>(sw_stream_kernel<C, G>);
+}
+
 hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t s) {
     if (a.nrep == 0) return hipSuccess;
-    const bool G = FECGPU_SWS_SGPR && a.gtab;
-    const void *fn = G ? (C == 2 ? reinterpret_cast<const void *>(sw_stream_kernel<2, true>)
-                                 : reinterpret_cast<const void *>(sw_stream_kernel<1, true>))
-                       : (C == 2 ? reinterpret_cast<const void *>(sw_stream_kernel<2, false>)
-                                 : reinterpret_cast<const void *>(sw_stream_kernel<1, false>));
+    const bool G = FECGPU_SWS_SGPR && a.gtab && C <= 2;
+    const void *fn = nullptr;
+    switch (C) {
+        case 1: fn = G ? sws_fn<1, true>() : sws_fn<1, false>(); break;
+        case 2: fn = G ? sws_fn<2, true>() : sws_fn<2, false>(); break;
+        case 3: fn = sws_fn<3, false>(); break;
+        case 4: fn = sws_fn<4, false>(); break;
+        case 5: fn = sws_fn<5, false>(); break;
+        default: return hipErrorInvalidValue;
+    }
     const int W = std::max(1, a.max_window);
     a.max_window = W;
     // column passes of at most 512 lanes, as even as 64-lane waves allow
     const uint32_t passes = (a.ncu + 511) / 512;
     a.cpass = ((a.ncu + passes - 1) / passes + 63) / 64 * 64;
+    // LDS per workgroup in proportion to its waves (kSwsWaveLds each, at most
+    // `budget`): a one-wave workgroup (C = 5 over a 1200-B row) with the whole
+    // budget would leave 3 waves on a CU
+    budget = std::min<uint32_t>(budget, std::max<uint32_t>(1, a.cpass / 64) * kSwsWaveLds);
     a.segcap = G ? kSwSeg : (int)std::max<uint32_t>(1, std::min<uint32_t>(kSwSeg, budget / sw_stream_rep_lds(W)));
     a.lds = G ? 0u : sw_stream_lds(a.segcap, W);
     if (G) {
@@ -566,15 +612,20 @@ hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t 
     a.segcap = (int)std::max<uint64_t>(1, (a.nrep + R * rounds - 1) / (R * rounds));
     a.nseg = (a.nrep + a.segcap - 1) / a.segcap;
     const uint64_t grid = std::min<uint64_t>(a.nseg, R);
-    if (G) {
-        if (C == 2)
-            hipLaunchKernelGGL((sw_stream_kernel<2, true>), dim3((unsigned)grid), dim3(a.cpass), 0, s, a);
-        else
-            hipLaunchKernelGGL((sw_stream_kernel<1, true>), dim3((unsigned)grid), dim3(a.cpass), 0, s, a);
-    } else if (C == 2) {
-        hipLaunchKernelGGL((sw_stream_kernel<2, false>), dim3((unsigned)grid), dim3(a.cpass), a.lds, s, a);
-    } else {
-        hipLaunchKernelGGL((sw_stream_kernel<1, false>), dim3((unsigned)grid), dim3(a.cpass), a.lds, s, a);
+    const dim3 gd((unsigned)grid), bd(a.cpass);
+    const uint32_t lds = G ? 0u : a.lds;
+    switch (C) {
+        case 1:
+            if (G) hipLaunchKernelGGL((sw_stream_kernel<1, true>), gd, bd, lds, s, a);
+            else hipLaunchKernelGGL((sw_stream_kernel<1, false>), gd, bd, lds, s, a);
+            break;
+        case 2:
+            if (G) hipLaunchKernelGGL((sw_stream_kernel<2, true>), gd, bd, lds, s, a);
+            else hipLaunchKernelGGL((sw_stream_kernel<2, false>), gd, bd, lds, s, a);
+            break;
+        case 3: hipLaunchKernelGGL((sw_stream_kernel<3, false>), gd, bd, lds, s, a); break;
+        case 4: hipLaunchKernelGGL((sw_stream_kernel<4, false>), gd, bd, lds, s, a); break;
+        default: hipLaunchKernelGGL((sw_stream_kernel<5, false>), gd, bd, lds, s, a); break;
     }
     return hipGetLastError();
 }

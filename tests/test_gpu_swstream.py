@@ -1,5 +1,5 @@
 """Streaming sliding-window encode (quic-fec-eps_amd/csrc/fec_swenc.hip; ctx tuning
-"sw_stream" 1 / 2 = 1 / 2 dwords per lane) against the CPU oracle
+"sw_stream" 1..5 = that many dwords per lane, 6 = chosen per symbol size) against the CPU oracle
 (oracle/fec_oracle.c orc_sw_encode) and against the combine-job encode
 ("sw_stream" 0).  Bit-exact on bytes [0, S) of every repair.
 
@@ -19,6 +19,7 @@ import oracle as O  # noqa: E402
 import np_oracle as N  # noqa: E402
 
 pytestmark = pytest.mark.gpu
+MODES = (0, 1, 2, 3, 4, 5, 6)   # 0 the combine-job encode; 3 / 5 fall back to a divisor of the row's dwords
 
 
 @pytest.fixture(scope="module")
@@ -26,7 +27,7 @@ def ctxs():
     assert torch.cuda.is_available()
     O.build()
     out = {}
-    for mode in (0, 1, 2):
+    for mode in MODES:
         c = fecgpu.Context()
         c.set_tuning("sw_stream", mode)
         out[mode] = c
@@ -93,7 +94,7 @@ NSRC = 1200
 CASES = list(schedules(NSRC, np.random.default_rng(0)).keys())
 
 
-@pytest.mark.parametrize("L", [1, 17, 1200, 9000])
+@pytest.mark.parametrize("L", [1, 17, 40, 1200, 9000])
 @pytest.mark.parametrize("name", CASES)
 def test_stream_encode_vs_oracle(ctxs, name, L):
     sched, mw = schedules(NSRC, np.random.default_rng(0))[name]
@@ -103,7 +104,7 @@ def test_stream_encode_vs_oracle(ctxs, name, L):
     src = stream(NSRC, L, stride, L + len(name))
     hdr = hdr_array(sched)
     o = O.sw_encode(src, hdr, L)
-    for mode in (1, 2, 0):
+    for mode in MODES:
         g = gpu_encode(ctxs[mode], src, hdr, L, mw)
         assert np.array_equal(g[:, :L], o[:, :L]), f"sw_stream {mode}"
 
@@ -121,7 +122,7 @@ def test_stream_encode_empty_and_clipped(ctxs):
     clipped = list(raw)
     clipped[11] = (nsrc - 3, 3, 78, 15)
     clipped[20] = (h[20][0], 32, 79, 15)
-    for mode in (1, 2):
+    for mode in MODES[1:]:
         g = gpu_encode(ctxs[mode], src, hdr_array(raw), L, 32)
         keep = [t for t in range(len(raw)) if t != 10]
         o = O.sw_encode(src, hdr_array([clipped[t] for t in keep]), L)
@@ -137,16 +138,16 @@ def test_stream_encode_segment_edges(ctxs, nrep):
     src = stream(nsrc, L, 112, nrep)
     hdr = hdr_array(N.sw_schedule(nsrc, k, W, key0=nrep)[:nrep])
     o = O.sw_encode(src, hdr, L)
-    for mode in (1, 2):
+    for mode in MODES[1:]:
         assert np.array_equal(gpu_encode(ctxs[mode], src, hdr, L, W)[:, :L], o[:, :L])
 
 
 def test_stream_tuning_values():
     c = fecgpu.Context()
     try:
-        for v in (0, 1, 2):
+        for v in MODES:
             c.set_tuning("sw_stream", v)
-        for v in (-1, 3):
+        for v in (-1, 7):
             with pytest.raises(fecgpu.FecError):
                 c.set_tuning("sw_stream", v)
     finally:
