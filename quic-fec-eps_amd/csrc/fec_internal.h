@@ -482,7 +482,9 @@ int ctx_sw_group(const fecgpu_ctx *ctx);
 int ctx_sw_stream(const fecgpu_ctx *ctx);
 constexpr int kSwStreamAuto = 6;
 #ifndef FECGPU_SW_STREAM_DEFAULT
-#define FECGPU_SW_STREAM_DEFAULT kSwStreamAuto  // the ctx's "sw_stream" default (A/B builds: 1)
+#define FECGPU_SW_STREAM_DEFAULT 1  // the ctx's "sw_stream" default: 1 dword per lane (cfg7 A/B, r04:
+                                   // C = 1 / 2 / 3 / 4 / 5 gave 0.213 / 0.240 / 0.226 / 0.258 / 0.235 ms;
+                                   // the VALU, not the LDS table reads, bounds the kernel)
 #endif
 int sw_stream_dwords(int stream, uint32_t S);
 // "sw_long_min": systems of at least this many unknowns take the long-system

@@ -140,11 +140,12 @@ bool sw_groups_fit(const fecgpu_sw_repair *h, uint64_t nrep, uint64_t nsrc, int 
 
 // Dwords per lane of the streaming encode for ctx "sw_stream" value `stream`
 // (1..5: that many, or the largest divisor of the row's dwords below it;
-// kSwStreamAuto: the cheapest by a per-row cost of waves x max(VALU, LDS)).
-// A lane's table reads (two LDS reads per product, the same on every lane)
-// are shared by its C dwords: at C = 1 the LDS, not the VALU, bounded the
-// kernel (profiles/r04, 62 % VALU busy).  The row's dwords D = 4 x 16-B
-// columns; C divides D so no lane runs past a row.
+// kSwStreamAuto: the fewest lane-slots per row, waves x C, ties to the
+// smaller C).  A lane's table reads (the same on every lane) are shared by
+// its C dwords, but the VALU work per dword is not, and C > 1 costs
+// registers: on cfg7 C = 1 was fastest (fec_internal.h
+// FECGPU_SW_STREAM_DEFAULT).  The row's dwords D = 4 x 16-B columns; C
+// divides D so no lane runs past a row.
 int sw_stream_dwords(int stream, uint32_t S) {
     const uint32_t D = ((S + 15u) >> 4) * 4u;
     if (stream != kSwStreamAuto) {
@@ -156,11 +157,8 @@ int sw_stream_dwords(int stream, uint32_t S) {
     uint64_t best_cost = ~0ull;
     for (int C = 1; C <= 5; C++) {
         if (D % (uint32_t)C) continue;
-        const uint64_t units = D / (uint32_t)C, waves = (units + 63) / 64;
-        // per source row: VALU ~26 instructions per dword and slot group, LDS
-        // ~40 CU cycles of table reads per wave (cfg7 ISA, r04)
-        const uint64_t cost = waves * std::max<uint64_t>(26u * (uint32_t)C, 40u);
-        if (cost <= best_cost) {
+        const uint64_t units = D / (uint32_t)C, cost = (units + 63) / 64 * (uint32_t)C;
+        if (cost < best_cost) {
             best_cost = cost;
             best = C;
         }

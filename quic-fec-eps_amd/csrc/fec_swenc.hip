@@ -41,6 +41,9 @@ constexpr int kSwsAmax = FECGPU_SWS_AMAX < kSwSlots ? FECGPU_SWS_AMAX : kSwSlots
 #ifndef FECGPU_SWS_PINGPONG
 #define FECGPU_SWS_PINGPONG 1  // row buffers trade roles between batches (else copied)
 #endif
+#ifndef FECGPU_SWS_LDSBATCH
+#define FECGPU_SWS_LDSBATCH 1  // a source pair's tables for every slot loaded before any product
+#endif
 #ifndef FECGPU_SWS_BUF
 #define FECGPU_SWS_BUF 1  // source rows by buffer loads (scalar row offsets)
 #endif
@@ -411,14 +414,37 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
 #pragma unroll
         for (int i = 0; i < U; i += 2) {
             const SplitC<C> s0 = split_c<C>(X[i]), s1 = split_c<C>(X[i + 1]);
+#if FECGPU_SWS_LDSBATCH
+            // every slot's tables for the pair in flight at once (one LDS wait,
+            // not one per slot)
+            uint4 A0[A], A1[A];
+            uint32_t C0[A], C1[A];
 #pragma unroll
             for (int m = 0; m < A; m++) {
+                A0[m] = tab[m][i];
+                A1[m] = tab[m][i + 1];
+                C0[m] = tcb[m][i];
+                C1[m] = tcb[m][i + 1];
+            }
+#pragma unroll
+            for (int m = 0; m < A; m++) {
+                asm("" : "+v"(A0[m].x), "+v"(A0[m].y), "+v"(A0[m].z), "+v"(A0[m].w), "+v"(C0[m]));
+                asm("" : "+v"(A1[m].x), "+v"(A1[m].y), "+v"(A1[m].z), "+v"(A1[m].w), "+v"(C1[m]));
+            }
+#endif
+#pragma unroll
+            for (int m = 0; m < A; m++) {
+#if FECGPU_SWS_LDSBATCH
+                const uint4 a0 = A0[m], a1 = A1[m];
+                const uint32_t c0 = C0[m], c1 = C1[m];
+#else
                 uint4 a0 = tab[m][i], a1 = tab[m][i + 1];
                 uint32_t c0 = tcb[m][i], c1 = tcb[m][i + 1];
                 // tables stay in vector registers (uniform values would be
                 // moved to scalar ones with a readfirstlane each)
                 asm("" : "+v"(a0.x), "+v"(a0.y), "+v"(a0.z), "+v"(a0.w), "+v"(c0));
                 asm("" : "+v"(a1.x), "+v"(a1.y), "+v"(a1.z), "+v"(a1.w), "+v"(c1));
+#endif
 #pragma unroll
                 for (int d = 0; d < C; d++) {
                     uint32_t t = xor3s(acc[m][d], __builtin_amdgcn_perm(a0.y, a0.x, s0.a[d]),
