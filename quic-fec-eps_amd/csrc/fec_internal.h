@@ -213,6 +213,9 @@ struct CombArgs {
     // non-empty jobs of its share (runs of kCombRun slots dealt round-robin)
     // into LDS and runs them in groups as large as `budget` holds
     int sparse;
+    // nonzero and below 4 GiB: every input row lies in [in_base, in_base + in_bytes)
+    // (the kernel reads rows by buffer loads with scalar row offsets)
+    uint64_t in_bytes;
     uint32_t budget;
     // every job has the same coefficient block (a block code's parity rows:
     // wide encode): [nout_max][nin_max] at coef, its tables built once per

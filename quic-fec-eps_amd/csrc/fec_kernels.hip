@@ -2060,11 +2060,32 @@ struct CombRegion {
     }
 };
 
+// Input rows of a combine slot: global pointers (row 0 of this lane's column),
+// or — CombArgs::in_bytes below 4 GiB — a buffer resource over the whole input
+// region with this lane's column offset and the row offset a scalar: no 64-bit
+// address arithmetic per row on the vector ALU, and a row past a lane's job
+// (its wave runs to the widest job's row count) reads data inside the region,
+// or zeros past it, and is never multiplied.
+constexpr int kCombRsrcWord3 = 0x00020000;  // raw 32-bit data (gfx9 buffer resource word 3)
+struct RowSrc {
+    const uint8_t *in;
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t voff;
+    bool buf;  // wave-uniform
+};
+__device__ __forceinline__ uint4 row_ld(const RowSrc &rs, int q, int nin, uint32_t stride) {
+    if (rs.buf) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs.r, (int)rs.voff, (int)((uint32_t)q * stride), 0);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return ld16(rs.in + (uint32_t)min(q, nin - 1) * stride);
+}
+
 // One slot (job, 16-B column) for NE outputs (wave-uniform): acc[u] = sum_q
 // T[q][u] * in_q over the job's nin rows (8 loads in flight), optional xor
 // row, stores for u < ne (this lane's job).
 template <int R, int NE>
-__device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, int nin, int ne, uint32_t col,
+__device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int nin, int ne, uint32_t col,
                                           const CombRegion<R> &rg, bool skip) {
     constexpr int U = FECGPU_COMB_U, RT = CombRegion<R>::RT;
     uint4 acc[NE];
@@ -2073,7 +2094,7 @@ __device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, in
     for (int q0 = 0; q0 < nin; q0 += U) {
         uint4 v[U];
 #pragma unroll
-        for (int t = 0; t < U; t++) v[t] = ld16(in + (uint32_t)min(q0 + t, nin - 1) * stride);
+        for (int t = 0; t < U; t++) v[t] = row_ld(rs, q0 + t, nin, stride);
 #pragma unroll
         for (int t = 0; t < U; t++) {
             if (q0 + t < nin) {
@@ -2113,6 +2134,13 @@ __device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, in
 #ifndef FECGPU_COMB_PF
 #define FECGPU_COMB_PF 1  // one-output combine jobs: next rows loaded while this batch multiplies
 #endif
+#ifndef FECGPU_COMB_PF8
+#define FECGPU_COMB_PF8 0  // ... and the 8-output ones (solves: their widest job's rows are
+                           // dependent round trips; 221 VGPRs instead of 128, A/B pending)
+#endif
+#ifndef FECGPU_COMB_PF_U
+#define FECGPU_COMB_PF_U 4  // rows per prefetched batch of the 8-output slots (registers)
+#endif
 // comb_slot with the rows of batch i + 1 in flight while batch i multiplies
 // (two 8-row buffers) and the xor row loaded with the first batch.  A
 // workgroup streams its jobs' slots pass after pass, so without the prefetch
@@ -2123,9 +2151,9 @@ __device__ __forceinline__ void comb_slot(const uint8_t *in, uint32_t stride, in
 // compiler's wait counts would merge to the stricter path.  Rows past a
 // lane's nin reload its last row and are not multiplied.
 template <int R, int NE>
-__device__ __forceinline__ void comb_slot_pf(const uint8_t *in, uint32_t stride, int nin, int ne, uint32_t col,
+__device__ __forceinline__ void comb_slot_pf(const RowSrc &rs, uint32_t stride, int nin, int ne, uint32_t col,
                                              const CombRegion<R> &rg, bool skip) {
-    constexpr int U = 8, RT = CombRegion<R>::RT;
+    constexpr int U = R == 1 ? 8 : FECGPU_COMB_PF_U, RT = CombRegion<R>::RT;
     uint4 acc[NE];
 #pragma unroll
     for (int m = 0; m < NE; m++) acc[m] = zero4();
@@ -2135,10 +2163,10 @@ __device__ __forceinline__ void comb_slot_pf(const uint8_t *in, uint32_t stride,
     nw = __builtin_amdgcn_readfirstlane(nw);
     const uint64_t xp = rg.optr[R];
     // without an xor row: a load of row 0 (a valid address), discarded
-    const uint4 xv = ld16(xp ? reinterpret_cast<const uint8_t *>(xp) + col * 16u : in);
+    const uint4 xv = ld16(xp ? reinterpret_cast<const uint8_t *>(xp) + col * 16u : rs.in);
     auto load = [&](uint4 (&v)[U], int q0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int t = 0; t < U; t++) v[t] = ld16(in + (uint32_t)min(q0 + t, nin - 1) * stride);
+        for (int t = 0; t < U; t++) v[t] = row_ld(rs, q0 + t, nin, stride);
     };
     auto mac = [&](const uint4 (&v)[U], int q0) __attribute__((always_inline)) {
 #pragma unroll
@@ -2184,19 +2212,19 @@ __device__ __forceinline__ void comb_slot_pf(const uint8_t *in, uint32_t stride,
 }
 
 template <int R, int NE = R>
-__device__ __forceinline__ void comb_dispatch(int nw, const uint8_t *in, uint32_t stride, int nin, int ne,
+__device__ __forceinline__ void comb_dispatch(int nw, const RowSrc &rs, uint32_t stride, int nin, int ne,
                                               uint32_t col, const CombRegion<R> &rg, bool skip) {
     if constexpr (NE >= 1) {
-        if constexpr (FECGPU_COMB_PF && R == 1) {
+        if constexpr (FECGPU_COMB_PF && (R == 1 || (FECGPU_COMB_PF8 && R == 8 && NE == 8))) {
             if (nw == NE) {
-                comb_slot_pf<R, NE>(in, stride, nin, ne, col, rg, skip);
+                comb_slot_pf<R, NE>(rs, stride, nin, ne, col, rg, skip);
                 return;
             }
         } else if (nw == NE) {
-            comb_slot<R, NE>(in, stride, nin, ne, col, rg, skip);
+            comb_slot<R, NE>(rs, stride, nin, ne, col, rg, skip);
             return;
         }
-        comb_dispatch<R, NE - 1>(nw, in, stride, nin, ne, col, rg, skip);
+        comb_dispatch<R, NE - 1>(nw, rs, stride, nin, ne, col, rg, skip);
     }
 }
 
@@ -2285,6 +2313,10 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
         return shared ? CombRegion<R>(regions, regions + tab_lds + (size_t)jl * job_lds, nin_max)
                       : CombRegion<R>(regions + (size_t)jl * job_lds, nin_max);
     };
+    // buffer loads of the input rows when the region fits 32-bit offsets (RowSrc)
+    const bool buf = !FECGPU_CHECK && a.in_bytes != 0 && a.in_bytes < (1ull << 32);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.in_base), 0, buf ? (int)(uint32_t)a.in_bytes : 0, kCombRsrcWord3);
     // one group of nb jobs (jobAt(jl): job jl of the group): tables, then its
     // (job, column) slots over the workgroup
     constexpr int NW = kBlock / 64;
@@ -2371,8 +2403,12 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
             const int ne = s_ne[jl];
             const int nw = __builtin_amdgcn_readfirstlane(ne);
             const CombRegion<R> rg = region(jl);
-            comb_dispatch<R>(nw, reinterpret_cast<const uint8_t *>(s_in[jl]) + col * 16u, a.stride,
-                             (int)s_nin[jl], ne, col, rg, a.skip && a.ncol >= 64);
+            RowSrc rs;
+            rs.in = reinterpret_cast<const uint8_t *>(s_in[jl]) + col * 16u;
+            rs.buf = buf;
+            rs.r = rsrc;
+            rs.voff = (uint32_t)(s_in[jl] - reinterpret_cast<uint64_t>(a.in_base)) + col * 16u;
+            comb_dispatch<R>(nw, rs, a.stride, (int)s_nin[jl], ne, col, rg, a.skip && a.ncol >= 64);
         }
         __syncthreads();
     };

@@ -383,6 +383,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     sa.interleave = 1;  // those are dense at the end: deal the groups round-robin
 #endif
     sa.sparse = FECGPU_SWD_SPARSE;
+    sa.in_bytes = nsrc * stride;
     sa.ncol = ncol;
     sa.stride = stride;
     sa.nin_max = kSwMaxWindow;
@@ -411,6 +412,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     va.nin_dev = &a.ctr->maxin;
     va.budget = kSolveBudget;
     va.sparse = FECGPU_SWD_SPARSE;
+    va.in_bytes = std::max<uint64_t>(1, nrep) * stride;  // the syndrome rows
     SW_TRY(launch_comb(va, kSwSolveOut, s), "sliding-window solve launch");
     SW_TRY(launch_sw_dec_replay(a, s), "sliding-window long-system replay launch");
     if (ctr_out) SW_TRY(hipMemcpyAsync(ctr_out, a.ctr, sizeof(SwDecCtr), hipMemcpyDeviceToHost, s), "D2H sw counters");
