@@ -2134,9 +2134,14 @@ __device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int
 #ifndef FECGPU_COMB_PF
 #define FECGPU_COMB_PF 1  // one-output combine jobs: next rows loaded while this batch multiplies
 #endif
+#ifndef FECGPU_COMB_BUF
+#define FECGPU_COMB_BUF 0  // RowSrc buffer loads (cfg7 decode A/B, r04: 0.238 vs 0.222 ms per call with
+                           // pointer loads: off)
+#endif
 #ifndef FECGPU_COMB_PF8
 #define FECGPU_COMB_PF8 0  // ... and the 8-output ones (solves: their widest job's rows are
-                           // dependent round trips; 221 VGPRs instead of 128, A/B pending)
+                           // dependent round trips; but 221 VGPRs instead of 128: cfg7 decode
+                           // 0.246 vs 0.238 ms, r04: off)
 #endif
 #ifndef FECGPU_COMB_PF_U
 #define FECGPU_COMB_PF_U 4  // rows per prefetched batch of the 8-output slots (registers)
@@ -2314,7 +2319,7 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
                       : CombRegion<R>(regions + (size_t)jl * job_lds, nin_max);
     };
     // buffer loads of the input rows when the region fits 32-bit offsets (RowSrc)
-    const bool buf = !FECGPU_CHECK && a.in_bytes != 0 && a.in_bytes < (1ull << 32);
+    const bool buf = FECGPU_COMB_BUF && !FECGPU_CHECK && a.in_bytes != 0 && a.in_bytes < (1ull << 32);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.in_base), 0, buf ? (int)(uint32_t)a.in_bytes : 0, kCombRsrcWord3);
     // one group of nb jobs (jobAt(jl): job jl of the group): tables, then its

@@ -42,7 +42,8 @@ constexpr int kSwsAmax = FECGPU_SWS_AMAX < kSwSlots ? FECGPU_SWS_AMAX : kSwSlots
 #define FECGPU_SWS_PINGPONG 1  // row buffers trade roles between batches (else copied)
 #endif
 #ifndef FECGPU_SWS_LDSBATCH
-#define FECGPU_SWS_LDSBATCH 1  // a source pair's tables for every slot loaded before any product
+#define FECGPU_SWS_LDSBATCH 0  // a source pair's tables for every slot loaded before any product
+                               // (108 VGPRs instead of 73: cfg7 encode 0.287 vs 0.213 ms, r04: off)
 #endif
 #ifndef FECGPU_SWS_BUF
 #define FECGPU_SWS_BUF 1  // source rows by buffer loads (scalar row offsets)
