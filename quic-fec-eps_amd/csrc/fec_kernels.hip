@@ -2143,6 +2143,9 @@ __device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int
                            // dependent round trips; but 221 VGPRs instead of 128: cfg7 decode
                            // 0.246 vs 0.238 ms, r04: off)
 #endif
+#ifndef FECGPU_COMB_PF_U1
+#define FECGPU_COMB_PF_U1 8  // rows per prefetched batch of the one-output slots
+#endif
 #ifndef FECGPU_COMB_PF_U
 #define FECGPU_COMB_PF_U 4  // rows per prefetched batch of the 8-output slots (registers)
 #endif
@@ -2158,7 +2161,7 @@ __device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int
 template <int R, int NE>
 __device__ __forceinline__ void comb_slot_pf(const RowSrc &rs, uint32_t stride, int nin, int ne, uint32_t col,
                                              const CombRegion<R> &rg, bool skip) {
-    constexpr int U = R == 1 ? 8 : FECGPU_COMB_PF_U, RT = CombRegion<R>::RT;
+    constexpr int U = R == 1 ? FECGPU_COMB_PF_U1 : FECGPU_COMB_PF_U, RT = CombRegion<R>::RT;
     uint4 acc[NE];
 #pragma unroll
     for (int m = 0; m < NE; m++) acc[m] = zero4();
@@ -2239,7 +2242,12 @@ __device__ __forceinline__ void comb_dispatch(int nw, const RowSrc &rs, uint32_t
 #ifndef FECGPU_COMB_MINW
 #define FECGPU_COMB_MINW 0  // >0: the grouped encode's combine (R = 4) asks for this many waves per SIMD
 #endif
-#if FECGPU_COMB_MINW > 0
+#ifndef FECGPU_COMB_MINW1
+#define FECGPU_COMB_MINW1 0  // >0: the one-output combine (R = 1) asks for this many waves per SIMD
+#endif
+#if FECGPU_COMB_MINW1 > 0
+#define COMB_WAVES __attribute__((amdgpu_waves_per_eu(R == 1 ? FECGPU_COMB_MINW1 : 1, 8)))
+#elif FECGPU_COMB_MINW > 0
 #define COMB_WAVES __attribute__((amdgpu_waves_per_eu(R == 4 ? FECGPU_COMB_MINW : 1, 8)))
 #else
 #define COMB_WAVES
