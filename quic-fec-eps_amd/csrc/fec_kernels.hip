@@ -2144,7 +2144,8 @@ __device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int
                            // 0.246 vs 0.238 ms, r04: off)
 #endif
 #ifndef FECGPU_COMB_PF_U1
-#define FECGPU_COMB_PF_U1 8  // rows per prefetched batch of the one-output slots
+#define FECGPU_COMB_PF_U1 4  // rows per prefetched batch of the one-output slots (cfg7 decode: 4 rows
+                             // 0.214 vs 8 rows 0.223 ms per call, r04: 107 VGPRs, 4 waves per SIMD)
 #endif
 #ifndef FECGPU_COMB_PF_U
 #define FECGPU_COMB_PF_U 4  // rows per prefetched batch of the 8-output slots (registers)
