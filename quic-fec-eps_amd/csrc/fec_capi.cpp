@@ -669,6 +669,12 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
         if (it == ctx->wide_rows.end()) {
             std::vector<uint8_t> rows;
             host_parity_rows(code, rows);
+            // then [P | I] (r x (k + r)): the two-stage decode's syndrome block
+            const size_t nP = rows.size();
+            rows.resize(nP + (size_t)r * n);
+            for (int i = 0; i < r; i++)
+                for (int q = 0; q < n; q++)
+                    rows[nP + (size_t)i * n + q] = q < k ? rows[(size_t)i * k + q] : (uint8_t)(q - k == i);
             void *d = nullptr;
             HIP_TRY(hipMalloc(&d, rows.size()), "hipMalloc wide parity rows");
             HIP_TRY(hipMemcpy(d, rows.data(), rows.size(), hipMemcpyHostToDevice), "H2D wide parity rows");
@@ -678,7 +684,11 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
     }
     const auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
     const size_t o_out = up(nwin * sizeof(CombJob)), o_coef = o_out + up(nwin * kMaxR * sizeof(uint64_t));
-    const size_t total = o_coef + (decode ? nwin * kMaxR * (size_t)n : 0);
+    const bool two = decode && FECGPU_WIDE_2STAGE;
+    const size_t coef_bytes = decode ? nwin * kMaxR * (size_t)(two ? kMaxR : n) : 0;
+    const size_t o_j1 = o_coef + up(coef_bytes), o_o1 = o_j1 + (two ? up(nwin * sizeof(CombJob)) : 0);
+    const size_t o_syn = o_o1 + (two ? up(nwin * (size_t)r * sizeof(uint64_t)) : 0);
+    const size_t total = o_syn + (two ? nwin * (size_t)r * stride : 0);
     ssize_t rc = ctx_sw_begin(ctx, s);
     if (rc) return rc;
     void *scratch = nullptr;
@@ -688,7 +698,8 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
     // per-window lengths: every window's columns up to the stride
     const uint32_t ncol = sym_len ? stride / 16u : (sym_len_all + 15u) / 16u;
     HIP_TRY(launch_wide(win, present, status, P, nwin, stride, ncol, k, r, decode, reinterpret_cast<CombJob *>(b),
-                        reinterpret_cast<uint64_t *>(b + o_out), b + o_coef, s),
+                        reinterpret_cast<uint64_t *>(b + o_out), b + o_coef, s, reinterpret_cast<CombJob *>(b + o_j1),
+                        reinterpret_cast<uint64_t *>(b + o_o1), b + o_syn),
             "wide batch launch");
     rc = ctx_sw_end(ctx, s);
     if (rc) return rc;

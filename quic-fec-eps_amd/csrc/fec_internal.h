@@ -245,7 +245,16 @@ hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
 // combine kernel over a job per window
 hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
                        uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
-                       uint64_t *outs, uint8_t *coef, hipStream_t s);
+                       uint64_t *outs, uint8_t *coef, hipStream_t s, CombJob *jobs1, uint64_t *outs1,
+                       uint8_t *syn);
+#ifndef FECGPU_WIDE_2STAGE
+// wide decode in two combine launches (fec_wide.hip): syndromes of every
+// repair with one coefficient block [P | I] for all windows (the missing
+// sources' rows zeroed first), then x = T s per window over its r syndromes.
+// Scratch: stage-1 jobs [nwin], their outputs [nwin][r], syndrome rows
+// [nwin][r][stride]; the parity-row block holds [P | I] after P.
+#define FECGPU_WIDE_2STAGE 1
+#endif
 
 // encode: job t = repair t (coefficients at coef + t * kSwCoefPitch, output rep row t).
 // group > 1: the repairs t0 = g * group .. t0 + group - 1 share job g when

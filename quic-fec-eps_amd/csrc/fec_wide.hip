@@ -25,6 +25,10 @@ namespace {
 
 __constant__ GfTables c_gfw = make_gf_tables();
 
+// FECGPU_WIDE_2STAGE (fec_internal.h): the one-launch decode built
+// (k + r + 1) x 161 B of tables per window, so 3 (k 120) or 1 (k 248) windows
+// per workgroup, 75 of its 256 lanes busy per 1200-B window; the two-stage one
+// builds [P | I]'s tables once per workgroup and its stage-2 jobs are 8 x 8.
 #ifndef FECGPU_WIDE_SHARED
 #define FECGPU_WIDE_SHARED 1  // wide encode: parity-row tables shared by a workgroup's jobs
 #endif
@@ -45,7 +49,11 @@ struct WideArgs {
     int k, r, nw;
     CombJob *jobs;   // [nwin]
     uint64_t *outs;  // [nwin][8] (encode: [nwin][r])
-    uint8_t *coef;   // decode: [nwin][8][k + r]
+    uint8_t *coef;   // decode: [nwin][8][k + r] (two-stage: [nwin][8][8], stage 2)
+    // two-stage decode: stage-1 jobs [nwin] and outputs [nwin][r] (syndrome
+    // rows in syn, [nwin][r][stride])
+    CombJob *jobs1;
+    uint64_t *outs1;
 };
 
 __global__ __launch_bounds__(kBlock) void wide_enc_jobs_kernel(WideArgs a) {
@@ -98,6 +106,7 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
         if (lane == 0) {
             a.status[w] = e == 0 ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
             a.jobs[w] = J;
+            if (FECGPU_WIDE_2STAGE) a.jobs1[w] = J;
         }
         return;
     }
@@ -121,6 +130,7 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
             if (lane == 0) {
                 a.status[w] = FECGPU_STATUS_UNRECOVERABLE;
                 a.jobs[w] = J;
+                if (FECGPU_WIDE_2STAGE) a.jobs1[w] = J;
             }
             return;
         }
@@ -141,6 +151,49 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
             xr ^= wmul(s_exp, s_log, f, rq);
         }
     }
+#if FECGPU_WIDE_2STAGE
+    // stage 2's block C[u][i] (8 x 8 per window): T[P_u][c] for the repair i
+    // of pivot row c, else 0; the missing rows zeroed for stage 1
+    {
+        uint8_t *C2 = a.coef + w * (uint64_t)(kMaxR * kMaxR);  // [e][r] used
+        const int cu = lane >> 3, ci = lane & 7;                 // lane = output u * 8 + repair i
+        const int pu = __shfl(my_piv, min(cu, e - 1), 64);      // every lane takes part in the shuffles
+        uint32_t v = 0;
+        for (int c = 0; c < e; c++) {
+            const int pc = __shfl(my_piv, c, 64);
+            const uint32_t tv = __shfl(xr, (pu * 8 + pc) & 63, 64);
+            uint32_t rr = rep;
+            for (int i2 = 0; i2 < pc && rr; i2++) rr &= rr - 1;
+            if (__ffs(rr) - 1 == ci) v = tv;  // repair ci is pivot row pc's
+        }
+        if (cu < e && ci < r) C2[cu * r + ci] = (uint8_t)v;
+        uint8_t *wb = a.win + w * a.wpitch;
+        for (int u2 = 0; u2 < e; u2++) {
+            uint4 *row = reinterpret_cast<uint4 *>(wb + (uint64_t)s_m[wave][u2] * a.stride);
+            for (uint32_t c16 = lane; c16 < a.stride / 16u; c16 += 64) row[c16] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    if (lane < r) a.outs1[w * (uint64_t)r + lane] = (w * (uint64_t)r + lane) * a.stride;
+    if (lane < e) a.outs[w * kMaxR + lane] = w * a.wpitch + (uint64_t)s_m[wave][lane] * a.stride;
+    if (lane == 0) {
+        CombJob J1;
+        J1.in_off = w * a.wpitch;
+        J1.coef_off = 0;
+        J1.out_list = w * (uint64_t)r;
+        J1.xor_off = kNoXor;
+        J1.nin = (uint32_t)n;
+        J1.nout = (uint32_t)r;
+        a.jobs1[w] = J1;
+        J.in_off = w * (uint64_t)r * a.stride;
+        J.coef_off = w * (uint64_t)(kMaxR * kMaxR) + 0;
+        J.out_list = w * kMaxR;
+        J.nin = (uint32_t)r;
+        J.nout = (uint32_t)e;
+        a.jobs[w] = J;
+        a.status[w] = FECGPU_STATUS_OK;
+    }
+    return;
+#endif
     // D[u][q] over the window's n rows, entry idx = u * n + q; T[P_u][P_c] =
     // xr of lane P_u * 8 + P_c, the repair of pivot row P_c = sel of row P_c
     uint8_t *D = a.coef + w * (uint64_t)(kMaxR * n);
@@ -184,7 +237,8 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
 // call against others that share the scratch.
 hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
                        uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
-                       uint64_t *outs, uint8_t *coef, hipStream_t s) {
+                       uint64_t *outs, uint8_t *coef, hipStream_t s, CombJob *jobs1, uint64_t *outs1,
+                       uint8_t *syn) {
     WideArgs a{};
     a.win = win;
     a.present = present;
@@ -199,6 +253,8 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
     a.jobs = jobs;
     a.outs = outs;
     a.coef = coef;
+    a.jobs1 = jobs1;
+    a.outs1 = outs1;
     if (decode)
         hipLaunchKernelGGL(wide_dec_plan_kernel, dim3((unsigned)((nwin + kBlock / 64 - 1) / (kBlock / 64))),
                            dim3(kBlock), 0, s, a);
@@ -207,6 +263,47 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
                            s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    constexpr uint32_t kBudget = 64u << 10;
+#if FECGPU_WIDE_2STAGE
+    if (decode) {
+        // (1) syndromes: every window's k + r rows times [P | I] (at P_dev + r k),
+        // tables shared by the workgroup's jobs, outputs the r syndrome rows
+        CombArgs c1{};
+        c1.jobs = jobs1;
+        c1.coef = P_dev + (size_t)r * k;
+        c1.outs = outs1;
+        c1.in_base = win;
+        c1.out_base = syn;
+        c1.njobs = nwin;
+        c1.ncol = ncol;
+        c1.stride = stride;
+        c1.nin_max = k + r;
+        c1.nout_max = r;
+        c1.job_lds = comb_job_lds(c1.nin_max, kMaxR);
+        c1.shared_coef = 1;
+        const uint32_t cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxWpb, nwin / 1024));
+        const uint32_t room =
+            std::min<uint32_t>(kBudget - comb_shared_lds(k + r, kMaxR), cap * comb_job_small_lds(kMaxR));
+        c1.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, comb_job_small_lds(kMaxR), room)));
+        e = launch_comb(c1, kMaxR, s);
+        if (e != hipSuccess) return e;
+        // (2) x_u = sum_c T[P_u][c] s_c over the window's r syndromes
+        CombArgs c2{};
+        c2.jobs = jobs;
+        c2.coef = coef;
+        c2.outs = outs;
+        c2.in_base = syn;
+        c2.out_base = win;
+        c2.njobs = nwin;
+        c2.ncol = ncol;
+        c2.stride = stride;
+        c2.nin_max = r;
+        c2.nout_max = kMaxR;
+        c2.job_lds = comb_job_lds(r, kMaxR);
+        c2.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c2.job_lds, kBudget / 2)));
+        return launch_comb(c2, kMaxR, s);
+    }
+#endif
     CombArgs c{};
     c.jobs = jobs;
     c.coef = decode ? coef : P_dev;
@@ -220,7 +317,6 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
     c.nin_max = decode ? k + r : k;
     c.nout_max = decode ? kMaxR : r;
     c.job_lds = comb_job_lds(c.nin_max, kMaxR);
-    constexpr uint32_t kBudget = 64u << 10;
 #if FECGPU_WIDE_SHARED
     if (!decode) {
         // every encode job multiplies by the same parity rows: one table block per

@@ -52,6 +52,19 @@ for s in "$@"; do
                       python bench.py --k 120 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 ;;
         profw248) step profw248 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profw248 -o run -- \
                       python bench.py --k 248 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 ;;
+        widetests) step widetests 300 python -u -m pytest tests/test_gpu_wide.py -q -x \
+                   --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+        abwide)  # k + r > 64: default build vs lib/libfecgpu_wide*.so, k 120 and 248, twice
+            for rep in 1 2; do
+                for kk in 120 248; do
+                    step abwide_base_${kk}_$rep 300 python bench.py --k $kk --r 8 --steps 10 --warmup 3 --cpu-seconds 0
+                    for v in quic-fec-eps_amd/lib/libfecgpu_wide*.so; do
+                        [ -e "$v" ] || continue
+                        n=$(basename $v .so); n=${n#libfecgpu_}
+                        FECGPU_LIB=$v step abwide_${n}_${kk}_$rep 300 python bench.py --k $kk --r 8 --steps 10 --warmup 3 --cpu-seconds 0
+                    done
+                done
+            done ;;
         bench5) step bench5 600 python bench.py --config 5 --steps 10 --warmup 2 --cpu-seconds 0 ;;
         bench6) step bench6 600 python bench.py --config 6 --steps 10 --warmup 2 --cpu-seconds 0 ;;
         dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
