@@ -30,11 +30,11 @@ def kind(name, config):
 
 def per_kernel(path, counter, config):
     out = collections.defaultdict(list)
-    calls = 0  # config 7: decode calls (one header kernel each); the chain's bytes are summed per call
+    calls = 0  # config 7: decode calls (one plan kernel each, or header kernel unfused); the chain summed per call
     for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
         if r["Counter_Name"] != counter:
             continue
-        if config == 7 and "sw_dec_hdr_kernel" in r["Kernel_Name"]:
+        if config == 7 and ("sw_dec_plan_kernel" in r["Kernel_Name"] or "sw_dec_hdr_kernel" in r["Kernel_Name"]):
             calls += 1
         kd = kind(r["Kernel_Name"], config)
         if kd:
