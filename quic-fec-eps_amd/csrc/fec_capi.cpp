@@ -456,6 +456,43 @@ void fecgpu_host_free(void *p) {
 
 namespace {
 
+// Plane picks of the runtime-mask bit-sliced encode (fec_kernels.hip rbs::,
+// rbs4::) for parity rows P[r][k]: for source j, output i and output plane p,
+// lo = the input planes q < 4 and hi = the planes q >= 4 (as bits q, q - 4)
+// for which bit p of P[i][j] * 2^q is set; stored as the kernel's index format
+// (kRbsDw4 dwords per 4 planes).  out: k * r * 2 * kRbsDw4 dwords.
+void rbs_masks(const uint8_t *P, int k, int r, uint32_t *out) {
+    static constexpr GfTables g = make_gf_tables();
+    std::fill(out, out + (size_t)k * r * 2 * kRbsDw4, 0u);
+    for (int j = 0; j < k; j++)
+        for (int i = 0; i < r; i++) {
+            const uint8_t c = P[(size_t)i * k + j];
+            uint32_t *row = &out[((size_t)j * r + i) * 2 * kRbsDw4];  // this repair's 8 planes
+            for (int p = 0; p < 8; p++) {
+                uint32_t lo = 0, hi = 0;
+                for (int q = 0; q < 8; q++) {
+                    const uint8_t col = c ? g.exp[g.log[c] + q] : 0;
+                    if ((col >> p) & 1) (q < 4 ? lo : hi) |= 1u << (q & 3);
+                }
+                if (kRbsCols == 4) {  // four-column units index register pairs: 2 x index
+                    if (kRbsDw4 == 8) {
+                        row[2 * p] = lo * 2;
+                        row[2 * p + 1] = hi * 2;
+                    } else if (kRbsDw4 == 4) {
+                        row[p] = lo * 2 | (hi * 2) << 16;
+                    } else {  // bytes lo, hi of plane p in dword p / 2
+                        row[p / 2] |= (lo * 2 | (hi * 2) << 8) << (16 * (p & 1));
+                    }
+                } else if (kRbsDw4 == 8) {
+                    row[2 * p] = lo;
+                    row[2 * p + 1] = hi;
+                } else {
+                    row[p] = lo | hi << 8;
+                }
+            }
+        }
+}
+
 // Encode tables for the code's parity rows on the current device, built once
 // per ctx (and, for non-Cauchy matrices, the raw rows for the decode plan).
 ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out) {
@@ -487,38 +524,8 @@ ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out)
     HIP_TRY(hipMemcpy(t.ab, ab.data(), ab.size() * sizeof(uint4), hipMemcpyHostToDevice), "hipMemcpy");
     HIP_TRY(hipMemcpy(t.c, cc.data(), cc.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy");
     {
-        // (j, i, p): lo = the planes q < 4, hi = the planes q >= 4 (as bits
-        // q, q - 4) for which bit p of P[i][j] * 2^q is set; stored lo | hi << 8,
-        // or as two dwords lo, hi (fec_kernels.hip rbs::)
-        static constexpr GfTables g = make_gf_tables();
         std::vector<uint32_t> m((size_t)k * r * 2 * kRbsDw4, 0);
-        for (int j = 0; j < k; j++)
-            for (int i = 0; i < r; i++) {
-                const uint8_t c = P[(size_t)i * k + j];
-                uint32_t *row = &m[((size_t)j * r + i) * 2 * kRbsDw4];  // this repair's 8 planes
-                for (int p = 0; p < 8; p++) {
-                    uint32_t lo = 0, hi = 0;
-                    for (int q = 0; q < 8; q++) {
-                        const uint8_t col = c ? g.exp[g.log[c] + q] : 0;
-                        if ((col >> p) & 1) (q < 4 ? lo : hi) |= 1u << (q & 3);
-                    }
-                    if (kRbsCols == 4) {  // four-column units index register pairs: 2 x index
-                        if (kRbsDw4 == 8) {
-                            row[2 * p] = lo * 2;
-                            row[2 * p + 1] = hi * 2;
-                        } else if (kRbsDw4 == 4) {
-                            row[p] = lo * 2 | (hi * 2) << 16;
-                        } else {  // bytes lo, hi of plane p in dword p / 2
-                            row[p / 2] |= (lo * 2 | (hi * 2) << 8) << (16 * (p & 1));
-                        }
-                    } else if (kRbsDw4 == 8) {
-                        row[2 * p] = lo;
-                        row[2 * p + 1] = hi;
-                    } else {
-                        row[p] = lo | hi << 8;
-                    }
-                }
-            }
+        rbs_masks(P.data(), k, r, m.data());
         HIP_TRY(hipMalloc(&t.bs, m.size() * sizeof(uint32_t)), "hipMalloc");
         HIP_TRY(hipMemcpy(t.bs, m.data(), m.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy");
     }
@@ -675,6 +682,14 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
             for (int i = 0; i < r; i++)
                 for (int q = 0; q < n; q++)
                     rows[nP + (size_t)i * n + q] = q < k ? rows[(size_t)i * k + q] : (uint8_t)(q - k == i);
+            // then the bit-sliced plane picks of P and of [P | I] (wide_masks)
+            const size_t o_m = (rows.size() + 255) & ~size_t(255);
+            std::vector<uint32_t> mP((size_t)k * r * 2 * kRbsDw4), mPI((size_t)n * r * 2 * kRbsDw4);
+            rbs_masks(rows.data(), k, r, mP.data());
+            rbs_masks(rows.data() + nP, n, r, mPI.data());
+            rows.resize(o_m + (mP.size() + mPI.size()) * 4);
+            std::memcpy(rows.data() + o_m, mP.data(), mP.size() * 4);
+            std::memcpy(rows.data() + o_m + mP.size() * 4, mPI.data(), mPI.size() * 4);
             void *d = nullptr;
             HIP_TRY(hipMalloc(&d, rows.size()), "hipMalloc wide parity rows");
             HIP_TRY(hipMemcpy(d, rows.data(), rows.size(), hipMemcpyHostToDevice), "H2D wide parity rows");
@@ -697,9 +712,16 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
     uint8_t *b = static_cast<uint8_t *>(scratch);
     // per-window lengths: every window's columns up to the stride
     const uint32_t ncol = sym_len ? stride / 16u : (sym_len_all + 15u) / 16u;
+    // plane picks (run_wide's row block: P, [P | I], then the picks of each)
+    const uint32_t *mP = nullptr, *mPI = nullptr;
+    if (FECGPU_WIDE_RBS && ctx->bitslice && r >= 4) {
+        const size_t o_m = ((size_t)r * k + (size_t)r * n + 255) & ~size_t(255);
+        mP = reinterpret_cast<const uint32_t *>(P + o_m);
+        mPI = mP + (size_t)k * r * 2 * kRbsDw4;
+    }
     HIP_TRY(launch_wide(win, present, status, P, nwin, stride, ncol, k, r, decode, reinterpret_cast<CombJob *>(b),
                         reinterpret_cast<uint64_t *>(b + o_out), b + o_coef, s, reinterpret_cast<CombJob *>(b + o_j1),
-                        reinterpret_cast<uint64_t *>(b + o_o1), b + o_syn),
+                        reinterpret_cast<uint64_t *>(b + o_o1), b + o_syn, mP, two ? mPI : nullptr),
             "wide batch launch");
     rc = ctx_sw_end(ctx, s);
     if (rc) return rc;

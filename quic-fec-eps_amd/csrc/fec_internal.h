@@ -241,12 +241,19 @@ __host__ __device__ inline uint32_t comb_job_small_lds(int R) {
     return (16u * R + 4u * rt + 8u * (R + 1) + 15u) & ~15u;
 }
 hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
+// the runtime-mask bit-sliced encode over uniform windows of any k (fec_kernels.hip)
+hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t stride, uint64_t wpitch, int k,
+                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s);
+#ifndef FECGPU_WIDE_RBS
+#define FECGPU_WIDE_RBS 1  // wide encode and the two-stage decode's syndromes by the runtime-mask
+                           // bit-sliced kernel (r >= 4; plane picks by scalar loads, no LDS tables)
+#endif
 // GF block codes with k + r > 64 (fec_wide.hip): a plan / job kernel, then the
 // combine kernel over a job per window
 hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
                        uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
                        uint64_t *outs, uint8_t *coef, hipStream_t s, CombJob *jobs1, uint64_t *outs1,
-                       uint8_t *syn);
+                       uint8_t *syn, const uint32_t *masks_P = nullptr, const uint32_t *masks_PI = nullptr);
 #ifndef FECGPU_WIDE_2STAGE
 // wide decode in two combine launches (fec_wide.hip): syndromes of every
 // repair with one coefficient block [P | I] for all windows (the missing

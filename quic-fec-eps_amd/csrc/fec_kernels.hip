@@ -2686,6 +2686,33 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
     else DISPATCH_R(a.r, launch(gf_encode_kernel<RR, false>, a, p, s, false))
 }
 
+// The runtime-mask bit-sliced encode over uniform windows of any k (fec_wide.hip:
+// the wide encode, and the two-stage wide decode's syndromes): window w at
+// win + w * wpitch, its k input rows first, output i at
+// (input row k + i's address) + out_delta + w * out_wdelta.  Flat unit space.
+hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t stride, uint64_t wpitch, int k,
+                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s) {
+    if (nwin == 0) return hipSuccess;
+    if (r < 4 || r > 8) return hipErrorInvalidValue;
+    BatchArgs a{};
+    a.win = win;
+    a.nwin = nwin;
+    a.ncol = ncol;
+    a.stride = stride;
+    a.wpitch = wpitch;
+    a.k = k;
+    a.r = r;
+    a.enc_bs = masks;
+    a.out_delta = out_delta;
+    a.out_wdelta = out_wdelta;
+    a.chk.lo[0] = 0;  // FECGPU_CHECK builds: rows addressed by the caller's layout, unchecked
+    a.chk.n[0] = ~0ull;
+    LaunchPlan p{};
+    p.flat = true;
+    p.rbitslice = true;
+    return launch_encode(FECGPU_SCHEME_GF256, a, p, s);
+}
+
 hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     if (scheme == 0) {

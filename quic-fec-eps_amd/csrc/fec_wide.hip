@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
 hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
                        uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
                        uint64_t *outs, uint8_t *coef, hipStream_t s, CombJob *jobs1, uint64_t *outs1,
-                       uint8_t *syn) {
+                       uint8_t *syn, const uint32_t *masks_P, const uint32_t *masks_PI) {
     WideArgs a{};
     a.win = win;
     a.present = present;
@@ -255,6 +255,10 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
     a.coef = coef;
     a.jobs1 = jobs1;
     a.outs1 = outs1;
+    const int n = k + r;
+    if (!decode && masks_P) {  // every window's k sources times P by plane picks
+        return launch_rbs_rows(win, nwin, ncol, stride, a.wpitch, k, r, masks_P, 0, 0, s);
+    }
     if (decode)
         hipLaunchKernelGGL(wide_dec_plan_kernel, dim3((unsigned)((nwin + kBlock / 64 - 1) / (kBlock / 64))),
                            dim3(kBlock), 0, s, a);
@@ -267,7 +271,15 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
 #if FECGPU_WIDE_2STAGE
     if (decode) {
         // (1) syndromes: every window's k + r rows times [P | I] (at P_dev + r k),
-        // tables shared by the workgroup's jobs, outputs the r syndrome rows
+        // outputs the r syndrome rows: by plane picks (output i of window w at
+        // syn + (w r + i) stride, i.e. its input row n + i's address plus
+        // syn - win - n stride + w (r stride - wpitch)), or combine jobs with the
+        // tables shared by the workgroup's jobs
+        if (masks_PI) {
+            e = launch_rbs_rows(win, nwin, ncol, stride, a.wpitch, n, r, masks_PI,
+                                (uint64_t)syn - (uint64_t)win - (uint64_t)n * stride,
+                                (uint64_t)r * stride - a.wpitch, s);
+        } else {
         CombArgs c1{};
         c1.jobs = jobs1;
         c1.coef = P_dev + (size_t)r * k;
@@ -286,6 +298,7 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
             std::min<uint32_t>(kBudget - comb_shared_lds(k + r, kMaxR), cap * comb_job_small_lds(kMaxR));
         c1.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, comb_job_small_lds(kMaxR), room)));
         e = launch_comb(c1, kMaxR, s);
+        }
         if (e != hipSuccess) return e;
         // (2) x_u = sum_c T[P_u][c] s_c over the window's r syndromes
         CombArgs c2{};
