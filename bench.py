@@ -71,7 +71,9 @@ def parse():
                     help="tuning: bit-sliced encode on per-window lengths, 256-unit passes per window group")
     ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
     ap.add_argument("--bpc", type=int, default=0, help="tuning: persistent workgroups per CU")
-    ap.add_argument("--sw-stream", type=int, default=-1, choices=[-1, 0, 1, 2],
+    ap.add_argument("--sw-long-min", type=int, default=0,
+                    help="tuning (config 7): unknowns from which a linked system takes the banded long path")
+    ap.add_argument("--sw-stream", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4, 5, 6],
                     help="sliding-window encode: 0 combine jobs, 1/2 streaming (dwords per lane); "
                          "-1 the library default")
     ap.add_argument("--sw-group", type=int, default=0, choices=[0, 1, 2, 4, 8],
@@ -285,6 +287,8 @@ def make_ctx(args):
         ctx.set_tuning("sw_group", args.sw_group)
     if args.sw_stream >= 0:
         ctx.set_tuning("sw_stream", args.sw_stream)
+    if args.sw_long_min:
+        ctx.set_tuning("sw_long_min", args.sw_long_min)
     if args.host_direct >= 0:
         ctx.set_tuning("host_direct", args.host_direct)
     if args.host_chunk_mb:

@@ -114,6 +114,14 @@ for s in "$@"; do
         prof7) prof prof7 7 ;;
         trace7) FECGPU_LIB=quic-fec-eps_amd/lib/libfecgpu_trace.so step trace7 300 python bench.py --config 7 \
                     --steps 3 --warmup 1 --cpu-seconds 0 --no-verify --extra-configs 0 ;;
+        prof7l10) prof prof7l10 7 --sw-loss 0.1 ;;
+        ablong)  # cfg7 at 10 % loss: sw_long_min values, twice
+            for rep in 1 2; do
+                for lm in 65 33 17 9; do
+                    step ablong_${lm}_$rep 300 python bench.py --config 7 --steps 20 --warmup 5 --cpu-seconds 0 \
+                        --no-verify --sw-loss 0.1 --sw-long-min $lm --extra-configs 0
+                done
+            done ;;
         prof7v)  # cfg7 rocprofv3 of every lib/libfecgpu_*.so variant (no check build)
             for v in quic-fec-eps_amd/lib/libfecgpu_*.so; do
                 n=$(basename $v .so); n=${n#libfecgpu_}
