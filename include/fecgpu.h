@@ -142,8 +142,11 @@ void    fecgpu_host_free(void *p);
  * encode of a code with a compiled bit-sliced kernel — Cauchy or Vandermonde
  * rows, r = 8, k in {16, 24, 32} — uses it, and of any other code with r >= 5
  * the runtime-mask bit-sliced kernel; 0: the table multiply for every code);
- * "sw_group" (sliding-window encode: consecutive repairs per combine job, each
- * source loaded once per group; 1, 2, 4 or 8, default 4); "sw_long_min"
+ * "sw_group" (sliding-window encode by combine jobs: consecutive repairs per
+ * job, each source loaded once per group; 1, 2, 4 or 8, default 4);
+ * "sw_stream" (sliding-window encode: 0 combine jobs, 1..5 the streaming
+ * kernel with that many dwords of a symbol per lane, 6 chosen per symbol
+ * size; default 1); "sw_long_min"
  * (sliding-window decode: linked systems of at least this many lost sources
  * take the banded long-system path, default 65 — systems of <= 64 lost
  * sources and <= 96 repairs are solved by one wave each); "sw_log_entries"
