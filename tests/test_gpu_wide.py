@@ -92,7 +92,9 @@ def _erasures(nwin, k, r, rng, max_e=None):
 @pytest.mark.parametrize("k,r,matrix,L", [(60, 8, "cauchy", 1200), (100, 4, "cauchy", 40),
                                           (200, 8, "cauchy", 1200), (248, 8, "cauchy", 300),
                                           (90, 6, "vandermonde", 1200), (150, 8, "rlc", 1200),
-                                          (250, 6, "rlc", 64)])
+                                          (250, 6, "rlc", 64),
+                                          # r < 4: the combine-job passes (the bit-sliced kernel takes r >= 4)
+                                          (70, 2, "cauchy", 1200), (130, 3, "rlc", 500), (65, 1, "cauchy", 100)])
 def test_wide_encode_decode_vs_oracle(ctx, k, r, matrix, L):
     nwin = 12
     rng = np.random.default_rng(k * 31 + r)
@@ -102,6 +104,17 @@ def test_wide_encode_decode_vs_oracle(ctx, k, r, matrix, L):
     bits[1, :r] = False       # exactly r sources, every repair present
     gst = _run(ctx, k, r, matrix, L, nwin, bits)
     assert gst[0] == 0 and gst[1] == 0
+
+
+def test_wide_many_windows(ctx):
+    """600 windows of k 120 r 8 (the bench's shape): the bit-sliced passes'
+    flat unit space over many workgroups, and the two-stage decode's syndrome
+    scratch past one workgroup's windows."""
+    k, r, nwin = 120, 8, 600
+    rng = np.random.default_rng(17)
+    bits = _erasures(nwin, k, r, rng, max_e=r)
+    gst = _run(ctx, k, r, "cauchy", 1200, nwin, bits)
+    assert (gst == 0).sum() > nwin // 2
 
 
 def test_wide_every_erasure_count(ctx):
