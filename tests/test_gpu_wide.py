@@ -83,7 +83,7 @@ def _erasures(nwin, k, r, rng, max_e=None):
     for w in range(nwin):
         e = int(rng.integers(0, (max_e if max_e is not None else r + 1) + 1))
         bits[w, rng.choice(k, e, replace=False)] = False
-        lr = int(rng.integers(0, 3))
+        lr = int(rng.integers(0, min(3, r + 1)))
         if lr:
             bits[w, k + rng.choice(r, lr, replace=False)] = False
     return bits
