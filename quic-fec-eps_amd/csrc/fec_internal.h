@@ -366,6 +366,10 @@ constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
 #define FECGPU_SWD_ONEPASS 1  // fused plan: the system pass takes systems of up to 64 unknowns /
                               // 96 equations itself (mid-size LDS per wave), no separate mid pass
 #endif
+#ifndef FECGPU_SWD_MIDLOCK
+#define FECGPU_SWD_MIDLOCK 1  // one-pass system kernel: 3 KB of LDS per wave for the common tiny
+                              // systems, one mid-size region per block taken under an LDS lock
+#endif
 #ifndef FECGPU_SWD_FUSED
 #define FECGPU_SWD_FUSED 1  // the decode plan as one look-back launch (sw_dec_plan_kernel) instead of
                             // a memset and five passes

@@ -682,8 +682,11 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
 // The system lost[x .. x + e) with candidate repairs [t_lo, t_hi): solved here
 // when its equations fit ME / MP (and the range of syndrome rows kSwSolveIn),
 // else queued for the next pass (mid, then long).
-template <int ME, int MP, bool MID>
-__device__ void sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, uint32_t x, uint32_t e,
+// LOCAL (FECGPU_SWD_MIDLOCK): a system too large for ME / MP but within the
+// mid size is not queued; the call returns true and the caller solves it in
+// its workgroup's shared mid region.
+template <int ME, int MP, bool MID, bool LOCAL = false>
+__device__ bool sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, uint32_t x, uint32_t e,
                         uint64_t t_lo, uint64_t t_hi, int lane, uint32_t &rec, uint32_t &maxin) {
     bool fits = (int)e <= ME && (int)e < a.long_min;
     uint32_t p = 0;
@@ -706,6 +709,7 @@ __device__ void sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, u
         if (fits && p && S.eq[p - 1] - S.eq[0] + 1 > (uint32_t)kSwSolveIn) fits = false;
     }
     if (!fits) {
+        if (LOCAL && (int)e <= kSwSmallE && (int)e < a.long_min) return true;
         if (lane == 0) {
             const bool to_mid = !MID && (int)e <= kSwSmallE && (int)e < a.long_min;
             const uint32_t k = atomicAdd(to_mid ? &a.ctr->nmid : &a.ctr->nlong, 1u);
@@ -720,13 +724,14 @@ __device__ void sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, u
                 dec_err(a, kSwErrCapacity);
             }
         }
-        return;
+        return false;
     }
-    if (p == 0) return;  // no received repair holds it: stays lost
+    if (p == 0) return false;  // no received repair holds it: stays lost
     uint32_t nin = 0;
     const int nd = small_solve<ME, MP>(a, g, x, (int)e, (int)p, S, lane, &nin);
     rec += (uint32_t)nd;
     if (nd) maxin = max(maxin, nin);
+    return false;
 }
 
 // The block's recovered count and widest solve into the call's counters: one
@@ -1415,7 +1420,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
 
 // A wave per lost source; the waves at a system start find its extent and
 // solve it (tiny) or queue it (mid, long).
-#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS
+#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS && FECGPU_SWD_MIDLOCK
+constexpr int kSysE = kSwTinyE, kSysP = kSwTinyP;  // per wave; one mid region per block, taken by a lock
+#elif FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS
 constexpr int kSysE = kSwSmallE, kSysP = kSwSmallP;  // the system pass's LDS per wave
 #else
 constexpr int kSysE = kSwTinyE, kSysP = kSwTinyP;
@@ -1423,6 +1430,11 @@ constexpr int kSysE = kSwTinyE, kSysP = kSwTinyP;
 __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     __shared__ GfLds g;
     __shared__ SysLds<kSysE, kSysP> s_sys[kBlock / 64];
+#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS && FECGPU_SWD_MIDLOCK
+    __shared__ SysLds<kSwSmallE, kSwSmallP> s_mid;
+    __shared__ int s_lock;
+    if (threadIdx.x == 0) s_lock = 0;
+#endif
     gf_load(g);
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1457,8 +1469,22 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
         // candidate repairs: fss in [lx - wmax + 1, last]
         const uint64_t t_lo = a.rcnt[lx >= wmax ? lx - wmax + 1 : 0], t_hi = a.rcnt[(uint64_t)last + 1];
         // one pass (FECGPU_SWD_ONEPASS): up to the mid size here, longer ones to the long pass
+#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS && FECGPU_SWD_MIDLOCK
+        // tiny systems in the wave's own 3 KB; a mid-size one takes the block's
+        // shared region (lane 0 spins on an LDS lock, the wave waits with it)
+        if (sys_one<kSysE, kSysP, false, true>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin)) {
+            if (lane == 0)
+                while (atomicCAS(&s_lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
+            SWD_WAVE_SYNC();
+            sys_one<kSwSmallE, kSwSmallP, true>(a, g, s_mid, (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin);
+            SWD_WAVE_SYNC();
+            __threadfence_block();  // the region's LDS traffic done before the next holder
+            if (lane == 0) atomicExch(&s_lock, 0);
+        }
+#else
         sys_one<kSysE, kSysP, FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi,
                                                                       lane, rec, maxin);
+#endif
     }
     block_counts(a, rec, maxin, lane, wave);
 }
@@ -2079,8 +2105,10 @@ hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
         // a wave per lost source at most; persistent beyond what fits the chip
         const uint64_t want = (a.nsrc + kBlock / 64 - 1) / (kBlock / 64);
 #if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS
-        // mid-size LDS (64 KB per block): two blocks per CU
-        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 2));
+        // mid-size LDS per wave (64 KB per block): two blocks per CU; with the
+        // shared mid region (~30 KB per block) five
+        const unsigned grid = (unsigned)std::max<uint64_t>(
+            1, std::min<uint64_t>(want, (uint64_t)cu_count() * (FECGPU_SWD_MIDLOCK ? 5 : 2)));
         hipLaunchKernelGGL(sw_dec_sys_kernel, dim3(grid), dim3(kBlock), 0, s, a);
 #else
         const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 6));
