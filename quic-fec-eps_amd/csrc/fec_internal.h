@@ -367,8 +367,9 @@ constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
                               // 96 equations itself (mid-size LDS per wave), no separate mid pass
 #endif
 #ifndef FECGPU_SWD_MIDLOCK
-#define FECGPU_SWD_MIDLOCK 1  // one-pass system kernel: 3 KB of LDS per wave for the common tiny
-                              // systems, one mid-size region per block taken under an LDS lock
+#define FECGPU_SWD_MIDLOCK 2  // one-pass system kernel: 3 KB of LDS per wave for the common tiny
+                              // systems, this many mid-size regions per block taken under LDS
+                              // locks (0: a mid-size region per wave)
 #endif
 #ifndef FECGPU_SWD_FUSED
 #define FECGPU_SWD_FUSED 1  // the decode plan as one look-back launch (sw_dec_plan_kernel) instead of

@@ -1421,7 +1421,8 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
 // A wave per lost source; the waves at a system start find its extent and
 // solve it (tiny) or queue it (mid, long).
 #if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS && FECGPU_SWD_MIDLOCK
-constexpr int kSysE = kSwTinyE, kSysP = kSwTinyP;  // per wave; one mid region per block, taken by a lock
+constexpr int kSysE = kSwTinyE, kSysP = kSwTinyP;  // per wave; mid regions per block, taken by a lock
+constexpr int kSysMid = FECGPU_SWD_MIDLOCK;
 #elif FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS
 constexpr int kSysE = kSwSmallE, kSysP = kSwSmallP;  // the system pass's LDS per wave
 #else
@@ -1431,9 +1432,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     __shared__ GfLds g;
     __shared__ SysLds<kSysE, kSysP> s_sys[kBlock / 64];
 #if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS && FECGPU_SWD_MIDLOCK
-    __shared__ SysLds<kSwSmallE, kSwSmallP> s_mid;
-    __shared__ int s_lock;
-    if (threadIdx.x == 0) s_lock = 0;
+    __shared__ SysLds<kSwSmallE, kSwSmallP> s_mid[kSysMid];
+    __shared__ int s_lock[kSysMid];
+    if (threadIdx.x < kSysMid) s_lock[threadIdx.x] = 0;
 #endif
     gf_load(g);
     __syncthreads();
@@ -1473,13 +1474,14 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
         // tiny systems in the wave's own 3 KB; a mid-size one takes the block's
         // shared region (lane 0 spins on an LDS lock, the wave waits with it)
         if (sys_one<kSysE, kSysP, false, true>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin)) {
+            const int m = wave % kSysMid;  // waves m, m + kSysMid, ... share region m
             if (lane == 0)
-                while (atomicCAS(&s_lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
+                while (atomicCAS(&s_lock[m], 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
             SWD_WAVE_SYNC();
-            sys_one<kSwSmallE, kSwSmallP, true>(a, g, s_mid, (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin);
+            sys_one<kSwSmallE, kSwSmallP, true>(a, g, s_mid[m], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin);
             SWD_WAVE_SYNC();
             __threadfence_block();  // the region's LDS traffic done before the next holder
-            if (lane == 0) atomicExch(&s_lock, 0);
+            if (lane == 0) atomicExch(&s_lock[m], 0);
         }
 #else
         sys_one<kSysE, kSysP, FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi,
@@ -2108,7 +2110,9 @@ hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
         // mid-size LDS per wave (64 KB per block): two blocks per CU; with the
         // shared mid region (~30 KB per block) five
         const unsigned grid = (unsigned)std::max<uint64_t>(
-            1, std::min<uint64_t>(want, (uint64_t)cu_count() * (FECGPU_SWD_MIDLOCK ? 5 : 2)));
+            1, std::min<uint64_t>(want, (uint64_t)cu_count() * (FECGPU_SWD_MIDLOCK == 1   ? 5
+                                                                : FECGPU_SWD_MIDLOCK == 2 ? 3
+                                                                                          : 2)));
         hipLaunchKernelGGL(sw_dec_sys_kernel, dim3(grid), dim3(kBlock), 0, s, a);
 #else
         const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 6));
