@@ -366,6 +366,11 @@ constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
 #define FECGPU_SWD_ONEPASS 1  // fused plan: the system pass takes systems of up to 64 unknowns /
                               // 96 equations itself (mid-size LDS per wave), no separate mid pass
 #endif
+#ifndef FECGPU_SWD_SOLVE_OUT
+#define FECGPU_SWD_SOLVE_OUT 8  // recovered sources per solve job (8, 4 or 2): the solve pass's
+                                // critical path is its widest system's job, nin rows x outputs per lane
+#endif
+constexpr int kSwSolveOut = FECGPU_SWD_SOLVE_OUT;
 #ifndef FECGPU_SWD_MIDLOCK
 #define FECGPU_SWD_MIDLOCK 2  // one-pass system kernel: 3 KB of LDS per wave for the common tiny
                               // systems, this many mid-size regions per block taken under LDS

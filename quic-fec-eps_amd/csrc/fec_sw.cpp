@@ -45,7 +45,7 @@ namespace {
 #endif
 constexpr uint32_t kCombBudget = FECGPU_COMB_BUDGET_KB << 10;
 constexpr uint32_t kCombBudgetWide = FECGPU_COMB_BUDGET_WIDE_KB << 10;
-constexpr int kSwSolveOut = 8;               // recovered sources per solve job
+// kSwSolveOut (fec_internal.h): recovered sources per solve job
 constexpr int kSwSolveIn = 128;              // syndrome rows a small system's solve reads (fec_swdec.hip)
 // LDS of a solve workgroup: its jobs' 8-output tables over the widest range of
 // syndrome rows (device-sized); more room than the encode's budget keeps
@@ -399,8 +399,8 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     va.out_base = src;
     va.xor_base = nullptr;
 #if FECGPU_SWD_FUSED && FECGPU_SWD_SOLVE_LIST
-    va.extra = &a.ctr->nsolout;  // the compact list: a job per 8 outputs
-    va.extra_shift = 3;
+    va.extra = &a.ctr->nsolout;  // the compact list: a job per kSwSolveOut outputs
+    va.extra_shift = kSwSolveOut == 8 ? 3 : kSwSolveOut == 4 ? 2 : 1;
     va.extra_max = nsrc + 8;
 #else
     va.extra = &a.ctr->nlost;  // a slot per unknown, filled by its small system

@@ -646,9 +646,9 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     const uint64_t c0 = (uint64_t)t_first * kSwSmallE;
 #if FECGPU_SWD_FUSED && FECGPU_SWD_SOLVE_LIST
     uint32_t ob = 0;
-    if (lane == 0) ob = atomicAdd(&a.ctr->nsolout, (uint32_t)(ndet + 7) & ~7u);
+    if (lane == 0) ob = atomicAdd(&a.ctr->nsolout, (uint32_t)(ndet + kSwSolveOut - 1) / kSwSolveOut * kSwSolveOut);
     ob = __shfl(ob, 0);
-    const uint64_t o0 = ob, j0 = ob >> 3;
+    const uint64_t o0 = ob, j0 = ob / kSwSolveOut;
 #else
     const uint64_t o0 = x, j0 = x;
 #endif
@@ -664,15 +664,15 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         a.sol_outs[o0 + d] = (uint64_t)U[lane] * a.stride;
         a.stat[U[lane]] = FECGPU_STATUS_OK;
     }
-    const int nj = (ndet + 7) / 8;
+    const int nj = (ndet + kSwSolveOut - 1) / kSwSolveOut;
     if (lane < nj) {
         CombJob J;
         J.in_off = (uint64_t)t_first * a.stride;
-        J.coef_off = c0 + (uint64_t)lane * 8 * nin;
-        J.out_list = o0 + (uint64_t)lane * 8;
+        J.coef_off = c0 + (uint64_t)lane * kSwSolveOut * nin;
+        J.out_list = o0 + (uint64_t)lane * kSwSolveOut;
         J.xor_off = kNoXor;
         J.nin = nin;
-        J.nout = (uint32_t)min(8, ndet - 8 * lane);
+        J.nout = (uint32_t)min(kSwSolveOut, ndet - kSwSolveOut * lane);
         a.sol_jobs[j0 + lane] = J;
     }
     *nin_out = nin;
