@@ -367,8 +367,9 @@ constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
                               // 96 equations itself (mid-size LDS per wave), no separate mid pass
 #endif
 #ifndef FECGPU_SWD_SOLVE_OUT
-#define FECGPU_SWD_SOLVE_OUT 8  // recovered sources per solve job (8, 4 or 2): the solve pass's
+#define FECGPU_SWD_SOLVE_OUT 4  // recovered sources per solve job (8, 4 or 2): the solve pass's
                                 // critical path is its widest system's job, nin rows x outputs per lane
+                                // (cfg7, r04: 4 gave 0.198 vs 8 0.206 ms at 2 % loss, 1.70 vs 1.76 at 10 %)
 #endif
 constexpr int kSwSolveOut = FECGPU_SWD_SOLVE_OUT;
 #ifndef FECGPU_SWD_MIDLOCK
