@@ -223,7 +223,10 @@ struct CombArgs {
     // output pointers), so more jobs fit a workgroup
     int shared_coef;
 };
-constexpr uint32_t kCombRun = 16;                                    // sparse launches: slots per run
+#ifndef FECGPU_COMB_RUN
+#define FECGPU_COMB_RUN 16
+#endif
+constexpr uint32_t kCombRun = FECGPU_COMB_RUN;                       // sparse launches: slots per run
 constexpr uint32_t kCombListLds = 256 * (uint32_t)sizeof(CombJob);   // sparse launches: one round's jobs
 // LDS bytes per job of comb_kernel<R> at nin_max inputs
 __host__ __device__ inline uint32_t comb_job_lds(int nin_max, int R) {
