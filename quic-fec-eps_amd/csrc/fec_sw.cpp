@@ -57,7 +57,7 @@ constexpr uint32_t kSolveBudget = FECGPU_SOLVE_BUDGET_KB << 10;
 // LDS for one streaming-encode workgroup's multiply tables (segment of up to
 // kSwSeg repairs x max_window coefficients x 21 B): 43 KB for 64 repairs at W 32
 #ifndef FECGPU_STREAM_BUDGET_KB
-#define FECGPU_STREAM_BUDGET_KB 44
+#define FECGPU_STREAM_BUDGET_KB 32  // cfg7 A/B (r04): 28 / 32 / 36 KB 0.200-0.202 vs 44 KB 0.216 ms (more workgroups per CU)
 #endif
 constexpr uint32_t kStreamBudget = FECGPU_STREAM_BUDGET_KB << 10;
 constexpr uint64_t kSwStreamSources = 1ull << 32;  // the streaming encode's source positions are 32-bit
