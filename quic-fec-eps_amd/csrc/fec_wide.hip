@@ -29,6 +29,9 @@ __constant__ GfTables c_gfw = make_gf_tables();
 // (k + r + 1) x 161 B of tables per window, so 3 (k 120) or 1 (k 248) windows
 // per workgroup, 75 of its 256 lanes busy per 1200-B window; the two-stage one
 // builds [P | I]'s tables once per workgroup and its stage-2 jobs are 8 x 8.
+#ifndef FECGPU_WIDE_S2_KB
+#define FECGPU_WIDE_S2_KB 32  // two-stage decode, stage 2: LDS budget of a workgroup's window jobs
+#endif
 #ifndef FECGPU_WIDE_SHARED
 #define FECGPU_WIDE_SHARED 1  // wide encode: parity-row tables shared by a workgroup's jobs
 #endif
@@ -313,7 +316,7 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
         c2.nin_max = r;
         c2.nout_max = kMaxR;
         c2.job_lds = comb_job_lds(r, kMaxR);
-        c2.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c2.job_lds, kBudget / 2)));
+        c2.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c2.job_lds, FECGPU_WIDE_S2_KB << 10)));
         return launch_comb(c2, kMaxR, s);
     }
 #endif
