@@ -30,7 +30,7 @@ __constant__ GfTables c_gfw = make_gf_tables();
 // per workgroup, 75 of its 256 lanes busy per 1200-B window; the two-stage one
 // builds [P | I]'s tables once per workgroup and its stage-2 jobs are 8 x 8.
 #ifndef FECGPU_WIDE_S2_KB
-#define FECGPU_WIDE_S2_KB 32  // two-stage decode, stage 2: LDS budget of a workgroup's window jobs
+#define FECGPU_WIDE_S2_KB 16  // two-stage decode, stage 2: LDS budget of a workgroup's window jobs (k120: 16 KB 1.656 vs 32 KB 1.683 ms)
 #endif
 #ifndef FECGPU_WIDE_SHARED
 #define FECGPU_WIDE_SHARED 1  // wide encode: parity-row tables shared by a workgroup's jobs
