@@ -18,13 +18,14 @@ import statistics
 
 def kind(name, config):
     """encode / decode / None for a kernel name (config 7, sliding window: the
-    encode is sw_stream_kernel, or comb_kernel<4> with sw_stream 0)."""
+    encode is sw_stream_kernel; every combine launch belongs to the decode —
+    syndromes comb_kernel<1>, solves comb_kernel<4>)."""
     if "fecgpu" not in name:
         return None
-    if config == 7:  # the streaming encode (or the combine-job one, sw_stream 0); the decode's chain
-        if "sw_stream_kernel" in name or "comb_kernel<4>" in name:
+    if config == 7:  # the streaming encode (the default); the decode's chain, its combine passes included
+        if "sw_stream_kernel" in name:
             return "encode"
-        return "decode" if ("sw_dec_" in name or "comb_kernel<1>" in name or "comb_kernel<8>" in name) else None
+        return "decode" if ("sw_dec_" in name or "comb_kernel<" in name) else None
     return "encode" if "encode" in name else "decode" if "decode" in name else None
 
 
