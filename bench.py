@@ -8,19 +8,20 @@ HBM.  value = source-packet bytes (sum of packet lengths, no prefix or
 padding) of all ranks x steps / max-over-ranks wall time.
 
 Workloads (BASELINE.json configs):
-  --config 2 (default): XOR k=8 r=2, 65,536 windows x 8 x 1200 B per GPU,
+  --config 2          : XOR k=8 r=2, 65,536 windows x 8 x 1200 B per GPU,
                         one source erased per XOR group (e = r = 2)
-  --config 3          : GF(2^8) Cauchy k=16 r=4, 262,144 windows x 16 x 1200 B,
-                        exactly r sources erased per window
+  --config 3 (default): GF(2^8) Cauchy k=16 r=4, 262,144 windows x 16 x 1200 B,
+                        exactly r sources erased per window (the largest
+                        device-resident BASELINE config that one GPU holds whole)
   --config 4          : GF(2^8) k=32 r=8, mixed MTU 1200/9000 LENPREFIX,
                         131,072 windows per GPU (1M over 8), i.i.d. 10% erasures
   --config 7          : sliding-window RLC (RFC 8681): 524,288 x 1200 B sources per
                         GPU, a repair after every 8 over the last 32, 2% i.i.d. loss
                         of sources and repairs (a widening row, not a BASELINE config)
-The default run (one GPU, config 2) also times configs 3, 4 and 7 in the same
-process and reports them under "configs" in the same JSON line (each with its
-own ms_per_step, roofline, cpu_baseline and verify); the headline fields are
-config 2's.
+The default run (one GPU, config 3) also times configs 2, 4, 5 and 7 in the
+same process and reports them under "configs" in the same JSON line (each with
+its own ms_per_step, roofline, cpu_baseline and verify); the headline fields
+are config 3's.
 Multi-GPU: one process per GPU, windows sharded by rank with no data-path
 collective (weak scaling); RCCL only carries the barrier, the max-over-ranks
 time reduction and the 8-byte digest all-gather.  `--gpus N` launched without
@@ -46,17 +47,21 @@ import fecgpu  # noqa: E402
 from fecgpu import shard, workloads  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-PCIE_PEAK_GBS = 126.0  # PCIe Gen5 x16, 63 GB/s per direction (spec), both directions
+PCIE_DIR_PEAK_GBS = 63.0  # PCIe Gen5 x16, per direction (spec; MI355X_MICROARCH.md host link)
+DEFAULT_CONFIG = 3
+# config -> (steps, warmup) when --steps / --warmup are not given; cfg3 warms up
+# longer (its first ~10 calls run slow while the clocks and TLBs settle)
+DEFAULT_STEPS = {2: (200, 20), 3: (50, 10), 4: (5, 2), 5: (10, 2), 6: (10, 2), 7: (50, 10)}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # one cfg2 step is ~0.3 ms: 200 steps keep the timed region (~60 ms) well
-    # above barrier / launch jitter across ranks, and still finish in seconds
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(workloads.CONFIGS))
+    # 0 = the config's default (DEFAULT_STEPS): cfg3 50 steps of ~2.7 ms keep the
+    # timed region (~0.14 s) well above barrier / launch jitter across ranks
+    ap.add_argument("--steps", type=int, default=0)
+    ap.add_argument("--warmup", type=int, default=-1)
+    ap.add_argument("--config", type=int, default=DEFAULT_CONFIG, choices=sorted(workloads.CONFIGS))
     ap.add_argument("--nwin", type=int, default=0, help="windows per GPU (0 = config default)")
     ap.add_argument("--matrix", default="cauchy", choices=["cauchy", "vandermonde", "rlc"],
                     help="GF configs: parity rows (rlc: RFC 8681 random linear code, dense)")
@@ -98,9 +103,13 @@ def parse():
                          "~5 GB of source bytes per GPU")
     ap.add_argument("--r", type=int, default=0, help="repairs per window for --k")
     ap.add_argument("--extra-configs", type=int, choices=[0, 1], default=1,
-                    help="one-GPU default run (config 2): also time configs 3, 4 and 7 in this process and "
-                         "report them under \"configs\" (0 = config 2 only)")
-    return ap.parse_args()
+                    help="default run (config 3): also time configs 2, 4, 5 and 7 in this process and "
+                         "report them under \"configs\" (0 = config 3 only)")
+    a = ap.parse_args()
+    st, wu = DEFAULT_STEPS[a.config]
+    a.steps = a.steps if a.steps > 0 else st
+    a.warmup = a.warmup if a.warmup >= 0 else wu
+    return a
 
 
 def pmc_traffic(cfgid: int, kernel: str):
@@ -260,15 +269,14 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd).returncode
 
 
-# extra configs timed by the default run:
-# config -> (steps, warmup); cfg3 warms up longer (its first ~10 calls run slow
-# while the clocks and TLBs settle).  One GPU: configs 3, 4, 5
-# (host buffers, PCIe-inclusive: bound "pcie", never the headline) and 7.  N
-# ranks: the device-resident configs, each rank on its own window shard (cfg4:
-# 131,072 windows per rank, the 1M windows of BASELINE config 4 at N = 8) with
-# the digest gathered over RCCL.
-EXTRA_CONFIGS = {3: (10, 10), 4: (5, 2), 5: (10, 2), 7: (50, 10)}
-EXTRA_CONFIGS_MULTI = (3, 4, 7)
+# extra configs timed by the default run (VERDICT r02 item 5, r03 items 6 and 8,
+# r04 item 2): config -> (steps, warmup).  One GPU: configs 2, 4, 5 (host
+# buffers, PCIe-inclusive: bound "pcie", never the headline) and 7.  N ranks:
+# the device-resident configs, each rank on its own window shard (cfg4: 131,072
+# windows per rank, the 1M windows of BASELINE config 4 at N = 8) with the
+# digest gathered over RCCL.
+EXTRA_CONFIGS = {2: (200, 20), 4: (5, 2), 5: (10, 2), 7: (50, 10)}
+EXTRA_CONFIGS_MULTI = (2, 4, 7)
 
 
 def make_ctx(args):
@@ -339,6 +347,7 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
         batch.make_erasures(ctx, w0)
     src_bytes = batch.source_bytes()      # per rank, per step
     alg = batch.algorithmic_bytes()       # {'encode': B, 'decode': B} per launch
+    batch_pcie = batch.pcie_bytes() if cfg.host else None
 
     log(f"{cfg.name}: warmup {warmup}")
     if cfg.scheme == "sw":
@@ -437,6 +446,15 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
     dom = "decode" if dec_ms > enc_ms else "encode"
     dom_ms = enc_ms if dom == "encode" else dec_ms
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+    pcie = None
+    if cfg.host:  # PCIe is full duplex: each direction against its own 63 GB/s
+        pb = batch_pcie
+        pcie = {call: {d: {"bytes": pb[call][d], "GBs": round(pb[call][d] / (ms * 1e-3) / 1e9, 2),
+                           "frac": round(pb[call][d] / (ms * 1e-3) / 1e9 / PCIE_DIR_PEAK_GBS, 4)}
+                       for d in ("h2d", "d2h")}
+                for call, ms in (("encode", enc_ms), ("decode", dec_ms))}
+        bound_dir = max(("h2d", "d2h"), key=lambda d: pb[dom][d])
+        achieved = pcie[dom][bound_dir]["GBs"]
     traffic, traffic_src = (pmc_traffic(cfgid, dom)
                             if nwin == cfg.nwin_per_gpu and cfg.name == workloads.CONFIGS[cfgid].name and not wide
                             and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
@@ -447,7 +465,7 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
         cpu = (cpu_baseline_sw(cfg, args.cpu_seconds, args.cpu_threads) if cfg.scheme == "sw" else
                None if wide else  # the CPU codec's block code is k + r <= 64
                cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads))
-    peak, bound = (PCIE_PEAK_GBS, "pcie") if cfg.host else (HBM_PEAK_GBS, "hbm")
+    peak, bound = (PCIE_DIR_PEAK_GBS, f"pcie-{bound_dir}") if cfg.host else (HBM_PEAK_GBS, "hbm")
     return {
         "metric": ("GB/s source-packet bytes FEC encode+decode, host buffers, PCIe-inclusive"
                    if cfg.host else
@@ -498,7 +516,10 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "alg_bytes_per_launch": alg[dom],
+            "alg_bytes_per_launch": (batch_pcie[dom][bound_dir] if cfg.host else alg[dom]),
+            **({"pcie_directions": pcie,
+                "note": "bytes of the bound direction of the slower call / its host wall time, "
+                        "against 63 GB/s per direction"} if cfg.host else {}),
         },
         "roofline_other": {
             k2: round(alg[k2] / (ms * 1e-3) / 1e9, 1)
@@ -551,10 +572,10 @@ def main():
     ctx = make_ctx(args)
     line = run_config(args.config, args, rank, world, dev, ctx, args.steps, args.warmup, args.nwin)
     ok = line is None or line["verify"] is None or line["verify"].get("ok", False)
-    # the default one-GPU run also times the other single-GPU configs in this
-    # process (each on its own batch, freed after), under "configs"; the
-    # headline line above is config 2's as before
-    if args.extra_configs and args.config == 2 and not args.nwin and not args.k:
+    # the default run also times the other configs in this process (each on
+    # its own batch, freed after), under "configs"; the headline line above is
+    # config 3's
+    if args.extra_configs and args.config == DEFAULT_CONFIG and not args.nwin and not args.k:
         extras = {}
         for cid, (st, wu) in EXTRA_CONFIGS.items():
             if world > 1 and cid not in EXTRA_CONFIGS_MULTI:

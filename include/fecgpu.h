@@ -383,7 +383,14 @@ typedef struct fecgpu_sw_repair {
     uint8_t  reserved[3];
 } fecgpu_sw_repair;
 
-/* rep[t] (nrep rows of `stride` bytes) from the sources of hdr[t]'s window.
+/* The first sliding-window call (encode, decode or a per-connection
+ * sliding-window object's launch) on a device draws the ctx's dense RFC 8681
+ * coefficient table there (every repair_key's coefficients at DT 15, 16 MiB
+ * of device memory): a hipMalloc and a wait on the caller's stream, once per
+ * ctx and device.  Later calls are asynchronous as documented; a caller that
+ * needs the first call asynchronous too makes a small synchronous one first.
+ *
+ * rep[t] (nrep rows of `stride` bytes) from the sources of hdr[t]'s window.
  * src, rep and hdr are device pointers (FECGPU_F_HOST_PTRS: host memory,
  * staged, synchronous).  max_window: the largest nss among the headers
  * (1..FECGPU_SW_MAX_WINDOW; 0 = FECGPU_SW_MAX_WINDOW), which sizes the
@@ -437,6 +444,9 @@ ssize_t fecgpu_sw_decode_device(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *sr
  * error. */
 #define FECGPU_SW_ERR_HEADER   1u /* a header was bad or out of order: that call recovered nothing */
 #define FECGPU_SW_ERR_CAPACITY 2u /* a long system's operation log did not fit: its sources stayed lost */
+#define FECGPU_SW_ERR_INTERNAL 4u /* the device plan's chunk look-back gave up (never expected): the call's
+                                     results are not to be trusted; a synchronous retry reports it as
+                                     FECGPU_ERR_DEVICE */
 ssize_t fecgpu_sw_decode_errors(fecgpu_ctx *ctx, uint32_t *flags);
 
 /* ---- sliding-window per-connection objects ----------------------------

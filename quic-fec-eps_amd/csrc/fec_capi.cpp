@@ -23,9 +23,6 @@ using namespace fecgpu;
 #ifndef FECGPU_CHECK
 #define FECGPU_CHECK 0  // bounds-checked debug build (fec_kernels.hip); lib/libfecgpu_check.so
 #endif
-#ifndef FECGPU_BS_FLAT
-#define FECGPU_BS_FLAT 1  // fec_kernels.hip: bit-sliced encode in a flat unit space on uniform windows
-#endif
 
 namespace {
 
@@ -159,8 +156,8 @@ struct fecgpu_ctx {
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
     int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
-    int sw_stream = FECGPU_SW_STREAM_DEFAULT;  // sliding-window encode: 0 combine jobs, 1..5 streaming
-                                               // (dwords per lane), kSwStreamAuto per symbol size
+    int sw_stream = kSwStreamDefault;  // sliding-window encode: 0 combine jobs, 1..5 streaming
+                                       // (dwords per lane), kSwStreamAuto per symbol size
     int sw_long_min = kSwSmallE + 1;  // sliding-window decode: unknowns that force the long-system path
     uint64_t sw_log_entries = 0;      // long-system operation log: fixed size (tuning), 0 = automatic
     uint64_t sw_log_seen = 0;         // the largest log an overflow asked for on this ctx
@@ -456,8 +453,7 @@ void fecgpu_host_free(void *p) {
 
 namespace {
 
-// Plane picks of the runtime-mask bit-sliced encode (fec_kernels.hip rbs::,
-// rbs4::) for parity rows P[r][k]: for source j, output i and output plane p,
+// Plane picks of the runtime-mask bit-sliced encode (fec_kernels.hip rbs4::) for parity rows P[r][k]: for source j, output i and output plane p,
 // lo = the input planes q < 4 and hi = the planes q >= 4 (as bits q, q - 4)
 // for which bit p of P[i][j] * 2^q is set; stored as the kernel's index format
 // (kRbsDw4 dwords per 4 planes).  out: k * r * 2 * kRbsDw4 dwords.
@@ -474,21 +470,9 @@ void rbs_masks(const uint8_t *P, int k, int r, uint32_t *out) {
                     const uint8_t col = c ? g.exp[g.log[c] + q] : 0;
                     if ((col >> p) & 1) (q < 4 ? lo : hi) |= 1u << (q & 3);
                 }
-                if (kRbsCols == 4) {  // four-column units index register pairs: 2 x index
-                    if (kRbsDw4 == 8) {
-                        row[2 * p] = lo * 2;
-                        row[2 * p + 1] = hi * 2;
-                    } else if (kRbsDw4 == 4) {
-                        row[p] = lo * 2 | (hi * 2) << 16;
-                    } else {  // bytes lo, hi of plane p in dword p / 2
-                        row[p / 2] |= (lo * 2 | (hi * 2) << 8) << (16 * (p & 1));
-                    }
-                } else if (kRbsDw4 == 8) {
-                    row[2 * p] = lo;
-                    row[2 * p + 1] = hi;
-                } else {
-                    row[p] = lo | hi << 8;
-                }
+                // four-column units index register pairs (2 x index); bytes lo, hi
+                // of plane p in dword p / 2
+                row[p / 2] |= (lo * 2 | (hi * 2) << 8) << (16 * (p & 1));
             }
         }
 }
@@ -699,8 +683,8 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
     }
     const auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
     const size_t o_out = up(nwin * sizeof(CombJob)), o_coef = o_out + up(nwin * kMaxR * sizeof(uint64_t));
-    const bool two = decode && FECGPU_WIDE_2STAGE;
-    const size_t coef_bytes = decode ? nwin * kMaxR * (size_t)(two ? kMaxR : n) : 0;
+    const bool two = decode;  // the two-stage decode (fec_wide.hip)
+    const size_t coef_bytes = decode ? nwin * kMaxR * (size_t)kMaxR : 0;
     const size_t o_j1 = o_coef + up(coef_bytes), o_o1 = o_j1 + (two ? up(nwin * sizeof(CombJob)) : 0);
     const size_t o_syn = o_o1 + (two ? up(nwin * (size_t)r * sizeof(uint64_t)) : 0);
     const size_t total = o_syn + (two ? nwin * (size_t)r * stride : 0);
@@ -714,7 +698,7 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
     const uint32_t ncol = sym_len ? stride / 16u : (sym_len_all + 15u) / 16u;
     // plane picks (run_wide's row block: P, [P | I], then the picks of each)
     const uint32_t *mP = nullptr, *mPI = nullptr;
-    if (FECGPU_WIDE_RBS && ctx->bitslice && r >= 4) {
+    if (ctx->bitslice && r >= 4) {
         const size_t o_m = ((size_t)r * k + (size_t)r * n + 255) & ~size_t(255);
         mP = reinterpret_cast<const uint32_t *>(P + o_m);
         mPI = mP + (size_t)k * r * 2 * kRbsDw4;
@@ -887,9 +871,6 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
     // flat slot space when every window has the same geometry (GF decode
     // always plans per window in LDS, so it always runs in group mode)
     p.flat = !win_off && !sym_len && !(decode && scheme == FECGPU_SCHEME_GF256);
-#ifdef FECGPU_FORCE_GROUP
-    p.flat = false;  // A/B knob: group mode for every kernel
-#endif
     a.ncol = (sym_len_all + 15u) >> 4;
     if (!decode) {
         if (scheme == FECGPU_SCHEME_GF256) {
@@ -934,21 +915,15 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         // so a partly idle last pass costs more than in the table kernels).
         p.bitslice = true;
         p.matrix = (int)code->matrix;
-#if !FECGPU_BS_FLAT
-        p.flat = false;
-#endif
         p.lds_bytes = 0;
         const uint32_t units = ncol ? (ncol + 1) / 2 : (uint32_t)((stride >> 4) + 1) / 2;
         const uint32_t want = (uint32_t)ctx->bs_passes * kBlock;
         p.wpb = units ? std::max(1, std::min<int>(kMaxWpb, (int)((want + units - 1) / units))) : kMaxWpb;
     }
-    else if (!decode && scheme == FECGPU_SCHEME_GF256 && !remote && ctx->bitslice && r >= FECGPU_RBS_MIN_R) {
+    else if (!decode && scheme == FECGPU_SCHEME_GF256 && !remote && ctx->bitslice && r >= kRbsMinR) {
         // no compiled masks for this code: the runtime-mask kernel, same unit
         // space and group sizing
         p.rbitslice = true;
-#if !FECGPU_BS_FLAT
-        p.flat = false;
-#endif
         p.lds_bytes = 0;
         // units of kRbsCols columns (the group sizing above counted pairs)
         const uint32_t c16 = ncol ? ncol : stride >> 4;

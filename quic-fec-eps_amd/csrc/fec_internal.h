@@ -72,31 +72,12 @@ struct LaunchPlan {
 
 // GF encode of r parity rows goes to the runtime-mask bit-sliced kernel
 // (fec_kernels.hip rbs::) when no compiled one exists: r >= this.
-#ifndef FECGPU_RBS_MIN_R
-#define FECGPU_RBS_MIN_R 5
-#endif
-#ifndef FECGPU_RBS_WIDE
-// runtime bit-sliced encode: 1 = a dword per plane index (lo, hi), loaded
-// straight into M0 with no unpacking; 0 = one dword per plane (lo | hi << 8)
-#define FECGPU_RBS_WIDE 1
-#endif
-#ifndef FECGPU_RBS_COLS
-// runtime bit-sliced encode: 16-B columns per lane (2: 32 byte positions, 4:
-// 64, half the index-mode switches per byte; needs FECGPU_RBS_WIDE)
-#define FECGPU_RBS_COLS 4
-#endif
-constexpr int kRbsCols = FECGPU_RBS_COLS;
-#ifndef FECGPU_RBS4_PACK
-// four-column units, index table format: 0 = two dwords per plane (lo x 2,
-// hi x 2); 1 = one dword per plane (lo x 2 | hi x 2 << 16, one s_lshr per
-// plane); 2 = one dword per two planes (a byte per index, 1.5 s_lshr per
-// plane).  Smaller tables stay in the scalar cache (k48 r8: 24 KB at 0)
-#define FECGPU_RBS4_PACK 2
-#endif
-// dwords of the index table per 4 output planes
-constexpr int kRbsDw4 = FECGPU_RBS_COLS == 4 ? (FECGPU_RBS4_PACK == 2 ? 2 : FECGPU_RBS4_PACK == 1 ? 4 : 8)
-                                             : (FECGPU_RBS_WIDE ? 8 : 4);
-constexpr int kRbsPlaneDw = kRbsDw4 >= 4 ? kRbsDw4 / 4 : 1;  // mask dwords per output plane (0.5: see kRbsDw4)
+constexpr int kRbsMinR = 5;
+// runtime bit-sliced encode: 16-B columns per lane (64 byte positions); its
+// index table holds a byte per index, two planes per dword: kRbsDw4 dwords per
+// 4 output planes (fec_kernels.hip rbs4::, fec_capi.cpp rbs_masks)
+constexpr int kRbsCols = 4;
+constexpr int kRbsDw4 = 2;
 
 // GF encode of (k, r, matrix) has a compiled bit-sliced kernel.
 bool bitslice_supported(int k, int r, int matrix);
@@ -213,20 +194,18 @@ struct CombArgs {
     // non-empty jobs of its share (runs of kCombRun slots dealt round-robin)
     // into LDS and runs them in groups as large as `budget` holds
     int sparse;
-    // nonzero and below 4 GiB: every input row lies in [in_base, in_base + in_bytes)
-    // (the kernel reads rows by buffer loads with scalar row offsets)
-    uint64_t in_bytes;
     uint32_t budget;
+    // nullable (sliding-window decode): the call's error bits; the launch does
+    // nothing when kSwErrHeader is set (a bad header list recovers nothing)
+    const uint32_t *err;
     // every job has the same coefficient block (a block code's parity rows:
     // wide encode): [nout_max][nin_max] at coef, its tables built once per
     // workgroup and shared by the workgroup's jobs (job regions hold only their
     // output pointers), so more jobs fit a workgroup
     int shared_coef;
 };
-#ifndef FECGPU_COMB_RUN
-#define FECGPU_COMB_RUN 16
-#endif
-constexpr uint32_t kCombRun = FECGPU_COMB_RUN;                       // sparse launches: slots per run
+// sparse launches: slots per run (8 / 16 / 32 gave 0.201 / 0.198 / 0.208 ms per cfg7 decode call, r04)
+constexpr uint32_t kCombRun = 16;
 constexpr uint32_t kCombListLds = 256 * (uint32_t)sizeof(CombJob);   // sparse launches: one round's jobs
 // LDS bytes per job of comb_kernel<R> at nin_max inputs
 __host__ __device__ inline uint32_t comb_job_lds(int nin_max, int R) {
@@ -247,24 +226,16 @@ hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
 // the runtime-mask bit-sliced encode over uniform windows of any k (fec_kernels.hip)
 hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t stride, uint64_t wpitch, int k,
                            int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s);
-#ifndef FECGPU_WIDE_RBS
-#define FECGPU_WIDE_RBS 1  // wide encode and the two-stage decode's syndromes by the runtime-mask
-                           // bit-sliced kernel (r >= 4; plane picks by scalar loads, no LDS tables)
-#endif
-// GF block codes with k + r > 64 (fec_wide.hip): a plan / job kernel, then the
-// combine kernel over a job per window
+// GF block codes with k + r > 64 (fec_wide.hip): encode by the runtime-mask
+// bit-sliced kernel (r >= 4) or a combine job per window; decode in two stages
+// (syndromes of every repair with one coefficient block [P | I] for all
+// windows, the missing sources' rows zeroed first; then x = T s per window over
+// its r syndromes).  Scratch: stage-1 jobs [nwin], their outputs [nwin][r],
+// syndrome rows [nwin][r][stride]; the parity-row block holds [P | I] after P.
 hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
                        uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
                        uint64_t *outs, uint8_t *coef, hipStream_t s, CombJob *jobs1, uint64_t *outs1,
                        uint8_t *syn, const uint32_t *masks_P = nullptr, const uint32_t *masks_PI = nullptr);
-#ifndef FECGPU_WIDE_2STAGE
-// wide decode in two combine launches (fec_wide.hip): syndromes of every
-// repair with one coefficient block [P | I] for all windows (the missing
-// sources' rows zeroed first), then x = T s per window over its r syndromes.
-// Scratch: stage-1 jobs [nwin], their outputs [nwin][r], syndrome rows
-// [nwin][r][stride]; the parity-row block holds [P | I] after P.
-#define FECGPU_WIDE_2STAGE 1
-#endif
 
 // encode: job t = repair t (coefficients at coef + t * kSwCoefPitch, output rep row t).
 // group > 1: the repairs t0 = g * group .. t0 + group - 1 share job g when
@@ -301,13 +272,6 @@ inline uint64_t sw_enc_jobs(uint64_t nrep, int group) {
 // to start at or after the end of the one A P repairs before it (P = 1 and
 // A = ceil(W / step) for a regular schedule; the workgroup picks the smallest
 // P, then A <= kSwSlots, that its segment's headers allow).
-#ifndef FECGPU_SWS_SGPR
-// streaming encode: multiply tables in global memory (a table pass first), read
-// by scalar loads: 4-entry tables over the bit pairs of a byte, so each v_perm
-// takes one SGPR (gfx950 reads at most one SGPR per VALU op) and no LDS read
-// per product (fec_swenc.hip)
-#define FECGPU_SWS_SGPR 0  // A/B pending (round 4)
-#endif
 constexpr int kSwSeg = 64;
 constexpr int kSwSlots = 8;
 constexpr int kSwStreamU = 8;  // sources per batch (a regular schedule's step divides it: whole batches)
@@ -323,16 +287,8 @@ struct SwStreamArgs {
     int segcap;         // repairs per segment (<= kSwSeg)
     uint64_t nseg;      // segments; workgroup b takes [b nseg / grid, (b + 1) nseg / grid)
     uint32_t lds;       // dynamic LDS bytes
-    // nullable: device scratch of sw_stream_gtab_bytes(nrep, max_window) for the
-    // multiply tables in global memory, read by scalar loads (FECGPU_SWS_SGPR):
-    // 4-entry tables (one SGPR feeds a v_perm), no LDS tables
-    void *gtab;
     const uint8_t *rlc;  // nullable: the dense coefficient table (ctx_rlc_table)
 };
-// [kSwStreamU zero entries][per repair: kSwStreamU zeros, max_window entries][kSwStreamU zeros], 16 B each
-inline uint64_t sw_stream_gtab_bytes(uint64_t nrep, int max_window) {
-    return (2ull * kSwStreamU + nrep * (uint64_t)(max_window + kSwStreamU)) * 16ull;
-}
 // C: dwords per lane (1..5, dividing the row's dwords); LDS budget per workgroup in bytes
 hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t s);
 // LDS per streaming-encode repair: kSwStreamU zero tables and max_window
@@ -355,40 +311,13 @@ constexpr int kSwSmallE = 64;   // unknowns of a small system
 constexpr int kSwSmallP = 96;   // equations (received repairs) of a small system
 constexpr int kSwRows = 256;    // long systems: row slots (more rows alive at one column are reduced
                                 // to a basis first: they span at most 255 columns, fec_swdec.hip)
-constexpr int kSwChunk = 4096;  // sources per planning chunk (FECGPU_SWD_FUSED 0)
-constexpr int kSwPlanChunk = 2048;  // sources per block of the fused plan
-#ifndef FECGPU_SWD_SOLVE_LIST
-#define FECGPU_SWD_SOLVE_LIST 0  // fused plan: solve jobs in a compact list (one atomic per system: 24 us slower on cfg7, r04)
-                                 // instead of slots per unknown (the solve pass walks every slot)
-#endif
-#ifndef FECGPU_SWD_SPARSE
-#define FECGPU_SWD_SPARSE 1  // the syndrome and solve launches gather their non-empty job slots
-                             // (CombArgs::sparse) instead of walking every slot in groups
-#endif
-#ifndef FECGPU_SWD_ONEPASS
-#define FECGPU_SWD_ONEPASS 1  // fused plan: the system pass takes systems of up to 64 unknowns /
-                              // 96 equations itself (mid-size LDS per wave), no separate mid pass
-#endif
-#ifndef FECGPU_SWD_SOLVE_OUT
-#define FECGPU_SWD_SOLVE_OUT 4  // recovered sources per solve job (8, 4 or 2): the solve pass's
-                                // critical path is its widest system's job, nin rows x outputs per lane
-                                // (cfg7, r04: 4 gave 0.198 vs 8 0.206 ms at 2 % loss, 1.70 vs 1.76 at 10 %)
-#endif
-constexpr int kSwSolveOut = FECGPU_SWD_SOLVE_OUT;
-#ifndef FECGPU_SWD_MIDLOCK
-#define FECGPU_SWD_MIDLOCK 2  // one-pass system kernel: 3 KB of LDS per wave for the common tiny
-                              // systems, this many mid-size regions per block taken under LDS
-                              // locks (0: a mid-size region per wave)
-#endif
-#ifndef FECGPU_SWD_FUSED
-#define FECGPU_SWD_FUSED 1  // the decode plan as one look-back launch (sw_dec_plan_kernel) instead of
-                            // a memset and five passes
-#endif
+constexpr int kSwPlanChunk = 2048;  // sources per block of the plan (one look-back launch; the
+                                    // five-pass plan it replaced measured 0.236 vs 0.215 ms, r04)
+// recovered sources per solve job (8, 4 or 2): the solve pass's critical path is
+// its widest system's job, nin rows x outputs per lane (cfg7, r04: 4 gave 0.198
+// vs 8 0.206 ms at 2 % loss, 1.70 vs 1.76 at 10 %)
+constexpr int kSwSolveOut = 4;
 
-#ifndef FECGPU_SW_RLCTAB
-#define FECGPU_SW_RLCTAB 1  // dense (dt 15) coefficient rows read from the ctx's table instead of
-                            // stepping TinyMT32 per coefficient (encode, decode plan, systems, long path)
-#endif
 // RFC 8681 coefficients at dt 15 depend on the repair key alone (a window takes
 // a prefix of the key's sequence): the table holds every key's 255, one
 // 256-byte row per key (byte 255 zero), 16 MiB per device (ctx_rlc_table)
@@ -400,16 +329,16 @@ hipError_t launch_rlc_table(uint8_t *tab, hipStream_t s);
 constexpr uint32_t kSwErrHeader = 1u;    // a bad or unordered header: the call recovers nothing
 constexpr uint32_t kSwErrCapacity = 2u;  // a long system's operation log (or the queue) did not fit:
                                          // that system stays lost (a larger log fixes it)
-constexpr uint32_t kSwErrInternal = 4u;  // the fused plan's look-back gave up (never expected)
-struct SwDecCtr {  // per call, zeroed before the first kernel
+constexpr uint32_t kSwErrInternal = 4u;  // the plan's look-back gave up (never expected)
+static_assert(kSwErrHeader == FECGPU_SW_ERR_HEADER && kSwErrCapacity == FECGPU_SW_ERR_CAPACITY &&
+                  kSwErrInternal == FECGPU_SW_ERR_INTERNAL,
+              "the public flags are the device's bits");
+struct SwDecCtr {  // per call, written by the plan's last block
     uint32_t nlost, wmax, maxp, err;   // err: kSwErr* bits
-    uint32_t nmid, nlong, npiv, recovered;  // queued mid / long systems, pivot rows, recovered
+    uint32_t pad3, nlong, npiv, recovered;  // queued long systems, pivot rows, recovered
     uint32_t maxin;                    // widest small-system solve (syndrome rows)
-    // fused plan: solve outputs handed out, 8 per solve job (a system takes
-    // ceil(determined / 8) jobs at once: job j writes outputs 8j ..), so the
-    // solve pass walks only real jobs (nsolout >> 3 of them)
-    uint32_t nsolout;
-    uint32_t nstart;                   // fused plan: larger systems' first unknowns listed (starts)
+    uint32_t pad4;
+    uint32_t nstart;                   // larger systems' first unknowns listed (starts)
     uint32_t pad0, pad1, pad2;
     unsigned long long nlog;           // long-system log entries
 };
@@ -441,26 +370,20 @@ struct SwDecArgs {
     const fecgpu_sw_repair *hdr;               // device
     uint8_t *stat;                             // [nsrc] out: 0 present / recovered, 1 lost
     uint64_t nsrc, nrep;
-    uint32_t stride, S, nchunk;
+    uint32_t stride, S;
     int long_min;                              // systems with e >= long_min take the long path
-    uint32_t *reach;                           // [nsrc + 1] max window end of the received repairs
-                                               // starting there, then rank[i] = lost sources before i
-    uint32_t *rcnt;                            // [nsrc + 1] repairs starting there, then repfirst[i] =
-                                               // repairs starting before i
-    uint32_t *chunk;                           // [3 * nchunk] lost count / max reach / repairs per chunk,
-                                               // then their exclusive scans
+    uint32_t *reach;                           // [nsrc + 1] rank[i] = lost sources before i
+    uint32_t *rcnt;                            // [nsrc + 1] repfirst[i] = repairs starting before i
     uint32_t *lost, *reachL;                   // [nsrc] lost sources; prefix max of reach at each
     SwDecCtr *ctr;
     CombJob *syn_jobs;                         // [nrep] syndrome job of repair t (empty unless needed),
-                                               // then [nsrc] (fused plan) the one-unknown systems'
-                                               // jobs by lost index
+                                               // then [nsrc] the one-unknown systems' jobs by lost index
     uint64_t *syn_outs;                        // [nrep + nsrc]
     uint8_t *coef;                             // [nrep + nsrc][kSwCoefPitch]: syndrome coefficients
     CombJob *sol_jobs;                         // [nsrc] solve jobs of a small system in its unknowns' slots
     uint64_t *sol_outs;                        // [nsrc] their outputs (unknown x + d)
     uint8_t *sol_coef;                         // [nrep * kSwSmallE] coefficients (64 B per repair)
     SwLong *longs;                             // [long_cap]
-    SwLong *mids;                              // [long_cap] small systems too wide for the tiny pass
     uint64_t long_cap;
     SwOp *log;                                 // [log_cap]
     uint64_t log_cap;
@@ -474,16 +397,16 @@ struct SwDecArgs {
     uint8_t *src;                              // the sources (replay writes recovered ones)
     const uint8_t *synd;                       // syndrome rows (g * stride)
     SwSticky *sticky;                          // nullable: asynchronous calls also raise errors here
-    // fused plan (FECGPU_SWD_FUSED): look-back state of the chunks, kept across
+    // plan: look-back state of the chunks, kept across
     // calls (ctx_sw_lookback): flags (epoch << 2 | state), aggregates, inclusive
     // prefixes, and the ticket counter that orders the chunks
     uint32_t *lb_flag;
     uint4 *lb_agg, *lb_inc;
     uint32_t *lb_ticket;  // [0] next chunk, [1] blocks done, [2] starts listed, [3] singles, [4] error bits
     uint32_t epoch;
-    uint8_t *lkind;       // [nsrc] per lost index, from the fused plan: 0 member of a larger
+    uint8_t *lkind;       // [nsrc] per lost index, from the plan: 0 member of a larger
                           // system, 1 recovered alone, 2 a larger system's first, 3 alone, lost
-    uint32_t *starts;     // [nsrc] fused plan: lost indices of the larger systems' first unknowns
+    uint32_t *starts;     // [nsrc] lost indices of the larger systems' first unknowns
                           // (ctr->nstart of them, in no particular order)
     const uint8_t *rlc;   // nullable: the dense coefficient table (kRlcRow bytes per repair key)
 };
@@ -506,19 +429,17 @@ ssize_t set_dev_error(hipError_t e, const char *what);
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *jobs,
                        void *coef, void *outs, hipStream_t s, int group = 1,
-                       const fecgpu_sw_repair *hdr_host = nullptr, int stream = 0, void *gtab = nullptr,
-                       const uint8_t *rlc = nullptr);
+                       const fecgpu_sw_repair *hdr_host = nullptr, int stream = 0, const uint8_t *rlc = nullptr);
 // the ctx's "sw_group" tuning (repairs per sliding-window encode job)
 int ctx_sw_group(const fecgpu_ctx *ctx);
 // the ctx's "sw_stream" tuning: 0 combine jobs, 1..5 the streaming encode
 // with that many dwords per lane, kSwStreamAuto (default) chosen per symbol size
 int ctx_sw_stream(const fecgpu_ctx *ctx);
 constexpr int kSwStreamAuto = 6;
-#ifndef FECGPU_SW_STREAM_DEFAULT
-#define FECGPU_SW_STREAM_DEFAULT 1  // the ctx's "sw_stream" default: 1 dword per lane (cfg7 A/B, r04:
-                                   // C = 1 / 2 / 3 / 4 / 5 gave 0.213 / 0.240 / 0.226 / 0.258 / 0.235 ms;
-                                   // the VALU, not the LDS table reads, bounds the kernel)
-#endif
+// the ctx's "sw_stream" default: 1 dword per lane (cfg7 A/B, r04: C = 1 / 2 /
+// 3 / 4 / 5 gave 0.213 / 0.240 / 0.226 / 0.258 / 0.235 ms; the VALU, not the
+// LDS table reads, bounds the kernel)
+constexpr int kSwStreamDefault = 1;
 int sw_stream_dwords(int stream, uint32_t S);
 // "sw_long_min": systems of at least this many unknowns take the long-system
 // path even when the small one would fit (default kSwSmallE + 1)

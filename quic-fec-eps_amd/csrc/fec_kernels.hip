@@ -22,71 +22,21 @@
 
 #include <utility>
 
-#ifndef FECGPU_NT
-#define FECGPU_NT 0  // nontemporal (streaming) loads/stores; A/B build knob
-#endif
-#ifndef FECGPU_XCD
-#define FECGPU_XCD 1  // XCD-aware split of the work units (A/B knob)
-#endif
-#ifndef FECGPU_XOR_LOADS
-#define FECGPU_XOR_LOADS 4  // XOR encode: input rows loaded per batch (rounded up to r);
-                            // 4 beat 2 and 8 at 2 workgroups/CU (scripts/sweep.py, r01)
-#endif
-#ifndef FECGPU_GF_U
-// GF bodies: input rows loaded per batch.  Swept on the box (scripts/sweep.py):
-// r = 4 runs best with 2 rows in flight per lane (fewer bytes in flight keep
-// HBM efficient), r = 8 with 8 (its long VALU phase needs more loads queued).
-#ifndef FECGPU_GF_U_HI
-#define FECGPU_GF_U_HI 8
-#endif
-#define FECGPU_GF_U (R <= 4 ? 2 : FECGPU_GF_U_HI)
-#endif
-#ifndef FECGPU_PLAN_TP
-#define FECGPU_PLAN_TP 1  // GF decode plans: table entries written along the output index first
-#endif
-#ifndef FECGPU_GFD_U
-// GF decode: input rows loaded per batch.  8 at every r: decode's input rows
-// come through an LDS index (received sources, chosen repairs), so a deeper
-// batch hides that extra latency; cfg3 decode -1.7% vs 2 (scripts/ab.py, r01),
-// cfg4 unchanged (already 8).
-#define FECGPU_GFD_U 8
-#endif
-#ifndef FECGPU_XDEC_ALL
-#define FECGPU_XDEC_ALL 0  // XOR decode: all recoverable groups in one row pass (A/B knob)
-#endif
-#ifndef FECGPU_NT_STORE
-// Nontemporal stores for repairs / recovered symbols (written once, not read
-// back by the kernel): +2.8% on cfg2, neutral on cfg3/cfg4 (scripts/ab.py, r01).
-#define FECGPU_NT_STORE 1
-#endif
-#ifndef FECGPU_GFE_MINW_HI
-// GF encode at r > 4 (VALU-bound, paired rows): ask for at least this many
-// waves per SIMD.  3 trades a few spilled registers for occupancy and ran
-// 7% faster than the unconstrained 2 waves on cfg4 (scripts/ab.py, r01).
-#define FECGPU_GFE_MINW_HI 3
-#endif
-#if FECGPU_GFE_MINW_HI > 0
-#define GFE_WAVES __attribute__((amdgpu_waves_per_eu(R > 4 ? FECGPU_GFE_MINW_HI : 1, 8)))
-#else
-#define GFE_WAVES
-#endif
-#ifndef FECGPU_GFD_MINW
-#define FECGPU_GFD_MINW 0  // >0: GF decode at r <= 4 asks for this many waves per SIMD
-#endif
-#if FECGPU_GFD_MINW > 0
-#define GFD_WAVES __attribute__((amdgpu_waves_per_eu(R <= 4 ? FECGPU_GFD_MINW : 1, 8)))
-#else
-#define GFD_WAVES
-#endif
-#ifndef FECGPU_PLAN_GJ
-#define FECGPU_PLAN_GJ 0  // GF decode plan by Gauss-Jordan instead of the closed form (A/B knob)
-#endif
-#ifndef FECGPU_DEC_PLANONLY
-#define FECGPU_DEC_PLANONLY 0  // measurement aid: GF decode plans only, no data pass
-#endif
-#ifndef FECGPU_ENC_SGPR
-#define FECGPU_ENC_SGPR 0  // GF encode tables via scalar loads instead of LDS (A/B knob)
-#endif
+// Tuning constants (measured on the box; the A/B knobs that lost were removed in r05)
+// XOR encode: input rows loaded per batch (rounded up to r); 4 beat 2 and 8 at
+// 2 workgroups/CU (scripts/sweep.py, r01)
+constexpr int kXorLoads = 4;
+// GF bodies: input rows loaded per batch.  r <= 4 runs best with 2 rows in
+// flight per lane (fewer bytes in flight keep HBM efficient), r = 8 with 8
+// (its long VALU phase needs more loads queued; scripts/sweep.py)
+#define GF_ENC_U(R) ((R) <= 4 ? 2 : 8)
+// GF decode: input rows loaded per batch.  Decode's input rows come through an
+// LDS index (received sources, chosen repairs), so a deeper batch hides that
+// extra latency; cfg3 decode -1.7% vs 2 (scripts/ab.py, r01)
+constexpr int kGfdU = 8;
+// GF encode at r > 4 (VALU-bound, paired rows): at least 3 waves per SIMD, a
+// few spilled registers for occupancy: 7% faster than 2 waves on cfg4 (r01)
+#define GFE_WAVES __attribute__((amdgpu_waves_per_eu(R > 4 ? 3 : 1, 8)))
 #ifndef FECGPU_CHECK
 // Bounds-checked debug build (GPU AddressSanitizer is not available
 // on this pool): every symbol load / store is checked against the byte ranges
@@ -94,10 +44,6 @@
 // not performed (loads return zero) and is recorded for the host, which fails
 // the call with FECGPU_ERR_DEVICE.  Built as lib/libfecgpu_check.so.
 #define FECGPU_CHECK 0
-#endif
-#ifndef FECGPU_PIPE
-#define FECGPU_PIPE 0  // register double-buffered input loads in the GF bodies (A/B: no gain,
-                       // costs VGPRs / occupancy on decode; profiles/r01 notes)
 #endif
 
 namespace fecgpu {
@@ -144,23 +90,17 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
 #if FECGPU_CHECK
     if (!chk_ok(p)) return make_uint4(0, 0, 0, 0);
 #endif
-#if FECGPU_NT
-    const u32x4 v = __builtin_nontemporal_load((gptr_c)(p));
-#else
     const u32x4 v = *(gptr_c)(p);
-#endif
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
 #if FECGPU_CHECK
     if (!chk_ok(p)) return;
 #endif
+    // nontemporal: repairs and recovered symbols are written once and not read
+    // back by the kernel (+2.8% on cfg2, neutral on cfg3 / cfg4; r01)
     const u32x4 x = {v.x, v.y, v.z, v.w};
-#if FECGPU_NT || FECGPU_NT_STORE
     __builtin_nontemporal_store(x, (gptr)(p));
-#else
-    *(gptr)(p) = x;
-#endif
 }
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
     return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
@@ -183,27 +123,9 @@ __device__ __forceinline__ Split split(uint4 v) {
     return s;
 }
 
-#ifndef FECGPU_BITOP3
-#define FECGPU_BITOP3 1  // gfx950 v_bitop3_b32 (3-input XOR) in the GF multiply-accumulate
-#endif
-#ifndef FECGPU_GF_PAIR
-// Fold two input rows per xor3 chain (1.5 instead of 2 ops per product, but
-// two rows' splits and tables live at once): 0 never, 1 encode at r > 4,
-// 2 every encode (default: cfg4 encode -14% time, cfg3 -1%), 3 encode and
-// decode: pairing in decode cost 12% on cfg3 through register pressure
-// (scripts/ab.py, r01).
-#define FECGPU_GF_PAIR 2
-#endif
-#define GF_PAIR_ENC(R) (FECGPU_BITOP3 && (FECGPU_GF_PAIR >= 2 || (FECGPU_GF_PAIR == 1 && (R) > 4)))
-#define GF_PAIR_DEC (FECGPU_BITOP3 && FECGPU_GF_PAIR >= 3)
-
 // a ^ b ^ c in one gfx950 VALU op (truth table 0x96)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-#if FECGPU_BITOP3
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-#else
-    return a ^ b ^ c;
-#endif
 }
 
 // acc ^= c*x for the 4 dwords of a column: 3 perm + 2 VALU per dword
@@ -355,7 +277,7 @@ __device__ __forceinline__ void group_geometry(const BatchArgs &a, GroupLds &g, 
 template <int R>
 __device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, int k, bool valid,
                                                 uint64_t od) {
-    constexpr int STEP = R * ((FECGPU_XOR_LOADS + R - 1) / R);
+    constexpr int STEP = R * ((kXorLoads + R - 1) / R);
     uint4 acc[R];
 #pragma unroll
     for (int g = 0; g < R; g++) acc[g] = zero4();
@@ -374,15 +296,16 @@ __device__ __forceinline__ void xor_encode_slot(uint8_t *base, uint32_t stride, 
     }
 }
 
-// Software-pipelined GF multiply-accumulate over k inputs of one slot:
-// acc[m] ^= D[q][m] * in_q for q < k, m < min(ne, R).  Inputs are loaded U at
-// a time into one of two register buffers while the other is multiplied, so
-// every wave keeps U 16-B loads in flight through the VALU phase.
-// `addr(q)` gives input q's column address, tables are [q][m] in LDS.
+// GF multiply-accumulate over k inputs of one slot: acc[m] ^= D[q][m] * in_q
+// for q < k, m < min(ne, R), U inputs loaded per batch (register double
+// buffering measured no gain and cost occupancy, r01).  `addr(q)` gives input
+// q's column address, tables are [q][m] in LDS.  PAIR: rows in pairs, one
+// xor3 chain folds both rows' lookups (1.5 instead of 2 ops per product:
+// encode, cfg4 -14 %; in decode the register pressure cost 12 % on cfg3, r01).
 template <int R, int U, bool PAIR, class Addr, class TabP, class TcP>
-__device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne, Addr &&addr,
-                                                 TabP tab, TcP tc) {
-    uint4 va[U], vb[U];
+__device__ __forceinline__ void gf_mac_batched(uint4 (&acc)[R], int k, int ne, Addr &&addr,
+                                               TabP tab, TcP tc) {
+    uint4 va[U];
     auto load = [&](uint4(&v)[U], int q0) {
 #pragma unroll
         for (int t = 0; t < U; t++) v[t] = ld16(addr(min(q0 + t, k - 1)));  // past k: unused re-read
@@ -413,33 +336,21 @@ __device__ __forceinline__ void gf_mac_pipelined(uint4 (&acc)[R], int k, int ne,
             }
         }
     };
-#if FECGPU_PIPE
-    load(va, 0);
-    for (int q0 = 0; q0 < k; q0 += 2 * U) {
-        if (q0 + U < k) load(vb, q0 + U);
-        mul(va, q0);
-        if (q0 + U >= k) break;
-        if (q0 + 2 * U < k) load(va, q0 + 2 * U);
-        mul(vb, q0 + U);
-    }
-#else
-    (void)vb;
     for (int q0 = 0; q0 < k; q0 += U) {
         load(va, q0);
         mul(va, q0);
     }
-#endif
 }
 
 // GF encode (a5): R_i = sum_j C[i][j] * S_j, tables [j][i] in LDS (broadcast reads).
 template <int R, int UO, class TabP, class TcP>
 __device__ __forceinline__ void gf_encode_slot(uint8_t *base, uint32_t stride, int k, TabP tab,
                                                TcP tc, bool valid, uint64_t od) {
-    constexpr int U = UO ? UO : FECGPU_GF_U;
+    constexpr int U = UO ? UO : GF_ENC_U(R);
     uint4 acc[R];
 #pragma unroll
     for (int m = 0; m < R; m++) acc[m] = zero4();
-    gf_mac_pipelined<R, U, GF_PAIR_ENC(R)>(acc, k, R, [&](int q) { return base + (uint32_t)q * stride; }, tab, tc);
+    gf_mac_batched<R, U, true>(acc, k, R, [&](int q) { return base + (uint32_t)q * stride; }, tab, tc);
     if (valid) {
 #pragma unroll
         for (int m = 0; m < R; m++) st16(base + od + (size_t)(k + m) * stride, acc[m]);
@@ -457,44 +368,6 @@ __device__ __forceinline__ uint32_t xor_decode_slot(const BatchArgs &a, uint8_t 
     const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
     const uint64_t miss = ~pres & kmask;
     uint32_t bad = 0;
-#if FECGPU_XDEC_ALL
-    // one pass over the window's rows for every recoverable group at once:
-    // row j feeds accumulator j mod r (the encode structure), rows of groups
-    // with nothing to rebuild and the missing rows themselves are not loaded
-    uint32_t recm = 0;
-    int mrow[R];
-#pragma unroll
-    for (int g = 0; g < R; g++) {
-        const uint64_t mg = miss & a.gmask[g];
-        mrow[g] = (int)__ffsll((unsigned long long)mg) - 1;
-        if (!mg) continue;
-        if (((mg & (mg - 1)) == 0) && ((pres >> (k + g)) & 1)) recm |= 1u << g;
-        else bad = 1;
-    }
-    if (!recm) return bad;
-    constexpr int STEP = R * ((8 + R - 1) / R);
-    uint4 acc[R];
-#pragma unroll
-    for (int g = 0; g < R; g++)
-        acc[g] = ((recm >> g) & 1) ? ld16(base + (size_t)(k + g) * stride) : zero4();
-    for (int j0 = 0; j0 < k; j0 += STEP) {
-        uint4 v[STEP];
-#pragma unroll
-        for (int t = 0; t < STEP; t++) {
-            const int j = j0 + t;
-            const bool need = j < k && ((recm >> (t % R)) & 1) && ((pres >> j) & 1);
-            v[t] = need ? ld16(base + (size_t)j * stride) : zero4();
-        }
-#pragma unroll
-        for (int t = 0; t < STEP; t++) acc[t % R] = xor4(acc[t % R], v[t]);
-    }
-    if (valid) {
-#pragma unroll
-        for (int g = 0; g < R; g++)
-            if ((recm >> g) & 1) st16(base + a.out_delta + (size_t)mrow[g] * stride, acc[g]);
-    }
-    return bad;
-#endif
 #pragma unroll
     for (int g = 0; g < R; g++) {
         const uint64_t gm = a.gmask[g];
@@ -548,26 +421,12 @@ __global__ __launch_bounds__(kBlock) void xor_encode_kernel(BatchArgs a) {
     }
 }
 
-// UO: input rows per load batch (0 = FECGPU_GF_U); 8 for windows in mapped
+// UO: input rows per load batch (0 = GF_ENC_U(R)); 8 for windows in mapped
 // host memory, where each batch of loads is a PCIe round trip.
 template <int R, bool FLAT, int UO = 0>
 __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
     const int k = a.k;
-#if FECGPU_ENC_SGPR
-    // kernel-uniform tables read through the constant address space with a
-    // wave-uniform index, i.e. scalar loads into SGPRs: no LDS traffic or
-    // latency in the multiply loop
-#if defined(__HIP_DEVICE_COMPILE__)
-    typedef __attribute__((address_space(4))) const uint4 *cptr4;
-    typedef __attribute__((address_space(4))) const uint32_t *cptr1;
-#else
-    typedef const uint4 *cptr4;
-    typedef const uint32_t *cptr1;
-#endif
-    const cptr4 tab = (cptr4)a.enc_ab;
-    const cptr1 tc = (cptr1)a.enc_c;
-#else
     extern __shared__ uint4 dyn[];
     uint4 *tab = dyn;
     uint32_t *tc = reinterpret_cast<uint32_t *>(dyn + k * R);
@@ -576,7 +435,6 @@ __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a
         tc[i] = a.enc_c[i];
     }
     __syncthreads();
-#endif
     if constexpr (FLAT) {
         for_flat_slots(a, [&](uint8_t *p, uint32_t stride, uint64_t w, uint32_t, bool valid) {
             gf_encode_slot<R, UO>(p, stride, k, tab, tc, valid, a.out_delta + w * a.out_wdelta);
@@ -680,11 +538,7 @@ inline constexpr Masks<K, R, M> kMasks{};
 // XOR over all sources' planes, undoes the shared combinations and keeps
 // planes of many sources live at once
 __device__ __forceinline__ uint32_t oxor(uint32_t a, uint32_t b) {
-#if FECGPU_BS_VOP2
-    return a ^ b;
-#else
     return __builtin_amdgcn_bitop3_b32(a, b, b, 0x3C);
-#endif
 }
 
 // output plane IP % 8 of repair IP / 8 takes source J's planes (compile time)
@@ -743,9 +597,8 @@ __device__ __forceinline__ void sources(const uint8_t *pa, const uint8_t *pb, ui
                                         uint32_t (&acc)[R][8]) {
     if constexpr (J0 < K) {
         batch<K, R, M, J0>(pa, pb, stride, acc, std::make_integer_sequence<int, ((K - J0) < U ? (K - J0) : U)>{});
-#if FECGPU_BS_SYNC
-        __syncthreads();  // keeps the workgroup's waves in one stretch of code
-#endif
+        // (no workgroup barrier per batch: the r01 knob for one was defined after
+        // its use and so never compiled in; every measurement ran without it)
         // advance opaquely, so the compiler does not keep K addresses live at once
         pa += U * stride;
         pb += U * stride;
@@ -756,51 +609,23 @@ __device__ __forceinline__ void sources(const uint8_t *pa, const uint8_t *pb, ui
 
 }  // namespace bs
 
-#ifndef FECGPU_BS_U
-#define FECGPU_BS_U 8  // bit-sliced encode, group mode: sources loaded per batch (8 > 4 > 2 by 1-3 % on cfg4, r01)
-#endif
-#ifndef FECGPU_BS_U_FLAT
-// bit-sliced encode, flat mode: sources loaded per batch (2 > 4 > 8: k32 r8
-// 4.72 / 4.60 / 4.59 TB/s at S = 1200, profiles/r01_bs_layout.txt)
-#define FECGPU_BS_U_FLAT 2
-#endif
-#ifndef FECGPU_BS_SYNC
-// bit-sliced encode: workgroup barrier after every batch, keeping the waves of a
-// workgroup in one stretch of the long straight-line code (+1-3 %, r01)
-#define FECGPU_BS_SYNC 1
-#endif
-#ifndef FECGPU_BS_VOP2
-#define FECGPU_BS_VOP2 0  // bit-sliced encode: plain (VOP2) XORs for combinations and single terms
-#endif
-
-#ifndef FECGPU_BS_FLAT
-// bit-sliced encode on uniform windows: one flat unit space over all windows
-// (no groups, so no partly idle last pass per group) instead of group mode:
-// S = 1200 k32 r8 3.84 -> 4.60 TB/s, k16 r8 4.01 -> 4.30
-// (profiles/r01_bs_layout.txt)
-#define FECGPU_BS_FLAT 1
-#endif
-#ifndef FECGPU_BS_ADJ
-// bit-sliced encode: a unit is two adjacent columns (2u, 2u + 1) instead of
-// u and u + h (A/B knob; 10-25 % slower: each load instruction then touches
-// every other 16 B of 2 KiB, profiles/r01_bs_layout.txt)
-#define FECGPU_BS_ADJ 0
-#endif
+// bit-sliced encode: sources loaded per batch.  Group mode 8 (> 4 > 2 by
+// 1-3 % on cfg4, r01); flat mode 2 (> 4 > 8: k32 r8 4.72 / 4.60 / 4.59 TB/s at
+// S = 1200, profiles/r01_bs_layout.txt).  Flat mode, one unit space over all
+// uniform windows, beat group mode there: S = 1200 k32 r8 3.84 -> 4.60 TB/s.
+constexpr int kBsU = 8, kBsUFlat = 2;
 
 namespace bs {
 
 // The two 16-B columns of unit u of a window with ncol columns (h = ceil(ncol / 2)
-// units).  Without a second column B repeats A: same inputs, same outputs, so
-// its stores rewrite A's bytes with equal values (no branch).
+// units): u and u + h, so each load instruction stays coalesced (two adjacent
+// columns per unit were 10-25 % slower, profiles/r01_bs_layout.txt).  Without
+// a second column B repeats A: same inputs, same outputs, so its stores
+// rewrite A's bytes with equal values (no branch).
 __device__ __forceinline__ void unit_cols(uint8_t *base, uint32_t u, uint32_t h, uint32_t ncol,
                                           uint8_t *&pa, uint8_t *&pb) {
-#if FECGPU_BS_ADJ
-    pa = base + u * 32u;
-    pb = 2 * u + 1 < ncol ? pa + 16 : pa;
-#else
     pa = base + u * 16u;
     pb = u + h < ncol ? pa + h * 16u : pa;
-#endif
 }
 
 // one unit: every source's planes into the R x 8 output planes (U sources
@@ -842,7 +667,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
             const uint32_t u = (uint32_t)(s - w * h);
             uint8_t *pa, *pb;
             bs::unit_cols(a.win + w * a.wpitch, u, h, ncol, pa, pb);
-            bs::unit<K, R, M, FECGPU_BS_U_FLAT>(pa, pb, a.stride, live, a.out_delta + w * a.out_wdelta);
+            bs::unit<K, R, M, kBsUFlat>(pa, pb, a.stride, live, a.out_delta + w * a.out_wdelta);
         }
         return;
     } else {
@@ -864,7 +689,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
                 uint8_t *pa, *pb;
                 bs::unit_cols(reinterpret_cast<uint8_t *>(g.base[wl]), s - g.pfx[wl], g.pfx[wl + 1] - g.pfx[wl],
                               g.ncol[wl], pa, pb);
-                bs::unit<K, R, M, FECGPU_BS_U>(pa, pb, g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
+                bs::unit<K, R, M, kBsU>(pa, pb, g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
             }
             __syncthreads();
         }
@@ -875,16 +700,12 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
 // The bit-sliced encode for a matrix known only at run time (RLC rows, and
 // every (k, r) without a compiled kernel): the same planes, combinations and
 // 3-input XORs as bs::, with each output plane's pick of lo[] / hi[] read from
-// a per-code mask table (a.enc_bs: byte (j, i, p) = lo | hi << 4, the input
-// planes of source j feeding plane p of repair i) through scalar loads.  The
-// wave-uniform index selects a combination by relative VGPR addressing
-// (s_set_gpr_idx_on / v_mov / off), so an output plane costs 3 VALU ops and a
-// few SALU ops where the table multiply spends 3 v_perm + XOR per dword and
-// repair.  Bytes equal the table multiply's (tests/test_gpu_parity.py).
-#ifndef FECGPU_RBS_U
-#define FECGPU_RBS_U 1  // runtime bit-sliced encode: sources loaded per batch (1 > 2 = 4 by 1-2 %, cfg4 rlc)
-#endif
-
+// a per-code index table (a.enc_bs, fec_capi.cpp rbs_masks) through scalar
+// loads.  The wave-uniform index selects a combination by relative VGPR
+// addressing (s_set_gpr_idx_on / _idx / _off, M0[7:0] = index), so an output
+// plane costs 2 VALU ops and a few SALU ops where the table multiply spends
+// 3 v_perm + XOR per dword and repair.  Bytes equal the table multiply's
+// (tests/test_gpu_parity.py).
 namespace rbs {
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -893,202 +714,26 @@ typedef __attribute__((address_space(4))) const uint32_t *cmask;
 typedef const uint32_t *cmask;
 #endif
 
-#ifndef FECGPU_RBS_FUSE
-// 1: the lo pick is the XOR's own indexed source operand (2 VALU per output
-// plane); 0: both picks by v_mov, then the XOR (3 VALU)
-#define FECGPU_RBS_FUSE 1
-#endif
-
-// a[q] ^= lo[d[q] & 0xff] ^ hi[d[q] >> 8] for four output planes q, where
-// d[q] (wave-uniform, SGPR) packs the plane's lo / hi indices.  Relative VGPR
-// addressing (s_set_gpr_idx_on / _idx / _off, M0[7:0] = index) needs each
-// table in consecutive registers, so lo / hi are pinned to v32-v47 / v48-v63 by
-// register constraints (the same registers in every block, so no copies), and
-// one asm block holds the picks and XORs: the compiler's own lowering of
-// lo[i] hoists every pick of a source ahead of the XORs and holds 128 of them
-// in VGPRs at once (251 VGPRs, 2 waves per SIMD).  Index mode stays on across
-// the block and only instructions whose source 0 is a table run in it.
-#define RBS_IN(A, N, R0) "{v" #R0 "}"(A[N])
-#if FECGPU_RBS_WIDE
-#define RBS_HI(Q) "s_set_gpr_idx_idx %[h" #Q "]\n\t"
-#define RBS_LO(Q) "s_set_gpr_idx_idx %[d" #Q "]\n\t"
-#else
-#define RBS_HI(Q) "s_lshr_b32 %[h], %[d" #Q "], 8\n\ts_set_gpr_idx_idx %[h]\n\t"
-#define RBS_LO(Q) "s_set_gpr_idx_idx %[d" #Q "]\n\t"
-#endif
-#ifndef FECGPU_RBS_PAIR
-#define FECGPU_RBS_PAIR 1  // 1: two planes' hi picks, then their lo picks + XORs (more distance per dependency)
-#endif
-#define RBS_PAIR(Q0, Q1)                                 \
-    RBS_HI(Q0) "v_mov_b32 %[t0], v48\n\t"                \
-    RBS_HI(Q1) "v_mov_b32 %[t1], v48\n\t"                \
-    RBS_LO(Q0) "v_bitop3_b32 %[a" #Q0 "], v32, %[a" #Q0 "], %[t0] bitop3:0x96\n\t" \
-    RBS_LO(Q1) "v_bitop3_b32 %[a" #Q1 "], v32, %[a" #Q1 "], %[t1] bitop3:0x96\n\t"
-#if FECGPU_RBS_FUSE
-#define RBS_PLANE(Q, T)                                  \
-    RBS_HI(Q)                                            \
-    "v_mov_b32 %[" #T "], v48\n\t"                       \
-    RBS_LO(Q)                                            \
-    "v_bitop3_b32 %[a" #Q "], v32, %[a" #Q "], %[" #T "] bitop3:0x96\n\t"
-#else
-#define RBS_PLANE(Q, T)                                  \
-    RBS_HI(Q)                                            \
-    "v_mov_b32 %[" #T "], v48\n\t"                       \
-    RBS_LO(Q)                                            \
-    "v_mov_b32 %[u], v32\n\t"                            \
-    "s_set_gpr_idx_off\n\t"                              \
-    "v_bitop3_b32 %[a" #Q "], %[u], %[a" #Q "], %[" #T "] bitop3:0x96\n\t" \
-    "s_set_gpr_idx_on %[d" #Q "], gpr_idx(SRC0)\n\t"
-#endif
-// M0 is a reserved register: clang warns that declaring it clobbered is not a
-// promise it will be preserved, but the declaration still puts an implicit def
-// of M0 on the asm, so no M0 def/use pair of the compiler's is scheduled across it
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void pick4(uint32_t &a0, uint32_t &a1, uint32_t &a2, uint32_t &a3,
-                                      const uint32_t (&d)[4], const uint32_t (&e)[4], const uint32_t (&lo)[16],
-                                      const uint32_t (&hi)[16]) {
-    uint32_t t0, t1, u, h;
-    asm("s_set_gpr_idx_on %[d0], gpr_idx(SRC0)\n\t"
-#if FECGPU_RBS_PAIR && FECGPU_RBS_FUSE
-        RBS_PAIR(0, 1) RBS_PAIR(2, 3)
-#else
-        RBS_PLANE(0, t0) RBS_PLANE(1, t1) RBS_PLANE(2, t0) RBS_PLANE(3, t1)
-#endif
-        "s_set_gpr_idx_off"
-        : [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2), [a3] "+v"(a3), [t0] "=&v"(t0), [t1] "=&v"(t1),
-          [u] "=&v"(u), [h] "=&s"(h)
-        : [d0] "s"(d[0]), [d1] "s"(d[1]), [d2] "s"(d[2]), [d3] "s"(d[3]),
-          [h0] "s"(e[0]), [h1] "s"(e[1]), [h2] "s"(e[2]), [h3] "s"(e[3]),
-          RBS_IN(lo, 0, 32), RBS_IN(lo, 1, 33), RBS_IN(lo, 2, 34), RBS_IN(lo, 3, 35),
-          RBS_IN(lo, 4, 36), RBS_IN(lo, 5, 37), RBS_IN(lo, 6, 38), RBS_IN(lo, 7, 39),
-          RBS_IN(lo, 8, 40), RBS_IN(lo, 9, 41), RBS_IN(lo, 10, 42), RBS_IN(lo, 11, 43),
-          RBS_IN(lo, 12, 44), RBS_IN(lo, 13, 45), RBS_IN(lo, 14, 46), RBS_IN(lo, 15, 47),
-          RBS_IN(hi, 0, 48), RBS_IN(hi, 1, 49), RBS_IN(hi, 2, 50), RBS_IN(hi, 3, 51),
-          RBS_IN(hi, 4, 52), RBS_IN(hi, 5, 53), RBS_IN(hi, 6, 54), RBS_IN(hi, 7, 55),
-          RBS_IN(hi, 8, 56), RBS_IN(hi, 9, 57), RBS_IN(hi, 10, 58), RBS_IN(hi, 11, 59),
-          RBS_IN(hi, 12, 60), RBS_IN(hi, 13, 61), RBS_IN(hi, 14, 62), RBS_IN(hi, 15, 63)
-        : "m0", "scc");  // index mode writes M0; s_lshr (packed indices) writes SCC
-}
-#pragma clang diagnostic pop
-#undef RBS_IN
-#undef RBS_PLANE
-#undef RBS_HI
-#undef RBS_LO
-#undef RBS_PAIR
-
-// acc ^= source planes x times the source's mask row mk ([R][8][kRbsPlaneDw] dwords)
-template <int R>
-__device__ __forceinline__ void source(const uint32_t (&x)[8], uint32_t (&acc)[R][8], cmask mk) {
-    uint32_t lo[16], hi[16];
-    lo[0] = hi[0] = 0;
-    asm volatile("" : "+v"(lo[0]), "+v"(hi[0]));  // opaque zeros (no re-materialisation per block)
-#pragma unroll
-    for (int s = 1; s < 16; s++) {
-        const int b = __builtin_ctz(s), rest = s & (s - 1);
-        lo[s] = rest ? bs::oxor(lo[rest], x[b]) : x[b];
-        hi[s] = rest ? bs::oxor(hi[rest], x[4 + b]) : x[4 + b];
-    }
-#pragma unroll
-    for (int i = 0; i < R; i++)
-#pragma unroll
-        for (int w = 0; w < 2; w++) {
-            const cmask m = mk + (i * 8 + w * 4) * kRbsPlaneDw;
-            uint32_t d[4], e[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                d[q] = m[q * kRbsPlaneDw];
-                e[q] = m[q * kRbsPlaneDw + kRbsPlaneDw - 1];  // unused when packed
-            }
-            uint32_t(&c)[8] = acc[i];
-            pick4(c[w * 4], c[w * 4 + 1], c[w * 4 + 2], c[w * 4 + 3], d, e, lo, hi);
-        }
-#pragma unroll
-    for (int i = 0; i < R; i++)
-#pragma unroll
-        for (int p = 0; p < 8; p++) asm volatile("" : "+v"(acc[i][p]));
-}
-
-template <int R, int U>
-__device__ __forceinline__ void unit(uint8_t *pa, uint8_t *pb, uint32_t stride, int k, cmask mk,
-                                     bool live, uint64_t od) {
-    uint32_t acc[R][8];
-#pragma unroll
-    for (int i = 0; i < R; i++)
-#pragma unroll
-        for (int p = 0; p < 8; p++) acc[i][p] = 0;
-    const uint8_t *qa = pa, *qb = pb;
-    for (int j0 = 0; j0 < k; j0 += U) {
-        uint32_t x[U][8];
-#pragma unroll
-        for (int t = 0; t < U; t++) {
-            // past k (k % U != 0): reload the last source, masked out below
-            const uint32_t off = (uint32_t)min(t, k - 1 - j0) * stride;
-            const uint4 va = ld16(qa + off), vb = ld16(qb + off);
-            x[t][0] = va.x; x[t][1] = va.y; x[t][2] = va.z; x[t][3] = va.w;
-            x[t][4] = vb.x; x[t][5] = vb.y; x[t][6] = vb.z; x[t][7] = vb.w;
-        }
-#pragma unroll
-        for (int t = 0; t < U; t++) {
-            if (t == 0 || j0 + t < k) {  // uniform
-                bs::tr8(x[t]);
-                source<R>(x[t], acc, mk + (size_t)(j0 + t) * (R * 8 * kRbsPlaneDw));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        qa += U * stride;
-        qb += U * stride;
-        asm volatile("" : "+v"(qa), "+v"(qb));
-    }
-#pragma unroll
-    for (int i = 0; i < R; i++) {
-        bs::tr8(acc[i]);
-        if (live) {
-            st16(pa + od + (size_t)(k + i) * stride, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
-            st16(pb + od + (size_t)(k + i) * stride, make_uint4(acc[i][4], acc[i][5], acc[i][6], acc[i][7]));
-        }
-    }
-}
-
 }  // namespace rbs
 
-// Four-column units (FECGPU_RBS_COLS = 4): a lane takes 64 byte positions,
-// so each output plane is a dword pair and one pair of index sets serves
-// 64 bytes instead of 32 (half the index-mode switches per byte, at ~240
-// VGPRs: 2 waves per SIMD).  lo / hi entries are pairs pinned at v32-v63 /
-// v64-v95 (entry s at v[32 + 2s : 33 + 2s]), so the table holds 2 x index.
+// Four-column units: a lane takes 64 byte positions, so each output plane is
+// a dword pair and one pair of index sets serves 64 bytes (two-column units,
+// 32 bytes per index pair, measured 16 % slower on cfg4 RLC, r02; removed r05)
+// at ~240 VGPRs: 2 waves per SIMD.  lo / hi entries are pairs pinned at
+// v32-v63 / v64-v95 (entry s at v[32 + 2s : 33 + 2s]), so the table holds
+// 2 x index, a byte per index, two planes per dword (k48 r8 0.497 -> 0.321 ms
+// against a dword per plane: the table stays in the scalar cache, r02).  The
+// compiler's own lowering of lo[i] hoists every pick of a source ahead of the
+// XORs (251 VGPRs), so one asm block holds the picks and XORs; M0 is declared
+// clobbered, which puts an implicit def of M0 on the asm so no M0 def / use
+// pair of the compiler's is scheduled across it.
 namespace rbs4 {
 
 using rbs::cmask;
 
 #define R4_IN(A, N, R0) "{v" #R0 "}"(A[N])
-#if FECGPU_RBS4_PACK  // l[q] = lo x 2 | hi x 2 << 16: M0[7:0] takes the low byte
-#define R4_HI(Q) "s_lshr_b32 %[t], %[l" #Q "], 16\n\ts_set_gpr_idx_idx %[t]\n\t"
-#define R4_ON "s_lshr_b32 %[t], %[l0], 16\n\ts_set_gpr_idx_on %[t], gpr_idx(SRC0)\n\t"
-#else
-#define R4_HI(Q) "s_set_gpr_idx_idx %[h" #Q "]\n\t"
-#define R4_ON "s_set_gpr_idx_on %[h0], gpr_idx(SRC0)\n\t"
-#endif
-#define R4_PAIR(Q0, Q1, TA, TB)                                                 \
-    R4_HI(Q0)                                                                   \
-    "v_mov_b64 v[" #TA ":" #TB "], v[64:65]\n\t"                               \
-    "s_set_gpr_idx_idx %[l" #Q0 "]\n\t"                                        \
-    "v_bitop3_b32 %[a" #Q0 "], v32, %[a" #Q0 "], v" #TA " bitop3:0x96\n\t"      \
-    "v_bitop3_b32 %[b" #Q0 "], v33, %[b" #Q0 "], v" #TB " bitop3:0x96\n\t"      \
-    R4_HI(Q1)                                                                   \
-    "v_mov_b64 v[" #TA ":" #TB "], v[64:65]\n\t"                               \
-    "s_set_gpr_idx_idx %[l" #Q1 "]\n\t"                                        \
-    "v_bitop3_b32 %[a" #Q1 "], v32, %[a" #Q1 "], v" #TA " bitop3:0x96\n\t"      \
-    "v_bitop3_b32 %[b" #Q1 "], v33, %[b" #Q1 "], v" #TB " bitop3:0x96\n\t"
-
-// planes q = 0..3 of one repair half: (a[q], b[q]) ^= lo[l[q]] ^ hi[h[q]]
-// (M0 declared clobbered as in rbs::pick4)
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void pick4(uint32_t (&a)[4], uint32_t (&b)[4], const uint32_t (&l)[4],
-                                      const uint32_t (&h)[4], const uint32_t (&lo)[32], const uint32_t (&hi)[32]) {
-    uint32_t t;  // packed indices: the index shifted down
-#if FECGPU_RBS4_PACK == 2  // l[0] = planes 0, 1 and l[1] = planes 2, 3, a byte per index
+// planes QA, QB of one repair half from the index dword D (a byte per index:
+// QA's hi, lo at bits 8, 0; QB's at 24, 16): (a[q], b[q]) ^= lo[l] ^ hi[h]
 #define R4_B(D, QA, QB, TA, TB)                                                 \
     "s_lshr_b32 %[t], %[" D "], 8\n\ts_set_gpr_idx_idx %[t]\n\t"               \
     "v_mov_b64 v[" #TA ":" #TB "], v[64:65]\n\t"                               \
@@ -1100,19 +745,19 @@ __device__ __forceinline__ void pick4(uint32_t (&a)[4], uint32_t (&b)[4], const 
     "s_lshr_b32 %[t], %[" D "], 16\n\ts_set_gpr_idx_idx %[t]\n\t"              \
     "v_bitop3_b32 %[a" #QB "], v32, %[a" #QB "], v" #TA " bitop3:0x96\n\t"      \
     "v_bitop3_b32 %[b" #QB "], v33, %[b" #QB "], v" #TB " bitop3:0x96\n\t"
+
+// planes q = 0..3 of one repair half: (a[q], b[q]) ^= lo[.] ^ hi[.], indices l[0..1]
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void pick4(uint32_t (&a)[4], uint32_t (&b)[4], const uint32_t (&l)[2],
+                                      const uint32_t (&lo)[32], const uint32_t (&hi)[32]) {
+    uint32_t t;  // an index shifted down
     asm("s_set_gpr_idx_on %[l0], gpr_idx(SRC0)\n\t"  // any index: the first set below replaces it
         R4_B("l0", 0, 1, 96, 97) R4_B("l1", 2, 3, 98, 99)
         "s_set_gpr_idx_off"
-#undef R4_B
-#else
-    asm(R4_ON
-        R4_PAIR(0, 1, 96, 97) R4_PAIR(2, 3, 98, 99)
-        "s_set_gpr_idx_off"
-#endif
         : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]),
           [b0] "+v"(b[0]), [b1] "+v"(b[1]), [b2] "+v"(b[2]), [b3] "+v"(b[3]), [t] "=&s"(t)
-        : [l0] "s"(l[0]), [l1] "s"(l[1]), [l2] "s"(l[2]), [l3] "s"(l[3]),
-          [h0] "s"(h[0]), [h1] "s"(h[1]), [h2] "s"(h[2]), [h3] "s"(h[3]),
+        : [l0] "s"(l[0]), [l1] "s"(l[1]),
           R4_IN(lo, 0, 32), R4_IN(lo, 1, 33), R4_IN(lo, 2, 34), R4_IN(lo, 3, 35),
           R4_IN(lo, 4, 36), R4_IN(lo, 5, 37), R4_IN(lo, 6, 38), R4_IN(lo, 7, 39),
           R4_IN(lo, 8, 40), R4_IN(lo, 9, 41), R4_IN(lo, 10, 42), R4_IN(lo, 11, 43),
@@ -1133,12 +778,10 @@ __device__ __forceinline__ void pick4(uint32_t (&a)[4], uint32_t (&b)[4], const 
 }
 #pragma clang diagnostic pop
 #undef R4_IN
-#undef R4_PAIR
-#undef R4_HI
-#undef R4_ON
+#undef R4_B
 
 // acc ^= one source (planes xa of columns 0-1, xb of columns 2-3) times its
-// mask row mk ([R][2][kRbsDw4] dwords: lo, hi indices x 2, or packed)
+// index row mk ([R][2][kRbsDw4] dwords)
 template <int R>
 __device__ __forceinline__ void source(const uint32_t (&xa)[8], const uint32_t (&xb)[8], uint32_t (&aa)[R][8],
                                        uint32_t (&ab)[R][8], cmask mk) {
@@ -1160,20 +803,10 @@ __device__ __forceinline__ void source(const uint32_t (&xa)[8], const uint32_t (
 #pragma unroll
         for (int w = 0; w < 2; w++) {
             const cmask m = mk + (i * 2 + w) * kRbsDw4;
-            uint32_t l[4], h[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (kRbsDw4 == 2) {  // two dwords for the 4 planes (l[2], l[3], h unused)
-                    l[q] = q < 2 ? m[q] : 0u;
-                    h[q] = l[q];
-                } else {
-                    l[q] = m[q * kRbsPlaneDw];
-                    h[q] = m[q * kRbsPlaneDw + kRbsPlaneDw - 1];  // = l[q] when packed (unused)
-                }
-            }
+            const uint32_t l[2] = {m[0], m[1]};  // two dwords for the 4 planes
             uint32_t(&ca)[4] = *reinterpret_cast<uint32_t(*)[4]>(&aa[i][w * 4]);
             uint32_t(&cb)[4] = *reinterpret_cast<uint32_t(*)[4]>(&ab[i][w * 4]);
-            pick4(ca, cb, l, h, lo, hi);
+            pick4(ca, cb, l, lo, hi);
         }
 #pragma unroll
     for (int i = 0; i < R; i++)
@@ -1240,27 +873,17 @@ __device__ __forceinline__ void unit_cols(uint8_t *base, uint32_t u, uint32_t h,
 
 // Unit spaces as gf_encode_bs_kernel (flat over uniform windows, group mode
 // otherwise); the masks are the code's, R = its r.
-#ifndef FECGPU_RBS_MINW
-#define FECGPU_RBS_MINW 4  // runtime bit-sliced encode: waves per SIMD asked of the register allocator
-#endif
 template <int R, bool FLAT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kRbsCols == 4 ? 1 : FECGPU_RBS_MINW, 8)))
-void gf_encode_rbs_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kBlock) void gf_encode_rbs_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
     const rbs::cmask mk = (rbs::cmask)a.enc_bs;
     const int k = a.k;
     constexpr uint32_t C = kRbsCols;  // columns per unit
     // one unit of window base (units h, columns ncol)
     auto run = [&](uint8_t *base, uint32_t u, uint32_t h, uint32_t ncol, uint32_t stride, bool live, uint64_t od) {
-        if constexpr (C == 4) {
-            uint8_t *pc[4];
-            rbs4::unit_cols(base, u, h, ncol, pc);
-            rbs4::unit<R>(pc, stride, k, mk, live, od);
-        } else {
-            uint8_t *pa, *pb;
-            bs::unit_cols(base, u, h, ncol, pa, pb);
-            rbs::unit<R, FECGPU_RBS_U>(pa, pb, stride, k, mk, live, od);
-        }
+        uint8_t *pc[4];
+        rbs4::unit_cols(base, u, h, ncol, pc);
+        rbs4::unit<R>(pc, stride, k, mk, live, od);
     };
     if constexpr (FLAT) {
         const uint32_t ncol = a.ncol, h = (ncol + C - 1) / C;
@@ -1472,13 +1095,10 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, uint64_t pres, int lane,
     // D[u][q] for idx = u*k + q; every __shfl with the whole wave active
     for (int base = 0; base < e * k; base += 64) {
         const int idx = base + lane;
-#if FECGPU_PLAN_TP
         // idx = dq * e + du: consecutive lanes write consecutive table entries
-        // (lanes along dq put 4 lanes of every 8 on the same LDS banks)
+        // (lanes along dq put 4 lanes of every 8 on the same LDS banks:
+        // SQ_LDS_BANK_CONFLICT 7.3e6 -> 0.52e6 on cfg3, r03)
         const int dq = idx / e, du = idx - dq * e;
-#else
-        const int du = idx / k, dq = idx - du * k;
-#endif
         const int Au = __shfl(A, du & 63, 64);
         const int Kq = __shfl(K, dq & 63, 64);
         const int z = __shfl(zq, dq & 63, 64);
@@ -1497,108 +1117,13 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, uint64_t pres, int lane,
     }
 }
 
-// The previous Gauss-Jordan plan, kept as an A/B knob (FECGPU_PLAN_GJ=1).
+// GF(2^8) multiply / inverse through the LDS copies of the exp / log tables
 __device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t *ex, const uint8_t *lg, uint32_t x,
                                                uint32_t y) {
     return (x && y) ? ex[lg[x] + lg[y]] : 0u;
 }
 __device__ __forceinline__ uint32_t gf_inv_lds(const uint8_t *ex, const uint8_t *lg, uint32_t x) {
     return ex[255 - lg[x]];
-}
-
-template <int R>
-__device__ void plan_gf_gj(const BatchArgs &a, uint64_t w, int lane, uint8_t *region,
-                           const uint8_t *ex, const uint8_t *lg, uint8_t &ne_out) {
-    const int k = a.k, r = a.r;
-    const DecRegion<R> rg(region, k);
-    uint8_t *insym = rg.insym, *outsym = rg.outsym;
-    const uint64_t kmask = (k >= 64) ? ~0ull : ((1ull << k) - 1);
-    const uint64_t pres = a.present[w];
-    const uint64_t miss = ~pres & kmask;
-    const uint64_t rep = (pres >> k) & ((1ull << r) - 1);
-    const int e = __popcll(miss);
-    if (e == 0 || __popcll(rep) < e || e > R) {
-        if (lane == 0) {
-            ne_out = 0;
-            a.status[w] = (e == 0) ? 0 : 1;
-        }
-        return;
-    }
-    // u-th missing source / t-th present repair for lane u, t < e
-    uint64_t mm = miss, rr = rep;
-    for (int i = 0; i < lane && i < e; i++) { mm &= mm - 1; rr &= rr - 1; }
-    const int my_m = (int)__ffsll((unsigned long long)mm) - 1;  // valid for lane < e
-    const int my_sel = (int)__ffsll((unsigned long long)rr) - 1;
-    // input list: received sources ascending, then the e chosen repairs
-    if (lane < k && ((pres >> lane) & 1)) insym[__popcll(pres & kmask & ((1ull << lane) - 1))] = (uint8_t)lane;
-    if (lane < e) {
-        insym[k - e + lane] = (uint8_t)(k + my_sel);
-        outsym[lane] = (uint8_t)my_m;
-    }
-    // [A | I], A[t][u] = inv((k + sel_t) ^ m_u); lane = t*8 + u.  Every
-    // __shfl below runs with the whole wave active: ds_bpermute returns 0 for
-    // a source lane that is masked off, so no shuffle sits inside a branch.
-    const int t = lane >> 3, u = lane & 7;
-    const int sel_t = __shfl(my_sel, t & 7, 64);
-    const int m_u = __shfl(my_m, u, 64);
-    const bool valid = (t < e) && (u < e);
-    uint32_t xl = valid ? gf_inv_lds(ex, lg, (uint32_t)((k + sel_t) ^ m_u)) : 0u;
-    uint32_t xr = (valid && t == u) ? 1u : 0u;
-    bool singular = false;
-    for (int c = 0; c < e; c++) {
-        const uint32_t piv = __shfl(xl, c * 8 + c, 64);
-        if (piv == 0) { singular = true; break; }  // never for Cauchy (leading minors are Cauchy)
-        const uint32_t ip = gf_inv_lds(ex, lg, piv);
-        if (t == c) {
-            xl = gf_mul_lds(ex, lg, xl, ip);
-            xr = gf_mul_lds(ex, lg, xr, ip);
-        }
-        const uint32_t f = __shfl(xl, (t & 7) * 8 + c, 64);
-        const uint32_t rl = __shfl(xl, c * 8 + u, 64);
-        const uint32_t rq = __shfl(xr, c * 8 + u, 64);
-        if (t != c && valid) {
-            xl ^= gf_mul_lds(ex, lg, f, rl);
-            xr ^= gf_mul_lds(ex, lg, f, rq);
-        }
-    }
-    if (singular) {
-        if (lane == 0) { ne_out = 0; a.status[w] = 1; }
-        return;
-    }
-    WAVE_SYNC();
-    // D[u][q] for idx = u*k + q; Ainv[u][t] = xr of lane u*8 + t.
-    const int kr = k - e;
-    for (int base = 0; base < e * k; base += 64) {
-        const int idx = base + lane;
-#if FECGPU_PLAN_TP
-        // idx = dq * e + du: consecutive lanes write consecutive table entries
-        // (lanes along dq put 4 lanes of every 8 on the same LDS banks)
-        const int dq = idx / e, du = idx - dq * e;
-#else
-        const int du = idx / k, dq = idx - du * k;
-#endif
-        const bool live = idx < e * k;
-        const bool is_src = dq < kr;
-        const uint32_t j = (live && is_src) ? insym[dq] : 0u;
-        uint32_t csrc = 0;
-        for (int tt = 0; tt < e; tt++) {
-            const uint32_t ai = __shfl(xr, ((du & 7) * 8 + tt) & 63, 64);
-            const int st = __shfl(my_sel, tt, 64);
-            if (is_src) csrc ^= gf_mul_lds(ex, lg, ai, gf_inv_lds(ex, lg, (uint32_t)((k + st) ^ j)));
-        }
-        const uint32_t crep = __shfl(xr, ((du & 7) * 8 + (is_src ? 0 : dq - kr)) & 63, 64);
-        const uint32_t c = is_src ? csrc : crep;
-        if (live) {
-            const CoefTab ct = make_coef_tab(c);
-            rg.ab[dq * R + du] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
-            rg.tc[dq * DecRegion<R>::R4 + du] = ct.c;
-        }
-    }
-    plan_offsets<R>(a, w, lane, rg, e);
-    if (lane == 0) {
-        ne_out = (uint8_t)e;
-        a.status[w] = 0;
-    }
 }
 
 // General-matrix plan (FECGPU_MATRIX_VANDERMONDE, FECGPU_MATRIX_RLC, any
@@ -1676,13 +1201,10 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
     // D[u][q] for idx = u*k + q; Ainv'[u][c] = T[P_u][P_c] = xr of lane P_u*8 + P_c
     for (int base = 0; base < e * k; base += 64) {
         const int idx = base + lane;
-#if FECGPU_PLAN_TP
         // idx = dq * e + du: consecutive lanes write consecutive table entries
-        // (lanes along dq put 4 lanes of every 8 on the same LDS banks)
+        // (lanes along dq put 4 lanes of every 8 on the same LDS banks:
+        // SQ_LDS_BANK_CONFLICT 7.3e6 -> 0.52e6 on cfg3, r03)
         const int dq = idx / e, du = idx - dq * e;
-#else
-        const int du = idx / k, dq = idx - du * k;
-#endif
         const bool live = idx < e * k;
         const bool is_src = dq < kr;
         const uint32_t j = (live && is_src) ? insym[dq] : 0u;
@@ -1718,7 +1240,7 @@ template <int R, int NE, int OFF = 0>
 __device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t out_delta,
                                          const DecRegion<R> &rg) {
     static_assert(OFF % 4 == 0 && OFF + NE <= R, "output range");
-    constexpr int U = FECGPU_GFD_U, R4 = DecRegion<R>::R4;
+    constexpr int U = kGfdU, R4 = DecRegion<R>::R4;
     static_assert(U == 2 || U == 4 || U == 8, "row offsets are padded to 8 rows");
     uint4 acc[NE];
 #pragma unroll
@@ -1738,31 +1260,9 @@ __device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t 
         }
 #pragma unroll
         for (int t = 0; t < U; t++) v[t] = ld16(base + ro[t]);
-        int t0 = 0;
-#if GF_PAIR_DEC
-#pragma unroll
-        for (int t = 0; t + 1 < U; t += 2) {
-            if (q0 + t + 1 < k) {
-                const Split s0 = split(v[t]), s1 = split(v[t + 1]);
-                const int q = q0 + t;
-                uint32_t c0[R4], c1[R4];
-#pragma unroll
-                for (int j = 0; j < (NE + 3) / 4; j++) {
-                    const uint4 x = *reinterpret_cast<const uint4 *>(rg.tc + q * R4 + OFF + 4 * j);
-                    const uint4 y = *reinterpret_cast<const uint4 *>(rg.tc + (q + 1) * R4 + OFF + 4 * j);
-                    c0[4 * j] = x.x; c0[4 * j + 1] = x.y; c0[4 * j + 2] = x.z; c0[4 * j + 3] = x.w;
-                    c1[4 * j] = y.x; c1[4 * j + 1] = y.y; c1[4 * j + 2] = y.z; c1[4 * j + 3] = y.w;
-                }
-#pragma unroll
-                for (int m = 0; m < NE; m++)
-                    gmac2(acc[m], s0, s1, rg.ab[q * R + OFF + m], c0[m], rg.ab[(q + 1) * R + OFF + m], c1[m]);
-                t0 = t + 2;
-            }
-        }
-#endif
 #pragma unroll
         for (int t = 0; t < U; t++) {
-            if (t >= t0 && q0 + t < k) {
+            if (q0 + t < k) {
                 const int q = q0 + t;
                 const Split sp = split(v[t]);
                 uint32_t c[R4];
@@ -1781,33 +1281,20 @@ __device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t 
         if (OFF + m < ne) st16(base + out_delta + rg.ooff[OFF + m], acc[m]);
 }
 
-#ifndef FECGPU_GFD_SPLIT
-// GF decode of more than 4 outputs per wave: two passes over the inputs (outputs
-// 0-3, then the rest; the second reads the rows from L2), so the kernel keeps
-// the 4-output register footprint (R = 8: 155 -> 122 VGPRs, 3 -> 4 waves/SIMD).
-// Off: in-process A/B (profiles/r03_gf_decode_ab.txt) the second pass costs
-// more than the extra wave gains (cfg4 decode 4.68 vs 4.56 ms, e = 8 rows -7 %)
-#define FECGPU_GFD_SPLIT 0
-#endif
 
 template <int R, int NE = R>
 __device__ __forceinline__ void dec_dispatch(int nw, uint8_t *base, int k, int ne, uint64_t out_delta,
                                              const DecRegion<R> &rg) {
+    // (two passes of 4 outputs at R = 8, for 4 waves per SIMD instead of 3:
+    // the second pass's reads cost more than the wave gained, r03)
     if constexpr (NE >= 1) {
-        if constexpr (FECGPU_GFD_SPLIT && NE > 4) {
-            if (nw == NE) {
-                dec_slot<R, 4, 0>(base, k, ne, out_delta, rg);
-                dec_slot<R, NE - 4, 4>(base, k, ne, out_delta, rg);
-                return;
-            }
-        }
         if (nw == NE) dec_slot<R, NE>(base, k, ne, out_delta, rg);
         else dec_dispatch<R, NE - 1>(nw, base, k, ne, out_delta, rg);
     }
 }
 
 template <int R>
-__global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
     extern __shared__ uint4 dyn[];
     __shared__ uint8_t s_exp[512];
@@ -1828,10 +1315,6 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
         const uint64_t w0 = xr.cur * a.wpb;
         const int nb = (int)min((uint64_t)a.wpb, a.nwin - w0);
         group_geometry(a, g, w0, nb);
-#if FECGPU_PLAN_GJ
-        for (int wl = wave; wl < nb; wl += kBlock / 64)
-            plan_gf_gj<R>(a, w0 + wl, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log, s_ne[wl]);
-#else
         {
             // this wave plans windows wave, wave + 4, ...: their masks in one load
             // (prefetching the next group's masks in persistent workgroups did
@@ -1851,7 +1334,6 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
                                s_ne[wl]);
             }
         }
-#endif
         __syncthreads();
         if (tid < 64) {
             // Windows in descending order of e (ties by index): a wave's first
@@ -1875,7 +1357,6 @@ __global__ __launch_bounds__(kBlock) GFD_WAVES void gf_decode_kernel(BatchArgs a
             block_prefix(g.pfx, (t < nb && s_ne[wl]) ? g.ncol[wl] : 0u, t);
         }
         __syncthreads();
-        if (FECGPU_DEC_PLANONLY) continue;
         const uint32_t total = g.pfx[nb];
         int i = 0;
         for (uint32_t s = tid; s < total; s += kBlock) {
@@ -2009,22 +1490,11 @@ __global__ __launch_bounds__(kBlock) void digest_kernel(DigestArgs a) {
 // the device (one lane per repair), the decode's linked systems are reduced
 // by one wave each (Gauss-Jordan with pivot search).
 
-#ifndef FECGPU_COMB_U
 // combine kernel: input rows loaded per batch.  One output (repairs,
 // syndromes): 16 (sliding-window encode k 8 W 32: 0.370 vs 0.387 ms at 8,
-// 0.466 at 4; profiles/r02_sw_ab.txt); solves (8 outputs, register-bound): 8.
-#ifndef FECGPU_COMB_U_GRP
-#define FECGPU_COMB_U_GRP 8  // grouped encode jobs (R = 2, 4)
-#endif
-#define FECGPU_COMB_U (R == 1 ? 16 : R == 8 ? 8 : FECGPU_COMB_U_GRP)
-#endif
-
-#ifndef FECGPU_COMB_SKIP
-// combine kernel: skip the multiply-accumulates of zero coefficients (a
-// wave-uniform test per input row and output; grouped sliding-window encode
-// jobs are zero outside each repair's window)
-#define FECGPU_COMB_SKIP 1
-#endif
+// 0.466 at 4; profiles/r02_sw_ab.txt); solves (8 outputs, register-bound) and
+// grouped encode jobs (2, 4 outputs): 8.
+#define COMB_U(R) ((R) == 1 ? 16 : 8)
 
 // Per-job LDS region of comb_kernel<R>: tables [nin_max][R] uint4 (TA/TB),
 // [nin_max][RT] u32 (TC), output column-0 pointers [R], xor pointer, and per
@@ -2060,34 +1530,21 @@ struct CombRegion {
     }
 };
 
-// Input rows of a combine slot: global pointers (row 0 of this lane's column),
-// or — CombArgs::in_bytes below 4 GiB — a buffer resource over the whole input
-// region with this lane's column offset and the row offset a scalar: no 64-bit
-// address arithmetic per row on the vector ALU, and a row past a lane's job
-// (its wave runs to the widest job's row count) reads data inside the region,
-// or zeros past it, and is never multiplied.
-constexpr int kCombRsrcWord3 = 0x00020000;  // raw 32-bit data (gfx9 buffer resource word 3)
-struct RowSrc {
-    const uint8_t *in;
-    __amdgpu_buffer_rsrc_t r;
-    uint32_t voff;
-    bool buf;  // wave-uniform
-};
-__device__ __forceinline__ uint4 row_ld(const RowSrc &rs, int q, int nin, uint32_t stride) {
-    if (rs.buf) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs.r, (int)rs.voff, (int)((uint32_t)q * stride), 0);
-        return make_uint4(v.x, v.y, v.z, v.w);
-    }
-    return ld16(rs.in + (uint32_t)min(q, nin - 1) * stride);
+// Input row q of a combine slot (row 0 at `in`, this lane's column); a row
+// past the lane's job (its wave runs to the widest job's row count) re-reads
+// the job's last row and is never multiplied.  (Buffer loads with scalar row
+// offsets measured 7 % slower on the cfg7 decode, r04; removed r05.)
+__device__ __forceinline__ uint4 row_ld(const uint8_t *in, int q, int nin, uint32_t stride) {
+    return ld16(in + (uint32_t)min(q, nin - 1) * stride);
 }
 
 // One slot (job, 16-B column) for NE outputs (wave-uniform): acc[u] = sum_q
 // T[q][u] * in_q over the job's nin rows (8 loads in flight), optional xor
 // row, stores for u < ne (this lane's job).
 template <int R, int NE>
-__device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int nin, int ne, uint32_t col,
+__device__ __forceinline__ void comb_slot(const uint8_t *rs, uint32_t stride, int nin, int ne, uint32_t col,
                                           const CombRegion<R> &rg, bool skip) {
-    constexpr int U = FECGPU_COMB_U, RT = CombRegion<R>::RT;
+    constexpr int U = COMB_U(R), RT = CombRegion<R>::RT;
     uint4 acc[NE];
 #pragma unroll
     for (int m = 0; m < NE; m++) acc[m] = zero4();
@@ -2099,7 +1556,6 @@ __device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int
         for (int t = 0; t < U; t++) {
             if (q0 + t < nin) {
                 const int q = q0 + t;
-#if FECGPU_COMB_SKIP
                 // the wave's lanes may belong to different jobs: skip what no
                 // active lane needs.  With >= 64 columns per job a wave spans at
                 // most two jobs, its first and last active lanes'; otherwise no skip.
@@ -2116,11 +1572,6 @@ __device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int
 #pragma unroll
                 for (int m = 0; m < NE; m++)
                     if ((nzm >> m) & 1u) gmac(acc[m], sp, rg.ab[q * R + m], rg.tc[q * RT + m]);
-#else
-                const Split sp = split(v[t]);
-#pragma unroll
-                for (int m = 0; m < NE; m++) gmac(acc[m], sp, rg.ab[q * R + m], rg.tc[q * RT + m]);
-#endif
             }
         }
     }
@@ -2131,25 +1582,11 @@ __device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int
         if (m < ne) st16(reinterpret_cast<uint8_t *>(rg.optr[m]) + col * 16u, acc[m]);
 }
 
-#ifndef FECGPU_COMB_PF
-#define FECGPU_COMB_PF 1  // one-output combine jobs: next rows loaded while this batch multiplies
-#endif
-#ifndef FECGPU_COMB_BUF
-#define FECGPU_COMB_BUF 0  // RowSrc buffer loads (cfg7 decode A/B, r04: 0.238 vs 0.222 ms per call with
-                           // pointer loads: off)
-#endif
-#ifndef FECGPU_COMB_PF8
-#define FECGPU_COMB_PF8 0  // ... and the 8-output ones (solves: their widest job's rows are
-                           // dependent round trips; but 221 VGPRs instead of 128: cfg7 decode
-                           // 0.246 vs 0.238 ms, r04: off)
-#endif
-#ifndef FECGPU_COMB_PF_U1
-#define FECGPU_COMB_PF_U1 4  // rows per prefetched batch of the one-output slots (cfg7 decode: 4 rows
-                             // 0.214 vs 8 rows 0.223 ms per call, r04: 107 VGPRs, 4 waves per SIMD)
-#endif
-#ifndef FECGPU_COMB_PF_U
-#define FECGPU_COMB_PF_U 4  // rows per prefetched batch of the 8-output slots (registers)
-#endif
+// rows per prefetched batch of the one-output slots (cfg7 decode: 4 rows 0.214
+// vs 8 rows 0.223 ms per call, r04: 107 VGPRs, 4 waves per SIMD).  The
+// 8-output slots do not prefetch (221 VGPRs instead of 128: cfg7 decode 0.246
+// vs 0.238 ms, r04).
+constexpr int kCombPfU = 4;
 // comb_slot with the rows of batch i + 1 in flight while batch i multiplies
 // (two 8-row buffers) and the xor row loaded with the first batch.  A
 // workgroup streams its jobs' slots pass after pass, so without the prefetch
@@ -2160,9 +1597,9 @@ __device__ __forceinline__ void comb_slot(const RowSrc &rs, uint32_t stride, int
 // compiler's wait counts would merge to the stricter path.  Rows past a
 // lane's nin reload its last row and are not multiplied.
 template <int R, int NE>
-__device__ __forceinline__ void comb_slot_pf(const RowSrc &rs, uint32_t stride, int nin, int ne, uint32_t col,
+__device__ __forceinline__ void comb_slot_pf(const uint8_t *rs, uint32_t stride, int nin, int ne, uint32_t col,
                                              const CombRegion<R> &rg, bool skip) {
-    constexpr int U = R == 1 ? FECGPU_COMB_PF_U1 : FECGPU_COMB_PF_U, RT = CombRegion<R>::RT;
+    constexpr int U = kCombPfU, RT = CombRegion<R>::RT;
     uint4 acc[NE];
 #pragma unroll
     for (int m = 0; m < NE; m++) acc[m] = zero4();
@@ -2172,7 +1609,7 @@ __device__ __forceinline__ void comb_slot_pf(const RowSrc &rs, uint32_t stride, 
     nw = __builtin_amdgcn_readfirstlane(nw);
     const uint64_t xp = rg.optr[R];
     // without an xor row: a load of row 0 (a valid address), discarded
-    const uint4 xv = ld16(xp ? reinterpret_cast<const uint8_t *>(xp) + col * 16u : rs.in);
+    const uint4 xv = ld16(xp ? reinterpret_cast<const uint8_t *>(xp) + col * 16u : rs);
     auto load = [&](uint4 (&v)[U], int q0) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < U; t++) v[t] = row_ld(rs, q0 + t, nin, stride);
@@ -2183,13 +1620,11 @@ __device__ __forceinline__ void comb_slot_pf(const RowSrc &rs, uint32_t stride, 
             const int q = q0 + t;
             if (q < nin) {
                 uint32_t nzm = 0xffu;
-#if FECGPU_COMB_SKIP
                 if (R > 1 && skip) {
                     const uint32_t z = rg.nz[q];
                     const int last = 63 - __builtin_clzll(__builtin_amdgcn_read_exec());
                     nzm = __builtin_amdgcn_readfirstlane(z) | __builtin_amdgcn_readlane(z, last);
                 }
-#endif
                 if (!nzm) continue;
                 const Split sp = split(v[t]);
 #pragma unroll
@@ -2221,10 +1656,10 @@ __device__ __forceinline__ void comb_slot_pf(const RowSrc &rs, uint32_t stride, 
 }
 
 template <int R, int NE = R>
-__device__ __forceinline__ void comb_dispatch(int nw, const RowSrc &rs, uint32_t stride, int nin, int ne,
+__device__ __forceinline__ void comb_dispatch(int nw, const uint8_t *rs, uint32_t stride, int nin, int ne,
                                               uint32_t col, const CombRegion<R> &rg, bool skip) {
     if constexpr (NE >= 1) {
-        if constexpr (FECGPU_COMB_PF && (R == 1 || (FECGPU_COMB_PF8 && R == 8 && NE == 8))) {
+        if constexpr (R == 1) {
             if (nw == NE) {
                 comb_slot_pf<R, NE>(rs, stride, nin, ne, col, rg, skip);
                 return;
@@ -2237,22 +1672,6 @@ __device__ __forceinline__ void comb_dispatch(int nw, const RowSrc &rs, uint32_t
     }
 }
 
-#ifndef FECGPU_COMB_HDR
-#define FECGPU_COMB_HDR 1  // combine plans: a wave's job headers in one round of loads
-#endif
-#ifndef FECGPU_COMB_MINW
-#define FECGPU_COMB_MINW 0  // >0: the grouped encode's combine (R = 4) asks for this many waves per SIMD
-#endif
-#ifndef FECGPU_COMB_MINW1
-#define FECGPU_COMB_MINW1 0  // >0: the one-output combine (R = 1) asks for this many waves per SIMD
-#endif
-#if FECGPU_COMB_MINW1 > 0
-#define COMB_WAVES __attribute__((amdgpu_waves_per_eu(R == 1 ? FECGPU_COMB_MINW1 : 1, 8)))
-#elif FECGPU_COMB_MINW > 0
-#define COMB_WAVES __attribute__((amdgpu_waves_per_eu(R == 4 ? FECGPU_COMB_MINW : 1, 8)))
-#else
-#define COMB_WAVES
-#endif
 // Device twin of the host's choose_wpb (fec_capi.cpp): jobs per workgroup that
 // fit `budget` bytes at job_lds each, picked for lane use over ncol columns.
 __device__ __forceinline__ int choose_wpb_dev(uint32_t ncol, uint32_t job_lds, uint32_t budget) {
@@ -2273,7 +1692,7 @@ __device__ __forceinline__ int choose_wpb_dev(uint32_t ncol, uint32_t job_lds, u
 }
 
 template <int R>
-__global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
+__global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
     extern __shared__ uint4 dyn[];
     __shared__ uint32_t s_pfx[kMaxWpb + 1];
     __shared__ uint64_t s_in[kMaxWpb];
@@ -2294,6 +1713,7 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
     }
     __syncthreads();
 #endif
+    if (a.err && (*a.err & kSwErrHeader)) return;  // the whole grid stands down (device-sized decode launches)
     const uint64_t njobs = a.njobs + (a.extra ? (uint64_t)(*a.extra >> a.extra_shift) : 0ull);
     int nin_max = a.nin_max, wpb = a.wpb;
     uint32_t job_lds = a.job_lds;
@@ -2327,10 +1747,6 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
         return shared ? CombRegion<R>(regions, regions + tab_lds + (size_t)jl * job_lds, nin_max)
                       : CombRegion<R>(regions + (size_t)jl * job_lds, nin_max);
     };
-    // buffer loads of the input rows when the region fits 32-bit offsets (RowSrc)
-    const bool buf = FECGPU_COMB_BUF && !FECGPU_CHECK && a.in_bytes != 0 && a.in_bytes < (1ull << 32);
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.in_base), 0, buf ? (int)(uint32_t)a.in_bytes : 0, kCombRsrcWord3);
     // one group of nb jobs (jobAt(jl): job jl of the group): tables, then its
     // (job, column) slots over the workgroup
     constexpr int NW = kBlock / 64;
@@ -2339,13 +1755,10 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
         // come in one round of loads, a lane each (the decode passes walk a
         // slot per repair or unknown, most of them empty: one dependent load
         // per job was most of those passes' time)
-#if FECGPU_COMB_HDR
         CombJob Jl{};
         Jl.xor_off = kNoXor;
         if (wave + NW * lane < nb) Jl = jobAt(wave + NW * lane);
-#endif
         for (int ji = 0, jl = wave; jl < nb; ji++, jl += NW) {
-#if FECGPU_COMB_HDR
             const auto rl64 = [&](uint64_t v) __attribute__((always_inline)) {
                 return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, ji) |
                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), ji) << 32);
@@ -2357,9 +1770,6 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
             J.xor_off = rl64(Jl.xor_off);
             J.nin = (uint32_t)__builtin_amdgcn_readlane((int)Jl.nin, ji);
             J.nout = (uint32_t)__builtin_amdgcn_readlane((int)Jl.nout, ji);
-#else
-            const CombJob J = jobAt(jl);
-#endif
             const int nin = min((int)J.nin, nin_max), nout = min((int)(J.nout & ~kCombXorScaled), R);
             const CombRegion<R> rg = region(jl);
             const uint8_t *cf = a.coef + J.coef_off;
@@ -2417,11 +1827,7 @@ __global__ __launch_bounds__(kBlock) COMB_WAVES void comb_kernel(CombArgs a) {
             const int ne = s_ne[jl];
             const int nw = __builtin_amdgcn_readfirstlane(ne);
             const CombRegion<R> rg = region(jl);
-            RowSrc rs;
-            rs.in = reinterpret_cast<const uint8_t *>(s_in[jl]) + col * 16u;
-            rs.buf = buf;
-            rs.r = rsrc;
-            rs.voff = (uint32_t)(s_in[jl] - reinterpret_cast<uint64_t>(a.in_base)) + col * 16u;
+            const uint8_t *rs = reinterpret_cast<const uint8_t *>(s_in[jl]) + col * 16u;
             comb_dispatch<R>(nw, rs, a.stride, (int)s_nin[jl], ne, col, rg, a.skip && a.ncol >= 64);
         }
         __syncthreads();
@@ -2596,7 +2002,7 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
         grid = std::min<uint64_t>(want, (uint64_t)resident_blocks(fn, p.lds_bytes) * (uint64_t)mult);
     }
     // XCD regions: grid a multiple of 8 so every region has the same walkers
-    a.nx = FECGPU_XCD ? 8 : 1;
+    a.nx = 8;
     if (a.nx == 1) {
         grid = std::max<uint64_t>(1, std::min(grid, want));
     } else if (want < 8) {
@@ -2636,43 +2042,41 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
 // k >= 16 only: there the table multiply is VALU-bound and the bit-sliced
 // kernel 1.1-1.4x faster; at r <= 4 (and k = 8, r = 8) the table kernel is
 // memory-bound and, at higher occupancy, 8-12 % faster (profiles/r01_bs_r4_and_alternation.txt).
-#ifndef FECGPU_BS_CODES
-#define FECGPU_BS_CODES(X) X(16, 8) X(24, 8) X(32, 8)
-#endif
+#define BS_CODES(X) X(16, 8) X(24, 8) X(32, 8)
 
 bool bitslice_supported(int k, int r, int matrix) {
     if (matrix != FECGPU_MATRIX_CAUCHY && matrix != FECGPU_MATRIX_VANDERMONDE) return false;
-#define FECGPU_BS_HAS(K_, R_) if (k == K_ && r == R_) return true;
-    FECGPU_BS_CODES(FECGPU_BS_HAS)
-#undef FECGPU_BS_HAS
+#define BS_HAS(K_, R_) if (k == K_ && r == R_) return true;
+    BS_CODES(BS_HAS)
+#undef BS_HAS
     return false;
 }
 
 hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     if (p.bitslice) {
-#define FECGPU_BS_LAUNCH_M(K_, R_, M_)                                                            \
+#define BS_LAUNCH_M(K_, R_, M_)                                                            \
         if (a.k == K_ && a.r == R_ && p.matrix == M_)                                             \
             return p.flat ? launch(gf_encode_bs_kernel<K_, R_, M_, true>, a, p, s, false,         \
                                    (a.nwin * ((a.ncol + 1) / 2) + kBlock - 1) / kBlock)             \
                           : launch(gf_encode_bs_kernel<K_, R_, M_, false>, a, p, s, false);
-#define FECGPU_BS_LAUNCH(K_, R_)                                 \
-        FECGPU_BS_LAUNCH_M(K_, R_, FECGPU_MATRIX_CAUCHY)         \
-        FECGPU_BS_LAUNCH_M(K_, R_, FECGPU_MATRIX_VANDERMONDE)
-        FECGPU_BS_CODES(FECGPU_BS_LAUNCH)
-#undef FECGPU_BS_LAUNCH
-#undef FECGPU_BS_LAUNCH_M
+#define BS_LAUNCH(K_, R_)                                 \
+        BS_LAUNCH_M(K_, R_, FECGPU_MATRIX_CAUCHY)         \
+        BS_LAUNCH_M(K_, R_, FECGPU_MATRIX_VANDERMONDE)
+        BS_CODES(BS_LAUNCH)
+#undef BS_LAUNCH
+#undef BS_LAUNCH_M
         return hipErrorInvalidValue;
     }
     if (p.rbitslice) {
         const uint64_t want = (a.nwin * ((a.ncol + kRbsCols - 1) / kRbsCols) + kBlock - 1) / kBlock;
         switch (a.r) {
-#define FECGPU_RBS_CASE(R_)                                                                        \
+#define RBS_CASE(R_)                                                                        \
             case R_:                                                                               \
                 return p.flat ? launch(gf_encode_rbs_kernel<R_, true>, a, p, s, false, want)       \
                               : launch(gf_encode_rbs_kernel<R_, false>, a, p, s, false);
-            FECGPU_RBS_CASE(4) FECGPU_RBS_CASE(5) FECGPU_RBS_CASE(6) FECGPU_RBS_CASE(7) FECGPU_RBS_CASE(8)
-#undef FECGPU_RBS_CASE
+            RBS_CASE(4) RBS_CASE(5) RBS_CASE(6) RBS_CASE(7) RBS_CASE(8)
+#undef RBS_CASE
             default: return hipErrorInvalidValue;
         }
     }

@@ -37,29 +37,20 @@ namespace {
 // CU.  cfg7 encode 0.249 -> 0.229 ms against 40 KB (7 jobs, 2 passes), 64 KB
 // 0.282 ms, 96 KB 0.513 ms (profiles/r02_comb_budget_ab.txt).  Narrow jobs
 // keep the larger budget, which packs more of them per pass.
-#ifndef FECGPU_COMB_BUDGET_KB
-#define FECGPU_COMB_BUDGET_KB 40
-#endif
-#ifndef FECGPU_COMB_BUDGET_WIDE_KB
-#define FECGPU_COMB_BUDGET_WIDE_KB 20
-#endif
-constexpr uint32_t kCombBudget = FECGPU_COMB_BUDGET_KB << 10;
-constexpr uint32_t kCombBudgetWide = FECGPU_COMB_BUDGET_WIDE_KB << 10;
+// (decode syndromes: 16 / 20 / 32 KB gave 0.197 / 0.198 / 0.209 ms per cfg7 call, r04)
+constexpr uint32_t kCombBudget = 40u << 10;
+constexpr uint32_t kCombBudgetWide = 20u << 10;
 // kSwSolveOut (fec_internal.h): recovered sources per solve job
 constexpr int kSwSolveIn = 128;              // syndrome rows a small system's solve reads (fec_swdec.hip)
 // LDS of a solve workgroup: its jobs' 8-output tables over the widest range of
 // syndrome rows (device-sized); more room than the encode's budget keeps
 // several jobs per workgroup
-#ifndef FECGPU_SOLVE_BUDGET_KB
-#define FECGPU_SOLVE_BUDGET_KB 32  // A/B (r03): 32 KB 0.235 vs 64 KB 0.241 ms per cfg7 decode call (1.62 vs 1.71 at 10 % loss)
-#endif
-constexpr uint32_t kSolveBudget = FECGPU_SOLVE_BUDGET_KB << 10;
+// (r03: 32 KB 0.235 vs 64 KB 0.241 ms per cfg7 decode call, 1.62 vs 1.71 at 10 % loss)
+constexpr uint32_t kSolveBudget = 32u << 10;
 // LDS for one streaming-encode workgroup's multiply tables (segment of up to
 // kSwSeg repairs x max_window coefficients x 21 B): 43 KB for 64 repairs at W 32
-#ifndef FECGPU_STREAM_BUDGET_KB
-#define FECGPU_STREAM_BUDGET_KB 32  // cfg7 A/B (r04): 28 / 32 / 36 KB 0.200-0.202 vs 44 KB 0.216 ms (more workgroups per CU)
-#endif
-constexpr uint32_t kStreamBudget = FECGPU_STREAM_BUDGET_KB << 10;
+// (cfg7, r04: 28 / 32 / 36 KB 0.200-0.202 vs 44 KB 0.216 ms: more workgroups per CU)
+constexpr uint32_t kStreamBudget = 32u << 10;
 constexpr uint64_t kSwStreamSources = 1ull << 32;  // the streaming encode's source positions are 32-bit
 // sources and repairs per call: the device plan numbers them in 32 bits
 constexpr uint64_t kSwMaxSources = (1ull << 32) - 256;
@@ -143,8 +134,7 @@ bool sw_groups_fit(const fecgpu_sw_repair *h, uint64_t nrep, uint64_t nsrc, int 
 // kSwStreamAuto: the fewest lane-slots per row, waves x C, ties to the
 // smaller C).  A lane's table reads (the same on every lane) are shared by
 // its C dwords, but the VALU work per dword is not, and C > 1 costs
-// registers: on cfg7 C = 1 was fastest (fec_internal.h
-// FECGPU_SW_STREAM_DEFAULT).  The row's dwords D = 4 x 16-B columns; C
+// registers: on cfg7 C = 1 was fastest (fec_internal.h kSwStreamDefault).  The row's dwords D = 4 x 16-B columns; C
 // divides D so no lane runs past a row.
 int sw_stream_dwords(int stream, uint32_t S) {
     const uint32_t D = ((S + 15u) >> 4) * 4u;
@@ -169,10 +159,9 @@ int sw_stream_dwords(int stream, uint32_t S) {
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *pj, void *pc,
                        void *po, hipStream_t s, int group, const fecgpu_sw_repair *hdr_host, int stream,
-                       void *gtab, const uint8_t *rlc) {
+                       const uint8_t *rlc) {
     if (stream > 0 && nsrc < kSwStreamSources) {
         SwStreamArgs sa{};
-        sa.gtab = gtab;
         sa.rlc = rlc;
         sa.src = src;
         sa.rep = rep;
@@ -223,19 +212,14 @@ ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_
     void *pj = nullptr, *pc = nullptr, *po = nullptr;
     const int group = ctx_sw_group(ctx), stream = ctx_sw_stream(ctx);
     const uint8_t *rlc = nullptr;
-    if (FECGPU_SW_RLCTAB) RC_TRY(ctx_rlc_table(ctx, s, &rlc));
-    if (stream > 0 && nsrc < kSwStreamSources) {
-        // the streaming encode's multiply tables in global memory (scalar loads)
-        void *gt = nullptr;
-        if (FECGPU_SWS_SGPR) RC_TRY(ctx_sw_scratch(ctx, 1, sw_stream_gtab_bytes(nrep, std::max(1, max_window)), &gt));
+    RC_TRY(ctx_rlc_table(ctx, s, &rlc));
+    if (stream > 0 && nsrc < kSwStreamSources)
         return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, nullptr, nullptr, nullptr, s,
-                              group, hdr_host, stream, gt, rlc);
-    }
+                              group, hdr_host, stream, rlc);
     RC_TRY(ctx_sw_scratch(ctx, 0, sw_enc_jobs(nrep, group) * sizeof(CombJob), &pj));
     RC_TRY(ctx_sw_scratch(ctx, 1, nrep * kSwCoefPitch, &pc));
     RC_TRY(ctx_sw_scratch(ctx, 2, nrep * sizeof(uint64_t), &po));
-    return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s, group, hdr_host, 0,
-                          nullptr, rlc);
+    return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s, group, hdr_host, 0, rlc);
 }
 
 // ---- decode (device plan: fec_swdec.hip) ----------------------------------
@@ -246,15 +230,13 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // rows), slot 9 (their operation log) and slot 10 (device copies of host
 // bookkeeping).
 struct DecBlock {
-    size_t o_reach, o_rcnt, o_chunk, o_lost, o_reachL, o_ctr, o_synj, o_syno, o_coef, o_solj, o_solo, o_solc,
-        o_long, o_mid, o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, o_lkind, o_starts, total;
+    size_t o_reach, o_rcnt, o_lost, o_reachL, o_ctr, o_synj, o_syno, o_coef, o_solj, o_solo, o_solc, o_long,
+        o_synrow, o_pivc, o_colpiv, o_pivhi, o_pivt, o_lkind, o_starts, total;
     uint64_t long_cap, piv_cap;
 };
-DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
+DecBlock dec_block(uint64_t nsrc, uint64_t nrep) {
     DecBlock L{};
-    const uint64_t nchunk = (nsrc + kSwChunk - 1) / kSwChunk;
-    (void)long_min;
-    L.long_cap = nsrc + 1;  // queued systems (mid or long): at most one per lost source
+    L.long_cap = nsrc + 1;  // queued long systems: at most one per lost source
     L.piv_cap = std::max<uint64_t>(1, nrep);
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -262,32 +244,29 @@ DecBlock dec_block(uint64_t nsrc, uint64_t nrep, int long_min) {
         o += align256(bytes);
         return at;
     };
-    L.o_ctr = take(sizeof(SwDecCtr));  // ctr, reach and rcnt adjacent: one memset clears them
+    L.o_ctr = take(sizeof(SwDecCtr));
     L.o_reach = take((nsrc + 1) * 4);
     L.o_rcnt = take((nsrc + 1) * 4);
-    L.o_chunk = take(3 * nchunk * 4);
     L.o_lost = take(nsrc * 4);
     L.o_reachL = take(nsrc * 4);
-    // syndrome slots: one per repair, and (fused plan) one per lost source for
-    // the one-unknown systems the plan solves
-    const uint64_t nsyn = nrep + (FECGPU_SWD_FUSED ? nsrc : 0);
+    // syndrome slots: one per repair, and one per lost source for the
+    // one-unknown systems the plan solves
+    const uint64_t nsyn = nrep + nsrc;
     L.o_synj = take(nsyn * sizeof(CombJob));
     L.o_syno = take(nsyn * 8);
     L.o_coef = take(nsyn * (size_t)kSwCoefPitch);
-    // solve jobs / outputs: a slot per unknown, or (fused plan) a compact list
-    // with outputs padded to 8 per system (multi-unknown systems: <= 4.5 per unknown)
+    // solve jobs / outputs: a slot per unknown
     L.o_solj = take((nsrc + 8) * sizeof(CombJob));
-    L.o_solo = take((FECGPU_SWD_FUSED && FECGPU_SWD_SOLVE_LIST ? 5 * nsrc + 8 : nsrc) * 8);
+    L.o_solo = take(nsrc * 8);
     L.o_solc = take(nrep * (size_t)kSwSmallE);
     L.o_long = take(L.long_cap * sizeof(SwLong));
-    L.o_mid = take(L.long_cap * sizeof(SwLong));
     L.o_synrow = take(nrep * 4);
     L.o_pivc = take(L.piv_cap * 256);
     L.o_colpiv = take(nsrc * 4);
     L.o_pivhi = take(L.piv_cap * 4);
     L.o_pivt = take(L.piv_cap * 4);
-    L.o_lkind = take(FECGPU_SWD_FUSED ? nsrc : 0);
-    L.o_starts = take(FECGPU_SWD_FUSED ? nsrc * 4 : 0);
+    L.o_lkind = take(nsrc);
+    L.o_starts = take(nsrc * 4);
     L.total = o;
     return L;
 }
@@ -301,7 +280,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
                        uint32_t stride, uint8_t *stat, hipStream_t s, SwDecCtr *ctr_out, uint64_t log_entries,
                        SwSticky *sticky = nullptr) {
     const int long_min = ctx_sw_long_min(ctx);
-    const DecBlock L = dec_block(nsrc, nrep, long_min);
+    const DecBlock L = dec_block(nsrc, nrep);
     void *pb = nullptr, *psyn = nullptr, *ppiv = nullptr, *plog = nullptr;
     RC_TRY(ctx_sw_scratch(ctx, 6, L.total, &pb));
     RC_TRY(ctx_sw_scratch(ctx, 7, std::max<uint64_t>(1, nrep) * stride, &psyn));
@@ -317,11 +296,9 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.nrep = nrep;
     a.stride = stride;
     a.S = S;
-    a.nchunk = (uint32_t)((nsrc + kSwChunk - 1) / kSwChunk);
     a.long_min = long_min;
     a.reach = reinterpret_cast<uint32_t *>(b + L.o_reach);
     a.rcnt = reinterpret_cast<uint32_t *>(b + L.o_rcnt);
-    a.chunk = reinterpret_cast<uint32_t *>(b + L.o_chunk);
     a.lost = reinterpret_cast<uint32_t *>(b + L.o_lost);
     a.reachL = reinterpret_cast<uint32_t *>(b + L.o_reachL);
     a.ctr = reinterpret_cast<SwDecCtr *>(b + L.o_ctr);
@@ -332,7 +309,6 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.sol_outs = reinterpret_cast<uint64_t *>(b + L.o_solo);
     a.sol_coef = b + L.o_solc;
     a.longs = reinterpret_cast<SwLong *>(b + L.o_long);
-    a.mids = reinterpret_cast<SwLong *>(b + L.o_mid);
     a.long_cap = L.long_cap;
     a.log = static_cast<SwOp *>(plog);
     a.log_cap = log_entries;
@@ -348,11 +324,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.src = src;
     a.synd = static_cast<const uint8_t *>(psyn);
     a.sticky = sticky;
-#if FECGPU_SW_RLCTAB
     RC_TRY(ctx_rlc_table(ctx, s, &a.rlc));
-#endif
-
-#if FECGPU_SWD_FUSED
     {  // the plan kernel writes the counters itself: nothing to clear
         SwLookback lb{};
         RC_TRY(ctx_sw_lookback(ctx, (nsrc + kSwPlanChunk - 1) / kSwPlanChunk, &lb, &a.epoch));
@@ -361,9 +333,6 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
         a.lb_inc = lb.inc;
         a.lb_ticket = lb.ticket;
     }
-#else
-    SW_TRY(hipMemsetAsync(a.ctr, 0, L.o_chunk - L.o_ctr, s), "sliding-window decode counters");
-#endif
     SW_TRY(launch_sw_dec_plan(a, s), "sliding-window decode plan launch");
     SW_TRY(launch_sw_dec_long(a, s), "sliding-window long-system plan launch");
     const uint32_t ncol = (S + 15u) >> 4;
@@ -377,18 +346,18 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     sa.out_base = static_cast<uint8_t *>(psyn);
     sa.xor_base = rep;
     sa.njobs = nrep;  // a slot per repair; the needed ones filled by their systems
-#if FECGPU_SWD_FUSED
     sa.extra = &a.ctr->nlost;  // then a slot per lost source: the plan's one-unknown systems
     sa.extra_max = nsrc;
     sa.interleave = 1;  // those are dense at the end: deal the groups round-robin
-#endif
-    sa.sparse = FECGPU_SWD_SPARSE;
-    sa.in_bytes = nsrc * stride;
+    // mostly empty slots: each workgroup gathers its share's non-empty jobs
+    // (decode 0.239 -> 0.223 ms per cfg7 call against walking every slot, r04)
+    sa.sparse = 1;
     sa.ncol = ncol;
     sa.stride = stride;
     sa.nin_max = kSwMaxWindow;
     sa.nout_max = 1;
     sa.nin_dev = &a.ctr->wmax;
+    sa.err = &a.ctr->err;
     sa.budget = ncol >= 64 ? kCombBudgetWide : kCombBudget;
     SW_TRY(launch_comb(sa, 1, s), "sliding-window syndrome launch");
     CombArgs va = sa;
@@ -398,21 +367,13 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     va.in_base = static_cast<const uint8_t *>(psyn);
     va.out_base = src;
     va.xor_base = nullptr;
-#if FECGPU_SWD_FUSED && FECGPU_SWD_SOLVE_LIST
-    va.extra = &a.ctr->nsolout;  // the compact list: a job per kSwSolveOut outputs
-    va.extra_shift = kSwSolveOut == 8 ? 3 : kSwSolveOut == 4 ? 2 : 1;
-    va.extra_max = nsrc + 8;
-#else
     va.extra = &a.ctr->nlost;  // a slot per unknown, filled by its small system
     va.extra_max = nsrc;
-#endif
     va.njobs = 0;
     va.nin_max = kSwSolveIn;
     va.nout_max = kSwSolveOut;
     va.nin_dev = &a.ctr->maxin;
     va.budget = kSolveBudget;
-    va.sparse = FECGPU_SWD_SPARSE;
-    va.in_bytes = std::max<uint64_t>(1, nrep) * stride;  // the syndrome rows
     SW_TRY(launch_comb(va, kSwSolveOut, s), "sliding-window solve launch");
     SW_TRY(launch_sw_dec_replay(a, s), "sliding-window long-system replay launch");
     if (ctr_out) SW_TRY(hipMemcpyAsync(ctr_out, a.ctr, sizeof(SwDecCtr), hipMemcpyDeviceToHost, s), "D2H sw counters");
@@ -574,7 +535,10 @@ ssize_t fecgpu_sw_decode_errors(fecgpu_ctx *ctx, uint32_t *flags) {
     RC_TRY(ctx_sw_wait(ctx));  // every sliding-window call issued so far on this device
     SwSticky h{};
     SW_TRY(hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost), "D2H sw error flags");
-    SW_TRY(hipMemset(d, 0, sizeof(h)), "sw error flags reset");
+    // cleared by a synchronous copy, complete on return (a null-stream memset
+    // may still be pending when the next asynchronous decode raises a flag)
+    const SwSticky z{};
+    SW_TRY(hipMemcpy(d, &z, sizeof(z), hipMemcpyHostToDevice), "sw error flags reset");
     // the next asynchronous calls reserve what the overflow asked for, twice over
     if (h.err & kSwErrCapacity) ctx_sw_log_grow(ctx, std::max<uint64_t>(2 * h.need, 1u << 16));
     *flags = h.err;

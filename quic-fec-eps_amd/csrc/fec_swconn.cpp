@@ -128,12 +128,10 @@ ssize_t enc_launch(fecgpu_sw_encoder *e) {
         S.hdr[t].fss -= e->base;
     }
     const uint8_t *rlc = nullptr;
-    ssize_t rc = ctx_fault_take(e->ctx) ? (ssize_t)FECGPU_ERR_DEVICE
-                 : FECGPU_SW_RLCTAB     ? ctx_rlc_table(e->ctx, e->s, &rlc)
-                                        : 0;
+    ssize_t rc = ctx_fault_take(e->ctx) ? (ssize_t)FECGPU_ERR_DEVICE : ctx_rlc_table(e->ctx, e->s, &rlc);
     if (rc >= 0)
         rc = sw_encode_core(e->src, e->cap, S.rep, S.hdr, n, e->p.window, e->p.symbol_size, e->stride, S.jobs, S.coef,
-                            S.outs, e->s, e->group, S.hdr, e->stream, nullptr, rlc);
+                            S.outs, e->s, e->group, S.hdr, e->stream, rlc);
     if (rc >= 0) {
         const hipError_t er = hipEventRecord(S.ev, e->s);
         if (er != hipSuccess) rc = set_dev_error(er, "hipEventRecord");

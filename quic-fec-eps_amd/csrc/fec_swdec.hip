@@ -4,18 +4,19 @@
 // checks: the receiver's arrival flags and repair headers go to the GPU and
 // every step below runs there.
 //
-//  1. plan (sw_dec_{hdr,count,scan,lost}_kernel): per-call scans over the
-//     arrival flags — statuses, the lost list in stream order, and for each
-//     lost source the farthest window end of the received repairs that start
-//     at or before it (a system ends where that reach stops short of the next
-//     lost source).  The reach array is then reused as rank[i] = lost sources
-//     before i, which gives any window's unknown range in two loads.
-//  2. systems (sw_dec_sys_kernel): a wave per system start.  A system of at
-//     most 64 unknowns and 96 equations is solved by that wave: coefficients
-//     from the RFC 8682 PRNG, Gauss-Jordan with pivot search on [A | I] in LDS,
-//     solve jobs x_u = sum_t T[u][t] s_t for the determined unknowns (also
-//     when the system is rank deficient), syndrome jobs only for the rows a
-//     solve reads.  A longer system is queued for step 3.
+//  1. plan (sw_dec_plan_kernel, one launch, decoupled look-back over chunks
+//     of sources): statuses, the lost list in stream order, and for each lost
+//     source the farthest window end of the received repairs that start at or
+//     before it (a system ends where that reach stops short of the next lost
+//     source).  The reach array is then reused as rank[i] = lost sources
+//     before i, which gives any window's unknown range in two loads.  The
+//     one-unknown systems are finished here (a combine job each).
+//  2. systems (sw_dec_sys_kernel): a wave per larger system's start.  A
+//     system of at most 64 unknowns and 96 equations is solved by that wave:
+//     Gauss-Jordan with pivot search on [A | I] in LDS, solve jobs x_u =
+//     sum_t T[u][t] s_t for the determined unknowns (also when the system is
+//     rank deficient), syndrome jobs only for the rows a solve reads.  A
+//     longer system is queued for step 3.
 //  3. long systems (sw_dec_long_kernel): a wave per system plans a banded
 //     elimination (oracle/fec_sw_banded.c is its CPU statement) into an
 //     operation log — forward elimination with the pivot whose range ends
@@ -71,6 +72,12 @@ __device__ __forceinline__ void set_tab(uint32_t (&t)[5], uint32_t c) {
 
 __device__ __forceinline__ uint64_t lanes_below(int lane) { return (1ull << lane) - 1ull; }
 
+// a header the plan may act on (fec_sw.cpp header_ok's device twin): a window
+// of 1..kSwMaxWindow sources inside the stream, dt <= 15
+__device__ __forceinline__ bool hdr_ok(const fecgpu_sw_repair &h, uint64_t nsrc) {
+    return h.nss >= 1 && h.nss <= kSwMaxWindow && h.dt <= 15 && h.fss <= nsrc && nsrc - h.fss >= h.nss;
+}
+
 // An error of this call (kSwErr* bits), also raised in the ctx's sticky word for
 // asynchronous calls (need: the log size an overflow asked for)
 __device__ __forceinline__ void dec_err(const SwDecArgs &a, uint32_t bits, unsigned long long need = 0) {
@@ -121,221 +128,8 @@ __device__ uint64_t wave_lower_bound(const fecgpu_sw_repair *h, uint64_t lo, uin
     return b ? lo + (uint64_t)(__ffsll((unsigned long long)b) - 1) : hi;
 }
 
-// ================================================================ plan ===
-// Headers: validity (device headers are checked here; host headers were
-// checked by the caller too), the widest received window, per source the
-// farthest end of the received repairs starting there and the number of
-// repairs starting there.
-__global__ __launch_bounds__(kBlock) void sw_dec_hdr_kernel(SwDecArgs a) {
-    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    bool bad = false;
-    uint32_t w = 0;
-    if (t < a.nrep) {
-        const fecgpu_sw_repair h = a.hdr[t];
-        bad = h.nss < 1 || h.nss > kSwMaxWindow || h.dt > 15 || h.fss > a.nsrc || a.nsrc - h.fss < h.nss;
-        if (t > 0 && a.hdr[t - 1].fss > h.fss) bad = true;
-        CombJob E{};
-        E.xor_off = kNoXor;
-        a.syn_jobs[t] = E;  // filled if repair t becomes a needed syndrome
-        if (!bad) {
-            atomicAdd(&a.rcnt[h.fss], 1u);
-            if (a.rep_present[t]) {
-                w = h.nss;
-                atomicMax(&a.reach[h.fss], (uint32_t)(h.fss + h.nss));
-            }
-        }
-    }
-    __shared__ uint32_t s_w[kBlock / 64];
-    w = wave_max(w);
-    const uint64_t anybad = __ballot(bad);
-    if ((threadIdx.x & 63) == 0) {
-        s_w[threadIdx.x >> 6] = w;
-        if (anybad) dec_err(a, kSwErrHeader);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t m = 0;
-        for (int i = 0; i < kBlock / 64; i++) m = max(m, s_w[i]);
-        if (m) atomicMax(&a.ctr->wmax, m);  // one atomic per block
-    }
-}
-
-// Block per chunk of 4096 sources (16 per thread): statuses (1 = lost), and
-// the chunk's lost count, max reach and repair count.
-__global__ __launch_bounds__(kBlock) void sw_dec_count_kernel(SwDecArgs a) {
-    __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64], s_r[kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t i0 = (uint64_t)blockIdx.x * kSwChunk + threadIdx.x * 16u;
-    uint32_t cnt = 0, mx = 0, rc = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const uint64_t i = i0 + j;
-        if (i < a.nsrc) {
-            const bool lost = a.src_present[i] == 0;
-            cnt += lost;
-            a.stat[i] = lost ? FECGPU_STATUS_UNRECOVERABLE : FECGPU_STATUS_OK;
-            mx = max(mx, a.reach[i]);
-            rc += a.rcnt[i];
-        }
-    }
-    cnt = wave_sum(cnt);
-    rc = wave_sum(rc);
-    mx = wave_max(mx);
-    if (lane == 0) {
-        s_c[wave] = cnt;
-        s_m[wave] = mx;
-        s_r[wave] = rc;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t c = 0, m = 0, r = 0;
-        for (int w = 0; w < kBlock / 64; w++) {
-            c += s_c[w];
-            m = max(m, s_m[w]);
-            r += s_r[w];
-        }
-        a.chunk[3 * blockIdx.x] = c;
-        a.chunk[3 * blockIdx.x + 1] = m;
-        a.chunk[3 * blockIdx.x + 2] = r;
-    }
-}
-
-// One block: exclusive scans of `cols` interleaved per-chunk columns of arr
-// (column 1 by max when max1, the others by sum); the totals of column 0 go to
-// *total0.
-__global__ __launch_bounds__(1024) void sw_dec_scan_kernel(uint32_t *arr, uint32_t n, int cols, int max1,
-                                                           uint32_t *total0) {
-    __shared__ uint32_t s_w[3][16];
-    __shared__ uint32_t s_carry[3];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x < 3) s_carry[threadIdx.x] = 0;
-    __syncthreads();
-    for (uint32_t b0 = 0; b0 < n; b0 += 1024) {
-        const uint32_t b = b0 + threadIdx.x;
-        uint32_t v[3], inc[3], exc[3];
-        for (int k = 0; k < cols; k++) {
-            v[k] = b < n ? arr[(uint64_t)cols * b + k] : 0u;
-            const bool mx = max1 && k == 1;
-            uint32_t x = v[k];
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o);
-                if (lane >= o) x = mx ? max(x, y) : x + y;
-            }
-            inc[k] = x;
-            uint32_t e = __shfl_up(x, 1);
-            exc[k] = lane == 0 ? 0u : e;
-            if (lane == 63) s_w[k][wave] = x;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int k = 0; k < cols; k++) {
-                const bool mx = max1 && k == 1;
-                uint32_t acc = s_carry[k];
-                for (int w = 0; w < 16; w++) {
-                    const uint32_t t = s_w[k][w];
-                    s_w[k][w] = acc;
-                    acc = mx ? max(acc, t) : acc + t;
-                }
-                s_carry[k] = acc;
-            }
-        }
-        __syncthreads();
-        if (b < n)
-            for (int k = 0; k < cols; k++) {
-                const bool mx = max1 && k == 1;
-                arr[(uint64_t)cols * b + k] = mx ? max(s_w[k][wave], exc[k]) : s_w[k][wave] + exc[k];
-            }
-        (void)inc;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && total0) *total0 = s_carry[0];
-}
-
-// Block per chunk of sources: the lost sources in order with the reach at
-// each (an empty solve job for each, which its system may fill), rank[i] =
-// lost sources before i (over reach) and repfirst[i] = repairs starting
-// before i (over rcnt).  Two passes over the thread's 16 sources (the second
-// re-reads them from cache; no other thread touches them) keep registers low;
-// the per-source outputs go out as 16-byte stores.
-__global__ __launch_bounds__(kBlock) void sw_dec_lost_kernel(SwDecArgs a) {
-    __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64], s_r[kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t b = blockIdx.x;
-    const uint64_t i0 = (uint64_t)b * kSwChunk + threadIdx.x * 16u;
-    const uint32_t n = (uint32_t)min<uint64_t>(16, a.nsrc > i0 ? a.nsrc - i0 : 0);
-    uint32_t cnt = 0, tm = 0, tr = 0;
-    for (uint32_t j = 0; j < n; j++) {
-        cnt += a.src_present[i0 + j] == 0;
-        tm = max(tm, a.reach[i0 + j]);
-        tr += a.rcnt[i0 + j];
-    }
-    uint32_t ic = cnt, im = tm, ir = tr;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(ic, o), ym = __shfl_up(im, o), yr = __shfl_up(ir, o);
-        if (lane >= o) {
-            ic += y;
-            im = max(im, ym);
-            ir += yr;
-        }
-    }
-    uint32_t em = __shfl_up(im, 1);
-    if (lane == 0) em = 0;
-    if (lane == 63) {
-        s_c[wave] = ic;
-        s_m[wave] = im;
-        s_r[wave] = ir;
-    }
-    __syncthreads();
-    uint32_t wc = 0, wm = 0, wr = 0;
-    for (int w = 0; w < wave; w++) {
-        wc += s_c[w];
-        wm = max(wm, s_m[w]);
-        wr += s_r[w];
-    }
-    uint32_t off = a.chunk[3 * b] + wc + ic - cnt;
-    uint32_t run = max(max(a.chunk[3 * b + 1], wm), em);
-    uint32_t rep = a.chunk[3 * b + 2] + wr + ir - tr;
-    CombJob E{};
-    E.xor_off = kNoXor;
-    for (uint32_t j0 = 0; j0 < n; j0 += 4) {
-        uint32_t rk[4], rf[4];
-        for (uint32_t j = j0; j < j0 + 4; j++) {
-            rk[j - j0] = off;
-            rf[j - j0] = rep;
-            if (j >= n) continue;
-            const uint64_t i = i0 + j;
-            run = max(run, a.reach[i]);
-            rep += a.rcnt[i];
-            if (a.src_present[i] == 0) {
-                a.lost[off] = (uint32_t)i;
-                a.reachL[off] = run;
-                a.sol_jobs[off] = E;
-                off++;
-            }
-        }
-        if (j0 + 4 <= n) {
-            *reinterpret_cast<uint4 *>(a.reach + i0 + j0) = make_uint4(rk[0], rk[1], rk[2], rk[3]);  // rank
-            *reinterpret_cast<uint4 *>(a.rcnt + i0 + j0) = make_uint4(rf[0], rf[1], rf[2], rf[3]);   // repfirst
-        } else {
-            for (uint32_t j = j0; j < n; j++) {
-                a.reach[i0 + j] = rk[j - j0];
-                a.rcnt[i0 + j] = rf[j - j0];
-            }
-        }
-    }
-    if (i0 <= a.nsrc && a.nsrc <= i0 + 16) {  // the thread holding the end: rank / repfirst of nsrc
-        a.reach[a.nsrc] = off;
-        a.rcnt[a.nsrc] = rep;
-    }
-}
-
-// the repair's window holds a lost source (rank = lost sources before i)
-__device__ __forceinline__ bool holds_any(const SwDecArgs &a, const fecgpu_sw_repair &h) {
-    return a.reach[h.fss + h.nss] > a.reach[h.fss];
-}
-// ... of the system lost[x .. x + e)
+// the repair's window holds one of the lost sources lost[x .. x + e) (rank =
+// lost sources before i)
 __device__ __forceinline__ bool holds(const SwDecArgs &a, const fecgpu_sw_repair &h, uint32_t x, uint32_t e) {
     const uint32_t r0 = a.reach[h.fss], r1 = a.reach[h.fss + h.nss];
     return r1 > r0 && r0 < x + e && r1 > x;
@@ -374,13 +168,7 @@ __global__ __launch_bounds__(kBlock) void rlc_table_kernel(uint8_t *tab) {
 static_assert(kRlcRow == 256 && kSwMaxWindow < (int)kRlcRow, "a table row holds a window's coefficients");
 
 __device__ __forceinline__ const uint4 *rlc_row(const SwDecArgs &a, const fecgpu_sw_repair &h) {
-#if FECGPU_SW_RLCTAB
     return a.rlc && h.dt == 15 ? reinterpret_cast<const uint4 *>(a.rlc + (size_t)h.key * kRlcRow) : nullptr;
-#else
-    (void)a;
-    (void)h;
-    return nullptr;
-#endif
 }
 
 // f(q, w) for the words q < ceil(nss / 4) of the window's coefficients, 4 per
@@ -466,20 +254,14 @@ struct RlcSeq {
 
 // ============================================================= systems ===
 // Small systems are solved by one wave each with [A | I] in LDS: "tiny" ones
-// (e <= 16, p <= 48: 3 KB of LDS per wave, so occupancy is set by registers)
-// in the pass over the lost sources, larger ones queued to a pass with room for
-// e <= 64, p <= 96.  Syndrome job / row of equation t: slot t (the hdr kernel
-// empties every slot); a system's solve reads its syndrome rows t_first ..
+// (e <= 16, p <= 48) in the wave's own 3 KB, larger ones (e <= 64, p <= 96)
+// in one of the block's shared mid-size regions, taken under an LDS lock.
+// Syndrome job / row of equation t: slot t (the plan empties every slot); a
+// system's solve reads its syndrome rows t_first ..
 // t_last (the repairs in between that are not its equations get coefficient
 // 0: the ranges of two systems never interleave, since a repair between two
 // equations of one system that held a lost source of another would link them).
-[[maybe_unused]] constexpr int kSwTinyE = 16, kSwTinyP = 48;
-#ifndef FECGPU_SWD_COEF
-#define FECGPU_SWD_COEF 1  // coefficients of the repairs holding lost sources drawn by a thread each, up front
-#endif
-#ifndef FECGPU_SWD_FUSE1
-#define FECGPU_SWD_FUSE1 1  // one-unknown systems: syndrome and solve as one combine job
-#endif
+constexpr int kSwTinyE = 16, kSwTinyP = 48;
 constexpr int kSwSolveIn = 128;  // widest syndrome range a small system's solve reads
 
 template <int ME, int MP>
@@ -509,13 +291,12 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     for (int q = lane; q < p; q += 64) {
         const uint32_t t = eq[q];
         const fecgpu_sw_repair h = a.hdr[t];
-#if FECGPU_SWD_COEF
-        if (true) {
-            // the row was drawn by the plan (or sw_dec_coef_kernel): move the
-            // unknowns' entries into A (the unknowns are ascending; the window
-            // holds a run of them).  (Reading dense rows from the table here
-            // instead, with the unknowns zeroed as the row goes out, cost the
-            // system pass 23 us on cfg7, r04: serial LDS lookups per coefficient.)
+        {
+            // the row was drawn by the plan: move the unknowns' entries into A
+            // (the unknowns are ascending; the window holds a run of them).
+            // (Reading dense rows from the table here instead, with the
+            // unknowns zeroed as the row goes out, cost the system pass 23 us
+            // on cfg7, r04: serial LDS lookups per coefficient.)
             uint8_t *cb = a.coef + (uint64_t)t * kSwCoefPitch;
             for (int u = 0; u < e; u++) {
                 const uint64_t i = U[u];
@@ -524,28 +305,6 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
                 M[q * kPitch + u] = cb[i - h.fss];
                 cb[i - h.fss] = 0;
             }
-        } else
-#endif
-        {  // FECGPU_SWD_COEF 0: the row drawn here
-            uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
-            RlcSeq sq(a, h);
-            int u = 0;
-            uint32_t word = 0;
-            for (int j = 0; j < (int)h.nss; j++) {
-                uint32_t c = sq.next((uint32_t)j);
-                const uint64_t i = h.fss + (uint64_t)j;
-                while (u < e && U[u] < i) u++;
-                if (u < e && U[u] == i) {
-                    M[q * kPitch + u] = (uint8_t)c;
-                    c = 0;
-                }
-                word |= c << (8 * (j & 3));
-                if ((j & 3) == 3) {
-                    cc[j >> 2] = word;
-                    word = 0;
-                }
-            }
-            if (h.nss & 3) cc[h.nss >> 2] = word;
         }
         CombJob J;
         J.in_off = h.fss * a.stride;
@@ -611,7 +370,6 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         if (!need) a.syn_jobs[eq[q]].nout = 0;
     }
     if (ndet == 0) return 0;
-#if FECGPU_SWD_FUSE1
     // One unknown (most systems at low loss): x = s_t / c for the pivot
     // equation t, s_t = repair_t + sum of its received sources' terms.  Its
     // syndrome job computes x directly: coefficients times 1/c, the repair row
@@ -636,22 +394,14 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         }
         return 1;
     }
-#endif
     // solve jobs (ndet <= e): inputs the syndrome rows t_first .. t_last,
     // coefficients at 64 bytes per repair from t_first (ndet <= 64, so
-    // ndet * nin fits).  Fused plan: outputs and jobs from one counter, 8
-    // outputs per job, so the solve pass walks only real jobs; else in the
-    // system's unknown slots x .. (outputs at x + d).
+    // ndet * nin fits), kSwSolveOut outputs per job, in the system's unknown
+    // slots x .. (outputs at x + d; a compact list of jobs, one atomic per
+    // system, measured 24 us slower on cfg7, r04)
     const uint32_t t_first = eq[0], nin = eq[p - 1] - t_first + 1;
     const uint64_t c0 = (uint64_t)t_first * kSwSmallE;
-#if FECGPU_SWD_FUSED && FECGPU_SWD_SOLVE_LIST
-    uint32_t ob = 0;
-    if (lane == 0) ob = atomicAdd(&a.ctr->nsolout, (uint32_t)(ndet + kSwSolveOut - 1) / kSwSolveOut * kSwSolveOut);
-    ob = __shfl(ob, 0);
-    const uint64_t o0 = ob, j0 = ob / kSwSolveOut;
-#else
     const uint64_t o0 = x, j0 = x;
-#endif
     if (det) {
         const int d = __popcll(dm & lanes_below(lane));
         uint8_t *cf = a.sol_coef + c0 + (uint64_t)d * nin;
@@ -681,11 +431,10 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
 
 // The system lost[x .. x + e) with candidate repairs [t_lo, t_hi): solved here
 // when its equations fit ME / MP (and the range of syndrome rows kSwSolveIn),
-// else queued for the next pass (mid, then long).
-// LOCAL (FECGPU_SWD_MIDLOCK): a system too large for ME / MP but within the
-// mid size is not queued; the call returns true and the caller solves it in
-// its workgroup's shared mid region.
-template <int ME, int MP, bool MID, bool LOCAL = false>
+// else queued for the long pass.  LOCAL: a system too large for ME / MP but
+// within the mid size (kSwSmallE) is not queued; the call returns true and the
+// caller solves it in its workgroup's shared mid region.
+template <int ME, int MP, bool LOCAL = false>
 __device__ bool sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, uint32_t x, uint32_t e,
                         uint64_t t_lo, uint64_t t_hi, int lane, uint32_t &rec, uint32_t &maxin) {
     bool fits = (int)e <= ME && (int)e < a.long_min;
@@ -711,15 +460,14 @@ __device__ bool sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, u
     if (!fits) {
         if (LOCAL && (int)e <= kSwSmallE && (int)e < a.long_min) return true;
         if (lane == 0) {
-            const bool to_mid = !MID && (int)e <= kSwSmallE && (int)e < a.long_min;
-            const uint32_t k = atomicAdd(to_mid ? &a.ctr->nmid : &a.ctr->nlong, 1u);
+            const uint32_t k = atomicAdd(&a.ctr->nlong, 1u);
             if (k < a.long_cap) {
                 SwLong L{};
                 L.x0 = x;
                 L.e = e;
                 L.t_lo = (uint32_t)t_lo;
                 L.t_hi = (uint32_t)t_hi;
-                (to_mid ? a.mids : a.longs)[k] = L;
+                a.longs[k] = L;
             } else {
                 dec_err(a, kSwErrCapacity);
             }
@@ -755,27 +503,19 @@ __device__ __forceinline__ void block_counts(const SwDecArgs &a, uint32_t rec, u
     }
 }
 
-// Thread per repair: the RFC 8681 coefficients of every received repair whose
-// window holds a lost source, into its syndrome coefficient row.  The system
-// passes then read them (small_solve moves the unknowns' entries into A and
-// zeroes them); drawn here, every lane of a wave draws one, instead of a
-// wave per system drawing its few equations' on as many lanes.  The
-// long-system pass draws its own rows again (and overwrites these).
+// The RFC 8681 coefficients of a received repair whose window holds a lost
+// source, into its syndrome coefficient row (the plan, a thread per repair).
+// The system pass then reads them (small_solve moves the unknowns' entries
+// into A and zeroes them): every lane of a wave draws one, instead of a wave
+// per system drawing its few equations' on as many lanes.  The long-system
+// pass draws its own rows again (and overwrites these).
 __device__ __forceinline__ void draw_row(const SwDecArgs &a, uint64_t t, const fecgpu_sw_repair &h) {
     uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + t * kSwCoefPitch);
     rlc_words(a, h, [&](uint32_t q, uint32_t w) { cc[q] = w; });
 }
 
-__global__ __launch_bounds__(kBlock) void sw_dec_coef_kernel(SwDecArgs a) {
-    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= a.nrep || (a.ctr->err & 1u) || !a.rep_present[t]) return;
-    const fecgpu_sw_repair h = a.hdr[t];
-    if (!holds_any(a, h)) return;
-    draw_row(a, t, h);
-}
-
 // ======================================================= fused plan ===
-// One launch for the whole plan (FECGPU_SWD_FUSED): a block per chunk of
+// One launch for the whole plan: a block per chunk of
 // kPlanChunk sources, in ticket order, chained by a decoupled look-back over
 // (lost sources, farthest reach, repairs, widest window | error bits) so no
 // pass waits for a separate scan.  Per chunk: its repairs' header range (the
@@ -834,7 +574,7 @@ __device__ __forceinline__ LbRec lb_read(const uint4 *src2) {
 // holding it with a nonzero coefficient there (the small solver's choice), and
 // x = s_t / c: a combine job in syndrome slot nrep + (x's lost index) over t's
 // window with the coefficients times 1/c and t's row times 1/c (as
-// FECGPU_SWD_FUSE1).  lkind[x] tells the system pass what is left: 0 a member
+// small_solve's one-unknown case).  lkind[x] tells the system pass what is left: 0 a member
 // of a larger system, 1 recovered here, 2 a larger system's first unknown,
 // 3 alone but undetermined.
 __device__ __forceinline__ uint8_t coef_at(const SwDecArgs &a, const fecgpu_sw_repair &h, uint32_t j) {
@@ -928,7 +668,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         for (uint64_t t = h0 + tid; t < h1; t += kBlock) {
             a.syn_jobs[t] = E;
             const fecgpu_sw_repair h = a.hdr[t];
-            bad |= h.nss < 1 || h.nss > kSwMaxWindow || h.dt > 15 || h.fss > a.nsrc || a.nsrc - h.fss < h.nss;
+            bad |= !hdr_ok(h, a.nsrc);
             if (t > 0 && a.hdr[t - 1].fss > h.fss) bad = true;
         }
     }
@@ -1225,7 +965,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         for (uint64_t t = t0 + (tid - 64); t < t1; t += kBlock - 64) {
             if (!a.rep_present[t]) continue;
             const fecgpu_sw_repair h = a.hdr[t];
-            if (h.fss < i0 || h.fss >= i1 || h.nss < 1 || h.nss > kSwMaxWindow || a.nsrc - h.fss < h.nss) continue;
+            if (h.fss < i0 || h.fss >= i1 || !hdr_ok(h, a.nsrc)) continue;
             const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
             if (before(hi) > before(lo)) draw_row(a, t, h);
         }
@@ -1241,11 +981,14 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                 const auto rfirst = [&](uint64_t p) -> uint64_t {
                     return p < i0 ? s_rfb[p - (i0 - kPlanHalo)] : s_rf[p - i0];
                 };
-                const uint64_t ta = rfirst(lo), te = rfirst(i + 1);
+                // (clamped to the headers this block searched: with a bad or
+                // unordered list the counts need not add up, and the call is
+                // void anyway, but no read may leave the arrays)
+                const uint64_t ta = max(rfirst(lo), tb), te = min(rfirst(i + 1), t1);
                 for (uint64_t t = ta; t < te; t++) {
                     const uint8_t rpt = a.rep_present[t];  // both loads in one round trip
                     const fecgpu_sw_repair h = a.hdr[t];
-                    if (!rpt) continue;
+                    if (!rpt || !hdr_ok(h, a.nsrc)) continue;
                     if (h.fss > i || h.fss + h.nss <= i) continue;
                     const uint32_t j = (uint32_t)(i - h.fss);
                     const uint8_t cj = coef_at(a, h, j);
@@ -1281,9 +1024,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             if ((lostm >> j) & 1u) {
                 a.lost[off] = (uint32_t)i;
                 a.reachL[off] = run;
-#if !FECGPU_SWD_SOLVE_LIST
                 a.sol_jobs[off] = E;  // solve jobs in the unknowns' slots: empty unless filled
-#endif
                 off++;
             }
         }
@@ -1418,42 +1159,39 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
 #endif
 }
 
-// A wave per lost source; the waves at a system start find its extent and
-// solve it (tiny) or queue it (mid, long).
-#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS && FECGPU_SWD_MIDLOCK
-constexpr int kSysE = kSwTinyE, kSysP = kSwTinyP;  // per wave; mid regions per block, taken by a lock
-constexpr int kSysMid = FECGPU_SWD_MIDLOCK;
-#elif FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS
-constexpr int kSysE = kSwSmallE, kSysP = kSwSmallP;  // the system pass's LDS per wave
-#else
-constexpr int kSysE = kSwTinyE, kSysP = kSwTinyP;
-#endif
+// A wave per listed start of a larger system (the plan's start list): its
+// extent, then solved (tiny or mid) or queued (long).  LDS: 3 KB tiny regions
+// per wave and kSysMid mid-size regions per block under LDS locks (cfg7, r04:
+// a 16 KB mid region per wave, 2 blocks per CU, measured 0.214 vs 0.207 ms
+// per call at 2 % loss, 1.73 vs 1.75 at 10 %, against 3 blocks per CU here).
+constexpr int kSysMid = 2;
 __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     __shared__ GfLds g;
-    __shared__ SysLds<kSysE, kSysP> s_sys[kBlock / 64];
-#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS && FECGPU_SWD_MIDLOCK
+    __shared__ SysLds<kSwTinyE, kSwTinyP> s_sys[kBlock / 64];
     __shared__ SysLds<kSwSmallE, kSwSmallP> s_mid[kSysMid];
     __shared__ int s_lock[kSysMid];
     if (threadIdx.x < kSysMid) s_lock[threadIdx.x] = 0;
-#endif
     gf_load(g);
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (a.ctr->err & 1u) return;
+    if (a.ctr->err & kSwErrHeader) {
+        // a bad or unordered header list: the call recovers nothing and the
+        // statuses are the arrival flags.  The plan's blocks finished the
+        // one-unknown systems of their chunks before every chunk's headers were
+        // checked, so their statuses are undone here (the combine launches
+        // stand down on the same flag, and write nothing).
+        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < a.nsrc; i += (uint64_t)gridDim.x * kBlock)
+            a.stat[i] = a.src_present[i] ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
+        return;
+    }
     const uint32_t nlost = a.ctr->nlost, wmax = max(1u, a.ctr->wmax);
     const uint64_t nwaves = (uint64_t)gridDim.x * (kBlock / 64);
     uint32_t rec = 0, maxin = 0;  // this wave's recovered count, widest solve
-#if FECGPU_SWD_FUSED
     // the plan solved the one-unknown systems and listed the larger ones' starts
     const uint32_t nstart = a.ctr->nstart;
     for (uint64_t k = (uint64_t)blockIdx.x * (kBlock / 64) + wave; k < nstart; k += nwaves) {
         const uint64_t x = a.starts[k];
         const uint32_t lx = a.lost[x];
-#else
-    for (uint64_t x = (uint64_t)blockIdx.x * (kBlock / 64) + wave; x < nlost; x += nwaves) {
-        const uint32_t lx = a.lost[x];
-        if (x > 0 && a.reachL[x - 1] > lx) continue;  // not a system start (uniform)
-#endif
         // extent: up to the next start
         uint32_t e = 1;
         for (;;) {
@@ -1469,45 +1207,19 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
         const uint32_t last = a.lost[x + e - 1];
         // candidate repairs: fss in [lx - wmax + 1, last]
         const uint64_t t_lo = a.rcnt[lx >= wmax ? lx - wmax + 1 : 0], t_hi = a.rcnt[(uint64_t)last + 1];
-        // one pass (FECGPU_SWD_ONEPASS): up to the mid size here, longer ones to the long pass
-#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS && FECGPU_SWD_MIDLOCK
         // tiny systems in the wave's own 3 KB; a mid-size one takes the block's
-        // shared region (lane 0 spins on an LDS lock, the wave waits with it)
-        if (sys_one<kSysE, kSysP, false, true>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin)) {
+        // shared region (lane 0 spins on an LDS lock, the wave waits with it);
+        // longer ones go to the long pass
+        if (sys_one<kSwTinyE, kSwTinyP, true>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin)) {
             const int m = wave % kSysMid;  // waves m, m + kSysMid, ... share region m
             if (lane == 0)
                 while (atomicCAS(&s_lock[m], 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
             SWD_WAVE_SYNC();
-            sys_one<kSwSmallE, kSwSmallP, true>(a, g, s_mid[m], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin);
+            sys_one<kSwSmallE, kSwSmallP>(a, g, s_mid[m], (uint32_t)x, e, t_lo, t_hi, lane, rec, maxin);
             SWD_WAVE_SYNC();
             __threadfence_block();  // the region's LDS traffic done before the next holder
             if (lane == 0) atomicExch(&s_lock[m], 0);
         }
-#else
-        sys_one<kSysE, kSysP, FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS>(a, g, s_sys[wave], (uint32_t)x, e, t_lo, t_hi,
-                                                                      lane, rec, maxin);
-#endif
-    }
-    block_counts(a, rec, maxin, lane, wave);
-}
-
-// The queued systems too wide for the tiny pass: a wave each, up to 64
-// unknowns and 96 equations; wider ones go on to the long-system pass.
-__global__ __launch_bounds__(kBlock) void sw_dec_mid_kernel(SwDecArgs a) {
-    __shared__ GfLds g;
-    __shared__ SysLds<kSwSmallE, kSwSmallP> s_sys[kBlock / 64];
-    // nothing queued for this block (the common case): out before the tables
-    // (a whole block leaves together: the counters are the previous kernels')
-    if ((a.ctr->err & 1u) || (uint64_t)blockIdx.x * (kBlock / 64) >= min(a.ctr->nmid, (uint32_t)a.long_cap)) return;
-    gf_load(g);
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (a.ctr->err & 1u) return;
-    const uint32_t nmid = min(a.ctr->nmid, (uint32_t)a.long_cap);
-    uint32_t rec = 0, maxin = 0;
-    for (uint32_t k = blockIdx.x * (kBlock / 64) + wave; k < nmid; k += gridDim.x * (kBlock / 64)) {
-        const SwLong L = a.mids[k];
-        sys_one<kSwSmallE, kSwSmallP, true>(a, g, s_sys[wave], L.x0, L.e, L.t_lo, L.t_hi, lane, rec, maxin);
     }
     block_counts(a, rec, maxin, lane, wave);
 }
@@ -2090,36 +1802,14 @@ hipError_t launch_rlc_table(uint8_t *tab, hipStream_t s) {
 }
 
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
-#if FECGPU_SWD_FUSED
     hipLaunchKernelGGL(sw_dec_plan_kernel, dim3((unsigned)((a.nsrc + kPlanChunk - 1) / kPlanChunk)), dim3(kBlock), 0, s,
                        a);
     if (a.nrep) {
-#else
-    if (a.nrep) hipLaunchKernelGGL(sw_dec_hdr_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(sw_dec_count_kernel, dim3(a.nchunk), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(sw_dec_scan_kernel, dim3(1), dim3(1024), 0, s, a.chunk, a.nchunk, 3, 1, &a.ctr->nlost);
-    hipLaunchKernelGGL(sw_dec_lost_kernel, dim3(a.nchunk), dim3(kBlock), 0, s, a);
-    if (a.nrep) {
-#if FECGPU_SWD_COEF
-        hipLaunchKernelGGL(sw_dec_coef_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
-#endif
-#endif
         // a wave per lost source at most; persistent beyond what fits the chip
+        // (two shared mid regions, ~30 KB per block with the tiny ones: 3 per CU)
         const uint64_t want = (a.nsrc + kBlock / 64 - 1) / (kBlock / 64);
-#if FECGPU_SWD_FUSED && FECGPU_SWD_ONEPASS
-        // mid-size LDS per wave (64 KB per block): two blocks per CU; with the
-        // shared mid region (~30 KB per block) five
-        const unsigned grid = (unsigned)std::max<uint64_t>(
-            1, std::min<uint64_t>(want, (uint64_t)cu_count() * (FECGPU_SWD_MIDLOCK == 1   ? 5
-                                                                : FECGPU_SWD_MIDLOCK == 2 ? 3
-                                                                                          : 2)));
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 3));
         hipLaunchKernelGGL(sw_dec_sys_kernel, dim3(grid), dim3(kBlock), 0, s, a);
-#else
-        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cu_count() * 6));
-        hipLaunchKernelGGL(sw_dec_sys_kernel, dim3(grid), dim3(kBlock), 0, s, a);
-        hipLaunchKernelGGL(sw_dec_mid_kernel, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(a.long_cap, (uint64_t)cu_count() * 2))),
-                           dim3(kBlock), 0, s, a);
-#endif
     }
     return hipGetLastError();
 }

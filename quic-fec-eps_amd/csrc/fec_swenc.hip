@@ -27,30 +27,17 @@ namespace fecgpu {
 namespace {
 
 constexpr int kSwsU = kSwStreamU;
-#ifndef FECGPU_SWS_WAVE_LDS_KB
-#define FECGPU_SWS_WAVE_LDS_KB 12  // multiply-table LDS per wave of a workgroup (capped by the budget)
-#endif
-constexpr uint32_t kSwsWaveLds = FECGPU_SWS_WAVE_LDS_KB << 10;
-#ifndef FECGPU_SWS_AMAX
-#define FECGPU_SWS_AMAX 4  // accumulator slots compiled (a segment needing more takes P > 1 passes)
-#endif
-constexpr int kSwsAmax = FECGPU_SWS_AMAX < kSwSlots ? FECGPU_SWS_AMAX : kSwSlots;
-#ifndef FECGPU_SWS_TPF
-#define FECGPU_SWS_TPF 0  // multiply tables read one source ahead (A/B: 0.35 vs 0.24 ms cfg7, registers)
-#endif
-#ifndef FECGPU_SWS_PINGPONG
-#define FECGPU_SWS_PINGPONG 1  // row buffers trade roles between batches (else copied)
-#endif
-#ifndef FECGPU_SWS_LDSBATCH
-#define FECGPU_SWS_LDSBATCH 0  // a source pair's tables for every slot loaded before any product
-                               // (108 VGPRs instead of 73: cfg7 encode 0.287 vs 0.213 ms, r04: off)
-#endif
-#ifndef FECGPU_SWS_BUF
-#define FECGPU_SWS_BUF 1  // source rows by buffer loads (scalar row offsets)
-#endif
+// multiply-table LDS per wave of a workgroup (capped by the budget)
+constexpr uint32_t kSwsWaveLds = 12u << 10;
+// accumulator slots compiled (a segment needing more takes P > 1 passes)
+constexpr int kSwsAmax = 4 < kSwSlots ? 4 : kSwSlots;
+// Measured and removed (r05): tables read one source ahead (0.35 vs 0.24 ms on
+// cfg7, registers), a source pair's tables for every slot loaded before any
+// product (108 VGPRs instead of 73: 0.287 vs 0.213 ms), 4-entry tables in
+// global memory read by scalar loads (0.45 vs 0.214 ms: four v_perm per
+// product and a scalar-load wait per (source, slot)).
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(4))) const u32x4 *k4p;  // uniform loads: s_load_dwordx4
 
 #define SWS_WAVE_SYNC()                                         \
     do {                                                        \
@@ -59,37 +46,16 @@ typedef __attribute__((address_space(4))) const u32x4 *k4p;  // uniform loads: s
     } while (0)
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(1))) const uint32_t *g32c;
 typedef __attribute__((address_space(1))) uint32_t *g32;
-typedef __attribute__((address_space(1))) const u32x2 *g64c;
 typedef __attribute__((address_space(1))) u32x2 *g64;
 
-// C dwords of a lane: one load / store for C = 1, 2, 4 (4: 16-B aligned, the
-// rows are), dword by dword for 3 and 5 (4-B aligned)
-typedef __attribute__((address_space(1))) const u32x4 *g128c;
+// C dwords of a lane: one store for C = 1, 2, 4 (4: 16-B aligned, the rows
+// are), dword by dword for 3 and 5 (4-B aligned)
 typedef __attribute__((address_space(1))) u32x4 *g128;
-template <int C>
-__device__ __forceinline__ void ldc(const uint8_t *p, uint32_t (&x)[C]) {
-    if constexpr (C == 1) {
-        x[0] = *(g32c)(p);
-    } else if constexpr (C == 2) {
-        const u32x2 v = *(g64c)(p);
-        x[0] = v.x;
-        x[1] = v.y;
-    } else if constexpr (C == 4) {
-        const u32x4 v = *(g128c)(p);
-        x[0] = v.x;
-        x[1] = v.y;
-        x[2] = v.z;
-        x[3] = v.w;
-    } else {
-#pragma unroll
-        for (int d = 0; d < C; d++) x[d] = ((g32c)(p))[d];
-    }
-}
-// Buffer loads: the resource (a batch's first row, scalar) plus a scalar row
-// offset plus this lane's column offset, no per-load address arithmetic on
-// the vector ALU.  Word 3 of the resource: raw 32-bit data on gfx9.
+// Source rows by buffer loads: the resource (a batch's first row, scalar) plus
+// a scalar row offset plus this lane's column offset, no per-load address
+// arithmetic on the vector ALU (global loads measured 3 % slower, r03).  Word
+// 3 of the resource: raw 32-bit data on gfx9.
 constexpr int kRsrcWord3 = 0x00020000;
 template <int C>
 __device__ __forceinline__ void ldc_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t (&x)[C]) {
@@ -153,7 +119,6 @@ struct SwsPlan {
 };
 
 __device__ __forceinline__ void sws_plan(const SwStreamArgs &a, SwsPlan &pl, uint8_t *CB, uint64_t j0, int n, int lane) {
-    // CB null: the tables are in global memory (FECGPU_SWS_SGPR), no coefficients here
     const int W = a.max_window;
     uint64_t fss = 0, end = 0;
     bool ne = false;
@@ -173,7 +138,7 @@ __device__ __forceinline__ void sws_plan(const SwStreamArgs &a, SwsPlan &pl, uin
         const int v = __popcll(bne & below);
         pl.fe[v] = make_uint2((uint32_t)(fss - lo), (uint32_t)(end - lo));
         pl.out[v] = (uint16_t)lane;
-        if (CB) rlc_coefs_tab(a.rlc, h.key, (int)(end - fss), min((uint32_t)h.dt, 15u), CB + (size_t)v * W);
+        rlc_coefs_tab(a.rlc, h.key, (int)(end - fss), min((uint32_t)h.dt, 15u), CB + (size_t)v * W);
     }
     if (lane < n && !ne) pl.empty[__popcll(bem & below)] = (uint16_t)lane;
     SWS_WAVE_SYNC();
@@ -233,70 +198,6 @@ __device__ __forceinline__ void gmac_c(uint32_t (&acc)[C], const SplitC<C> &s, u
                  __builtin_amdgcn_perm(tc, tc, s.c[d]);
 }
 
-// 4-entry tables: c*x = Q0[x & 3] ^ Q1[(x >> 2) & 3] ^ Q2[(x >> 4) & 3] ^ Q3[x >> 6]
-// with Qk[b] = c * (b << 2k): Q0 = TA's low dword, Q3 = TC (make_coef_tab)
-template <int C>
-struct Split4 {
-    uint32_t i[4][C];
-};
-template <int C>
-__device__ __forceinline__ Split4<C> split4(const uint32_t (&x)[C]) {
-    Split4<C> s;
-#pragma unroll
-    for (int d = 0; d < C; d++) {
-        s.i[0][d] = x[d] & 0x03030303u;
-        s.i[1][d] = (x[d] >> 2) & 0x03030303u;
-        s.i[2][d] = (x[d] >> 4) & 0x03030303u;
-        s.i[3][d] = (x[d] >> 6) & 0x03030303u;
-    }
-    return s;
-}
-__device__ __forceinline__ u32x4 quad_tab(uint32_t c) {
-    uint32_t p[8];
-    p[0] = c & 0xFFu;
-    for (int b = 1; b < 8; b++) p[b] = gf_xtime(p[b - 1]);
-    u32x4 q;
-    q.x = (p[0] << 8) ^ (p[1] << 16) ^ ((p[0] ^ p[1]) << 24);
-    q.y = (p[2] << 8) ^ (p[3] << 16) ^ ((p[2] ^ p[3]) << 24);
-    q.z = (p[4] << 8) ^ (p[5] << 16) ^ ((p[4] ^ p[5]) << 24);
-    q.w = (p[6] << 8) ^ (p[7] << 16) ^ ((p[6] ^ p[7]) << 24);
-    return q;
-}
-
-// The global tables (FECGPU_SWS_SGPR): a thread per repair draws its clipped
-// window's coefficients and writes their 4-entry tables after a run of
-// kSwStreamU zero tables; entries past its window are zero; the array starts
-// and ends with kSwStreamU zero tables (sw_stream_gtab_bytes).
-__global__ __launch_bounds__(kBlock) void sws_tab_kernel(SwStreamArgs a) {
-    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    u32x4 *G = reinterpret_cast<u32x4 *>(a.gtab);
-    const int W = a.max_window, RW = W + kSwsU;
-    const u32x4 z = {0u, 0u, 0u, 0u};
-    if (t == 0)
-        for (int i = 0; i < kSwsU; i++) {
-            G[i] = z;
-            G[kSwsU + a.nrep * (uint64_t)RW + i] = z;
-        }
-    if (t >= a.nrep) return;
-    const fecgpu_sw_repair h = a.hdr[t];
-    const uint64_t fss = min(h.fss, a.nsrc);
-    const int nss = (int)min((uint64_t)min((int)h.nss, W), a.nsrc - fss);
-    u32x4 *row = G + kSwsU + t * (uint64_t)RW;
-    for (int i = 0; i < kSwsU; i++) row[i] = z;
-    Tinymt32 st;
-    tinymt32_init(st, h.key & 0xFFFFu);
-    const uint32_t dt = min((uint32_t)h.dt, 15u);
-    for (int q = 0; q < W; q++) {
-        uint32_t c = 0;
-        if (q < nss && (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt)) {
-            do {
-                c = tinymt32_u32(st) & 0xFFu;
-            } while (c == 0);
-        }
-        row[kSwsU + q] = c ? quad_tab(c) : z;
-    }
-}
-
 // Pass p of a segment over this lane's column (byte offset loff in a row):
 // A slots, repairs p, p + P, ... in slot order; every window is met in source
 // order, a slot's repair is stored when its last source is in.  Sources go in
@@ -317,11 +218,10 @@ __device__ __forceinline__ void sws_window(const SwsPlan &pl, uint32_t v, uint32
     }
 }
 
-template <int A, int C, bool G>
+template <int A, int C>
 __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &pl, const uint4 *AB,
                                          const uint32_t *TC, uint64_t j0, int p, int P, uint32_t loff,
                                          bool live) {
-    const k4p GT = (k4p)a.gtab;  // G: the global tables
     constexpr int U = kSwsU;
     static_assert(U % 2 == 0, "sources go in pairs");
     const uint32_t RW = (uint32_t)a.max_window + U, nn = rfl((uint32_t)pl.nn), stepv = (uint32_t)(A * P);
@@ -346,16 +246,11 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
     // for the rows it had just prefetched (s_waitcnt vmcnt(7..0) in its body).
     auto load = [&](uint32_t s0, uint32_t (&x)[U][C]) __attribute__((always_inline)) {
         s0 = rfl(min(s0, hi - 1));
-#if FECGPU_SWS_BUF
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t *>(base + (uint64_t)s0 * stride), 0, (int)(U * stride), kRsrcWord3);
         const uint32_t last = rfl(hi - 1 - s0);  // scalar: rows past it reload row hi - 1
 #pragma unroll
         for (int i = 0; i < U; i++) ldc_buf<C>(r, loff, min((uint32_t)i, last) * (uint32_t)stride, x[i]);
-#else
-#pragma unroll
-        for (int i = 0; i < U; i++) ldc<C>(base + (uint64_t)min(s0 + (uint32_t)i, hi - 1) * stride + loff, x[i]);
-#endif
     };
     // one batch: multiply the rows in X, while the next batch's rows load into Y
     auto batch = [&](uint32_t (&X)[U][C], uint32_t (&Y)[U][C]) __attribute__((always_inline)) -> bool {
@@ -370,17 +265,11 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
         // before the window; repair 0's zero run while the window is ahead)
         const uint4 *tab[A];
         const uint32_t *tcb[A];
-        uint64_t gb[A];  // G: entry of source s of slot m's repair (0: the leading zero run)
 #pragma unroll
         for (int m = 0; m < A; m++) {
-            if constexpr (G) {
-                const uint64_t t = j0 + (dense ? v[m] : rfl(pl.out[min(v[m], (uint32_t)kSwSeg - 1)]));
-                gb[m] = f[m] < sn ? (uint64_t)kSwsU + t * RW + U + s - f[m] : 0ull;
-            } else {
-                const uint32_t tb = f[m] < sn ? v[m] * RW + U + s - f[m] : 0u;
-                tab[m] = AB + tb;
-                tcb[m] = TC + tb;
-            }
+            const uint32_t tb = f[m] < sn ? v[m] * RW + U + s - f[m] : 0u;
+            tab[m] = AB + tb;
+            tcb[m] = TC + tb;
         }
         // a batch cut short by a window end multiplies zero rows past it (their
         // table reads stay inside the LDS tables: kSwsU spare entries at the end)
@@ -390,62 +279,19 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
 #pragma unroll
                 for (int d = 0; d < C; d++) X[i][d] = (uint32_t)i < L ? X[i][d] : 0u;
         }
-        if constexpr (G) {
-            // per source and slot: one s_load_dwordx4 of 4 tables, 4 v_perm
-            // with an SGPR table each, two 3-input XORs
-#pragma unroll
-            for (int i = 0; i < U; i++) {
-                const Split4<C> q = split4<C>(X[i]);
-#pragma unroll
-                for (int m = 0; m < A; m++) {
-                    const u32x4 tq = GT[gb[m] + i];
-#pragma unroll
-                    for (int d = 0; d < C; d++) {
-                        uint32_t t = xor3s(acc[m][d], __builtin_amdgcn_perm(tq.x, tq.x, q.i[0][d]),
-                                           __builtin_amdgcn_perm(tq.y, tq.y, q.i[1][d]));
-                        acc[m][d] = xor3s(t, __builtin_amdgcn_perm(tq.z, tq.z, q.i[2][d]),
-                                          __builtin_amdgcn_perm(tq.w, tq.w, q.i[3][d]));
-                        asm volatile("" : "+v"(acc[m][d]));
-                    }
-                }
-            }
-        } else
         // sources in pairs: the six table lookups of two products fold into
         // the accumulator with three 3-input XORs
 #pragma unroll
         for (int i = 0; i < U; i += 2) {
             const SplitC<C> s0 = split_c<C>(X[i]), s1 = split_c<C>(X[i + 1]);
-#if FECGPU_SWS_LDSBATCH
-            // every slot's tables for the pair in flight at once (one LDS wait,
-            // not one per slot)
-            uint4 A0[A], A1[A];
-            uint32_t C0[A], C1[A];
 #pragma unroll
             for (int m = 0; m < A; m++) {
-                A0[m] = tab[m][i];
-                A1[m] = tab[m][i + 1];
-                C0[m] = tcb[m][i];
-                C1[m] = tcb[m][i + 1];
-            }
-#pragma unroll
-            for (int m = 0; m < A; m++) {
-                asm("" : "+v"(A0[m].x), "+v"(A0[m].y), "+v"(A0[m].z), "+v"(A0[m].w), "+v"(C0[m]));
-                asm("" : "+v"(A1[m].x), "+v"(A1[m].y), "+v"(A1[m].z), "+v"(A1[m].w), "+v"(C1[m]));
-            }
-#endif
-#pragma unroll
-            for (int m = 0; m < A; m++) {
-#if FECGPU_SWS_LDSBATCH
-                const uint4 a0 = A0[m], a1 = A1[m];
-                const uint32_t c0 = C0[m], c1 = C1[m];
-#else
                 uint4 a0 = tab[m][i], a1 = tab[m][i + 1];
                 uint32_t c0 = tcb[m][i], c1 = tcb[m][i + 1];
                 // tables stay in vector registers (uniform values would be
                 // moved to scalar ones with a readfirstlane each)
                 asm("" : "+v"(a0.x), "+v"(a0.y), "+v"(a0.z), "+v"(a0.w), "+v"(c0));
                 asm("" : "+v"(a1.x), "+v"(a1.y), "+v"(a1.z), "+v"(a1.w), "+v"(c1));
-#endif
 #pragma unroll
                 for (int d = 0; d < C; d++) {
                     uint32_t t = xor3s(acc[m][d], __builtin_amdgcn_perm(a0.y, a0.x, s0.a[d]),
@@ -483,7 +329,6 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
     };
     uint32_t XA[U][C], XB[U][C];
     load(s, XA);
-#if FECGPU_SWS_PINGPONG
     // two batches per trip, the row buffers trading roles (no copies); one
     // exit on a flag (a loop with two exits loses the bookkeeping's
     // uniformity: vector registers and readfirstlane loops around the loads)
@@ -492,17 +337,9 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
         go = batch(XA, XB);
         if (go) go = batch(XB, XA);
     }
-#else
-    while (batch(XA, XB)) {
-#pragma unroll
-        for (int i = 0; i < U; i++)
-#pragma unroll
-            for (int d = 0; d < C; d++) XA[i][d] = XB[i][d];
-    }
-#endif
 }
 
-template <int C, bool G>
+template <int C>
 __global__ __launch_bounds__(512) void sw_stream_kernel(SwStreamArgs a) {
     extern __shared__ uint4 sws_dyn[];
     __shared__ SwsPlan pl;
@@ -518,13 +355,13 @@ __global__ __launch_bounds__(512) void sw_stream_kernel(SwStreamArgs a) {
     for (uint64_t sg = sb; sg < se; sg++) {
         const uint64_t j0 = sg * (uint64_t)a.segcap;
         const int n = (int)min((uint64_t)a.segcap, a.nrep - j0);
-        if (wave == 0) sws_plan(a, pl, G ? nullptr : CB, j0, n, lane);
+        if (wave == 0) sws_plan(a, pl, CB, j0, n, lane);
         __syncthreads();
         const int nn = (int)rfl((uint32_t)pl.nn);
         // every entry a batch may read is a table: zero runs, coefficients,
         // zeros past a window (a cut-short batch reads up to kSwsU - 1 entries
         // on, and multiplies them by zero rows: the zero table gives 0)
-        for (int i = tid; !G && i < nn * RW + kSwsU; i += blockDim.x) {
+        for (int i = tid; i < nn * RW + kSwsU; i += blockDim.x) {
             const int v = i / RW, q = i - v * RW - kSwsU;
             CoefTab ct{0u, 0u, 0u, 0u, 0u};
             if (q >= 0 && v < nn && (uint32_t)q < pl.fe[v].y - pl.fe[v].x) ct = make_coef_tab(CB[v * W + q]);
@@ -544,18 +381,10 @@ __global__ __launch_bounds__(512) void sw_stream_kernel(SwStreamArgs a) {
             const uint32_t loff = min(cu, a.ncu - 1) * 4u * C;
             for (int p = 0; p < P; p++) {
                 switch (A) {
-                case 1: sws_pass<1, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 2: sws_pass<2, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 3: sws_pass<3, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
-#if FECGPU_SWS_AMAX > 4
-                case 4: sws_pass<4, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 5: sws_pass<5, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 6: sws_pass<6, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                case 7: sws_pass<7, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
-                default: sws_pass<8, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
-#else
-                default: sws_pass<4, C, G>(a, pl, AB, TC, j0, p, P, loff, live); break;
-#endif
+                case 1: sws_pass<1, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                case 2: sws_pass<2, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                case 3: sws_pass<3, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
+                default: sws_pass<kSwsAmax, C>(a, pl, AB, TC, j0, p, P, loff, live); break;
                 }
             }
         }
@@ -594,21 +423,20 @@ uint64_t resident(const void *fn, int C, uint32_t block, uint32_t lds) {
 }
 }  // namespace
 
-template <int C, bool G>
+template <int C>
 const void *sws_fn() {
-    return reinterpret_cast<const void *>(sw_stream_kernel<C, G>);
+    return reinterpret_cast<const void *>(sw_stream_kernel<C>);
 }
 
 hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t s) {
     if (a.nrep == 0) return hipSuccess;
-    const bool G = FECGPU_SWS_SGPR && a.gtab && C <= 2;
     const void *fn = nullptr;
     switch (C) {
-        case 1: fn = G ? sws_fn<1, true>() : sws_fn<1, false>(); break;
-        case 2: fn = G ? sws_fn<2, true>() : sws_fn<2, false>(); break;
-        case 3: fn = sws_fn<3, false>(); break;
-        case 4: fn = sws_fn<4, false>(); break;
-        case 5: fn = sws_fn<5, false>(); break;
+        case 1: fn = sws_fn<1>(); break;
+        case 2: fn = sws_fn<2>(); break;
+        case 3: fn = sws_fn<3>(); break;
+        case 4: fn = sws_fn<4>(); break;
+        case 5: fn = sws_fn<5>(); break;
         default: return hipErrorInvalidValue;
     }
     const int W = std::max(1, a.max_window);
@@ -620,13 +448,8 @@ hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t 
     // `budget`): a one-wave workgroup (C = 5 over a 1200-B row) with the whole
     // budget would leave 3 waves on a CU
     budget = std::min<uint32_t>(budget, std::max<uint32_t>(1, a.cpass / 64) * kSwsWaveLds);
-    a.segcap = G ? kSwSeg : (int)std::max<uint32_t>(1, std::min<uint32_t>(kSwSeg, budget / sw_stream_rep_lds(W)));
-    a.lds = G ? 0u : sw_stream_lds(a.segcap, W);
-    if (G) {
-        hipLaunchKernelGGL(sws_tab_kernel, dim3((unsigned)((a.nrep + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
-        const hipError_t e0 = hipGetLastError();
-        if (e0 != hipSuccess) return e0;
-    }
+    a.segcap = (int)std::max<uint32_t>(1, std::min<uint32_t>(kSwSeg, budget / sw_stream_rep_lds(W)));
+    a.lds = sw_stream_lds(a.segcap, W);
     hipError_t e = hipSuccess;
     if (a.lds > 64u * 1024u) {
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds);
@@ -640,19 +463,13 @@ hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t 
     a.nseg = (a.nrep + a.segcap - 1) / a.segcap;
     const uint64_t grid = std::min<uint64_t>(a.nseg, R);
     const dim3 gd((unsigned)grid), bd(a.cpass);
-    const uint32_t lds = G ? 0u : a.lds;
+    const uint32_t lds = a.lds;
     switch (C) {
-        case 1:
-            if (G) hipLaunchKernelGGL((sw_stream_kernel<1, true>), gd, bd, lds, s, a);
-            else hipLaunchKernelGGL((sw_stream_kernel<1, false>), gd, bd, lds, s, a);
-            break;
-        case 2:
-            if (G) hipLaunchKernelGGL((sw_stream_kernel<2, true>), gd, bd, lds, s, a);
-            else hipLaunchKernelGGL((sw_stream_kernel<2, false>), gd, bd, lds, s, a);
-            break;
-        case 3: hipLaunchKernelGGL((sw_stream_kernel<3, false>), gd, bd, lds, s, a); break;
-        case 4: hipLaunchKernelGGL((sw_stream_kernel<4, false>), gd, bd, lds, s, a); break;
-        default: hipLaunchKernelGGL((sw_stream_kernel<5, false>), gd, bd, lds, s, a); break;
+        case 1: hipLaunchKernelGGL((sw_stream_kernel<1>), gd, bd, lds, s, a); break;
+        case 2: hipLaunchKernelGGL((sw_stream_kernel<2>), gd, bd, lds, s, a); break;
+        case 3: hipLaunchKernelGGL((sw_stream_kernel<3>), gd, bd, lds, s, a); break;
+        case 4: hipLaunchKernelGGL((sw_stream_kernel<4>), gd, bd, lds, s, a); break;
+        default: hipLaunchKernelGGL((sw_stream_kernel<5>), gd, bd, lds, s, a); break;
     }
     return hipGetLastError();
 }

@@ -3,20 +3,19 @@
 // through fecgpu_encode_batch / fecgpu_decode_batch (include/fecgpu.h: present
 // masks of ceil((k + r) / 64) words per window).
 //
-// The windows run through the sliding-window path's combine kernel
-// (fec_kernels.hip comb_kernel<8>): a job per window, its input rows one
-// contiguous range of the window, up to 8 outputs, a coefficient block
-// [nout][nin].
-//  * encode: inputs the k sources, outputs the r repairs, coefficients the
-//    code's parity rows P[r][k] (one block shared by every job);
+//  * encode: the runtime-mask bit-sliced kernel (fec_kernels.hip rbs4::, r >= 4)
+//    over every window's k sources, or else the sliding-window path's combine
+//    kernel (comb_kernel<8>) with a job per window: inputs the k sources,
+//    outputs the r repairs, coefficients the code's parity rows P[r][k] (one
+//    block whose tables every workgroup builds once);
 //  * decode: a wave per window plans it (wide_dec_plan_kernel): the missing
 //    sources m_u (e <= r), the system A[t][u] = P[sel_t][m_u] of every present
 //    repair reduced by Gauss-Jordan with pivot search (so an RLC window is
-//    recovered whenever its present repairs have rank e), and the decode
-//    matrix D[u][q] over all k + r rows of the window: received sources
-//    sum_c T[P_u][P_c] P[sel_c][q], the pivot repairs T[P_u][P_c], zero for
-//    missing sources and unused repairs (their rows are read and multiplied
-//    by zero).  The job writes x_u to the missing rows in place.
+//    recovered whenever its present repairs have rank e), the stage-2 block
+//    C[u][i] = T[P_u][c] for the repair i of pivot row c.  Stage 1: every
+//    repair's syndrome s_i = rep_i + sum_j P[i][j] src_j (the missing rows
+//    zeroed by the plan) by one coefficient block [P | I] for all windows;
+//    stage 2: x_u = sum_i C[u][i] s_i, a combine job per window.
 #include "fec_internal.h"
 
 namespace fecgpu {
@@ -25,16 +24,12 @@ namespace {
 
 __constant__ GfTables c_gfw = make_gf_tables();
 
-// FECGPU_WIDE_2STAGE (fec_internal.h): the one-launch decode built
-// (k + r + 1) x 161 B of tables per window, so 3 (k 120) or 1 (k 248) windows
-// per workgroup, 75 of its 256 lanes busy per 1200-B window; the two-stage one
-// builds [P | I]'s tables once per workgroup and its stage-2 jobs are 8 x 8.
-#ifndef FECGPU_WIDE_S2_KB
-#define FECGPU_WIDE_S2_KB 16  // two-stage decode, stage 2: LDS budget of a workgroup's window jobs (k120: 16 KB 1.656 vs 32 KB 1.683 ms)
-#endif
-#ifndef FECGPU_WIDE_SHARED
-#define FECGPU_WIDE_SHARED 1  // wide encode: parity-row tables shared by a workgroup's jobs
-#endif
+// (A one-launch decode with a job of all k + r rows per window built
+// (k + r + 1) x 161 B of tables per window: 3 (k 120) or 1 (k 248) windows
+// per workgroup, 75 of its 256 lanes busy per 1200-B window; k120 decode
+// 3.22 ms against 1.71 for the two stages, r04.)
+// stage 2: LDS budget of a workgroup's window jobs (k120: 16 KB 1.656 vs 32 KB 1.683 ms, r04)
+constexpr uint32_t kWideS2Budget = 16u << 10;
 
 #define WIDE_WAVE_SYNC()                                        \
     do {                                                        \
@@ -52,7 +47,7 @@ struct WideArgs {
     int k, r, nw;
     CombJob *jobs;   // [nwin]
     uint64_t *outs;  // [nwin][8] (encode: [nwin][r])
-    uint8_t *coef;   // decode: [nwin][8][k + r] (two-stage: [nwin][8][8], stage 2)
+    uint8_t *coef;   // decode: [nwin][8][8], stage 2
     // two-stage decode: stage-1 jobs [nwin] and outputs [nwin][r] (syndrome
     // rows in syn, [nwin][r][stride])
     CombJob *jobs1;
@@ -109,7 +104,7 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
         if (lane == 0) {
             a.status[w] = e == 0 ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
             a.jobs[w] = J;
-            if (FECGPU_WIDE_2STAGE) a.jobs1[w] = J;
+            a.jobs1[w] = J;
         }
         return;
     }
@@ -133,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
             if (lane == 0) {
                 a.status[w] = FECGPU_STATUS_UNRECOVERABLE;
                 a.jobs[w] = J;
-                if (FECGPU_WIDE_2STAGE) a.jobs1[w] = J;
+                a.jobs1[w] = J;
             }
             return;
         }
@@ -154,7 +149,6 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
             xr ^= wmul(s_exp, s_log, f, rq);
         }
     }
-#if FECGPU_WIDE_2STAGE
     // stage 2's block C[u][i] (8 x 8 per window): T[P_u][c] for the repair i
     // of pivot row c, else 0; the missing rows zeroed for stage 1
     {
@@ -191,42 +185,6 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
         J.coef_off = w * (uint64_t)(kMaxR * kMaxR) + 0;
         J.out_list = w * kMaxR;
         J.nin = (uint32_t)r;
-        J.nout = (uint32_t)e;
-        a.jobs[w] = J;
-        a.status[w] = FECGPU_STATUS_OK;
-    }
-    return;
-#endif
-    // D[u][q] over the window's n rows, entry idx = u * n + q; T[P_u][P_c] =
-    // xr of lane P_u * 8 + P_c, the repair of pivot row P_c = sel of row P_c
-    uint8_t *D = a.coef + w * (uint64_t)(kMaxR * n);
-    for (int base = 0; base < e * n; base += 64) {
-        const int idx = base + lane;
-        const int du = min(idx / n, e - 1), q = idx - du * n;
-        const int pu = __shfl(my_piv, du, 64);
-        uint32_t d = 0;
-        bool miss = false;
-        if (q < k) miss = !((pw[q >> 6] >> (q & 63)) & 1ull);
-        for (int c = 0; c < e; c++) {
-            const int pc = __shfl(my_piv, c, 64);
-            const uint32_t tv = __shfl(xr, (pu * 8 + pc) & 63, 64);
-            uint32_t rr = rep;
-            for (int i = 0; i < pc && rr; i++) rr &= rr - 1;
-            const int sc = __ffs(rr) - 1;  // repair of pivot row pc
-            if (q < k) {
-                if (!miss) d ^= wmul(s_exp, s_log, tv, a.P[(size_t)sc * k + q]);
-            } else if (q - k == sc) {
-                d = tv;
-            }
-        }
-        if (idx < e * n) D[idx] = (uint8_t)d;
-    }
-    if (lane < e) a.outs[w * kMaxR + lane] = w * a.wpitch + (uint64_t)s_m[wave][lane] * a.stride;
-    if (lane == 0) {
-        J.in_off = w * a.wpitch;
-        J.coef_off = w * (uint64_t)(kMaxR * n);
-        J.out_list = w * kMaxR;
-        J.nin = (uint32_t)n;
         J.nout = (uint32_t)e;
         a.jobs[w] = J;
         a.status[w] = FECGPU_STATUS_OK;
@@ -271,7 +229,6 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     constexpr uint32_t kBudget = 64u << 10;
-#if FECGPU_WIDE_2STAGE
     if (decode) {
         // (1) syndromes: every window's k + r rows times [P | I] (at P_dev + r k),
         // outputs the r syndrome rows: by plane picks (output i of window w at
@@ -316,13 +273,12 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
         c2.nin_max = r;
         c2.nout_max = kMaxR;
         c2.job_lds = comb_job_lds(r, kMaxR);
-        c2.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c2.job_lds, FECGPU_WIDE_S2_KB << 10)));
+        c2.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c2.job_lds, kWideS2Budget)));
         return launch_comb(c2, kMaxR, s);
     }
-#endif
     CombArgs c{};
     c.jobs = jobs;
-    c.coef = decode ? coef : P_dev;
+    c.coef = P_dev;
     c.outs = outs;
     c.in_base = win;
     c.out_base = win;
@@ -330,23 +286,17 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
     c.njobs = nwin;
     c.ncol = ncol;
     c.stride = stride;
-    c.nin_max = decode ? k + r : k;
-    c.nout_max = decode ? kMaxR : r;
+    c.nin_max = k;
+    c.nout_max = r;
     c.job_lds = comb_job_lds(c.nin_max, kMaxR);
-#if FECGPU_WIDE_SHARED
-    if (!decode) {
-        // every encode job multiplies by the same parity rows: one table block per
-        // workgroup, so the jobs per workgroup follow lane use alone (1200-B rows
-        // are 75 of a workgroup's 256 lanes)
-        c.shared_coef = 1;
-        // at most nwin / 1024 jobs each, so the grid keeps >= 4 workgroups per CU
-        const uint32_t cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxWpb, nwin / 1024));
-        const uint32_t room = std::min<uint32_t>(kBudget - comb_shared_lds(k, kMaxR), cap * comb_job_small_lds(kMaxR));
-        c.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, comb_job_small_lds(kMaxR), room)));
-        return launch_comb(c, kMaxR, s);
-    }
-#endif
-    c.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c.job_lds, kBudget)));
+    // every encode job multiplies by the same parity rows: one table block per
+    // workgroup, so the jobs per workgroup follow lane use alone (1200-B rows
+    // are 75 of a workgroup's 256 lanes)
+    c.shared_coef = 1;
+    // at most nwin / 1024 jobs each, so the grid keeps >= 4 workgroups per CU
+    const uint32_t cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxWpb, nwin / 1024));
+    const uint32_t room = std::min<uint32_t>(kBudget - comb_shared_lds(k, kMaxR), cap * comb_job_small_lds(kMaxR));
+    c.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, comb_job_small_lds(kMaxR), room)));
     return launch_comb(c, kMaxR, s);
 }
 

@@ -32,7 +32,7 @@ _MATRIX_IDS = {"cauchy": MATRIX_CAUCHY, "vandermonde": MATRIX_VANDERMONDE, "rlc"
 FRAMING_FIXED, FRAMING_LENPREFIX = 0, 1
 STATUS_OK, STATUS_UNRECOVERABLE = 0, 1
 F_HOST_PTRS, F_SYNC = 1, 2
-SW_ERR_HEADER, SW_ERR_CAPACITY = 1, 2  # fecgpu_sw_decode_errors flags
+SW_ERR_HEADER, SW_ERR_CAPACITY, SW_ERR_INTERNAL = 1, 2, 4  # fecgpu_sw_decode_errors flags
 MAX_K, MAX_R = 64, 8
 WORKLOAD_FIXED, WORKLOAD_MIXED = 0, 1
 ERASURE_NONE, ERASURE_EXACT, ERASURE_IID = 0, 1, 2

@@ -274,6 +274,19 @@ class HostBatch:
         return {"encode": n * (c.k + c.r) * c.stride,
                 "decode": n * (c.k * c.stride + 8 + 1) + e * c.stride}
 
+    def pcie_bytes(self) -> dict:
+        """Bytes per call in each PCIe direction (the link is full duplex, 63 GB/s
+        each way): encode copies the k source rows up (2-D copy) and the r repair
+        rows down; the zero-copy decode reads its k solving rows and the mask
+        over the link and writes the e recovered rows and the status back."""
+        import numpy as np
+        c, n = self.cfg, self.nwin
+        kmask = np.uint64((1 << c.k) - 1)
+        miss = (~self.present) & kmask
+        e = int(sum(int(((miss >> np.uint64(j)) & np.uint64(1)).sum()) for j in range(c.k)))
+        return {"encode": {"h2d": n * c.k * c.stride, "d2h": n * c.r * c.stride},
+                "decode": {"h2d": n * (c.k * c.stride + 8), "d2h": e * c.stride + n}}
+
     def verify(self, ctx: Context, w0: int) -> dict:
         import numpy as np
         c = self.cfg

@@ -151,12 +151,6 @@ for s in "$@"; do
                 for gsz in 2 4 8; do
                     step abgroup_g${gsz}_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify --sw-group $gsz
                 done
-            done ;;  # host-only: the decode plan's phases
-        abplan)  # cfg7: decode host plan on the caller alone vs the helper pool, interleaved twice
-            for rep in 1 2; do
-                FECGPU_PLAN_THREADS=1 step abplan_t1_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
-                step abplan_t4_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
-                FECGPU_PLAN_THREADS=8 step abplan_t8_$rep 300 python bench.py --config 7 --steps 50 --warmup 5 --cpu-seconds 0 --no-verify
             done ;;
         prof3) prof prof3 3 ;;
         prof4) prof prof4 4 ;;
@@ -179,6 +173,12 @@ for s in "$@"; do
         sqa*) c=${s#sqa}; pmc sqa$c $c SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
         sqb*) c=${s#sqb}; pmc sqb$c $c SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE ;;
         micro) step micro 600 python scripts/microbench.py ;;
+        clk*)  # clkN: effective shader clock (GRBM_GUI_ACTIVE / duration) and UTCL1 translation per dispatch
+            c=${s#clk}; pmc clk$c $c GRBM_GUI_ACTIVE GRBM_COUNT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU \
+                TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum ;;
+        cfg4probe) step cfg4probe 600 python scripts/cfg4_probe.py ABC ;;
+        listctr) step listctr 120 rocprofv3 -L ;;
+        benchdef) step benchdef 900 python bench.py ;;  # the driver's default command
         probe) step probe 300 ./scripts/stream_probe ;;
         layout) step layout 300 ./scripts/layout_probe ;;
         readp) step readp 300 ./scripts/read_probe ;;

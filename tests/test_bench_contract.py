@@ -16,10 +16,10 @@ def bench():
     return b
 
 
-def test_defaults_are_one_gpu_config2(bench, monkeypatch):
+def test_defaults_are_one_gpu_config3(bench, monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = bench.parse()
-    assert (a.gpus, a.config, a.dist_backend) == (1, 2, "nccl")
+    assert (a.gpus, a.config, a.dist_backend) == (1, 3, "nccl")
     assert a.steps > 0 and a.warmup > 0 and a.cpu_seconds > 0
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "7", "--warmup", "2"])
     a = bench.parse()

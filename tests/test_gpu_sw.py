@@ -528,6 +528,56 @@ def test_sw_decode_async_error_flags():
         c.close()
 
 
+@pytest.mark.parametrize("bad", ["swap", "nss300", "past_end", "dt16"])
+def test_sw_decode_bad_headers_recover_nothing(bad):
+    """A bad or unordered device header list: the plan's blocks
+    finish their chunks' one-unknown systems before every chunk's headers are
+    checked, so the combine launches must stand down and the statuses be
+    restored.  Several plan chunks (nsrc > 2048), one bad header near the end:
+    the asynchronous call raises SW_ERR_HEADER, every status equals the arrival
+    flag and no source byte changes; the synchronous call is INVALID_ARG."""
+    c = fecgpu.Context()
+    try:
+        nsrc, L, k, W = 9000, 64, 4, 32
+        stride = O.round_up(L, 16)
+        src = stream(nsrc, L, stride, 301)
+        hdr = hdr_array(N.sw_schedule(nsrc, k, W, key0=11, dt=15))
+        rep = O.sw_encode(src, hdr, L)
+        rng = np.random.default_rng(301)
+        sp = (rng.random(nsrc) >= 0.03).astype(np.uint8)   # mostly one-unknown systems
+        rp = np.ones(len(hdr), np.uint8)
+        t = len(hdr) - 40
+        if bad == "swap":
+            hdr[[t, t + 1]] = hdr[[t + 1, t]]
+            assert hdr[t]["fss"] > hdr[t + 1]["fss"]
+        elif bad == "nss300":
+            hdr[t]["nss"] = 300
+        elif bad == "past_end":
+            hdr[t]["fss"], hdr[t]["nss"] = nsrc - 2, 8
+        else:
+            hdr[t]["dt"] = 16
+        d = src.copy()
+        d[sp == 0] = 0xAB
+        d_src = torch.from_numpy(d).cuda()
+        d_st = torch.full((nsrc,), 9, dtype=torch.uint8, device="cuda")
+        args = (torch.from_numpy(sp).cuda(), torch.from_numpy(rep).cuda(), torch.from_numpy(rp).cuda(),
+                torch.from_numpy(hdr.view(np.uint8).copy()).cuda(), d_st)
+        assert c.sw_decode_errors() == 0
+        assert c.sw_decode_device(d_src, *args, nsrc=nsrc, nrep=len(hdr), sym_len=L, stride=stride) == 0
+        torch.cuda.synchronize()
+        assert c.sw_decode_errors() & fecgpu.SW_ERR_HEADER
+        assert np.array_equal(d_st.cpu().numpy(), 1 - sp)
+        assert np.array_equal(d_src.cpu().numpy(), d)
+        with pytest.raises(fecgpu.FecError) as ei:
+            c.sw_decode_device(d_src, *args, nsrc=nsrc, nrep=len(hdr), sym_len=L, stride=stride,
+                               flags=fecgpu.F_SYNC)
+        assert ei.value.code == fecgpu.ERR_INVALID_ARG
+        assert np.array_equal(d_st.cpu().numpy(), 1 - sp)
+        assert np.array_equal(d_src.cpu().numpy(), d)
+    finally:
+        c.close()
+
+
 def test_sw_decode_host_pointers_and_args(ctx):
     nsrc, L, stride = 200, 40, 48
     src = stream(nsrc, L, stride, 29)
