@@ -54,6 +54,7 @@ struct EncTables {
     uint32_t *c = nullptr;
     uint8_t *coef = nullptr;  // parity rows P[r][k] (non-Cauchy matrices: the decode plan reads them)
     uint32_t *bs = nullptr;   // plane masks [k][r][8] (runtime bit-sliced encode)
+    uint8_t *rows = nullptr;  // parity rows P[r][k] of any matrix (the bit-sliced decode's plan)
 };
 
 uint8_t host_gf_pow(uint8_t a, int n) {  // a^n, 0^0 = 1
@@ -155,6 +156,9 @@ struct fecgpu_ctx {
     size_t pinned_cache_cap = (size_t)1 << 30;
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
+    // GF decode: windows with at least this many erasures take the bit-sliced
+    // decode (fec_kernels.hip gf_decode_bs_kernel; 0 = never)
+    int bsd_min_e = 6;
     int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
     int sw_stream = kSwStreamDefault;  // sliding-window encode: 0 combine jobs, 1..5 streaming
                                        // (dwords per lane), kSwStreamAuto per symbol size
@@ -313,6 +317,11 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         ctx->fault_launches = (int)value;
         return 0;
     }
+    if (!std::strcmp(key, "bsd_min_e")) {
+        if (value < 0 || value > kMaxR) return FECGPU_ERR_INVALID_ARG;
+        ctx->bsd_min_e = (int)value;
+        return 0;
+    }
     if (!std::strcmp(key, "bs_passes")) {
         if (value < 1 || value > 256) return FECGPU_ERR_INVALID_ARG;
         ctx->bs_passes = (int)value;
@@ -376,7 +385,7 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
         (void)hipSetDevice(std::get<0>(kv.first));
         (void)hipFree(kv.second.ab);
         (void)hipFree(kv.second.c);
-        if (kv.second.coef) (void)hipFree(kv.second.coef);
+        if (kv.second.rows) (void)hipFree(kv.second.rows);
         if (kv.second.bs) (void)hipFree(kv.second.bs);
     }
     for (auto &kv : ctx->stage) {
@@ -513,13 +522,22 @@ ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out)
         HIP_TRY(hipMalloc(&t.bs, m.size() * sizeof(uint32_t)), "hipMalloc");
         HIP_TRY(hipMemcpy(t.bs, m.data(), m.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy");
     }
-    if (code->matrix != FECGPU_MATRIX_CAUCHY) {
-        HIP_TRY(hipMalloc(&t.coef, P.size()), "hipMalloc");
-        HIP_TRY(hipMemcpy(t.coef, P.data(), P.size(), hipMemcpyHostToDevice), "hipMemcpy");
-    }
+    HIP_TRY(hipMalloc(&t.rows, P.size()), "hipMalloc");
+    HIP_TRY(hipMemcpy(t.rows, P.data(), P.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    if (code->matrix != FECGPU_MATRIX_CAUCHY) t.coef = t.rows;
     ctx->enc[key] = t;
     out = t;
     return 0;
+}
+
+// Bit-sliced decode: windows per group for windows of ncol 16-B columns in
+// units of `cols` columns, >= 8 passes of the workgroup at the longest window,
+// the groups' plan regions and the parity rows (kr bytes) within 40 KB of LDS.
+int bsd_wpb(uint32_t ncol, uint32_t cols, int kr) {
+    const uint32_t units = std::max<uint32_t>(1, (ncol + cols - 1) / cols);
+    const int want = (int)((8u * kBlock + units - 1) / units);
+    const int cap = (int)(((40u << 10) - (((uint32_t)kr + 15u) & ~15u)) / sizeof(BsdRegion));
+    return std::max(1, std::min({want, cap, kMaxWpb}));
 }
 
 // Windows per workgroup: fill the 256 lanes with whole passes over the
@@ -681,19 +699,6 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
         }
         P = it->second;
     }
-    const auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
-    const size_t o_out = up(nwin * sizeof(CombJob)), o_coef = o_out + up(nwin * kMaxR * sizeof(uint64_t));
-    const bool two = decode;  // the two-stage decode (fec_wide.hip)
-    const size_t coef_bytes = decode ? nwin * kMaxR * (size_t)kMaxR : 0;
-    const size_t o_j1 = o_coef + up(coef_bytes), o_o1 = o_j1 + (two ? up(nwin * sizeof(CombJob)) : 0);
-    const size_t o_syn = o_o1 + (two ? up(nwin * (size_t)r * sizeof(uint64_t)) : 0);
-    const size_t total = o_syn + (two ? nwin * (size_t)r * stride : 0);
-    ssize_t rc = ctx_sw_begin(ctx, s);
-    if (rc) return rc;
-    void *scratch = nullptr;
-    rc = ctx_sw_scratch(ctx, 11, total, &scratch);
-    if (rc) return rc;
-    uint8_t *b = static_cast<uint8_t *>(scratch);
     // per-window lengths: every window's columns up to the stride
     const uint32_t ncol = sym_len ? stride / 16u : (sym_len_all + 15u) / 16u;
     // plane picks (run_wide's row block: P, [P | I], then the picks of each)
@@ -703,10 +708,48 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
         mP = reinterpret_cast<const uint32_t *>(P + o_m);
         mPI = mP + (size_t)k * r * 2 * kRbsDw4;
     }
-    HIP_TRY(launch_wide(win, present, status, P, nwin, stride, ncol, k, r, decode, reinterpret_cast<CombJob *>(b),
-                        reinterpret_cast<uint64_t *>(b + o_out), b + o_coef, s, reinterpret_cast<CombJob *>(b + o_j1),
-                        reinterpret_cast<uint64_t *>(b + o_o1), b + o_syn, mP, two ? mPI : nullptr),
-            "wide batch launch");
+    ssize_t rc = ctx_sw_begin(ctx, s);
+    if (rc) return rc;
+    if (decode && mP) {
+        // the bit-sliced decode (fec_kernels.hip gf_decode_bs_kernel): a plan
+        // per window in LDS, syndromes of the received sources by the plane
+        // picks of P, the solve on the unit's columns; one launch, no scratch
+        BatchArgs a{};
+        a.win = win;
+        a.sym_len = sym_len;
+        a.S_all = sym_len_all;
+        a.stride = stride;
+        a.wpitch = (uint64_t)n * stride;
+        a.present = present;
+        a.status = status;
+        a.nwin = nwin;
+        a.k = k;
+        a.r = r;
+        a.nw = (n + 63) / 64;
+        a.prows = P;
+        a.enc_bs = mP;
+        a.wpb = bsd_wpb(ncol, kRbsCols, k * r);
+        a.chk.lo[0] = reinterpret_cast<uint64_t>(win);
+        a.chk.n[0] = nwin * a.wpitch;
+        HIP_TRY(launch_decode_bs(a, (int)code->matrix, s), "wide bit-sliced decode launch");
+    } else {
+        // the two-stage decode (fec_wide.hip; no plane picks: bitslice off or r < 4)
+        const auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
+        const size_t o_out = up(nwin * sizeof(CombJob)), o_coef = o_out + up(nwin * kMaxR * sizeof(uint64_t));
+        const size_t coef_bytes = decode ? nwin * kMaxR * (size_t)kMaxR : 0;
+        const size_t o_j1 = o_coef + up(coef_bytes), o_o1 = o_j1 + (decode ? up(nwin * sizeof(CombJob)) : 0);
+        const size_t o_syn = o_o1 + (decode ? up(nwin * (size_t)r * sizeof(uint64_t)) : 0);
+        const size_t total = o_syn + (decode ? nwin * (size_t)r * stride : 0);
+        void *scratch = nullptr;
+        rc = ctx_sw_scratch(ctx, 11, total, &scratch);
+        if (rc) return rc;
+        uint8_t *b = static_cast<uint8_t *>(scratch);
+        HIP_TRY(launch_wide(win, present, status, P, nwin, stride, ncol, k, r, decode, reinterpret_cast<CombJob *>(b),
+                            reinterpret_cast<uint64_t *>(b + o_out), b + o_coef, s,
+                            reinterpret_cast<CombJob *>(b + o_j1), reinterpret_cast<uint64_t *>(b + o_o1), b + o_syn,
+                            mP, decode ? mPI : nullptr),
+                "wide batch launch");
+    }
     rc = ctx_sw_end(ctx, s);
     if (rc) return rc;
     if (flags & FECGPU_F_SYNC) HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
@@ -885,11 +928,21 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         p.wpb = choose_wpb(ncol, 0, 0);
     } else {
         if (scheme == FECGPU_SCHEME_GF256) {
-            if (code->matrix != FECGPU_MATRIX_CAUCHY) {  // the plan reads the parity rows
-                EncTables t;
-                rc = get_enc_tables(ctx, code, t);
-                if (rc) return rc;
-                a.coef = t.coef;
+            EncTables t;
+            rc = get_enc_tables(ctx, code, t);
+            if (rc) return rc;
+            a.coef = t.coef;  // non-Cauchy matrices: the plan reads the parity rows
+            // windows with many erasures: the bit-sliced decode after the table
+            // kernel (codes with compiled plane masks; device windows in place,
+            // uniform stride; the routed windows are scattered, which the
+            // runtime-mask kernel's buffer resource over a group cannot span)
+            if (ctx->bsd_min_e > 0 && ctx->bitslice && !remote && !win_off && !a.out_delta &&
+                r >= ctx->bsd_min_e && bitslice_supported(k, r, (int)code->matrix)) {
+                a.bsd_min_e = ctx->bsd_min_e;
+                a.prows = t.rows;
+                a.nw = 1;
+                p.matrix = (int)code->matrix;
+                p.bsd_wpb = bsd_wpb(ncol ? ncol : stride >> 4, 2, k * r);
             }
             p.win_lds = gf_dec_win_lds(k, r);
             p.wpb = choose_wpb(ncol, p.win_lds, 40 * 1024);
@@ -951,8 +1004,22 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
     rc = set_check_ranges(ctx, code, decode, a, s);
     if (rc) return rc;
 #endif
+    if (a.bsd_min_e) {  // the routed windows' list and count: ctx scratch, ordered like the SW calls'
+        rc = ctx_sw_begin(ctx, s);
+        if (rc) return rc;
+        void *lp = nullptr;
+        rc = ctx_sw_scratch(ctx, 12, 256 + a.nwin * 4, &lp);
+        if (rc) return rc;
+        a.bsd_count = static_cast<uint32_t *>(lp);
+        a.bsd_list = a.bsd_count + 64;
+        HIP_TRY(hipMemsetAsync(a.bsd_count, 0, sizeof(uint32_t), s), "bit-sliced decode count reset");
+    }
     hipError_t e = decode ? launch_decode(scheme, a, p, s) : launch_encode(scheme, a, p, s);
     if (e != hipSuccess) return dev_err(e, decode ? "decode launch" : "encode launch");
+    if (a.bsd_min_e) {
+        rc = ctx_sw_end(ctx, s);
+        if (rc) return rc;
+    }
 #if FECGPU_CHECK
     HIP_TRY(hipStreamSynchronize(s), "check: sync");
     uint64_t nbad = 0, first = 0;

@@ -1027,6 +1027,18 @@ __device__ __forceinline__ void plan_offsets(const BatchArgs &a, uint64_t w, int
     if (lane < 8) rg.ooff[lane] = lane < e ? (uint32_t)rg.outsym[lane] * stride : 0u;
 }
 
+// Windows of many erasures go to the bit-sliced decode (gf_decode_bs_kernel
+// below, launched after this kernel over the list): e >= a.bsd_min_e (0: off).
+// The window's status is that kernel's to write.
+__device__ __forceinline__ bool bsd_route(const BatchArgs &a, uint64_t w, int e, int lane, uint8_t &ne_out) {
+    if (!a.bsd_min_e || e < a.bsd_min_e) return false;
+    if (lane == 0) {
+        ne_out = 0;
+        a.bsd_list[atomicAdd(a.bsd_count, 1u)] = (uint32_t)w;
+    }
+    return true;
+}
+
 // GF plan (a6/a7) by one wave, closed form.  Missing sources m_0..m_{e-1},
 // the first e present repairs with points x_t = k + sel_t; the system is the
 // Cauchy matrix A[t][u] = 1/(x_t ^ m_u).  Its inverse folded
@@ -1056,6 +1068,7 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, uint64_t pres, int lane,
         }
         return;
     }
+    if (bsd_route(a, w, e, lane, ne_out)) return;
     // wave-uniform m_v and x_t (pres is uniform: SGPR bit scans)
     int mv[R], xt[R];
     {
@@ -1153,6 +1166,7 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
         }
         return;
     }
+    if (bsd_route(a, w, e, lane, ne_out)) return;
     uint64_t mm = miss, rr = rep;
     for (int i = 0; i < lane && i < 8; i++) { mm &= mm - 1; rr &= rr - 1; }
     const int my_m = (int)__ffsll((unsigned long long)mm) - 1;    // lane u < e: u-th missing source
@@ -1367,6 +1381,360 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
             uint8_t *base = reinterpret_cast<uint8_t *>(g.base[wl]) + (s - g.pfx[i]) * 16u;
             const DecRegion<R> rg(regions + (size_t)wl * a.win_lds, k);
             dec_dispatch<R>(nw, base, k, ne, a.out_delta, rg);
+        }
+        __syncthreads();
+    }
+}
+
+// ================================= bit-sliced GF decode (many erasures) ===
+//   The table decode costs 5 + 6e VALU per source dword, so
+// windows with many erasures are VALU-bound (e = 8: 2.2-2.8 TB/s).  Here a
+// window is decoded in two stages inside one unit of work:
+//   1. syndromes s_i = rep_i + sum_j P[i][j] src_j over the received sources,
+//      for every repair i, by the bit-sliced products of the encode (compiled
+//      plane masks, bs::, or runtime ones, rbs4::): ~19 VALU per source dword
+//      for all r outputs at once.  A missing source's load goes to a row the
+//      lane reads anyway (BsdRegion::alt) and is masked to zero, so only the
+//      received sources and the repairs the solve uses come from HBM;
+//   2. x_u = sum_i C[u][i] s_i over the pivot repairs (C from the window's
+//      plan: [A | I] reduced with pivot search, A[t][u] = P[sel_t][m_u], as
+//      plan_gf_mat), by the table multiply on the unit's few columns.
+// The plan is one wave per window in LDS, like gf_decode_kernel's.  Windows
+// come in groups of a.wpb from a.bsd_list (routed by the table decode's plan)
+// or, with no list, every window (the wide codes).
+namespace bsd {
+
+constexpr int kRsrcRaw = 0x00020000;  // buffer resource word 3: raw 32-bit data (gfx9)
+
+// One wave: the plan of window w into rg (status too).  pw: the window's
+// present words; P: parity rows [r][k] in LDS.
+__device__ void plan(const BatchArgs &a, uint64_t w, int lane, BsdRegion &rg, const uint8_t *ex, const uint8_t *lg,
+                     const uint8_t *P) {
+    const int k = a.k, r = a.r, nw = a.nw;
+    const uint64_t pl = lane < nw ? a.present[w * (uint64_t)nw + lane] : 0ull;
+    uint64_t pw[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        pw[q] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl, q) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pl >> 32), q) << 32);
+    const auto bit = [&](int j) -> uint32_t {  // per-lane j
+        const int q = j >> 6;
+        const uint64_t v = q == 0 ? pw[0] : q == 1 ? pw[1] : q == 2 ? pw[2] : pw[3];
+        return (uint32_t)(v >> (j & 63)) & 1u;
+    };
+    int e = 0, first = -1;  // missing sources; the first received source
+    for (int c0 = 0; c0 < k; c0 += 64) {
+        const int i = c0 + lane;
+        const bool in = i < k, miss = in && !bit(i);
+        const uint64_t b = __ballot(miss), h = __ballot(in && !miss);
+        const int pos = e + __popcll(b & ((1ull << lane) - 1ull));
+        if (miss && pos < kMaxR) rg.m[pos] = (uint8_t)i;
+        e += __popcll(b);
+        if (first < 0 && h) first = c0 + __ffsll((unsigned long long)h) - 1;
+    }
+    const uint32_t rep = (uint32_t)__ballot(lane < r && bit(k + lane));
+    const int np = __popcll(rep);
+    if (e == 0 || e > r || np < e) {
+        if (lane == 0) {
+            rg.ne = 0;
+            a.status[w] = e == 0 ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
+        }
+        return;
+    }
+    WAVE_SYNC();
+    uint32_t rr = rep;
+    for (int i = 0; i < lane && i < 8; i++) rr &= rr - 1;
+    const int my_sel = rr ? __ffs(rr) - 1 : 0;  // lane t < np: the t-th present repair
+    // [A | I], lane = t * 8 + u; every __shfl and ballot with the whole wave active
+    const int t = lane >> 3, u = lane & 7;
+    const int sel_t = __shfl(my_sel, t, 64);
+    const int m_u = u < e ? (int)rg.m[u] : 0;
+    const bool row = t < np;
+    uint32_t xl = (row && u < e) ? P[sel_t * k + m_u] : 0u;
+    uint32_t xr = (row && t == u) ? 1u : 0u;
+    uint32_t used = 0;  // rows already pivots (wave-uniform)
+    int my_piv = 0;     // lane c < e: pivot row of column c
+    for (int c = 0; c < e; c++) {
+        const uint64_t cand = __ballot(row && u == c && !((used >> t) & 1u) && xl != 0);
+        if (!cand) {  // rank < e (random linear codes): the window stays lost
+            if (lane == 0) {
+                rg.ne = 0;
+                a.status[w] = FECGPU_STATUS_UNRECOVERABLE;
+            }
+            return;
+        }
+        const int pr = (int)(__ffsll((unsigned long long)cand) - 1) >> 3;
+        used |= 1u << pr;
+        if (lane == c) my_piv = pr;
+        const uint32_t ip = gf_inv_lds(ex, lg, __shfl(xl, pr * 8 + c, 64));
+        if (t == pr) {
+            xl = gf_mul_lds(ex, lg, xl, ip);
+            xr = gf_mul_lds(ex, lg, xr, ip);
+        }
+        const uint32_t f = __shfl(xl, t * 8 + c, 64);
+        const uint32_t rl = __shfl(xl, pr * 8 + u, 64);
+        const uint32_t rq = __shfl(xr, pr * 8 + u, 64);
+        if (t != pr && row) {
+            xl ^= gf_mul_lds(ex, lg, f, rl);
+            xr ^= gf_mul_lds(ex, lg, f, rq);
+        }
+    }
+    // C[u][i], lane = u * 8 + i: T[P_u][c] where repair i is pivot row c's, else 0
+    const int cu = lane >> 3, ci = lane & 7;
+    const int pu = __shfl(my_piv, min(cu, e - 1), 64);
+    uint32_t v = 0, ub = 0;
+    for (int c = 0; c < e; c++) {
+        const int pc = __shfl(my_piv, c, 64);
+        const uint32_t tv = __shfl(xr, (pu * 8 + pc) & 63, 64);
+        const int sc = __shfl(my_sel, pc, 64);  // the repair of pivot row pc
+        ub |= 1u << sc;
+        if (sc == ci) v = tv;
+    }
+    const CoefTab ct = make_coef_tab(cu < e ? v : 0u);
+    rg.ab[lane] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+    rg.tc[lane] = ct.c;
+    if (lane < 4) rg.pw[lane] = lane == 0 ? pw[0] : lane == 1 ? pw[1] : lane == 2 ? pw[2] : pw[3];
+    if (lane == 0) {
+        rg.ne = (uint32_t)e;
+        rg.used = ub;
+        rg.alt = first >= 0 ? (uint32_t)first : (uint32_t)(k + __ffs(ub) - 1);
+        a.status[w] = FECGPU_STATUS_OK;
+    }
+}
+
+// Stage 2 on one 16-B column: acc[i][H .. H + 3] the column of syndrome i
+// after stage 1 (bytes); the repair row i is added here where the window uses
+// it (bit i of `used`), then x_u = sum_i C[u][i] s_i for u < nw (wave-uniform),
+// stored to row m[u] when u < ne.  col: the column's address in row 0.
+template <int R, int H, int K>
+__device__ __forceinline__ void solve_col(const uint32_t (&acc)[R][8], uint8_t *col, uint32_t stride, int k,
+                                          const BsdRegion &rg, int nw, int ne, bool live) {
+    const uint32_t used = rg.used;
+    uint4 x[R];
+#pragma unroll
+    for (int u = 0; u < R; u++) x[u] = zero4();
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        uint4 si = make_uint4(acc[i][H], acc[i][H + 1], acc[i][H + 2], acc[i][H + 3]);
+        if ((used >> i) & 1u) si = xor4(si, ld16(col + (uint32_t)((K ? K : k) + i) * stride));
+        const Split sp = split(si);
+#pragma unroll
+        for (int u = 0; u < R; u++)
+            if (u < nw) gmac(x[u], sp, rg.ab[u * kMaxR + i], rg.tc[u * kMaxR + i]);
+    }
+#pragma unroll
+    for (int u = 0; u < R; u++)
+        if (u < nw && u < ne && live) st16(col + (uint32_t)rg.m[u] * stride, x[u]);
+}
+
+}  // namespace bsd
+
+namespace bs {
+
+// dec_sources: sources() with each source's load sent to the alt row and
+// masked to zero where the lane's window misses it (pm bit j clear)
+template <int T, int J>
+__device__ __forceinline__ void dload(const uint8_t *pa, const uint8_t *pb, uint32_t stride, uint64_t pm,
+                                      const uint8_t *qa, const uint8_t *qb, uint32_t (&x)[8]) {
+    const bool p = (pm >> J) & 1ull;
+    const uint4 va = ld16(p ? pa + T * stride : qa), vb = ld16(p ? pb + T * stride : qb);
+    const uint32_t mk = p ? ~0u : 0u;
+    x[0] = va.x & mk; x[1] = va.y & mk; x[2] = va.z & mk; x[3] = va.w & mk;
+    x[4] = vb.x & mk; x[5] = vb.y & mk; x[6] = vb.z & mk; x[7] = vb.w & mk;
+}
+
+template <int K, int R, int M, int J0, int... T>
+__device__ __forceinline__ void dbatch(const uint8_t *pa, const uint8_t *pb, uint32_t stride, uint64_t pm,
+                                       const uint8_t *qa, const uint8_t *qb, uint32_t (&acc)[R][8],
+                                       std::integer_sequence<int, T...>) {
+    uint32_t x[sizeof...(T)][8];
+    (dload<T, J0 + T>(pa, pb, stride, pm, qa, qb, x[T]), ...);
+    ((tr8(x[T]), source<K, R, M, J0 + T>(x[T], acc, std::make_integer_sequence<int, R * 8>{}),
+      __builtin_amdgcn_sched_barrier(0)), ...);
+}
+
+template <int K, int R, int M, int U, int J0>
+__device__ __forceinline__ void dsources(const uint8_t *pa, const uint8_t *pb, uint32_t stride, uint64_t pm,
+                                         const uint8_t *qa, const uint8_t *qb, uint32_t (&acc)[R][8]) {
+    if constexpr (J0 < K) {
+        dbatch<K, R, M, J0>(pa, pb, stride, pm, qa, qb, acc,
+                            std::make_integer_sequence<int, ((K - J0) < U ? (K - J0) : U)>{});
+        pa += U * stride;
+        pb += U * stride;
+        asm volatile("" : "+v"(pa), "+v"(pb));
+        dsources<K, R, M, U, J0 + U>(pa, pb, stride, pm, qa, qb, acc);
+    }
+}
+
+// one decode unit (columns pa, pb of a window planned in rg): syndromes, then
+// the solve on each column
+template <int K, int R, int M, int U>
+__device__ __forceinline__ void dec_unit(uint8_t *pa, uint8_t *pb, uint32_t stride, bool live, const BsdRegion &rg,
+                                         int nw) {
+    const uint64_t pm = rg.pw[0];
+    const uint32_t alt = rg.alt;
+    uint32_t acc[R][8];
+    dsources<K, R, M, U, 0>(pa, pb, stride, pm, pa + alt * stride, pb + alt * stride, acc);
+#pragma unroll
+    for (int i = 0; i < R; i++) tr8(acc[i]);
+    const int ne = (int)rg.ne;
+    bsd::solve_col<R, 0, K>(acc, pa, stride, K, rg, nw, ne, live);
+    bsd::solve_col<R, 4, K>(acc, pb, stride, K, rg, nw, ne, pb != pa && live);
+}
+
+}  // namespace bs
+
+namespace rbs4 {
+
+// rbs4::unit for decode over a group of consecutive windows (the wide codes):
+// the source rows by buffer loads — one resource over the group's windows,
+// this lane's column offsets coff[c] from the group's base (32-bit VGPRs, no
+// 64-bit address arithmetic per load), the row offset a scalar — and a source
+// the lane's window misses is read at an offset past the resource (2^31
+// added), which the hardware returns as zeros without a memory access: no
+// masking, no traffic for missing rows.  Then the repairs the solve uses and
+// the solve on each column (pointers pc[c]).
+constexpr uint32_t kOob = 0x80000000u;  // added to a column offset: past any group's records
+template <int R>
+__device__ __forceinline__ void dec_unit(__amdgpu_buffer_rsrc_t rs, const uint32_t (&coff)[4], uint8_t *const (&pc)[4],
+                                         uint32_t stride, int k, cmask mk, bool live, const BsdRegion &rg, int nw) {
+    // present bits 32 at a time from the region (one LDS read per 32 sources)
+    const uint32_t *pw32 = reinterpret_cast<const uint32_t *>(rg.pw);
+    const auto vo = [&](int j) -> uint32_t { return ((pw32[j >> 5] >> (j & 31)) & 1u) ? 0u : kOob; };  // uniform j
+    // the row offset goes in the vector offset too (soffset 0): the range
+    // check then covers the whole offset whatever soffset's treatment
+    const auto bload = [&](uint32_t off, uint32_t (&xa)[8], uint32_t (&xb)[8]) __attribute__((always_inline)) {
+        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(coff[0] + off), 0, 0);
+        const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(coff[1] + off), 0, 0);
+        const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(coff[2] + off), 0, 0);
+        const u32x4 v3 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(coff[3] + off), 0, 0);
+        xa[0] = v0.x; xa[1] = v0.y; xa[2] = v0.z; xa[3] = v0.w;
+        xa[4] = v1.x; xa[5] = v1.y; xa[6] = v1.z; xa[7] = v1.w;
+        xb[0] = v2.x; xb[1] = v2.y; xb[2] = v2.z; xb[3] = v2.w;
+        xb[4] = v3.x; xb[5] = v3.y; xb[6] = v3.z; xb[7] = v3.w;
+    };
+    uint32_t aa[R][8], ab[R][8];
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int p = 0; p < 8; p++) aa[i][p] = ab[i][p] = 0;
+    uint32_t xa[8], xb[8];
+    bload(vo(0), xa, xb);
+    for (int j = 0; j < k; j++) {
+        uint32_t na[8], nb[8];
+        const int jn = min(j + 1, k - 1);
+        bload((uint32_t)jn * stride + vo(jn), na, nb);
+        bs::tr8(xa);
+        bs::tr8(xb);
+        source<R>(xa, xb, aa, ab, mk + (size_t)j * (R * 2 * kRbsDw4));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            xa[q] = na[q];
+            xb[q] = nb[q];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        bs::tr8(aa[i]);
+        bs::tr8(ab[i]);
+    }
+    const int ne = (int)rg.ne;
+    bsd::solve_col<R, 0, 0>(aa, pc[0], stride, k, rg, nw, ne, live);
+    bsd::solve_col<R, 4, 0>(aa, pc[1], stride, k, rg, nw, ne, live && pc[1] != pc[0]);
+    bsd::solve_col<R, 0, 0>(ab, pc[2], stride, k, rg, nw, ne, live && pc[2] != pc[0]);
+    bsd::solve_col<R, 4, 0>(ab, pc[3], stride, k, rg, nw, ne, live && pc[3] != pc[0]);
+}
+
+}  // namespace rbs4
+
+// The decode kernel: groups of a.wpb windows (from the list, or every window),
+// planned a wave per window into BsdRegion's in LDS, ordered by descending e
+// (a wave's first lane holds its largest e: the solve loops run that many
+// outputs, uniform), then their units streamed.  RT: true for the runtime-mask
+// stage 1 (four-column units, a.enc_bs), false for the compiled masks of
+// (K, R, M) (two-column units).  Workgroup-uniform trip counts (lanes past the
+// end redo the last unit without storing).
+template <int K, int R, int M, bool RT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8)))
+void gf_decode_bs_kernel(BatchArgs a) {
+    CHK_PROLOGUE(a);
+    extern __shared__ uint4 dyn[];
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ GroupLds g;
+    __shared__ uint32_t s_w[kMaxWpb];
+    __shared__ uint8_t s_perm[kMaxWpb];
+    BsdRegion *rgn = reinterpret_cast<BsdRegion *>(dyn);
+    uint8_t *s_P = reinterpret_cast<uint8_t *>(rgn + a.wpb);  // parity rows [r][k]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
+    for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
+    for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
+    for (int i = tid; i < a.r * k; i += kBlock) s_P[i] = a.prows[i];
+    const uint64_t count = a.bsd_count ? (uint64_t)*a.bsd_count : a.nwin;
+    constexpr uint32_t C = RT ? kRbsCols : 2;  // columns per unit
+    __syncthreads();
+    for (XcdRange xr = xcd_range((count + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
+        const uint64_t g0 = xr.cur * a.wpb;
+        const int nb = (int)min((uint64_t)a.wpb, count - g0);
+        if (tid < nb) {
+            const uint64_t w = a.bsd_list ? (uint64_t)a.bsd_list[g0 + tid] : g0 + tid;
+            s_w[tid] = (uint32_t)w;
+            uint64_t base;
+            uint32_t stride, S;
+            win_geom(a, w, base, stride, S);
+            g.base[tid] = base;
+            g.stride[tid] = stride;
+            g.ncol[tid] = (S + 15u) >> 4;
+        }
+        __syncthreads();
+        for (int wl = wave; wl < nb; wl += kBlock / 64) bsd::plan(a, s_w[wl], lane, rgn[wl], s_exp, s_log, s_P);
+        __syncthreads();
+        if (tid < 64) {  // descending e (ties by index), then unit prefix sums in that order
+            const int t = tid;
+            const int ne_t = t < nb ? (int)rgn[t].ne : -1;
+            const uint64_t below = (1ull << t) - 1;
+            int rank = 0;
+#pragma unroll
+            for (int v = R; v >= 0; v--) {
+                const uint64_t b = __ballot(ne_t == v);
+                if (v > ne_t) rank += __popcll(b);
+                else if (v == ne_t) rank += __popcll(b & below);
+            }
+            if (t < nb) s_perm[rank] = (uint8_t)t;
+            WAVE_SYNC();
+            const int wl = t < nb ? (int)s_perm[t] : 0;
+            block_prefix(g.pfx, (t < nb && rgn[wl].ne) ? (g.ncol[wl] + C - 1) / C : 0u, t);
+        }
+        __syncthreads();
+        const uint32_t total = g.pfx[nb];
+        int i = 0;
+        for (uint32_t s0 = 0; s0 < total; s0 += kBlock) {
+            const bool live = s0 + tid < total;
+            const uint32_t s = live ? s0 + tid : total - 1;
+            while (s >= g.pfx[i + 1]) i++;
+            const int wl = s_perm[i];
+            const BsdRegion &rg = rgn[wl];
+            const int nw = __builtin_amdgcn_readfirstlane((int)rg.ne);  // the wave's largest e
+            uint8_t *base = reinterpret_cast<uint8_t *>(g.base[wl]);
+            const uint32_t u = s - g.pfx[i], h = g.pfx[i + 1] - g.pfx[i];
+            if constexpr (RT) {
+                // the group's windows are consecutive (no list): one resource from
+                // the first window over wpb window pitches
+                uint8_t *pc[4];
+                rbs4::unit_cols(base, u, h, g.ncol[wl], pc);
+                const uint8_t *gb = reinterpret_cast<const uint8_t *>(g.base[0]);
+                uint32_t coff[4];
+#pragma unroll
+                for (int c = 0; c < 4; c++) coff[c] = (uint32_t)(pc[c] - gb);
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t *>(gb), 0, (int)(uint32_t)((uint64_t)nb * a.wpitch), bsd::kRsrcRaw);
+                rbs4::dec_unit<R>(rs, coff, pc, g.stride[wl], k, (rbs::cmask)a.enc_bs, live, rg, nw);
+            } else {
+                uint8_t *pa, *pb;
+                bs::unit_cols(base, u, h, g.ncol[wl], pa, pb);
+                bs::dec_unit<K, R, M, kBsU>(pa, pb, g.stride[wl], live, rg, nw);
+            }
         }
         __syncthreads();
     }
@@ -2117,13 +2485,63 @@ hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t 
     return launch_encode(FECGPU_SCHEME_GF256, a, p, s);
 }
 
+namespace {
+hipError_t launch_gf_decode_table(const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
+    DISPATCH_R(a.r, launch(gf_decode_kernel<RR>, a, p, s, false))
+}
+}  // namespace
+
+// The bit-sliced decode over a.bsd_list (*a.bsd_count windows) or, without a
+// list, every window; a.wpb windows per group, persistent grid.  Compiled
+// masks when the code has them (matrix: fecgpu_matrix), else runtime ones
+// (a.enc_bs).
+hipError_t launch_decode_bs(BatchArgs a, int matrix, hipStream_t s) {
+    if (a.nwin == 0) return hipSuccess;
+    if (a.r < 4 || a.r > kMaxR || !a.prows) return hipErrorInvalidValue;
+    LaunchPlan p{};
+    p.wpb = a.wpb;
+    p.lds_bytes = (uint32_t)(a.wpb * sizeof(BsdRegion)) + (((uint32_t)(a.k * a.r) + 15u) & ~15u);
+    const uint64_t groups = (a.nwin + a.wpb - 1) / a.wpb;
+    const auto go = [&](auto kernel) -> hipError_t {
+        if (p.lds_bytes > 64u * 1024u) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes);
+            if (e != hipSuccess) return e;
+        }
+        return launch(kernel, a, p, s, false, groups);
+    };
+    if (a.k + a.r <= kMaxK && bitslice_supported(a.k, a.r, matrix)) {
+#define BSD_LAUNCH_M(K_, R_, M_) \
+        if (a.k == K_ && a.r == R_ && matrix == M_) return go(gf_decode_bs_kernel<K_, R_, M_, false>);
+#define BSD_LAUNCH(K_, R_)                              \
+        BSD_LAUNCH_M(K_, R_, FECGPU_MATRIX_CAUCHY)      \
+        BSD_LAUNCH_M(K_, R_, FECGPU_MATRIX_VANDERMONDE)
+        BS_CODES(BSD_LAUNCH)
+#undef BSD_LAUNCH
+#undef BSD_LAUNCH_M
+    }
+    if (!a.enc_bs || a.bsd_list) return hipErrorInvalidValue;  // the runtime-mask kernel: consecutive windows
+    switch (a.r) {
+        case 4: return go(gf_decode_bs_kernel<0, 4, 0, true>);
+        case 5: return go(gf_decode_bs_kernel<0, 5, 0, true>);
+        case 6: return go(gf_decode_bs_kernel<0, 6, 0, true>);
+        case 7: return go(gf_decode_bs_kernel<0, 7, 0, true>);
+        default: return go(gf_decode_bs_kernel<0, 8, 0, true>);
+    }
+}
+
 hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     if (scheme == 0) {
         if (p.flat) DISPATCH_R(a.r, launch(xor_decode_kernel<RR, true>, a, p, s, true))
         else DISPATCH_R(a.r, launch(xor_decode_kernel<RR, false>, a, p, s, false))
     }
-    DISPATCH_R(a.r, launch(gf_decode_kernel<RR>, a, p, s, false))
+    const hipError_t e = launch_gf_decode_table(a, p, s);
+    if (e != hipSuccess || !a.bsd_min_e) return e;
+    // the windows the table plan routed (e >= bsd_min_e), after it on the stream
+    BatchArgs b = a;
+    b.wpb = p.bsd_wpb;
+    return launch_decode_bs(b, p.matrix, s);
 }
 
 hipError_t take_bounds_faults(uint64_t *count, uint64_t *first) {

@@ -1,0 +1,143 @@
+"""GPU parity of the bit-sliced decode of windows with many erasures
+(fec_kernels.hip gf_decode_bs_kernel): the table decode's plan
+routes windows with e >= the ctx's "bsd_min_e" erasures (default 6) to it for
+the codes with compiled plane masks (k in 16, 24, 32; r = 8; Cauchy and
+systematic Vandermonde rows).  Recovered bytes equal the originals, statuses
+equal the numpy oracle's (oracle/np_oracle.py decode), missing rows poisoned
+first; routing on and off give the same bytes.  The wide codes (k + r > 64,
+every window through this kernel with runtime plane masks) are covered by
+tests/test_gpu_wide.py.
+PARITY UNPINNED vs the reference fec branch."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import fecgpu  # noqa: E402
+import np_oracle as N  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(min_e):
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    c = fecgpu.Context()
+    c.set_tuning("bsd_min_e", min_e)
+    return c
+
+
+def _erasures(nwin, k, r, rng, lo=0):
+    """Per window: e in lo..r+1 missing sources (most windows many), 0..2 missing repairs."""
+    bits = np.ones((nwin, k + r), bool)
+    for w in range(nwin):
+        e = int(rng.integers(lo, r + 2))
+        bits[w, rng.choice(k, e, replace=False)] = False
+        lr = int(rng.integers(0, 3))
+        if lr:
+            bits[w, k + rng.choice(r, lr, replace=False)] = False
+    return bits
+
+
+def _run(c, k, r, matrix, L, nwin, bits, sym_len=None, seed=0):
+    """Encode on the GPU, poison the missing symbols, decode; check against the
+    oracle and the originals.  Returns (decoded windows, statuses)."""
+    n = k + r
+    stride = (L + 15) // 16 * 16
+    rng = np.random.default_rng(seed + 7 * k + r)
+    wins = np.zeros((nwin, n, stride), np.uint8)
+    wins[:, :k, :L] = rng.integers(0, 256, (nwin, k, L), dtype=np.uint8)
+    code = fecgpu.Code("gf256", k, r, matrix=matrix)
+    d = torch.from_numpy(wins.copy()).cuda()
+    sl = None if sym_len is None else torch.from_numpy(sym_len).cuda()
+    kw = dict(nwin=nwin, stride=stride, sym_len_all=L if sym_len is None else 0, sym_len=sl)
+    c.encode_batch(code, d, **kw)
+    torch.cuda.synchronize()
+    enc = d.cpu().numpy()
+    mask = torch.from_numpy(bits).cuda()
+    d[~mask] = 0xAB
+    pres = np.zeros(nwin, np.uint64)
+    for i in range(n):
+        pres |= bits[:, i].astype(np.uint64) << np.uint64(i)
+    st = torch.full((nwin,), 7, dtype=torch.uint8, device="cuda")
+    c.decode_batch(code, d, torch.from_numpy(pres.view(np.int64)).cuda(), st, **kw)
+    torch.cuda.synchronize()
+    got, gst = d.cpu().numpy(), st.cpu().numpy()
+    scheme = "gf" if matrix == "cauchy" else "gf-vdm"
+    for w in range(nwin):
+        S = L if sym_len is None else int(sym_len[w])
+        sym = enc[w, :, :S].copy()
+        sym[~bits[w]] = 0xAB
+        _, ok = N.decode(scheme, k, r, sym, int(pres[w]))
+        assert gst[w] == (0 if ok else 1), f"window {w}: status {gst[w]}, oracle ok={ok}"
+        if ok:
+            assert np.array_equal(got[w, :k, :S], wins[w, :k, :S]), f"window {w}: recovered bytes differ"
+    return got, gst
+
+
+@pytest.mark.parametrize("matrix", ["cauchy", "vandermonde"])
+@pytest.mark.parametrize("k", [16, 24, 32])
+@pytest.mark.parametrize("L", [1, 33, 1200])
+def test_bsdec_vs_oracle(k, matrix, L):
+    c = _ctx(6)
+    try:
+        rng = np.random.default_rng(k + L)
+        bits = _erasures(96, k, 8, rng, lo=3)
+        bits[0] = True
+        bits[1, :8] = False  # exactly r = 8 sources, every repair present
+        _, gst = _run(c, k, 8, matrix, L, 96, bits)
+        assert gst[0] == 0 and gst[1] == 0
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("min_e", [1, 4, 8])
+def test_bsdec_threshold_and_off_agree(min_e):
+    """Routing at several thresholds, and none (0): the same bytes and statuses."""
+    k, r, L, nwin = 32, 8, 300, 120
+    rng = np.random.default_rng(min_e)
+    bits = _erasures(nwin, k, r, rng)
+    outs = []
+    for m in (0, min_e):
+        c = _ctx(m)
+        try:
+            outs.append(_run(c, k, r, "cauchy", L, nwin, bits, seed=5))
+        finally:
+            c.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_bsdec_mixed_lengths_config4_shape():
+    """Per-window lengths 1200/9000 mixed (config 4's shape, stride 9008) with
+    many erasures: the routed windows' units span one or several passes."""
+    k, r, nwin = 32, 8, 64
+    rng = np.random.default_rng(44)
+    bits = _erasures(nwin, k, r, rng, lo=5)
+    sl = np.where(rng.random(nwin) < 0.5, 1202, 9002).astype(np.uint32)
+    sl[::7] = rng.integers(1, 9002, len(sl[::7]))
+    c = _ctx(6)
+    try:
+        _run(c, k, r, "cauchy", 9002, nwin, bits, sym_len=sl)
+    finally:
+        c.close()
+
+
+def test_bsdec_every_routed_pattern_small():
+    """k 16 r 8: every e = 6..8 with a fixed repair loss pattern sweep over windows
+    (exactly which repairs are present moves the pivots)."""
+    k, r = 16, 8
+    rows = []
+    rng = np.random.default_rng(8)
+    for e in (6, 7, 8):
+        for lost_rep in range(0, r - e + 1):
+            b = np.ones(k + r, bool)
+            b[rng.choice(k, e, replace=False)] = False
+            if lost_rep:
+                b[k + rng.choice(r, lost_rep, replace=False)] = False
+            rows.append(b)
+    bits = np.array(rows)
+    c = _ctx(6)
+    try:
+        _, gst = _run(c, k, r, "vandermonde", 64, len(bits), bits)
+        assert (gst == 0).all()
+    finally:
+        c.close()

@@ -92,7 +92,8 @@ def _erasures(nwin, k, r, rng, max_e=None):
 @pytest.mark.parametrize("k,r,matrix,L", [(60, 8, "cauchy", 1200), (100, 4, "cauchy", 40),
                                           (200, 8, "cauchy", 1200), (248, 8, "cauchy", 300),
                                           (90, 6, "vandermonde", 1200), (150, 8, "rlc", 1200),
-                                          (250, 6, "rlc", 64),
+                                          (250, 6, "rlc", 64), (75, 5, "cauchy", 200),
+                                          (180, 7, "vandermonde", 1200), (68, 4, "rlc", 16),
                                           # r < 4: the combine-job passes (the bit-sliced kernel takes r >= 4)
                                           (70, 2, "cauchy", 1200), (130, 3, "rlc", 500), (65, 1, "cauchy", 100)])
 def test_wide_encode_decode_vs_oracle(ctx, k, r, matrix, L):
@@ -136,6 +137,19 @@ def test_wide_per_window_lengths(ctx):
     bits = _erasures(nwin, k, r, rng, max_e=r)
     sl = rng.integers(100, L + 1, nwin).astype(np.uint32)
     _run(ctx, k, r, "cauchy", L, nwin, bits, sym_len=sl)
+
+
+def test_wide_two_stage_path():
+    """With the bit-sliced kernels off (tuning "bitslice" 0) the wide decode takes
+    the two-stage combine passes (fec_wide.hip): the same bytes and statuses."""
+    c = fecgpu.Context()
+    try:
+        c.set_tuning("bitslice", 0)
+        k, r, nwin = 120, 8, 24
+        bits = _erasures(nwin, k, r, np.random.default_rng(21))
+        _run(c, k, r, "cauchy", 700, nwin, bits)
+    finally:
+        c.close()
 
 
 def test_wide_narrow_only_entry_points(ctx):
