@@ -20,9 +20,6 @@
 
 using namespace fecgpu;
 
-#ifndef FECGPU_CHECK
-#define FECGPU_CHECK 0  // bounds-checked debug build (fec_kernels.hip); lib/libfecgpu_check.so
-#endif
 
 namespace {
 
@@ -175,6 +172,7 @@ struct fecgpu_ctx {
     std::map<int, std::vector<std::pair<void *, size_t>>> sw_scratch;
     std::map<int, hipEvent_t> sw_event;
     std::map<int, SwSticky *> sw_sticky;  // asynchronous decodes' error flags, per device
+    std::map<int, ChkRec *> chk_rec;      // FECGPU_CHECK builds: the index-checking kernels' fault record
     struct LbState {
         void *mem = nullptr;
         uint64_t nchunk = 0;
@@ -400,6 +398,10 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
             if (b.first) (void)hipFree(b.first);
     }
     if (ctx->sw_host) (void)hipHostFree(ctx->sw_host);
+    for (auto &kv : ctx->chk_rec) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second);
+    }
     for (auto &kv : ctx->sw_sticky) {
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second);
@@ -710,6 +712,9 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
     }
     ssize_t rc = ctx_sw_begin(ctx, s);
     if (rc) return rc;
+    ChkRec *chk = nullptr;
+    rc = ctx_chk_record(ctx, &chk);
+    if (rc) return rc;
     if (decode && mP) {
         // the bit-sliced decode (fec_kernels.hip gf_decode_bs_kernel): a plan
         // per window in LDS, syndromes of the received sources by the plane
@@ -747,9 +752,11 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
         HIP_TRY(launch_wide(win, present, status, P, nwin, stride, ncol, k, r, decode, reinterpret_cast<CombJob *>(b),
                             reinterpret_cast<uint64_t *>(b + o_out), b + o_coef, s,
                             reinterpret_cast<CombJob *>(b + o_j1), reinterpret_cast<uint64_t *>(b + o_o1), b + o_syn,
-                            mP, decode ? mPI : nullptr),
+                            mP, decode ? mPI : nullptr, chk),
                 "wide batch launch");
     }
+    rc = ctx_chk_finish(ctx, s, decode ? "wide decode" : "wide encode");  // FECGPU_CHECK builds (release: nothing)
+    if (rc) return rc;
     rc = ctx_sw_end(ctx, s);
     if (rc) return rc;
     if (flags & FECGPU_F_SYNC) HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
@@ -877,7 +884,7 @@ ssize_t set_check_ranges(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, 
             a.chk.n[1] = (n - 1) * (a.wpitch + a.out_wdelta) + r * a.stride;
         }
     }
-    for (int i = 0; i < 2; i++) a.chk.n[i] -= std::min<uint64_t>(a.chk.n[i], (uint64_t)ctx->check_shrink);
+    for (int i = 0; i < kChkRanges; i++) a.chk.n[i] -= std::min<uint64_t>(a.chk.n[i], (uint64_t)ctx->check_shrink);
     return 0;
 }
 #endif
@@ -1286,6 +1293,54 @@ ssize_t ctx_sw_sticky(fecgpu_ctx *ctx, SwSticky **p) {
     *p = w;
     return 0;
 }
+
+ssize_t ctx_chk_record(fecgpu_ctx *ctx, ChkRec **p) {
+    *p = nullptr;
+    if (!FECGPU_CHECK) return 0;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    ChkRec *&w = ctx->chk_rec[dev];
+    if (!w) {
+        void *m = nullptr;
+        HIP_TRY(hipMalloc(&m, sizeof(ChkRec)), "hipMalloc check record");
+        const hipError_t e = hipMemset(m, 0, sizeof(ChkRec));
+        if (e != hipSuccess) {
+            (void)hipFree(m);
+            return dev_err(e, "hipMemset check record");
+        }
+        w = static_cast<ChkRec *>(m);
+    }
+    *p = w;
+    return 0;
+}
+
+ssize_t ctx_chk_finish(fecgpu_ctx *ctx, hipStream_t s, const char *what) {
+    if (!FECGPU_CHECK) return 0;
+    HIP_TRY(hipStreamSynchronize(s), "check: sync");
+    ChkRec *d = nullptr;
+    ssize_t rc = ctx_chk_record(ctx, &d);
+    if (rc) return rc;
+    ChkRec h{};
+    HIP_TRY(hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost), "check: read record");
+    if (h.bad) {
+        const ChkRec z{};
+        HIP_TRY(hipMemcpy(d, &z, sizeof(z), hipMemcpyHostToDevice), "check: reset record");
+    }
+    uint64_t nbad = 0, first = 0;
+    HIP_TRY(take_bounds_faults(&nbad, &first), "check: read faults");
+    if (!h.bad && !nbad) return 0;
+    char msg[320];
+    if (h.bad)
+        snprintf(msg, sizeof msg, "bounds check: %s made %llu accesses outside their allocations (first: site %llu, index %llu)",
+                 what, h.bad, h.first >> 48, h.first & 0xFFFFFFFFFFFFull);
+    else
+        snprintf(msg, sizeof msg, "bounds check: %s made %llu symbol accesses outside their rows (first at %#llx)", what,
+                 (unsigned long long)nbad, (unsigned long long)first);
+    g_last_error = msg;
+    return FECGPU_ERR_DEVICE;
+}
+
+uint64_t ctx_check_shrink(const fecgpu_ctx *ctx) { return (uint64_t)ctx->check_shrink; }
 
 ssize_t ctx_sw_lookback(fecgpu_ctx *ctx, uint64_t nchunk, SwLookback *lb, uint32_t *epoch) {
     int dev = 0;

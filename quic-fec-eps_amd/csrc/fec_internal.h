@@ -9,6 +9,17 @@
 #include "../../include/fecgpu.h"
 #include "fec_spec.h"
 
+#ifndef FECGPU_CHECK
+// Bounds-checked debug build (GPU AddressSanitizer is not available
+// on this pool), lib/libfecgpu_check.so: every symbol load / store of the block
+// kernels is checked against the byte ranges the host computed for the launch
+// (ChkRange), and the sliding-window, wide and combine kernels check the
+// indices of the rows, jobs, records and log entries they address against
+// their allocations (CHK_IDX).  An access outside is not performed (loads
+// give zero) and is recorded; the host fails the call with FECGPU_ERR_DEVICE.
+#define FECGPU_CHECK 0
+#endif
+
 namespace fecgpu {
 
 constexpr int kBlock = 256;   // 4 waves of 64
@@ -19,9 +30,30 @@ constexpr int kMaxR = 8;
 // Geometry + decode inputs of one batch, passed by value as the kernel argument.
 // Byte ranges [lo, lo + n) that symbol loads / stores of one launch may touch
 // (FECGPU_CHECK builds; lo is an address, n == 0 = range unused).
+constexpr int kChkRanges = 4;
 struct ChkRange {
-    uint64_t lo[2], n[2];
+    uint64_t lo[kChkRanges], n[kChkRanges];
 };
+
+// FECGPU_CHECK builds: the fault record of the kernels that check indices
+// (device memory, ctx_chk_record): faults, and the first one's site << 48 |
+// index.  Release builds pass a null record and check nothing.
+struct ChkRec {
+    unsigned long long bad, first;
+};
+#if FECGPU_CHECK
+__device__ __forceinline__ bool chk_index(ChkRec *rec, uint64_t i, uint64_t n, uint32_t site) {
+    if (i < n) return true;
+    if (rec) {
+        atomicAdd(&rec->bad, 1ull);
+        atomicCAS(&rec->first, 0ull, ((unsigned long long)site << 48) | (i & 0xFFFFFFFFFFFFull));
+    }
+    return false;
+}
+#define CHK_IDX(rec, i, n, site) ::fecgpu::chk_index((rec), (uint64_t)(i), (uint64_t)(n), (uint32_t)(site))
+#else
+#define CHK_IDX(rec, i, n, site) true
+#endif
 
 struct BatchArgs {
     uint8_t *win;
@@ -228,6 +260,7 @@ struct CombArgs {
     // nullable (sliding-window decode): the call's error bits; the launch does
     // nothing when kSwErrHeader is set (a bad header list recovers nothing)
     const uint32_t *err;
+    ChkRange chk;  // FECGPU_CHECK builds: the arrays the jobs' rows lie in (inputs, xor rows, outputs)
     // every job has the same coefficient block (a block code's parity rows:
     // wide encode): [nout_max][nin_max] at coef, its tables built once per
     // workgroup and shared by the workgroup's jobs (job regions hold only their
@@ -265,7 +298,8 @@ hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t 
 hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
                        uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
                        uint64_t *outs, uint8_t *coef, hipStream_t s, CombJob *jobs1, uint64_t *outs1,
-                       uint8_t *syn, const uint32_t *masks_P = nullptr, const uint32_t *masks_PI = nullptr);
+                       uint8_t *syn, const uint32_t *masks_P = nullptr, const uint32_t *masks_PI = nullptr,
+                       ChkRec *chk = nullptr);
 
 // encode: job t = repair t (coefficients at coef + t * kSwCoefPitch, output rep row t).
 // group > 1: the repairs t0 = g * group .. t0 + group - 1 share job g when
@@ -317,7 +351,8 @@ struct SwStreamArgs {
     int segcap;         // repairs per segment (<= kSwSeg)
     uint64_t nseg;      // segments; workgroup b takes [b nseg / grid, (b + 1) nseg / grid)
     uint32_t lds;       // dynamic LDS bytes
-    const uint8_t *rlc;  // nullable: the dense coefficient table (ctx_rlc_table)
+    const uint8_t *rlc;
+    ChkRec *chk;        // FECGPU_CHECK builds: the fault record (release: null)  // nullable: the dense coefficient table (ctx_rlc_table)
 };
 // C: dwords per lane (1..5, dividing the row's dwords); LDS budget per workgroup in bytes
 hipError_t launch_sw_stream(SwStreamArgs a, int C, uint32_t budget, hipStream_t s);
@@ -439,6 +474,8 @@ struct SwDecArgs {
     uint32_t *starts;     // [nsrc] lost indices of the larger systems' first unknowns
                           // (ctr->nstart of them, in no particular order)
     const uint8_t *rlc;   // nullable: the dense coefficient table (kRlcRow bytes per repair key)
+    uint64_t lb_cap;      // look-back records allocated (chunks)
+    ChkRec *chk;          // FECGPU_CHECK builds: the fault record (release: null)
 };
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s);    // statuses, lost list, systems
 hipError_t launch_sw_dec_long(const SwDecArgs &a, hipStream_t s);    // long systems: logs, syndrome jobs
@@ -459,7 +496,8 @@ ssize_t set_dev_error(hipError_t e, const char *what);
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *jobs,
                        void *coef, void *outs, hipStream_t s, int group = 1,
-                       const fecgpu_sw_repair *hdr_host = nullptr, int stream = 0, const uint8_t *rlc = nullptr);
+                       const fecgpu_sw_repair *hdr_host = nullptr, int stream = 0, const uint8_t *rlc = nullptr,
+                       ChkRec *chk = nullptr);
 // the ctx's "sw_group" tuning (repairs per sliding-window encode job)
 int ctx_sw_group(const fecgpu_ctx *ctx);
 // the ctx's "sw_stream" tuning: 0 combine jobs, 1..5 the streaming encode
@@ -487,6 +525,14 @@ ssize_t ctx_sw_scratch(fecgpu_ctx *ctx, int slot, size_t bytes, void **p);
 // the ctx's pinned host staging block for sliding-window decodes (grown on
 // demand; a decode synchronizes before returning, so the next may reuse it)
 ssize_t ctx_sw_host(fecgpu_ctx *ctx, size_t bytes, void **p);
+// FECGPU_CHECK builds: the current device's fault record of the index-checking
+// kernels (allocated zeroed; release builds: null), and the end of a checked
+// call: `s` synchronized, the record and the block kernels' symbol faults read
+// and cleared, FECGPU_ERR_DEVICE (with the site) if any (release: nothing)
+ssize_t ctx_chk_record(fecgpu_ctx *ctx, ChkRec **p);
+ssize_t ctx_chk_finish(fecgpu_ctx *ctx, hipStream_t s, const char *what);
+// bytes a test takes off the end of every checked range ("check_shrink")
+uint64_t ctx_check_shrink(const fecgpu_ctx *ctx);
 // the current device's sticky error word of asynchronous decodes (allocated zeroed)
 ssize_t ctx_sw_sticky(fecgpu_ctx *ctx, SwSticky **p);
 // Look-back state of the fused decode plan on the current device for nchunk

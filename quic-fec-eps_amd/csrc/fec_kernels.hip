@@ -37,14 +37,6 @@ constexpr int kGfdU = 8;
 // GF encode at r > 4 (VALU-bound, paired rows): at least 3 waves per SIMD, a
 // few spilled registers for occupancy: 7% faster than 2 waves on cfg4 (r01)
 #define GFE_WAVES __attribute__((amdgpu_waves_per_eu(R > 4 ? 3 : 1, 8)))
-#ifndef FECGPU_CHECK
-// Bounds-checked debug build (GPU AddressSanitizer is not available
-// on this pool): every symbol load / store is checked against the byte ranges
-// the host computed for the launch (BatchArgs::chk); an access outside them is
-// not performed (loads return zero) and is recorded for the host, which fails
-// the call with FECGPU_ERR_DEVICE.  Built as lib/libfecgpu_check.so.
-#define FECGPU_CHECK 0
-#endif
 
 namespace fecgpu {
 
@@ -68,7 +60,7 @@ __device__ __forceinline__ bool chk_ok(const uint8_t *p) {
     const uint64_t x = reinterpret_cast<uint64_t>(p);
     bool ok = false;
 #pragma unroll
-    for (int i = 0; i < 2; i++) ok |= s_chk.n[i] >= 16 && x - s_chk.lo[i] <= s_chk.n[i] - 16;
+    for (int i = 0; i < kChkRanges; i++) ok |= s_chk.n[i] >= 16 && x - s_chk.lo[i] <= s_chk.n[i] - 16;
     if (!ok) {
         atomicAdd(&g_chk_bad[0], 1ull);
         atomicCAS(&g_chk_bad[1], 0ull, (unsigned long long)x);
@@ -1729,6 +1721,13 @@ void gf_decode_bs_kernel(BatchArgs a) {
                 for (int c = 0; c < 4; c++) coff[c] = (uint32_t)(pc[c] - gb);
                 const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                     const_cast<uint8_t *>(gb), 0, (int)(uint32_t)((uint64_t)nb * a.wpitch), bsd::kRsrcRaw);
+#if FECGPU_CHECK
+                // the resource's span lies in the launch's windows (its loads stay inside it)
+                if (tid == 0 && s0 == 0) {
+                    (void)chk_ok(gb);
+                    (void)chk_ok(gb + (uint64_t)nb * a.wpitch - 16);
+                }
+#endif
                 rbs4::dec_unit<R>(rs, coff, pc, g.stride[wl], k, (rbs::cmask)a.enc_bs, live, rg, nw);
             } else {
                 uint8_t *pa, *pb;
@@ -2070,17 +2069,9 @@ __global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
     // sparse launches: the gathered jobs' headers first (kCombListLds)
     uint8_t *regions = reinterpret_cast<uint8_t *>(dyn) + (a.sparse ? kCombListLds : 0u);
     constexpr int RT = CombRegion<R>::RT;
-#if FECGPU_CHECK
-    // the checked build bounds the block kernels' symbol accesses; the
-    // sliding-window jobs address rows through their own tables: unchecked
-    if (tid == 0) {
-        s_chk.lo[0] = 0;
-        s_chk.n[0] = ~0ull;
-        s_chk.lo[1] = 0;
-        s_chk.n[1] = 0;
-    }
-    __syncthreads();
-#endif
+    // checked builds: every row a job reads or writes lies in the launch's
+    // arrays (CombArgs::chk: inputs, xor rows, outputs)
+    CHK_PROLOGUE(a);
     if (a.err && (*a.err & kSwErrHeader)) return;  // the whole grid stands down (device-sized decode launches)
     const uint64_t njobs = a.njobs + (a.extra ? (uint64_t)(*a.extra >> a.extra_shift) : 0ull);
     int nin_max = a.nin_max, wpb = a.wpb;
@@ -2477,8 +2468,12 @@ hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t 
     a.enc_bs = masks;
     a.out_delta = out_delta;
     a.out_wdelta = out_wdelta;
-    a.chk.lo[0] = 0;  // FECGPU_CHECK builds: rows addressed by the caller's layout, unchecked
-    a.chk.n[0] = ~0ull;
+    // FECGPU_CHECK builds: the input rows, and the outputs (out_delta /
+    // out_wdelta may send them to another array: the wide decode's syndromes)
+    a.chk.lo[0] = reinterpret_cast<uint64_t>(win);
+    a.chk.n[0] = nwin * wpitch;
+    a.chk.lo[1] = reinterpret_cast<uint64_t>(win) + (uint64_t)k * stride + out_delta;
+    a.chk.n[1] = (nwin - 1) * (wpitch + out_wdelta) + (uint64_t)r * stride;
     LaunchPlan p{};
     p.flat = true;
     p.rbitslice = true;

@@ -71,16 +71,20 @@ bool header_ok(const fecgpu_sw_repair &h, uint64_t nsrc) {
 // One combine launch (fec_internal.h CombJob) over njobs jobs (plus *extra
 // more, at most extra_max, when extra is given).
 ssize_t run_comb(const CombJob *jobs, uint64_t njobs, const uint8_t *coef, const uint64_t *outs,
-                 const uint8_t *in_base, uint8_t *out_base, const uint8_t *xor_base, uint32_t S,
+                 const uint8_t *in_base, uint64_t in_bytes, uint8_t *out_base, uint64_t out_bytes, uint32_t S,
                  uint32_t stride, int R, int nin_max, hipStream_t s, const uint32_t *extra = nullptr,
                  uint64_t extra_max = 0, bool skip = false) {
     CombArgs a{};
+    a.chk.lo[0] = reinterpret_cast<uint64_t>(in_base);  // FECGPU_CHECK builds: the sources and the repairs
+    a.chk.n[0] = in_bytes;
+    a.chk.lo[1] = reinterpret_cast<uint64_t>(out_base);
+    a.chk.n[1] = out_bytes;
     a.jobs = jobs;
     a.coef = coef;
     a.outs = outs;
     a.in_base = in_base;
     a.out_base = out_base;
-    a.xor_base = xor_base;
+    a.xor_base = nullptr;
     a.njobs = njobs;
     a.extra = extra;
     a.extra_max = extra_max;
@@ -159,10 +163,11 @@ int sw_stream_dwords(int stream, uint32_t S) {
 ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fecgpu_sw_repair *hdr,
                        uint64_t nrep, int max_window, uint32_t S, uint32_t stride, void *pj, void *pc,
                        void *po, hipStream_t s, int group, const fecgpu_sw_repair *hdr_host, int stream,
-                       const uint8_t *rlc) {
+                       const uint8_t *rlc, ChkRec *chk) {
     if (stream > 0 && nsrc < kSwStreamSources) {
         SwStreamArgs sa{};
         sa.rlc = rlc;
+        sa.chk = chk;
         sa.src = src;
         sa.rep = rep;
         sa.hdr = hdr;
@@ -189,7 +194,8 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
     ca.rlc = rlc;
     if (ca.group == 1) {
         SW_TRY(launch_sw_enc_coef(ca, s), "sliding-window coefficient launch");
-        return run_comb(ca.jobs, nrep, ca.coef, ca.outs, src, rep, nullptr, S, stride, 1, max_window, s);
+        return run_comb(ca.jobs, nrep, ca.coef, ca.outs, src, nsrc * stride, rep, nrep * stride, S, stride, 1,
+                        max_window, s);
     }
     // the tail counter sits after the jobs (sw_enc_jobs leaves room); the host
     // copy of the headers, when given, says whether a tail can occur at all
@@ -198,7 +204,7 @@ ssize_t sw_encode_core(const uint8_t *src, uint64_t nsrc, uint8_t *rep, const fe
     ca.tail = reinterpret_cast<uint32_t *>(ca.jobs + ngroups + nrep);
     SW_TRY(hipMemsetAsync(ca.tail, 0, sizeof(uint32_t), s), "sliding-window tail reset");
     SW_TRY(launch_sw_enc_coef(ca, s), "sliding-window coefficient launch");
-    return run_comb(ca.jobs, ngroups, ca.coef, ca.outs, src, rep, nullptr, S, stride, ca.group,
+    return run_comb(ca.jobs, ngroups, ca.coef, ca.outs, src, nsrc * stride, rep, nrep * stride, S, stride, ca.group,
                     std::max(ca.span_max, max_window), s, tail ? ca.tail : nullptr, nrep, true);
 }
 
@@ -213,13 +219,16 @@ ssize_t sw_encode_dev(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uint8_
     const int group = ctx_sw_group(ctx), stream = ctx_sw_stream(ctx);
     const uint8_t *rlc = nullptr;
     RC_TRY(ctx_rlc_table(ctx, s, &rlc));
+    ChkRec *chk = nullptr;
+    RC_TRY(ctx_chk_record(ctx, &chk));
     if (stream > 0 && nsrc < kSwStreamSources)
         return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, nullptr, nullptr, nullptr, s,
-                              group, hdr_host, stream, rlc);
+                              group, hdr_host, stream, rlc, chk);
     RC_TRY(ctx_sw_scratch(ctx, 0, sw_enc_jobs(nrep, group) * sizeof(CombJob), &pj));
     RC_TRY(ctx_sw_scratch(ctx, 1, nrep * kSwCoefPitch, &pc));
     RC_TRY(ctx_sw_scratch(ctx, 2, nrep * sizeof(uint64_t), &po));
-    return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s, group, hdr_host, 0, rlc);
+    return sw_encode_core(src, nsrc, rep, hdr, nrep, max_window, S, stride, pj, pc, po, s, group, hdr_host, 0, rlc,
+                          chk);
 }
 
 // ---- decode (device plan: fec_swdec.hip) ----------------------------------
@@ -324,10 +333,12 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     a.src = src;
     a.synd = static_cast<const uint8_t *>(psyn);
     a.sticky = sticky;
+    RC_TRY(ctx_chk_record(ctx, &a.chk));
     RC_TRY(ctx_rlc_table(ctx, s, &a.rlc));
     {  // the plan kernel writes the counters itself: nothing to clear
         SwLookback lb{};
         RC_TRY(ctx_sw_lookback(ctx, (nsrc + kSwPlanChunk - 1) / kSwPlanChunk, &lb, &a.epoch));
+        a.lb_cap = (nsrc + kSwPlanChunk - 1) / kSwPlanChunk;
         a.lb_flag = lb.flag;
         a.lb_agg = lb.agg;
         a.lb_inc = lb.inc;
@@ -358,6 +369,16 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     sa.nout_max = 1;
     sa.nin_dev = &a.ctr->wmax;
     sa.err = &a.ctr->err;
+    // FECGPU_CHECK builds: sources in (and out: the one-unknown systems), repairs
+    // xor-ed in, syndrome rows out; less "check_shrink" bytes each
+    const uint64_t shrink = ctx_check_shrink(ctx);
+    const auto range = [&](CombArgs &c, int i, const void *p, uint64_t n) {
+        c.chk.lo[i] = reinterpret_cast<uint64_t>(p);
+        c.chk.n[i] = n - std::min(n, shrink);
+    };
+    range(sa, 0, src, nsrc * stride);
+    range(sa, 1, rep, nrep * stride);
+    range(sa, 2, psyn, nrep * stride);
     sa.budget = ncol >= 64 ? kCombBudgetWide : kCombBudget;
     SW_TRY(launch_comb(sa, 1, s), "sliding-window syndrome launch");
     CombArgs va = sa;
@@ -367,6 +388,9 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     va.in_base = static_cast<const uint8_t *>(psyn);
     va.out_base = src;
     va.xor_base = nullptr;
+    va.chk = ChkRange{};
+    range(va, 0, psyn, nrep * stride);
+    range(va, 1, src, nsrc * stride);
     va.extra = &a.ctr->nlost;  // a slot per unknown, filled by its small system
     va.extra_max = nsrc;
     va.njobs = 0;
@@ -440,12 +464,14 @@ ssize_t fecgpu_sw_encode(fecgpu_ctx *ctx, const uint8_t *src, uint64_t nsrc, uin
         RC_TRY(sw_encode_dev(ctx, static_cast<uint8_t *>(ds), nsrc, static_cast<uint8_t *>(dr),
                              static_cast<fecgpu_sw_repair *>(dh), nrep, hmax, sym_len, stride, s, hdr));
         SW_TRY(hipMemcpyAsync(rep, dr, nrep * stride, hipMemcpyDeviceToHost, s), "D2H sw repairs");
+        RC_TRY(ctx_chk_finish(ctx, s, "sliding-window encode"));  // FECGPU_CHECK builds (release: nothing)
         RC_TRY(ctx_sw_end(ctx, s));
         SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
         return (ssize_t)nrep;
     }
     RC_TRY(ctx_sw_begin(ctx, s));
     RC_TRY(sw_encode_dev(ctx, src, nsrc, rep, hdr, nrep, mw, sym_len, stride, s));
+    RC_TRY(ctx_chk_finish(ctx, s, "sliding-window encode"));  // FECGPU_CHECK builds (release: nothing)
     RC_TRY(ctx_sw_end(ctx, s));
     if (flags & FECGPU_F_SYNC) SW_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
     return (ssize_t)nrep;
@@ -498,6 +524,7 @@ ssize_t fecgpu_sw_decode(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *src_prese
                 SW_TRY(hipMemcpyAsync(src, dsrc, nsrc * stride, hipMemcpyDeviceToHost, s), "D2H sw sources");
             return 0;
         });
+    RC_TRY(ctx_chk_finish(ctx, s, "sliding-window decode"));  // FECGPU_CHECK builds (release: nothing)
     RC_TRY(ctx_sw_end(ctx, s));
     return rc;
 }
@@ -523,6 +550,7 @@ ssize_t fecgpu_sw_decode_device(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *sr
         rc = sw_decode_core(ctx, src, src_present, nsrc, rep, rep_present, hdr, nrep, sym_len, stride, src_status, s,
                             nullptr, ctx_sw_log_entries(ctx, nsrc, nrep), sticky);
     }
+    RC_TRY(ctx_chk_finish(ctx, s, "sliding-window decode"));  // FECGPU_CHECK builds (release: nothing)
     RC_TRY(ctx_sw_end(ctx, s));
     return rc;
 }

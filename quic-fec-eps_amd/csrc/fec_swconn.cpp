@@ -128,10 +128,12 @@ ssize_t enc_launch(fecgpu_sw_encoder *e) {
         S.hdr[t].fss -= e->base;
     }
     const uint8_t *rlc = nullptr;
+    ChkRec *chk = nullptr;  // FECGPU_CHECK builds: faults surface at the ctx's next checked call
     ssize_t rc = ctx_fault_take(e->ctx) ? (ssize_t)FECGPU_ERR_DEVICE : ctx_rlc_table(e->ctx, e->s, &rlc);
+    if (rc >= 0) rc = ctx_chk_record(e->ctx, &chk);
     if (rc >= 0)
         rc = sw_encode_core(e->src, e->cap, S.rep, S.hdr, n, e->p.window, e->p.symbol_size, e->stride, S.jobs, S.coef,
-                            S.outs, e->s, e->group, S.hdr, e->stream, rlc);
+                            S.outs, e->s, e->group, S.hdr, e->stream, rlc, chk);
     if (rc >= 0) {
         const hipError_t er = hipEventRecord(S.ev, e->s);
         if (er != hipSuccess) rc = set_dev_error(er, "hipEventRecord");

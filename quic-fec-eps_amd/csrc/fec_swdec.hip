@@ -72,6 +72,27 @@ __device__ __forceinline__ void set_tab(uint32_t (&t)[5], uint32_t c) {
 
 __device__ __forceinline__ uint64_t lanes_below(int lane) { return (1ull << lane) - 1ull; }
 
+// FECGPU_CHECK builds: every row, job slot, record and log entry an index
+// addresses is checked against its allocation (SwDecArgs sizes); a failing
+// access is skipped and recorded in a.chk with its site (the host fails the
+// call).  Sites:
+enum : uint32_t {
+    kChkSynJob = 1,    // syn_jobs / syn_outs / coef rows: nrep + nsrc slots
+    kChkSolJob = 2,    // sol_jobs / sol_outs: nsrc + 8 slots
+    kChkSolCoef = 3,   // sol_coef bytes: nrep * kSwSmallE
+    kChkSrcRow = 4,    // sources (stat, arrival flags, src rows): nsrc
+    kChkLost = 5,      // lost list / reachL / lkind / starts: nsrc
+    kChkRank = 6,      // reach / rcnt: nsrc + 1
+    kChkHdr = 7,       // headers / repair flags / synrow: nrep
+    kChkLook = 8,      // look-back records and flags: lb_cap chunks
+    kChkLong = 9,      // queued long systems: long_cap
+    kChkLog = 10,      // operation log entries: log_cap
+    kChkPiv = 11,      // pivot rows (pivcoef / pivhi / pivt / pivdata): piv_cap
+    kChkSynRow = 12,   // syndrome rows: nrep
+    kChkColumn = 13,   // byte offset within a row: stride
+};
+#define SWC(i, n, site) CHK_IDX(a.chk, (i), (n), (site))
+
 // a header the plan may act on (fec_sw.cpp header_ok's device twin): a window
 // of 1..kSwMaxWindow sources inside the stream, dt <= 15
 __device__ __forceinline__ bool hdr_ok(const fecgpu_sw_repair &h, uint64_t nsrc) {
@@ -273,6 +294,8 @@ struct SysLds {
     int8_t piv[ME];
 };
 
+__device__ __forceinline__ int d_of(uint64_t dm, int lane) { return __popcll(dm & lanes_below(lane)); }
+
 // One wave solves the small system lost[x .. x + e) with its p equations
 // (repair indices eq[], ascending): the round-2 sw_plan_kernel, fed on the
 // device.  Returns the unknowns it determined; *nin the solve's input rows.
@@ -290,6 +313,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     // go into A, the received sources' into its syndrome job
     for (int q = lane; q < p; q += 64) {
         const uint32_t t = eq[q];
+        if (!SWC(t, a.nrep, kChkHdr)) continue;
         const fecgpu_sw_repair h = a.hdr[t];
         {
             // the row was drawn by the plan: move the unknowns' entries into A
@@ -302,6 +326,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
                 const uint64_t i = U[u];
                 if (i < h.fss) continue;
                 if (i >= h.fss + h.nss) break;
+                if (!SWC(i - h.fss, kSwCoefPitch, kChkSynJob)) break;
                 M[q * kPitch + u] = cb[i - h.fss];
                 cb[i - h.fss] = 0;
             }
@@ -367,7 +392,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     for (int q = lane; q < p; q += 64) {
         bool need = false;
         for (int col = 0; col < e && !need; col++) need = ((dm >> col) & 1) && M[S.piv[col] * kPitch + e + q] != 0;
-        if (!need) a.syn_jobs[eq[q]].nout = 0;
+        if (!need && SWC(eq[q], a.nrep, kChkSynJob)) a.syn_jobs[eq[q]].nout = 0;
     }
     if (ndet == 0) return 0;
     // One unknown (most systems at low loss): x = s_t / c for the pivot
@@ -380,6 +405,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         const int pr = S.piv[0];
         const uint32_t t = eq[pr];
         const uint32_t iv = M[pr * kPitch + e + pr];  // T[pr][pr] = 1 / c
+        if (!SWC(t, a.nrep, kChkSynJob) || !SWC(U[0], a.nsrc, kChkSrcRow)) return 0;
         const uint32_t nss = a.hdr[t].nss;
         uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
         uint32_t tab[5];
@@ -402,7 +428,8 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     const uint32_t t_first = eq[0], nin = eq[p - 1] - t_first + 1;
     const uint64_t c0 = (uint64_t)t_first * kSwSmallE;
     const uint64_t o0 = x, j0 = x;
-    if (det) {
+    if (det && SWC(c0 + (uint64_t)(d_of(dm, lane) + 1) * nin - 1, (uint64_t)a.nrep * kSwSmallE, kChkSolCoef) &&
+        SWC(o0 + d_of(dm, lane), a.nsrc + 8, kChkSolJob) && SWC(U[lane], a.nsrc, kChkSrcRow)) {
         const int d = __popcll(dm & lanes_below(lane));
         uint8_t *cf = a.sol_coef + c0 + (uint64_t)d * nin;
         int q = 0;
@@ -415,7 +442,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         a.stat[U[lane]] = FECGPU_STATUS_OK;
     }
     const int nj = (ndet + kSwSolveOut - 1) / kSwSolveOut;
-    if (lane < nj) {
+    if (lane < nj && SWC(j0 + lane, a.nsrc + 8, kChkSolJob)) {
         CombJob J;
         J.in_off = (uint64_t)t_first * a.stride;
         J.coef_off = c0 + (uint64_t)lane * kSwSolveOut * nin;
@@ -440,7 +467,7 @@ __device__ bool sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, u
     bool fits = (int)e <= ME && (int)e < a.long_min;
     uint32_t p = 0;
     if (fits) {
-        if (lane < (int)e) S.U[lane] = a.lost[x + lane];
+        if (lane < (int)e && SWC(x + lane, a.nsrc, kChkLost)) S.U[lane] = a.lost[x + lane];
         for (uint64_t t0 = t_lo; t0 < t_hi; t0 += 64) {
             const uint64_t t = t0 + lane;
             bool hd = false;
@@ -461,7 +488,7 @@ __device__ bool sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, u
         if (LOCAL && (int)e <= kSwSmallE && (int)e < a.long_min) return true;
         if (lane == 0) {
             const uint32_t k = atomicAdd(&a.ctr->nlong, 1u);
-            if (k < a.long_cap) {
+            if (k < a.long_cap) {  // (the capacity test is the check: a full queue is kSwErrCapacity)
                 SwLong L{};
                 L.x0 = x;
                 L.e = e;
@@ -510,6 +537,7 @@ __device__ __forceinline__ void block_counts(const SwDecArgs &a, uint32_t rec, u
 // per system drawing its few equations' on as many lanes.  The long-system
 // pass draws its own rows again (and overwrites these).
 __device__ __forceinline__ void draw_row(const SwDecArgs &a, uint64_t t, const fecgpu_sw_repair &h) {
+    if (!SWC(t, a.nrep, kChkSynJob)) return;
     uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + t * kSwCoefPitch);
     rlc_words(a, h, [&](uint32_t q, uint32_t w) { cc[q] = w; });
 }
@@ -552,6 +580,7 @@ __device__ __forceinline__ uint32_t lb_flag_load(const uint32_t *f) {
 // records are two uint4 per chunk (lb_agg / lb_inc [2 * chunk]; kLbRecBytes)
 static_assert(kLbRecBytes == 2 * sizeof(uint4), "look-back record size");
 __device__ __forceinline__ void lb_publish(const SwDecArgs &a, uint32_t c, const LbRec &r, uint32_t state) {
+    if (!SWC(c, a.lb_cap, kChkLook)) return;
     uint32_t *dst = reinterpret_cast<uint32_t *>((state == kLbInc ? a.lb_inc : a.lb_agg) + 2 * (size_t)c);
     const uint32_t v[5] = {r.lost, r.reach, r.rep, r.wme, r.L};
 #pragma unroll
@@ -631,6 +660,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     __shared__ LbRec s_excl, s_agg;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t nch = (uint32_t)((a.nsrc + kPlanChunk - 1) / kPlanChunk);
+    if (!SWC(nch - 1, a.lb_cap, kChkLook)) return;  // (uniform: the look-back state must hold every chunk)
     if (tid == 0) {
         // chunks in dispatch order, so the look-back never waits on a block not
         // yet running (the counter starts every launch at 0; modulo: a counter
@@ -666,6 +696,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         CombJob E{};
         E.xor_off = kNoXor;
         for (uint64_t t = h0 + tid; t < h1; t += kBlock) {
+            if (!SWC(t, a.nrep, kChkSynJob)) break;
             a.syn_jobs[t] = E;
             const fecgpu_sw_repair h = a.hdr[t];
             bad |= !hdr_ok(h, a.nsrc);
@@ -1021,7 +1052,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             const uint64_t i = i0 + my0 + j;
             run = max(run, s_reach[my0 + j]);
             repc += s_rcnt[my0 + j];
-            if ((lostm >> j) & 1u) {
+            if (((lostm >> j) & 1u) && SWC(off, a.nsrc, kChkLost)) {
                 a.lost[off] = (uint32_t)i;
                 a.reachL[off] = run;
                 a.sol_jobs[off] = E;  // solve jobs in the unknowns' slots: empty unless filled
@@ -1041,7 +1072,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             a.rcnt[i0 + my0 + j] = rf[j];
         }
     }
-    if (my0 <= n && n <= my0 + kPlanPer && i1 == a.nsrc) {  // the thread holding the end
+    if (my0 <= n && n <= my0 + kPlanPer && i1 == a.nsrc) {  // the thread holding the end (reach / rcnt: nsrc + 1)
         a.reach[a.nsrc] = off;
         a.rcnt[a.nsrc] = repc;
     }
@@ -1051,6 +1082,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     // the chunk's lost sources: one-unknown systems solved, the rest classified
     for (uint32_t k = tid; k < nl; k += kBlock) {
         const uint32_t u = ex.lost + k, pos = s_lpos[k], rl = max(ex.reach, s_rl[k]);
+        if (!SWC(u, a.nsrc, kChkLost)) break;
         const uint64_t i = i0 + pos;
         const uint32_t prl = k > 0 ? max(ex.reach, s_rl[k - 1]) : (ex.lost ? ex.L : 0u);
         const bool start = u == 0 || prl <= i;
@@ -1073,7 +1105,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         if (single) {
             kind = 3;
             const uint2 pv = s_pv[k];  // the pivot found during the look-back
-            if (pv.x != ~0u) {
+            if (pv.x != ~0u && SWC(pv.x, a.nrep, kChkHdr)) {
                 const uint64_t t = pv.x;
                 const uint32_t cd = s_pcd[k], j = pv.y >> 24;
                 fecgpu_sw_repair h{};
@@ -1191,6 +1223,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     const uint32_t nstart = a.ctr->nstart;
     for (uint64_t k = (uint64_t)blockIdx.x * (kBlock / 64) + wave; k < nstart; k += nwaves) {
         const uint64_t x = a.starts[k];
+        if (!SWC(x, a.nsrc, kChkLost)) continue;
         const uint32_t lx = a.lost[x];
         // extent: up to the next start
         uint32_t e = 1;
@@ -1204,6 +1237,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
             }
             e += 64;
         }
+        if (!SWC(x + e - 1, a.nsrc, kChkLost)) continue;
         const uint32_t last = a.lost[x + e - 1];
         // candidate repairs: fss in [lx - wmax + 1, last]
         const uint64_t t_lo = a.rcnt[lx >= wmax ? lx - wmax + 1 : 0], t_hi = a.rcnt[(uint64_t)last + 1];
@@ -1251,6 +1285,12 @@ __device__ __forceinline__ void emit(SwOp *op, uint32_t kind, uint32_t sa, uint3
     *op = o;
 }
 
+// emit into log entry pos (checked against log_cap in FECGPU_CHECK builds)
+__device__ __forceinline__ void emit_at(const SwDecArgs &a, uint64_t pos, uint32_t kind, uint32_t sa, uint32_t sb,
+                                        uint32_t aux, uint32_t aux2, const uint32_t (&tab)[5]) {
+    if (SWC(pos, a.log_cap, kChkLog)) emit(a.log + pos, kind, sa, sb, aux, aux2, tab);
+}
+
 // Generate the next batch of rows (up to 64 equations from repair *next on)
 // into the staging area; returns the number staged (0: no more repairs).
 __device__ int long_refill(const SwDecArgs &a, LongLds &L, const SwLong &S, uint64_t &next, int lane) {
@@ -1274,6 +1314,7 @@ __device__ int long_refill(const SwDecArgs &a, LongLds &L, const SwLong &S, uint
             uint8_t *row = L.stg[k];
             for (uint32_t u = lo; u <= hi; u++) row[u & 255] = 0;
             uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
+            (void)SWC(t, a.nrep, kChkSynJob);  // (t < S.t_hi <= nrep: recorded if not)
             RlcSeq sq(a, h);
             uint32_t word = 0;
             for (int j = 0; j < (int)h.nss; j++) {
@@ -1320,7 +1361,7 @@ __device__ bool log_room(const SwDecArgs &a, LogW &w, uint32_t n, int lane) {
     }
     if (lane == 0) {
         const uint32_t notab[5] = {0, 0, 0, 0, 0};
-        emit(a.log + w.pos, kOpJump, 0, 0, (uint32_t)base, (uint32_t)(base >> 32), notab);
+        emit_at(a, w.pos, kOpJump, 0, 0, (uint32_t)base, (uint32_t)(base >> 32), notab);
     }
     w.pos = base;
     w.end = base + size;
@@ -1368,7 +1409,7 @@ __device__ bool long_compact(const SwDecArgs &a, LongLds &L, uint32_t c, int &na
             if (f) {
                 uint32_t tab[5];
                 set_tab(tab, f);
-                emit(a.log + fw.pos + __popcll(b & lanes_below(lane)), kOpElim, L.act[i], P, 0, 0, tab);
+                emit_at(a, fw.pos + __popcll(b & lanes_below(lane)), kOpElim, L.act[i], P, 0, 0, tab);
             }
             fw.pos += __popcll(b);
             fw.count += __popcll(b);
@@ -1464,7 +1505,7 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
             continue;
         }
         LogW fw{base, base + nfw0, 0};
-        SwOp *bwd = a.log + base + nfw0;
+        const uint64_t bwd0 = base + nfw0;  // the backward log's first entry
         // ---- forward elimination ----
         for (int i = lane; i < kSwRows; i += 64) L.freel[i] = (uint8_t)(kSwRows - 1 - i);
         int nfree = kSwRows, nact = 0, sh = 0, sn = 0;
@@ -1496,8 +1537,8 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                     L.row_hi[slot] = L.stg_hi[sh];
                     L.row_t[slot] = L.stg_t[sh];
                     L.act[nact] = slot;
-                    a.synrow[L.stg_t[sh]] = ~0u;
-                    emit(a.log + fw.pos, kOpLoad, slot, 0, L.stg_t[sh], 0, notab);
+                    if (SWC(L.stg_t[sh], a.nrep, kChkHdr)) a.synrow[L.stg_t[sh]] = ~0u;
+                    emit_at(a, fw.pos, kOpLoad, slot, 0, L.stg_t[sh], 0, notab);
                 }
                 nact++;
                 fw.pos++;
@@ -1515,7 +1556,7 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
             }
             best = wave_min64(best);
             if (best == ~0ull) {
-                if (lane == 0) a.colpiv[x0 + c] = ~0u;
+                if (lane == 0 && SWC(x0 + c, a.nsrc, kChkLost)) a.colpiv[x0 + c] = ~0u;
             } else {
                 const int ppos = (int)(best & 511);
                 const uint32_t P = L.act[ppos];
@@ -1535,7 +1576,7 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                     if (f) {
                         uint32_t tab[5];
                         set_tab(tab, f);
-                        emit(a.log + fw.pos + __popcll(b & lanes_below(lane)), kOpElim, L.act[i], P, 0, 0, tab);
+                        emit_at(a, fw.pos + __popcll(b & lanes_below(lane)), kOpElim, L.act[i], P, 0, 0, tab);
                     }
                     fw.pos += __popcll(b);
                     fw.count += __popcll(b);
@@ -1562,13 +1603,14 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                 SWD_WAVE_SYNC();
                 // the pivot row: coefficients to the pivot area, STORE
                 const uint32_t pv = piv0 + npiv;
-                reinterpret_cast<uint32_t *>(a.pivcoef + (uint64_t)pv * 256)[lane] =
-                    reinterpret_cast<const uint32_t *>(L.rowc[P])[lane];
-                if (lane == 0) {
+                if (SWC(pv, a.piv_cap, kChkPiv))
+                    reinterpret_cast<uint32_t *>(a.pivcoef + (uint64_t)pv * 256)[lane] =
+                        reinterpret_cast<const uint32_t *>(L.rowc[P])[lane];
+                if (lane == 0 && SWC(pv, a.piv_cap, kChkPiv) && SWC(x0 + c, a.nsrc, kChkLost)) {
                     a.pivhi[pv] = hiP;
                     a.pivt[pv] = L.row_t[P];
                     a.colpiv[x0 + c] = pv;
-                    emit(a.log + fw.pos, kOpStore, P, 0, pv, 0, notab);
+                    emit_at(a, fw.pos, kOpStore, P, 0, pv, 0, notab);
                 }
                 fw.pos++;
                 fw.count++;
@@ -1600,7 +1642,9 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
         // syndrome jobs for the pivot rows (the only rows whose data is used), in
         // their repairs' slots; the other slots stay empty
         for (uint32_t q = lane; q < npiv; q += 64) {
+            if (!SWC(piv0 + q, a.piv_cap, kChkPiv)) break;
             const uint32_t t = a.pivt[piv0 + q];
+            if (!SWC(t, a.nrep, kChkSynJob)) continue;
             const uint32_t gq = t;
             const fecgpu_sw_repair h = a.hdr[t];
             CombJob J;
@@ -1620,7 +1664,7 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
         uint32_t nv = 0, nb = 0, ndet = 0;
         for (int c = (int)e - 1; c >= 0; c--) {
             const uint32_t cs = (uint32_t)c & 255;
-            const uint32_t pv = a.colpiv[x0 + c];
+            const uint32_t pv = SWC(x0 + c, a.nsrc, kChkLost) ? a.colpiv[x0 + c] : ~0u;
             if (pv == ~0u) {
                 if (nv == (uint32_t)kSwRows) {
                     // reduce to a basis of the projection on [c + 1, c + B)
@@ -1662,11 +1706,12 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                 SWD_WAVE_SYNC();
                 for (int cc2 = lane; cc2 < 256; cc2 += 64) VT[cc2][nv] = (uint8_t)(cc2 == (int)cs);
                 nv++;
-                if (lane == 0) emit(bwd + nb, kOpXFree, cs, 0, 0, 0, notab);
+                if (lane == 0) emit_at(a, bwd0 + nb, kOpXFree, cs, 0, 0, 0, notab);
                 nb++;
                 SWD_WAVE_SYNC();
                 continue;
             }
+            if (!SWC(pv, a.piv_cap, kChkPiv)) break;
             reinterpret_cast<uint32_t *>(L.prow)[lane] = reinterpret_cast<const uint32_t *>(a.pivcoef + (uint64_t)pv * 256)[lane];
             const uint32_t hi = a.pivhi[pv];
             SWD_WAVE_SYNC();
@@ -1691,11 +1736,12 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                 reinterpret_cast<uint32_t *>(VT[cs])[lane] = acc;
                 det = __ballot(acc != 0) ? 0u : 1u;
             }
+            const uint32_t src_i = a.lost[x0 + c];  // (x0 + c < nsrc: checked with colpiv above)
             // back substitution entries: x_c = ip * y_P + sum (ip * a_Pj) x_j
             {
                 uint32_t tip[5];
                 set_tab(tip, ip);
-                if (lane == 0) emit(bwd + nb, kOpXBegin, cs, 0, pv, 0, tip);
+                if (lane == 0) emit_at(a, bwd0 + nb, kOpXBegin, cs, 0, pv, 0, tip);
                 nb++;
                 const uint32_t w = hi >= (uint32_t)c ? hi - (uint32_t)c : 0u;  // a pivot row ends at or after its column
                 for (uint32_t j0 = 0; j0 < w; j0 += 64) {
@@ -1705,16 +1751,15 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
                     if (cj) {
                         uint32_t tab[5];
                         set_tab(tab, gmul(L.g, cj, ip));
-                        emit(bwd + nb + __popcll(b & lanes_below(lane)), kOpXTerm, j & 255, 0, 0, 0, tab);
+                        emit_at(a, bwd0 + nb + __popcll(b & lanes_below(lane)), kOpXTerm, j & 255, 0, 0, 0, tab);
                     }
                     nb += __popcll(b);
                 }
-                const uint32_t src_i = a.lost[x0 + c];
-                if (lane == 0) emit(bwd + nb, kOpXEnd, 0, cs, det ? src_i : ~0u, 0, notab);
+                if (lane == 0) emit_at(a, bwd0 + nb, kOpXEnd, 0, cs, det ? src_i : ~0u, 0, notab);
                 nb++;
             }
             if (det) {
-                if (lane == 0) a.stat[a.lost[x0 + c]] = FECGPU_STATUS_OK;
+                if (lane == 0 && SWC(src_i, a.nsrc, kChkSrcRow)) a.stat[src_i] = FECGPU_STATUS_OK;
                 ndet++;
             }
             SWD_WAVE_SYNC();
@@ -1750,6 +1795,7 @@ __global__ __launch_bounds__(64) void sw_dec_replay_kernel(SwDecArgs a) {
         const uint64_t boff = (uint64_t)dw * 4;
         uint64_t at = S.fwd;
         for (uint32_t i = 0; i < S.nfwd; i++) {
+            if (!SWC(at, a.log_cap, kChkLog)) break;
             const SwOp o = a.log[at++];
             const uint32_t kind = o.op & 0xFFu, sa = (o.op >> 8) & 0xFFu, sb = (o.op >> 16) & 0xFFu;
             if (kind == kOpJump) {
@@ -1758,28 +1804,33 @@ __global__ __launch_bounds__(64) void sw_dec_replay_kernel(SwDecArgs a) {
                 const uint32_t t[5] = {o.tab[0], o.tab[1], o.tab[2], o.tab[3], o.tab[4]};
                 slots[sa][lane] ^= tmul(slots[sb][lane], t);
             } else if (kind == kOpLoad) {
-                const uint32_t g = a.synrow[o.aux];
+                const uint32_t g = SWC(o.aux, a.nrep, kChkHdr) ? a.synrow[o.aux] : ~0u;
                 uint32_t v = 0;
-                if (g != ~0u && live) v = *reinterpret_cast<const uint32_t *>(a.synd + (uint64_t)g * a.stride + boff);
+                if (g != ~0u && live && SWC(g, a.nrep, kChkSynRow) && SWC(boff + 3, a.stride, kChkColumn))
+                    v = *reinterpret_cast<const uint32_t *>(a.synd + (uint64_t)g * a.stride + boff);
                 slots[sa][lane] = v;
             } else if (kind == kOpStore) {
-                if (live) *reinterpret_cast<uint32_t *>(a.pivdata + (uint64_t)o.aux * a.stride + boff) = slots[sa][lane];
+                if (live && SWC(o.aux, a.piv_cap, kChkPiv) && SWC(boff + 3, a.stride, kChkColumn))
+                    *reinterpret_cast<uint32_t *>(a.pivdata + (uint64_t)o.aux * a.stride + boff) = slots[sa][lane];
             }
         }
         const SwOp *op = a.log + S.bwd;
         uint32_t x = 0;
         for (uint32_t i = 0; i < S.nbwd; i++) {
+            if (!SWC(S.bwd + i, a.log_cap, kChkLog)) break;
             const SwOp o = op[i];
             const uint32_t kind = o.op & 0xFFu, sa = (o.op >> 8) & 0xFFu, sb = (o.op >> 16) & 0xFFu;
             const uint32_t t[5] = {o.tab[0], o.tab[1], o.tab[2], o.tab[3], o.tab[4]};
             if (kind == kOpXTerm) {
                 x ^= tmul(slots[sa][lane], t);
             } else if (kind == kOpXBegin) {
-                x = live ? tmul(*reinterpret_cast<const uint32_t *>(a.pivdata + (uint64_t)o.aux * a.stride + boff), t)
-                         : 0u;
+                x = live && SWC(o.aux, a.piv_cap, kChkPiv)
+                        ? tmul(*reinterpret_cast<const uint32_t *>(a.pivdata + (uint64_t)o.aux * a.stride + boff), t)
+                        : 0u;
             } else if (kind == kOpXEnd) {
                 slots[sb][lane] = x;
-                if (o.aux != ~0u && live) *reinterpret_cast<uint32_t *>(a.src + (uint64_t)o.aux * a.stride + boff) = x;
+                if (o.aux != ~0u && live && SWC(o.aux, a.nsrc, kChkSrcRow) && SWC(boff + 3, a.stride, kChkColumn))
+                    *reinterpret_cast<uint32_t *>(a.src + (uint64_t)o.aux * a.stride + boff) = x;
             } else if (kind == kOpXFree) {
                 slots[sa][lane] = 0;
             }

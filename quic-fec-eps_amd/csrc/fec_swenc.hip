@@ -239,6 +239,8 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
     const uint32_t hi = rfl(pl.phi[p]);
     uint32_t s = rfl(pl.plo[p]);
     if (s >= hi) return;  // an empty pass (hi >= 1 below)
+    // FECGPU_CHECK builds: the pass's rows lie in the sources, its column in a row
+    if (!CHK_IDX(a.chk, rfl64(pl.lo) + hi - 1, a.nsrc, 1) || !CHK_IDX(a.chk, loff + 4 * C - 1, stride, 2)) return;
     const uint8_t *base = a.src + rfl64(pl.lo) * stride;
     // rows s0 .. s0 + U - 1, clamped to hi - 1 (valid rows only).  Every batch
     // issues its loads unconditionally: with a load under a branch the
@@ -309,7 +311,7 @@ __device__ __forceinline__ void sws_pass(const SwStreamArgs &a, const SwsPlan &p
         for (int m = 0; m < A; m++) {
             if (e[m] == sn) {
                 const uint32_t o = dense ? v[m] : rfl(pl.out[v[m]]);
-                if (live) stc<C>(a.rep + (j0 + o) * stride + loff, acc[m]);
+                if (live && CHK_IDX(a.chk, j0 + o, a.nrep, 3)) stc<C>(a.rep + (j0 + o) * stride + loff, acc[m]);
 #pragma unroll
                 for (int d = 0; d < C; d++) acc[m][d] = 0;
                 v[m] += stepv;
@@ -369,7 +371,7 @@ __global__ __launch_bounds__(512) void sw_stream_kernel(SwStreamArgs a) {
             TC[i] = ct.c;
         }
         for (int k = 0; k < (int)rfl((uint32_t)pl.nempty); k++)
-            for (uint32_t cu = tid; cu < a.ncu; cu += blockDim.x) {
+            for (uint32_t cu = tid; cu < a.ncu && CHK_IDX(a.chk, j0 + pl.empty[k], a.nrep, 3); cu += blockDim.x) {
                 const uint32_t z[C] = {};
                 stc<C>(a.rep + (j0 + pl.empty[k]) * a.stride + cu * 4u * C, z);
             }

@@ -52,6 +52,7 @@ struct WideArgs {
     // rows in syn, [nwin][r][stride])
     CombJob *jobs1;
     uint64_t *outs1;
+    ChkRec *chk;  // FECGPU_CHECK builds: the fault record (release: null)
 };
 
 __global__ __launch_bounds__(kBlock) void wide_enc_jobs_kernel(WideArgs a) {
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
         }
         if (cu < e && ci < r) C2[cu * r + ci] = (uint8_t)v;
         uint8_t *wb = a.win + w * a.wpitch;
-        for (int u2 = 0; u2 < e; u2++) {
+        for (int u2 = 0; u2 < e && CHK_IDX(a.chk, s_m[wave][u2], k, 1); u2++) {
             uint4 *row = reinterpret_cast<uint4 *>(wb + (uint64_t)s_m[wave][u2] * a.stride);
             for (uint32_t c16 = lane; c16 < a.stride / 16u; c16 += 64) row[c16] = make_uint4(0, 0, 0, 0);
         }
@@ -199,8 +200,9 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
 hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
                        uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
                        uint64_t *outs, uint8_t *coef, hipStream_t s, CombJob *jobs1, uint64_t *outs1,
-                       uint8_t *syn, const uint32_t *masks_P, const uint32_t *masks_PI) {
+                       uint8_t *syn, const uint32_t *masks_P, const uint32_t *masks_PI, ChkRec *chk) {
     WideArgs a{};
+    a.chk = chk;
     a.win = win;
     a.present = present;
     a.status = status;
@@ -253,6 +255,10 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
         c1.nout_max = r;
         c1.job_lds = comb_job_lds(c1.nin_max, kMaxR);
         c1.shared_coef = 1;
+        c1.chk.lo[0] = reinterpret_cast<uint64_t>(win);  // FECGPU_CHECK builds: windows in, syndromes out
+        c1.chk.n[0] = nwin * a.wpitch;
+        c1.chk.lo[1] = reinterpret_cast<uint64_t>(syn);
+        c1.chk.n[1] = nwin * (uint64_t)r * stride;
         const uint32_t cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxWpb, nwin / 1024));
         const uint32_t room =
             std::min<uint32_t>(kBudget - comb_shared_lds(k + r, kMaxR), cap * comb_job_small_lds(kMaxR));
@@ -273,6 +279,10 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
         c2.nin_max = r;
         c2.nout_max = kMaxR;
         c2.job_lds = comb_job_lds(r, kMaxR);
+        c2.chk.lo[0] = reinterpret_cast<uint64_t>(syn);  // FECGPU_CHECK builds: syndromes in, windows out
+        c2.chk.n[0] = nwin * (uint64_t)r * stride;
+        c2.chk.lo[1] = reinterpret_cast<uint64_t>(win);
+        c2.chk.n[1] = nwin * a.wpitch;
         c2.wpb = std::max(1, std::min(kMaxWpb, choose_wpb_for(ncol, c2.job_lds, kWideS2Budget)));
         return launch_comb(c2, kMaxR, s);
     }
@@ -293,6 +303,8 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
     // workgroup, so the jobs per workgroup follow lane use alone (1200-B rows
     // are 75 of a workgroup's 256 lanes)
     c.shared_coef = 1;
+    c.chk.lo[0] = reinterpret_cast<uint64_t>(win);  // FECGPU_CHECK builds: the windows, in and out
+    c.chk.n[0] = nwin * a.wpitch;
     // at most nwin / 1024 jobs each, so the grid keeps >= 4 workgroups per CU
     const uint32_t cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxWpb, nwin / 1024));
     const uint32_t room = std::min<uint32_t>(kBudget - comb_shared_lds(k, kMaxR), cap * comb_job_small_lds(kMaxR));

@@ -327,3 +327,132 @@ def test_checked_encoder_failed_launch_recovers(chk):
         ref = N.encode("gf", 4, 2, np.frombuffer(b"".join(pk[4 * w:4 * w + 4]), np.uint8).reshape(4, 256))
         assert [enc.repair(w, i) for i in range(2)] == [ref[i].tobytes() for i in range(2)], w
     enc.close()
+
+
+# ---- sliding-window, wide and bit-sliced decode kernels ----
+# The checked build also bounds the sliding-window kernels (fec_swdec.hip,
+# fec_swenc.hip: every row, job slot, look-back record, start-list entry and
+# operation-log entry an index addresses, against its allocation), the combine
+# launches (their rows against the call's arrays), the wide plan and the
+# bit-sliced decode.  Each case below runs equal to the oracle AND clean.
+
+def _sw():
+    import test_gpu_sw as T
+    return T
+
+
+def test_checked_sw_decode_config7_scale(chk):
+    """Config 7's stream shape at full length (524,288 sources: the plan's 256
+    look-back chunks), short symbols; encode and decode on the checked build."""
+    T = _sw()
+    m, ctx = chk
+    nsrc, L, k, W = 524288, 32, 8, 32
+    stride = O.round_up(L, 16)
+    src = T.stream(nsrc, L, stride, 7)
+    hdr = T.hdr_array(T.N.sw_schedule(nsrc, k, W, key0=1, dt=15))
+    rep = T.gpu_encode(ctx, src, hdr, L, max_window=W)
+    assert np.array_equal(rep[:, :L], O.sw_encode(src, hdr, L)[:, :L])
+    rng = np.random.default_rng(7)
+    sp = (rng.random(nsrc) >= 0.02).astype(np.uint8)
+    rp = (rng.random(len(hdr)) >= 0.02).astype(np.uint8)
+    T.check_vs_oracle(ctx, src, sp, rep, rp, hdr, L)
+
+
+@pytest.mark.parametrize("loss", [0.10, 0.30])
+def test_checked_sw_two_repairs_per_step_W255(chk, loss):
+    """W 255, two repairs per step: long systems, row-slot compaction, chained logs."""
+    T = _sw()
+    m, ctx = chk
+    nsrc, L, W = 2500, 24, 255
+    stride = O.round_up(L, 16)
+    src = T.stream(nsrc, L, stride, 255 + int(loss * 100))
+    hdr = T.two_per_step(nsrc, W, key0=int(loss * 1000))
+    rep = O.sw_encode(src, hdr, L)
+    rng = np.random.default_rng(int(loss * 1000) + 1)
+    sp = (rng.random(nsrc) >= loss).astype(np.uint8)
+    rp = (rng.random(len(hdr)) >= loss).astype(np.uint8)
+    assert T.max_system(sp, rp, hdr) > 100
+    T.check_vs_oracle(ctx, src, sp, rep, rp, hdr, L)
+
+
+def test_checked_sw_compaction_with_small_log(chk):
+    """sw_log_entries 16: every long system overflows its log chunk and the
+    synchronous retries grow it; equal to the oracle, no access outside the log."""
+    T = _sw()
+    m, _ = chk
+    c = m.Context()
+    try:
+        c.set_tuning("sw_log_entries", 16)
+        nsrc, L, W = 1500, 16, 255
+        stride = O.round_up(L, 16)
+        src = T.stream(nsrc, L, stride, 77)
+        hdr = T.two_per_step(nsrc, W, key0=77)
+        rep = O.sw_encode(src, hdr, L)
+        rng = np.random.default_rng(77)
+        sp = (rng.random(nsrc) >= 0.2).astype(np.uint8)
+        rp = (rng.random(len(hdr)) >= 0.2).astype(np.uint8)
+        T.check_vs_oracle(c, src, sp, rep, rp, hdr, L)
+    finally:
+        c.close()
+
+
+def test_checked_sw_checker_fires_when_the_range_is_short(chk):
+    """check_shrink=16 hides the last 16 bytes of each of a decode's arrays from
+    the combine launches' checker: a syndrome job reading the last source row
+    (a source lost near the end) must be reported."""
+    T = _sw()
+    m, ctx = chk
+    nsrc, L, k, W = 400, 64, 4, 16
+    stride = O.round_up(L, 16)
+    src = T.stream(nsrc, L, stride, 3)
+    hdr = T.hdr_array(T.N.sw_schedule(nsrc, k, W, key0=3, dt=15))
+    rep = O.sw_encode(src, hdr, L)
+    sp = np.ones(nsrc, np.uint8)
+    sp[nsrc - 2] = 0
+    rp = np.ones(len(hdr), np.uint8)
+    ctx.set_tuning("check_shrink", 16)
+    try:
+        with pytest.raises(m.FecError, match="bounds check"):
+            T.gpu_decode(ctx, src, sp, rep, rp, hdr, L)
+    finally:
+        ctx.set_tuning("check_shrink", 0)
+    T.check_vs_oracle(ctx, src, sp, rep, rp, hdr, L)  # and clean again
+
+
+@pytest.mark.parametrize("k,r,matrix,L", [(248, 8, "cauchy", 300), (120, 8, "rlc", 1200), (150, 5, "cauchy", 64)])
+def test_checked_wide_encode_decode(chk, k, r, matrix, L):
+    """k + r up to 256 (the bit-sliced wide decode with buffer loads, the plan)."""
+    import test_gpu_wide as TW
+    m, ctx = chk
+    rng = np.random.default_rng(k + r)
+    bits = TW._erasures(10, k, r, rng)
+    TW._run(ctx, k, r, matrix, L, 10, bits, m=m)
+
+
+def test_checked_wide_two_stage(chk):
+    """The wide two-stage combine decode (bitslice off) on the checked build."""
+    import test_gpu_wide as TW
+    m, _ = chk
+    c = m.Context()
+    try:
+        c.set_tuning("bitslice", 0)
+        bits = TW._erasures(10, 200, 6, np.random.default_rng(5))
+        TW._run(c, 200, 6, "cauchy", 500, 10, bits, m=m)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("matrix", ["cauchy", "vandermonde"])
+def test_checked_bsdec_routed(chk, matrix):
+    """Narrow windows with many erasures routed to the bit-sliced decode, mixed lengths."""
+    import test_gpu_bsdec as TB
+    m, _ = chk
+    c = m.Context()
+    try:
+        c.set_tuning("bsd_min_e", 5)
+        rng = np.random.default_rng(11)
+        bits = TB._erasures(40, 32, 8, rng, lo=4)
+        sl = np.where(rng.random(40) < 0.5, 1202, 9002).astype(np.uint32)
+        TB._run(c, 32, 8, matrix, 9002, 40, bits, sym_len=sl, m=m)
+    finally:
+        c.close()

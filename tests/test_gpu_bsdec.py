@@ -38,7 +38,7 @@ def _erasures(nwin, k, r, rng, lo=0):
     return bits
 
 
-def _run(c, k, r, matrix, L, nwin, bits, sym_len=None, seed=0):
+def _run(c, k, r, matrix, L, nwin, bits, sym_len=None, seed=0, m=fecgpu):
     """Encode on the GPU, poison the missing symbols, decode; check against the
     oracle and the originals.  Returns (decoded windows, statuses)."""
     n = k + r
@@ -46,7 +46,7 @@ def _run(c, k, r, matrix, L, nwin, bits, sym_len=None, seed=0):
     rng = np.random.default_rng(seed + 7 * k + r)
     wins = np.zeros((nwin, n, stride), np.uint8)
     wins[:, :k, :L] = rng.integers(0, 256, (nwin, k, L), dtype=np.uint8)
-    code = fecgpu.Code("gf256", k, r, matrix=matrix)
+    code = m.Code("gf256", k, r, matrix=matrix)
     d = torch.from_numpy(wins.copy()).cuda()
     sl = None if sym_len is None else torch.from_numpy(sym_len).cuda()
     kw = dict(nwin=nwin, stride=stride, sym_len_all=L if sym_len is None else 0, sym_len=sl)

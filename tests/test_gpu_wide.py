@@ -38,13 +38,13 @@ def _masks(pres_bits: np.ndarray) -> np.ndarray:
     return out
 
 
-def _run(ctx, k, r, matrix, L, nwin, pres_bits, key=5, dt=15, sym_len=None, seed=0):
+def _run(ctx, k, r, matrix, L, nwin, pres_bits, key=5, dt=15, sym_len=None, seed=0, m=fecgpu):
     n = k + r
     stride = (L + 15) // 16 * 16
     rng = np.random.default_rng(seed + k * 7 + r)
     wins = np.zeros((nwin, n, stride), np.uint8)
     wins[:, :k, :L] = rng.integers(0, 256, (nwin, k, L), dtype=np.uint8)
-    code = fecgpu.Code("gf256", k, r, matrix=matrix, rlc_key=key, rlc_dt=dt)
+    code = m.Code("gf256", k, r, matrix=matrix, rlc_key=key, rlc_dt=dt)
     d = torch.from_numpy(wins.copy()).cuda()
     sl = None if sym_len is None else torch.from_numpy(sym_len).cuda()
     ctx.encode_batch(code, d, nwin=nwin, stride=stride, sym_len_all=L if sym_len is None else 0, sym_len=sl)
