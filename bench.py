@@ -202,6 +202,47 @@ def cpu_baseline(cfg, seconds: float, threads: int) -> dict:
                       f"the sample repeated {reps}x at most), {dt:.1f} s on {threads} host threads"}
 
 
+def cpu_baseline_wide(cfg, seconds: float, threads: int = 0) -> dict:
+    """Codes with k + r > 64 (--k / --r): the CPU codec (oracle/fec_cpu_simd.c,
+    multi-word present masks; outputs equal to the numpy restatement,
+    tests/test_oracle_simd.py) on a bounded sample of the same shape: windows
+    of k sources of L random bytes, exactly r sources erased per window."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(_ROOT, "oracle"))
+    import oracle as O  # test/baseline infrastructure only
+
+    O.lib()
+    if threads <= 0:
+        threads = host_share()
+    k, r, L, n = cfg.k, cfg.r, cfg.L, cfg.k + cfg.r
+    stride = O.round_up(L, 16)
+    nwin = max(threads, int((1 << 30) // (n * stride)))  # ~1 GiB sample
+    rng = np.random.default_rng(workloads.SEED)
+    wins = np.zeros((nwin, n, stride), np.uint8)
+    wins[:, :k, :L] = rng.integers(0, 256, (nwin, k, L), dtype=np.uint8)
+    S = np.full(nwin, L, np.uint32)
+    nw = (n + 63) // 64
+    pres = np.zeros((nwin, nw), np.uint64)
+    for q in range(nw):
+        lo, hi = 64 * q, min(n, 64 * q + 64)
+        pres[:, q] = np.uint64((1 << (hi - lo)) - 1) if hi - lo < 64 else np.uint64(2**64 - 1)
+    for w in range(nwin):
+        for j in rng.choice(k, r, replace=False):
+            pres[w, j // 64] &= ~np.uint64(1 << (j % 64))
+    tot, reps = 0.0, 0
+    while tot < seconds and reps < 1000:
+        t0 = time.perf_counter()
+        O.encode_batch_simd(O.GF256, k, r, S, wins, threads)
+        O.decode_batch_simd(O.GF256, k, r, S, wins, pres, threads)
+        tot += time.perf_counter() - t0
+        reps += 1
+    return {"value": round(reps * nwin * k * L / tot / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "codec": f"oracle/fec_cpu_simd.c ({O.SIMD_NAMES[O.simd_level()]}; k + r up to 256, multi-word masks; "
+                     f"equal outputs to np_oracle: tests/test_oracle_simd.py)",
+            "sample": f"{reps} passes over {nwin} windows of k {k} r {r} x {L} B (exactly r sources erased), "
+                      f"{tot:.1f} s on {threads} host threads"}
+
+
 def cpu_baseline_sw(cfg, seconds: float, threads: int = 0, nsrc: int = 0) -> dict:
     """Config 7: the sliding-window CPU codec (oracle/fec_cpu_simd.c
     orc_sw_encode_simd / orc_sw_decode_simd: AVX2 / GFNI products, threads over
@@ -463,7 +504,7 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
     if args.cpu_seconds > 0 and world == 1 and not cfg.host:  # cfg5's codec and shape are cfg2's
         log(f"{cfg.name}: cpu baseline")
         cpu = (cpu_baseline_sw(cfg, args.cpu_seconds, args.cpu_threads) if cfg.scheme == "sw" else
-               None if wide else  # the CPU codec's block code is k + r <= 64
+               cpu_baseline_wide(cfg, args.cpu_seconds, args.cpu_threads) if wide else
                cpu_baseline(cfg, args.cpu_seconds, args.cpu_threads))
     peak, bound = (PCIE_DIR_PEAK_GBS, f"pcie-{bound_dir}") if cfg.host else (HBM_PEAK_GBS, "hbm")
     return {

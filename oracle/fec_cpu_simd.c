@@ -20,6 +20,7 @@
 #include "fec_oracle.h"
 
 static int g_level = -1;  /* -1: detect */
+#define ORC_SIMD_MAX_N 256  /* k + r of the block codes (Cauchy rows exist up to 256) */
 
 int orc_simd_detect(void) {
     __builtin_cpu_init();
@@ -216,7 +217,7 @@ static void encode_window(int level, int scheme, int k, int r, const coef_t *tab
         }
         return;
     }
-    const uint8_t *in[64];
+    const uint8_t *in[ORC_SIMD_MAX_N];
     uint8_t *out[8];
     for (int j = 0; j < k; j++) in[j] = win + (size_t)j * stride;
     for (int i = 0; i < r; i++) out[i] = win + (size_t)(k + i) * stride;
@@ -247,8 +248,42 @@ static int inv_small(int e, uint8_t *A, uint8_t *Ai) {
     return 1;
 }
 
+/* orc_select_rows over multi-word present masks (bit i in word i / 64; codes
+ * with k + r up to 256): the missing sources and e present repairs whose rows
+ * restricted to them are independent, greedily in repair order */
+static int pbit(const uint64_t *pw, int i) { return (int)((pw[i >> 6] >> (i & 63)) & 1u); }
+static int select_rows_w(int k, int r, const uint8_t *C, const uint64_t *pw, int *miss, int *sel) {
+    int e = 0, n = 0;
+    for (int j = 0; j < k; j++)
+        if (!pbit(pw, j)) miss[e++] = j;
+    if (e == 0) return 0;
+    if (e > 8) return -1;
+    uint8_t basis[8][8];
+    int pivc[8];
+    for (int i = 0; i < r && n < e; i++) {
+        if (!pbit(pw, k + i)) continue;
+        uint8_t v[8];
+        for (int u = 0; u < e; u++) v[u] = C[i * k + miss[u]];
+        for (int b = 0; b < n; b++) {
+            const uint8_t f = v[pivc[b]];
+            if (!f) continue;
+            for (int u = 0; u < e; u++) v[u] ^= gmul(f, basis[b][u]);
+        }
+        int pc = -1;
+        for (int u = 0; u < e; u++)
+            if (v[u]) { pc = u; break; }
+        if (pc < 0) continue;
+        const uint8_t iv = ginv(v[pc]);
+        for (int u = 0; u < e; u++) basis[n][u] = gmul(v[u], iv);
+        pivc[n] = pc;
+        sel[n++] = i;
+    }
+    return n == e ? e : -1;
+}
+
 static int decode_window(int level, int scheme, int k, int r, const uint8_t *C, uint32_t S,
-                         uint32_t stride, uint64_t present, uint8_t *win) {
+                         uint32_t stride, const uint64_t *pw, uint8_t *win) {
+    const uint64_t present = pw[0];  /* XOR codes: k + r <= 64 */
     if (scheme == ORC_XOR) {
         int status = ORC_OK;
         for (int g = 0; g < r; g++) {
@@ -264,8 +299,8 @@ static int decode_window(int level, int scheme, int k, int r, const uint8_t *C, 
         }
         return status;
     }
-    int miss[64], sel[64];
-    const int e = orc_select_rows(k, r, C, present, miss, sel);
+    int miss[ORC_SIMD_MAX_N], sel[8];
+    const int e = select_rows_w(k, r, C, pw, miss, sel);
     if (e == 0) return ORC_OK;
     if (e < 0 || e > 8) return ORC_UNRECOVERABLE;
     /* A[t][u] = C[sel_t][miss_u]; recovered_u = sum_t Ainv[u][t] (R_sel_t + sum_j C[sel_t][j] S_j)
@@ -274,12 +309,12 @@ static int decode_window(int level, int scheme, int k, int r, const uint8_t *C, 
     for (int t = 0; t < e; t++)
         for (int u = 0; u < e; u++) A[t * e + u] = C[sel[t] * k + miss[u]];
     if (!inv_small(e, A, Ai)) return ORC_UNRECOVERABLE;
-    const uint8_t *in[64];
+    const uint8_t *in[ORC_SIMD_MAX_N];
     uint8_t *out[8];
-    coef_t tab[64 * 8];
+    coef_t tab[ORC_SIMD_MAX_N * 8];
     int q = 0;
     for (int j = 0; j < k; j++) {
-        if (!((present >> j) & 1)) continue;
+        if (!pbit(pw, j)) continue;
         for (int u = 0; u < e; u++) {
             uint8_t c = 0;
             for (int t = 0; t < e; t++) c ^= gmul(Ai[u * e + t], C[sel[t] * k + j]);
@@ -298,11 +333,11 @@ static int decode_window(int level, int scheme, int k, int r, const uint8_t *C, 
 
 /* -------------------------------------------------------------- batch --- */
 typedef struct {
-    int op, level, scheme, k, r;
+    int op, level, scheme, k, r, nw;
     const uint32_t *S;
     uint32_t stride;
     uint64_t lo, hi;
-    const uint64_t *present;
+    const uint64_t *present;  /* nw words per window */
     uint8_t *status, *wins;
     const coef_t *tab;
     const uint8_t *C;
@@ -317,15 +352,15 @@ static void *run_sjob(void *p) {
             encode_window(j->level, j->scheme, j->k, j->r, j->tab, j->S[w], j->stride, win);
         else
             j->status[w] = (uint8_t)decode_window(j->level, j->scheme, j->k, j->r, j->C, j->S[w],
-                                                  j->stride, j->present[w], win);
+                                                  j->stride, j->present + w * (uint64_t)j->nw, win);
     }
     return NULL;
 }
 
 static void run_sbatch(int op, int scheme, int k, int r, const uint32_t *S, uint32_t stride,
-                       uint64_t nwin, const uint64_t *present, uint8_t *status, uint8_t *wins,
+                       uint64_t nwin, int nw, const uint64_t *present, uint8_t *status, uint8_t *wins,
                        int nthreads) {
-    uint8_t C[64 * 64];
+    uint8_t *C = (uint8_t *)calloc((size_t)k * r + 1, 1);
     coef_t *tab = NULL;
     tables_init();
     if (scheme != ORC_XOR) {
@@ -339,7 +374,7 @@ static void run_sbatch(int op, int scheme, int k, int r, const uint32_t *S, uint
     pthread_t th[256];
     sjob_t jobs[256];
     for (int t = 0; t < nthreads; t++) {
-        sjob_t x = {op, orc_simd_level(), scheme, k, r, S, stride,
+        sjob_t x = {op, orc_simd_level(), scheme, k, r, nw, S, stride,
                     nwin * (uint64_t)t / (uint64_t)nthreads, nwin * (uint64_t)(t + 1) / (uint64_t)nthreads,
                     present, status, wins, tab, C};
         jobs[t] = x;
@@ -349,17 +384,27 @@ static void run_sbatch(int op, int scheme, int k, int r, const uint32_t *S, uint
     if (nthreads > 1)
         for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
     free(tab);
+    free(C);
 }
 
+/* k + r <= ORC_SIMD_MAX_N (256) for the GF schemes (the systematic Vandermonde
+ * rows: k <= 64), 64 for XOR */
 void orc_encode_batch_simd(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
                            uint64_t nwin, uint8_t *wins, int nthreads) {
-    run_sbatch(0, scheme, k, r, S, stride, nwin, NULL, NULL, wins, nthreads);
+    run_sbatch(0, scheme, k, r, S, stride, nwin, 1, NULL, NULL, wins, nthreads);
 }
 
 void orc_decode_batch_simd(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
                            uint64_t nwin, const uint64_t *present, uint8_t *status, uint8_t *wins,
                            int nthreads) {
-    run_sbatch(1, scheme, k, r, S, stride, nwin, present, status, wins, nthreads);
+    run_sbatch(1, scheme, k, r, S, stride, nwin, 1, present, status, wins, nthreads);
+}
+
+/* present: nw = ceil((k + r) / 64) words per window (bit i in word i / 64) */
+void orc_decode_batch_simd_w(int scheme, int k, int r, const uint32_t *S, uint32_t stride,
+                             uint64_t nwin, int nw, const uint64_t *present, uint8_t *status, uint8_t *wins,
+                             int nthreads) {
+    run_sbatch(1, scheme, k, r, S, stride, nwin, nw, present, status, wins, nthreads);
 }
 
 /* ------------------------------------------ sliding-window RLC (cfg7) --- */

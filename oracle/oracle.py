@@ -76,6 +76,7 @@ def lib():
             "orc_simd_set_level": (None, [i32]),
             "orc_encode_batch_simd": (None, [i32, i32, i32, vp, u32, u64, vp, i32]),
             "orc_decode_batch_simd": (None, [i32, i32, i32, vp, u32, u64, vp, vp, vp, i32]),
+            "orc_decode_batch_simd_w": (None, [i32, i32, i32, vp, u32, u64, i32, vp, vp, vp, i32]),
             "orc_sw_encode_simd": (None, [vp, u64, u32, u32, vp, u64, vp, i32]),
             "orc_sw_decode_simd": (ctypes.c_int64, [vp, vp, u64, vp, vp, vp, u64, u32, u32, vp, i32]),
         }
@@ -280,12 +281,17 @@ def encode_batch_simd(scheme: int, k: int, r: int, S: np.ndarray, wins: np.ndarr
 
 def decode_batch_simd(scheme: int, k: int, r: int, S: np.ndarray, wins: np.ndarray,
                       present: np.ndarray, nthreads: int = 1) -> np.ndarray:
+    """present: [nwin] u64, or [nwin, ceil((k + r) / 64)] u64 words (k + r > 64)."""
     nwin, _, stride = wins.shape
     S = np.ascontiguousarray(S, np.uint32)
     present = np.ascontiguousarray(present, np.uint64)
     status = np.zeros(nwin, np.uint8)
-    lib().orc_decode_batch_simd(scheme, k, r, _p(S), stride, nwin, _p(present), _p(status),
-                                _p(wins), nthreads)
+    if present.ndim == 2:
+        lib().orc_decode_batch_simd_w(scheme, k, r, _p(S), stride, nwin, present.shape[1], _p(present),
+                                      _p(status), _p(wins), nthreads)
+    else:
+        lib().orc_decode_batch_simd(scheme, k, r, _p(S), stride, nwin, _p(present), _p(status),
+                                    _p(wins), nthreads)
     return status
 
 

@@ -5,6 +5,8 @@ of config 4's 44 GiB batch under different allocation histories, in one process.
   A  cfg4 allocated first in a fresh process
   B  after cfg3's batch (6.3 GB) was allocated, used and freed (the bench order)
   C  the same cfg4 batch re-used after B, data re-synthesised
+  D  cfg3 allocated in the memory cfg4's batch freed
+  E  cfg3 first in a fresh process
 Prints one JSON line per phase: per-call HIP-event ms (min / median / max) and
 the batch's base address (2 MiB / 1 GiB alignment)."""
 from __future__ import annotations
@@ -89,6 +91,19 @@ def main():
         elif ph == "C":
             b4.synthesize(ctx, 0)
             phase("C-cfg4-again", ctx, b4)
+        elif ph == "D":  # cfg3 in the memory cfg4 freed
+            del b4
+            b4 = None
+            torch.cuda.empty_cache()
+            b3 = make(3, ctx, dev)
+            phase("D-cfg3-after-cfg4", ctx, b3, n=10)
+            del b3
+            torch.cuda.empty_cache()
+        elif ph == "E":  # cfg3 first in a fresh process
+            b3 = make(3, ctx, dev)
+            phase("E-cfg3-first", ctx, b3, n=10)
+            del b3
+            torch.cuda.empty_cache()
     ctx.close()
 
 

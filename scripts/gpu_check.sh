@@ -177,6 +177,7 @@ for s in "$@"; do
             c=${s#clk}; pmc clk$c $c GRBM_GUI_ACTIVE GRBM_COUNT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU \
                 TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum ;;
         cfg4probe) step cfg4probe 600 python scripts/cfg4_probe.py ABC ;;
+        cfg4order) step cfg4order_ad 600 python scripts/cfg4_probe.py AD && step cfg4order_eb 600 python scripts/cfg4_probe.py EB ;;
         listctr) step listctr 120 rocprofv3 -L ;;
         benchdef) step benchdef 900 python bench.py ;;  # the driver's default command
         probe) step probe 300 ./scripts/stream_probe ;;

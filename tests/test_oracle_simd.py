@@ -87,3 +87,47 @@ def test_sw_simd_codec_matches_oracle(O, nsrc, k, W, dt, L, loss):
             assert np.array_equal(st, ost) and n == on, (level, nth)
             assert np.array_equal(d[:, :L], od[:, :L]), (level, nth)
     O.simd_set_level(-1)
+
+
+@pytest.mark.parametrize("k,r,scheme,L", [(120, 8, "gf", 300), (248, 8, "gf", 64), (100, 5, "rlc", 97)])
+def test_simd_codec_wide_codes_match_numpy_oracle(O, k, r, scheme, L):
+    """k + r > 64 (the wide bench lines' CPU baseline): repairs equal the numpy
+    restatement's (np_oracle.encode), and the decode over multi-word present masks
+    recovers exactly the windows np_oracle.decode does, byte-exact."""
+    import np_oracle as N
+    key, dt = 9, 15
+    sid = O.GF256 if scheme == "gf" else O.RLC(key, dt)
+    nps = "gf" if scheme == "gf" else f"rlc:{key}:{dt}"
+    nwin, n = 6, k + r
+    stride = O.round_up(L, 16)
+    rng = np.random.default_rng(k + r)
+    wins = np.zeros((nwin, n, stride), np.uint8)
+    wins[:, :k, :L] = rng.integers(0, 256, (nwin, k, L), dtype=np.uint8)
+    S = np.full(nwin, L, np.uint32)
+    enc = wins.copy()
+    O.encode_batch_simd(sid, k, r, S, enc, 2)
+    for w in range(nwin):
+        assert np.array_equal(enc[w, k:, :L], N.encode(nps, k, r, wins[w, :k, :L])), w
+    nw = (n + 63) // 64
+    pres = np.zeros((nwin, nw), np.uint64)
+    bits = np.ones((nwin, n), bool)
+    for w in range(nwin):
+        e = w % (r + 2)  # 0 .. r + 1 missing sources
+        bits[w, rng.choice(k, e, replace=False)] = False
+        if w % 3 == 1:
+            bits[w, k + rng.integers(0, r)] = False
+    for i in range(n):
+        pres[:, i // 64] |= bits[:, i].astype(np.uint64) << np.uint64(i % 64)
+    dec = enc.copy()
+    dec[~bits] = 0xAB
+    st = O.decode_batch_simd(sid, k, r, S, dec, pres, 2)
+    for w in range(nwin):
+        p = 0
+        for i in np.flatnonzero(bits[w]):
+            p |= 1 << int(i)
+        sym = enc[w, :, :L].copy()
+        sym[~bits[w]] = 0xAB
+        _, ok = N.decode(nps, k, r, sym, p)
+        assert st[w] == (0 if ok else 1), w
+        if ok:
+            assert np.array_equal(dec[w, :k, :L], wins[w, :k, :L]), w
