@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--bs-passes", type=int, default=0,
                     help="tuning: bit-sliced encode on per-window lengths, 256-unit passes per window group")
     ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
+    ap.add_argument("--bsd-min-e", type=int, default=-1,
+                    help="tuning: GF decode erasures from which a window takes the bit-sliced decode (0 = never)")
     ap.add_argument("--bpc", type=int, default=0, help="tuning: persistent workgroups per CU")
     ap.add_argument("--sw-long-min", type=int, default=0,
                     help="tuning (config 7): unknowns from which a linked system takes the banded long path")
@@ -330,6 +332,8 @@ def make_ctx(args):
         ctx.set_tuning("bs_passes", args.bs_passes)
     if args.wpb:
         ctx.set_tuning("wpb", args.wpb)
+    if args.bsd_min_e >= 0:
+        ctx.set_tuning("bsd_min_e", args.bsd_min_e)
     if args.bpc:
         ctx.set_tuning("blocks_per_cu", args.bpc)
     if args.sw_group:

@@ -715,8 +715,9 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
     ChkRec *chk = nullptr;
     rc = ctx_chk_record(ctx, &chk);
     if (rc) return rc;
-    if (decode && mP) {
-        // the bit-sliced decode (fec_kernels.hip gf_decode_bs_kernel): a plan
+    if (decode && mP && ctx->bsd_min_e > 0) {
+        // the bit-sliced decode (tuning "bsd_min_e" 0: the two-stage one;
+        // fec_kernels.hip gf_decode_bs_kernel): a plan
         // per window in LDS, syndromes of the received sources by the plane
         // picks of P, the solve on the unit's columns; one launch, no scratch
         BatchArgs a{};
@@ -732,7 +733,7 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
         a.r = r;
         a.nw = (n + 63) / 64;
         a.prows = P;
-        a.enc_bs = mP;
+        a.enc_bs = mPI;  // [P | I]: the pivot repairs add themselves to their syndromes
         a.wpb = bsd_wpb(ncol, kRbsCols, k * r);
         a.chk.lo[0] = reinterpret_cast<uint64_t>(win);
         a.chk.n[0] = nwin * a.wpitch;

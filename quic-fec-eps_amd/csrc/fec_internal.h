@@ -97,6 +97,7 @@ struct BatchArgs {
     uint32_t *bsd_count;
     int bsd_min_e;
     int nw;
+    int bsd_cauchy;  // prows are the Cauchy rows (A.2): the closed-form plan
 };
 
 // Per-window LDS region of the bit-sliced decode (fec_kernels.hip

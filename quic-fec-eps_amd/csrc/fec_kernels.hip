@@ -97,6 +97,7 @@ __device__ __forceinline__ void st16(uint8_t *p, uint4 v) {
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
     return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
+__device__ __forceinline__ uint4 and4(uint4 a, uint32_t m) { return make_uint4(a.x & m, a.y & m, a.z & m, a.w & m); }
 __device__ __forceinline__ uint4 zero4() { return make_uint4(0, 0, 0, 0); }
 
 struct Split {
@@ -1391,7 +1392,8 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
 //   2. x_u = sum_i C[u][i] s_i over the pivot repairs (C from the window's
 //      plan: [A | I] reduced with pivot search, A[t][u] = P[sel_t][m_u], as
 //      plan_gf_mat), by the table multiply on the unit's few columns.
-// The plan is one wave per window in LDS, like gf_decode_kernel's.  Windows
+// The plan is one wave per window in LDS, like gf_decode_kernel's (Cauchy
+// rows in closed form as plan_gf, other rows by elimination).  Windows
 // come in groups of a.wpb from a.bsd_list (routed by the table decode's plan)
 // or, with no list, every window (the wide codes).
 namespace bsd {
@@ -1434,6 +1436,45 @@ __device__ void plan(const BatchArgs &a, uint64_t w, int lane, BsdRegion &rg, co
         return;
     }
     WAVE_SYNC();
+    if (a.bsd_cauchy) {
+        // Cauchy rows: the first e present repairs, and C in closed form (as
+        // plan_gf: log C[u][i] = A_u + K_i - log(x_i ^ m_u), x_i = k + i), lane
+        // u * 8 + i, independent LDS lookups instead of the elimination chain
+        uint32_t ub = 0;
+        {
+            uint32_t rb = rep;
+            for (int c = 0; c < e; c++) {
+                ub |= rb & (0u - rb);
+                rb &= rb - 1;
+            }
+        }
+        const int u = lane >> 3, i = lane & 7;
+        uint32_t v = 0;
+        if (u < e && ((ub >> i) & 1u)) {
+            const int mu = rg.m[u], x = k + i;
+            int L = 255 * 32 - (int)lg[x ^ mu];
+            for (uint32_t b = ub; b; b &= b - 1) {
+                const int xt = k + __ffs(b) - 1;
+                L += (int)lg[xt ^ mu] - (xt != x ? (int)lg[xt ^ x] : 0);
+            }
+            for (int q = 0; q < e; q++) {
+                const int mv = rg.m[q];
+                L += (int)lg[x ^ mv] - (q != u ? (int)lg[mu ^ mv] : 0);
+            }
+            v = ex[L % 255];
+        }
+        const CoefTab ct = make_coef_tab(v);
+        rg.ab[lane] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+        rg.tc[lane] = ct.c;
+        if (lane < 4) rg.pw[lane] = lane == 0 ? pw[0] : lane == 1 ? pw[1] : lane == 2 ? pw[2] : pw[3];
+        if (lane == 0) {
+            rg.ne = (uint32_t)e;
+            rg.used = ub;
+            rg.alt = first >= 0 ? (uint32_t)first : (uint32_t)(k + __ffs(ub) - 1);
+            a.status[w] = FECGPU_STATUS_OK;
+        }
+        return;
+    }
     uint32_t rr = rep;
     for (int i = 0; i < lane && i < 8; i++) rr &= rr - 1;
     const int my_sel = rr ? __ffs(rr) - 1 : 0;  // lane t < np: the t-th present repair
@@ -1495,28 +1536,44 @@ __device__ void plan(const BatchArgs &a, uint64_t w, int lane, BsdRegion &rg, co
 }
 
 // Stage 2 on one 16-B column: acc[i][H .. H + 3] the column of syndrome i
-// after stage 1 (bytes); the repair row i is added here where the window uses
-// it (bit i of `used`), then x_u = sum_i C[u][i] s_i for u < nw (wave-uniform),
-// stored to row m[u] when u < ne.  col: the column's address in row 0.
-template <int R, int H, int K>
-__device__ __forceinline__ void solve_col(const uint32_t (&acc)[R][8], uint8_t *col, uint32_t stride, int k,
+// (bytes, the repair rows the window uses already added: a load per syndrome
+// here was a dependent round trip each), x_u = sum_i C[u][i] s_i for u < nw
+// (wave-uniform), stored to row m[u] when u < ne.  col: the column's address
+// in row 0.
+// Outputs UC at a time (UC < R: fewer live accumulators, each syndrome split
+// R / UC times).
+template <int R, int H, int UC = R>
+__device__ __forceinline__ void solve_col(const uint32_t (&acc)[R][8], uint8_t *col, uint32_t stride,
                                           const BsdRegion &rg, int nw, int ne, bool live) {
-    const uint32_t used = rg.used;
-    uint4 x[R];
 #pragma unroll
-    for (int u = 0; u < R; u++) x[u] = zero4();
+    for (int u0 = 0; u0 < R; u0 += UC) {
+        if (u0 >= nw) break;  // wave-uniform
+        uint4 x[UC];
+#pragma unroll
+        for (int u = 0; u < UC; u++) x[u] = zero4();
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            const Split sp = split(make_uint4(acc[i][H], acc[i][H + 1], acc[i][H + 2], acc[i][H + 3]));
+#pragma unroll
+            for (int u = 0; u < UC; u++)
+                if (u0 + u < R && u0 + u < nw) gmac(x[u], sp, rg.ab[(u0 + u) * kMaxR + i], rg.tc[(u0 + u) * kMaxR + i]);
+        }
+#pragma unroll
+        for (int u = 0; u < UC; u++)
+            if (u0 + u < R && u0 + u < nw && u0 + u < ne && live) st16(col + (uint32_t)rg.m[u0 + u] * stride, x[u]);
+    }
+}
+
+// acc[i][H .. H + 3] ^= v[i] (a column of syndrome i, bytes)
+template <int R, int H>
+__device__ __forceinline__ void add_col(uint32_t (&acc)[R][8], const uint4 (&v)[R]) {
 #pragma unroll
     for (int i = 0; i < R; i++) {
-        uint4 si = make_uint4(acc[i][H], acc[i][H + 1], acc[i][H + 2], acc[i][H + 3]);
-        if ((used >> i) & 1u) si = xor4(si, ld16(col + (uint32_t)((K ? K : k) + i) * stride));
-        const Split sp = split(si);
-#pragma unroll
-        for (int u = 0; u < R; u++)
-            if (u < nw) gmac(x[u], sp, rg.ab[u * kMaxR + i], rg.tc[u * kMaxR + i]);
+        acc[i][H] ^= v[i].x;
+        acc[i][H + 1] ^= v[i].y;
+        acc[i][H + 2] ^= v[i].z;
+        acc[i][H + 3] ^= v[i].w;
     }
-#pragma unroll
-    for (int u = 0; u < R; u++)
-        if (u < nw && u < ne && live) st16(col + (uint32_t)rg.m[u] * stride, x[u]);
 }
 
 }  // namespace bsd
@@ -1566,12 +1623,30 @@ __device__ __forceinline__ void dec_unit(uint8_t *pa, uint8_t *pb, uint32_t stri
     const uint64_t pm = rg.pw[0];
     const uint32_t alt = rg.alt;
     uint32_t acc[R][8];
-    dsources<K, R, M, U, 0>(pa, pb, stride, pm, pa + alt * stride, pb + alt * stride, acc);
+    const uint8_t *qa = pa + alt * stride, *qb = pb + alt * stride;
+    dsources<K, R, M, U, 0>(pa, pb, stride, pm, qa, qb, acc);
+    // the repairs the window uses, one batch (the others read at the alt row
+    // and masked to zero), added to the syndromes' bytes
+    const uint32_t used = rg.used;
+    uint4 ra[R], rb[R];
 #pragma unroll
-    for (int i = 0; i < R; i++) tr8(acc[i]);
+    for (int i = 0; i < R; i++) {
+        const bool p = (used >> i) & 1u;
+        ra[i] = ld16(p ? pa + (K + i) * stride : qa);
+        rb[i] = ld16(p ? pb + (K + i) * stride : qb);
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        tr8(acc[i]);
+        const uint32_t mk = ((used >> i) & 1u) ? ~0u : 0u;
+        ra[i] = and4(ra[i], mk);
+        rb[i] = and4(rb[i], mk);
+    }
+    bsd::add_col<R, 0>(acc, ra);
+    bsd::add_col<R, 4>(acc, rb);
     const int ne = (int)rg.ne;
-    bsd::solve_col<R, 0, K>(acc, pa, stride, K, rg, nw, ne, live);
-    bsd::solve_col<R, 4, K>(acc, pb, stride, K, rg, nw, ne, pb != pa && live);
+    bsd::solve_col<R, 0>(acc, pa, stride, rg, nw, ne, live);
+    bsd::solve_col<R, 4>(acc, pb, stride, rg, nw, ne, pb != pa && live);
 }
 
 }  // namespace bs
@@ -1584,15 +1659,23 @@ namespace rbs4 {
 // 64-bit address arithmetic per load), the row offset a scalar — and a source
 // the lane's window misses is read at an offset past the resource (2^31
 // added), which the hardware returns as zeros without a memory access: no
-// masking, no traffic for missing rows.  Then the repairs the solve uses and
-// the solve on each column (pointers pc[c]).
+// masking, no traffic for missing rows.  The repairs the solve uses are k + i
+// more inputs (identity picks), then the solve on each column (pointers pc[c]).
 constexpr uint32_t kOob = 0x80000000u;  // added to a column offset: past any group's records
 template <int R>
 __device__ __forceinline__ void dec_unit(__amdgpu_buffer_rsrc_t rs, const uint32_t (&coff)[4], uint8_t *const (&pc)[4],
                                          uint32_t stride, int k, cmask mk, bool live, const BsdRegion &rg, int nw) {
     // present bits 32 at a time from the region (one LDS read per 32 sources)
+    // inputs j < k the sources (present bits), j >= k the repairs, read only
+    // where the window's solve uses them (mk: the picks of [P | I], so repair i
+    // adds itself to syndrome i)
     const uint32_t *pw32 = reinterpret_cast<const uint32_t *>(rg.pw);
-    const auto vo = [&](int j) -> uint32_t { return ((pw32[j >> 5] >> (j & 31)) & 1u) ? 0u : kOob; };  // uniform j
+    const uint32_t used = rg.used;
+    const auto vo = [&](int j) -> uint32_t {  // uniform j
+        const uint32_t b = j < k ? (pw32[j >> 5] >> (j & 31)) : (used >> (j - k));
+        return (b & 1u) ? 0u : kOob;
+    };
+    const int n = k + R;
     // the row offset goes in the vector offset too (soffset 0): the range
     // check then covers the whole offset whatever soffset's treatment
     const auto bload = [&](uint32_t off, uint32_t (&xa)[8], uint32_t (&xb)[8]) __attribute__((always_inline)) {
@@ -1612,9 +1695,9 @@ __device__ __forceinline__ void dec_unit(__amdgpu_buffer_rsrc_t rs, const uint32
         for (int p = 0; p < 8; p++) aa[i][p] = ab[i][p] = 0;
     uint32_t xa[8], xb[8];
     bload(vo(0), xa, xb);
-    for (int j = 0; j < k; j++) {
+    for (int j = 0; j < n; j++) {
         uint32_t na[8], nb[8];
-        const int jn = min(j + 1, k - 1);
+        const int jn = min(j + 1, n - 1);
         bload((uint32_t)jn * stride + vo(jn), na, nb);
         bs::tr8(xa);
         bs::tr8(xb);
@@ -1632,10 +1715,11 @@ __device__ __forceinline__ void dec_unit(__amdgpu_buffer_rsrc_t rs, const uint32
         bs::tr8(ab[i]);
     }
     const int ne = (int)rg.ne;
-    bsd::solve_col<R, 0, 0>(aa, pc[0], stride, k, rg, nw, ne, live);
-    bsd::solve_col<R, 4, 0>(aa, pc[1], stride, k, rg, nw, ne, live && pc[1] != pc[0]);
-    bsd::solve_col<R, 0, 0>(ab, pc[2], stride, k, rg, nw, ne, live && pc[2] != pc[0]);
-    bsd::solve_col<R, 4, 0>(ab, pc[3], stride, k, rg, nw, ne, live && pc[3] != pc[0]);
+    constexpr int UC = R;
+    bsd::solve_col<R, 0, UC>(aa, pc[0], stride, rg, nw, ne, live);
+    bsd::solve_col<R, 4, UC>(aa, pc[1], stride, rg, nw, ne, live && pc[1] != pc[0]);
+    bsd::solve_col<R, 0, UC>(ab, pc[2], stride, rg, nw, ne, live && pc[2] != pc[0]);
+    bsd::solve_col<R, 4, UC>(ab, pc[3], stride, rg, nw, ne, live && pc[3] != pc[0]);
 }
 
 }  // namespace rbs4
@@ -2493,6 +2577,7 @@ hipError_t launch_gf_decode_table(const BatchArgs &a, const LaunchPlan &p, hipSt
 hipError_t launch_decode_bs(BatchArgs a, int matrix, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     if (a.r < 4 || a.r > kMaxR || !a.prows) return hipErrorInvalidValue;
+    a.bsd_cauchy = matrix == FECGPU_MATRIX_CAUCHY;
     LaunchPlan p{};
     p.wpb = a.wpb;
     p.lds_bytes = (uint32_t)(a.wpb * sizeof(BsdRegion)) + (((uint32_t)(a.k * a.r) + 15u) & ~15u);

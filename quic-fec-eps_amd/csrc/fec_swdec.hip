@@ -148,6 +148,20 @@ __device__ uint64_t wave_lower_bound(const fecgpu_sw_repair *h, uint64_t lo, uin
     const uint64_t b = __ballot(pos < hi && h[pos].fss >= key);
     return b ? lo + (uint64_t)(__ffsll((unsigned long long)b) - 1) : hi;
 }
+// The same answer starting from a guess g (repairs spread evenly over the
+// stream put the answer near key * nrep / nsrc): one round of 64 loads around
+// g decides it when the answer lies inside, else the 64-ary search over the
+// side it lies on.
+__device__ uint64_t wave_lower_bound_near(const fecgpu_sw_repair *h, uint64_t hi, uint64_t key, uint64_t g, int lane) {
+    const uint64_t lo = g > 32 ? min(g - 32, hi > 64 ? hi - 64 : 0) : 0;
+    const uint64_t pos = lo + (uint64_t)lane;
+    const bool in = pos < hi;
+    const uint64_t b = __ballot(in && h[pos].fss >= key);
+    const bool first_below = !(b & 1ull) || lo == 0;  // lane 0's header is below key (or there is none before it)
+    if (b && first_below) return lo + (uint64_t)(__ffsll((unsigned long long)b) - 1);
+    if (!b) return lo + 64 >= hi ? hi : wave_lower_bound(h, lo + 64, hi, key, lane);
+    return wave_lower_bound(h, 0, lo + 1, key, lane);  // the answer is at or before lo
+}
 
 // the repair's window holds one of the lost sources lost[x .. x + e) (rank =
 // lost sources before i)
@@ -681,59 +695,33 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     const uint32_t c = s_chunk;
     const uint64_t i0 = (uint64_t)c * kPlanChunk, i1 = min(i0 + kPlanChunk, a.nsrc);
     const uint64_t ib = i0 >= (uint64_t)kPlanHalo ? i0 - kPlanHalo : 0;  // back region [ib, i0)
-    // the chunk's repairs (fss in [i0, i1)) and those of the back region: three
-    // searches, a wave each
-    if (wave < 3) {
-        const uint64_t key = wave == 0 ? i0 : wave == 1 ? i1 : ib;
-        const uint64_t t = (wave == 1 && i1 == a.nsrc) ? a.nrep : wave_lower_bound(a.hdr, 0, a.nrep, key, lane);
-        if (lane == 0) (wave == 0 ? s_t0 : wave == 1 ? s_t1 : s_tb) = t;
-    }
-    // this block's share of the header checks, and of emptying the syndrome job
-    // slots (every slot, whatever the headers hold: the syndrome pass walks them all)
-    bool bad = false;
-    {
-        const uint64_t h0 = (uint64_t)c * a.nrep / nch, h1 = (uint64_t)(c + 1) * a.nrep / nch;
-        CombJob E{};
-        E.xor_off = kNoXor;
-        for (uint64_t t = h0 + tid; t < h1; t += kBlock) {
-            if (!SWC(t, a.nrep, kChkSynJob)) break;
-            a.syn_jobs[t] = E;
-            const fecgpu_sw_repair h = a.hdr[t];
-            bad |= !hdr_ok(h, a.nsrc);
-            if (t > 0 && a.hdr[t - 1].fss > h.fss) bad = true;
-        }
-    }
-    if (__ballot(bad) && lane == 0) s_bad = 1;
-    __syncthreads();
-    SWD_TRACE(2);
-    const uint64_t t0 = s_t0, t1 = max(s_t0, s_t1), tb = min(s_tb, t0);
-    // reach / repair counts of the chunk's sources and the back region's
-    // repair counts; the widest received window among them (pivot searches)
-    uint32_t wm = 0, wmb = 0;
-    for (uint64_t t = tb + tid; t < t1; t += kBlock) {
-        const fecgpu_sw_repair h = a.hdr[t];
-        const bool rp = a.rep_present[t] != 0;
-        if (h.nss < 1 || h.nss > kSwMaxWindow) continue;
-        if (h.fss >= i0 && h.fss < i1) {
-            atomicAdd(&s_rcnt[h.fss - i0], 1u);
-            if (rp) {
-                wm = max(wm, (uint32_t)h.nss);
-                atomicMax(&s_reach[h.fss - i0], (uint32_t)(h.fss + h.nss));
-            }
-        } else if (h.fss >= ib && h.fss < i0) {
-            atomicAdd(&s_rcb[h.fss - (i0 - kPlanHalo)], 1u);
-        }
-        if (rp) wmb = max(wmb, (uint32_t)h.nss);
-    }
-    wmb = wave_max(wmb);
-    if (lane == 0 && wmb) atomicMax(&s_wmb, wmb);
-    // arrival flags: 8 sources per thread, and the halo past the chunk
+    // the arrival flags' loads first (no dependence on the headers, so they are
+    // in flight with the searches' first round): 8 sources per thread, and the
+    // halo past the chunk (8 flags per lane of wave 0's lanes 0-31, full chunks only)
     const uint32_t n = (uint32_t)(i1 - i0), my0 = (uint32_t)tid * kPlanPer;
-    uint32_t lostm = 0;  // bit j: source i0 + my0 + j lost
     // 8-byte flag loads / status stores where both arrays allow (caller pointers)
     const bool vec = ((reinterpret_cast<uintptr_t>(a.src_present) | reinterpret_cast<uintptr_t>(a.stat)) & 7u) == 0;
-    if (vec && my0 + kPlanPer <= n) {
-        const uint2 pv = *reinterpret_cast<const uint2 *>(a.src_present + i0 + my0);
+    const bool fast = vec && my0 + kPlanPer <= n;
+    const bool hl = wave == 0 && lane < kPlanHalo / 8 && n == (uint32_t)kPlanChunk;
+    const uint64_t hh0 = i1 + (uint64_t)lane * 8;
+    const bool hfast = hl && vec && hh0 + 8 <= a.nsrc;  // one 8-byte load (the chunk is 8-aligned)
+    uint2 pv = make_uint2(0, 0), hpv = make_uint2(0, 0);
+    if (fast) pv = *reinterpret_cast<const uint2 *>(a.src_present + i0 + my0);
+    if (hfast) hpv = *reinterpret_cast<const uint2 *>(a.src_present + hh0);
+    // the chunk's repairs (fss in [i0, i1)) and those of the back region: three
+    // searches, a wave each, from the even-spread guess (one round of loads when
+    // the repairs are spread evenly).  Chunk c's range ends where chunk c + 1's
+    // begins (the same search), so the ranges cover every header whatever the
+    // list holds (t1 = max(t0, search(i1)): the first chunk at or before a
+    // header whose range starts at or before it holds it)
+    if (wave < 3) {
+        const uint64_t key = wave == 0 ? i0 : wave == 1 ? i1 : ib;
+        const uint64_t g = (uint64_t)(((unsigned __int128)key * a.nrep) / max<uint64_t>(a.nsrc, 1));
+        const uint64_t t = (wave == 1 && i1 == a.nsrc) ? a.nrep : wave_lower_bound_near(a.hdr, a.nrep, key, g, lane);
+        if (lane == 0) (wave == 0 ? s_t0 : wave == 1 ? s_t1 : s_tb) = t;
+    }
+    uint32_t lostm = 0;  // bit j: source i0 + my0 + j lost
+    if (fast) {
         uint2 st;
         for (int j = 0; j < 8; j++) {
             const uint32_t byte = ((j < 4 ? pv.x : pv.y) >> (8 * (j & 3))) & 0xFFu;
@@ -758,17 +746,14 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         wv |= __shfl_xor(wv, 2);
         if ((tid & 3) == 0) s_bits[tid >> 2] = wv;
     }
-    if (wave == 0) {  // halo: 8 flags per lane of lanes 0-31, 4 lanes per word (full chunks only)
-        const bool hl = lane < kPlanHalo / 8 && n == (uint32_t)kPlanChunk;
+    if (wave == 0) {  // halo words, 4 lanes per word
         uint32_t hw = 0;
         if (hl) {
-            const uint64_t h0 = i1 + (uint64_t)lane * 8;
             uint32_t m8 = 0;
-            if (vec && h0 + 8 <= a.nsrc) {  // one 8-byte load (the chunk is 8-aligned)
-                const uint2 pv = *reinterpret_cast<const uint2 *>(a.src_present + h0);
-                for (int j = 0; j < 8; j++) m8 |= ((((j < 4 ? pv.x : pv.y) >> (8 * (j & 3))) & 0xFFu) == 0 ? 1u : 0u) << j;
+            if (hfast) {
+                for (int j = 0; j < 8; j++) m8 |= ((((j < 4 ? hpv.x : hpv.y) >> (8 * (j & 3))) & 0xFFu) == 0 ? 1u : 0u) << j;
             } else {
-                for (int j = 0; j < 8; j++) m8 |= (h0 + j < a.nsrc && a.src_present[h0 + j] == 0 ? 1u : 0u) << j;
+                for (int j = 0; j < 8; j++) m8 |= (hh0 + j < a.nsrc && a.src_present[hh0 + j] == 0 ? 1u : 0u) << j;
             }
             hw = m8 << ((lane & 3) * 8);
         }
@@ -780,6 +765,42 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         for (uint32_t w = tid; w < (kPlanChunk + kPlanHalo) / 32; w += kBlock)
             if (w * 32 >= ((n + 31) & ~31u)) s_bits[w] = 0;
     }
+    __syncthreads();
+    SWD_TRACE(2);
+    const uint64_t t0 = s_t0, t1 = max(s_t0, s_t1), tb = min(s_tb, t0);
+    // reach / repair counts of the chunk's sources and the back region's
+    // repair counts; the widest received window among them (pivot searches);
+    // and, for the chunk's own range [t0, t1), the header checks (a bad or
+    // unordered list raises kSwErrHeader) and emptying the syndrome job slots
+    // (every slot, whatever the headers hold: the syndrome pass walks them all)
+    uint32_t wm = 0, wmb = 0;
+    bool bad = false;
+    CombJob E0{};
+    E0.xor_off = kNoXor;
+    for (uint64_t t = tb + tid; t < t1; t += kBlock) {
+        if (!SWC(t, a.nrep, kChkSynJob)) break;
+        const fecgpu_sw_repair h = a.hdr[t];
+        const bool rp = a.rep_present[t] != 0;
+        if (t >= t0) {
+            a.syn_jobs[t] = E0;
+            bad |= !hdr_ok(h, a.nsrc);
+            if (t > 0 && a.hdr[t - 1].fss > h.fss) bad = true;
+        }
+        if (h.nss < 1 || h.nss > kSwMaxWindow) continue;
+        if (h.fss >= i0 && h.fss < i1) {
+            atomicAdd(&s_rcnt[h.fss - i0], 1u);
+            if (rp) {
+                wm = max(wm, (uint32_t)h.nss);
+                atomicMax(&s_reach[h.fss - i0], (uint32_t)(h.fss + h.nss));
+            }
+        } else if (h.fss >= ib && h.fss < i0) {
+            atomicAdd(&s_rcb[h.fss - (i0 - kPlanHalo)], 1u);
+        }
+        if (rp) wmb = max(wmb, (uint32_t)h.nss);
+    }
+    if (__ballot(bad) && lane == 0) s_bad = 1;
+    wmb = wave_max(wmb);
+    if (lane == 0 && wmb) atomicMax(&s_wmb, wmb);
     __syncthreads();
     SWD_TRACE(3);
     // per thread: its 8 sources' lost count, max reach, repair count

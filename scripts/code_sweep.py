@@ -38,12 +38,16 @@ def kernel_name(ctx_bs: bool, scheme, matrix, k, r):
 def main():
     only = sys.argv[1] if len(sys.argv) > 1 else ""  # "rbs": the runtime-mask shapes only
     ctx = fecgpu.Context()
+    if os.environ.get("BSD_MIN_E"):  # GF decode: erasures from which the bit-sliced decode runs
+        ctx.set_tuning("bsd_min_e", int(os.environ["BSD_MIN_E"]))
     dev = torch.device("cuda")
     base = workloads.CONFIGS[3]
     for scheme, matrix, k, r in SHAPES:
         if only == "rbs" and kernel_name(True, scheme, matrix, k, r) != "bit-sliced (runtime masks)":
             continue
         if only == "r8" and (scheme != "gf256" or r != 8):  # the e = r = 8 decode rows
+            continue
+        if only.startswith("shape=") and only[6:] != f"{scheme}-{matrix}-{k}-{r}":  # e.g. shape=gf256-cauchy-32-8
             continue
         stride = 1216
         nwin = int(1.2e9 // ((k + r) * stride))

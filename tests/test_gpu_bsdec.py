@@ -83,6 +83,7 @@ def test_bsdec_vs_oracle(k, matrix, L):
         rng = np.random.default_rng(k + L)
         bits = _erasures(96, k, 8, rng, lo=3)
         bits[0] = True
+        bits[1] = True
         bits[1, :8] = False  # exactly r = 8 sources, every repair present
         _, gst = _run(c, k, 8, matrix, L, 96, bits)
         assert gst[0] == 0 and gst[1] == 0

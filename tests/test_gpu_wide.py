@@ -52,8 +52,9 @@ def _run(ctx, k, r, matrix, L, nwin, pres_bits, key=5, dt=15, sym_len=None, seed
     enc = d.cpu().numpy()
     scheme = _scheme(matrix, key, dt)
     for w in range(nwin):
-        ref = N.encode(scheme, k, r, wins[w, :k, :L])
-        assert np.array_equal(enc[w, k:, :L], ref), f"window {w}: repairs differ"
+        S = L if sym_len is None else int(sym_len[w])
+        ref = N.encode(scheme, k, r, wins[w, :k, :S])
+        assert np.array_equal(enc[w, k:, :S], ref), f"window {w}: repairs differ"
     mask = torch.from_numpy(pres_bits).cuda()
     d[~mask] = 0xAB  # poison every missing symbol
     st = torch.full((nwin,), 7, dtype=torch.uint8, device="cuda")
@@ -66,13 +67,14 @@ def _run(ctx, k, r, matrix, L, nwin, pres_bits, key=5, dt=15, sym_len=None, seed
         p = 0
         for i in np.flatnonzero(pres_bits[w]):
             p |= 1 << int(i)
-        sym = enc[w, :, :L].copy()
+        S = L if sym_len is None else int(sym_len[w])  # bytes past S_w are padding (fecgpu.h)
+        sym = enc[w, :, :S].copy()
         sym[~pres_bits[w]] = 0xAB
         ref, ok = N.decode(scheme, k, r, sym, p)
         assert gst[w] == (0 if ok else 1), f"window {w}: status {gst[w]}, oracle ok={ok}"
         if ok:
-            assert np.array_equal(got[w, :k, :L], wins[w, :k, :L]), f"window {w}: recovered bytes differ"
-            assert np.array_equal(ref, wins[w, :k, :L])
+            assert np.array_equal(got[w, :k, :S], wins[w, :k, :S]), f"window {w}: recovered bytes differ"
+            assert np.array_equal(ref, wins[w, :k, :S])
     return gst
 
 
