@@ -87,14 +87,15 @@ struct BatchArgs {
     uint32_t off_stride;
     ChkRange chk;              // FECGPU_CHECK builds: where this launch's symbols lie
     // bit-sliced decode of windows with many erasures (gf_decode_bs_kernel):
-    // the table decode's plan sends windows with e >= bsd_min_e (0: none) to
-    // bsd_list (window indices, *bsd_count of them, zeroed by the host before
-    // the launch); the bit-sliced kernel plans them from the parity rows prows
-    // P[r][k] (any matrix).  nw: present-mask words per window (1, or
-    // ceil((k + r) / 64) for the wide codes, whose kernel takes every window).
+    // the table decode's plan flags windows with e >= bsd_min_e (0: none) in
+    // bsd_flag[w] (1, else 0: it writes every window's), and the bit-sliced
+    // kernel takes them range by range in batch order, planning them from the
+    // parity rows prows P[r][k] (any matrix).  Without flags it takes every
+    // window (the wide codes).  nw: present-mask words per window (1, or
+    // ceil((k + r) / 64) for the wide codes).
     const uint8_t *prows;
-    uint32_t *bsd_list;
-    uint32_t *bsd_count;
+    uint8_t *bsd_flag;
+    int bsd_range;  // flagged windows: windows per range (launch_decode_bs)
     int bsd_min_e;
     int nw;
     int bsd_cauchy;  // prows are the Cauchy rows (A.2): the closed-form plan
@@ -478,7 +479,8 @@ struct SwDecArgs {
     uint64_t lb_cap;      // look-back records allocated (chunks)
     ChkRec *chk;          // FECGPU_CHECK builds: the fault record (release: null)
 };
-hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s);    // statuses, lost list, systems
+hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s);    // statuses, lost list, one-unknown systems
+hipError_t launch_sw_dec_sys(const SwDecArgs &a, hipStream_t s);     // the larger systems
 hipError_t launch_sw_dec_long(const SwDecArgs &a, hipStream_t s);    // long systems: logs, syndrome jobs
 hipError_t launch_sw_dec_replay(const SwDecArgs &a, hipStream_t s);  // long systems: data
 
@@ -555,5 +557,10 @@ ssize_t ctx_rlc_table(fecgpu_ctx *ctx, hipStream_t s, const uint8_t **tab);
 ssize_t ctx_sw_wait(fecgpu_ctx *ctx);
 ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);
 ssize_t ctx_sw_end(fecgpu_ctx *ctx, hipStream_t s);
+// A second stream of the current device for work of one call that runs
+// beside the rest: fork = *s2 waits for what `s` holds so far (nullptr when
+// the ctx's "sw_fork" tuning is 0); join = `s` waits for what *s2 holds.
+ssize_t ctx_sw_fork(fecgpu_ctx *ctx, hipStream_t s, hipStream_t *s2);
+ssize_t ctx_sw_join(fecgpu_ctx *ctx, hipStream_t s, hipStream_t s2);
 
 }  // namespace fecgpu

@@ -1021,13 +1021,14 @@ __device__ __forceinline__ void plan_offsets(const BatchArgs &a, uint64_t w, int
 }
 
 // Windows of many erasures go to the bit-sliced decode (gf_decode_bs_kernel
-// below, launched after this kernel over the list): e >= a.bsd_min_e (0: off).
-// The window's status is that kernel's to write.
+// below, launched after this kernel over the flags): e >= a.bsd_min_e (0:
+// off).  The window's status is that kernel's to write.  (Lane 0 of the
+// planning wave cleared the flag before the plan: same lane, same address.)
 __device__ __forceinline__ bool bsd_route(const BatchArgs &a, uint64_t w, int e, int lane, uint8_t &ne_out) {
     if (!a.bsd_min_e || e < a.bsd_min_e) return false;
     if (lane == 0) {
         ne_out = 0;
-        a.bsd_list[atomicAdd(a.bsd_count, 1u)] = (uint32_t)w;
+        a.bsd_flag[w] = 1;
     }
     return true;
 }
@@ -1333,6 +1334,7 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
                 const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl, i);
                 const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pl >> 32), i);
                 const uint64_t pw = ((uint64_t)hi << 32) | lo;
+                if (a.bsd_min_e && lane == 0) a.bsd_flag[w0 + wl] = 0;  // bsd_route sets it
                 if (a.coef)  // wave-uniform: one code per launch
                     plan_gf_mat<R>(a, w0 + wl, pw, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log,
                                    s_coef, s_ne[wl]);
@@ -1540,28 +1542,22 @@ __device__ void plan(const BatchArgs &a, uint64_t w, int lane, BsdRegion &rg, co
 // here was a dependent round trip each), x_u = sum_i C[u][i] s_i for u < nw
 // (wave-uniform), stored to row m[u] when u < ne.  col: the column's address
 // in row 0.
-// Outputs UC at a time (UC < R: fewer live accumulators, each syndrome split
-// R / UC times).
-template <int R, int H, int UC = R>
+template <int R, int H>
 __device__ __forceinline__ void solve_col(const uint32_t (&acc)[R][8], uint8_t *col, uint32_t stride,
                                           const BsdRegion &rg, int nw, int ne, bool live) {
+    uint4 x[R];
 #pragma unroll
-    for (int u0 = 0; u0 < R; u0 += UC) {
-        if (u0 >= nw) break;  // wave-uniform
-        uint4 x[UC];
+    for (int u = 0; u < R; u++) x[u] = zero4();
 #pragma unroll
-        for (int u = 0; u < UC; u++) x[u] = zero4();
+    for (int i = 0; i < R; i++) {
+        const Split sp = split(make_uint4(acc[i][H], acc[i][H + 1], acc[i][H + 2], acc[i][H + 3]));
 #pragma unroll
-        for (int i = 0; i < R; i++) {
-            const Split sp = split(make_uint4(acc[i][H], acc[i][H + 1], acc[i][H + 2], acc[i][H + 3]));
-#pragma unroll
-            for (int u = 0; u < UC; u++)
-                if (u0 + u < R && u0 + u < nw) gmac(x[u], sp, rg.ab[(u0 + u) * kMaxR + i], rg.tc[(u0 + u) * kMaxR + i]);
-        }
-#pragma unroll
-        for (int u = 0; u < UC; u++)
-            if (u0 + u < R && u0 + u < nw && u0 + u < ne && live) st16(col + (uint32_t)rg.m[u0 + u] * stride, x[u]);
+        for (int u = 0; u < R; u++)
+            if (u < nw) gmac(x[u], sp, rg.ab[u * kMaxR + i], rg.tc[u * kMaxR + i]);
     }
+#pragma unroll
+    for (int u = 0; u < R; u++)
+        if (u < nw && u < ne && live) st16(col + (uint32_t)rg.m[u] * stride, x[u]);
 }
 
 // acc[i][H .. H + 3] ^= v[i] (a column of syndrome i, bytes)
@@ -1715,11 +1711,10 @@ __device__ __forceinline__ void dec_unit(__amdgpu_buffer_rsrc_t rs, const uint32
         bs::tr8(ab[i]);
     }
     const int ne = (int)rg.ne;
-    constexpr int UC = R;
-    bsd::solve_col<R, 0, UC>(aa, pc[0], stride, rg, nw, ne, live);
-    bsd::solve_col<R, 4, UC>(aa, pc[1], stride, rg, nw, ne, live && pc[1] != pc[0]);
-    bsd::solve_col<R, 0, UC>(ab, pc[2], stride, rg, nw, ne, live && pc[2] != pc[0]);
-    bsd::solve_col<R, 4, UC>(ab, pc[3], stride, rg, nw, ne, live && pc[3] != pc[0]);
+    bsd::solve_col<R, 0>(aa, pc[0], stride, rg, nw, ne, live);
+    bsd::solve_col<R, 4>(aa, pc[1], stride, rg, nw, ne, live && pc[1] != pc[0]);
+    bsd::solve_col<R, 0>(ab, pc[2], stride, rg, nw, ne, live && pc[2] != pc[0]);
+    bsd::solve_col<R, 4>(ab, pc[3], stride, rg, nw, ne, live && pc[3] != pc[0]);
 }
 
 }  // namespace rbs4
@@ -1741,20 +1736,55 @@ void gf_decode_bs_kernel(BatchArgs a) {
     __shared__ GroupLds g;
     __shared__ uint32_t s_w[kMaxWpb];
     __shared__ uint8_t s_perm[kMaxWpb];
+    __shared__ uint16_t s_list[kBlock];
+    __shared__ uint32_t s_cnt[kBlock / 64];
     BsdRegion *rgn = reinterpret_cast<BsdRegion *>(dyn);
     uint8_t *s_P = reinterpret_cast<uint8_t *>(rgn + a.wpb);  // parity rows [r][k]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
     for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
     for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
     for (int i = tid; i < a.r * k; i += kBlock) s_P[i] = a.prows[i];
-    const uint64_t count = a.bsd_count ? (uint64_t)*a.bsd_count : a.nwin;
     constexpr uint32_t C = RT ? kRbsCols : 2;  // columns per unit
+    // flagged windows: ranges of kBlock windows in batch order, their flagged
+    // ones listed in LDS and taken a.wpb at a time; else groups of a.wpb
+    const bool flagged = a.bsd_flag != nullptr;
+    const uint32_t range = (uint32_t)a.bsd_range;  // <= kBlock, a multiple of 64
+    const uint64_t nunit = flagged ? (a.nwin + range - 1) / range : (a.nwin + a.wpb - 1) / a.wpb;
     __syncthreads();
-    for (XcdRange xr = xcd_range((count + a.wpb - 1) / a.wpb, a.nx); xr.cur < xr.hi; xr.cur += xr.step) {
-        const uint64_t g0 = xr.cur * a.wpb;
-        const int nb = (int)min((uint64_t)a.wpb, count - g0);
+    // one loop over sub-batches (a nested loop per range spilled the unit's registers)
+    XcdRange xr = xcd_range(nunit, a.nx);
+    uint64_t r0 = 0;
+    uint32_t nl = 0, b0 = 0;
+    bool first = true;
+    for (;;) {
+        if (b0 >= nl) {  // the next range / group
+            if (!first) xr.cur += xr.step;
+            first = false;
+            if (xr.cur >= xr.hi) break;
+            b0 = 0;
+            if (flagged) {
+                r0 = xr.cur * range;
+                const bool f = (uint32_t)tid < range && r0 + tid < a.nwin && a.bsd_flag[r0 + tid];
+                const uint64_t b = __ballot(f);
+                if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(b);
+                __syncthreads();
+                uint32_t off = 0;
+                nl = 0;
+                for (int v = 0; v < kBlock / 64; v++) {
+                    if (v < wave) off += s_cnt[v];
+                    nl += s_cnt[v];
+                }
+                if (f) s_list[off + __popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)tid;
+                __syncthreads();
+                if (nl == 0) continue;
+            } else {
+                r0 = xr.cur * a.wpb;
+                nl = (uint32_t)min((uint64_t)a.wpb, a.nwin - r0);
+            }
+        }
+        const int nb = (int)min((uint32_t)a.wpb, nl - b0);
         if (tid < nb) {
-            const uint64_t w = a.bsd_list ? (uint64_t)a.bsd_list[g0 + tid] : g0 + tid;
+            const uint64_t w = r0 + (flagged ? (uint64_t)s_list[b0 + tid] : (uint64_t)tid);
             s_w[tid] = (uint32_t)w;
             uint64_t base;
             uint32_t stride, S;
@@ -1820,6 +1850,7 @@ void gf_decode_bs_kernel(BatchArgs a) {
             }
         }
         __syncthreads();
+        b0 += (uint32_t)a.wpb;
     }
 }
 
@@ -2581,7 +2612,16 @@ hipError_t launch_decode_bs(BatchArgs a, int matrix, hipStream_t s) {
     LaunchPlan p{};
     p.wpb = a.wpb;
     p.lds_bytes = (uint32_t)(a.wpb * sizeof(BsdRegion)) + (((uint32_t)(a.k * a.r) + 15u) & ~15u);
-    const uint64_t groups = (a.nwin + a.wpb - 1) / a.wpb;
+    // flagged windows: ranges of 64..256 windows, about two per resident
+    // workgroup (one all-flagged range is ~8 groups of a.wpb)
+    if (a.bsd_flag) {
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint64_t per = (a.nwin + 4ull * cus - 1) / (4ull * cus);
+        a.bsd_range = (int)std::min<uint64_t>(kBlock, std::max<uint64_t>(64, (per + 63) / 64 * 64));
+    }
+    const uint64_t groups = a.bsd_flag ? (a.nwin + a.bsd_range - 1) / a.bsd_range : (a.nwin + a.wpb - 1) / a.wpb;
     const auto go = [&](auto kernel) -> hipError_t {
         if (p.lds_bytes > 64u * 1024u) {
             const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
@@ -2600,7 +2640,7 @@ hipError_t launch_decode_bs(BatchArgs a, int matrix, hipStream_t s) {
 #undef BSD_LAUNCH
 #undef BSD_LAUNCH_M
     }
-    if (!a.enc_bs || a.bsd_list) return hipErrorInvalidValue;  // the runtime-mask kernel: consecutive windows
+    if (!a.enc_bs || a.bsd_flag) return hipErrorInvalidValue;  // the runtime-mask kernel: consecutive windows
     switch (a.r) {
         case 4: return go(gf_decode_bs_kernel<0, 4, 0, true>);
         case 5: return go(gf_decode_bs_kernel<0, 5, 0, true>);

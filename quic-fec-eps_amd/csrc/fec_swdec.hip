@@ -573,6 +573,7 @@ constexpr int kPlanPer = kPlanChunk / kBlock;  // sources per thread
 constexpr int kPlanHalo = 256;                 // >= kSwMaxWindow
 static_assert(kPlanPer == 8, "the per-thread source loads are 8 bytes");
 constexpr uint32_t kLbAgg = 1u, kLbInc = 2u;
+constexpr int kPlanHdr = 512;  // headers cached per chunk (cfg7: 288 from tb to t1)
 
 // lost sources, max reach, repairs, widest window | error bits << 16, and the
 // reach at the last lost source (prefix max of reach up to it: its reachL)
@@ -668,6 +669,11 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     __shared__ uint32_t s_wpfx[(kPlanChunk + kPlanHalo) / 32 + 1];  // lost before each word
     __shared__ uint32_t s_c[kBlock / 64], s_m[kBlock / 64], s_r[kBlock / 64], s_w[kBlock / 64];
     __shared__ uint32_t s_lh[kBlock / 64], s_lv[kBlock / 64];
+    // the headers [tb, tb + kPlanHdr) and their arrival flags, cached by the
+    // reach pass for the row draws and pivot searches (one global round trip
+    // less each; later headers are read from global memory)
+    __shared__ fecgpu_sw_repair s_hc[kPlanHdr];
+    __shared__ uint8_t s_hp[kPlanHdr];
     __shared__ uint32_t s_chunk, s_bad, s_wmb;
     __shared__ uint32_t s_nst, s_nsg, s_stbase;  // the chunk's larger-system starts, singles recovered
     __shared__ uint64_t s_t0, s_t1, s_tb;
@@ -780,7 +786,12 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     for (uint64_t t = tb + tid; t < t1; t += kBlock) {
         if (!SWC(t, a.nrep, kChkSynJob)) break;
         const fecgpu_sw_repair h = a.hdr[t];
-        const bool rp = a.rep_present[t] != 0;
+        const uint8_t rpb = a.rep_present[t];
+        const bool rp = rpb != 0;
+        if (t - tb < (uint64_t)kPlanHdr) {
+            s_hc[t - tb] = h;
+            s_hp[t - tb] = rpb;
+        }
         if (t >= t0) {
             a.syn_jobs[t] = E0;
             bad |= !hdr_ok(h, a.nsrc);
@@ -1014,9 +1025,16 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         const auto before = [&](uint32_t j) {  // lost sources in [i0, i0 + j), j <= chunk + halo
             return s_wpfx[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u));
         };
+        // the cached header / arrival flag of repair t (tb <= t < t1)
+        const auto hdr_at = [&](uint64_t t) -> fecgpu_sw_repair {
+            return t - tb < (uint64_t)kPlanHdr ? s_hc[t - tb] : a.hdr[t];
+        };
+        const auto rp_at = [&](uint64_t t) -> uint8_t {
+            return t - tb < (uint64_t)kPlanHdr ? s_hp[t - tb] : a.rep_present[t];
+        };
         for (uint64_t t = t0 + (tid - 64); t < t1; t += kBlock - 64) {
-            if (!a.rep_present[t]) continue;
-            const fecgpu_sw_repair h = a.hdr[t];
+            if (!rp_at(t)) continue;
+            const fecgpu_sw_repair h = hdr_at(t);
             if (h.fss < i0 || h.fss >= i1 || !hdr_ok(h, a.nsrc)) continue;
             const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
             if (before(hi) > before(lo)) draw_row(a, t, h);
@@ -1038,8 +1056,8 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                 // void anyway, but no read may leave the arrays)
                 const uint64_t ta = max(rfirst(lo), tb), te = min(rfirst(i + 1), t1);
                 for (uint64_t t = ta; t < te; t++) {
-                    const uint8_t rpt = a.rep_present[t];  // both loads in one round trip
-                    const fecgpu_sw_repair h = a.hdr[t];
+                    const uint8_t rpt = rp_at(t);  // (ta >= tb)
+                    const fecgpu_sw_repair h = hdr_at(t);
                     if (!rpt || !hdr_ok(h, a.nsrc)) continue;
                     if (h.fss > i || h.fss + h.nss <= i) continue;
                     const uint32_t j = (uint32_t)(i - h.fss);
@@ -1876,6 +1894,10 @@ hipError_t launch_rlc_table(uint8_t *tab, hipStream_t s) {
 hipError_t launch_sw_dec_plan(const SwDecArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(sw_dec_plan_kernel, dim3((unsigned)((a.nsrc + kPlanChunk - 1) / kPlanChunk)), dim3(kBlock), 0, s,
                        a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sw_dec_sys(const SwDecArgs &a, hipStream_t s) {
     if (a.nrep) {
         // a wave per lost source at most; persistent beyond what fits the chip
         // (two shared mid regions, ~30 KB per block with the tiny ones: 3 per CU)
