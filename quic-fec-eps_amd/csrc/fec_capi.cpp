@@ -171,13 +171,6 @@ struct fecgpu_ctx {
     // sliding-window calls: device scratch slots and the last call's end event, per device
     std::map<int, std::vector<std::pair<void *, size_t>>> sw_scratch;
     std::map<int, hipEvent_t> sw_event;
-    // ctx_sw_fork: per device a second stream and its fork / join events
-    struct SwFork {
-        hipStream_t st = nullptr;
-        hipEvent_t fork = nullptr, join = nullptr;
-    };
-    std::map<int, SwFork> sw_fork;
-    int sw_fork_on = 1;  // tuning "sw_fork": the decode's one-unknown syndromes beside the systems
     std::map<int, SwSticky *> sw_sticky;  // asynchronous decodes' error flags, per device
     std::map<int, ChkRec *> chk_rec;      // FECGPU_CHECK builds: the index-checking kernels' fault record
     struct LbState {
@@ -359,11 +352,6 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         ctx->sw_stream = (int)value;  // calls and objects created from now on
         return 0;
     }
-    if (!std::strcmp(key, "sw_fork")) {
-        if (value < 0 || value > 1) return FECGPU_ERR_INVALID_ARG;
-        ctx->sw_fork_on = (int)value;
-        return 0;
-    }
     if (!std::strcmp(key, "sw_long_min")) {
         if (value < 1 || value > (1 << 30)) return FECGPU_ERR_INVALID_ARG;
         ctx->sw_long_min = (int)value;
@@ -433,13 +421,6 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
     for (auto &kv : ctx->sw_event) {
         (void)hipSetDevice(kv.first);
         (void)hipEventDestroy(kv.second);
-    }
-    for (auto &kv : ctx->sw_fork) {
-        (void)hipSetDevice(kv.first);
-        (void)hipStreamSynchronize(kv.second.st);
-        (void)hipStreamDestroy(kv.second.st);
-        (void)hipEventDestroy(kv.second.fork);
-        (void)hipEventDestroy(kv.second.join);
     }
     for (auto &kv : ctx->conn_streams) {
         (void)hipSetDevice(kv.first);
@@ -552,13 +533,23 @@ ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out)
 }
 
 // Bit-sliced decode: windows per group for windows of ncol 16-B columns in
-// units of `cols` columns, >= 8 passes of the workgroup at the longest window,
-// the groups' plan regions and the parity rows (kr bytes) within 40 KB of LDS.
-int bsd_wpb(uint32_t ncol, uint32_t cols, int kr) {
+// units of `cols` columns, their regions within 40 KB of LDS: the largest
+// group whose passes of the workgroup are >= 97 % full, else the largest of
+// the fullest (k120 at 1200 B, 19 units per window: 26 windows, 494 units).
+int bsd_wpb(uint32_t ncol, uint32_t cols) {
     const uint32_t units = std::max<uint32_t>(1, (ncol + cols - 1) / cols);
-    const int want = (int)((8u * kBlock + units - 1) / units);
-    const int cap = (int)(((40u << 10) - (((uint32_t)kr + 15u) & ~15u)) / sizeof(BsdRegion));
-    return std::max(1, std::min({want, cap, kMaxWpb}));
+    const int cap = std::min<int>(kMaxWpb, (int)((40u << 10) / sizeof(BsdRegion)));
+    int best = 1;
+    double best_u = 0.0;
+    for (int w = 1; w <= cap; w++) {
+        const uint64_t n = (uint64_t)w * units, passes = (n + kBlock - 1) / kBlock;
+        const double u = (double)n / (double)(passes * kBlock);
+        if (u >= 0.97 || u >= best_u - 1e-9) {  // ties: the larger group
+            best = w;
+            best_u = std::max(best_u, u);
+        }
+    }
+    return best;
 }
 
 // Windows per workgroup: fill the 256 lanes with whole passes over the
@@ -753,7 +744,11 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
         a.nw = (n + 63) / 64;
         a.prows = P;
         a.enc_bs = mPI;  // [P | I]: the pivot repairs add themselves to their syndromes
-        a.wpb = bsd_wpb(ncol, kRbsCols, k * r);
+        void *rp = nullptr;
+        rc = ctx_sw_scratch(ctx, 11, nwin * sizeof(BsdRec), &rp);
+        if (rc) return rc;
+        a.bsd_rec = static_cast<BsdRec *>(rp);
+        a.wpb = bsd_wpb(ncol, kRbsCols);
         a.chk.lo[0] = reinterpret_cast<uint64_t>(win);
         a.chk.n[0] = nwin * a.wpitch;
         HIP_TRY(launch_decode_bs(a, (int)code->matrix, s), "wide bit-sliced decode launch");
@@ -966,10 +961,11 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
             if (ctx->bsd_min_e > 0 && ctx->bitslice && !remote && !win_off && !a.out_delta &&
                 r >= ctx->bsd_min_e && bitslice_supported(k, r, (int)code->matrix)) {
                 a.bsd_min_e = ctx->bsd_min_e;
+                a.bsd_cauchy = code->matrix == FECGPU_MATRIX_CAUCHY;
                 a.prows = t.rows;
                 a.nw = 1;
                 p.matrix = (int)code->matrix;
-                p.bsd_wpb = bsd_wpb(ncol ? ncol : stride >> 4, 2, k * r);
+                p.bsd_wpb = bsd_wpb(ncol ? ncol : stride >> 4, 2);
             }
             p.win_lds = gf_dec_win_lds(k, r);
             p.wpb = choose_wpb(ncol, p.win_lds, 40 * 1024);
@@ -1035,9 +1031,11 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         rc = ctx_sw_begin(ctx, s);
         if (rc) return rc;
         void *lp = nullptr;
-        rc = ctx_sw_scratch(ctx, 12, a.nwin, &lp);
+        const size_t o_rec = (a.nwin + 255) & ~size_t(255);
+        rc = ctx_sw_scratch(ctx, 12, o_rec + a.nwin * sizeof(BsdRec), &lp);
         if (rc) return rc;
         a.bsd_flag = static_cast<uint8_t *>(lp);  // every window's written by the table decode's plan
+        a.bsd_rec = reinterpret_cast<BsdRec *>(static_cast<uint8_t *>(lp) + o_rec);  // the routed windows' plans
     }
     hipError_t e = decode ? launch_decode(scheme, a, p, s) : launch_encode(scheme, a, p, s);
     if (e != hipSuccess) return dev_err(e, decode ? "decode launch" : "encode launch");
@@ -1435,33 +1433,6 @@ ssize_t ctx_sw_end(fecgpu_ctx *ctx, hipStream_t s) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
     HIP_TRY(hipEventRecord(ctx->sw_event[dev], s), "hipEventRecord");
-    return 0;
-}
-
-ssize_t ctx_sw_fork(fecgpu_ctx *ctx, hipStream_t s, hipStream_t *s2) {
-    *s2 = nullptr;
-    if (!ctx->sw_fork_on) return 0;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    fecgpu_ctx::SwFork &f = ctx->sw_fork[dev];
-    if (!f.st) {
-        HIP_TRY(hipStreamCreateWithFlags(&f.st, hipStreamNonBlocking), "hipStreamCreate");
-        HIP_TRY(hipEventCreateWithFlags(&f.fork, hipEventDisableTiming), "hipEventCreate");
-        HIP_TRY(hipEventCreateWithFlags(&f.join, hipEventDisableTiming), "hipEventCreate");
-    }
-    HIP_TRY(hipEventRecord(f.fork, s), "hipEventRecord");
-    HIP_TRY(hipStreamWaitEvent(f.st, f.fork, 0), "hipStreamWaitEvent");
-    *s2 = f.st;
-    return 0;
-}
-
-ssize_t ctx_sw_join(fecgpu_ctx *ctx, hipStream_t s, hipStream_t s2) {
-    if (!s2) return 0;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    fecgpu_ctx::SwFork &f = ctx->sw_fork[dev];
-    HIP_TRY(hipEventRecord(f.join, s2), "hipEventRecord");
-    HIP_TRY(hipStreamWaitEvent(s, f.join, 0), "hipStreamWaitEvent");
     return 0;
 }
 

@@ -94,12 +94,26 @@ struct BatchArgs {
     // window (the wide codes).  nw: present-mask words per window (1, or
     // ceil((k + r) / 64) for the wide codes).
     const uint8_t *prows;
+    struct BsdRec *bsd_rec;  // the windows' plans (indexed by window)
     uint8_t *bsd_flag;
     int bsd_range;  // flagged windows: windows per range (launch_decode_bs)
     int bsd_min_e;
     int nw;
     int bsd_cauchy;  // prows are the Cauchy rows (A.2): the closed-form plan
 };
+
+// A window's plan for the bit-sliced decode (global memory, written by the
+// table decode's plan for the windows it routes, or by gf_decode_bs_plan_kernel
+// for the wide codes; read into a BsdRegion): C[u][i] (u * 8 + i), the present
+// words, the missing rows, e (0: nothing to do), the repairs read, the alt row.
+struct BsdRec {
+    uint8_t c[kMaxR * kMaxR];
+    uint64_t pw[4];
+    uint8_t m[kMaxR];
+    uint32_t ne, used, alt, pad;
+    uint8_t pad2[8];
+};
+static_assert(sizeof(BsdRec) == 128, "plan records are 128 B");
 
 // Per-window LDS region of the bit-sliced decode (fec_kernels.hip
 // gf_decode_bs_kernel): the window's stage-2 tables C[u][i] (missing source u
@@ -557,10 +571,5 @@ ssize_t ctx_rlc_table(fecgpu_ctx *ctx, hipStream_t s, const uint8_t **tab);
 ssize_t ctx_sw_wait(fecgpu_ctx *ctx);
 ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);
 ssize_t ctx_sw_end(fecgpu_ctx *ctx, hipStream_t s);
-// A second stream of the current device for work of one call that runs
-// beside the rest: fork = *s2 waits for what `s` holds so far (nullptr when
-// the ctx's "sw_fork" tuning is 0); join = `s` waits for what *s2 holds.
-ssize_t ctx_sw_fork(fecgpu_ctx *ctx, hipStream_t s, hipStream_t *s2);
-ssize_t ctx_sw_join(fecgpu_ctx *ctx, hipStream_t s, hipStream_t s2);
 
 }  // namespace fecgpu

@@ -1024,13 +1024,21 @@ __device__ __forceinline__ void plan_offsets(const BatchArgs &a, uint64_t w, int
 // below, launched after this kernel over the flags): e >= a.bsd_min_e (0:
 // off).  The window's status is that kernel's to write.  (Lane 0 of the
 // planning wave cleared the flag before the plan: same lane, same address.)
+// ne_out = kBsdRouted tells the kernel to write the window's bit-sliced plan.
+constexpr uint8_t kBsdRouted = 0xFF;
 __device__ __forceinline__ bool bsd_route(const BatchArgs &a, uint64_t w, int e, int lane, uint8_t &ne_out) {
     if (!a.bsd_min_e || e < a.bsd_min_e) return false;
     if (lane == 0) {
-        ne_out = 0;
+        ne_out = kBsdRouted;
         a.bsd_flag[w] = 1;
     }
     return true;
+}
+namespace bsd {
+// (inlined into the table decode's R = 8 kernel only: 156 -> 167 VGPRs, still
+// 3 waves per SIMD; as a call it took 336 B of scratch per lane)
+__device__ void plan(const BatchArgs &a, uint64_t w, int lane, uint8_t *ms, BsdRec *out, const uint8_t *ex,
+                     const uint8_t *lg, const uint8_t *P);
 }
 
 // GF plan (a6/a7) by one wave, closed form.  Missing sources m_0..m_{e-1},
@@ -1341,6 +1349,17 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
                 else
                     plan_gf<R>(a, w0 + wl, pw, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log,
                                s_ne[wl]);
+                // routed (codes with compiled plane masks: r = 8): its bit-sliced
+                // plan instead (the region is scratch)
+                if constexpr (R == kMaxR) if (a.bsd_min_e) {
+                    WAVE_SYNC();
+                    if (s_ne[wl] == kBsdRouted) {
+                        bsd::plan(a, w0 + wl, lane, regions + (size_t)wl * a.win_lds, a.bsd_rec + w0 + wl, s_exp,
+                                  s_log, s_coef);
+                        WAVE_SYNC();
+                        if (lane == 0) s_ne[wl] = 0;
+                    }
+                }
             }
         }
         __syncthreads();
@@ -1402,10 +1421,11 @@ namespace bsd {
 
 constexpr int kRsrcRaw = 0x00020000;  // buffer resource word 3: raw 32-bit data (gfx9)
 
-// One wave: the plan of window w into rg (status too).  pw: the window's
-// present words; P: parity rows [r][k] in LDS.
-__device__ void plan(const BatchArgs &a, uint64_t w, int lane, BsdRegion &rg, const uint8_t *ex, const uint8_t *lg,
-                     const uint8_t *P) {
+// One wave: the plan of window w into its record (status too).  ms: 8 bytes
+// of LDS for the missing rows; P: parity rows [r][k] in LDS (unused for the
+// Cauchy rows, a.bsd_cauchy).
+__device__ void plan(const BatchArgs &a, uint64_t w, int lane, uint8_t *ms, BsdRec *out, const uint8_t *ex,
+                     const uint8_t *lg, const uint8_t *P) {
     const int k = a.k, r = a.r, nw = a.nw;
     const uint64_t pl = lane < nw ? a.present[w * (uint64_t)nw + lane] : 0ull;
     uint64_t pw[4];
@@ -1424,7 +1444,7 @@ __device__ void plan(const BatchArgs &a, uint64_t w, int lane, BsdRegion &rg, co
         const bool in = i < k, miss = in && !bit(i);
         const uint64_t b = __ballot(miss), h = __ballot(in && !miss);
         const int pos = e + __popcll(b & ((1ull << lane) - 1ull));
-        if (miss && pos < kMaxR) rg.m[pos] = (uint8_t)i;
+        if (miss && pos < kMaxR) ms[pos] = (uint8_t)i;
         e += __popcll(b);
         if (first < 0 && h) first = c0 + __ffsll((unsigned long long)h) - 1;
     }
@@ -1432,17 +1452,17 @@ __device__ void plan(const BatchArgs &a, uint64_t w, int lane, BsdRegion &rg, co
     const int np = __popcll(rep);
     if (e == 0 || e > r || np < e) {
         if (lane == 0) {
-            rg.ne = 0;
+            out->ne = 0;
             a.status[w] = e == 0 ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
         }
         return;
     }
     WAVE_SYNC();
+    uint32_t v = 0, ub = 0;  // this lane's C[u][i] (lane = u * 8 + i); the repairs read
     if (a.bsd_cauchy) {
         // Cauchy rows: the first e present repairs, and C in closed form (as
-        // plan_gf: log C[u][i] = A_u + K_i - log(x_i ^ m_u), x_i = k + i), lane
-        // u * 8 + i, independent LDS lookups instead of the elimination chain
-        uint32_t ub = 0;
+        // plan_gf: log C[u][i] = A_u + K_i - log(x_i ^ m_u), x_i = k + i),
+        // independent LDS lookups instead of the elimination chain
         {
             uint32_t rb = rep;
             for (int c = 0; c < e; c++) {
@@ -1451,89 +1471,91 @@ __device__ void plan(const BatchArgs &a, uint64_t w, int lane, BsdRegion &rg, co
             }
         }
         const int u = lane >> 3, i = lane & 7;
-        uint32_t v = 0;
         if (u < e && ((ub >> i) & 1u)) {
-            const int mu = rg.m[u], x = k + i;
+            const int mu = ms[u], x = k + i;
             int L = 255 * 32 - (int)lg[x ^ mu];
             for (uint32_t b = ub; b; b &= b - 1) {
                 const int xt = k + __ffs(b) - 1;
                 L += (int)lg[xt ^ mu] - (xt != x ? (int)lg[xt ^ x] : 0);
             }
             for (int q = 0; q < e; q++) {
-                const int mv = rg.m[q];
+                const int mv = ms[q];
                 L += (int)lg[x ^ mv] - (q != u ? (int)lg[mu ^ mv] : 0);
             }
             v = ex[L % 255];
         }
-        const CoefTab ct = make_coef_tab(v);
-        rg.ab[lane] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
-        rg.tc[lane] = ct.c;
-        if (lane < 4) rg.pw[lane] = lane == 0 ? pw[0] : lane == 1 ? pw[1] : lane == 2 ? pw[2] : pw[3];
-        if (lane == 0) {
-            rg.ne = (uint32_t)e;
-            rg.used = ub;
-            rg.alt = first >= 0 ? (uint32_t)first : (uint32_t)(k + __ffs(ub) - 1);
-            a.status[w] = FECGPU_STATUS_OK;
-        }
-        return;
-    }
-    uint32_t rr = rep;
-    for (int i = 0; i < lane && i < 8; i++) rr &= rr - 1;
-    const int my_sel = rr ? __ffs(rr) - 1 : 0;  // lane t < np: the t-th present repair
-    // [A | I], lane = t * 8 + u; every __shfl and ballot with the whole wave active
-    const int t = lane >> 3, u = lane & 7;
-    const int sel_t = __shfl(my_sel, t, 64);
-    const int m_u = u < e ? (int)rg.m[u] : 0;
-    const bool row = t < np;
-    uint32_t xl = (row && u < e) ? P[sel_t * k + m_u] : 0u;
-    uint32_t xr = (row && t == u) ? 1u : 0u;
-    uint32_t used = 0;  // rows already pivots (wave-uniform)
-    int my_piv = 0;     // lane c < e: pivot row of column c
-    for (int c = 0; c < e; c++) {
-        const uint64_t cand = __ballot(row && u == c && !((used >> t) & 1u) && xl != 0);
-        if (!cand) {  // rank < e (random linear codes): the window stays lost
-            if (lane == 0) {
-                rg.ne = 0;
-                a.status[w] = FECGPU_STATUS_UNRECOVERABLE;
+    } else {
+        uint32_t rr = rep;
+        for (int i = 0; i < lane && i < 8; i++) rr &= rr - 1;
+        const int my_sel = rr ? __ffs(rr) - 1 : 0;  // lane t < np: the t-th present repair
+        // [A | I], lane = t * 8 + u; every __shfl and ballot with the whole wave active
+        const int t = lane >> 3, u = lane & 7;
+        const int sel_t = __shfl(my_sel, t, 64);
+        const int m_u = u < e ? (int)ms[u] : 0;
+        const bool row = t < np;
+        uint32_t xl = (row && u < e) ? P[sel_t * k + m_u] : 0u;
+        uint32_t xr = (row && t == u) ? 1u : 0u;
+        uint32_t used = 0;  // rows already pivots (wave-uniform)
+        int my_piv = 0;     // lane c < e: pivot row of column c
+        for (int c = 0; c < e; c++) {
+            const uint64_t cand = __ballot(row && u == c && !((used >> t) & 1u) && xl != 0);
+            if (!cand) {  // rank < e (random linear codes): the window stays lost
+                if (lane == 0) {
+                    out->ne = 0;
+                    a.status[w] = FECGPU_STATUS_UNRECOVERABLE;
+                }
+                return;
             }
-            return;
+            const int pr = (int)(__ffsll((unsigned long long)cand) - 1) >> 3;
+            used |= 1u << pr;
+            if (lane == c) my_piv = pr;
+            const uint32_t ip = gf_inv_lds(ex, lg, __shfl(xl, pr * 8 + c, 64));
+            if (t == pr) {
+                xl = gf_mul_lds(ex, lg, xl, ip);
+                xr = gf_mul_lds(ex, lg, xr, ip);
+            }
+            const uint32_t f = __shfl(xl, t * 8 + c, 64);
+            const uint32_t rl = __shfl(xl, pr * 8 + u, 64);
+            const uint32_t rq = __shfl(xr, pr * 8 + u, 64);
+            if (t != pr && row) {
+                xl ^= gf_mul_lds(ex, lg, f, rl);
+                xr ^= gf_mul_lds(ex, lg, f, rq);
+            }
         }
-        const int pr = (int)(__ffsll((unsigned long long)cand) - 1) >> 3;
-        used |= 1u << pr;
-        if (lane == c) my_piv = pr;
-        const uint32_t ip = gf_inv_lds(ex, lg, __shfl(xl, pr * 8 + c, 64));
-        if (t == pr) {
-            xl = gf_mul_lds(ex, lg, xl, ip);
-            xr = gf_mul_lds(ex, lg, xr, ip);
+        // C[u][i], lane = u * 8 + i: T[P_u][c] where repair i is pivot row c's, else 0
+        const int cu = lane >> 3, ci = lane & 7;
+        const int pu = __shfl(my_piv, min(cu, e - 1), 64);
+        for (int c = 0; c < e; c++) {
+            const int pc = __shfl(my_piv, c, 64);
+            const uint32_t tv = __shfl(xr, (pu * 8 + pc) & 63, 64);
+            const int sc = __shfl(my_sel, pc, 64);  // the repair of pivot row pc
+            ub |= 1u << sc;
+            if (sc == ci) v = tv;
         }
-        const uint32_t f = __shfl(xl, t * 8 + c, 64);
-        const uint32_t rl = __shfl(xl, pr * 8 + u, 64);
-        const uint32_t rq = __shfl(xr, pr * 8 + u, 64);
-        if (t != pr && row) {
-            xl ^= gf_mul_lds(ex, lg, f, rl);
-            xr ^= gf_mul_lds(ex, lg, f, rq);
-        }
+        if (cu >= e) v = 0;
     }
-    // C[u][i], lane = u * 8 + i: T[P_u][c] where repair i is pivot row c's, else 0
-    const int cu = lane >> 3, ci = lane & 7;
-    const int pu = __shfl(my_piv, min(cu, e - 1), 64);
-    uint32_t v = 0, ub = 0;
-    for (int c = 0; c < e; c++) {
-        const int pc = __shfl(my_piv, c, 64);
-        const uint32_t tv = __shfl(xr, (pu * 8 + pc) & 63, 64);
-        const int sc = __shfl(my_sel, pc, 64);  // the repair of pivot row pc
-        ub |= 1u << sc;
-        if (sc == ci) v = tv;
+    out->c[lane] = (uint8_t)v;
+    if (lane < 4) out->pw[lane] = lane == 0 ? pw[0] : lane == 1 ? pw[1] : lane == 2 ? pw[2] : pw[3];
+    if (lane < kMaxR) out->m[lane] = lane < e ? ms[lane] : 0;
+    if (lane == 0) {
+        out->ne = (uint32_t)e;
+        out->used = ub;
+        out->alt = first >= 0 ? (uint32_t)first : (uint32_t)(k + __ffs(ub) - 1);
+        a.status[w] = FECGPU_STATUS_OK;
     }
-    const CoefTab ct = make_coef_tab(cu < e ? v : 0u);
+}
+
+// A window's record into its LDS region (one wave; the stage-2 multiply tables)
+__device__ __forceinline__ void load_rec(const BsdRec &rc, BsdRegion &rg, int lane) {
+    const CoefTab ct = make_coef_tab(rc.c[lane]);
     rg.ab[lane] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
     rg.tc[lane] = ct.c;
-    if (lane < 4) rg.pw[lane] = lane == 0 ? pw[0] : lane == 1 ? pw[1] : lane == 2 ? pw[2] : pw[3];
+    if (lane < 4) rg.pw[lane] = rc.pw[lane];
+    if (lane < kMaxR) rg.m[lane] = rc.m[lane];
     if (lane == 0) {
-        rg.ne = (uint32_t)e;
-        rg.used = ub;
-        rg.alt = first >= 0 ? (uint32_t)first : (uint32_t)(k + __ffs(ub) - 1);
-        a.status[w] = FECGPU_STATUS_OK;
+        rg.ne = rc.ne;
+        rg.used = rc.used;
+        rg.alt = rc.alt;
     }
 }
 
@@ -1731,19 +1753,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8)))
 void gf_decode_bs_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
     extern __shared__ uint4 dyn[];
-    __shared__ uint8_t s_exp[512];
-    __shared__ uint8_t s_log[256];
     __shared__ GroupLds g;
     __shared__ uint32_t s_w[kMaxWpb];
     __shared__ uint8_t s_perm[kMaxWpb];
     __shared__ uint16_t s_list[kBlock];
     __shared__ uint32_t s_cnt[kBlock / 64];
     BsdRegion *rgn = reinterpret_cast<BsdRegion *>(dyn);
-    uint8_t *s_P = reinterpret_cast<uint8_t *>(rgn + a.wpb);  // parity rows [r][k]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
-    for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
-    for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
-    for (int i = tid; i < a.r * k; i += kBlock) s_P[i] = a.prows[i];
     constexpr uint32_t C = RT ? kRbsCols : 2;  // columns per unit
     // flagged windows: ranges of kBlock windows in batch order, their flagged
     // ones listed in LDS and taken a.wpb at a time; else groups of a.wpb
@@ -1794,7 +1810,7 @@ void gf_decode_bs_kernel(BatchArgs a) {
             g.ncol[tid] = (S + 15u) >> 4;
         }
         __syncthreads();
-        for (int wl = wave; wl < nb; wl += kBlock / 64) bsd::plan(a, s_w[wl], lane, rgn[wl], s_exp, s_log, s_P);
+        for (int wl = wave; wl < nb; wl += kBlock / 64) bsd::load_rec(a.bsd_rec[s_w[wl]], rgn[wl], lane);
         __syncthreads();
         if (tid < 64) {  // descending e (ties by index), then unit prefix sums in that order
             const int t = tid;
@@ -1852,6 +1868,22 @@ void gf_decode_bs_kernel(BatchArgs a) {
         __syncthreads();
         b0 += (uint32_t)a.wpb;
     }
+}
+
+// The wide codes' plans: a wave per window into a.bsd_rec (statuses too).
+__global__ __launch_bounds__(kBlock) void gf_decode_bs_plan_kernel(BatchArgs a) {
+    extern __shared__ uint8_t s_P[];  // parity rows [r][k]
+    __shared__ uint8_t s_exp[512];
+    __shared__ uint8_t s_log[256];
+    __shared__ uint8_t s_m[kBlock / 64][kMaxR];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
+    for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
+    if (!a.bsd_cauchy)
+        for (int i = tid; i < a.r * a.k; i += kBlock) s_P[i] = a.prows[i];
+    __syncthreads();
+    const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+    if (w < a.nwin) bsd::plan(a, w, lane, s_m[wave], a.bsd_rec + w, s_exp, s_log, s_P);
 }
 
 // ========================================================= workloads ===
@@ -2601,17 +2633,24 @@ hipError_t launch_gf_decode_table(const BatchArgs &a, const LaunchPlan &p, hipSt
 }
 }  // namespace
 
-// The bit-sliced decode over a.bsd_list (*a.bsd_count windows) or, without a
-// list, every window; a.wpb windows per group, persistent grid.  Compiled
-// masks when the code has them (matrix: fecgpu_matrix), else runtime ones
-// (a.enc_bs).
+// The bit-sliced decode over the flagged windows (a.bsd_flag, planned by the
+// table decode) or, without flags, every window (planned here first); a.wpb
+// windows per group, persistent grid.  Compiled masks when the code has them
+// (matrix: fecgpu_matrix), else runtime ones (a.enc_bs).
 hipError_t launch_decode_bs(BatchArgs a, int matrix, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     if (a.r < 4 || a.r > kMaxR || !a.prows) return hipErrorInvalidValue;
     a.bsd_cauchy = matrix == FECGPU_MATRIX_CAUCHY;
+    if (!a.bsd_rec) return hipErrorInvalidValue;
+    if (!a.bsd_flag) {  // the wide codes: every window's plan first (the routed ones are planned by the table decode)
+        hipLaunchKernelGGL(gf_decode_bs_plan_kernel, dim3((unsigned)((a.nwin + kBlock / 64 - 1) / (kBlock / 64))),
+                           dim3(kBlock), a.bsd_cauchy ? 0 : (size_t)a.k * a.r, s, a);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     LaunchPlan p{};
     p.wpb = a.wpb;
-    p.lds_bytes = (uint32_t)(a.wpb * sizeof(BsdRegion)) + (((uint32_t)(a.k * a.r) + 15u) & ~15u);
+    p.lds_bytes = (uint32_t)(a.wpb * sizeof(BsdRegion));
     // flagged windows: ranges of 64..256 windows, about two per resident
     // workgroup (one all-flagged range is ~8 groups of a.wpb)
     if (a.bsd_flag) {

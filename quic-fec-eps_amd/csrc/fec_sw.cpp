@@ -345,12 +345,9 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
         a.lb_ticket = lb.ticket;
     }
     SW_TRY(launch_sw_dec_plan(a, s), "sliding-window decode plan launch");
-    // The one-unknown systems the plan solved (their syndrome jobs output the
-    // lost rows) touch nothing the larger systems read or write, so their
-    // syndrome launch runs on a second stream beside the systems, long,
-    // syndrome and solve launches and joins before the call ends
-    hipStream_t s2 = nullptr;
-    RC_TRY(ctx_sw_fork(ctx, s, &s2));
+    // (the one-unknown systems' syndromes on a second stream beside the
+    // systems launch, joined at the end, measured 0.209 vs 0.197 ms per cfg7
+    // call, r05: removed)
     SW_TRY(launch_sw_dec_sys(a, s), "sliding-window decode systems launch");
     SW_TRY(launch_sw_dec_long(a, s), "sliding-window long-system plan launch");
     const uint32_t ncol = (S + 15u) >> 4;
@@ -387,14 +384,6 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     range(sa, 1, rep, nrep * stride);
     range(sa, 2, psyn, nrep * stride);
     sa.budget = ncol >= 64 ? kCombBudgetWide : kCombBudget;
-    if (s2) {
-        CombArgs one = sa;  // slots nrep .. nrep + nlost: the plan's one-unknown systems
-        one.jobs = a.syn_jobs + nrep;
-        one.njobs = 0;
-        SW_TRY(launch_comb(one, 1, s2), "sliding-window one-unknown syndrome launch");
-        sa.extra = nullptr;  // the repairs' slots: the larger systems' syndromes
-        sa.extra_max = 0;
-    }
     SW_TRY(launch_comb(sa, 1, s), "sliding-window syndrome launch");
     CombArgs va = sa;
     va.jobs = a.sol_jobs;
@@ -415,7 +404,6 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     va.budget = kSolveBudget;
     SW_TRY(launch_comb(va, kSwSolveOut, s), "sliding-window solve launch");
     SW_TRY(launch_sw_dec_replay(a, s), "sliding-window long-system replay launch");
-    RC_TRY(ctx_sw_join(ctx, s, s2));
     if (ctr_out) SW_TRY(hipMemcpyAsync(ctr_out, a.ctr, sizeof(SwDecCtr), hipMemcpyDeviceToHost, s), "D2H sw counters");
     return 0;
 }

@@ -654,7 +654,7 @@ __device__ __forceinline__ uint8_t coef_at(const SwDecArgs &a, const fecgpu_sw_r
 #endif
 __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
 #if FECGPU_SWD_TRACE
-    __shared__ unsigned long long s_tr[12];
+    __shared__ unsigned long long s_tr[16];
     if (threadIdx.x == 0) s_tr[0] = wall_clock64();
 #endif
     __shared__ uint32_t s_reach[kPlanChunk], s_rcnt[kPlanChunk];
@@ -1039,6 +1039,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
             if (before(hi) > before(lo)) draw_row(a, t, h);
         }
+#if FECGPU_SWD_TRACE
+        if (tid == 64) s_tr[12] = wall_clock64();  // wave 1: its row draws issued
+#endif
         for (uint32_t k = tid - 64; k < nl; k += kBlock - 64) {
             uint32_t pt = ~0u, pw = 0, pc = 0;
             const uint32_t pos = s_lpos[k];
@@ -1072,6 +1075,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             s_pv[k] = make_uint2(pt, pw);
             s_pcd[k] = (uint16_t)pc;
         }
+#if FECGPU_SWD_TRACE
+        if (tid == 64) s_tr[13] = wall_clock64();  // wave 1: its pivots found
+#endif
     }
     __syncthreads();
     SWD_TRACE(7);
@@ -1226,6 +1232,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                s_tr[1] - s_tr[0], s_tr[2] - s_tr[0], s_tr[3] - s_tr[0], s_tr[4] - s_tr[0], s_tr[5] - s_tr[0],
                s_tr[6] - s_tr[0], s_tr[7] - s_tr[0], s_tr[8] - s_tr[0], s_tr[9] - s_tr[0], s_tr[10] - s_tr[0],
                t11 - s_tr[0], s_tr[0]);
+        printf("swd plan chunk %u: wave 1 draws %llu pivots %llu\n", s_chunk, s_tr[12] - s_tr[0], s_tr[13] - s_tr[0]);
     }
 #endif
 }

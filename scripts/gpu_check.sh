@@ -194,17 +194,6 @@ for s in "$@"; do
                 BSD_MIN_E=$m step profbsd_$m 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profbsd_$m -o run -- \
                     python scripts/code_sweep.py shape=gf256-cauchy-32-8
             done ;;
-        abfork)  # cfg7: one-unknown syndromes on a second stream (1) or not (0), interleaved 3 times
-            for rep in 1 2 3; do
-                for f in 1 0; do
-                    step abfork_${f}_$rep 300 python bench.py --config 7 --steps 50 --warmup 10 --cpu-seconds 0 \
-                        --no-verify --extra-configs 0 --sw-fork $f
-                done
-            done ;;
-        abfork10) for f in 1 0; do
-                step abfork10_$f 300 python bench.py --config 7 --steps 20 --warmup 5 --cpu-seconds 0 --no-verify \
-                    --extra-configs 0 --sw-loss 0.1 --sw-fork $f
-            done ;;
         gpufix) step gpufix 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_sw.py \
                     tests/test_gpu_boundscheck.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         bsdtests) step bsdtests 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_boundscheck.py \
