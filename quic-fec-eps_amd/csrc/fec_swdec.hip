@@ -252,6 +252,43 @@ __device__ __forceinline__ void rlc_words(const SwDecArgs &a, const fecgpu_sw_re
     if (nss & 3u) f(nss >> 2, word);
 }
 
+// f(g, v) for the window's coefficients 16 at a time (uint4 g < ceil(nss /
+// 16), bytes past nss zero): rows go out as 16-B stores (the 4-B ones of
+// rlc_words, 64 lanes on 64 rows, were most of the plan's store time)
+template <class F>
+__device__ __forceinline__ void rlc_quads(const SwDecArgs &a, const fecgpu_sw_repair &h, F f) {
+    const uint32_t nss = h.nss, ng = (nss + 15u) >> 4;
+    const auto tail = [&](uint32_t g, uint4 v) {  // bytes past nss zero
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const uint32_t b0 = g * 16 + d * 4;  // first byte of word d
+            if (b0 >= nss) w[d] = 0;
+            else if (nss - b0 < 4) w[d] &= (1u << (8 * (nss - b0))) - 1u;
+        }
+        return make_uint4(w[0], w[1], w[2], w[3]);
+    };
+    if (const uint4 *row = rlc_row(a, h)) {
+        for (uint32_t g0 = 0; g0 < ng; g0 += 4) {  // four loads in flight
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = row[min(g0 + k, kRlcRow / 16 - 1)];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (g0 + k < ng) f(g0 + k, tail(g0 + k, v[k]));
+        }
+        return;
+    }
+    uint32_t w[4] = {0, 0, 0, 0};
+    rlc_words(a, h, [&](uint32_t q, uint32_t x) {
+        w[q & 3] = x;
+        if ((q & 3) == 3 || q == ((nss + 3u) >> 2) - 1) {
+            f(q >> 2, tail(q >> 2, make_uint4(w[0], w[1], w[2], w[3])));
+            w[0] = w[1] = w[2] = w[3] = 0;
+        }
+    });
+}
+
 // The window's coefficients one at a time (next(j) for j = 0, 1, ... in
 // order); from the table 16 per load, the next 16 loaded ahead
 struct RlcSeq {
@@ -552,8 +589,8 @@ __device__ __forceinline__ void block_counts(const SwDecArgs &a, uint32_t rec, u
 // pass draws its own rows again (and overwrites these).
 __device__ __forceinline__ void draw_row(const SwDecArgs &a, uint64_t t, const fecgpu_sw_repair &h) {
     if (!SWC(t, a.nrep, kChkSynJob)) return;
-    uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + t * kSwCoefPitch);
-    rlc_words(a, h, [&](uint32_t q, uint32_t w) { cc[q] = w; });
+    uint4 *cc = reinterpret_cast<uint4 *>(a.coef + t * kSwCoefPitch);
+    rlc_quads(a, h, [&](uint32_t g, uint4 v) { cc[g] = v; });
 }
 
 // ======================================================= fused plan ===
@@ -1032,12 +1069,26 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         const auto rp_at = [&](uint64_t t) -> uint8_t {
             return t - tb < (uint64_t)kPlanHdr ? s_hp[t - tb] : a.rep_present[t];
         };
+        // A lost source of the chunk that will be alone in its system (a
+        // one-unknown system: the plan writes its pivot's scaled row itself)
+        // needs no drawn rows: no repair holding it holds another lost source.
+        // Decided here without the look-back, conservatively: not the chunk's
+        // first or last lost source, beyond the reach of earlier chunks'
+        // windows (pos >= wmb_all), the reach before it stops at it and its
+        // own stops before the next.  (At 2 % loss most rows drawn were such
+        // systems' and went unused; their scattered dword stores cost the
+        // plan ~15 us on cfg7, r05 trace.)
+        const auto alone = [&](uint32_t k) {
+            return a.long_min > 1 && k > 0 && k + 1 < nl && s_lpos[k] >= wmb_all &&
+                   s_rl[k - 1] <= i0 + s_lpos[k] && s_rl[k] <= i0 + s_lpos[k + 1];
+        };
         for (uint64_t t = t0 + (tid - 64); t < t1; t += kBlock - 64) {
             if (!rp_at(t)) continue;
             const fecgpu_sw_repair h = hdr_at(t);
             if (h.fss < i0 || h.fss >= i1 || !hdr_ok(h, a.nsrc)) continue;
             const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
-            if (before(hi) > before(lo)) draw_row(a, t, h);
+            const uint32_t bl = before(lo), bh = before(hi);
+            if (bh > bl && !(bh == bl + 1 && alone(bl))) draw_row(a, t, h);
         }
 #if FECGPU_SWD_TRACE
         if (tid == 64) s_tr[12] = wall_clock64();  // wave 1: its row draws issued
@@ -1166,13 +1217,17 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                 uint32_t tab[5];
                 set_tab(tab, iv);
                 // the xor row's multiplier follows the coefficients (nss < kSwCoefPitch):
-                // in the last partial word, or a word of its own
+                // in the last partial quad, or a quad of its own
                 const uint32_t nq = h.nss >> 2, ivw = iv << (8 * (h.nss & 3));
-                rlc_words(a, h, [&](uint32_t q, uint32_t w) {
+                const auto scale = [&](uint32_t q, uint32_t w) {
                     if (q == (j >> 2)) w &= ~(0xFFu << (8 * (j & 3)));
-                    reinterpret_cast<uint32_t *>(row)[q] = tmul(w, tab) | (q == nq ? ivw : 0u);
+                    return tmul(w, tab) | (q == nq ? ivw : 0u);
+                };
+                rlc_quads(a, h, [&](uint32_t g, uint4 v) {
+                    reinterpret_cast<uint4 *>(row)[g] =
+                        make_uint4(scale(4 * g, v.x), scale(4 * g + 1, v.y), scale(4 * g + 2, v.z), scale(4 * g + 3, v.w));
                 });
-                if (!(h.nss & 3)) reinterpret_cast<uint32_t *>(row)[nq] = ivw;
+                if (!(h.nss & 15)) reinterpret_cast<uint4 *>(row)[h.nss >> 4] = make_uint4(ivw, 0, 0, 0);
                 J.in_off = h.fss * a.stride;
                 J.coef_off = slot * kSwCoefPitch;
                 J.out_list = slot;

@@ -194,6 +194,21 @@ for s in "$@"; do
                 BSD_MIN_E=$m step profbsd_$m 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profbsd_$m -o run -- \
                     python scripts/code_sweep.py shape=gf256-cauchy-32-8
             done ;;
+        tracex)  # cfg7 plan trace of every lib/libfecgpu_trace*.so (measurement variants)
+            for v in quic-fec-eps_amd/lib/libfecgpu_trace*.so; do
+                n=$(basename $v .so); n=${n#libfecgpu_}
+                FECGPU_LIB=$v step tracex_$n 300 python bench.py --config 7 --steps 3 --warmup 1 --cpu-seconds 0 \
+                    --no-verify --extra-configs 0
+            done ;;
+        abbsdu)  # bit-sliced decode: default lib vs lib/libfecgpu_bsdu8.so (8 inputs per load batch)
+            for v in "" quic-fec-eps_amd/lib/libfecgpu_bsdu8.so; do
+                n=${v:+u8}; n=${n:-u2}
+                FECGPU_LIB=$v step abbsdu_sweep_$n 300 python scripts/code_sweep.py r8
+                FECGPU_LIB=$v step abbsdu_cfg4_$n 300 python bench.py --config 4 --steps 5 --warmup 2 --cpu-seconds 0 \
+                    --no-verify --extra-configs 0
+                FECGPU_LIB=$v step abbsdu_w120_$n 300 python bench.py --k 120 --r 8 --steps 10 --warmup 3 \
+                    --cpu-seconds 0 --no-verify
+            done ;;
         gpufix) step gpufix 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_sw.py \
                     tests/test_gpu_boundscheck.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         bsdtests) step bsdtests 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_boundscheck.py \
