@@ -114,10 +114,12 @@ def parse():
     return a
 
 
-def pmc_traffic(cfgid: int, kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
-    summary for this config (profiles/rNN_cfgN_traffic.json, written by
-    scripts/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE passes)."""
+def pmc_traffic(cfgid, kernel: str):
+    """HBM bytes per launch of `kernel` (per call for the wide codes) from the
+    newest committed rocprofv3 PMC summary for this config
+    (profiles/rNN_cfgN_traffic.json, or rNN_cfgwideKrR_traffic.json for
+    `--k K --r R`; written by scripts/pmc_traffic.py from separate FETCH_SIZE /
+    WRITE_SIZE passes)."""
     import glob
     files = sorted(glob.glob(os.path.join(_ROOT, "profiles", f"r*_cfg{cfgid}_traffic.json")))
     if not files:
@@ -500,8 +502,8 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
                 for call, ms in (("encode", enc_ms), ("decode", dec_ms))}
         bound_dir = max(("h2d", "d2h"), key=lambda d: pb[dom][d])
         achieved = pcie[dom][bound_dir]["GBs"]
-    traffic, traffic_src = (pmc_traffic(cfgid, dom)
-                            if nwin == cfg.nwin_per_gpu and cfg.name == workloads.CONFIGS[cfgid].name and not wide
+    traffic, traffic_src = (pmc_traffic(f"wide{cfg.k}r{cfg.r}" if wide else cfgid, dom)
+                            if nwin == cfg.nwin_per_gpu and (wide or cfg.name == workloads.CONFIGS[cfgid].name)
                             and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
                             else (None, None))
     cpu = None

@@ -154,8 +154,12 @@ struct fecgpu_ctx {
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
     // GF decode: windows with at least this many erasures take the bit-sliced
-    // decode (fec_kernels.hip gf_decode_bs_kernel; 0 = never)
-    int bsd_min_e = 6;
+    // decode (fec_kernels.hip gf_decode_bs_kernel; 0 = never, and the wide
+    // codes decode in two stages).  Off by default: on cfg4 the
+    // table decode hides those windows' VALU cost in its memory-bound stream
+    // (4.65 vs 4.96 ms with 6), and the two-stage wide decode measured 1.67
+    // vs 1.81 ms at k120 (r05)
+    int bsd_min_e = 0;
     int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
     int sw_stream = kSwStreamDefault;  // sliding-window encode: 0 combine jobs, 1..5 streaming
                                        // (dwords per lane), kSwStreamAuto per symbol size

@@ -607,12 +607,6 @@ __device__ __forceinline__ void sources(const uint8_t *pa, const uint8_t *pb, ui
 // S = 1200, profiles/r01_bs_layout.txt).  Flat mode, one unit space over all
 // uniform windows, beat group mode there: S = 1200 k32 r8 3.84 -> 4.60 TB/s.
 constexpr int kBsU = 8, kBsUFlat = 2;
-// bit-sliced decode: inputs per load batch (2: <= 168 VGPRs, 3 waves per SIMD;
-// 8 took 227, 2 waves)
-#ifndef FECGPU_BSD_U
-#define FECGPU_BSD_U 2
-#endif
-constexpr int kBsdU = FECGPU_BSD_U;
 
 namespace bs {
 
@@ -1616,38 +1610,22 @@ __device__ __forceinline__ void dload(const uint8_t *pa, const uint8_t *pb, uint
     x[4] = vb.x & mk; x[5] = vb.y & mk; x[6] = vb.z & mk; x[7] = vb.w & mk;
 }
 
-// input J >= K is repair J - K: its planes add to that syndrome's (identity)
-template <int K, int R, int M, int J>
-__device__ __forceinline__ void input(const uint32_t (&x)[8], uint32_t (&acc)[R][8]) {
-    if constexpr (J < K) {
-        source<K, R, M, J>(x, acc, std::make_integer_sequence<int, R * 8>{});
-    } else {
-#pragma unroll
-        for (int p = 0; p < 8; p++) acc[J - K][p] = oxor(acc[J - K][p], x[p]);
-#pragma unroll
-        for (int i = 0; i < R; i++)
-#pragma unroll
-            for (int p = 0; p < 8; p++) asm volatile("" : "+v"(acc[i][p]));
-    }
-}
-
 template <int K, int R, int M, int J0, int... T>
 __device__ __forceinline__ void dbatch(const uint8_t *pa, const uint8_t *pb, uint32_t stride, uint64_t pm,
                                        const uint8_t *qa, const uint8_t *qb, uint32_t (&acc)[R][8],
                                        std::integer_sequence<int, T...>) {
     uint32_t x[sizeof...(T)][8];
     (dload<T, J0 + T>(pa, pb, stride, pm, qa, qb, x[T]), ...);
-    ((tr8(x[T]), input<K, R, M, J0 + T>(x[T], acc), __builtin_amdgcn_sched_barrier(0)), ...);
+    ((tr8(x[T]), source<K, R, M, J0 + T>(x[T], acc, std::make_integer_sequence<int, R * 8>{}),
+      __builtin_amdgcn_sched_barrier(0)), ...);
 }
 
-// the K sources, then the R repairs (inputs K .. K + R - 1: pm bit K + i set
-// where the window's solve uses repair i)
 template <int K, int R, int M, int U, int J0>
 __device__ __forceinline__ void dsources(const uint8_t *pa, const uint8_t *pb, uint32_t stride, uint64_t pm,
                                          const uint8_t *qa, const uint8_t *qb, uint32_t (&acc)[R][8]) {
-    if constexpr (J0 < K + R) {
+    if constexpr (J0 < K) {
         dbatch<K, R, M, J0>(pa, pb, stride, pm, qa, qb, acc,
-                            std::make_integer_sequence<int, ((K + R - J0) < U ? (K + R - J0) : U)>{});
+                            std::make_integer_sequence<int, ((K - J0) < U ? (K - J0) : U)>{});
         pa += U * stride;
         pb += U * stride;
         asm volatile("" : "+v"(pa), "+v"(pb));
@@ -1660,18 +1638,30 @@ __device__ __forceinline__ void dsources(const uint8_t *pa, const uint8_t *pb, u
 template <int K, int R, int M, int U>
 __device__ __forceinline__ void dec_unit(uint8_t *pa, uint8_t *pb, uint32_t stride, bool live, const BsdRegion &rg,
                                          int nw) {
-    static_assert(K + R <= 64, "one present word");
-    // the received sources and the repairs the solve uses (the others' loads
-    // go to the alt row and are masked to zero): a repair's planes are added
-    // to its syndrome's as one more input (a separate batch of repair loads
-    // after the sources held 64 more VGPRs across the solve)
-    const uint64_t pm = (rg.pw[0] & ((1ull << K) - 1ull)) | ((uint64_t)rg.used << K);
+    const uint64_t pm = rg.pw[0];
     const uint32_t alt = rg.alt;
     uint32_t acc[R][8];
     const uint8_t *qa = pa + alt * stride, *qb = pb + alt * stride;
     dsources<K, R, M, U, 0>(pa, pb, stride, pm, qa, qb, acc);
+    // the repairs the window uses, one batch (the others read at the alt row
+    // and masked to zero), added to the syndromes' bytes
+    const uint32_t used = rg.used;
+    uint4 ra[R], rb[R];
 #pragma unroll
-    for (int i = 0; i < R; i++) tr8(acc[i]);
+    for (int i = 0; i < R; i++) {
+        const bool p = (used >> i) & 1u;
+        ra[i] = ld16(p ? pa + (K + i) * stride : qa);
+        rb[i] = ld16(p ? pb + (K + i) * stride : qb);
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        tr8(acc[i]);
+        const uint32_t mk = ((used >> i) & 1u) ? ~0u : 0u;
+        ra[i] = and4(ra[i], mk);
+        rb[i] = and4(rb[i], mk);
+    }
+    bsd::add_col<R, 0>(acc, ra);
+    bsd::add_col<R, 4>(acc, rb);
     const int ne = (int)rg.ne;
     bsd::solve_col<R, 0>(acc, pa, stride, rg, nw, ne, live);
     bsd::solve_col<R, 4>(acc, pb, stride, rg, nw, ne, pb != pa && live);
@@ -1872,7 +1862,7 @@ void gf_decode_bs_kernel(BatchArgs a) {
             } else {
                 uint8_t *pa, *pb;
                 bs::unit_cols(base, u, h, g.ncol[wl], pa, pb);
-                bs::dec_unit<K, R, M, kBsdU>(pa, pb, g.stride[wl], live, rg, nw);
+                bs::dec_unit<K, R, M, kBsU>(pa, pb, g.stride[wl], live, rg, nw);
             }
         }
         __syncthreads();

@@ -155,6 +155,11 @@ for s in "$@"; do
         prof3) prof prof3 3 ;;
         prof4) prof prof4 4 ;;
         prof4rlc) prof prof4rlc 4 --matrix rlc ;;
+        pmcw*)  # pmcw<K>r / pmcw<K>w: FETCH_SIZE / WRITE_SIZE pass of `bench.py --k K --r 8`
+            kk=${s#pmcw}; c=${kk: -1}; kk=${kk%?}
+            [ "$c" = r ] && ctr=FETCH_SIZE || ctr=WRITE_SIZE
+            step pmcw$kk$c 600 rocprofv3 --kernel-trace --pmc $ctr -f csv -d gpurun_out/pmcw$kk$c -o run -- \
+                python bench.py --k $kk --r 8 --steps 3 --warmup 1 --cpu-seconds 0 --no-verify ;;
         pmc2r) pmc pmc2r 2 FETCH_SIZE ;;
         pmc2w) pmc pmc2w 2 WRITE_SIZE ;;
         pmc3r) pmc pmc3r 3 FETCH_SIZE ;;

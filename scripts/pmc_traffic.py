@@ -29,7 +29,42 @@ def kind(name, config):
     return "encode" if "encode" in name else "decode" if "decode" in name else None
 
 
+def per_call_wide(path, counter):
+    """Wide codes (k + r > 64, `--k`): bytes per encode / decode CALL.  In
+    dispatch order a decode is wide_dec_plan_kernel, the stage-1 bit-sliced
+    pass (gf_encode_rbs_kernel right after the plan) and the stage-2 combine
+    pass; an encode is a gf_encode_rbs_kernel on its own (or the bit-sliced
+    decode's plan and data kernels when bsd_min_e > 0: gf_decode_bs_*)."""
+    rows = [r for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")) if r["Counter_Name"] == counter]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    enc, dec = [], []
+    cur = None  # the decode call being summed
+    for r in rows:
+        n, v = r["Kernel_Name"], float(r["Counter_Value"])
+        if "fecgpu" not in n:
+            continue
+        if "wide_dec_plan_kernel" in n or "gf_decode_bs_plan_kernel" in n:
+            cur = [v, False]
+            dec.append(cur)
+        elif "gf_encode_rbs_kernel" in n and cur is not None and not cur[1]:
+            cur[0] += v
+            cur[1] = True  # stage 1 of the current decode
+        elif ("comb_kernel" in n or "gf_decode_bs_kernel" in n) and cur is not None:
+            cur[0] += v
+            cur = None
+        elif "gf_encode_rbs_kernel" in n:
+            enc.append(v)
+    out = {}
+    if enc:
+        out["encode"] = statistics.median(enc)
+    if dec:
+        out["decode"] = statistics.median([d[0] for d in dec])
+    return out
+
+
 def per_kernel(path, counter, config):
+    if config == "wide":
+        return per_call_wide(path, counter)
     out = collections.defaultdict(list)
     calls = 0  # config 7: decode calls (one plan kernel each, or header kernel unfused); the chain summed per call
     for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
@@ -48,11 +83,13 @@ def per_kernel(path, counter, config):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True)
+    ap.add_argument("--config", required=True, help="config id, or 'wide' (bench.py --k K --r R)")
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
+    if a.config != "wide":
+        a.config = int(a.config)
     f = per_kernel(a.fetch, "FETCH_SIZE", a.config)
     w = per_kernel(a.write, "WRITE_SIZE", a.config)
     res = {"config": a.config, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "

@@ -420,13 +420,20 @@ def test_checked_sw_checker_fires_when_the_range_is_short(chk):
 
 
 @pytest.mark.parametrize("k,r,matrix,L", [(248, 8, "cauchy", 300), (120, 8, "rlc", 1200), (150, 5, "cauchy", 64)])
-def test_checked_wide_encode_decode(chk, k, r, matrix, L):
-    """k + r up to 256 (the bit-sliced wide decode with buffer loads, the plan)."""
+@pytest.mark.parametrize("bsd", [0, 6])
+def test_checked_wide_encode_decode(chk, k, r, matrix, L, bsd):
+    """k + r up to 256: the two-stage decode (default) and the bit-sliced one
+    (bsd_min_e 6: buffer loads past the resource, the plan kernel)."""
     import test_gpu_wide as TW
-    m, ctx = chk
-    rng = np.random.default_rng(k + r)
-    bits = TW._erasures(10, k, r, rng)
-    TW._run(ctx, k, r, matrix, L, 10, bits, m=m)
+    m, _ = chk
+    c = m.Context()
+    try:
+        c.set_tuning("bsd_min_e", bsd)
+        rng = np.random.default_rng(k + r)
+        bits = TW._erasures(10, k, r, rng)
+        TW._run(c, k, r, matrix, L, 10, bits, m=m)
+    finally:
+        c.close()
 
 
 def test_checked_wide_two_stage(chk):

@@ -1,12 +1,12 @@
 """GPU parity of the bit-sliced decode of windows with many erasures
 (fec_kernels.hip gf_decode_bs_kernel): the table decode's plan
-routes windows with e >= the ctx's "bsd_min_e" erasures (default 6) to it for
+routes windows with e >= the ctx's "bsd_min_e" erasures (default 0: off) to it for
 the codes with compiled plane masks (k in 16, 24, 32; r = 8; Cauchy and
 systematic Vandermonde rows).  Recovered bytes equal the originals, statuses
 equal the numpy oracle's (oracle/np_oracle.py decode), missing rows poisoned
 first; routing on and off give the same bytes.  The wide codes (k + r > 64,
-every window through this kernel with runtime plane masks) are covered by
-tests/test_gpu_wide.py.
+every window through this kernel with runtime plane picks when bsd_min_e > 0)
+are covered by tests/test_gpu_wide.py::test_wide_bitsliced_decode.
 PARITY UNPINNED vs the reference fec branch."""
 import numpy as np
 import pytest

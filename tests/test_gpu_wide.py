@@ -141,9 +141,39 @@ def test_wide_per_window_lengths(ctx):
     _run(ctx, k, r, "cauchy", L, nwin, bits, sym_len=sl)
 
 
+@pytest.fixture(scope="module")
+def bsctx():
+    """A ctx with the bit-sliced wide decode on (tuning "bsd_min_e" > 0)."""
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    c = fecgpu.Context()
+    c.set_tuning("bsd_min_e", 6)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("k,r,matrix,L", [(60, 8, "cauchy", 1200), (120, 8, "cauchy", 1200), (248, 8, "cauchy", 300),
+                                          (90, 6, "vandermonde", 1200), (150, 8, "rlc", 1200), (250, 6, "rlc", 64),
+                                          (75, 5, "cauchy", 200), (68, 4, "rlc", 16)])
+def test_wide_bitsliced_decode(bsctx, k, r, matrix, L):
+    """The bit-sliced wide decode (gf_decode_bs_plan_kernel + gf_decode_bs_kernel,
+    runtime plane picks of [P | I]): bytes and statuses as the
+    oracle's, every erasure count, per-window lengths."""
+    nwin = 40
+    rng = np.random.default_rng(k * 13 + r)
+    bits = _erasures(nwin, k, r, rng)
+    for e in range(min(r + 2, nwin)):
+        bits[e] = True
+        bits[e, rng.choice(k, e, replace=False)] = False
+    gst = _run(bsctx, k, r, matrix, L, nwin, bits)
+    if matrix == "cauchy":  # MDS: any e <= r present repairs suffice
+        assert list(gst[:r + 2]) == [0] * (r + 1) + [1]
+    sl = rng.integers(1, L + 1, nwin).astype(np.uint32)
+    _run(bsctx, k, r, matrix, L, nwin, bits, sym_len=sl, seed=1)
+
+
 def test_wide_two_stage_path():
-    """With the bit-sliced kernels off (tuning "bitslice" 0) the wide decode takes
-    the two-stage combine passes (fec_wide.hip): the same bytes and statuses."""
+    """With the bit-sliced kernels off (tuning "bitslice" 0) the wide decode's two
+    stages run as combine passes (fec_wide.hip): the same bytes and statuses."""
     c = fecgpu.Context()
     try:
         c.set_tuning("bitslice", 0)
