@@ -1082,17 +1082,8 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             return a.long_min > 1 && k > 0 && k + 1 < nl && s_lpos[k] >= wmb_all &&
                    s_rl[k - 1] <= i0 + s_lpos[k] && s_rl[k] <= i0 + s_lpos[k + 1];
         };
-        for (uint64_t t = t0 + (tid - 64); t < t1; t += kBlock - 64) {
-            if (!rp_at(t)) continue;
-            const fecgpu_sw_repair h = hdr_at(t);
-            if (h.fss < i0 || h.fss >= i1 || !hdr_ok(h, a.nsrc)) continue;
-            const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
-            const uint32_t bl = before(lo), bh = before(hi);
-            if (bh > bl && !(bh == bl + 1 && alone(bl))) draw_row(a, t, h);
-        }
-#if FECGPU_SWD_TRACE
-        if (tid == 64) s_tr[12] = wall_clock64();  // wave 1: its row draws issued
-#endif
+        // pivots first: loads only (behind the draws' stores, their loads
+        // waited for those to complete: the memory counter is in order)
         for (uint32_t k = tid - 64; k < nl; k += kBlock - 64) {
             uint32_t pt = ~0u, pw = 0, pc = 0;
             const uint32_t pos = s_lpos[k];
@@ -1128,6 +1119,17 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         }
 #if FECGPU_SWD_TRACE
         if (tid == 64) s_tr[13] = wall_clock64();  // wave 1: its pivots found
+#endif
+        for (uint64_t t = t0 + (tid - 64); t < t1; t += kBlock - 64) {
+            if (!rp_at(t)) continue;
+            const fecgpu_sw_repair h = hdr_at(t);
+            if (h.fss < i0 || h.fss >= i1 || !hdr_ok(h, a.nsrc)) continue;
+            const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
+            const uint32_t bl = before(lo), bh = before(hi);
+            if (bh > bl && !(bh == bl + 1 && alone(bl))) draw_row(a, t, h);
+        }
+#if FECGPU_SWD_TRACE
+        if (tid == 64) s_tr[12] = wall_clock64();  // wave 1: its row draws issued
 #endif
     }
     __syncthreads();
