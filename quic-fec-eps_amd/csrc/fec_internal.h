@@ -303,11 +303,8 @@ __host__ __device__ inline uint32_t comb_job_small_lds(int R) {
 }
 hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
 // the runtime-mask bit-sliced encode over uniform windows of any k (fec_kernels.hip)
-// (present: nw words per window; inputs a window misses are not read and
-// count as zero rows — the wide decode's syndromes)
 hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t stride, uint64_t wpitch, int k,
-                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s,
-                           const uint64_t *present = nullptr, int nw = 0);
+                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s);
 // GF block codes with k + r > 64 (fec_wide.hip): encode by the runtime-mask
 // bit-sliced kernel (r >= 4) or a combine job per window; decode in two stages
 // (syndromes of every repair with one coefficient block [P | I] for all

@@ -815,46 +815,21 @@ __device__ __forceinline__ void load(uint8_t *const (&pc)[4], uint32_t off, uint
     xb[4] = v3.x; xb[5] = v3.y; xb[6] = v3.z; xb[7] = v3.w;
 }
 
-// input j of the unit's window present (PRES: bit j of its present words pw,
-// up to 4 in registers; the select is on a wave-uniform index)
-__device__ __forceinline__ bool pres_bit(const uint64_t (&pw)[4], int j) {
-    const int q = j >> 6;
-    const uint64_t w = q == 0 ? pw[0] : q == 1 ? pw[1] : q == 2 ? pw[2] : pw[3];
-    return (w >> (j & 63)) & 1ull;
-}
-// load() of a present input; zeros for a missing one (exec-masked: no access)
-__device__ __forceinline__ void load_if(bool p, uint8_t *const (&pc)[4], uint32_t off, uint32_t (&xa)[8],
-                                        uint32_t (&xb)[8]) {
-#pragma unroll
-    for (int q = 0; q < 8; q++) xa[q] = xb[q] = 0;
-    if (p) load(pc, off, xa, xb);
-}
-
 // one unit: columns pc[0..3]; the next source's loads are issued before the
-// current one's XOR work.  PRES (the wide decode's syndromes): inputs the
-// window misses (present words pw) are not read and count as zero rows.
-template <int R, bool PRES = false>
+// current one's XOR work
+template <int R>
 __device__ __forceinline__ void unit(uint8_t *const (&pc)[4], uint32_t stride, int k, cmask mk, bool live,
-                                     uint64_t od, const uint64_t *pw_g = nullptr, int nw = 0) {
+                                     uint64_t od) {
     uint32_t aa[R][8], ab[R][8];
 #pragma unroll
     for (int i = 0; i < R; i++)
 #pragma unroll
         for (int p = 0; p < 8; p++) aa[i][p] = ab[i][p] = 0;
-    uint64_t pw[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-    if constexpr (PRES) {
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (q < nw) pw[q] = pw_g[q];
-    }
     uint32_t xa[8], xb[8];
-    if constexpr (PRES) load_if(pres_bit(pw, 0), pc, 0, xa, xb);
-    else load(pc, 0, xa, xb);
+    load(pc, 0, xa, xb);
     for (int j = 0; j < k; j++) {
         uint32_t na[8], nb[8];
-        const int jn = min(j + 1, k - 1);
-        if constexpr (PRES) load_if(pres_bit(pw, jn), pc, (uint32_t)jn * stride, na, nb);
-        else load(pc, (uint32_t)jn * stride, na, nb);
+        load(pc, (uint32_t)min(j + 1, k - 1) * stride, na, nb);
         bs::tr8(xa);
         bs::tr8(xb);
         source<R>(xa, xb, aa, ab, mk + (size_t)j * (R * 2 * kRbsDw4));
@@ -891,19 +866,17 @@ __device__ __forceinline__ void unit_cols(uint8_t *base, uint32_t u, uint32_t h,
 
 // Unit spaces as gf_encode_bs_kernel (flat over uniform windows, group mode
 // otherwise); the masks are the code's, R = its r.
-template <int R, bool FLAT, bool PRES = false>
+template <int R, bool FLAT>
 __global__ __launch_bounds__(kBlock) void gf_encode_rbs_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
     const rbs::cmask mk = (rbs::cmask)a.enc_bs;
     const int k = a.k;
     constexpr uint32_t C = kRbsCols;  // columns per unit
     // one unit of window base (units h, columns ncol)
-    auto run = [&](uint8_t *base, uint32_t u, uint32_t h, uint32_t ncol, uint32_t stride, bool live, uint64_t od,
-                   uint64_t w) {
+    auto run = [&](uint8_t *base, uint32_t u, uint32_t h, uint32_t ncol, uint32_t stride, bool live, uint64_t od) {
         uint8_t *pc[4];
         rbs4::unit_cols(base, u, h, ncol, pc);
-        if constexpr (PRES) rbs4::unit<R, true>(pc, stride, k, mk, live, od, a.present + w * (uint64_t)a.nw, a.nw);
-        else rbs4::unit<R>(pc, stride, k, mk, live, od);
+        rbs4::unit<R>(pc, stride, k, mk, live, od);
     };
     if constexpr (FLAT) {
         const uint32_t ncol = a.ncol, h = (ncol + C - 1) / C;
@@ -913,8 +886,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_rbs_kernel(BatchArgs a) {
             const bool live = s < total;
             if (!live) s = total - 1;
             const uint64_t w = s / h;
-            run(a.win + w * a.wpitch, (uint32_t)(s - w * h), h, ncol, a.stride, live, a.out_delta + w * a.out_wdelta,
-                w);
+            run(a.win + w * a.wpitch, (uint32_t)(s - w * h), h, ncol, a.stride, live, a.out_delta + w * a.out_wdelta);
         }
     } else {
         __shared__ GroupLds g;
@@ -933,7 +905,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_rbs_kernel(BatchArgs a) {
                 const uint32_t s = live ? s0 + threadIdx.x : total - 1;
                 while (s >= g.pfx[wl + 1]) wl++;
                 run(reinterpret_cast<uint8_t *>(g.base[wl]), s - g.pfx[wl], g.pfx[wl + 1] - g.pfx[wl], g.ncol[wl],
-                    g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta, w0 + wl);
+                    g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
             }
             __syncthreads();
         }
@@ -2607,8 +2579,7 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
         switch (a.r) {
 #define RBS_CASE(R_)                                                                        \
             case R_:                                                                               \
-                return p.flat ? (a.present ? launch(gf_encode_rbs_kernel<R_, true, true>, a, p, s, false, want) \
-                                           : launch(gf_encode_rbs_kernel<R_, true>, a, p, s, false, want))   \
+                return p.flat ? launch(gf_encode_rbs_kernel<R_, true>, a, p, s, false, want)       \
                               : launch(gf_encode_rbs_kernel<R_, false>, a, p, s, false);
             RBS_CASE(4) RBS_CASE(5) RBS_CASE(6) RBS_CASE(7) RBS_CASE(8)
 #undef RBS_CASE
@@ -2630,13 +2601,10 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
 // win + w * wpitch, its k input rows first, output i at
 // (input row k + i's address) + out_delta + w * out_wdelta.  Flat unit space.
 hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t stride, uint64_t wpitch, int k,
-                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s,
-                           const uint64_t *present, int nw) {
+                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s) {
     if (nwin == 0) return hipSuccess;
-    if (r < 4 || r > 8 || nw > 4) return hipErrorInvalidValue;
+    if (r < 4 || r > 8) return hipErrorInvalidValue;
     BatchArgs a{};
-    a.present = present;  // (non-null: inputs the windows miss are not read, zero rows)
-    a.nw = nw;
     a.win = win;
     a.nwin = nwin;
     a.ncol = ncol;

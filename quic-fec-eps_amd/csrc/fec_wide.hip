@@ -13,9 +13,8 @@
 //    repair reduced by Gauss-Jordan with pivot search (so an RLC window is
 //    recovered whenever its present repairs have rank e), the stage-2 block
 //    C[u][i] = T[P_u][c] for the repair i of pivot row c.  Stage 1: every
-//    repair's syndrome s_i = rep_i + sum_j P[i][j] src_j by one coefficient
-//    block [P | I] for all windows, the rows a window misses not read (plane
-//    picks) or zeroed by the plan (combine passes);
+//    repair's syndrome s_i = rep_i + sum_j P[i][j] src_j (the missing rows
+//    zeroed by the plan) by one coefficient block [P | I] for all windows;
 //    stage 2: x_u = sum_i C[u][i] s_i, a combine job per window.
 #include "fec_internal.h"
 
@@ -54,7 +53,6 @@ struct WideArgs {
     CombJob *jobs1;
     uint64_t *outs1;
     ChkRec *chk;  // FECGPU_CHECK builds: the fault record (release: null)
-    int zero_missing;  // decode: the plan zeroes the missing rows (stage 1 as combine passes)
 };
 
 __global__ __launch_bounds__(kBlock) void wide_enc_jobs_kernel(WideArgs a) {
@@ -153,8 +151,7 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
         }
     }
     // stage 2's block C[u][i] (8 x 8 per window): T[P_u][c] for the repair i
-    // of pivot row c, else 0; the missing rows zeroed for stage 1 when it runs
-    // as combine passes (the plane-pick pass skips them by the present words)
+    // of pivot row c, else 0; the missing rows zeroed for stage 1
     {
         uint8_t *C2 = a.coef + w * (uint64_t)(kMaxR * kMaxR);  // [e][r] used
         const int cu = lane >> 3, ci = lane & 7;                 // lane = output u * 8 + repair i
@@ -169,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
         }
         if (cu < e && ci < r) C2[cu * r + ci] = (uint8_t)v;
         uint8_t *wb = a.win + w * a.wpitch;
-        for (int u2 = 0; a.zero_missing && u2 < e && CHK_IDX(a.chk, s_m[wave][u2], k, 1); u2++) {
+        for (int u2 = 0; u2 < e && CHK_IDX(a.chk, s_m[wave][u2], k, 1); u2++) {
             uint4 *row = reinterpret_cast<uint4 *>(wb + (uint64_t)s_m[wave][u2] * a.stride);
             for (uint32_t c16 = lane; c16 < a.stride / 16u; c16 += 64) row[c16] = make_uint4(0, 0, 0, 0);
         }
@@ -225,7 +222,6 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
     if (!decode && masks_P) {  // every window's k sources times P by plane picks
         return launch_rbs_rows(win, nwin, ncol, stride, a.wpitch, k, r, masks_P, 0, 0, s);
     }
-    a.zero_missing = masks_PI == nullptr;  // the combine passes read every row; the picks skip missing ones
     if (decode)
         hipLaunchKernelGGL(wide_dec_plan_kernel, dim3((unsigned)((nwin + kBlock / 64 - 1) / (kBlock / 64))),
                            dim3(kBlock), 0, s, a);
@@ -244,7 +240,7 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
         if (masks_PI) {
             e = launch_rbs_rows(win, nwin, ncol, stride, a.wpitch, n, r, masks_PI,
                                 (uint64_t)syn - (uint64_t)win - (uint64_t)n * stride,
-                                (uint64_t)r * stride - a.wpitch, s, present, a.nw);
+                                (uint64_t)r * stride - a.wpitch, s);
         } else {
         CombArgs c1{};
         c1.jobs = jobs1;

@@ -48,6 +48,9 @@ for s in "$@"; do
         bench7l10) step bench7l10 600 python bench.py --config 7 --steps 20 --warmup 5 --cpu-seconds 0 --sw-loss 0.1 ;;
         benchw120) step benchw120 600 python bench.py --k 120 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 ;;
         benchw248) step benchw248 600 python bench.py --k 248 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 ;;
+        benchwc) for kk in 120 248; do  # the wide lines with their CPU baselines
+                step benchwc$kk 600 python bench.py --k $kk --r 8 --steps 10 --warmup 3 --cpu-seconds 10
+            done ;;
         profw120) step profw120 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profw120 -o run -- \
                       python bench.py --k 120 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 ;;
         profw248) step profw248 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profw248 -o run -- \
