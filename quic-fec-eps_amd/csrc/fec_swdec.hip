@@ -255,19 +255,21 @@ __device__ __forceinline__ void rlc_words(const SwDecArgs &a, const fecgpu_sw_re
 // f(g, v) for the window's coefficients 16 at a time (uint4 g < ceil(nss /
 // 16), bytes past nss zero): rows go out as 16-B stores (the 4-B ones of
 // rlc_words, 64 lanes on 64 rows, were most of the plan's store time)
+// quad g of a coefficient row with bytes past nss zero
+__device__ __forceinline__ uint4 quad_tail(uint32_t g, uint4 v, uint32_t nss) {
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const uint32_t b0 = g * 16 + d * 4;  // first byte of word d
+        if (b0 >= nss) w[d] = 0;
+        else if (nss - b0 < 4) w[d] &= (1u << (8 * (nss - b0))) - 1u;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
 template <class F>
 __device__ __forceinline__ void rlc_quads(const SwDecArgs &a, const fecgpu_sw_repair &h, F f) {
     const uint32_t nss = h.nss, ng = (nss + 15u) >> 4;
-    const auto tail = [&](uint32_t g, uint4 v) {  // bytes past nss zero
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int d = 0; d < 4; d++) {
-            const uint32_t b0 = g * 16 + d * 4;  // first byte of word d
-            if (b0 >= nss) w[d] = 0;
-            else if (nss - b0 < 4) w[d] &= (1u << (8 * (nss - b0))) - 1u;
-        }
-        return make_uint4(w[0], w[1], w[2], w[3]);
-    };
+    const auto tail = [&](uint32_t g, uint4 v) { return quad_tail(g, v, nss); };
     if (const uint4 *row = rlc_row(a, h)) {
         for (uint32_t g0 = 0; g0 < ng; g0 += 4) {  // four loads in flight
             uint4 v[4];
@@ -342,6 +344,8 @@ struct SysLds {
     uint8_t M[MP * kPitch];
     uint32_t U[ME];
     uint32_t eq[MP];
+    uint64_t efss[MP];  // the equations' windows, kept from the candidate scan
+    uint16_t enss[MP];
     int8_t piv[ME];
 };
 
@@ -365,7 +369,9 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     for (int q = lane; q < p; q += 64) {
         const uint32_t t = eq[q];
         if (!SWC(t, a.nrep, kChkHdr)) continue;
-        const fecgpu_sw_repair h = a.hdr[t];
+        fecgpu_sw_repair h{};  // (the scan's copy: fss and nss)
+        h.fss = S.efss[q];
+        h.nss = S.enss[q];
         {
             // the row was drawn by the plan: move the unknowns' entries into A
             // (the unknowns are ascending; the window holds a run of them).
@@ -457,7 +463,7 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
         const uint32_t t = eq[pr];
         const uint32_t iv = M[pr * kPitch + e + pr];  // T[pr][pr] = 1 / c
         if (!SWC(t, a.nrep, kChkSynJob) || !SWC(U[0], a.nsrc, kChkSrcRow)) return 0;
-        const uint32_t nss = a.hdr[t].nss;
+        const uint32_t nss = S.enss[pr];
         uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
         uint32_t tab[5];
         set_tab(tab, iv);
@@ -518,20 +524,29 @@ __device__ bool sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, u
     bool fits = (int)e <= ME && (int)e < a.long_min;
     uint32_t p = 0;
     if (fits) {
-        if (lane < (int)e && SWC(x + lane, a.nsrc, kChkLost)) S.U[lane] = a.lost[x + lane];
+        // the unknowns' positions load beside the candidate scan's first loads;
+        // a candidate's arrival flag and header in one round trip (clamped index)
+        const uint32_t ux = lane < (int)e && SWC(x + lane, a.nsrc, kChkLost) ? a.lost[x + lane] : 0u;
         for (uint64_t t0 = t_lo; t0 < t_hi; t0 += 64) {
-            const uint64_t t = t0 + lane;
-            bool hd = false;
-            if (t < t_hi && a.rep_present[t]) hd = holds(a, a.hdr[t], x, e);
+            const uint64_t t = t0 + lane, tc = min(t, t_hi - 1);
+            const uint8_t rp = a.rep_present[tc];
+            const fecgpu_sw_repair h = a.hdr[tc];
+            const bool hd = t < t_hi && rp && holds(a, h, x, e);
             const uint64_t b = __ballot(hd);
             const uint32_t n = __popcll(b);
             if (p + n > (uint32_t)MP) {
                 fits = false;
                 break;
             }
-            if (hd) S.eq[p + __popcll(b & lanes_below(lane))] = (uint32_t)t;
+            if (hd) {
+                const uint32_t q = p + __popcll(b & lanes_below(lane));
+                S.eq[q] = (uint32_t)t;
+                S.efss[q] = h.fss;
+                S.enss[q] = h.nss;
+            }
             p += n;
         }
+        if (lane < (int)e) S.U[lane] = ux;
         SWD_WAVE_SYNC();
         if (fits && p && S.eq[p - 1] - S.eq[0] + 1 > (uint32_t)kSwSolveIn) fits = false;
     }
@@ -1134,6 +1149,21 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     }
     __syncthreads();
     SWD_TRACE(7);
+    // this thread's first lost source, if alone with a dense pivot row of <= 32
+    // coefficients: the row's two quads load now, beside the lost-list stores
+    // below (loads issued after those stores would wait for them)
+    uint4 pre[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    bool pre_ok = false;
+    if ((uint32_t)tid < nl && a.rlc) {
+        const uint2 pv = s_pv[tid];
+        const uint32_t nssp = (pv.y >> 16) & 0xFFu;
+        pre_ok = pv.x != ~0u && (s_pcd[tid] >> 8) == 15u && nssp <= 32u;
+        if (pre_ok) {
+            const uint4 *row = reinterpret_cast<const uint4 *>(a.rlc + (size_t)(pv.y & 0xFFFFu) * kRlcRow);
+            pre[0] = row[0];
+            pre[1] = row[1];
+        }
+    }
     const LbRec ex = s_excl;
     // lost list, rank / repfirst (as sw_dec_lost_kernel)
     uint32_t off = ex.lost + wc + ic - cnt;
@@ -1225,10 +1255,16 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
                     if (q == (j >> 2)) w &= ~(0xFFu << (8 * (j & 3)));
                     return tmul(w, tab) | (q == nq ? ivw : 0u);
                 };
-                rlc_quads(a, h, [&](uint32_t g, uint4 v) {
+                const auto put = [&](uint32_t g, uint4 v) {
                     reinterpret_cast<uint4 *>(row)[g] =
                         make_uint4(scale(4 * g, v.x), scale(4 * g + 1, v.y), scale(4 * g + 2, v.z), scale(4 * g + 3, v.w));
-                });
+                };
+                if (k == (uint32_t)tid && pre_ok) {  // the prefetched quads
+                    put(0, quad_tail(0, pre[0], h.nss));
+                    if (h.nss > 16) put(1, quad_tail(1, pre[1], h.nss));
+                } else {
+                    rlc_quads(a, h, put);
+                }
                 if (!(h.nss & 15)) reinterpret_cast<uint4 *>(row)[h.nss >> 4] = make_uint4(ivw, 0, 0, 0);
                 J.in_off = h.fss * a.stride;
                 J.coef_off = slot * kSwCoefPitch;
