@@ -75,8 +75,6 @@ def parse():
     ap.add_argument("--bs-passes", type=int, default=0,
                     help="tuning: bit-sliced encode on per-window lengths, 256-unit passes per window group")
     ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
-    ap.add_argument("--sw-overlap", type=int, default=-1, choices=[-1, 0, 1],
-                    help="tuning (config 7): the decode's syndrome pass beside its systems passes (1, default)")
     ap.add_argument("--bsd-min-e", type=int, default=-1,
                     help="tuning: GF decode erasures from which a window takes the bit-sliced decode (0 = never)")
     ap.add_argument("--bpc", type=int, default=0, help="tuning: persistent workgroups per CU")
@@ -336,8 +334,6 @@ def make_ctx(args):
         ctx.set_tuning("bs_passes", args.bs_passes)
     if args.wpb:
         ctx.set_tuning("wpb", args.wpb)
-    if args.sw_overlap >= 0:
-        ctx.set_tuning("sw_overlap", args.sw_overlap)
     if args.bsd_min_e >= 0:
         ctx.set_tuning("bsd_min_e", args.bsd_min_e)
     if args.bpc:

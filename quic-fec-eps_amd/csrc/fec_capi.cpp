@@ -175,13 +175,6 @@ struct fecgpu_ctx {
     // sliding-window calls: device scratch slots and the last call's end event, per device
     std::map<int, std::vector<std::pair<void *, size_t>>> sw_scratch;
     std::map<int, hipEvent_t> sw_event;
-    // ctx_sw_fork: per device a second stream and its fork / join events
-    struct SwFork {
-        hipStream_t st = nullptr;
-        hipEvent_t fork = nullptr, join = nullptr;
-    };
-    std::map<int, SwFork> sw_fork;
-    int sw_overlap = 1;  // tuning "sw_overlap": the decode's syndrome pass beside its systems passes
     std::map<int, SwSticky *> sw_sticky;  // asynchronous decodes' error flags, per device
     std::map<int, ChkRec *> chk_rec;      // FECGPU_CHECK builds: the index-checking kernels' fault record
     struct LbState {
@@ -363,11 +356,6 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         ctx->sw_stream = (int)value;  // calls and objects created from now on
         return 0;
     }
-    if (!std::strcmp(key, "sw_overlap")) {
-        if (value < 0 || value > 1) return FECGPU_ERR_INVALID_ARG;
-        ctx->sw_overlap = (int)value;
-        return 0;
-    }
     if (!std::strcmp(key, "sw_long_min")) {
         if (value < 1 || value > (1 << 30)) return FECGPU_ERR_INVALID_ARG;
         ctx->sw_long_min = (int)value;
@@ -437,13 +425,6 @@ void fecgpu_ctx_free(fecgpu_ctx *ctx) {
     for (auto &kv : ctx->sw_event) {
         (void)hipSetDevice(kv.first);
         (void)hipEventDestroy(kv.second);
-    }
-    for (auto &kv : ctx->sw_fork) {
-        (void)hipSetDevice(kv.first);
-        (void)hipStreamSynchronize(kv.second.st);
-        (void)hipStreamDestroy(kv.second.st);
-        (void)hipEventDestroy(kv.second.fork);
-        (void)hipEventDestroy(kv.second.join);
     }
     for (auto &kv : ctx->conn_streams) {
         (void)hipSetDevice(kv.first);
@@ -1456,33 +1437,6 @@ ssize_t ctx_sw_end(fecgpu_ctx *ctx, hipStream_t s) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
     HIP_TRY(hipEventRecord(ctx->sw_event[dev], s), "hipEventRecord");
-    return 0;
-}
-
-ssize_t ctx_sw_fork(fecgpu_ctx *ctx, hipStream_t s, hipStream_t *s2) {
-    *s2 = nullptr;
-    if (!ctx->sw_overlap) return 0;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    fecgpu_ctx::SwFork &f = ctx->sw_fork[dev];
-    if (!f.st) {
-        HIP_TRY(hipStreamCreateWithFlags(&f.st, hipStreamNonBlocking), "hipStreamCreate");
-        HIP_TRY(hipEventCreateWithFlags(&f.fork, hipEventDisableTiming), "hipEventCreate");
-        HIP_TRY(hipEventCreateWithFlags(&f.join, hipEventDisableTiming), "hipEventCreate");
-    }
-    HIP_TRY(hipEventRecord(f.fork, s), "hipEventRecord");
-    HIP_TRY(hipStreamWaitEvent(f.st, f.fork, 0), "hipStreamWaitEvent");
-    *s2 = f.st;
-    return 0;
-}
-
-ssize_t ctx_sw_join(fecgpu_ctx *ctx, hipStream_t s, hipStream_t s2) {
-    if (!s2) return 0;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    fecgpu_ctx::SwFork &f = ctx->sw_fork[dev];
-    HIP_TRY(hipEventRecord(f.join, s2), "hipEventRecord");
-    HIP_TRY(hipStreamWaitEvent(s, f.join, 0), "hipStreamWaitEvent");
     return 0;
 }
 

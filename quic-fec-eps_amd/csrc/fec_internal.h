@@ -571,10 +571,5 @@ ssize_t ctx_rlc_table(fecgpu_ctx *ctx, hipStream_t s, const uint8_t **tab);
 ssize_t ctx_sw_wait(fecgpu_ctx *ctx);
 ssize_t ctx_sw_begin(fecgpu_ctx *ctx, hipStream_t s);
 ssize_t ctx_sw_end(fecgpu_ctx *ctx, hipStream_t s);
-// A second stream of the current device for work of one call that runs
-// beside the rest: fork = *s2 waits for what `s` holds so far (nullptr when
-// the ctx's "sw_overlap" tuning is 0); join = `s` waits for what *s2 holds.
-ssize_t ctx_sw_fork(fecgpu_ctx *ctx, hipStream_t s, hipStream_t *s2);
-ssize_t ctx_sw_join(fecgpu_ctx *ctx, hipStream_t s, hipStream_t s2);
 
 }  // namespace fecgpu

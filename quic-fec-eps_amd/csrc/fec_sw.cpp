@@ -345,15 +345,9 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
         a.lb_ticket = lb.ticket;
     }
     SW_TRY(launch_sw_dec_plan(a, s), "sliding-window decode plan launch");
-    // The plan writes every syndrome job (one-unknown systems' in the lost
-    // slots, the larger systems' equations in their repairs' slots, lost
-    // positions zeroed), so the syndrome pass runs on a second stream beside
-    // the systems and long-system passes (which write solve jobs and logs
-    // only; the long pass rewrites its equations' rows and jobs with the same
-    // bytes) and joins before the solves.  (r05: a split of the syndrome pass
-    // alone measured slower, 0.209 vs 0.197 ms.)
-    hipStream_t s2 = nullptr;
-    RC_TRY(ctx_sw_fork(ctx, s, &s2));
+    // (the one-unknown systems' syndromes on a second stream beside the
+    // systems launch, joined at the end, measured 0.209 vs 0.197 ms per cfg7
+    // call, r05: removed)
     SW_TRY(launch_sw_dec_sys(a, s), "sliding-window decode systems launch");
     SW_TRY(launch_sw_dec_long(a, s), "sliding-window long-system plan launch");
     const uint32_t ncol = (S + 15u) >> 4;
@@ -390,8 +384,7 @@ ssize_t sw_decode_core(fecgpu_ctx *ctx, uint8_t *src, const uint8_t *present, ui
     range(sa, 1, rep, nrep * stride);
     range(sa, 2, psyn, nrep * stride);
     sa.budget = ncol >= 64 ? kCombBudgetWide : kCombBudget;
-    SW_TRY(launch_comb(sa, 1, s2 ? s2 : s), "sliding-window syndrome launch");
-    RC_TRY(ctx_sw_join(ctx, s, s2));
+    SW_TRY(launch_comb(sa, 1, s), "sliding-window syndrome launch");
     CombArgs va = sa;
     va.jobs = a.sol_jobs;
     va.coef = a.sol_coef;

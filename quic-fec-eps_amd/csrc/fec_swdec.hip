@@ -326,36 +326,15 @@ struct RlcSeq {
     }
 };
 
-// RFC 8681 coefficient j of repair h (the table row for dense repairs)
-__device__ __forceinline__ uint8_t coef_at(const SwDecArgs &a, const fecgpu_sw_repair &h, uint32_t j) {
-    // RFC 8681 coefficient j
-    if (const uint4 *row = rlc_row(a, h)) return reinterpret_cast<const uint8_t *>(row)[j];
-    Tinymt32 st;
-    tinymt32_init(st, h.key);
-    const uint32_t dt = h.dt;
-    uint32_t c = 0;
-    for (uint32_t q = 0; q <= j; q++) {
-        c = 0;
-        if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
-            do {
-                c = tinymt32_u32(st) & 0xFFu;
-            } while (c == 0);
-        }
-    }
-    return (uint8_t)c;
-}
-
 // ============================================================= systems ===
 // Small systems are solved by one wave each with [A | I] in LDS: "tiny" ones
 // (e <= 16, p <= 48) in the wave's own 3 KB, larger ones (e <= 64, p <= 96)
 // in one of the block's shared mid-size regions, taken under an LDS lock.
-// Syndrome job / row of equation t: slot t, written by the plan (lost
-// positions zeroed) for every received repair holding a lost source of a
-// system of more than one unknown; a system's solve reads its syndrome rows
-// t_first .. t_last (the repairs in between that are not its equations get
-// coefficient 0: the ranges of two systems never interleave, since a repair
-// between two equations of one system that held a lost source of another
-// would link them).
+// Syndrome job / row of equation t: slot t (the plan empties every slot); a
+// system's solve reads its syndrome rows t_first ..
+// t_last (the repairs in between that are not its equations get coefficient
+// 0: the ranges of two systems never interleave, since a repair between two
+// equations of one system that held a lost source of another would link them).
 constexpr int kSwTinyE = 16, kSwTinyP = 48;
 constexpr int kSwSolveIn = 128;  // widest syndrome range a small system's solve reads
 
@@ -365,9 +344,8 @@ struct SysLds {
     uint8_t M[MP * kPitch];
     uint32_t U[ME];
     uint32_t eq[MP];
-    uint64_t efss[MP];  // the equations' headers, kept from the candidate scan
-    uint16_t enss[MP], ekey[MP];
-    uint8_t edt[MP];
+    uint64_t efss[MP];  // the equations' windows, kept from the candidate scan
+    uint16_t enss[MP];
     int8_t piv[ME];
 };
 
@@ -391,21 +369,34 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     for (int q = lane; q < p; q += 64) {
         const uint32_t t = eq[q];
         if (!SWC(t, a.nrep, kChkHdr)) continue;
-        fecgpu_sw_repair h{};  // (the scan's copy)
+        fecgpu_sw_repair h{};  // (the scan's copy: fss and nss)
         h.fss = S.efss[q];
         h.nss = S.enss[q];
-        h.key = S.ekey[q];
-        h.dt = S.edt[q];
-        // the unknowns' coefficients into A (the unknowns are ascending; the
-        // window holds a run of them), from the coefficient table (dense rows)
-        // or the PRNG: the plan wrote the syndrome job and its row with these
-        // zeroed, and the syndrome pass may be reading it now
-        for (int u = 0; u < e; u++) {
-            const uint64_t i = U[u];
-            if (i < h.fss) continue;
-            if (i >= h.fss + h.nss) break;
-            M[q * kPitch + u] = coef_at(a, h, (uint32_t)(i - h.fss));
+        {
+            // the row was drawn by the plan: move the unknowns' entries into A
+            // (the unknowns are ascending; the window holds a run of them).
+            // (Reading dense rows from the table here instead, with the
+            // unknowns zeroed as the row goes out, cost the system pass 23 us
+            // on cfg7, r04: serial LDS lookups per coefficient.)
+            uint8_t *cb = a.coef + (uint64_t)t * kSwCoefPitch;
+            for (int u = 0; u < e; u++) {
+                const uint64_t i = U[u];
+                if (i < h.fss) continue;
+                if (i >= h.fss + h.nss) break;
+                if (!SWC(i - h.fss, kSwCoefPitch, kChkSynJob)) break;
+                M[q * kPitch + u] = cb[i - h.fss];
+                cb[i - h.fss] = 0;
+            }
         }
+        CombJob J;
+        J.in_off = h.fss * a.stride;
+        J.coef_off = (uint64_t)t * kSwCoefPitch;
+        J.out_list = t;
+        J.xor_off = (uint64_t)t * a.stride;
+        J.nin = h.nss;
+        J.nout = 1;
+        a.syn_jobs[t] = J;
+        a.syn_outs[t] = (uint64_t)t * a.stride;
     }
     SWD_WAVE_SYNC();
     uint64_t used0 = 0, used1 = 0;  // wave-uniform: rows 0..63, 64..127 already pivots
@@ -453,10 +444,39 @@ __device__ int small_solve(const SwDecArgs &a, const GfLds &g, uint32_t x, int e
     }
     const uint64_t dm = __ballot(det);
     const int ndet = __popcll(dm);
+    // syndromes no solve reads (non-pivot rows, undetermined unknowns' rows)
+    // are not computed: only pivot rows can appear in a solve row
+    for (int q = lane; q < p; q += 64) {
+        bool need = false;
+        for (int col = 0; col < e && !need; col++) need = ((dm >> col) & 1) && M[S.piv[col] * kPitch + e + q] != 0;
+        if (!need && SWC(eq[q], a.nrep, kChkSynJob)) a.syn_jobs[eq[q]].nout = 0;
+    }
     if (ndet == 0) return 0;
-    // (every equation's syndrome is computed, pivots or not: the plan wrote
-    // the jobs before this pass ran, and one-unknown systems here solve
-    // through a solve job like the others)
+    // One unknown (most systems at low loss): x = s_t / c for the pivot
+    // equation t, s_t = repair_t + sum of its received sources' terms.  Its
+    // syndrome job computes x directly: coefficients times 1/c, the repair row
+    // times 1/c (kCombXorScaled), output the lost source's row.  No syndrome
+    // row, no solve job.  Nothing else reads that row with a nonzero
+    // coefficient: a received repair holding it is an equation of this system.
+    if (e == 1) {
+        const int pr = S.piv[0];
+        const uint32_t t = eq[pr];
+        const uint32_t iv = M[pr * kPitch + e + pr];  // T[pr][pr] = 1 / c
+        if (!SWC(t, a.nrep, kChkSynJob) || !SWC(U[0], a.nsrc, kChkSrcRow)) return 0;
+        const uint32_t nss = S.enss[pr];
+        uint32_t *cc = reinterpret_cast<uint32_t *>(a.coef + (uint64_t)t * kSwCoefPitch);
+        uint32_t tab[5];
+        set_tab(tab, iv);
+        for (uint32_t j = lane; j < (nss + 3) / 4; j += 64) cc[j] = tmul(cc[j], tab);
+        SWD_WAVE_SYNC();
+        if (lane == 0) {
+            a.coef[(uint64_t)t * kSwCoefPitch + nss] = (uint8_t)iv;  // nss < kSwCoefPitch
+            a.syn_jobs[t].nout = 1u | kCombXorScaled;
+            a.syn_outs[t] = (uint64_t)(a.src + (uint64_t)U[0] * a.stride) - (uint64_t)a.synd;
+            a.stat[U[0]] = FECGPU_STATUS_OK;
+        }
+        return 1;
+    }
     // solve jobs (ndet <= e): inputs the syndrome rows t_first .. t_last,
     // coefficients at 64 bytes per repair from t_first (ndet <= 64, so
     // ndet * nin fits), kSwSolveOut outputs per job, in the system's unknown
@@ -523,8 +543,6 @@ __device__ bool sys_one(const SwDecArgs &a, const GfLds &g, SysLds<ME, MP> &S, u
                 S.eq[q] = (uint32_t)t;
                 S.efss[q] = h.fss;
                 S.enss[q] = h.nss;
-                S.ekey[q] = h.key;
-                S.edt[q] = h.dt;
             }
             p += n;
         }
@@ -576,6 +594,18 @@ __device__ __forceinline__ void block_counts(const SwDecArgs &a, uint32_t rec, u
         if (r) atomicAdd(&a.ctr->recovered, r);
         if (m) atomicMax(&a.ctr->maxin, m);
     }
+}
+
+// The RFC 8681 coefficients of a received repair whose window holds a lost
+// source, into its syndrome coefficient row (the plan, a thread per repair).
+// The system pass then reads them (small_solve moves the unknowns' entries
+// into A and zeroes them): every lane of a wave draws one, instead of a wave
+// per system drawing its few equations' on as many lanes.  The long-system
+// pass draws its own rows again (and overwrites these).
+__device__ __forceinline__ void draw_row(const SwDecArgs &a, uint64_t t, const fecgpu_sw_repair &h) {
+    if (!SWC(t, a.nrep, kChkSynJob)) return;
+    uint4 *cc = reinterpret_cast<uint4 *>(a.coef + t * kSwCoefPitch);
+    rlc_quads(a, h, [&](uint32_t g, uint4 v) { cc[g] = v; });
 }
 
 // ======================================================= fused plan ===
@@ -643,6 +673,23 @@ __device__ __forceinline__ LbRec lb_read(const uint4 *src2) {
 // small_solve's one-unknown case).  lkind[x] tells the system pass what is left: 0 a member
 // of a larger system, 1 recovered here, 2 a larger system's first unknown,
 // 3 alone but undetermined.
+__device__ __forceinline__ uint8_t coef_at(const SwDecArgs &a, const fecgpu_sw_repair &h, uint32_t j) {
+    // RFC 8681 coefficient j
+    if (const uint4 *row = rlc_row(a, h)) return reinterpret_cast<const uint8_t *>(row)[j];
+    Tinymt32 st;
+    tinymt32_init(st, h.key);
+    const uint32_t dt = h.dt;
+    uint32_t c = 0;
+    for (uint32_t q = 0; q <= j; q++) {
+        c = 0;
+        if (dt == 15 || (tinymt32_u32(st) & 0xFu) <= dt) {
+            do {
+                c = tinymt32_u32(st) & 0xFFu;
+            } while (c == 0);
+        }
+    }
+    return (uint8_t)c;
+}
 
 #ifndef FECGPU_SWD_TRACE
 #define FECGPU_SWD_TRACE 0  // measurement aid: the plan kernel prints its phases' times (3 blocks)
@@ -1046,32 +1093,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         // own stops before the next.  (At 2 % loss most rows drawn were such
         // systems' and went unused; their scattered dword stores cost the
         // plan ~15 us on cfg7, r05 trace.)
-        // Exact (the final classification below agrees) for a lost source
-        // past the earlier chunks' reach (pos >= wmb_all: no window from
-        // before the chunk holds it, so the look-back changes nothing); the
-        // next lost source from the chunk or its halo.
         const auto alone = [&](uint32_t k) {
-            const uint32_t pos = s_lpos[k];
-            if (a.long_min <= 1 || pos < wmb_all || (k > 0 && s_rl[k - 1] > i0 + pos)) return false;
-            uint64_t nxt = ~0ull;
-            if (k + 1 < nl) {
-                nxt = i0 + s_lpos[k + 1];
-            } else {
-                for (uint32_t w = (pos + 1) >> 5; w < (kPlanChunk + kPlanHalo) / 32 && nxt == ~0ull; w++) {
-                    uint32_t bits = s_bits[w];
-                    if (w == (pos + 1) >> 5) bits &= ~((1u << ((pos + 1) & 31)) - 1u);
-                    if (bits) nxt = i0 + w * 32 + __ffs(bits) - 1;
-                }
-            }
-            return nxt == ~0ull || s_rl[k] <= nxt;
-        };
-        // the row with the lost sources' coefficients zeroed (the systems pass
-        // reads those from the table), and its syndrome job: the syndrome
-        // pass needs nothing from the systems pass
-        const auto lost_at = [&](uint32_t b) -> uint32_t {  // 16 lost flags from chunk position b
-            const uint32_t q = b >> 5, w0 = s_bits[q];
-            const uint32_t w1 = q + 1 < (kPlanChunk + kPlanHalo) / 32 ? s_bits[q + 1] : 0u;
-            return (uint32_t)(((uint64_t)w0 | (uint64_t)w1 << 32) >> (b & 31)) & 0xFFFFu;
+            return a.long_min > 1 && k > 0 && k + 1 < nl && s_lpos[k] >= wmb_all &&
+                   s_rl[k - 1] <= i0 + s_lpos[k] && s_rl[k] <= i0 + s_lpos[k + 1];
         };
         // pivots first: loads only (behind the draws' stores, their loads
         // waited for those to complete: the memory counter is in order)
@@ -1117,30 +1141,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
             if (h.fss < i0 || h.fss >= i1 || !hdr_ok(h, a.nsrc)) continue;
             const uint32_t lo = (uint32_t)(h.fss - i0), hi = lo + h.nss;  // hi <= chunk + halo
             const uint32_t bl = before(lo), bh = before(hi);
-            if (bh > bl && !(bh == bl + 1 && alone(bl)) && SWC(t, a.nrep, kChkSynJob)) {
-                uint4 *cc = reinterpret_cast<uint4 *>(a.coef + t * kSwCoefPitch);
-                rlc_quads(a, h, [&](uint32_t g, uint4 v) {
-                    const uint32_t m = lost_at(lo + 16 * g);
-                    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int d = 0; d < 4; d++) {
-                        const uint32_t n4 = (m >> (4 * d)) & 0xFu;
-                        const uint32_t z = ((n4 & 1u) ? 0xFFu : 0u) | ((n4 & 2u) ? 0xFF00u : 0u) |
-                                           ((n4 & 4u) ? 0xFF0000u : 0u) | ((n4 & 8u) ? 0xFF000000u : 0u);
-                        w[d] &= ~z;
-                    }
-                    cc[g] = make_uint4(w[0], w[1], w[2], w[3]);
-                });
-                CombJob J;
-                J.in_off = h.fss * a.stride;
-                J.coef_off = t * kSwCoefPitch;
-                J.out_list = t;
-                J.xor_off = t * a.stride;
-                J.nin = h.nss;
-                J.nout = 1;
-                a.syn_jobs[t] = J;
-                a.syn_outs[t] = t * a.stride;
-            }
+            if (bh > bl && !(bh == bl + 1 && alone(bl))) draw_row(a, t, h);
         }
 #if FECGPU_SWD_TRACE
         if (tid == 64) s_tr[12] = wall_clock64();  // wave 1: its row draws issued

@@ -217,15 +217,6 @@ for s in "$@"; do
                 FECGPU_LIB=$v step abbsdu_w120_$n 300 python bench.py --k 120 --r 8 --steps 10 --warmup 3 \
                     --cpu-seconds 0 --no-verify
             done ;;
-        abov)  # cfg7: syndrome pass beside the systems passes (1) or after them (0), interleaved 3 times
-            for rep in 1 2 3; do
-                for f in 1 0; do
-                    step abov_${f}_$rep 300 python bench.py --config 7 --steps 50 --warmup 10 --cpu-seconds 0 \
-                        --no-verify --extra-configs 0 --sw-overlap $f
-                done
-            done ;;
-        swchk) step swchk 300 python -u -m pytest tests/test_gpu_boundscheck.py -q -x -k "sw" -p no:cacheprovider \
-                    --timeout 120 --timeout-method thread ;;
         gpufix) step gpufix 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_sw.py \
                     tests/test_gpu_boundscheck.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         bsdtests) step bsdtests 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_boundscheck.py \
