@@ -2097,9 +2097,9 @@ __device__ __forceinline__ void comb_slot(const uint8_t *rs, uint32_t stride, in
 }
 
 // rows per prefetched batch of the one-output slots (cfg7 decode: 4 rows 0.214
-// vs 8 rows 0.223 ms per call, r04: 107 VGPRs, 4 waves per SIMD).  The
-// 8-output slots do not prefetch (221 VGPRs instead of 128: cfg7 decode 0.246
-// vs 0.238 ms, r04).
+// vs 8 rows 0.223 ms per call, r04: 107 VGPRs, 4 waves per SIMD; 5 and 6 rows,
+// 115 / 123 VGPRs, within 1 % of 4, r05).  The 8-output slots do not prefetch
+// (221 VGPRs instead of 128: cfg7 decode 0.246 vs 0.238 ms, r04).
 constexpr int kCombPfU = 4;
 // comb_slot with the rows of batch i + 1 in flight while batch i multiplies
 // (two 8-row buffers) and the xor row loaded with the first batch.  A
