@@ -1204,8 +1204,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         a.reach[a.nsrc] = off;
         a.rcnt[a.nsrc] = repc;
     }
-    // s_rcnt is read above and reused for the starts list below
-    __syncthreads();
+    // (no barrier: the starts list below goes to s_rf, free since the pivot
+    // searches, so the lost-list stores above and the one-unknown jobs below
+    // complete together, r05)
     SWD_TRACE(8);
     // the chunk's lost sources: one-unknown systems solved, the rest classified
     for (uint32_t k = tid; k < nl; k += kBlock) {
@@ -1280,7 +1281,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
         a.syn_jobs[a.nrep + u] = J;
         a.lkind[u] = kind;
         if (kind == 1) atomicAdd(&s_nsg, 1u);
-        if (kind == 2) s_rcnt[atomicAdd(&s_nst, 1u)] = u;  // s_rcnt is free after the lost list
+        if (kind == 2) s_rf[atomicAdd(&s_nst, 1u)] = u;  // s_rf (the pivot searches') is free now
     }
     // the chunk's larger-system starts onto the call's list (one atomic per block;
     // ticket[2] / [3] count starts / singles and are cleared by the last block out)
@@ -1295,7 +1296,7 @@ __global__ __launch_bounds__(kBlock) void sw_dec_plan_kernel(SwDecArgs a) {
     if ((uint64_t)s_stbase + s_nst > a.nsrc) {
         if (tid == 0) atomicOr(&a.lb_ticket[4], kSwErrInternal);  // into the counters by the last block out
     } else {
-        for (uint32_t k = tid; k < s_nst; k += kBlock) a.starts[s_stbase + k] = s_rcnt[k];
+        for (uint32_t k = tid; k < s_nst; k += kBlock) a.starts[s_stbase + k] = s_rf[k];
     }
     // the last block out writes the call's counters (nothing was cleared before
     // the launch) and resets the tickets for the next launch
