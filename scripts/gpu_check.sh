@@ -217,6 +217,16 @@ for s in "$@"; do
                 FECGPU_LIB=$v step abbsdu_w120_$n 300 python bench.py --k 120 --r 8 --steps 10 --warmup 3 \
                     --cpu-seconds 0 --no-verify
             done ;;
+        abpf)  # cfg4: bit-sliced encode, default vs lib/libfecgpu_bspf*.so (prefetching batches), interleaved twice
+            for rep in 1 2; do
+                step abpf_base_$rep 300 python bench.py --config 4 --steps 10 --warmup 2 --cpu-seconds 0 --no-verify \
+                    --extra-configs 0
+                for v in quic-fec-eps_amd/lib/libfecgpu_bspf*.so; do
+                    n=$(basename $v .so); n=${n#libfecgpu_}
+                    FECGPU_LIB=$v step abpf_${n}_$rep 300 python bench.py --config 4 --steps 10 --warmup 2 --cpu-seconds 0 \
+                        --no-verify --extra-configs 0
+                done
+            done ;;
         gpufix) step gpufix 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_sw.py \
                     tests/test_gpu_boundscheck.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         bsdtests) step bsdtests 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_boundscheck.py \
