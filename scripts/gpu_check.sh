@@ -222,6 +222,7 @@ for s in "$@"; do
                 step abpf_base_$rep 300 python bench.py --config 4 --steps 10 --warmup 2 --cpu-seconds 0 --no-verify \
                     --extra-configs 0
                 for v in quic-fec-eps_amd/lib/libfecgpu_bspf*.so; do
+                    [ -e "$v" ] || continue
                     n=$(basename $v .so); n=${n#libfecgpu_}
                     FECGPU_LIB=$v step abpf_${n}_$rep 300 python bench.py --config 4 --steps 10 --warmup 2 --cpu-seconds 0 \
                         --no-verify --extra-configs 0
