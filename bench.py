@@ -75,8 +75,9 @@ def parse():
     ap.add_argument("--bs-passes", type=int, default=0,
                     help="tuning: bit-sliced encode on per-window lengths, 256-unit passes per window group")
     ap.add_argument("--wpb", type=int, default=0, help="tuning: windows per workgroup")
-    ap.add_argument("--bsd-min-e", type=int, default=-1,
-                    help="tuning: GF decode erasures from which a window takes the bit-sliced decode (0 = never)")
+    ap.add_argument("--gs", type=int, choices=[0, 1], default=None,
+                    help="tuning: bit-sliced encode of short uniform rows with the repairs stored through LDS "
+                         "(1, default) or the flat bit-sliced kernel (0)")
     ap.add_argument("--bpc", type=int, default=0, help="tuning: persistent workgroups per CU")
     ap.add_argument("--sw-long-min", type=int, default=0,
                     help="tuning (config 7): unknowns from which a linked system takes the banded long path")
@@ -334,8 +335,8 @@ def make_ctx(args):
         ctx.set_tuning("bs_passes", args.bs_passes)
     if args.wpb:
         ctx.set_tuning("wpb", args.wpb)
-    if args.bsd_min_e >= 0:
-        ctx.set_tuning("bsd_min_e", args.bsd_min_e)
+    if args.gs is not None:
+        ctx.set_tuning("gs", args.gs)
     if args.bpc:
         ctx.set_tuning("blocks_per_cu", args.bpc)
     if args.sw_group:
@@ -472,6 +473,9 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
     # fails the line
     async_errors = ctx.sw_decode_errors() if cfg.scheme == "sw" else None
     elapsed, tot = shard.reduce_run(elapsed, src_bytes, dev if args.dist_backend == "nccl" else None)
+    # every rank's own HIP-event kernel times (north_star: the roofline fraction
+    # at 1, 2, 4 and 8 GPUs per GPU, not rank 0's alone)
+    rank_ms = shard.gather_floats([enc_ms, dec_ms], dev if args.dist_backend == "nccl" else None)
     total_src = float(tot) * steps
     value = total_src / elapsed / 1e9
 
@@ -564,6 +568,7 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
             "traffic": traffic,
             "traffic_source": traffic_src,
             "alg_bytes_per_launch": (batch_pcie[dom][bound_dir] if cfg.host else alg[dom]),
+            **({} if cfg.host else {"per_rank": shard.per_rank_roofline(rank_ms, alg, peak)}),
             **({"pcie_directions": pcie,
                 "note": "bytes of the bound direction of the slower call / its host wall time, "
                         "against 63 GB/s per direction"} if cfg.host else {}),

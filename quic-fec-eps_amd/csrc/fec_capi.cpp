@@ -153,13 +153,9 @@ struct fecgpu_ctx {
     size_t pinned_cache_cap = (size_t)1 << 30;
     // bit-sliced encode in group mode: passes per group at the longest window
     int bs_passes = 8;
-    // GF decode: windows with at least this many erasures take the bit-sliced
-    // decode (fec_kernels.hip gf_decode_bs_kernel; 0 = never, and the wide
-    // codes decode in two stages).  Off by default: on cfg4 the
-    // table decode hides those windows' VALU cost in its memory-bound stream
-    // (4.65 vs 4.96 ms with 6), and the two-stage wide decode measured 1.67
-    // vs 1.81 ms at k120 (r05)
-    int bsd_min_e = 0;
+    // bit-sliced encode of short uniform rows with gathered stores
+    // (gf_encode_bs_gs_kernel): 1 on, 0 the flat bit-sliced kernel
+    int gs = 1;
     int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
     int sw_stream = kSwStreamDefault;  // sliding-window encode: 0 combine jobs, 1..5 streaming
                                        // (dwords per lane), kSwStreamAuto per symbol size
@@ -319,9 +315,9 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
         ctx->fault_launches = (int)value;
         return 0;
     }
-    if (!std::strcmp(key, "bsd_min_e")) {
-        if (value < 0 || value > kMaxR) return FECGPU_ERR_INVALID_ARG;
-        ctx->bsd_min_e = (int)value;
+    if (!std::strcmp(key, "gs")) {
+        if (value < 0 || value > 1) return FECGPU_ERR_INVALID_ARG;
+        ctx->gs = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "bs_passes")) {
@@ -536,26 +532,6 @@ ssize_t get_enc_tables(fecgpu_ctx *ctx, const fecgpu_code *code, EncTables &out)
     return 0;
 }
 
-// Bit-sliced decode: windows per group for windows of ncol 16-B columns in
-// units of `cols` columns, their regions within 40 KB of LDS: the largest
-// group whose passes of the workgroup are >= 97 % full, else the largest of
-// the fullest (k120 at 1200 B, 19 units per window: 26 windows, 494 units).
-int bsd_wpb(uint32_t ncol, uint32_t cols) {
-    const uint32_t units = std::max<uint32_t>(1, (ncol + cols - 1) / cols);
-    const int cap = std::min<int>(kMaxWpb, (int)((40u << 10) / sizeof(BsdRegion)));
-    int best = 1;
-    double best_u = 0.0;
-    for (int w = 1; w <= cap; w++) {
-        const uint64_t n = (uint64_t)w * units, passes = (n + kBlock - 1) / kBlock;
-        const double u = (double)n / (double)(passes * kBlock);
-        if (u >= 0.97 || u >= best_u - 1e-9) {  // ties: the larger group
-            best = w;
-            best_u = std::max(best_u, u);
-        }
-    }
-    return best;
-}
-
 // Windows per workgroup: fill the 256 lanes with whole passes over the
 // flattened column range while keeping the LDS footprint small enough for
 // >= 4 workgroups per CU.
@@ -729,35 +705,8 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
     ChkRec *chk = nullptr;
     rc = ctx_chk_record(ctx, &chk);
     if (rc) return rc;
-    if (decode && mP && ctx->bsd_min_e > 0) {
-        // the bit-sliced decode (tuning "bsd_min_e" 0: the two-stage one;
-        // fec_kernels.hip gf_decode_bs_kernel): a plan
-        // per window in LDS, syndromes of the received sources by the plane
-        // picks of P, the solve on the unit's columns; one launch, no scratch
-        BatchArgs a{};
-        a.win = win;
-        a.sym_len = sym_len;
-        a.S_all = sym_len_all;
-        a.stride = stride;
-        a.wpitch = (uint64_t)n * stride;
-        a.present = present;
-        a.status = status;
-        a.nwin = nwin;
-        a.k = k;
-        a.r = r;
-        a.nw = (n + 63) / 64;
-        a.prows = P;
-        a.enc_bs = mPI;  // [P | I]: the pivot repairs add themselves to their syndromes
-        void *rp = nullptr;
-        rc = ctx_sw_scratch(ctx, 11, nwin * sizeof(BsdRec), &rp);
-        if (rc) return rc;
-        a.bsd_rec = static_cast<BsdRec *>(rp);
-        a.wpb = bsd_wpb(ncol, kRbsCols);
-        a.chk.lo[0] = reinterpret_cast<uint64_t>(win);
-        a.chk.n[0] = nwin * a.wpitch;
-        HIP_TRY(launch_decode_bs(a, (int)code->matrix, s), "wide bit-sliced decode launch");
-    } else {
-        // the two-stage decode (fec_wide.hip; no plane picks: bitslice off or r < 4)
+    {
+        // the two-stage decode (fec_wide.hip; plane picks when bitslice is on and r >= 4)
         const auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
         const size_t o_out = up(nwin * sizeof(CombJob)), o_coef = o_out + up(nwin * kMaxR * sizeof(uint64_t));
         const size_t coef_bytes = decode ? nwin * kMaxR * (size_t)kMaxR : 0;
@@ -958,19 +907,6 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
             rc = get_enc_tables(ctx, code, t);
             if (rc) return rc;
             a.coef = t.coef;  // non-Cauchy matrices: the plan reads the parity rows
-            // windows with many erasures: the bit-sliced decode after the table
-            // kernel (codes with compiled plane masks; device windows in place,
-            // uniform stride; the routed windows are scattered, which the
-            // runtime-mask kernel's buffer resource over a group cannot span)
-            if (ctx->bsd_min_e > 0 && ctx->bitslice && !remote && !win_off && !a.out_delta &&
-                r >= ctx->bsd_min_e && bitslice_supported(k, r, (int)code->matrix)) {
-                a.bsd_min_e = ctx->bsd_min_e;
-                a.bsd_cauchy = code->matrix == FECGPU_MATRIX_CAUCHY;
-                a.prows = t.rows;
-                a.nw = 1;
-                p.matrix = (int)code->matrix;
-                p.bsd_wpb = bsd_wpb(ncol ? ncol : stride >> 4, 2);
-            }
             p.win_lds = gf_dec_win_lds(k, r);
             p.wpb = choose_wpb(ncol, p.win_lds, 40 * 1024);
             p.lds_bytes = p.win_lds * (uint32_t)p.wpb;
@@ -999,6 +935,20 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         const uint32_t units = ncol ? (ncol + 1) / 2 : (uint32_t)((stride >> 4) + 1) / 2;
         const uint32_t want = (uint32_t)ctx->bs_passes * kBlock;
         p.wpb = units ? std::max(1, std::min<int>(kMaxWpb, (int)((want + units - 1) / units))) : kMaxWpb;
+        // uniform short rows: whole windows per step, repairs stored through LDS
+        // (gf_encode_bs_gs_kernel; both images within 64 KB), at the workgroups
+        // the LDS allows (2 per CU at cfg3) unless a grid is forced
+        if (p.flat && ctx->gs && ctx->wpb_override <= 0 && ncol && units <= (uint32_t)kBlock) {
+            const uint32_t img = 2u * (uint32_t)r * ncol * 16u;  // one window, both images
+            const uint32_t G = std::min<uint32_t>((uint32_t)kBlock / units, (64u << 10) / img);
+            if (G >= 1) {
+                p.bsgs = true;
+                p.flat = false;
+                p.wpb = (int)G;
+                p.lds_bytes = G * img;
+                if (p.grid_mult <= 0 && p.blocks_per_cu <= 0) p.grid_mult = 1;
+            }
+        }
     }
     else if (!decode && scheme == FECGPU_SCHEME_GF256 && !remote && ctx->bitslice && r >= kRbsMinR) {
         // no compiled masks for this code: the runtime-mask kernel, same unit
@@ -1031,22 +981,8 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
     rc = set_check_ranges(ctx, code, decode, a, s);
     if (rc) return rc;
 #endif
-    if (a.bsd_min_e) {  // the routed windows' flags: ctx scratch, ordered like the SW calls'
-        rc = ctx_sw_begin(ctx, s);
-        if (rc) return rc;
-        void *lp = nullptr;
-        const size_t o_rec = (a.nwin + 255) & ~size_t(255);
-        rc = ctx_sw_scratch(ctx, 12, o_rec + a.nwin * sizeof(BsdRec), &lp);
-        if (rc) return rc;
-        a.bsd_flag = static_cast<uint8_t *>(lp);  // every window's written by the table decode's plan
-        a.bsd_rec = reinterpret_cast<BsdRec *>(static_cast<uint8_t *>(lp) + o_rec);  // the routed windows' plans
-    }
     hipError_t e = decode ? launch_decode(scheme, a, p, s) : launch_encode(scheme, a, p, s);
     if (e != hipSuccess) return dev_err(e, decode ? "decode launch" : "encode launch");
-    if (a.bsd_min_e) {
-        rc = ctx_sw_end(ctx, s);
-        if (rc) return rc;
-    }
 #if FECGPU_CHECK
     HIP_TRY(hipStreamSynchronize(s), "check: sync");
     uint64_t nbad = 0, first = 0;

@@ -86,49 +86,7 @@ struct BatchArgs {
     // round_up(S_w, 16)
     uint32_t off_stride;
     ChkRange chk;              // FECGPU_CHECK builds: where this launch's symbols lie
-    // bit-sliced decode of windows with many erasures (gf_decode_bs_kernel):
-    // the table decode's plan flags windows with e >= bsd_min_e (0: none) in
-    // bsd_flag[w] (1, else 0: it writes every window's), and the bit-sliced
-    // kernel takes them range by range in batch order, planning them from the
-    // parity rows prows P[r][k] (any matrix).  Without flags it takes every
-    // window (the wide codes).  nw: present-mask words per window (1, or
-    // ceil((k + r) / 64) for the wide codes).
-    const uint8_t *prows;
-    struct BsdRec *bsd_rec;  // the windows' plans (indexed by window)
-    uint8_t *bsd_flag;
-    int bsd_range;  // flagged windows: windows per range (launch_decode_bs)
-    int bsd_min_e;
-    int nw;
-    int bsd_cauchy;  // prows are the Cauchy rows (A.2): the closed-form plan
 };
-
-// A window's plan for the bit-sliced decode (global memory, written by the
-// table decode's plan for the windows it routes, or by gf_decode_bs_plan_kernel
-// for the wide codes; read into a BsdRegion): C[u][i] (u * 8 + i), the present
-// words, the missing rows, e (0: nothing to do), the repairs read, the alt row.
-struct BsdRec {
-    uint8_t c[kMaxR * kMaxR];
-    uint64_t pw[4];
-    uint8_t m[kMaxR];
-    uint32_t ne, used, alt, pad;
-    uint8_t pad2[8];
-};
-static_assert(sizeof(BsdRec) == 128, "plan records are 128 B");
-
-// Per-window LDS region of the bit-sliced decode (fec_kernels.hip
-// gf_decode_bs_kernel): the window's stage-2 tables C[u][i] (missing source u
-// from the syndrome of repair i; 20 B each, 8 x 8), its present words, the
-// repairs it reads, a row the missing sources' loads are sent to, the missing
-// rows.
-struct BsdRegion {
-    uint4 ab[kMaxR * kMaxR];
-    uint32_t tc[kMaxR * kMaxR];
-    uint64_t pw[4];
-    uint32_t ne, used, alt, pad;
-    uint8_t m[kMaxR];
-    uint8_t pad2[8];
-};
-static_assert(sizeof(BsdRegion) % 16 == 0, "regions are 16-B aligned");
 
 struct LaunchPlan {
     bool flat;           // uniform S and stride: flat slot space
@@ -142,7 +100,7 @@ struct LaunchPlan {
     bool bitslice;       // GF encode by the bit-sliced kernel (compile-time matrix)
     int matrix;          // bitslice: the code's matrix (fecgpu_matrix)
     bool rbitslice;      // GF encode by the runtime-mask bit-sliced kernel (any matrix)
-    int bsd_wpb;         // bit-sliced decode (a.bsd_min_e > 0): windows per workgroup
+    bool bsgs;           // bit-sliced encode with gathered stores (gf_encode_bs_gs_kernel)
 };
 
 // GF encode of r parity rows goes to the runtime-mask bit-sliced kernel
@@ -177,9 +135,6 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
 ssize_t launch_batch(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, BatchArgs &a,
                      hipStream_t s, bool remote = false, int dev = -1);
 hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s);
-// the bit-sliced decode alone (every window: a.bsd_list null; the wide codes),
-// a.wpb windows per group
-hipError_t launch_decode_bs(BatchArgs a, int matrix, hipStream_t s);
 
 // FECGPU_CHECK builds: symbol accesses outside their launch's ChkRange since
 // the last call (count, first offending address), then resets the record.

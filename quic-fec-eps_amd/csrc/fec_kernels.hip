@@ -450,6 +450,26 @@ __global__ __launch_bounds__(kBlock) GFE_WAVES void gf_encode_kernel(BatchArgs a
     }
 }
 
+// ================================== gathered-store encode (round 6) ===
+// Uniform windows of short symbols (a row of at most kBlock 16-B columns).
+// A 1200-B row is 9.4 128-B lines, and the flat kernels' wave of 64 slots
+// stores a repair row in one or two pieces that straddle windows, so most of
+// a row's lines are completed by two different waves at different times.
+// The same HBM bytes then move at 4.8 TB/s on cfg3's mix against 5.25-5.4
+// when every repair row is stored as one contiguous run
+// (scripts/win_probe.hip, profiles/r06_store_pattern_probe.json).  Here a
+// workgroup takes a.wpb whole windows per step with the flat kernels' lanes
+// (lane = window, 16-B column; rows loaded from HBM as before), writes the
+// repairs to LDS, and after one barrier stores each window's r repair rows
+// front to back, consecutive lanes on consecutive 16-B chunks.  Two LDS
+// images alternate, so the next step's writes never meet this step's reads
+// and one barrier per step suffices.
+struct FastDiv {
+    uint32_t d, m;  // q / d = umulhi(q, m) for q * d < 2^32 (m = ceil(2^32 / d))
+};
+__device__ __forceinline__ FastDiv fdiv_make(uint32_t d) { return {d, d > 1 ? 0xFFFFFFFFu / d + 1u : 0u}; }
+__device__ __forceinline__ uint32_t fdiv(uint32_t q, FastDiv f) { return f.d > 1 ? __umulhi(q, f.m) : q; }
+
 // ================================================ bit-sliced GF encode ===
 // GF encode for codes whose matrix is known at compile time (DESIGN.md §GF
 // bit-slicing).  Multiplying by a constant c is linear over GF(2): output bit
@@ -685,6 +705,53 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
                 bs::unit<K, R, M, kBsU>(pa, pb, g.stride[wl], live, a.out_delta + (w0 + wl) * a.out_wdelta);
             }
             __syncthreads();
+        }
+    }
+}
+
+// Bit-sliced encode of uniform windows with short rows, stores gathered
+// (DESIGN.md §4g): a.wpb whole windows per step (a.wpb * ceil(ncol / 2) <=
+// kBlock units, one pass), a lane per unit with the flat kernel's column pair
+// (u, u + h).  The repair planes, back in bytes, go to an LDS image
+// [window][repair][column]; after one barrier every window's r repair rows
+// are stored front to back, consecutive lanes on consecutive 16-B chunks.
+// Two images alternate, so the next step's writes never meet these reads.
+template <int K, int R, int M>
+__global__ __launch_bounds__(kBlock) void gf_encode_bs_gs_kernel(BatchArgs a) {
+    CHK_PROLOGUE(a);
+    extern __shared__ uint4 dyn[];
+    const uint32_t ncol = a.ncol, h = (ncol + 1) >> 1, G = (uint32_t)a.wpb, per = G * R * ncol;
+    const FastDiv dh = fdiv_make(h), dn = fdiv_make(ncol), drn = fdiv_make(R * ncol);
+    int buf = 0;
+    for (XcdRange xr = xcd_range((a.nwin + G - 1) / G, a.nx); xr.cur < xr.hi; xr.cur += xr.step, buf ^= 1) {
+        const uint64_t w0 = xr.cur * G;
+        const uint32_t nb = (uint32_t)min((uint64_t)G, a.nwin - w0);
+        uint4 *im = dyn + buf * per;
+        const uint32_t nu = nb * h;
+        {
+            // lanes past the last unit redo it and write nothing (uniform trip count)
+            const bool live = threadIdx.x < nu;
+            const uint32_t s = live ? threadIdx.x : nu - 1;
+            const uint32_t wl = fdiv(s, dh), u = s - wl * h;
+            uint8_t *pa, *pb;
+            bs::unit_cols(a.win + (w0 + wl) * a.wpitch, u, h, ncol, pa, pb);
+            uint32_t acc[R][8];
+            bs::sources<K, R, M, kBsUFlat, 0>(pa, pb, a.stride, acc);
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                bs::tr8(acc[i]);
+                if (live) {
+                    im[(wl * R + i) * ncol + u] = make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+                    if (u + h < ncol)
+                        im[(wl * R + i) * ncol + u + h] = make_uint4(acc[i][4], acc[i][5], acc[i][6], acc[i][7]);
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < nb * R * ncol; q += kBlock) {
+            const uint32_t wl = fdiv(q, drn), o = q - wl * R * ncol, i = fdiv(o, dn), c = o - i * ncol;
+            const uint64_t w = w0 + wl;
+            st16(a.win + w * a.wpitch + a.out_delta + w * a.out_wdelta + (size_t)(K + i) * a.stride + c * 16u, im[q]);
         }
     }
 }
@@ -1020,27 +1087,6 @@ __device__ __forceinline__ void plan_offsets(const BatchArgs &a, uint64_t w, int
     if (lane < 8) rg.ooff[lane] = lane < e ? (uint32_t)rg.outsym[lane] * stride : 0u;
 }
 
-// Windows of many erasures go to the bit-sliced decode (gf_decode_bs_kernel
-// below, launched after this kernel over the flags): e >= a.bsd_min_e (0:
-// off).  The window's status is that kernel's to write.  (Lane 0 of the
-// planning wave cleared the flag before the plan: same lane, same address.)
-// ne_out = kBsdRouted tells the kernel to write the window's bit-sliced plan.
-constexpr uint8_t kBsdRouted = 0xFF;
-__device__ __forceinline__ bool bsd_route(const BatchArgs &a, uint64_t w, int e, int lane, uint8_t &ne_out) {
-    if (!a.bsd_min_e || e < a.bsd_min_e) return false;
-    if (lane == 0) {
-        ne_out = kBsdRouted;
-        a.bsd_flag[w] = 1;
-    }
-    return true;
-}
-namespace bsd {
-// (inlined into the table decode's R = 8 kernel only: 156 -> 167 VGPRs, still
-// 3 waves per SIMD; as a call it took 336 B of scratch per lane)
-__device__ void plan(const BatchArgs &a, uint64_t w, int lane, uint8_t *ms, BsdRec *out, const uint8_t *ex,
-                     const uint8_t *lg, const uint8_t *P);
-}
-
 // GF plan (a6/a7) by one wave, closed form.  Missing sources m_0..m_{e-1},
 // the first e present repairs with points x_t = k + sel_t; the system is the
 // Cauchy matrix A[t][u] = 1/(x_t ^ m_u).  Its inverse folded
@@ -1070,7 +1116,6 @@ __device__ void plan_gf(const BatchArgs &a, uint64_t w, uint64_t pres, int lane,
         }
         return;
     }
-    if (bsd_route(a, w, e, lane, ne_out)) return;
     // wave-uniform m_v and x_t (pres is uniform: SGPR bit scans)
     int mv[R], xt[R];
     {
@@ -1168,7 +1213,6 @@ __device__ void plan_gf_mat(const BatchArgs &a, uint64_t w, uint64_t pres, int l
         }
         return;
     }
-    if (bsd_route(a, w, e, lane, ne_out)) return;
     uint64_t mm = miss, rr = rep;
     for (int i = 0; i < lane && i < 8; i++) { mm &= mm - 1; rr &= rr - 1; }
     const int my_m = (int)__ffsll((unsigned long long)mm) - 1;    // lane u < e: u-th missing source
@@ -1342,24 +1386,12 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
                 const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl, i);
                 const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pl >> 32), i);
                 const uint64_t pw = ((uint64_t)hi << 32) | lo;
-                if (a.bsd_min_e && lane == 0) a.bsd_flag[w0 + wl] = 0;  // bsd_route sets it
                 if (a.coef)  // wave-uniform: one code per launch
                     plan_gf_mat<R>(a, w0 + wl, pw, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log,
                                    s_coef, s_ne[wl]);
                 else
                     plan_gf<R>(a, w0 + wl, pw, lane, regions + (size_t)wl * a.win_lds, s_exp, s_log,
                                s_ne[wl]);
-                // routed (codes with compiled plane masks: r = 8): its bit-sliced
-                // plan instead (the region is scratch)
-                if constexpr (R == kMaxR) if (a.bsd_min_e) {
-                    WAVE_SYNC();
-                    if (s_ne[wl] == kBsdRouted) {
-                        bsd::plan(a, w0 + wl, lane, regions + (size_t)wl * a.win_lds, a.bsd_rec + w0 + wl, s_exp,
-                                  s_log, s_coef);
-                        WAVE_SYNC();
-                        if (lane == 0) s_ne[wl] = 0;
-                    }
-                }
             }
         }
         __syncthreads();
@@ -1398,492 +1430,6 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
         }
         __syncthreads();
     }
-}
-
-// ================================= bit-sliced GF decode (many erasures) ===
-//   The table decode costs 5 + 6e VALU per source dword, so
-// windows with many erasures are VALU-bound (e = 8: 2.2-2.8 TB/s).  Here a
-// window is decoded in two stages inside one unit of work:
-//   1. syndromes s_i = rep_i + sum_j P[i][j] src_j over the received sources,
-//      for every repair i, by the bit-sliced products of the encode (compiled
-//      plane masks, bs::, or runtime ones, rbs4::): ~19 VALU per source dword
-//      for all r outputs at once.  A missing source's load goes to a row the
-//      lane reads anyway (BsdRegion::alt) and is masked to zero, so only the
-//      received sources and the repairs the solve uses come from HBM;
-//   2. x_u = sum_i C[u][i] s_i over the pivot repairs (C from the window's
-//      plan: [A | I] reduced with pivot search, A[t][u] = P[sel_t][m_u], as
-//      plan_gf_mat), by the table multiply on the unit's few columns.
-// The plan is one wave per window in LDS, like gf_decode_kernel's (Cauchy
-// rows in closed form as plan_gf, other rows by elimination).  Windows
-// come in groups of a.wpb from a.bsd_list (routed by the table decode's plan)
-// or, with no list, every window (the wide codes).
-namespace bsd {
-
-constexpr int kRsrcRaw = 0x00020000;  // buffer resource word 3: raw 32-bit data (gfx9)
-
-// One wave: the plan of window w into its record (status too).  ms: 8 bytes
-// of LDS for the missing rows; P: parity rows [r][k] in LDS (unused for the
-// Cauchy rows, a.bsd_cauchy).
-__device__ void plan(const BatchArgs &a, uint64_t w, int lane, uint8_t *ms, BsdRec *out, const uint8_t *ex,
-                     const uint8_t *lg, const uint8_t *P) {
-    const int k = a.k, r = a.r, nw = a.nw;
-    const uint64_t pl = lane < nw ? a.present[w * (uint64_t)nw + lane] : 0ull;
-    uint64_t pw[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-        pw[q] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl, q) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pl >> 32), q) << 32);
-    const auto bit = [&](int j) -> uint32_t {  // per-lane j
-        const int q = j >> 6;
-        const uint64_t v = q == 0 ? pw[0] : q == 1 ? pw[1] : q == 2 ? pw[2] : pw[3];
-        return (uint32_t)(v >> (j & 63)) & 1u;
-    };
-    int e = 0, first = -1;  // missing sources; the first received source
-    for (int c0 = 0; c0 < k; c0 += 64) {
-        const int i = c0 + lane;
-        const bool in = i < k, miss = in && !bit(i);
-        const uint64_t b = __ballot(miss), h = __ballot(in && !miss);
-        const int pos = e + __popcll(b & ((1ull << lane) - 1ull));
-        if (miss && pos < kMaxR) ms[pos] = (uint8_t)i;
-        e += __popcll(b);
-        if (first < 0 && h) first = c0 + __ffsll((unsigned long long)h) - 1;
-    }
-    const uint32_t rep = (uint32_t)__ballot(lane < r && bit(k + lane));
-    const int np = __popcll(rep);
-    if (e == 0 || e > r || np < e) {
-        if (lane == 0) {
-            out->ne = 0;
-            a.status[w] = e == 0 ? FECGPU_STATUS_OK : FECGPU_STATUS_UNRECOVERABLE;
-        }
-        return;
-    }
-    WAVE_SYNC();
-    uint32_t v = 0, ub = 0;  // this lane's C[u][i] (lane = u * 8 + i); the repairs read
-    if (a.bsd_cauchy) {
-        // Cauchy rows: the first e present repairs, and C in closed form (as
-        // plan_gf: log C[u][i] = A_u + K_i - log(x_i ^ m_u), x_i = k + i),
-        // independent LDS lookups instead of the elimination chain
-        {
-            uint32_t rb = rep;
-            for (int c = 0; c < e; c++) {
-                ub |= rb & (0u - rb);
-                rb &= rb - 1;
-            }
-        }
-        const int u = lane >> 3, i = lane & 7;
-        if (u < e && ((ub >> i) & 1u)) {
-            const int mu = ms[u], x = k + i;
-            int L = 255 * 32 - (int)lg[x ^ mu];
-            for (uint32_t b = ub; b; b &= b - 1) {
-                const int xt = k + __ffs(b) - 1;
-                L += (int)lg[xt ^ mu] - (xt != x ? (int)lg[xt ^ x] : 0);
-            }
-            for (int q = 0; q < e; q++) {
-                const int mv = ms[q];
-                L += (int)lg[x ^ mv] - (q != u ? (int)lg[mu ^ mv] : 0);
-            }
-            v = ex[L % 255];
-        }
-    } else {
-        uint32_t rr = rep;
-        for (int i = 0; i < lane && i < 8; i++) rr &= rr - 1;
-        const int my_sel = rr ? __ffs(rr) - 1 : 0;  // lane t < np: the t-th present repair
-        // [A | I], lane = t * 8 + u; every __shfl and ballot with the whole wave active
-        const int t = lane >> 3, u = lane & 7;
-        const int sel_t = __shfl(my_sel, t, 64);
-        const int m_u = u < e ? (int)ms[u] : 0;
-        const bool row = t < np;
-        uint32_t xl = (row && u < e) ? P[sel_t * k + m_u] : 0u;
-        uint32_t xr = (row && t == u) ? 1u : 0u;
-        uint32_t used = 0;  // rows already pivots (wave-uniform)
-        int my_piv = 0;     // lane c < e: pivot row of column c
-        for (int c = 0; c < e; c++) {
-            const uint64_t cand = __ballot(row && u == c && !((used >> t) & 1u) && xl != 0);
-            if (!cand) {  // rank < e (random linear codes): the window stays lost
-                if (lane == 0) {
-                    out->ne = 0;
-                    a.status[w] = FECGPU_STATUS_UNRECOVERABLE;
-                }
-                return;
-            }
-            const int pr = (int)(__ffsll((unsigned long long)cand) - 1) >> 3;
-            used |= 1u << pr;
-            if (lane == c) my_piv = pr;
-            const uint32_t ip = gf_inv_lds(ex, lg, __shfl(xl, pr * 8 + c, 64));
-            if (t == pr) {
-                xl = gf_mul_lds(ex, lg, xl, ip);
-                xr = gf_mul_lds(ex, lg, xr, ip);
-            }
-            const uint32_t f = __shfl(xl, t * 8 + c, 64);
-            const uint32_t rl = __shfl(xl, pr * 8 + u, 64);
-            const uint32_t rq = __shfl(xr, pr * 8 + u, 64);
-            if (t != pr && row) {
-                xl ^= gf_mul_lds(ex, lg, f, rl);
-                xr ^= gf_mul_lds(ex, lg, f, rq);
-            }
-        }
-        // C[u][i], lane = u * 8 + i: T[P_u][c] where repair i is pivot row c's, else 0
-        const int cu = lane >> 3, ci = lane & 7;
-        const int pu = __shfl(my_piv, min(cu, e - 1), 64);
-        for (int c = 0; c < e; c++) {
-            const int pc = __shfl(my_piv, c, 64);
-            const uint32_t tv = __shfl(xr, (pu * 8 + pc) & 63, 64);
-            const int sc = __shfl(my_sel, pc, 64);  // the repair of pivot row pc
-            ub |= 1u << sc;
-            if (sc == ci) v = tv;
-        }
-        if (cu >= e) v = 0;
-    }
-    out->c[lane] = (uint8_t)v;
-    if (lane < 4) out->pw[lane] = lane == 0 ? pw[0] : lane == 1 ? pw[1] : lane == 2 ? pw[2] : pw[3];
-    if (lane < kMaxR) out->m[lane] = lane < e ? ms[lane] : 0;
-    if (lane == 0) {
-        out->ne = (uint32_t)e;
-        out->used = ub;
-        out->alt = first >= 0 ? (uint32_t)first : (uint32_t)(k + __ffs(ub) - 1);
-        a.status[w] = FECGPU_STATUS_OK;
-    }
-}
-
-// A window's record into its LDS region (one wave; the stage-2 multiply tables)
-__device__ __forceinline__ void load_rec(const BsdRec &rc, BsdRegion &rg, int lane) {
-    const CoefTab ct = make_coef_tab(rc.c[lane]);
-    rg.ab[lane] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
-    rg.tc[lane] = ct.c;
-    if (lane < 4) rg.pw[lane] = rc.pw[lane];
-    if (lane < kMaxR) rg.m[lane] = rc.m[lane];
-    if (lane == 0) {
-        rg.ne = rc.ne;
-        rg.used = rc.used;
-        rg.alt = rc.alt;
-    }
-}
-
-// Stage 2 on one 16-B column: acc[i][H .. H + 3] the column of syndrome i
-// (bytes, the repair rows the window uses already added: a load per syndrome
-// here was a dependent round trip each), x_u = sum_i C[u][i] s_i for u < nw
-// (wave-uniform), stored to row m[u] when u < ne.  col: the column's address
-// in row 0.
-template <int R, int H>
-__device__ __forceinline__ void solve_col(const uint32_t (&acc)[R][8], uint8_t *col, uint32_t stride,
-                                          const BsdRegion &rg, int nw, int ne, bool live) {
-    uint4 x[R];
-#pragma unroll
-    for (int u = 0; u < R; u++) x[u] = zero4();
-#pragma unroll
-    for (int i = 0; i < R; i++) {
-        const Split sp = split(make_uint4(acc[i][H], acc[i][H + 1], acc[i][H + 2], acc[i][H + 3]));
-#pragma unroll
-        for (int u = 0; u < R; u++)
-            if (u < nw) gmac(x[u], sp, rg.ab[u * kMaxR + i], rg.tc[u * kMaxR + i]);
-    }
-#pragma unroll
-    for (int u = 0; u < R; u++)
-        if (u < nw && u < ne && live) st16(col + (uint32_t)rg.m[u] * stride, x[u]);
-}
-
-// acc[i][H .. H + 3] ^= v[i] (a column of syndrome i, bytes)
-template <int R, int H>
-__device__ __forceinline__ void add_col(uint32_t (&acc)[R][8], const uint4 (&v)[R]) {
-#pragma unroll
-    for (int i = 0; i < R; i++) {
-        acc[i][H] ^= v[i].x;
-        acc[i][H + 1] ^= v[i].y;
-        acc[i][H + 2] ^= v[i].z;
-        acc[i][H + 3] ^= v[i].w;
-    }
-}
-
-}  // namespace bsd
-
-namespace bs {
-
-// dec_sources: sources() with each source's load sent to the alt row and
-// masked to zero where the lane's window misses it (pm bit j clear)
-template <int T, int J>
-__device__ __forceinline__ void dload(const uint8_t *pa, const uint8_t *pb, uint32_t stride, uint64_t pm,
-                                      const uint8_t *qa, const uint8_t *qb, uint32_t (&x)[8]) {
-    const bool p = (pm >> J) & 1ull;
-    const uint4 va = ld16(p ? pa + T * stride : qa), vb = ld16(p ? pb + T * stride : qb);
-    const uint32_t mk = p ? ~0u : 0u;
-    x[0] = va.x & mk; x[1] = va.y & mk; x[2] = va.z & mk; x[3] = va.w & mk;
-    x[4] = vb.x & mk; x[5] = vb.y & mk; x[6] = vb.z & mk; x[7] = vb.w & mk;
-}
-
-template <int K, int R, int M, int J0, int... T>
-__device__ __forceinline__ void dbatch(const uint8_t *pa, const uint8_t *pb, uint32_t stride, uint64_t pm,
-                                       const uint8_t *qa, const uint8_t *qb, uint32_t (&acc)[R][8],
-                                       std::integer_sequence<int, T...>) {
-    uint32_t x[sizeof...(T)][8];
-    (dload<T, J0 + T>(pa, pb, stride, pm, qa, qb, x[T]), ...);
-    ((tr8(x[T]), source<K, R, M, J0 + T>(x[T], acc, std::make_integer_sequence<int, R * 8>{}),
-      __builtin_amdgcn_sched_barrier(0)), ...);
-}
-
-template <int K, int R, int M, int U, int J0>
-__device__ __forceinline__ void dsources(const uint8_t *pa, const uint8_t *pb, uint32_t stride, uint64_t pm,
-                                         const uint8_t *qa, const uint8_t *qb, uint32_t (&acc)[R][8]) {
-    if constexpr (J0 < K) {
-        dbatch<K, R, M, J0>(pa, pb, stride, pm, qa, qb, acc,
-                            std::make_integer_sequence<int, ((K - J0) < U ? (K - J0) : U)>{});
-        pa += U * stride;
-        pb += U * stride;
-        asm volatile("" : "+v"(pa), "+v"(pb));
-        dsources<K, R, M, U, J0 + U>(pa, pb, stride, pm, qa, qb, acc);
-    }
-}
-
-// one decode unit (columns pa, pb of a window planned in rg): syndromes, then
-// the solve on each column
-template <int K, int R, int M, int U>
-__device__ __forceinline__ void dec_unit(uint8_t *pa, uint8_t *pb, uint32_t stride, bool live, const BsdRegion &rg,
-                                         int nw) {
-    const uint64_t pm = rg.pw[0];
-    const uint32_t alt = rg.alt;
-    uint32_t acc[R][8];
-    const uint8_t *qa = pa + alt * stride, *qb = pb + alt * stride;
-    dsources<K, R, M, U, 0>(pa, pb, stride, pm, qa, qb, acc);
-    // the repairs the window uses, one batch (the others read at the alt row
-    // and masked to zero), added to the syndromes' bytes
-    const uint32_t used = rg.used;
-    uint4 ra[R], rb[R];
-#pragma unroll
-    for (int i = 0; i < R; i++) {
-        const bool p = (used >> i) & 1u;
-        ra[i] = ld16(p ? pa + (K + i) * stride : qa);
-        rb[i] = ld16(p ? pb + (K + i) * stride : qb);
-    }
-#pragma unroll
-    for (int i = 0; i < R; i++) {
-        tr8(acc[i]);
-        const uint32_t mk = ((used >> i) & 1u) ? ~0u : 0u;
-        ra[i] = and4(ra[i], mk);
-        rb[i] = and4(rb[i], mk);
-    }
-    bsd::add_col<R, 0>(acc, ra);
-    bsd::add_col<R, 4>(acc, rb);
-    const int ne = (int)rg.ne;
-    bsd::solve_col<R, 0>(acc, pa, stride, rg, nw, ne, live);
-    bsd::solve_col<R, 4>(acc, pb, stride, rg, nw, ne, pb != pa && live);
-}
-
-}  // namespace bs
-
-namespace rbs4 {
-
-// rbs4::unit for decode over a group of consecutive windows (the wide codes):
-// the source rows by buffer loads — one resource over the group's windows,
-// this lane's column offsets coff[c] from the group's base (32-bit VGPRs, no
-// 64-bit address arithmetic per load), the row offset a scalar — and a source
-// the lane's window misses is read at an offset past the resource (2^31
-// added), which the hardware returns as zeros without a memory access: no
-// masking, no traffic for missing rows.  The repairs the solve uses are k + i
-// more inputs (identity picks), then the solve on each column (pointers pc[c]).
-constexpr uint32_t kOob = 0x80000000u;  // added to a column offset: past any group's records
-template <int R>
-__device__ __forceinline__ void dec_unit(__amdgpu_buffer_rsrc_t rs, const uint32_t (&coff)[4], uint8_t *const (&pc)[4],
-                                         uint32_t stride, int k, cmask mk, bool live, const BsdRegion &rg, int nw) {
-    // present bits 32 at a time from the region (one LDS read per 32 sources)
-    // inputs j < k the sources (present bits), j >= k the repairs, read only
-    // where the window's solve uses them (mk: the picks of [P | I], so repair i
-    // adds itself to syndrome i)
-    const uint32_t *pw32 = reinterpret_cast<const uint32_t *>(rg.pw);
-    const uint32_t used = rg.used;
-    const auto vo = [&](int j) -> uint32_t {  // uniform j
-        const uint32_t b = j < k ? (pw32[j >> 5] >> (j & 31)) : (used >> (j - k));
-        return (b & 1u) ? 0u : kOob;
-    };
-    const int n = k + R;
-    // the row offset goes in the vector offset too (soffset 0): the range
-    // check then covers the whole offset whatever soffset's treatment
-    const auto bload = [&](uint32_t off, uint32_t (&xa)[8], uint32_t (&xb)[8]) __attribute__((always_inline)) {
-        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(coff[0] + off), 0, 0);
-        const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(coff[1] + off), 0, 0);
-        const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(coff[2] + off), 0, 0);
-        const u32x4 v3 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(coff[3] + off), 0, 0);
-        xa[0] = v0.x; xa[1] = v0.y; xa[2] = v0.z; xa[3] = v0.w;
-        xa[4] = v1.x; xa[5] = v1.y; xa[6] = v1.z; xa[7] = v1.w;
-        xb[0] = v2.x; xb[1] = v2.y; xb[2] = v2.z; xb[3] = v2.w;
-        xb[4] = v3.x; xb[5] = v3.y; xb[6] = v3.z; xb[7] = v3.w;
-    };
-    uint32_t aa[R][8], ab[R][8];
-#pragma unroll
-    for (int i = 0; i < R; i++)
-#pragma unroll
-        for (int p = 0; p < 8; p++) aa[i][p] = ab[i][p] = 0;
-    uint32_t xa[8], xb[8];
-    bload(vo(0), xa, xb);
-    for (int j = 0; j < n; j++) {
-        uint32_t na[8], nb[8];
-        const int jn = min(j + 1, n - 1);
-        bload((uint32_t)jn * stride + vo(jn), na, nb);
-        bs::tr8(xa);
-        bs::tr8(xb);
-        source<R>(xa, xb, aa, ab, mk + (size_t)j * (R * 2 * kRbsDw4));
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            xa[q] = na[q];
-            xb[q] = nb[q];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < R; i++) {
-        bs::tr8(aa[i]);
-        bs::tr8(ab[i]);
-    }
-    const int ne = (int)rg.ne;
-    bsd::solve_col<R, 0>(aa, pc[0], stride, rg, nw, ne, live);
-    bsd::solve_col<R, 4>(aa, pc[1], stride, rg, nw, ne, live && pc[1] != pc[0]);
-    bsd::solve_col<R, 0>(ab, pc[2], stride, rg, nw, ne, live && pc[2] != pc[0]);
-    bsd::solve_col<R, 4>(ab, pc[3], stride, rg, nw, ne, live && pc[3] != pc[0]);
-}
-
-}  // namespace rbs4
-
-// The decode kernel: groups of a.wpb windows (from the list, or every window),
-// planned a wave per window into BsdRegion's in LDS, ordered by descending e
-// (a wave's first lane holds its largest e: the solve loops run that many
-// outputs, uniform), then their units streamed.  RT: true for the runtime-mask
-// stage 1 (four-column units, a.enc_bs), false for the compiled masks of
-// (K, R, M) (two-column units).  Workgroup-uniform trip counts (lanes past the
-// end redo the last unit without storing).
-template <int K, int R, int M, bool RT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8)))
-void gf_decode_bs_kernel(BatchArgs a) {
-    CHK_PROLOGUE(a);
-    extern __shared__ uint4 dyn[];
-    __shared__ GroupLds g;
-    __shared__ uint32_t s_w[kMaxWpb];
-    __shared__ uint8_t s_perm[kMaxWpb];
-    __shared__ uint16_t s_list[kBlock];
-    __shared__ uint32_t s_cnt[kBlock / 64];
-    BsdRegion *rgn = reinterpret_cast<BsdRegion *>(dyn);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k = a.k;
-    constexpr uint32_t C = RT ? kRbsCols : 2;  // columns per unit
-    // flagged windows: ranges of kBlock windows in batch order, their flagged
-    // ones listed in LDS and taken a.wpb at a time; else groups of a.wpb
-    const bool flagged = a.bsd_flag != nullptr;
-    const uint32_t range = (uint32_t)a.bsd_range;  // <= kBlock, a multiple of 64
-    const uint64_t nunit = flagged ? (a.nwin + range - 1) / range : (a.nwin + a.wpb - 1) / a.wpb;
-    __syncthreads();
-    // one loop over sub-batches (a nested loop per range spilled the unit's registers)
-    XcdRange xr = xcd_range(nunit, a.nx);
-    uint64_t r0 = 0;
-    uint32_t nl = 0, b0 = 0;
-    bool first = true;
-    for (;;) {
-        if (b0 >= nl) {  // the next range / group
-            if (!first) xr.cur += xr.step;
-            first = false;
-            if (xr.cur >= xr.hi) break;
-            b0 = 0;
-            if (flagged) {
-                r0 = xr.cur * range;
-                const bool f = (uint32_t)tid < range && r0 + tid < a.nwin && a.bsd_flag[r0 + tid];
-                const uint64_t b = __ballot(f);
-                if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(b);
-                __syncthreads();
-                uint32_t off = 0;
-                nl = 0;
-                for (int v = 0; v < kBlock / 64; v++) {
-                    if (v < wave) off += s_cnt[v];
-                    nl += s_cnt[v];
-                }
-                if (f) s_list[off + __popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)tid;
-                __syncthreads();
-                if (nl == 0) continue;
-            } else {
-                r0 = xr.cur * a.wpb;
-                nl = (uint32_t)min((uint64_t)a.wpb, a.nwin - r0);
-            }
-        }
-        const int nb = (int)min((uint32_t)a.wpb, nl - b0);
-        if (tid < nb) {
-            const uint64_t w = r0 + (flagged ? (uint64_t)s_list[b0 + tid] : (uint64_t)tid);
-            s_w[tid] = (uint32_t)w;
-            uint64_t base;
-            uint32_t stride, S;
-            win_geom(a, w, base, stride, S);
-            g.base[tid] = base;
-            g.stride[tid] = stride;
-            g.ncol[tid] = (S + 15u) >> 4;
-        }
-        __syncthreads();
-        for (int wl = wave; wl < nb; wl += kBlock / 64) bsd::load_rec(a.bsd_rec[s_w[wl]], rgn[wl], lane);
-        __syncthreads();
-        if (tid < 64) {  // descending e (ties by index), then unit prefix sums in that order
-            const int t = tid;
-            const int ne_t = t < nb ? (int)rgn[t].ne : -1;
-            const uint64_t below = (1ull << t) - 1;
-            int rank = 0;
-#pragma unroll
-            for (int v = R; v >= 0; v--) {
-                const uint64_t b = __ballot(ne_t == v);
-                if (v > ne_t) rank += __popcll(b);
-                else if (v == ne_t) rank += __popcll(b & below);
-            }
-            if (t < nb) s_perm[rank] = (uint8_t)t;
-            WAVE_SYNC();
-            const int wl = t < nb ? (int)s_perm[t] : 0;
-            block_prefix(g.pfx, (t < nb && rgn[wl].ne) ? (g.ncol[wl] + C - 1) / C : 0u, t);
-        }
-        __syncthreads();
-        const uint32_t total = g.pfx[nb];
-        int i = 0;
-        for (uint32_t s0 = 0; s0 < total; s0 += kBlock) {
-            const bool live = s0 + tid < total;
-            const uint32_t s = live ? s0 + tid : total - 1;
-            while (s >= g.pfx[i + 1]) i++;
-            const int wl = s_perm[i];
-            const BsdRegion &rg = rgn[wl];
-            const int nw = __builtin_amdgcn_readfirstlane((int)rg.ne);  // the wave's largest e
-            uint8_t *base = reinterpret_cast<uint8_t *>(g.base[wl]);
-            const uint32_t u = s - g.pfx[i], h = g.pfx[i + 1] - g.pfx[i];
-            if constexpr (RT) {
-                // the group's windows are consecutive (no list): one resource from
-                // the first window over wpb window pitches
-                uint8_t *pc[4];
-                rbs4::unit_cols(base, u, h, g.ncol[wl], pc);
-                const uint8_t *gb = reinterpret_cast<const uint8_t *>(g.base[0]);
-                uint32_t coff[4];
-#pragma unroll
-                for (int c = 0; c < 4; c++) coff[c] = (uint32_t)(pc[c] - gb);
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint8_t *>(gb), 0, (int)(uint32_t)((uint64_t)nb * a.wpitch), bsd::kRsrcRaw);
-#if FECGPU_CHECK
-                // the resource's span lies in the launch's windows (its loads stay inside it)
-                if (tid == 0 && s0 == 0) {
-                    (void)chk_ok(gb);
-                    (void)chk_ok(gb + (uint64_t)nb * a.wpitch - 16);
-                }
-#endif
-                rbs4::dec_unit<R>(rs, coff, pc, g.stride[wl], k, (rbs::cmask)a.enc_bs, live, rg, nw);
-            } else {
-                uint8_t *pa, *pb;
-                bs::unit_cols(base, u, h, g.ncol[wl], pa, pb);
-                bs::dec_unit<K, R, M, kBsU>(pa, pb, g.stride[wl], live, rg, nw);
-            }
-        }
-        __syncthreads();
-        b0 += (uint32_t)a.wpb;
-    }
-}
-
-// The wide codes' plans: a wave per window into a.bsd_rec (statuses too).
-__global__ __launch_bounds__(kBlock) void gf_decode_bs_plan_kernel(BatchArgs a) {
-    extern __shared__ uint8_t s_P[];  // parity rows [r][k]
-    __shared__ uint8_t s_exp[512];
-    __shared__ uint8_t s_log[256];
-    __shared__ uint8_t s_m[kBlock / 64][kMaxR];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < 512; i += kBlock) s_exp[i] = c_gf.exp[i];
-    for (int i = tid; i < 256; i += kBlock) s_log[i] = c_gf.log[i];
-    if (!a.bsd_cauchy)
-        for (int i = tid; i < a.r * a.k; i += kBlock) s_P[i] = a.prows[i];
-    __syncthreads();
-    const uint64_t w = (uint64_t)blockIdx.x * (kBlock / 64) + wave;
-    if (w < a.nwin) bsd::plan(a, w, lane, s_m[wave], a.bsd_rec + w, s_exp, s_log, s_P);
 }
 
 // ========================================================= workloads ===
@@ -2544,11 +2090,14 @@ hipError_t launch(K kernel, BatchArgs a, const LaunchPlan &p, hipStream_t s, boo
         default: return hipErrorInvalidValue;   \
     }
 
-// Codes with a bit-sliced encode (Cauchy and Vandermonde rows, compiled in).  r = 8 and
-// k >= 16 only: there the table multiply is VALU-bound and the bit-sliced
-// kernel 1.1-1.4x faster; at r <= 4 (and k = 8, r = 8) the table kernel is
-// memory-bound and, at higher occupancy, 8-12 % faster (profiles/r01_bs_r4_and_alternation.txt).
-#define BS_CODES(X) X(16, 8) X(24, 8) X(32, 8)
+// Codes with a bit-sliced encode (Cauchy and Vandermonde rows, compiled in).
+// r = 8, k >= 16: the table multiply is VALU-bound and the bit-sliced kernel
+// 1.1-1.4x faster.  k 16 r 4 (cfg3): with its stores gathered (uniform short
+// rows, gf_encode_bs_gs_kernel) it runs at 2 workgroups per CU, where HBM
+// moves the mix fastest, and beats the table multiply that needs 4-5 waves
+// per SIMD for its VALU work (profiles/r06_*); other r <= 4
+// codes stay on the table multiply (profiles/r01_bs_r4_and_alternation.txt).
+#define BS_CODES(X) X(16, 4) X(16, 8) X(24, 8) X(32, 8)
 
 bool bitslice_supported(int k, int r, int matrix) {
     if (matrix != FECGPU_MATRIX_CAUCHY && matrix != FECGPU_MATRIX_VANDERMONDE) return false;
@@ -2563,7 +2112,9 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
     if (p.bitslice) {
 #define BS_LAUNCH_M(K_, R_, M_)                                                            \
         if (a.k == K_ && a.r == R_ && p.matrix == M_)                                             \
-            return p.flat ? launch(gf_encode_bs_kernel<K_, R_, M_, true>, a, p, s, false,         \
+            return p.bsgs ? launch(gf_encode_bs_gs_kernel<K_, R_, M_>, a, p, s, false,           \
+                                   (a.nwin + a.wpb - 1) / a.wpb)                                   \
+                 : p.flat ? launch(gf_encode_bs_kernel<K_, R_, M_, true>, a, p, s, false,         \
                                    (a.nwin * ((a.ncol + 1) / 2) + kBlock - 1) / kBlock)             \
                           : launch(gf_encode_bs_kernel<K_, R_, M_, false>, a, p, s, false);
 #define BS_LAUNCH(K_, R_)                                 \
@@ -2633,74 +2184,13 @@ hipError_t launch_gf_decode_table(const BatchArgs &a, const LaunchPlan &p, hipSt
 }
 }  // namespace
 
-// The bit-sliced decode over the flagged windows (a.bsd_flag, planned by the
-// table decode) or, without flags, every window (planned here first); a.wpb
-// windows per group, persistent grid.  Compiled masks when the code has them
-// (matrix: fecgpu_matrix), else runtime ones (a.enc_bs).
-hipError_t launch_decode_bs(BatchArgs a, int matrix, hipStream_t s) {
-    if (a.nwin == 0) return hipSuccess;
-    if (a.r < 4 || a.r > kMaxR || !a.prows) return hipErrorInvalidValue;
-    a.bsd_cauchy = matrix == FECGPU_MATRIX_CAUCHY;
-    if (!a.bsd_rec) return hipErrorInvalidValue;
-    if (!a.bsd_flag) {  // the wide codes: every window's plan first (the routed ones are planned by the table decode)
-        hipLaunchKernelGGL(gf_decode_bs_plan_kernel, dim3((unsigned)((a.nwin + kBlock / 64 - 1) / (kBlock / 64))),
-                           dim3(kBlock), a.bsd_cauchy ? 0 : (size_t)a.k * a.r, s, a);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    LaunchPlan p{};
-    p.wpb = a.wpb;
-    p.lds_bytes = (uint32_t)(a.wpb * sizeof(BsdRegion));
-    // flagged windows: ranges of 64..256 windows, about two per resident
-    // workgroup (one all-flagged range is ~8 groups of a.wpb)
-    if (a.bsd_flag) {
-        int dev = 0, cus = 256;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const uint64_t per = (a.nwin + 4ull * cus - 1) / (4ull * cus);
-        a.bsd_range = (int)std::min<uint64_t>(kBlock, std::max<uint64_t>(64, (per + 63) / 64 * 64));
-    }
-    const uint64_t groups = a.bsd_flag ? (a.nwin + a.bsd_range - 1) / a.bsd_range : (a.nwin + a.wpb - 1) / a.wpb;
-    const auto go = [&](auto kernel) -> hipError_t {
-        if (p.lds_bytes > 64u * 1024u) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes);
-            if (e != hipSuccess) return e;
-        }
-        return launch(kernel, a, p, s, false, groups);
-    };
-    if (a.k + a.r <= kMaxK && bitslice_supported(a.k, a.r, matrix)) {
-#define BSD_LAUNCH_M(K_, R_, M_) \
-        if (a.k == K_ && a.r == R_ && matrix == M_) return go(gf_decode_bs_kernel<K_, R_, M_, false>);
-#define BSD_LAUNCH(K_, R_)                              \
-        BSD_LAUNCH_M(K_, R_, FECGPU_MATRIX_CAUCHY)      \
-        BSD_LAUNCH_M(K_, R_, FECGPU_MATRIX_VANDERMONDE)
-        BS_CODES(BSD_LAUNCH)
-#undef BSD_LAUNCH
-#undef BSD_LAUNCH_M
-    }
-    if (!a.enc_bs || a.bsd_flag) return hipErrorInvalidValue;  // the runtime-mask kernel: consecutive windows
-    switch (a.r) {
-        case 4: return go(gf_decode_bs_kernel<0, 4, 0, true>);
-        case 5: return go(gf_decode_bs_kernel<0, 5, 0, true>);
-        case 6: return go(gf_decode_bs_kernel<0, 6, 0, true>);
-        case 7: return go(gf_decode_bs_kernel<0, 7, 0, true>);
-        default: return go(gf_decode_bs_kernel<0, 8, 0, true>);
-    }
-}
-
 hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     if (scheme == 0) {
         if (p.flat) DISPATCH_R(a.r, launch(xor_decode_kernel<RR, true>, a, p, s, true))
         else DISPATCH_R(a.r, launch(xor_decode_kernel<RR, false>, a, p, s, false))
     }
-    const hipError_t e = launch_gf_decode_table(a, p, s);
-    if (e != hipSuccess || !a.bsd_min_e) return e;
-    // the windows the table plan routed (e >= bsd_min_e), after it on the stream
-    BatchArgs b = a;
-    b.wpb = p.bsd_wpb;
-    return launch_decode_bs(b, p.matrix, s);
+    return launch_gf_decode_table(a, p, s);
 }
 
 hipError_t take_bounds_faults(uint64_t *count, uint64_t *first) {

@@ -48,3 +48,40 @@ def gather_digest(digest: int, device=None) -> int:
     for o in out:
         x ^= int(o.item()) & (2**64 - 1)
     return x
+
+
+def gather_floats(values, device=None) -> list[list[float]]:
+    """Every rank's `values` (same length on every rank), in rank order: the
+    per-rank kernel times bench.py turns into per-GPU roofline fractions, so an
+    N-rank line shows the slowest GPU and not rank 0's alone."""
+    vals = [float(v) for v in values]
+    if not _active():
+        return [vals]
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(x) for x in o.cpu().tolist()] for o in out]
+
+
+def per_rank_roofline(kernel_ms, alg_bytes: dict, peak_gbs: float) -> dict:
+    """kernel_ms: [[encode_ms, decode_ms], ...] per rank; alg_bytes: algorithmic
+    bytes per launch of each kernel (the same shard shape on every rank).
+    Returns each rank's rate and fraction of `peak_gbs` for both kernels, and
+    per kernel the min / max fraction over the ranks (None where a rank has no
+    kernel time, e.g. HIP events switched off)."""
+    ranks = []
+    for r, (enc, dec) in enumerate(kernel_ms):
+        row = {"rank": r}
+        for name, ms in (("encode", enc), ("decode", dec)):
+            ok = ms == ms and ms > 0  # not NaN, positive
+            gbs = alg_bytes[name] / (ms * 1e-3) / 1e9 if ok else None
+            row[f"{name}_ms"] = round(ms, 4) if ok else None
+            row[f"{name}_GBs"] = round(gbs, 1) if ok else None
+            row[f"{name}_frac"] = round(gbs / peak_gbs, 4) if ok else None
+        ranks.append(row)
+    out = {"ranks": ranks}
+    for name in ("encode", "decode"):
+        fr = [row[f"{name}_frac"] for row in ranks if row[f"{name}_frac"] is not None]
+        out[f"{name}_frac_min"] = min(fr) if fr else None
+        out[f"{name}_frac_max"] = max(fr) if fr else None
+    return out

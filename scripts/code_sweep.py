@@ -38,8 +38,6 @@ def kernel_name(ctx_bs: bool, scheme, matrix, k, r):
 def main():
     only = sys.argv[1] if len(sys.argv) > 1 else ""  # "rbs": the runtime-mask shapes only
     ctx = fecgpu.Context()
-    if os.environ.get("BSD_MIN_E"):  # GF decode: erasures from which the bit-sliced decode runs
-        ctx.set_tuning("bsd_min_e", int(os.environ["BSD_MIN_E"]))
     dev = torch.device("cuda")
     base = workloads.CONFIGS[3]
     for scheme, matrix, k, r in SHAPES:

@@ -187,50 +187,15 @@ for s in "$@"; do
         cfg4probe) step cfg4probe 600 python scripts/cfg4_probe.py ABC ;;
         cfg4order) step cfg4order_ad 600 python scripts/cfg4_probe.py AD && step cfg4order_eb 600 python scripts/cfg4_probe.py EB ;;
         listctr) step listctr 120 rocprofv3 -L ;;
-        abbsd)  # GF decode: bit-sliced decode routing off (0) vs on (6, 4): e = r = 8 rows, cfg4, wide k120
-            for rep in ${BSD_REPS:-1}; do
-                for m in ${BSD_VALS:-0 6}; do
-                    BSD_MIN_E=$m step abbsd_sweep_${m}_$rep 300 python scripts/code_sweep.py r8
-                    step abbsd_cfg4_${m}_$rep 300 python bench.py --config 4 --steps 5 --warmup 2 --cpu-seconds 0 \
-                        --no-verify --extra-configs 0 --bsd-min-e $m
-                    step abbsd_w120_${m}_$rep 300 python bench.py --k 120 --r 8 --steps 10 --warmup 3 --cpu-seconds 0 \
-                        --no-verify --bsd-min-e $m
-                done
-            done ;;
-        profbsd)  # rocprofv3 of the k32 r8 e = 8 sweep row, bit-sliced decode on (6) and off (0)
-            for m in 6 0; do
-                BSD_MIN_E=$m step profbsd_$m 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profbsd_$m -o run -- \
-                    python scripts/code_sweep.py shape=gf256-cauchy-32-8
-            done ;;
         tracex)  # cfg7 plan trace of every lib/libfecgpu_trace*.so (measurement variants)
             for v in quic-fec-eps_amd/lib/libfecgpu_trace*.so; do
                 n=$(basename $v .so); n=${n#libfecgpu_}
                 FECGPU_LIB=$v step tracex_$n 300 python bench.py --config 7 --steps 3 --warmup 1 --cpu-seconds 0 \
                     --no-verify --extra-configs 0
             done ;;
-        abbsdu)  # bit-sliced decode: default lib vs lib/libfecgpu_bsdu8.so (8 inputs per load batch)
-            for v in "" quic-fec-eps_amd/lib/libfecgpu_bsdu8.so; do
-                n=${v:+u8}; n=${n:-u2}
-                FECGPU_LIB=$v step abbsdu_sweep_$n 300 python scripts/code_sweep.py r8
-                FECGPU_LIB=$v step abbsdu_cfg4_$n 300 python bench.py --config 4 --steps 5 --warmup 2 --cpu-seconds 0 \
-                    --no-verify --extra-configs 0
-                FECGPU_LIB=$v step abbsdu_w120_$n 300 python bench.py --k 120 --r 8 --steps 10 --warmup 3 \
-                    --cpu-seconds 0 --no-verify
-            done ;;
-        abpf)  # cfg4: bit-sliced encode, default vs lib/libfecgpu_bspf*.so (prefetching batches), interleaved twice
-            for rep in 1 2; do
-                step abpf_base_$rep 300 python bench.py --config 4 --steps 10 --warmup 2 --cpu-seconds 0 --no-verify \
-                    --extra-configs 0
-                for v in quic-fec-eps_amd/lib/libfecgpu_bspf*.so; do
-                    [ -e "$v" ] || continue
-                    n=$(basename $v .so); n=${n#libfecgpu_}
-                    FECGPU_LIB=$v step abpf_${n}_$rep 300 python bench.py --config 4 --steps 10 --warmup 2 --cpu-seconds 0 \
-                        --no-verify --extra-configs 0
-                done
-            done ;;
-        gpufix) step gpufix 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_sw.py \
+        gpufix) step gpufix 300 python -u -m pytest tests/test_gpu_gfdec_many.py tests/test_gpu_wide.py tests/test_gpu_sw.py \
                     tests/test_gpu_boundscheck.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
-        bsdtests) step bsdtests 300 python -u -m pytest tests/test_gpu_bsdec.py tests/test_gpu_wide.py tests/test_gpu_boundscheck.py \
+        bsdtests) step bsdtests 300 python -u -m pytest tests/test_gpu_gfdec_many.py tests/test_gpu_wide.py tests/test_gpu_boundscheck.py \
                     tests/test_gpu_parity.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         benchdef) step benchdef 900 python bench.py ;;  # the driver's default command
         probe) step probe 300 ./scripts/stream_probe ;;

@@ -33,8 +33,7 @@ def per_call_wide(path, counter):
     """Wide codes (k + r > 64, `--k`): bytes per encode / decode CALL.  In
     dispatch order a decode is wide_dec_plan_kernel, the stage-1 bit-sliced
     pass (gf_encode_rbs_kernel right after the plan) and the stage-2 combine
-    pass; an encode is a gf_encode_rbs_kernel on its own (or the bit-sliced
-    decode's plan and data kernels when bsd_min_e > 0: gf_decode_bs_*)."""
+    pass; an encode is a gf_encode_rbs_kernel on its own."""
     rows = [r for r in csv.DictReader(open(f"{path}/run_counter_collection.csv")) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     enc, dec = [], []

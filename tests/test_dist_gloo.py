@@ -42,7 +42,10 @@ def _worker(rank, world, port, q):
     w0, n = shard.weak_shard(rank, world, NPER)
     d = shard.gather_digest(_digest(O, w0, n))
     t, b = shard.reduce_run(0.5 + rank, 1000 * (rank + 1))
-    q.put((rank, d, t, b))
+    # per-rank kernel times as bench.py gathers them for the N-rank roofline
+    ms = shard.gather_floats([1.0 + rank, 2.0 + rank])
+    roof = shard.per_rank_roofline(ms, {"encode": 4e9, "decode": 6e9}, 8000.0)
+    q.put((rank, d, t, b, ms, roof))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -60,10 +63,16 @@ def test_two_rank_shards_match_single_process(oracle_lib):
         p.join(60)
         assert p.exitcode == 0
     whole = _digest(oracle_lib, 0, NPER * world)
-    for rank, d, t, b in res:
+    for rank, d, t, b, ms, roof in res:
         assert d == whole
         assert t == 1.5
         assert b == 3000
+        # every rank sees both ranks' kernel times, in rank order
+        assert ms == [[1.0, 2.0], [2.0, 3.0]]
+        assert [row["rank"] for row in roof["ranks"]] == [0, 1]
+        assert roof["ranks"][1]["encode_GBs"] == 2000.0  # 4e9 B / 2 ms
+        assert roof["encode_frac_max"] == 0.5 and roof["encode_frac_min"] == 0.25
+        assert roof["decode_frac_max"] == 0.375 and roof["decode_frac_min"] == 0.25
 
 
 def test_shard_ranges():
@@ -74,3 +83,7 @@ def test_shard_ranges():
     got = [shard.strong_shard(g, 3, 10) for g in range(3)]
     assert got == [(0, 3), (3, 3), (6, 4)]
     assert shard.reduce_run(1.25, 7) == (1.25, 7)
+    assert shard.gather_floats([1.5, 2.5]) == [[1.5, 2.5]]
+    roof = shard.per_rank_roofline([[float("nan"), 2.0]], {"encode": 1e9, "decode": 1e9}, 8000.0)
+    assert roof["encode_frac_min"] is None and roof["ranks"][0]["encode_ms"] is None
+    assert roof["decode_frac_min"] == roof["decode_frac_max"] == 0.0625

@@ -70,7 +70,8 @@ def _emitted_equal(a, b, S):
 
 CASES = [
     # scheme, k, r, workload, L, erasure, nwin: flat and group modes, per-window S,
-    # tiny and large symbols, r > k, the bit-sliced codes
+    # tiny and large symbols, r > k, the bit-sliced codes (k 16 r 4 at 1200 B: the
+    # gathered-store kernel, 64 windows = 10 steps of 6 and one of 4)
     ("xor", 8, 2, 0, 1200, 1, 64),
     ("xor", 5, 3, 0, 17, 2, 64),
     ("xor", 8, 2, 1, 0, 2, 12),
@@ -329,12 +330,12 @@ def test_checked_encoder_failed_launch_recovers(chk):
     enc.close()
 
 
-# ---- sliding-window, wide and bit-sliced decode kernels ----
+# ---- sliding-window and wide kernels ----
 # The checked build also bounds the sliding-window kernels (fec_swdec.hip,
 # fec_swenc.hip: every row, job slot, look-back record, start-list entry and
 # operation-log entry an index addresses, against its allocation), the combine
-# launches (their rows against the call's arrays), the wide plan and the
-# bit-sliced decode.  Each case below runs equal to the oracle AND clean.
+# launches (their rows against the call's arrays) and the wide plan.  Each case
+# below runs equal to the oracle AND clean.
 
 def _sw():
     import test_gpu_sw as T
@@ -420,15 +421,12 @@ def test_checked_sw_checker_fires_when_the_range_is_short(chk):
 
 
 @pytest.mark.parametrize("k,r,matrix,L", [(248, 8, "cauchy", 300), (120, 8, "rlc", 1200), (150, 5, "cauchy", 64)])
-@pytest.mark.parametrize("bsd", [0, 6])
-def test_checked_wide_encode_decode(chk, k, r, matrix, L, bsd):
-    """k + r up to 256: the two-stage decode (default) and the bit-sliced one
-    (bsd_min_e 6: buffer loads past the resource, the plan kernel)."""
+def test_checked_wide_encode_decode(chk, k, r, matrix, L):
+    """k + r up to 256: the runtime-mask encode and the two-stage decode."""
     import test_gpu_wide as TW
     m, _ = chk
     c = m.Context()
     try:
-        c.set_tuning("bsd_min_e", bsd)
         rng = np.random.default_rng(k + r)
         bits = TW._erasures(10, k, r, rng)
         TW._run(c, k, r, matrix, L, 10, bits, m=m)
@@ -450,13 +448,12 @@ def test_checked_wide_two_stage(chk):
 
 
 @pytest.mark.parametrize("matrix", ["cauchy", "vandermonde"])
-def test_checked_bsdec_routed(chk, matrix):
-    """Narrow windows with many erasures routed to the bit-sliced decode, mixed lengths."""
-    import test_gpu_bsdec as TB
+def test_checked_gf_decode_many_erasures(chk, matrix):
+    """Windows with many erasures (k 32 r 8), mixed lengths, on the checked build."""
+    import test_gpu_gfdec_many as TB
     m, _ = chk
     c = m.Context()
     try:
-        c.set_tuning("bsd_min_e", 5)
         rng = np.random.default_rng(11)
         bits = TB._erasures(40, 32, 8, rng, lo=4)
         sl = np.where(rng.random(40) < 0.5, 1202, 9002).astype(np.uint32)

@@ -1,12 +1,11 @@
-"""GPU parity of the bit-sliced decode of windows with many erasures
-(fec_kernels.hip gf_decode_bs_kernel): the table decode's plan
-routes windows with e >= the ctx's "bsd_min_e" erasures (default 0: off) to it for
-the codes with compiled plane masks (k in 16, 24, 32; r = 8; Cauchy and
-systematic Vandermonde rows).  Recovered bytes equal the originals, statuses
-equal the numpy oracle's (oracle/np_oracle.py decode), missing rows poisoned
-first; routing on and off give the same bytes.  The wide codes (k + r > 64,
-every window through this kernel with runtime plane picks when bsd_min_e > 0)
-are covered by tests/test_gpu_wide.py::test_wide_bitsliced_decode.
+"""GPU parity of the GF decode (fec_kernels.hip gf_decode_kernel) on windows
+with many erasures: e up to r + 1 missing sources and up to 2 missing repairs
+per window, for k in 16, 24, 32 and r = 8 with Cauchy and systematic
+Vandermonde rows, fixed and per-window lengths.  Recovered bytes equal the
+originals, statuses equal the numpy oracle's (oracle/np_oracle.py decode),
+missing rows poisoned first.  (These cases were written for the bit-sliced
+decode of round 5, which measured slower than this kernel and was removed in
+round 6; the wide codes are in tests/test_gpu_wide.py.)
 PARITY UNPINNED vs the reference fec branch."""
 import numpy as np
 import pytest
@@ -19,11 +18,9 @@ import np_oracle as N  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _ctx(min_e):
+def _ctx():
     assert torch.cuda.is_available(), "gpu tests need a GPU"
-    c = fecgpu.Context()
-    c.set_tuning("bsd_min_e", min_e)
-    return c
+    return fecgpu.Context()
 
 
 def _erasures(nwin, k, r, rng, lo=0):
@@ -77,8 +74,8 @@ def _run(c, k, r, matrix, L, nwin, bits, sym_len=None, seed=0, m=fecgpu):
 @pytest.mark.parametrize("matrix", ["cauchy", "vandermonde"])
 @pytest.mark.parametrize("k", [16, 24, 32])
 @pytest.mark.parametrize("L", [1, 33, 1200])
-def test_bsdec_vs_oracle(k, matrix, L):
-    c = _ctx(6)
+def test_many_erasures_vs_oracle(k, matrix, L):
+    c = _ctx()
     try:
         rng = np.random.default_rng(k + L)
         bits = _erasures(96, k, 8, rng, lo=3)
@@ -91,38 +88,22 @@ def test_bsdec_vs_oracle(k, matrix, L):
         c.close()
 
 
-@pytest.mark.parametrize("min_e", [1, 4, 8])
-def test_bsdec_threshold_and_off_agree(min_e):
-    """Routing at several thresholds, and none (0): the same bytes and statuses."""
-    k, r, L, nwin = 32, 8, 300, 120
-    rng = np.random.default_rng(min_e)
-    bits = _erasures(nwin, k, r, rng)
-    outs = []
-    for m in (0, min_e):
-        c = _ctx(m)
-        try:
-            outs.append(_run(c, k, r, "cauchy", L, nwin, bits, seed=5))
-        finally:
-            c.close()
-    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
-
-
-def test_bsdec_mixed_lengths_config4_shape():
+def test_many_erasures_mixed_lengths_config4_shape():
     """Per-window lengths 1200/9000 mixed (config 4's shape, stride 9008) with
-    many erasures: the routed windows' units span one or several passes."""
+    many erasures per window."""
     k, r, nwin = 32, 8, 64
     rng = np.random.default_rng(44)
     bits = _erasures(nwin, k, r, rng, lo=5)
     sl = np.where(rng.random(nwin) < 0.5, 1202, 9002).astype(np.uint32)
     sl[::7] = rng.integers(1, 9002, len(sl[::7]))
-    c = _ctx(6)
+    c = _ctx()
     try:
         _run(c, k, r, "cauchy", 9002, nwin, bits, sym_len=sl)
     finally:
         c.close()
 
 
-def test_bsdec_every_routed_pattern_small():
+def test_every_high_erasure_pattern_small():
     """k 16 r 8: every e = 6..8 with a fixed repair loss pattern sweep over windows
     (exactly which repairs are present moves the pivots)."""
     k, r = 16, 8
@@ -136,7 +117,7 @@ def test_bsdec_every_routed_pattern_small():
                 b[k + rng.choice(r, lost_rep, replace=False)] = False
             rows.append(b)
     bits = np.array(rows)
-    c = _ctx(6)
+    c = _ctx()
     try:
         _, gst = _run(c, k, r, "vandermonde", 64, len(bits), bits)
         assert (gst == 0).all()

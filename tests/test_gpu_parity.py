@@ -575,7 +575,9 @@ def test_linearity_full_size(ctx):
     assert torch.equal(a.view[:, cfg.k:], ra ^ rb)
 
 
-# (16|24|32, 8): compiled masks; r >= 5 otherwise: runtime masks (rbs); (16, 4): table kernel
+# (16|24|32, 8) and (16, 4): compiled masks (16, 4 on uniform short rows with the
+# repairs gathered in LDS, gf_encode_bs_gs_kernel); r >= 5 otherwise: runtime
+# masks (rbs); (8, 8): table kernel
 BS_CODES = [(16, 8), (24, 8), (32, 8), (8, 8), (16, 4), (1, 5), (13, 6), (45, 7), (56, 8)]
 
 
@@ -614,7 +616,7 @@ def test_bitslice_encode_vs_oracle(ctx, ctx_tables, k, r, wl, L, nwin, matrix):
     _cmp_emitted(outs[1], oe, S, "table encode")
 
 
-@pytest.mark.parametrize("k,r", [(16, 8), (32, 8), (8, 8), (20, 5)])
+@pytest.mark.parametrize("k,r", [(16, 8), (32, 8), (8, 8), (20, 5), (16, 4)])
 def test_bitslice_ragged_and_split(ctx, k, r):
     """Bit-sliced encode through the ragged (win_off) and split (src / repair arrays) layouts."""
     nwin = 11
@@ -652,6 +654,28 @@ def test_bitslice_ragged_and_split(ctx, k, r):
     ctx.encode_split(fecgpu.Code("gf256", k, r), src, rep, nwin=nwin, stride=1104, sym_len_all=1100)
     torch.cuda.synchronize()
     assert np.array_equal(rep.cpu().numpy()[:, :, :1100], oe[:, k:, :1100])
+
+
+@pytest.mark.parametrize("matrix", ["cauchy", "vandermonde"])
+@pytest.mark.parametrize("L,stride,nwin", [(1200, 1200, 1000), (1200, 1264, 301), (496, 496, 777), (4096, 4096, 40),
+                                           (4112, 4112, 9), (16, 16, 2000)])
+def test_bitslice_gathered_stores_vs_oracle(ctx, ctx_tables, matrix, L, stride, nwin):
+    """k 16 r 4 on uniform windows (gf_encode_bs_gs_kernel):
+    many steps of whole windows, a last step with fewer windows, strides above
+    the row length, rows up to 256 units (4096 B: one window per step) and just
+    past it (4112 B: the flat kernel); bytes equal the oracle's and the table
+    kernel's."""
+    k, r = 16, 4
+    S = np.full(nwin, L, np.uint32)
+    wins = O.make_windows(0, SEED + L, 0, nwin, k, r, L, stride)
+    oe = wins.copy()
+    O.encode_batch(O.GF256 if matrix == "cauchy" else O.GF256_VDM, k, r, S, oe, 4)
+    code = fecgpu.Code("gf256", k, r, matrix=matrix)
+    for c, what in ((ctx, "gathered-store encode"), (ctx_tables, "table encode")):
+        d = torch.from_numpy(wins.copy()).cuda()
+        c.encode_batch(code, d, nwin=nwin, stride=stride, sym_len_all=L)
+        torch.cuda.synchronize()
+        _cmp_emitted(d.cpu().numpy(), oe, S, what)
 
 
 # ---- FECGPU_MATRIX_RLC: RFC 8681 random linear code rows (tests/test_rlc_spec.py pins the

@@ -141,6 +141,56 @@ def test_wide_per_window_lengths(ctx):
     _run(ctx, k, r, "cauchy", L, nwin, bits, sym_len=sl)
 
 
+@pytest.mark.parametrize("k,r,matrix,L", [(60, 8, "cauchy", 1200), (100, 4, "cauchy", 40),
+                                          (200, 8, "cauchy", 1200), (248, 8, "cauchy", 300),
+                                          (90, 6, "vandermonde", 1200), (150, 8, "rlc", 1200),
+                                          (250, 6, "rlc", 64), (75, 5, "cauchy", 200),
+                                          (180, 7, "vandermonde", 1200), (68, 4, "rlc", 16),
+                                          # r < 4: the combine-job passes (the bit-sliced kernel takes r >= 4)
+                                          (70, 2, "cauchy", 1200), (130, 3, "rlc", 500), (65, 1, "cauchy", 100)])
+def test_wide_encode_decode_vs_oracle(ctx, k, r, matrix, L):
+    nwin = 12
+    rng = np.random.default_rng(k * 31 + r)
+    bits = _erasures(nwin, k, r, rng)
+    bits[0] = True            # nothing missing
+    bits[1] = True
+    bits[1, :r] = False       # exactly r sources, every repair present
+    gst = _run(ctx, k, r, matrix, L, nwin, bits)
+    assert gst[0] == 0 and gst[1] == 0
+
+
+def test_wide_many_windows(ctx):
+    """600 windows of k 120 r 8 (the bench's shape): the bit-sliced passes'
+    flat unit space over many workgroups, and the two-stage decode's syndrome
+    scratch past one workgroup's windows."""
+    k, r, nwin = 120, 8, 600
+    rng = np.random.default_rng(17)
+    bits = _erasures(nwin, k, r, rng, max_e=r)
+    gst = _run(ctx, k, r, "cauchy", 1200, nwin, bits)
+    assert (gst == 0).sum() > nwin // 2
+
+
+def test_wide_every_erasure_count(ctx):
+    """k 120 r 8 Cauchy: e = 0..8 missing sources with every repair present (all
+    recoverable), then e = 9 (never)."""
+    k, r = 120, 8
+    bits = np.ones((10, k + r), bool)
+    rng = np.random.default_rng(3)
+    for e in range(10):
+        bits[e, rng.choice(k, e, replace=False)] = False
+    gst = _run(ctx, k, r, "cauchy", 1200, 10, bits)
+    assert list(gst) == [0] * 9 + [1]
+
+
+def test_wide_per_window_lengths(ctx):
+    """Per-window symbol lengths (sym_len): every byte below each window's length."""
+    k, r, nwin, L = 80, 8, 8, 1200
+    rng = np.random.default_rng(9)
+    bits = _erasures(nwin, k, r, rng, max_e=r)
+    sl = rng.integers(100, L + 1, nwin).astype(np.uint32)
+    _run(ctx, k, r, "cauchy", L, nwin, bits, sym_len=sl)
+
+
 @pytest.fixture(scope="module")
 def bsctx():
     """A ctx with the bit-sliced wide decode on (tuning "bsd_min_e" > 0)."""
@@ -154,21 +204,20 @@ def bsctx():
 @pytest.mark.parametrize("k,r,matrix,L", [(60, 8, "cauchy", 1200), (120, 8, "cauchy", 1200), (248, 8, "cauchy", 300),
                                           (90, 6, "vandermonde", 1200), (150, 8, "rlc", 1200), (250, 6, "rlc", 64),
                                           (75, 5, "cauchy", 200), (68, 4, "rlc", 16)])
-def test_wide_bitsliced_decode(bsctx, k, r, matrix, L):
-    """The bit-sliced wide decode (gf_decode_bs_plan_kernel + gf_decode_bs_kernel,
-    runtime plane picks of [P | I]): bytes and statuses as the
-    oracle's, every erasure count, per-window lengths."""
+def test_wide_codes_every_erasure_count(ctx, k, r, matrix, L):
+    """The wide decode (two stages, fec_wide.hip): bytes and statuses as the
+    oracle's for every erasure count 0..r+1, then per-window lengths."""
     nwin = 40
     rng = np.random.default_rng(k * 13 + r)
     bits = _erasures(nwin, k, r, rng)
     for e in range(min(r + 2, nwin)):
         bits[e] = True
         bits[e, rng.choice(k, e, replace=False)] = False
-    gst = _run(bsctx, k, r, matrix, L, nwin, bits)
+    gst = _run(ctx, k, r, matrix, L, nwin, bits)
     if matrix == "cauchy":  # MDS: any e <= r present repairs suffice
         assert list(gst[:r + 2]) == [0] * (r + 1) + [1]
     sl = rng.integers(1, L + 1, nwin).astype(np.uint32)
-    _run(bsctx, k, r, matrix, L, nwin, bits, sym_len=sl, seed=1)
+    _run(ctx, k, r, matrix, L, nwin, bits, sym_len=sl, seed=1)
 
 
 def test_wide_two_stage_path():
