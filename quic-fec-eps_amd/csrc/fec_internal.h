@@ -229,7 +229,8 @@ struct CombArgs {
     int sparse;
     uint32_t budget;
     // nullable (sliding-window decode): the call's error bits; the launch does
-    // nothing when kSwErrHeader is set (a bad header list recovers nothing)
+    // nothing when a kSwErrStop bit is set (a bad header list or a failed
+    // look-back recovers nothing)
     const uint32_t *err;
     ChkRange chk;  // FECGPU_CHECK builds: the arrays the jobs' rows lie in (inputs, xor rows, outputs)
     // every job has the same coefficient block (a block code's parity rows:
@@ -366,6 +367,10 @@ constexpr uint32_t kSwErrHeader = 1u;    // a bad or unordered header: the call 
 constexpr uint32_t kSwErrCapacity = 2u;  // a long system's operation log (or the queue) did not fit:
                                          // that system stays lost (a larger log fixes it)
 constexpr uint32_t kSwErrInternal = 4u;  // the plan's look-back gave up (never expected)
+// the flags on which every launch after the plan stands down: the lost-list
+// offsets and jobs would be built from a partial prefix (and stale scratch),
+// and writing recovered rows from them could overwrite received ones
+constexpr uint32_t kSwErrStop = kSwErrHeader | kSwErrInternal;
 static_assert(kSwErrHeader == FECGPU_SW_ERR_HEADER && kSwErrCapacity == FECGPU_SW_ERR_CAPACITY &&
                   kSwErrInternal == FECGPU_SW_ERR_INTERNAL,
               "the public flags are the device's bits");

@@ -32,8 +32,10 @@ constexpr int kXorLoads = 4;
 #define GF_ENC_U(R) ((R) <= 4 ? 2 : 8)
 // GF decode: input rows loaded per batch.  Decode's input rows come through an
 // LDS index (received sources, chosen repairs), so a deeper batch hides that
-// extra latency; cfg3 decode -1.7% vs 2 (scripts/ab.py, r01)
-constexpr int kGfdU = 8;
+// extra latency: 8 rows at r <= 4 (cfg3 decode -1.7% vs 2, scripts/ab.py r01);
+// at r > 4, 4 rows, which with the paired-row products below leave the
+// registers for 3 waves per SIMD (cfg4 decode 4.55 vs 4.59 ms, r06)
+#define GF_DEC_U(R) ((R) > 4 ? 4 : 8)
 // GF encode at r > 4 (VALU-bound, paired rows): at least 3 waves per SIMD, a
 // few spilled registers for occupancy: 7% faster than 2 waves on cfg4 (r01)
 #define GFE_WAVES __attribute__((amdgpu_waves_per_eu(R > 4 ? 3 : 1, 8)))
@@ -1300,7 +1302,7 @@ template <int R, int NE, int OFF = 0>
 __device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t out_delta,
                                          const DecRegion<R> &rg) {
     static_assert(OFF % 4 == 0 && OFF + NE <= R, "output range");
-    constexpr int U = kGfdU, R4 = DecRegion<R>::R4;
+    constexpr int U = GF_DEC_U(R), R4 = DecRegion<R>::R4;
     static_assert(U == 2 || U == 4 || U == 8, "row offsets are padded to 8 rows");
     uint4 acc[NE];
 #pragma unroll
@@ -1320,9 +1322,33 @@ __device__ __forceinline__ void dec_slot(uint8_t *base, int k, int ne, uint64_t 
         }
 #pragma unroll
         for (int t = 0; t < U; t++) v[t] = ld16(base + ro[t]);
+        // rows in pairs: one xor3 chain folds both rows' lookups (1.5 instead of
+        // 2 ops per product; cfg3 1.360 vs 1.372 ms, cfg4 4.55 vs 4.59 at 4-row
+        // batches, r06 — in r01, before the LDS index and 8-row batches, the
+        // pairs' registers cost more than they saved)
+        int t0 = 0;
+#pragma unroll
+        for (int t = 0; t + 1 < U; t += 2) {
+            if (q0 + t + 1 < k) {
+                const int q = q0 + t;
+                const Split s0 = split(v[t]), s1 = split(v[t + 1]);
+                uint32_t c0[R4], c1[R4];
+#pragma unroll
+                for (int j = 0; j < (NE + 3) / 4; j++) {
+                    const uint4 x = *reinterpret_cast<const uint4 *>(rg.tc + q * R4 + OFF + 4 * j);
+                    const uint4 y = *reinterpret_cast<const uint4 *>(rg.tc + (q + 1) * R4 + OFF + 4 * j);
+                    c0[4 * j] = x.x; c0[4 * j + 1] = x.y; c0[4 * j + 2] = x.z; c0[4 * j + 3] = x.w;
+                    c1[4 * j] = y.x; c1[4 * j + 1] = y.y; c1[4 * j + 2] = y.z; c1[4 * j + 3] = y.w;
+                }
+#pragma unroll
+                for (int m = 0; m < NE; m++)
+                    gmac2(acc[m], s0, s1, rg.ab[q * R + OFF + m], c0[m], rg.ab[(q + 1) * R + OFF + m], c1[m]);
+                t0 = t + 2;
+            }
+        }
 #pragma unroll
         for (int t = 0; t < U; t++) {
-            if (q0 + t < k) {
+            if (t >= t0 && q0 + t < k) {
                 const int q = q0 + t;
                 const Split sp = split(v[t]);
                 uint32_t c[R4];
@@ -1765,7 +1791,7 @@ __global__ __launch_bounds__(kBlock) void comb_kernel(CombArgs a) {
     // checked builds: every row a job reads or writes lies in the launch's
     // arrays (CombArgs::chk: inputs, xor rows, outputs)
     CHK_PROLOGUE(a);
-    if (a.err && (*a.err & kSwErrHeader)) return;  // the whole grid stands down (device-sized decode launches)
+    if (a.err && (*a.err & kSwErrStop)) return;  // the whole grid stands down (device-sized decode launches)
     const uint64_t njobs = a.njobs + (a.extra ? (uint64_t)(*a.extra >> a.extra_shift) : 0ull);
     int nin_max = a.nin_max, wpb = a.wpb;
     uint32_t job_lds = a.job_lds;

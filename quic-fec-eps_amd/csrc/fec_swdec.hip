@@ -1346,9 +1346,9 @@ __global__ __launch_bounds__(kBlock) void sw_dec_sys_kernel(SwDecArgs a) {
     gf_load(g);
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (a.ctr->err & kSwErrHeader) {
-        // a bad or unordered header list: the call recovers nothing and the
-        // statuses are the arrival flags.  The plan's blocks finished the
+    if (a.ctr->err & kSwErrStop) {
+        // a bad or unordered header list (or a failed look-back): the call
+        // recovers nothing and the statuses are the arrival flags.  The plan's blocks finished the
         // one-unknown systems of their chunks before every chunk's headers were
         // checked, so their statuses are undone here (the combine launches
         // stand down on the same flag, and write nothing).
@@ -1593,11 +1593,11 @@ __device__ bool long_compact(const SwDecArgs &a, LongLds &L, uint32_t c, int &na
 __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
     extern __shared__ uint4 dyn_long[];
     LongLds &L = *reinterpret_cast<LongLds *>(dyn_long);
-    if ((a.ctr->err & 1u) || blockIdx.x >= min(a.ctr->nlong, (uint32_t)a.long_cap)) return;  // nothing for this block
+    if ((a.ctr->err & kSwErrStop) || blockIdx.x >= min(a.ctr->nlong, (uint32_t)a.long_cap)) return;  // nothing for this block
     gf_load(L.g);
     __syncthreads();
     const int lane = threadIdx.x;
-    if (a.ctr->err & 1u) return;
+    if (a.ctr->err & kSwErrStop) return;
     const uint32_t nlong = min(a.ctr->nlong, (uint32_t)a.long_cap);
     uint32_t notab[5] = {0, 0, 0, 0, 0};
     for (uint32_t k = blockIdx.x; k < nlong; k += gridDim.x) {
@@ -1921,7 +1921,7 @@ __global__ __launch_bounds__(64) void sw_dec_long_kernel(SwDecArgs a) {
 __global__ __launch_bounds__(64) void sw_dec_replay_kernel(SwDecArgs a) {
     __shared__ uint32_t slots[kSwRows][64];
     const int lane = threadIdx.x;
-    if (a.ctr->err & 1u) return;
+    if (a.ctr->err & kSwErrStop) return;
     const uint32_t nlong = min(a.ctr->nlong, (uint32_t)a.long_cap);
     const uint32_t ndw = ((a.S + 15u) >> 4) * 4u;  // whole 16-B columns, as the combine passes
     const uint32_t nch = (ndw + 63) / 64;

@@ -576,6 +576,90 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W, 8))) void
     }
 }
 
+// three phases per step of G windows: (A) syndromes by the network, one
+// 32-B unit per lane, written to LDS in bytes; (B) the 4 x 4 solve, one 16-B
+// column per lane, in place in LDS; (C) the recovered rows stored front to back
+template <int G, int U, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void bs_dec3(
+    uint8_t *win, size_t nwin, const uint32_t *miss, const uint4 *sd, const uint32_t *sc) {
+    __shared__ uint4 img[G * R * NCOL];
+    __shared__ uint4 tab[G][R * R];
+    __shared__ uint32_t tcs[G][R * R];
+    __shared__ uint32_t sm[G];
+    for (XR xr = xr_make((nwin + G - 1) / G); xr.cur < xr.hi; xr.cur += xr.step) {
+        const size_t w0 = xr.cur * G;
+        const uint32_t nb = (uint32_t)std::min((size_t)G, nwin - w0);
+        for (uint32_t i = threadIdx.x; i < nb * R * R; i += 256) {
+            const uint32_t wl = i / (R * R), e = i - wl * R * R;
+            tab[wl][e] = sd[(w0 + wl) * R * R + e];
+            tcs[wl][e] = sc[(w0 + wl) * R * R + e];
+        }
+        if (threadIdx.x < nb) sm[threadIdx.x] = miss[w0 + threadIdx.x];
+        __syncthreads();
+        {   // (A)
+            const bool live = threadIdx.x < nb * H;
+            const uint32_t s = live ? threadIdx.x : nb * H - 1;
+            const uint32_t wl = s / H, u = s - wl * H;
+            const uint32_t m = sm[wl];
+            uint32_t pm = 0xFFFFu;
+#pragma unroll
+            for (int t = 0; t < R; t++) pm &= ~(1u << mrow(m, t));
+            uint8_t *pa = win + (w0 + wl) * WB + u * 16u;
+            uint8_t *pb = u + H < NCOL ? pa + H * 16u : pa;
+            uint32_t acc[R][8];
+            uint32_t x0[U][8];
+            dload<U, 0>(pa, pb, pm, x0);
+            dsources_pf<U, 0>(pa, pb, pm, x0, acc);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                const uint4 ra = ld16(pa + (size_t)(K + i) * S), rb = ld16(pb + (size_t)(K + i) * S);
+                bs::tr8(acc[i]);
+                if (live) {
+                    img[(wl * R + i) * NCOL + u] =
+                        make_uint4(acc[i][0] ^ ra.x, acc[i][1] ^ ra.y, acc[i][2] ^ ra.z, acc[i][3] ^ ra.w);
+                    if (u + H < NCOL)
+                        img[(wl * R + i) * NCOL + u + H] =
+                            make_uint4(acc[i][4] ^ rb.x, acc[i][5] ^ rb.y, acc[i][6] ^ rb.z, acc[i][7] ^ rb.w);
+                }
+            }
+        }
+        __syncthreads();
+        // (B)
+        for (uint32_t s = threadIdx.x; s < nb * NCOL; s += 256) {
+            const uint32_t wl = s / NCOL, c = s - wl * NCOL;
+            uint4 sg[R];
+#pragma unroll
+            for (int i = 0; i < R; i++) sg[i] = img[(wl * R + i) * NCOL + c];
+            uint4 out[R];
+#pragma unroll
+            for (int v = 0; v < R; v++) out[v] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < R; t += 2) {
+                const Split s0 = split(sg[t]), s1 = split(sg[t + 1]);
+#pragma unroll
+                for (int v = 0; v < R; v++) {
+                    const uint4 a0 = tab[wl][t * R + v], a1 = tab[wl][(t + 1) * R + v];
+                    const uint32_t c0 = tcs[wl][t * R + v], c1 = tcs[wl][(t + 1) * R + v];
+                    out[v].x = gm2(out[v].x, s0, s1, 0, a0, c0, a1, c1);
+                    out[v].y = gm2(out[v].y, s0, s1, 1, a0, c0, a1, c1);
+                    out[v].z = gm2(out[v].z, s0, s1, 2, a0, c0, a1, c1);
+                    out[v].w = gm2(out[v].w, s0, s1, 3, a0, c0, a1, c1);
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < R; v++) img[(wl * R + v) * NCOL + c] = out[v];
+        }
+        __syncthreads();
+        // (C)
+        for (uint32_t q = threadIdx.x; q < nb * R * NCOL; q += 256) {
+            const uint32_t wl = q / (R * NCOL), o = q - wl * (R * NCOL), v = o / NCOL, c = o - v * NCOL;
+            st16(win + (w0 + wl) * WB + (size_t)mrow(sm[wl], v) * S + c * 16u, img[q]);
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace fecgpu
 
 using namespace fecgpu;
@@ -660,7 +744,7 @@ int main() {
             const double ms = time_ms([&] { hipLaunchKernelGGL(tab_flat, cus * gm, 256, 0, 0, win, nwin, gab, gc); });
             report("tab_flat", gm, ms);
         }
-        for (int gm : {1, 2, 3, 4}) {
+        for (int gm : {2}) {
             double ms = time_ms([&] { hipLaunchKernelGGL((bs_flat<2>), cus * gm, 256, 0, 0, win, nwin); });
             report("bs_flat_U2", gm, ms);
         }
@@ -751,19 +835,16 @@ int main() {
                 const double ms = time_ms([&] { hipLaunchKernelGGL((bs_dec2<G, NT, U, PF, GS>), cus * gm, NT, 0, 0, win, nwin, dm, dsd, dsc); }); \
                 report("bs_dec2_G" #G "_" #NT "_U" #U "_pf" #PF "_gs" #GS, gm, ms);                           \
             }
-            DEC2(3, 128, 2, true, false, (std::initializer_list<int>{4}))
             DEC2(6, 256, 2, true, false, (std::initializer_list<int>{2}))
-#define DEC3(G, NT, U, PF, GS, W, GMS)                                                                       \
+#define DEC4(G, U, W, GMS)                                                                                   \
             for (int gm : GMS) {                                                                             \
-                const double ms = time_ms([&] { hipLaunchKernelGGL((bs_dec2<G, NT, U, PF, GS, W>), cus * gm, NT, 0, 0, win, nwin, dm, dsd, dsc); }); \
-                report("bs_dec2_G" #G "_" #NT "_U" #U "_pf" #PF "_gs" #GS "_w" #W, gm, ms);                 \
+                const double ms = time_ms([&] { hipLaunchKernelGGL((bs_dec3<G, U, W>), cus * gm, 256, 0, 0, win, nwin, dm, dsd, dsc); }); \
+                report("bs_dec3_G" #G "_U" #U "_w" #W, gm, ms);                                             \
             }
-            DEC3(3, 128, 2, true, false, 3, (std::initializer_list<int>{6}))
-            DEC3(3, 128, 2, true, false, 4, (std::initializer_list<int>{8}))
-            DEC3(6, 256, 2, true, false, 3, (std::initializer_list<int>{3}))
-            DEC3(6, 256, 2, true, false, 4, (std::initializer_list<int>{4}))
-            DEC3(3, 128, 2, true, true, 3, (std::initializer_list<int>{5}))
-            DEC3(6, 256, 2, true, true, 3, (std::initializer_list<int>{2}))
+            DEC4(6, 2, 1, (std::initializer_list<int>{2, 3, 4}))
+            DEC4(6, 2, 4, (std::initializer_list<int>{4}))
+            DEC4(6, 1, 4, (std::initializer_list<int>{4}))
+            DEC4(3, 2, 4, (std::initializer_list<int>{4, 6}))
         }
     }
     printf("  {\"end\": true}\n]}\n");
