@@ -142,6 +142,9 @@ void    fecgpu_host_free(void *p);
  * encode of a code with a compiled bit-sliced kernel — Cauchy or Vandermonde
  * rows, r = 8, k in {16, 24, 32} — uses it, and of any other code with r >= 5
  * the runtime-mask bit-sliced kernel; 0: the table multiply for every code);
+ * "bsdec" (1 default: GF decode of Cauchy k 16 r 4 on uniform rows whose
+ * windows fill a 512-thread workgroup — about 1-8 KiB — by the bit-sliced
+ * syndrome kernel; 0: the table decode; the bytes are the same);
  * "sw_group" (sliding-window encode by combine jobs: consecutive repairs per
  * job, each source loaded once per group; 1, 2, 4 or 8, default 4);
  * "sw_stream" (sliding-window encode: 0 combine jobs, 1..5 the streaming

@@ -156,6 +156,9 @@ struct fecgpu_ctx {
     // bit-sliced encode of short uniform rows with gathered stores
     // (gf_encode_bs_gs_kernel): 1 on, 0 the flat bit-sliced kernel
     int gs = 1;
+    // GF decode of Cauchy k 16 r 4 on uniform short rows by the bit-sliced
+    // syndrome kernel (gf_decode_bs_gs_kernel): 1 on, 0 the table decode
+    int bsdec = 1;
     int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
     int sw_stream = kSwStreamDefault;  // sliding-window encode: 0 combine jobs, 1..5 streaming
                                        // (dwords per lane), kSwStreamAuto per symbol size
@@ -318,6 +321,11 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
     if (!std::strcmp(key, "gs")) {
         if (value < 0 || value > 1) return FECGPU_ERR_INVALID_ARG;
         ctx->gs = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "bsdec")) {
+        if (value < 0 || value > 1) return FECGPU_ERR_INVALID_ARG;
+        ctx->bsdec = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "bs_passes")) {
@@ -960,6 +968,24 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         const uint32_t units = (c16 + kRbsCols - 1) / kRbsCols;
         const uint32_t want = (uint32_t)ctx->bs_passes * kBlock;
         p.wpb = units ? std::max(1, std::min<int>(kMaxWpb, (int)((want + units - 1) / units))) : kMaxWpb;
+    }
+    if (decode && scheme == FECGPU_SCHEME_GF256 && !remote && ctx->bsdec && ctx->bitslice && !win_off &&
+        !sym_len && ncol && ctx->wpb_override <= 0 && bsdec_supported(k, r, (int)code->matrix)) {
+        // whole windows per step, a lane per unit of two 16-B columns (at least
+        // 3/4 of the lanes busy), the step's syndromes / recovered rows in one
+        // LDS image within 64 KB, and the kernel's buffer resource over the
+        // step's windows (G pitches < 2^31 B)
+        const uint32_t units = (ncol + 1) / 2, nt = (uint32_t)kBsdBlock;
+        const uint32_t G = std::min<uint32_t>(nt / std::max(units, 1u), (uint32_t)kBsdMaxG);
+        const uint32_t img = (uint32_t)r * ncol * 16u;
+        if (units <= nt && G >= 1 && G * units * 4 >= 3u * nt && G * img <= (64u << 10) &&
+            (uint64_t)G * a.wpitch < (1ull << 31)) {
+            p.bsdec = true;
+            p.wpb = (int)G;
+            p.win_lds = 0;
+            p.lds_bytes = G * img;
+            if (p.grid_mult <= 0 && p.blocks_per_cu <= 0) p.grid_mult = 1;
+        }
     }
     if (remote) {  // PCIe-latency bound: as many workgroups as windows
         p.remote = true;

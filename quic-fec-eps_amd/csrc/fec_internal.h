@@ -101,6 +101,7 @@ struct LaunchPlan {
     int matrix;          // bitslice: the code's matrix (fecgpu_matrix)
     bool rbitslice;      // GF encode by the runtime-mask bit-sliced kernel (any matrix)
     bool bsgs;           // bit-sliced encode with gathered stores (gf_encode_bs_gs_kernel)
+    bool bsdec;          // GF decode by the bit-sliced syndrome kernel (gf_decode_bs_gs_kernel)
 };
 
 // GF encode of r parity rows goes to the runtime-mask bit-sliced kernel
@@ -114,6 +115,12 @@ constexpr int kRbsDw4 = 2;
 
 // GF encode of (k, r, matrix) has a compiled bit-sliced kernel.
 bool bitslice_supported(int k, int r, int matrix);
+// GF decode of (k, r, matrix) has a bit-sliced syndrome kernel (gf_decode_bs_gs_kernel).
+bool bsdec_supported(int k, int r, int matrix);
+// bit-sliced syndrome decode: threads per workgroup, and most windows per
+// workgroup step (per-window plan tables in static LDS)
+constexpr int kBsdBlock = 512;
+constexpr int kBsdMaxG = 16;
 
 // Per-window LDS region of the GF decode kernel (fec_kernels.hip DecRegion):
 // tables [k][R] uint4 (TA/TB) + [k][round_up(R, 4)] u32 (TC), input row byte
