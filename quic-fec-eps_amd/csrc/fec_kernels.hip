@@ -774,9 +774,9 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_gs_kernel(BatchArgs a) {
         const uint32_t nu = nb * h;
         {
             // lanes past the last unit redo it and write nothing (uniform trip count)
-#if GSE_PRIO
-            __builtin_amdgcn_s_setprio(GSE_PRIO);
-#endif
+            // the network at priority 1, the stores below at 0 (1.203 vs
+            // 1.211 ms on cfg3, r06)
+            __builtin_amdgcn_s_setprio(1);
             const bool live = threadIdx.x < nu;
             const uint32_t s = live ? threadIdx.x : nu - 1;
             const uint32_t wl = fdiv(s, dh), u = s - wl * h;
@@ -794,9 +794,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_gs_kernel(BatchArgs a) {
                 }
             }
         }
-#if GSE_PRIO
         __builtin_amdgcn_s_setprio(0);
-#endif
         __syncthreads();
         for (uint32_t q = threadIdx.x; q < nb * R * ncol; q += kBlock) {
             const uint32_t wl = fdiv(q, drn), o = q - wl * R * ncol, i = fdiv(o, dn), c = o - i * ncol;
@@ -1527,19 +1525,6 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
 // solve in registers right after the network (199-225 VGPRs, 2 waves per
 // SIMD: 1.47 ms with per-lane stores, 1.53 gathered) and (B) storing its
 // columns directly (1.61 ms).
-// wave priority during phase (A) (s_setprio: the waves issuing loads win
-// issue arbitration over the other workgroup's solve; 1: cfg3 1.280 vs 1.310
-// ms at 0, r06) and during the stores of phase (C)
-#ifndef BSD_PRIO
-#define BSD_PRIO 1
-#endif
-#ifndef BSD_PRIO_C
-#define BSD_PRIO_C 0
-#endif
-// the gathered-store encode: priority while the network runs (stores at 0)
-#ifndef GSE_PRIO
-#define GSE_PRIO 0
-#endif
 namespace bsd {
 
 constexpr int kMaxG = kBsdMaxG;
@@ -1657,9 +1642,10 @@ __global__ __launch_bounds__(kBsdBlock) void gf_decode_bs_gs_kernel(BatchArgs a)
         {
             // (A) syndromes: lane = unit; lanes past the last unit redo it and
             // write nothing (uniform trip count)
-#if BSD_PRIO
-            __builtin_amdgcn_s_setprio(BSD_PRIO);
-#endif
+            // waves issuing loads win issue arbitration over the other
+            // workgroup's solve (s_setprio 1: 1.277 vs 1.310 ms on cfg3; 2,
+            // and 1 for the stores of (C) as well, the same, r06)
+            __builtin_amdgcn_s_setprio(1);
             const bool live = threadIdx.x < nu;
             const uint32_t s = live ? threadIdx.x : nu - 1;
             const uint32_t wl = fdiv(s, dh), u = s - wl * h;
@@ -1705,9 +1691,7 @@ __global__ __launch_bounds__(kBsdBlock) void gf_decode_bs_gs_kernel(BatchArgs a)
                 }
             }
         }
-#if BSD_PRIO
         __builtin_amdgcn_s_setprio(0);
-#endif
         __syncthreads();
         // (B) the e x e solve per 16-B column, in place
         for (uint32_t q = threadIdx.x; q < nb * ncol; q += NT) {
@@ -1720,9 +1704,6 @@ __global__ __launch_bounds__(kBsdBlock) void gf_decode_bs_gs_kernel(BatchArgs a)
             for (int v = 0; v < R; v++) im[(wl * R + v) * ncol + c] = out[v];
         }
         __syncthreads();
-#if BSD_PRIO_C
-        __builtin_amdgcn_s_setprio(BSD_PRIO_C);
-#endif
         // (C) recovered rows front to back: consecutive lanes on consecutive
         // 16-B chunks, a whole step's rows in one burst (storing from (B)
         // instead, where a row's lines are finished by two waves at different
@@ -1734,9 +1715,6 @@ __global__ __launch_bounds__(kBsdBlock) void gf_decode_bs_gs_kernel(BatchArgs a)
                 st16(a.win + (w0 + wl) * a.wpitch + a.out_delta + (size_t)row * a.stride + c * 16u, im[q]);
             }
         }
-#if BSD_PRIO_C
-        __builtin_amdgcn_s_setprio(0);
-#endif
         const uint64_t nx = xr.cur + xr.step;
         if (nx < xr.hi) bsd::plan<K, R>(a, L, buf ^ 1, nx * G, (uint32_t)min((uint64_t)G, a.nwin - nx * G));
         __syncthreads();
