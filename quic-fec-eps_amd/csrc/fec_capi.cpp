@@ -976,14 +976,14 @@ ssize_t launch_device(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, Bat
         // LDS image within 64 KB, and the kernel's buffer resource over the
         // step's windows (G pitches < 2^31 B)
         const uint32_t units = (ncol + 1) / 2, nt = (uint32_t)kBsdBlock;
-        const uint32_t G = std::min<uint32_t>(nt / std::max(units, 1u), (uint32_t)kBsdMaxG);
+        const uint32_t G = std::min<uint32_t>(nt / std::max(units, 1u), nt / (uint32_t)(r * r));
         const uint32_t img = (uint32_t)r * ncol * 16u;
         if (units <= nt && G >= 1 && G * units * 4 >= 3u * nt && G * img <= (64u << 10) &&
             (uint64_t)G * a.wpitch < (1ull << 31)) {
             p.bsdec = true;
             p.wpb = (int)G;
             p.win_lds = 0;
-            p.lds_bytes = G * img;
+            p.lds_bytes = bsd_lds_bytes(G, r, ncol);
             if (p.grid_mult <= 0 && p.blocks_per_cu <= 0) p.grid_mult = 1;
         }
     }

@@ -117,10 +117,14 @@ constexpr int kRbsDw4 = 2;
 bool bitslice_supported(int k, int r, int matrix);
 // GF decode of (k, r, matrix) has a bit-sliced syndrome kernel (gf_decode_bs_gs_kernel).
 bool bsdec_supported(int k, int r, int matrix);
-// bit-sliced syndrome decode: threads per workgroup, and most windows per
-// workgroup step (per-window plan tables in static LDS)
+// bit-sliced syndrome decode: threads per workgroup; dynamic LDS of a workgroup taking G windows of
+// ncol columns per step (fec_kernels.hip bsd::Lds): the image, then two
+// buffers of solve tables (20 B per entry, r * r + 1 per window) and three
+// words per window.  The plan uses r * r lanes per window: G * r * r <= threads.
 constexpr int kBsdBlock = 512;
-constexpr int kBsdMaxG = 16;
+inline uint32_t bsd_lds_bytes(uint32_t G, int r, uint32_t ncol) {
+    return G * (uint32_t)r * ncol * 16u + 2u * G * (uint32_t)(r * r + 1) * 20u + 6u * G * 4u;
+}
 
 // Per-window LDS region of the GF decode kernel (fec_kernels.hip DecRegion):
 // tables [k][R] uint4 (TA/TB) + [k][round_up(R, 4)] u32 (TC), input row byte

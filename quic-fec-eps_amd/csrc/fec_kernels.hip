@@ -1516,34 +1516,48 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
 // Ainv of the Cauchy block A[t][u] = 1 / (x_t ^ m_u), x_t = k + i_t, in closed
 // form (the repair entries of plan_gf's D): log Ainv[u][t] = A_u + K_t -
 // log(x_t ^ m_u), one lane per entry.  A workgroup takes G whole windows per
-// step (G * ceil(ncol / 2) <= kBsdBlock units of two 16-B columns, as the
+// step (G * ceil(ncol / 2) <= NT units of two 16-B columns, as the
 // gathered-store encode) in three phases: (A) syndromes by the network, a lane
 // per unit, to an LDS image [window][repair][column] in bytes; (B) the solve
 // per 16-B column, in place; (C) the recovered rows stored front to back.
-// cfg3: 1.295 ms against 1.357 for the table decode in-process (512 threads,
-// 13 windows a step; 256 threads 1.306).  Measured and removed (r06): the
+// cfg3: 1.28 ms against 1.36 for the table decode in-process (512 threads,
+// 13 windows a step; 256 threads, 6 windows, 4 workgroups per CU: 1.29-1.30).  Measured and removed (r06): the
 // solve in registers right after the network (199-225 VGPRs, 2 waves per
 // SIMD: 1.47 ms with per-lane stores, 1.53 gathered) and (B) storing its
 // columns directly (1.61 ms).
 namespace bsd {
 
-constexpr int kMaxG = kBsdMaxG;
 
+// Per-step LDS after the image (fec_internal.h bsd_lds_bytes), two buffers:
+// ab / tc [buf][window][i * R + u] the solve's tables, syndrome of repair i ->
+// output u (0 unless chosen; one pad entry per window, so two windows' tables
+// read by one wave start on different LDS banks); pm the rows to load
+// (received sources: bits < k, chosen repairs: k + i; 0: no work); rows byte
+// u: missing source m_u; ne: sources recovered
 template <int R>
 struct Lds {
-    // [buf][window][i * R + u]: syndrome of repair i -> output u (0 unless
-    // chosen); one pad entry per window, so two windows' tables read by one
-    // wave start on different LDS banks
-    uint4 ab[2][kMaxG][R * R + 1];
-    uint32_t tc[2][kMaxG][R * R + 1];
-    uint32_t pm[2][kMaxG];      // rows to load: received sources (bits < k), chosen repairs (k + i); 0: no work
-    uint32_t rows[2][kMaxG];    // byte u: missing source m_u
-    uint32_t ne[2][kMaxG];
-    uint8_t ex[512], lg[256];
+    static constexpr uint32_t E = R * R + 1;
+    uint4 *ab_;
+    uint32_t *tc_, *pm_, *rows_, *ne_;
+    uint32_t G;
+    const uint8_t *ex, *lg;
+    __device__ __forceinline__ Lds(uint4 *im, uint32_t G_, uint32_t ncol, const uint8_t *ex_, const uint8_t *lg_)
+        : G(G_), ex(ex_), lg(lg_) {
+        ab_ = im + (size_t)G * R * ncol;
+        tc_ = reinterpret_cast<uint32_t *>(ab_ + 2 * G * E);
+        pm_ = tc_ + 2 * G * E;
+        rows_ = pm_ + 2 * G;
+        ne_ = rows_ + 2 * G;
+    }
+    __device__ __forceinline__ uint4 *ab(int buf, uint32_t wl) const { return ab_ + (buf * G + wl) * E; }
+    __device__ __forceinline__ uint32_t *tc(int buf, uint32_t wl) const { return tc_ + (buf * G + wl) * E; }
+    __device__ __forceinline__ uint32_t &pm(int buf, uint32_t wl) const { return pm_[buf * G + wl]; }
+    __device__ __forceinline__ uint32_t &rows(int buf, uint32_t wl) const { return rows_[buf * G + wl]; }
+    __device__ __forceinline__ uint32_t &ne(int buf, uint32_t wl) const { return ne_[buf * G + wl]; }
 };
 
 template <int K, int R>
-__device__ __forceinline__ void plan(const BatchArgs &a, Lds<R> &L, int buf, uint64_t w0, uint32_t nb) {
+__device__ __forceinline__ void plan(const BatchArgs &a, const Lds<R> &L, int buf, uint64_t w0, uint32_t nb) {
     const uint32_t tid = threadIdx.x;
     if (tid >= nb * R * R) return;
     const uint32_t wl = tid / (R * R), idx = tid - wl * (R * R), i = idx / R, u = idx - i * R;
@@ -1584,16 +1598,16 @@ __device__ __forceinline__ void plan(const BatchArgs &a, Lds<R> &L, int buf, uin
         c = L.ex[s % 255];
     }
     const CoefTab ct = make_coef_tab(c);
-    L.ab[buf][wl][idx] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
-    L.tc[buf][wl][idx] = ct.c;
+    L.ab(buf, wl)[idx] = make_uint4(ct.a_lo, ct.a_hi, ct.b_lo, ct.b_hi);
+    L.tc(buf, wl)[idx] = ct.c;
     if (idx == 0) {
         a.status[w0 + wl] = (e == 0 || ok) ? 0 : 1;
-        L.pm[buf][wl] = ok ? ((~miss & kmask) | (chosen << K)) : 0u;
+        L.pm(buf, wl) = ok ? ((~miss & kmask) | (chosen << K)) : 0u;
         uint32_t rows = 0;
 #pragma unroll
         for (int v = 0; v < R; v++) rows |= (uint32_t)mv[v] << (8 * v);
-        L.rows[buf][wl] = rows;
-        L.ne[buf][wl] = ok ? (uint32_t)e : 0u;
+        L.rows(buf, wl) = rows;
+        L.ne(buf, wl) = ok ? (uint32_t)e : 0u;
     }
 }
 
@@ -1618,17 +1632,17 @@ __device__ __forceinline__ void solve_col(const uint4 (&s)[R], uint4 (&out)[R], 
 
 }  // namespace bsd
 
-template <int K, int R, int M>
-__global__ __launch_bounds__(kBsdBlock) void gf_decode_bs_gs_kernel(BatchArgs a) {
+template <int K, int R, int M, int NT>
+__global__ __launch_bounds__(NT) void gf_decode_bs_gs_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
     static_assert(M == FECGPU_MATRIX_CAUCHY, "closed-form plan: Cauchy rows");
-    constexpr uint32_t NT = kBsdBlock;
-    extern __shared__ uint4 im[];  // [window][syndrome, then output][column]
-    __shared__ bsd::Lds<R> L;
+    extern __shared__ uint4 im[];  // [window][syndrome, then output][column], then bsd::Lds
+    __shared__ uint8_t s_ex[512], s_lg[256];
     const uint32_t ncol = a.ncol, h = (ncol + 1) >> 1, G = (uint32_t)a.wpb;
+    const bsd::Lds<R> L(im, G, ncol, s_ex, s_lg);
     const FastDiv dh = fdiv_make(h), dn = fdiv_make(ncol), drn = fdiv_make(R * ncol);
-    for (uint32_t i = threadIdx.x; i < 512; i += NT) L.ex[i] = c_gf.exp[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += NT) L.lg[i] = c_gf.log[i];
+    for (uint32_t i = threadIdx.x; i < 512; i += NT) s_ex[i] = c_gf.exp[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += NT) s_lg[i] = c_gf.log[i];
     __syncthreads();
     XcdRange xr = xcd_range((a.nwin + G - 1) / G, a.nx);
     // the next step's plan is made before each step's last barrier (its LDS
@@ -1649,7 +1663,7 @@ __global__ __launch_bounds__(kBsdBlock) void gf_decode_bs_gs_kernel(BatchArgs a)
             const bool live = threadIdx.x < nu;
             const uint32_t s = live ? threadIdx.x : nu - 1;
             const uint32_t wl = fdiv(s, dh), u = s - wl * h;
-            const uint32_t pm = L.pm[buf][wl];
+            const uint32_t pm = L.pm(buf, wl);
             uint8_t *pa, *pb;
             bs::unit_cols(a.win + (w0 + wl) * a.wpitch, u, h, ncol, pa, pb);
             uint32_t acc[R][8];
@@ -1699,7 +1713,7 @@ __global__ __launch_bounds__(kBsdBlock) void gf_decode_bs_gs_kernel(BatchArgs a)
             uint4 sg[R], out[R];
 #pragma unroll
             for (int i = 0; i < R; i++) sg[i] = im[(wl * R + i) * ncol + c];
-            bsd::solve_col<R>(sg, out, L.ab[buf][wl], L.tc[buf][wl]);
+            bsd::solve_col<R>(sg, out, L.ab(buf, wl), L.tc(buf, wl));
 #pragma unroll
             for (int v = 0; v < R; v++) im[(wl * R + v) * ncol + c] = out[v];
         }
@@ -1710,8 +1724,8 @@ __global__ __launch_bounds__(kBsdBlock) void gf_decode_bs_gs_kernel(BatchArgs a)
         // times, measured 1.61 vs 1.31 ms on cfg3, r06)
         for (uint32_t q = threadIdx.x; q < nb * R * ncol; q += NT) {
             const uint32_t wl = fdiv(q, drn), o = q - wl * R * ncol, v = fdiv(o, dn), c = o - v * ncol;
-            if (v < L.ne[buf][wl]) {
-                const uint32_t row = (L.rows[buf][wl] >> (8 * v)) & 0xFFu;
+            if (v < L.ne(buf, wl)) {
+                const uint32_t row = (L.rows(buf, wl) >> (8 * v)) & 0xFFu;
                 st16(a.win + (w0 + wl) * a.wpitch + a.out_delta + (size_t)row * a.stride + c * 16u, im[q]);
             }
         }
@@ -2479,9 +2493,17 @@ bool bsdec_supported(int k, int r, int matrix) { return matrix == FECGPU_MATRIX_
 hipError_t launch_decode(int scheme, const BatchArgs &a, const LaunchPlan &p, hipStream_t s) {
     if (a.nwin == 0) return hipSuccess;
     if (p.bsdec) {
-        if (a.k != 16 || a.r != 4 || a.wpb < 1 || a.wpb > bsd::kMaxG) return hipErrorInvalidValue;
-        return launch(gf_decode_bs_gs_kernel<16, 4, FECGPU_MATRIX_CAUCHY>, a, p, s, false, (a.nwin + a.wpb - 1) / a.wpb,
-                      kBsdBlock);
+        if (a.k != 16 || a.r != 4 || a.wpb < 1 || a.wpb * 16 > kBsdBlock) return hipErrorInvalidValue;
+        const uint64_t chunks = (a.nwin + a.wpb - 1) / a.wpb;
+        auto go = [&](auto kernel, int nt) {
+            if (p.lds_bytes > (64u << 10)) {  // past the default dynamic LDS cap
+                const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes);
+                if (e != hipSuccess) return e;
+            }
+            return launch(kernel, a, p, s, false, chunks, nt);
+        };
+        return go(gf_decode_bs_gs_kernel<16, 4, FECGPU_MATRIX_CAUCHY, kBsdBlock>, kBsdBlock);
     }
     if (scheme == 0) {
         if (p.flat) DISPATCH_R(a.r, launch(xor_decode_kernel<RR, true>, a, p, s, true))
