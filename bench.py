@@ -105,6 +105,8 @@ def parse():
                          "--r, config 3's workload (1200-B packets, exactly r sources erased) on that code, "
                          "~5 GB of source bytes per GPU")
     ap.add_argument("--r", type=int, default=0, help="repairs per window for --k")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VAL",
+                    help="tuning: fecgpu_ctx_set_tuning(KEY, VAL), repeatable")
     ap.add_argument("--extra-configs", type=int, choices=[0, 1], default=1,
                     help="default run (config 3): also time configs 2, 4, 5 and 7 in this process and "
                          "report them under \"configs\" (0 = config 3 only)")
@@ -349,6 +351,9 @@ def make_ctx(args):
         ctx.set_tuning("host_direct", args.host_direct)
     if args.host_chunk_mb:
         ctx.set_tuning("host_chunk_mb", args.host_chunk_mb)
+    for kv in args.tune:
+        key, val = kv.split("=", 1)
+        ctx.set_tuning(key, int(val))
     return ctx
 
 

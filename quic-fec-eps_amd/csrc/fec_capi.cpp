@@ -159,6 +159,9 @@ struct fecgpu_ctx {
     // GF decode of Cauchy k 16 r 4 on uniform short rows by the bit-sliced
     // syndrome kernel (gf_decode_bs_gs_kernel): 1 on, 0 the table decode
     int bsdec = 1;
+    // wide decode (k + r > 64): stage 1 by plane picks skips the missing rows
+    // (1, default) instead of reading the rows the plan zeroed (0)
+    int wide_mask = 1;
     int sw_group = 4;  // sliding-window encode: repairs per combine job (1, 2, 4, 8)
     int sw_stream = kSwStreamDefault;  // sliding-window encode: 0 combine jobs, 1..5 streaming
                                        // (dwords per lane), kSwStreamAuto per symbol size
@@ -326,6 +329,11 @@ ssize_t fecgpu_ctx_set_tuning(fecgpu_ctx *ctx, const char *key, int64_t value) {
     if (!std::strcmp(key, "bsdec")) {
         if (value < 0 || value > 1) return FECGPU_ERR_INVALID_ARG;
         ctx->bsdec = (int)value;
+        return 0;
+    }
+    if (!std::strcmp(key, "wide_mask")) {
+        if (value < 0 || value > 1) return FECGPU_ERR_INVALID_ARG;
+        ctx->wide_mask = (int)value;
         return 0;
     }
     if (!std::strcmp(key, "bs_passes")) {
@@ -728,7 +736,7 @@ ssize_t run_wide(fecgpu_ctx *ctx, const fecgpu_code *code, bool decode, uint8_t 
         HIP_TRY(launch_wide(win, present, status, P, nwin, stride, ncol, k, r, decode, reinterpret_cast<CombJob *>(b),
                             reinterpret_cast<uint64_t *>(b + o_out), b + o_coef, s,
                             reinterpret_cast<CombJob *>(b + o_j1), reinterpret_cast<uint64_t *>(b + o_o1), b + o_syn,
-                            mP, decode ? mPI : nullptr, chk),
+                            mP, decode ? mPI : nullptr, chk, ctx->wide_mask != 0),
                 "wide batch launch");
     }
     rc = ctx_chk_finish(ctx, s, decode ? "wide decode" : "wide encode");  // FECGPU_CHECK builds (release: nothing)

@@ -85,6 +85,10 @@ struct BatchArgs {
     // ragged layout (win_off): symbol pitch of every window; 0 = packed
     // round_up(S_w, 16)
     uint32_t off_stride;
+    // runtime bit-sliced rows (launch_rbs_rows) of the wide decode's stage 1:
+    // present words per window in `present` (0: every input row is read); an
+    // absent row is read as zeros, with no memory access
+    uint32_t pres_nw;
     ChkRange chk;              // FECGPU_CHECK builds: where this launch's symbols lie
 };
 
@@ -115,6 +119,9 @@ constexpr int kRbsDw4 = 2;
 
 // GF encode of (k, r, matrix) has a compiled bit-sliced kernel.
 bool bitslice_supported(int k, int r, int matrix);
+// launch_rbs_rows with present masks reads through a raw buffer resource per
+// wave over the windows its lanes touch: true when that span stays below 2^31 B
+bool rbs_masked_ok(uint32_t ncol, uint64_t wpitch);
 // GF decode of (k, r, matrix) has a bit-sliced syndrome kernel (gf_decode_bs_gs_kernel).
 bool bsdec_supported(int k, int r, int matrix);
 // bit-sliced syndrome decode: threads per workgroup; dynamic LDS of a workgroup taking G windows of
@@ -271,7 +278,8 @@ __host__ __device__ inline uint32_t comb_job_small_lds(int R) {
 hipError_t launch_comb(CombArgs a, int R, hipStream_t s);
 // the runtime-mask bit-sliced encode over uniform windows of any k (fec_kernels.hip)
 hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t stride, uint64_t wpitch, int k,
-                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s);
+                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s,
+                           const uint64_t *present = nullptr, uint32_t pres_nw = 0);
 // GF block codes with k + r > 64 (fec_wide.hip): encode by the runtime-mask
 // bit-sliced kernel (r >= 4) or a combine job per window; decode in two stages
 // (syndromes of every repair with one coefficient block [P | I] for all
@@ -282,7 +290,7 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
                        uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
                        uint64_t *outs, uint8_t *coef, hipStream_t s, CombJob *jobs1, uint64_t *outs1,
                        uint8_t *syn, const uint32_t *masks_P = nullptr, const uint32_t *masks_PI = nullptr,
-                       ChkRec *chk = nullptr);
+                       ChkRec *chk = nullptr, bool mask_rows = true);
 
 // encode: job t = repair t (coefficients at coef + t * kSwCoefPitch, output rep row t).
 // group > 1: the repairs t0 = g * group .. t0 + group - 1 share job g when

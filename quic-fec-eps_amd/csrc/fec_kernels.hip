@@ -977,11 +977,87 @@ __device__ __forceinline__ void unit_cols(uint8_t *base, uint32_t u, uint32_t h,
     for (int c = 1; c < 4; c++) pc[c] = u + c * h < ncol ? pc[0] + c * h * 16u : pc[0];
 }
 
+// unit() over the rows present in the window (pw: its presence words, row j =
+// bit j % 64 of word j / 64); an absent row reads as zeros.  Release builds
+// load through the wave's buffer resource rs over gb (co: the unit's column
+// offsets from gb, row j at scalar offset j * stride; 4 VGPRs instead of the
+// columns' 8 pointer words), an absent row's offset
+// pushed past the records (bs::kOob): no branch, no memory access (exec-masked
+// ld16 loads measured 1.87 vs 1.67 ms at k 120, r05).  Checked builds use ld16
+// under the mask.
+template <int R>
+__device__ __forceinline__ void unit_m(__amdgpu_buffer_rsrc_t rs, uint8_t *gb, const uint32_t (&co)[4],
+                                       uint32_t stride, int k, cmask mk, bool live, uint64_t od,
+                                       const uint64_t *pw) {
+    uint32_t aa[R][8], ab[R][8];
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int p = 0; p < 8; p++) aa[i][p] = ab[i][p] = 0;
+    uint64_t cur = pw[0];
+    auto ldm = [&](int j, uint32_t (&xa)[8], uint32_t (&xb)[8]) {
+        const bool on = (cur >> (j & 63)) & 1ull;
+#if FECGPU_CHECK
+        (void)rs;
+        (void)co;
+        uint4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) v[c] = on ? ld16(gb + co[c] + (size_t)j * stride) : zero4();
+        xa[0] = v[0].x; xa[1] = v[0].y; xa[2] = v[0].z; xa[3] = v[0].w;
+        xa[4] = v[1].x; xa[5] = v[1].y; xa[6] = v[1].z; xa[7] = v[1].w;
+        xb[0] = v[2].x; xb[1] = v[2].y; xb[2] = v[2].z; xb[3] = v[2].w;
+        xb[4] = v[3].x; xb[5] = v[3].y; xb[6] = v[3].z; xb[7] = v[3].w;
+#else
+        const uint32_t d = on ? 0u : bs::kOob;
+        const int so = (int)((uint32_t)j * stride);
+        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(co[0] + d), so, 0);
+        const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(co[1] + d), so, 0);
+        const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(co[2] + d), so, 0);
+        const u32x4 v3 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(co[3] + d), so, 0);
+        xa[0] = v0.x; xa[1] = v0.y; xa[2] = v0.z; xa[3] = v0.w;
+        xa[4] = v1.x; xa[5] = v1.y; xa[6] = v1.z; xa[7] = v1.w;
+        xb[0] = v2.x; xb[1] = v2.y; xb[2] = v2.z; xb[3] = v2.w;
+        xb[4] = v3.x; xb[5] = v3.y; xb[6] = v3.z; xb[7] = v3.w;
+#endif
+    };
+    uint32_t xa[8], xb[8];
+    ldm(0, xa, xb);
+    for (int j = 0; j < k; j++) {
+        const int jn = min(j + 1, k - 1);
+        if (jn != j && (jn & 63) == 0) cur = pw[jn >> 6];  // wave-uniform: once per 64 rows
+        uint32_t na[8], nb[8];
+        ldm(jn, na, nb);
+        bs::tr8(xa);
+        bs::tr8(xb);
+        source<R>(xa, xb, aa, ab, mk + (size_t)j * (R * 2 * kRbsDw4));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            xa[q] = na[q];
+            xb[q] = nb[q];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        bs::tr8(aa[i]);
+        bs::tr8(ab[i]);
+        if (live) {
+            uint8_t *o = gb + od + (size_t)(k + i) * stride;
+            st16(o + co[0], make_uint4(aa[i][0], aa[i][1], aa[i][2], aa[i][3]));
+            st16(o + co[1], make_uint4(aa[i][4], aa[i][5], aa[i][6], aa[i][7]));
+            st16(o + co[2], make_uint4(ab[i][0], ab[i][1], ab[i][2], ab[i][3]));
+            st16(o + co[3], make_uint4(ab[i][4], ab[i][5], ab[i][6], ab[i][7]));
+        }
+    }
+}
+
 }  // namespace rbs4
 
 // Unit spaces as gf_encode_bs_kernel (flat over uniform windows, group mode
 // otherwise); the masks are the code's, R = its r.
-template <int R, bool FLAT>
+// MASKED (flat only, launch_rbs_rows with present masks): rows absent from a
+// window read as zeros (rbs4::unit_m).
+template <int R, bool FLAT, bool MASKED = false>
 __global__ __launch_bounds__(kBlock) void gf_encode_rbs_kernel(BatchArgs a) {
     CHK_PROLOGUE(a);
     const rbs::cmask mk = (rbs::cmask)a.enc_bs;
@@ -1001,7 +1077,27 @@ __global__ __launch_bounds__(kBlock) void gf_encode_rbs_kernel(BatchArgs a) {
             const bool live = s < total;
             if (!live) s = total - 1;
             const uint64_t w = s / h;
-            run(a.win + w * a.wpitch, (uint32_t)(s - w * h), h, ncol, a.stride, live, a.out_delta + w * a.out_wdelta);
+            if constexpr (MASKED) {
+                // the wave's resource: from its first lane's window over the
+                // windows to the batch's end (capped; the host keeps a wave's
+                // span below 2^31 B, rbs_masked_ok)
+                const uint64_t wf = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)w) |
+                                    ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) << 32);
+                uint8_t *gb = a.win + wf * a.wpitch;
+                const uint64_t span = (a.nwin - wf) * a.wpitch;
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    gb, 0, (int)(uint32_t)min(span, (uint64_t)0x7FFFFFFFu), bs::kRsrcRaw);
+                uint8_t *pc[4];
+                rbs4::unit_cols(a.win + w * a.wpitch, (uint32_t)(s - w * h), h, ncol, pc);
+                uint32_t co[4];
+#pragma unroll
+                for (int c = 0; c < 4; c++) co[c] = (uint32_t)(pc[c] - gb);
+                rbs4::unit_m<R>(rs, gb, co, a.stride, k, mk, live, a.out_delta + w * a.out_wdelta,
+                                a.present + w * a.pres_nw);
+            } else {
+                run(a.win + w * a.wpitch, (uint32_t)(s - w * h), h, ncol, a.stride, live,
+                    a.out_delta + w * a.out_wdelta);
+            }
         }
     } else {
         __shared__ GroupLds g;
@@ -2433,7 +2529,8 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
         switch (a.r) {
 #define RBS_CASE(R_)                                                                        \
             case R_:                                                                               \
-                return p.flat ? launch(gf_encode_rbs_kernel<R_, true>, a, p, s, false, want)       \
+                return a.pres_nw ? launch(gf_encode_rbs_kernel<R_, true, true>, a, p, s, false, want)  \
+                     : p.flat ? launch(gf_encode_rbs_kernel<R_, true>, a, p, s, false, want)       \
                               : launch(gf_encode_rbs_kernel<R_, false>, a, p, s, false);
             RBS_CASE(4) RBS_CASE(5) RBS_CASE(6) RBS_CASE(7) RBS_CASE(8)
 #undef RBS_CASE
@@ -2454,10 +2551,17 @@ hipError_t launch_encode(int scheme, const BatchArgs &a, const LaunchPlan &p, hi
 // the wide encode, and the two-stage wide decode's syndromes): window w at
 // win + w * wpitch, its k input rows first, output i at
 // (input row k + i's address) + out_delta + w * out_wdelta.  Flat unit space.
+bool rbs_masked_ok(uint32_t ncol, uint64_t wpitch) {
+    const uint32_t h = (ncol + kRbsCols - 1) / kRbsCols;
+    return h > 0 && (uint64_t)(64 / h + 2) * wpitch < (1ull << 31);
+}
+
 hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t stride, uint64_t wpitch, int k,
-                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s) {
+                           int r, const uint32_t *masks, uint64_t out_delta, uint64_t out_wdelta, hipStream_t s,
+                           const uint64_t *present, uint32_t pres_nw) {
     if (nwin == 0) return hipSuccess;
     if (r < 4 || r > 8) return hipErrorInvalidValue;
+    if (present && (pres_nw == 0 || !rbs_masked_ok(ncol, wpitch))) return hipErrorInvalidValue;
     BatchArgs a{};
     a.win = win;
     a.nwin = nwin;
@@ -2469,6 +2573,8 @@ hipError_t launch_rbs_rows(uint8_t *win, uint64_t nwin, uint32_t ncol, uint32_t 
     a.enc_bs = masks;
     a.out_delta = out_delta;
     a.out_wdelta = out_wdelta;
+    a.present = present;
+    a.pres_nw = present ? pres_nw : 0u;
     // FECGPU_CHECK builds: the input rows, and the outputs (out_delta /
     // out_wdelta may send them to another array: the wide decode's syndromes)
     a.chk.lo[0] = reinterpret_cast<uint64_t>(win);

@@ -53,6 +53,7 @@ struct WideArgs {
     CombJob *jobs1;
     uint64_t *outs1;
     ChkRec *chk;  // FECGPU_CHECK builds: the fault record (release: null)
+    bool zero_missing;  // stage 1 reads every row: the plan zeroes the missing ones
 };
 
 __global__ __launch_bounds__(kBlock) void wide_enc_jobs_kernel(WideArgs a) {
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
         }
         if (cu < e && ci < r) C2[cu * r + ci] = (uint8_t)v;
         uint8_t *wb = a.win + w * a.wpitch;
-        for (int u2 = 0; u2 < e && CHK_IDX(a.chk, s_m[wave][u2], k, 1); u2++) {
+        for (int u2 = 0; a.zero_missing && u2 < e && CHK_IDX(a.chk, s_m[wave][u2], k, 1); u2++) {
             uint4 *row = reinterpret_cast<uint4 *>(wb + (uint64_t)s_m[wave][u2] * a.stride);
             for (uint32_t c16 = lane; c16 < a.stride / 16u; c16 += 64) row[c16] = make_uint4(0, 0, 0, 0);
         }
@@ -200,7 +201,8 @@ __global__ __launch_bounds__(kBlock) void wide_dec_plan_kernel(WideArgs a) {
 hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, const uint8_t *P_dev,
                        uint64_t nwin, uint32_t stride, uint32_t ncol, int k, int r, bool decode, CombJob *jobs,
                        uint64_t *outs, uint8_t *coef, hipStream_t s, CombJob *jobs1, uint64_t *outs1,
-                       uint8_t *syn, const uint32_t *masks_P, const uint32_t *masks_PI, ChkRec *chk) {
+                       uint8_t *syn, const uint32_t *masks_P, const uint32_t *masks_PI, ChkRec *chk,
+                       bool mask_rows) {
     WideArgs a{};
     a.chk = chk;
     a.win = win;
@@ -219,6 +221,11 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
     a.jobs1 = jobs1;
     a.outs1 = outs1;
     const int n = k + r;
+    // stage 1 by plane picks skips the missing rows itself (absent rows read as
+    // zeros through a buffer resource: no zeroing writes, no reads of them);
+    // the combine-job stage 1 reads every row, so the plan zeroes them
+    const bool masked = decode && masks_PI && mask_rows && rbs_masked_ok(ncol, a.wpitch);
+    a.zero_missing = !masked;
     if (!decode && masks_P) {  // every window's k sources times P by plane picks
         return launch_rbs_rows(win, nwin, ncol, stride, a.wpitch, k, r, masks_P, 0, 0, s);
     }
@@ -240,7 +247,8 @@ hipError_t launch_wide(uint8_t *win, const uint64_t *present, uint8_t *status, c
         if (masks_PI) {
             e = launch_rbs_rows(win, nwin, ncol, stride, a.wpitch, n, r, masks_PI,
                                 (uint64_t)syn - (uint64_t)win - (uint64_t)n * stride,
-                                (uint64_t)r * stride - a.wpitch, s);
+                                (uint64_t)r * stride - a.wpitch, s, masked ? present : nullptr,
+                                masked ? (uint32_t)a.nw : 0u);
         } else {
         CombArgs c1{};
         c1.jobs = jobs1;
