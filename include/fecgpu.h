@@ -182,9 +182,10 @@ ssize_t fecgpu_encode_split(fecgpu_ctx *ctx, const fecgpu_code *code, const uint
 /* Recovery: present[w] bit i = symbol i received; codes
  * with k + r > 64 take ceil((k + r) / 64) words per window (bit i of window w
  * in word present[w * words + i / 64], bit i % 64), device pointers and a
- * uniform stride only, and their missing rows are read (times zero).
- * Missing sources are recovered in place; status[w] = FECGPU_STATUS_*.
- * Symbols whose bit is clear are never read.  XOR recovers every group with
+ * uniform stride only; when r < 4, the "bitslice" knob is 0 or a wave's span
+ * of windows reaches 2 GiB, their missing rows are zeroed and read (times
+ * zero).  Missing sources are recovered in place; status[w] =
+ * FECGPU_STATUS_*.  Otherwise symbols whose bit is clear are never read.  XOR recovers every group with
  * exactly one missing source and its repair, even when others are lost.
  * Returns nwin or a negative error. */
 ssize_t fecgpu_decode_batch(fecgpu_ctx *ctx, const fecgpu_code *code, uint8_t *win,
