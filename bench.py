@@ -511,8 +511,13 @@ def run_config(cfgid: int, args, rank: int, world: int, dev, ctx, steps: int, wa
                 for call, ms in (("encode", enc_ms), ("decode", dec_ms))}
         bound_dir = max(("h2d", "d2h"), key=lambda d: pb[dom][d])
         achieved = pcie[dom][bound_dir]["GBs"]
-    traffic, traffic_src = (pmc_traffic(f"wide{cfg.k}r{cfg.r}" if wide else cfgid, dom)
-                            if nwin == cfg.nwin_per_gpu and (wide or cfg.name == workloads.CONFIGS[cfgid].name)
+    # traffic files: profiles/rNN_cfg<key>_traffic.json; a sliding-window run
+    # with another loss / window has its own (key 7w<W>l<loss>)
+    sw_variant = cfg.scheme == "sw" and cfg.name != workloads.CONFIGS[cfgid].name
+    tkey = (f"wide{cfg.k}r{cfg.r}" if wide else f"{cfgid}w{cfg.window}l{cfg.loss:g}" if sw_variant else cfgid)
+    traffic, traffic_src = (pmc_traffic(tkey, dom)
+                            if nwin == cfg.nwin_per_gpu
+                            and (wide or sw_variant or cfg.name == workloads.CONFIGS[cfgid].name)
                             and (cfg.matrix == "cauchy" or cfg.scheme == "sw")
                             else (None, None))
     cpu = None
