@@ -145,6 +145,8 @@ void    fecgpu_host_free(void *p);
  * "bsdec" (1 default: GF decode of Cauchy k 16 r 4 on uniform rows whose
  * windows fill a 512-thread workgroup — about 1-8 KiB — by the bit-sliced
  * syndrome kernel; 0: the table decode; the bytes are the same);
+ * "wide_mask" (1 default: the decode of a code with k + r > 64 skips the
+ * missing rows in its syndrome pass; 0: they are zeroed and read);
  * "sw_group" (sliding-window encode by combine jobs: consecutive repairs per
  * job, each source loaded once per group; 1, 2, 4 or 8, default 4);
  * "sw_stream" (sliding-window encode: 0 combine jobs, 1..5 the streaming
