@@ -753,6 +753,10 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_kernel(BatchArgs a) {
     }
 }
 
+// gathered-store encode: sources loaded per batch (3: 1.196 vs 1.202 ms at 2, r06)
+#ifndef GSE_U
+#define GSE_U 3
+#endif
 // Bit-sliced encode of uniform windows with short rows, stores gathered
 // (DESIGN.md §4g): a.wpb whole windows per step (a.wpb * ceil(ncol / 2) <=
 // kBlock units, one pass), a lane per unit with the flat kernel's column pair
@@ -783,7 +787,7 @@ __global__ __launch_bounds__(kBlock) void gf_encode_bs_gs_kernel(BatchArgs a) {
             uint8_t *pa, *pb;
             bs::unit_cols(a.win + (w0 + wl) * a.wpitch, u, h, ncol, pa, pb);
             uint32_t acc[R][8];
-            bs::sources<K, R, M, kBsUFlat, 0>(pa, pb, a.stride, acc);
+            bs::sources<K, R, M, GSE_U, 0>(pa, pb, a.stride, acc);
 #pragma unroll
             for (int i = 0; i < R; i++) {
                 bs::tr8(acc[i]);
@@ -1621,6 +1625,10 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
 // solve in registers right after the network (199-225 VGPRs, 2 waves per
 // SIMD: 1.47 ms with per-lane stores, 1.53 gathered) and (B) storing its
 // columns directly (1.61 ms).
+// syndrome decode: sources loaded per batch (3: 1.259 vs 1.271 ms at 2, r06)
+#ifndef BSD_U
+#define BSD_U 3
+#endif
 namespace bsd {
 
 
@@ -1783,7 +1791,7 @@ __global__ __launch_bounds__(NT) void gf_decode_bs_gs_kernel(BatchArgs a) {
                 const __amdgpu_buffer_rsrc_t rs =
                     __builtin_amdgcn_make_buffer_rsrc(gb, 0, (int)(uint32_t)((uint64_t)nb * a.wpitch), bs::kRsrcRaw);
                 const uint32_t oa = (uint32_t)(pa - gb), ob = (uint32_t)(pb - gb);
-                bs::sources_rs<K, R, M, kBsUFlat, 0>(rs, oa, ob, a.stride, acc, pm);
+                bs::sources_rs<K, R, M, BSD_U, 0>(rs, oa, ob, a.stride, acc, pm);
 #pragma unroll
                 for (int i = 0; i < R; i++)
                     bs::load_rs(rs, oa, ob, ((pm >> (K + i)) & 1u) ? (uint32_t)(K + i) * a.stride : bs::kOob, rep[i]);
