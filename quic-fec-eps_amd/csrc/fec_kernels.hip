@@ -1620,17 +1620,16 @@ __global__ __launch_bounds__(kBlock) void gf_decode_kernel(BatchArgs a) {
 // gathered-store encode) in three phases: (A) syndromes by the network, a lane
 // per unit, to an LDS image [window][repair][column] in bytes; (B) the solve
 // per 16-B column, in place; (C) the recovered rows stored front to back.
-// cfg3: 1.28 ms against 1.36 for the table decode in-process (512 threads,
-// 13 windows a step; 256 threads, 6 windows, 4 workgroups per CU: 1.29-1.30).  Measured and removed (r06): the
-// solve in registers right after the network (199-225 VGPRs, 2 waves per
-// SIMD: 1.47 ms with per-lane stores, 1.53 gathered) and (B) storing its
-// columns directly (1.61 ms).
-// syndrome decode: sources loaded per batch (3: 1.259 vs 1.271 ms at 2, r06)
+// cfg3: 1.26-1.27 ms against 1.36 for the table decode in-process (512
+// threads, 13 windows a step; 256 threads, 6 windows, 4 workgroups per CU:
+// 1.29-1.30).  Measured and removed (r06): the solve in registers right after
+// the network (199-225 VGPRs, 2 waves per SIMD: 1.47 ms with per-lane stores,
+// 1.53 gathered) and (B) storing its columns directly (1.61 ms).
+// Sources loaded per batch in (A): 3 (1.259 vs 1.271 ms at 2, r06).
 #ifndef BSD_U
 #define BSD_U 3
 #endif
 namespace bsd {
-
 
 // Per-step LDS after the image (fec_internal.h bsd_lds_bytes), two buffers:
 // ab / tc [buf][window][i * R + u] the solve's tables, syndrome of repair i ->
