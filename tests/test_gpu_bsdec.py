@@ -113,3 +113,29 @@ def test_bsdec_every_erasure_pattern_of_one_window_size():
         assert np.array_equal(got[:, :K], enc[:, :K]), "recovered sources differ from the encoded ones"
     finally:
         c.close()
+
+
+def test_bsdec_full_size_iid_erasures():
+    """cfg3's geometry at full size (262,144 windows of k 16 r 4 x 1200 B) with
+    i.i.d. 10 % erasures over all 20 symbols: windows with 0-4 missing sources,
+    missing repairs, and unrecoverable ones (more missing sources than present
+    repairs) in one launch of the syndrome decode.  Every recoverable window's
+    sources equal the originals, every status equals the one predicted from the
+    masks (workloads.Batch.verify), and the table decode reports the same."""
+    import dataclasses
+    from fecgpu import workloads as WL
+    cfg = dataclasses.replace(WL.CONFIGS[3], erasure=WL.ERASURE_IID, name="cfg3-iid10")
+    b = WL.Batch.allocate(cfg, cfg.nwin_per_gpu, torch.device("cuda"))
+    res = {}
+    for knob in (1, 0):
+        c = fecgpu.Context()
+        c.set_tuning("bsdec", knob)
+        try:
+            b.synthesize(c, 0)
+            b.make_erasures(c, 0)
+            res[knob] = b.verify(c, 0)
+        finally:
+            c.close()
+    assert res[1]["ok"] and res[1]["status_matches_expected"], res[1]
+    assert res[1]["unrecoverable"] > 0
+    assert res[1]["unrecoverable"] == res[0]["unrecoverable"] and res[0]["ok"], res
