@@ -48,7 +48,8 @@ def _decode(c, code, enc, bits, L, stride):
 
 
 @pytest.mark.parametrize("L,stride,nwin", [(1200, 1200, 301), (1000, 1008, 97), (1500, 1520, 203),
-                                           (2048, 2048, 64), (1183, 1200, 150), (4000, 4000, 23)])
+                                           (2048, 2048, 64), (1183, 1200, 150), (4000, 4000, 23),
+                                           (1200, 1216, 1), (1200, 1200, 12), (1200, 1200, 13)])
 def test_bsdec_vs_oracle_and_table_decode(L, stride, nwin):
     rng = np.random.default_rng(L + nwin)
     wins = np.zeros((nwin, K + R, stride), np.uint8)
